@@ -1,0 +1,212 @@
+"""Benchmark: committed txns/sec of the batched CC engine on YCSB (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--cc NO_WAIT|WAIT_DIE|OCC|CALVIN]
+                    [--config D|C|B] [--mpr 0.1]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step is one epoch through the hot path (probe -> sort -> decide -> execute)
+with its accesses already resident in HBM.  Default workload (config D of
+SURVEY.md 8d, the headline "YCSB zipf 0.9 at 1/2/4/8 GPUs"): 16,777,216 rows
+and 1,048,576 txns per GPU per epoch, 10 requests/txn, zipf 0.9, 50 % of the
+accesses writes (TXN_WRITE_PERC 1.0, TUP_WRITE_PERC 0.5), NO_WAIT.  With N>1,
+rank r owns partition r and multi-partition txns (MPR gate, 2 partitions)
+exchange fragments by all-to-all and votes by all-reduce (RCCL over xGMI).
+Weak scaling: rows and txns per GPU are fixed.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "deneva-plus_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import dvcc  # noqa: E402
+from dvcc.partitioned import EnginePartition, PartitionedEpoch, PartitionedRunner  # noqa: E402
+
+METRIC = "committed txns/sec (node) YCSB zipf0.9 at 1/2/4/8 GPUs; abort-set bit-exact"
+HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+BYTES_PER_ACCESS = 67        # algorithmic bytes per access
+
+CONFIGS = {
+    # name: rows per partition, txns per GPU-epoch, zipf theta, description
+    "D": (16_777_216, 1_048_576, 0.9, "YCSB config D: 16,777,216 rows/partition, 1,048,576-txn epoch/GPU"),
+    "C": (100_000_000, 1_048_576, 0.9, "YCSB config C: 100,000,000 rows, 1,048,576-txn epoch"),
+    "B": (16_777_216, 65_536, 0.6, "YCSB config B: 16,777,216 rows, 65,536-txn epoch"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cc", default="NO_WAIT")
+    ap.add_argument("--config", default="D")
+    ap.add_argument("--mpr", type=float, default=0.1)
+    ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def gen_epochs(gen, n_txn, rank, count):
+    with ThreadPoolExecutor(max_workers=min(count, 8)) as ex:  # dv_ycsb_gen releases the GIL
+        futs = [ex.submit(gen.gen, n_txn, dvcc.epoch_seed(rank, e), rank) for e in range(count)]
+        return [f.result() for f in futs]
+
+
+def cpu_baseline(epochs, rows, cc_name, seconds):
+    """The oracle (single-thread E-schedule restatement of the reference CC,
+    not the reference binary) on the same epochs, cycled for ~`seconds`."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    cc = {"NO_WAIT": O.NO_WAIT, "WAIT_DIE": O.WAIT_DIE, "OCC": O.OCC, "CALVIN": O.CALVIN}[cc_name]
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    committed = txns = 0
+    t0 = time.perf_counter()
+    i = 0
+    while True:
+        e = epochs[i % len(epochs)]
+        _, _, st = O.epoch_run(cc, tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types)
+        committed += st.committed
+        txns += e.n_txn
+        i += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": committed / el, "unit": "committed txns/s", "cores": 1, "kind": "port",
+            "sample": f"oracle E-schedule ({cc_name}) over {i} epoch(s) of {epochs[0].n_txn} txns "
+                      f"of the bench workload, {txns} txns in {el:.1f} s on 1 host core; "
+                      f"restatement of the reference CC, not the reference binary"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        a.gpus = world if world > 1 else a.gpus
+    if a.gpus > 1 and world == 1:
+        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    cc_name = a.cc.upper()
+    rows, n_txn, theta, desc = CONFIGS[a.config]
+    R = 10
+    mpr = a.mpr if world > 1 else -1.0  # N=1: the reference zipf generator, unmodified
+    gen = dvcc.YCSBQueryGenerator(rows * world, part_cnt=world, req_per_query=R, zipf_theta=theta,
+                                  txn_write_perc=1.0, tup_write_perc=0.5,
+                                  part_per_txn=min(2, world), strict_ppt=1, mpr=mpr)
+    n_epochs = max(1, min(a.epochs, a.steps + a.warmup))
+    t_gen = time.perf_counter()
+    epochs = gen_epochs(gen, n_txn, rank, n_epochs)
+    t_gen = time.perf_counter() - t_gen
+
+    if world == 1:
+        eng = dvcc.CCEngine(cc_name, n_txn, n_txn * R, device=local_rank, timing=True)
+        eng.load_ycsb_partition(rows)
+        deps = [dvcc.DeviceEpoch(e) for e in epochs]
+        d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+
+        def step(i):
+            return eng.run_epoch_device(deps[i % n_epochs], d_commit)
+    else:
+        max_acc = int(n_txn * R * 1.5) + 4096
+        eng = dvcc.CCEngine(cc_name, n_txn * world, max_acc, device=local_rank, part_cnt=world,
+                            part_id=rank, timing=True)
+        eng.load_ycsb_partition(rows)
+        runner = PartitionedRunner(EnginePartition(eng), world, rank)
+        pes = [PartitionedEpoch(e, rank, world, n_txn, "cuda") for e in epochs]
+        d_commit = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+
+        def step(i):
+            st, _ = runner.run(pes[i % n_epochs], commit=d_commit)
+            return st
+
+    for i in range(a.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    stats = [step(a.warmup + i) for i in range(a.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    # commits are global (every rank holds the same decision vector): count once
+    committed = sum(s.committed for s in stats)
+    txns = sum(s.n_txn for s in stats)
+    acc_local = sum(s.n_acc for s in stats)
+    value = committed / el
+    sc_ms = [s.ms_scatter / max(1, s.scatter_launches) for s in stats if s.scatter_launches]
+    sc_avg = float(np.mean(sc_ms)) if sc_ms else 0.0
+    n_acc_step = acc_local / max(1, len(stats))
+    scatter_bytes = n_acc_step * 16  # one radix pass: read + write of one packed u64 per access
+    achieved = scatter_bytes / (sc_avg * 1e-3) / 1e9 if sc_avg > 0 else 0.0
+    epoch_gbps = (txns / el) * (BYTES_PER_ACCESS * R + 1) / 1e9
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "committed txns/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": el / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic: Deneva YCSB zipf generator (myrand LCG, seeded SEED+97*part+epoch)",
+        "config": {
+            "workload": desc, "cc_alg": cc_name, "rows_per_partition": rows,
+            "txns_per_epoch_per_gpu": n_txn, "req_per_query": R, "zipf_theta": theta,
+            "txn_write_perc": 1.0, "tup_write_perc": 0.5, "mpr": mpr if world > 1 else 0.0,
+            "part_per_txn": min(2, world), "parallelism": f"partitioned x{world} (PART_CNT={world})",
+            "distinct_epochs": n_epochs,
+        },
+        "roofline": {
+            "kernel": "k_radix_scatter",
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": None,
+            "bytes_per_launch": scatter_bytes,
+            "avg_launch_ms": sc_avg,
+        },
+        "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1, "achieved_GBps": epoch_gbps,
+                           "frac": epoch_gbps / HBM_PEAK_GBPS},
+        "abort_rate": 1.0 - committed / max(1, txns),
+        "decided_txns_per_s": txns / el,
+        "rounds_mean": float(np.mean([s.rounds for s in stats])),
+        "stage_ms_mean": {k: float(np.mean([getattr(s, k) for s in stats]))
+                          for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")},
+        "gen_seconds": t_gen,
+    }
+    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(epochs, rows, cc_name, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

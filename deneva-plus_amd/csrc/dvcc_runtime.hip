@@ -1,0 +1,600 @@
+// dvcc_runtime.hip -- epoch runtime and C ABI (include/dvcc.h).
+//
+// Host side of the engine: owns the device, the stream, the HBM row store and
+// hash index, and the per-epoch workspace; sequences the kernels of
+// dvcc_kernels.hip.  Replaces the per-txn machinery of the reference
+// (TxnManager/txn_table/worker loop, system/txn.cpp, txn_table.cpp,
+// worker_thread.cpp:183-518) with dense epoch arrays: txn sequence number ==
+// array index, one byte of decision state per txn.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "dvcc_internal.h"
+
+using namespace dvcc;
+
+namespace {
+
+struct HostTable {
+    bool created = false, loaded = false;
+    uint64_t cap_rows = 0, n_rows = 0, nbuckets = 0, row_base = 0;
+    uint32_t hash_kind = DV_HASH_YCSB;
+    IxEntry *ix = nullptr;      // device
+    uint32_t *bstart = nullptr; // device (chained only)
+    uint64_t ix_cap = 0;
+};
+
+}  // namespace
+
+struct dv_ctx {
+    dv_config cfg{};
+    hipStream_t stream = nullptr;      // where work is launched
+    hipStream_t own_stream = nullptr;  // created by dv_open
+    HostTable tab[kMaxTables];
+    uint64_t total_rows = 0;
+    uint64_t *f0 = nullptr;    // hot column, global row id
+    uint64_t *pkey = nullptr;  // primary key per row (row_t::get_primary_key)
+
+    // workspace (capacities from cfg)
+    uint64_t *pairs[2] = {nullptr, nullptr};
+    uint32_t *vals[2] = {nullptr, nullptr};
+    uint32_t *el = nullptr;
+    uint8_t *ew = nullptr;
+    uint32_t *counts = nullptr, *digit_tot = nullptr;
+    uint32_t *agg_f = nullptr, *agg_v = nullptr, *carry = nullptr;
+    uint8_t *status = nullptr, *verdict = nullptr;
+    Counters *ctr = nullptr;    // device
+    Counters *h_ctr = nullptr;  // pinned host mirror
+    uint32_t n_txn_cap_pad = 0;
+
+    // staging for dv_epoch_run (host-buffer entry point)
+    dv_access *d_acc = nullptr;
+    uint64_t *d_keys = nullptr;
+    uint8_t *d_types = nullptr, *d_tables = nullptr, *d_commit = nullptr;
+    uint32_t *d_txn = nullptr, *d_grant = nullptr;
+
+    // epoch state
+    int phase = 0;  // 0 idle, 1 begun
+    uint64_t n_acc = 0;
+    uint32_t n_txn = 0, n_txn_pad = 0;
+    int sorted = 0;
+    uint32_t rounds = 0, sort_passes = 0;
+
+    // timing
+    hipEvent_t ev[32] = {};
+    hipEvent_t sev[16] = {};
+    float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
+};
+
+namespace {
+
+inline void dfree(void *p) {
+    if (p) (void)hipFree(p);
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    if (e == hipSuccess) return DV_OK;
+    std::fprintf(stderr, "dvcc: %s failed: %s\n", what, hipGetErrorString(e));
+    return DV_ERR_HIP;
+}
+#define HIPCHK(x)                                         \
+    do {                                                  \
+        int _r = hip_fail((x), #x);                       \
+        if (_r) return _r;                                \
+    } while (0)
+
+template <class T>
+int dalloc(T **p, uint64_t count) {
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * count);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        std::fprintf(stderr, "dvcc: hipMalloc(%llu B) failed: %s\n",
+                     (unsigned long long)(sizeof(T) * count), hipGetErrorString(e));
+        return DV_ERR_NOMEM;
+    }
+    return DV_OK;
+}
+
+int bits_for(uint64_t n) {  // bits needed to represent values in [0, n)
+    int b = 0;
+    while (b < 64 && (1ull << b) < n) b++;
+    return b;
+}
+
+Tables make_tables(dv_ctx *c) {
+    Tables t{};
+    t.n = 0;
+    for (uint32_t i = 0; i < kMaxTables; i++) {
+        const HostTable &h = c->tab[i];
+        if (!h.created) continue;
+        t.n = i + 1;
+        t.t[i].ix = h.ix;
+        t.t[i].bstart = h.bstart;
+        t.t[i].nbuckets = h.nbuckets ? h.nbuckets : 1;
+        t.t[i].row_base = h.row_base;
+        t.t[i].hash_kind = h.hash_kind;
+        t.t[i].part_cnt = c->cfg.part_cnt ? c->cfg.part_cnt : 1;
+    }
+    return t;
+}
+
+int err_from_bits(uint32_t b) {
+    if (b & ERRB_TABLE) return DV_ERR_NO_TABLE;
+    if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
+    if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
+    if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
+    return DV_OK;
+}
+
+bool timing(dv_ctx *c) { return (c->cfg.flags & DV_FLAG_TIMING) != 0; }
+
+void rec(dv_ctx *c, int i) {
+    if (timing(c)) (void)hipEventRecord(c->ev[i], c->stream);
+}
+
+float elapsed(dv_ctx *c, int a, int b) {
+    float ms = 0;
+    if (timing(c)) (void)hipEventElapsedTime(&ms, c->ev[a], c->ev[b]);
+    return ms;
+}
+
+int sync_counters(dv_ctx *c) {
+    HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *dv_strerror(int code) {
+    switch (code) {
+    case DV_OK: return "ok";
+    case DV_ERR_ARG: return "bad argument or capacity exceeded";
+    case DV_ERR_HIP: return "HIP runtime error";
+    case DV_ERR_NOMEM: return "device allocation failed";
+    case DV_ERR_KEY_NOT_FOUND: return "key does not exist in the index";
+    case DV_ERR_DUP_ROW: return "a 2PL/OCC txn accesses the same row twice";
+    case DV_ERR_NO_TABLE: return "table not created or not loaded";
+    case DV_ERR_STATE: return "call out of order";
+    case DV_ERR_NO_DEVICE: return "no HIP device";
+    case DV_ERR_TXN_RANGE: return "access names a txn outside the epoch or txns out of order";
+    default: return "unknown error";
+    }
+}
+
+int dv_device_count(int *count) {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (count) *count = (e == hipSuccess) ? n : 0;
+    return (e == hipSuccess && n > 0) ? DV_OK : DV_ERR_NO_DEVICE;
+}
+
+void dv_close(dv_ctx *c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &t : c->tab) {
+        dfree(t.ix);
+        dfree(t.bstart);
+    }
+    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->vals[0], c->vals[1], c->el,
+                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->status,
+                    c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
+                    c->d_commit, c->d_txn, c->d_grant};
+    for (void *b : bufs) dfree(b);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
+    for (auto &e : c->sev) if (e) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+}
+
+int dv_open(dv_ctx **out, const dv_config *cfg) {
+    if (!out || !cfg) return DV_ERR_ARG;
+    *out = nullptr;
+    if (cfg->cc_alg != DV_NO_WAIT && cfg->cc_alg != DV_WAIT_DIE && cfg->cc_alg != DV_OCC &&
+        cfg->cc_alg != DV_CALVIN)
+        return DV_ERR_ARG;
+    if (cfg->max_txn == 0 || cfg->max_txn > kMaxTxn || cfg->max_acc == 0 ||
+        cfg->max_acc > 0x7FFFFFFFull || cfg->part_cnt == 0 || cfg->part_id >= cfg->part_cnt)
+        return DV_ERR_ARG;
+    int ndev = 0;
+    if (dv_device_count(&ndev) != DV_OK || cfg->device < 0 || cfg->device >= ndev)
+        return DV_ERR_NO_DEVICE;
+    dv_ctx *c = new (std::nothrow) dv_ctx();
+    if (!c) return DV_ERR_NOMEM;
+    c->cfg = *cfg;
+    int r = hip_fail(hipSetDevice(cfg->device), "hipSetDevice");
+    if (!r) r = hip_fail(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream");
+    c->stream = c->own_stream;
+    const uint64_t A = cfg->max_acc;
+    const uint32_t T = cfg->max_txn;
+    c->n_txn_cap_pad = (T + 3u) & ~3u;
+    const uint32_t nb = nblocks_for(A);
+    if (!r) r = dalloc(&c->pairs[0], A);
+    if (!r) r = dalloc(&c->pairs[1], A);
+    if (!r) r = dalloc(&c->el, A);
+    if (!r) r = dalloc(&c->counts, (uint64_t)kRadix * nb);
+    if (!r) r = dalloc(&c->digit_tot, kRadix);
+    if (!r) r = dalloc(&c->agg_f, nb);
+    if (!r) r = dalloc(&c->agg_v, nb);
+    if (!r) r = dalloc(&c->carry, nb);
+    if (!r) r = dalloc(&c->status, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->ctr, 1);
+    if (!r && cfg->cc_alg == DV_CALVIN) {
+        r = dalloc(&c->vals[0], A);
+        if (!r) r = dalloc(&c->vals[1], A);
+        if (!r) r = dalloc(&c->ew, A);
+    }
+    if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)),
+                         "hipHostMalloc");
+    if (!r && timing(c)) {
+        for (auto &e : c->ev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
+        for (auto &e : c->sev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
+    }
+    if (!r) r = hip_fail(hipMemsetAsync(c->verdict, 0, c->n_txn_cap_pad, c->stream), "memset");
+    if (!r) r = hip_fail(hipStreamSynchronize(c->stream), "sync");
+    if (r) {
+        dv_close(c);
+        return r;
+    }
+    *out = c;
+    return DV_OK;
+}
+
+void *dv_stream(dv_ctx *c) { return c ? (void *)c->stream : nullptr; }
+
+int dv_set_stream(dv_ctx *c, void *stream) {
+    if (!c) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own_stream;
+    return DV_OK;
+}
+
+// Workload::init_schema (system/wl.cpp:31-149) + IndexHash::init (index_hash.cpp:22-42)
+int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t nbuckets,
+                    uint32_t hash_kind) {
+    if (!c || table >= kMaxTables || capacity_rows == 0 || nbuckets == 0 ||
+        (hash_kind != DV_HASH_YCSB && hash_kind != DV_HASH_MOD))
+        return DV_ERR_ARG;
+    HostTable &t = c->tab[table];
+    if (t.created) return DV_ERR_STATE;
+    if (c->total_rows + capacity_rows > 0xFFFFFFFFull) return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    // grow the global hot column / primary-key arrays (load-time only)
+    const uint64_t new_total = c->total_rows + capacity_rows;
+    uint64_t *nf0 = nullptr, *npk = nullptr;
+    int r = dalloc(&nf0, new_total);
+    if (!r) r = dalloc(&npk, new_total);
+    if (r) { dfree(nf0); return r; }
+    if (c->total_rows) {
+        HIPCHK(hipMemcpyAsync(nf0, c->f0, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(npk, c->pkey, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+    }
+    HIPCHK(hipMemsetAsync(nf0 + c->total_rows, 0, capacity_rows * 8, c->stream));
+    HIPCHK(hipMemsetAsync(npk + c->total_rows, 0xFF, capacity_rows * 8, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    dfree(c->f0);
+    dfree(c->pkey);
+    c->f0 = nf0;
+    c->pkey = npk;
+    t.created = true;
+    t.cap_rows = capacity_rows;
+    t.row_base = c->total_rows;
+    t.nbuckets = nbuckets;
+    t.hash_kind = hash_kind;
+    c->total_rows = new_total;
+    return DV_OK;
+}
+
+// table_t::get_new_row + IndexHash::index_insert for n rows (row i = keys[i]).
+// Chains keep BucketHeader::insert_item order (index_hash.cpp:172-201): distinct
+// keys in first-insertion order, repeated keys newest first.
+int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_t *f0, uint64_t n) {
+    if (!c || table >= kMaxTables || (!keys && n)) return DV_ERR_ARG;
+    HostTable &t = c->tab[table];
+    if (!t.created) return DV_ERR_NO_TABLE;
+    if (n > t.cap_rows) return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const uint64_t nb = t.nbuckets;
+    const uint32_t P = c->cfg.part_cnt;
+    auto bucket = [&](uint64_t k) { return t.hash_kind == DV_HASH_YCSB ? (k / P) % nb : k % nb; };
+    std::vector<uint32_t> cnt(nb + 1, 0);
+    for (uint64_t i = 0; i < n; i++) cnt[bucket(keys[i]) + 1]++;
+    bool direct = (n == nb);
+    for (uint64_t b = 0; b < nb && direct; b++) direct = cnt[b + 1] == 1;
+    for (uint64_t b = 0; b < nb; b++) cnt[b + 1] += cnt[b];
+    std::vector<IxEntry> ent(n ? n : 1);
+    {
+        std::vector<uint32_t> fill(cnt.begin(), cnt.end() - 1);
+        for (uint64_t i = 0; i < n; i++) ent[fill[bucket(keys[i])]++] = IxEntry{keys[i], i};
+        // within a bucket: group equal keys at the first occurrence, newest first
+        for (uint64_t b = 0; b < nb && !direct; b++) {
+            const uint32_t lo = cnt[b], hi = cnt[b + 1];
+            if (hi - lo < 2) continue;
+            std::vector<IxEntry> tmp(ent.begin() + lo, ent.begin() + hi), outv;
+            std::vector<bool> used(tmp.size(), false);
+            for (size_t a = 0; a < tmp.size(); a++) {
+                if (used[a]) continue;
+                std::vector<IxEntry> same;
+                for (size_t z = a; z < tmp.size(); z++)
+                    if (!used[z] && tmp[z].key == tmp[a].key) { same.push_back(tmp[z]); used[z] = true; }
+                for (auto it = same.rbegin(); it != same.rend(); ++it) outv.push_back(*it);
+            }
+            std::copy(outv.begin(), outv.end(), ent.begin() + lo);
+        }
+    }
+    dfree(t.ix);
+    dfree(t.bstart);
+    t.ix = nullptr;
+    t.bstart = nullptr;
+    int r = dalloc(&t.ix, direct ? nb : (n ? n : 1));
+    if (r) return r;
+    if (direct) {
+        std::vector<IxEntry> d(nb);
+        for (uint64_t b = 0; b < nb; b++) d[b] = ent[cnt[b]];
+        HIPCHK(hipMemcpy(t.ix, d.data(), nb * sizeof(IxEntry), hipMemcpyHostToDevice));
+    } else {
+        r = dalloc(&t.bstart, nb + 1);
+        if (r) return r;
+        if (n) HIPCHK(hipMemcpy(t.ix, ent.data(), n * sizeof(IxEntry), hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(t.bstart, cnt.data(), (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    if (n) {
+        if (f0) HIPCHK(hipMemcpy(c->f0 + t.row_base, f0, n * 8, hipMemcpyHostToDevice));
+        HIPCHK(hipMemcpy(c->pkey + t.row_base, keys, n * 8, hipMemcpyHostToDevice));
+    }
+    t.n_rows = n;
+    t.loaded = true;
+    return DV_OK;
+}
+
+int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
+    if (!c || rows_per_part == 0) return DV_ERR_ARG;
+    HostTable &t = c->tab[0];
+    if (!t.created) {
+        int r = dv_create_table(c, 0, rows_per_part, rows_per_part, DV_HASH_YCSB);
+        if (r) return r;
+    }
+    if (t.cap_rows < rows_per_part || t.nbuckets != rows_per_part || t.hash_kind != DV_HASH_YCSB)
+        return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    dfree(t.ix);
+    dfree(t.bstart);
+    t.bstart = nullptr;
+    int r = dalloc(&t.ix, rows_per_part);
+    if (r) return r;
+    launch_ycsb_load(c->stream, rows_per_part, c->cfg.part_cnt, c->cfg.part_id, c->f0 + t.row_base,
+                     c->pkey + t.row_base, t.ix);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    t.n_rows = rows_per_part;
+    t.loaded = true;
+    return DV_OK;
+}
+
+int dv_read_rows(dv_ctx *c, uint32_t table, const uint64_t *keys, uint64_t n, uint64_t *out_f0) {
+    if (!c || table >= kMaxTables || (n && (!keys || !out_f0))) return DV_ERR_ARG;
+    if (!c->tab[table].loaded) return DV_ERR_NO_TABLE;
+    if (!n) return DV_OK;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    uint64_t *dk = nullptr, *dout = nullptr;
+    int r = dalloc(&dk, n);
+    if (!r) r = dalloc(&dout, n);
+    if (!r) {
+        HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+        HIPCHK(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
+        launch_gather_rows(c->stream, make_tables(c), table, dk, n, c->f0, dout, c->ctr);
+        HIPCHK(hipMemcpyAsync(out_f0, dout, n * 8, hipMemcpyDeviceToHost, c->stream));
+        r = sync_counters(c);
+        if (!r) r = err_from_bits(c->h_ctr->err);
+    }
+    dfree(dk);
+    dfree(dout);
+    return r;
+}
+
+int dv_read_table(dv_ctx *c, uint32_t table, uint64_t first_row, uint64_t n, uint64_t *out_f0) {
+    if (!c || table >= kMaxTables || (n && !out_f0)) return DV_ERR_ARG;
+    const HostTable &t = c->tab[table];
+    if (!t.created) return DV_ERR_NO_TABLE;
+    if (first_row + n > t.cap_rows) return DV_ERR_ARG;
+    if (!n) return DV_OK;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipMemcpyAsync(out_f0, c->f0 + t.row_base + first_row, n * 8, hipMemcpyDeviceToHost,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+// ---------------------------------------------------------------- epoch
+// Probe + sort + per-row queue construction; for CALVIN also the grant groups
+// (the lock thread's whole job for the epoch, calvin_thread.cpp:40-100).
+int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
+    if (!c || !ep) return DV_ERR_ARG;
+    if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
+    if (ep->n_acc && (!ep->keys || !ep->types || !ep->acc_txn)) return DV_ERR_ARG;
+    bool any = false;
+    for (auto &t : c->tab) any |= t.loaded;
+    if (!any) return DV_ERR_NO_TABLE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    if (ep->n_txn > kMaxTxn) return DV_ERR_ARG;
+    c->n_acc = ep->n_acc;
+    c->n_txn = ep->n_txn;
+    c->n_txn_pad = (ep->n_txn + 3u) & ~3u;
+    c->rounds = 0;
+    c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
+    rec(c, 0);
+    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
+    HIPCHK(hipMemsetAsync(c->verdict, 0, c->n_txn_pad ? c->n_txn_pad : 4, c->stream));
+    launch_status_init(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC);
+    launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
+                 ep->n_txn, c->pairs[0], calvin ? c->vals[0] : nullptr, c->ctr);
+    rec(c, 1);
+    const int key_bits = bits_for(c->total_rows);
+    c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
+    c->sorted = radix_sort_rows(c->stream, c->pairs, calvin ? c->vals : nullptr, ep->n_acc, key_bits,
+                                c->counts, c->digit_tot, timing(c) ? c->sev : nullptr);
+    launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, calvin ? 1 : 0, c->el, c->ctr);
+    rec(c, 2);
+    if (calvin) {
+        calvin_grant(c->stream, c->el, c->vals[c->sorted], ep->n_acc, d_grant, c->ew, c->agg_f,
+                     c->agg_v, c->carry);
+    }
+    rec(c, 3);
+    HIPCHK(hipGetLastError());
+    c->phase = 1;
+    return DV_OK;
+}
+
+// one decision round on this partition's accesses: verdict bytes (wait/abort)
+// for every undecided txn that has an access here
+int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
+    if (!c || c->phase != 1) return DV_ERR_STATE;
+    if (c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
+    uint8_t *v = d_verdict ? d_verdict : c->verdict;
+    if (d_verdict) HIPCHK(hipMemsetAsync(v, 0, c->n_txn_pad, c->stream));
+    round_local(c->stream, c->cfg.cc_alg != DV_OCC, c->el, c->n_acc, c->status, v, c->agg_f,
+                c->agg_v, c->carry);
+    HIPCHK(hipGetLastError());
+    return DV_OK;
+}
+
+int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
+    if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
+    uint8_t *v = d_verdict ? const_cast<uint8_t *>(d_verdict) : c->verdict;
+    HIPCHK(hipMemsetAsync(&c->ctr->undecided, 0, sizeof(uint32_t), c->stream));
+    launch_round_apply(c->stream, c->status, v, c->n_txn_pad, c->ctr);
+    HIPCHK(hipGetLastError());
+    c->rounds++;
+    int r = sync_counters(c);
+    if (r) return r;
+    r = err_from_bits(c->h_ctr->err);
+    if (r) { c->phase = 0; return r; }
+    if (undecided) *undecided = c->h_ctr->undecided;
+    return DV_OK;
+}
+
+int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
+    if (!c || c->phase != 1) return DV_ERR_STATE;
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    rec(c, 4);
+    launch_exec(c->stream, calvin ? 1 : 0, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status,
+                c->f0, c->pkey, c->ctr);
+    launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
+    rec(c, 5);
+    HIPCHK(hipGetLastError());
+    int r = sync_counters(c);
+    c->phase = 0;
+    if (r) return r;
+    r = err_from_bits(c->h_ctr->err);
+    if (r) return r;
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->n_txn = c->n_txn;
+        st->n_acc = c->n_acc;
+        st->committed = c->h_ctr->committed;
+        st->aborted = c->n_txn - c->h_ctr->committed;
+        st->write_cnt = c->h_ctr->write_cnt;
+        st->read_digest = c->h_ctr->read_digest;
+        st->rounds = c->rounds;
+        st->sort_passes = c->sort_passes;
+        if (timing(c)) {
+            st->ms_probe = elapsed(c, 0, 1);
+            st->ms_sort = elapsed(c, 1, 2);
+            st->ms_decide = elapsed(c, 2, 4);
+            st->ms_exec = elapsed(c, 4, 5);
+            st->ms_total = elapsed(c, 0, 5);
+            float s = 0;
+            for (uint32_t p = 0; p < c->sort_passes && p < 8; p++) {
+                float m = 0;
+                (void)hipEventElapsedTime(&m, c->sev[2 * p], c->sev[2 * p + 1]);
+                s += m;
+            }
+            st->ms_scatter = s;
+            st->scatter_launches = c->n_acc ? c->sort_passes : 0;
+        }
+    }
+    return DV_OK;
+}
+
+int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, uint32_t *d_grant,
+                        dv_stats *st) {
+    int r = dv_epoch_begin(c, ep, d_grant);
+    if (r) return r;
+    if (c->cfg.cc_alg != DV_CALVIN) {
+        // rounds until every txn is decided; each round decides at least the
+        // lowest undecided txn, so the undecided count strictly falls
+        uint32_t prev = c->n_txn + 1;
+        for (;;) {
+            uint32_t und = 0;
+            r = dv_epoch_round_local(c, nullptr);
+            if (!r) r = dv_epoch_round_apply(c, nullptr, &und);
+            if (!r && und >= prev) r = DV_ERR_STATE;  // no progress: internal error
+            if (r) { c->phase = 0; return r; }
+            if (und == 0) break;
+            prev = und;
+        }
+    }
+    return dv_epoch_finish(c, d_commit, st);
+}
+
+int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                 uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
+                 dv_stats *st) {
+    (void)ts;  // decisions follow sequence order; TS_CAS timestamps are monotone in it
+    if (!c || (n_acc && !acc) || !out_commit) return DV_ERR_ARG;
+    if (n_acc > c->cfg.max_acc || n_txn > c->cfg.max_txn) return DV_ERR_ARG;
+    if (txn_begin) {  // CSR form must agree with acc[].txn_seq
+        if (txn_begin[0] != 0 || txn_begin[n_txn] != n_acc) return DV_ERR_ARG;
+        for (uint32_t t = 0; t < n_txn; t++)
+            for (uint64_t a = txn_begin[t]; a < txn_begin[t + 1]; a++)
+                if (acc[a].txn_seq != t) return DV_ERR_TXN_RANGE;
+    }
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int r = DV_OK;
+    if (!c->d_acc) {
+        const uint64_t A = c->cfg.max_acc;
+        r = dalloc(&c->d_acc, A);
+        if (!r) r = dalloc(&c->d_keys, A);
+        if (!r) r = dalloc(&c->d_types, A);
+        if (!r) r = dalloc(&c->d_tables, A);
+        if (!r) r = dalloc(&c->d_txn, A);
+        if (!r) r = dalloc(&c->d_commit, c->cfg.max_txn);
+        if (!r && c->cfg.cc_alg == DV_CALVIN) r = dalloc(&c->d_grant, A);
+        if (r) return r;
+    }
+    if (n_acc) {
+        HIPCHK(hipMemcpyAsync(c->d_acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice,
+                              c->stream));
+        launch_split_access(c->stream, c->d_acc, n_acc, c->d_keys, c->d_types, c->d_txn, c->d_tables);
+    }
+    dv_epoch_dev ep{};
+    ep.keys = c->d_keys;
+    ep.types = c->d_types;
+    ep.acc_txn = c->d_txn;
+    ep.tables = c->d_tables;
+    ep.n_acc = n_acc;
+    ep.n_txn = n_txn;
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
+    if (r) return r;
+    if (n_txn)
+        HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
+    if (calvin && out_grant && n_acc)
+        HIPCHK(hipMemcpyAsync(out_grant, c->d_grant, n_acc * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+}  // extern "C"

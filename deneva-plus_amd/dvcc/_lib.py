@@ -1,0 +1,130 @@
+"""ctypes binding of libdvcc.so (the C ABI of include/dvcc.h).
+
+The library is loaded from the in-tree build (deneva-plus_amd/build/libdvcc.so).
+If it is missing the import fails loudly: there is no CPU fallback for the
+engine -- the HIP path is the product.
+"""
+import ctypes
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "build", "libdvcc.so")
+
+DV_OK = 0
+DV_ERR_ARG = -1
+DV_ERR_HIP = -2
+DV_ERR_NOMEM = -3
+DV_ERR_KEY_NOT_FOUND = -4
+DV_ERR_DUP_ROW = -5
+DV_ERR_NO_TABLE = -6
+DV_ERR_STATE = -7
+DV_ERR_NO_DEVICE = -8
+DV_ERR_TXN_RANGE = -9
+
+# CC_ALG (config.h)
+NO_WAIT, WAIT_DIE, OCC, CALVIN = 1, 2, 8, 10
+CC_NAMES = {"NO_WAIT": NO_WAIT, "WAIT_DIE": WAIT_DIE, "OCC": OCC, "CALVIN": CALVIN}
+YCSB, TPCC = 1, 2
+RD, WR, SCAN = 0, 1, 3
+HASH_YCSB, HASH_MOD = 0, 1
+FLAG_TIMING = 1
+
+
+class DvccError(RuntimeError):
+    def __init__(self, code, what=""):
+        self.code = code
+        msg = lib().dv_strerror(code).decode() if _lib is not None else str(code)
+        super().__init__(f"{what}: dvcc error {code} ({msg})" if what else f"dvcc error {code} ({msg})")
+
+
+class Config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("cc_alg", ctypes.c_int32), ("workload", ctypes.c_int32),
+                ("part_cnt", ctypes.c_uint32), ("part_id", ctypes.c_uint32),
+                ("max_txn", ctypes.c_uint32), ("max_acc", ctypes.c_uint64),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+class Access(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_uint64), ("txn_seq", ctypes.c_uint32), ("type", ctypes.c_uint8),
+                ("table", ctypes.c_uint8), ("flags", ctypes.c_uint16)]
+
+
+class EpochDev(ctypes.Structure):
+    _fields_ = [("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("acc_txn", ctypes.c_void_p),
+                ("tables", ctypes.c_void_p), ("n_acc", ctypes.c_uint64), ("n_txn", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("n_txn", ctypes.c_uint64), ("n_acc", ctypes.c_uint64),
+                ("committed", ctypes.c_uint64), ("aborted", ctypes.c_uint64),
+                ("write_cnt", ctypes.c_uint64), ("read_digest", ctypes.c_uint64),
+                ("rounds", ctypes.c_uint32), ("sort_passes", ctypes.c_uint32),
+                ("ms_total", ctypes.c_float), ("ms_probe", ctypes.c_float),
+                ("ms_sort", ctypes.c_float), ("ms_decide", ctypes.c_float),
+                ("ms_exec", ctypes.c_float), ("ms_scatter", ctypes.c_float),
+                ("scatter_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class YcsbParams(ctypes.Structure):
+    _fields_ = [("synth_table_size", ctypes.c_uint64), ("part_cnt", ctypes.c_uint32),
+                ("req_per_query", ctypes.c_uint32), ("zipf_theta", ctypes.c_double),
+                ("txn_write_perc", ctypes.c_double), ("tup_write_perc", ctypes.c_double),
+                ("part_per_txn", ctypes.c_uint32), ("strict_ppt", ctypes.c_uint32),
+                ("mpr", ctypes.c_double)]
+
+
+# every symbol include/dvcc.h declares: (name, restype, argtypes)
+_P = ctypes.POINTER
+_vp = ctypes.c_void_p
+SIGNATURES = [
+    ("dv_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("dv_device_count", ctypes.c_int, [_P(ctypes.c_int)]),
+    ("dv_open", ctypes.c_int, [_P(_vp), _P(Config)]),
+    ("dv_close", None, [_vp]),
+    ("dv_stream", _vp, [_vp]),
+    ("dv_set_stream", ctypes.c_int, [_vp, _vp]),
+    ("dv_create_table", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.c_uint32]),
+    ("dv_load_table", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64]),
+    ("dv_load_ycsb_partition", ctypes.c_int, [_vp, ctypes.c_uint64]),
+    ("dv_read_rows", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint64, _vp]),
+    ("dv_read_table", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, _vp]),
+    ("dv_epoch_run", ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, _vp,
+                                    _P(Stats)]),
+    ("dv_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _P(Stats)]),
+    ("dv_epoch_begin", ctypes.c_int, [_vp, _P(EpochDev), _vp]),
+    ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
+    ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),
+    ("dv_epoch_finish", ctypes.c_int, [_vp, _vp, _P(Stats)]),
+    ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.c_uint32, _vp, _vp, _vp]),
+]
+
+_lib = None
+
+
+def lib():
+    """Loads libdvcc.so; raises if the HIP extension has not been built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"libdvcc.so not found at {LIB_PATH}: build it with "
+                f"`python deneva-plus_amd/build.py` (there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc, what=""):
+    if rc != DV_OK:
+        raise DvccError(rc, what)
+    return rc

@@ -1,0 +1,186 @@
+"""Host-side mirror of Deneva's CC plugin surface over the HIP engine.
+
+`CCEngine` is what a workload driver calls once per epoch instead of calling
+Row_lock::lock_get/lock_release, OptCC::validate/finish, Row_occ and
+IndexHash::index_read once per access (concurrency_control/row_lock.cpp:52-373,
+occ.cpp:42-294, row_occ.cpp:33-79, storage/index_hash.cpp:137-153).  Return
+values keep the reference's meaning: commit byte 1 == RCOK/Commit, 0 == Abort.
+
+Everything here is plumbing around libdvcc.so: no decision is computed in
+Python, and nothing falls back to the CPU.
+"""
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_void_p(int(a.data_ptr()))  # torch tensor (device memory)
+
+
+@dataclass
+class Epoch:
+    """One host-side epoch in sequence order."""
+    keys: np.ndarray       # uint64 [n_acc]
+    types: np.ndarray      # uint8  [n_acc] RD/WR/SCAN
+    txn_begin: np.ndarray  # uint32 [n_txn+1]
+    tables: np.ndarray = None  # uint8 [n_acc] or None (all table 0)
+
+    @property
+    def n_txn(self):
+        return len(self.txn_begin) - 1
+
+    @property
+    def n_acc(self):
+        return int(self.txn_begin[-1])
+
+    def acc_txn(self):
+        counts = np.diff(self.txn_begin.astype(np.int64))
+        return np.repeat(np.arange(self.n_txn, dtype=np.uint32), counts)
+
+    def to_access_array(self):
+        a = np.zeros(self.n_acc, dtype=[("key", "<u8"), ("txn_seq", "<u4"), ("type", "u1"),
+                                        ("table", "u1"), ("flags", "<u2")])
+        a["key"] = self.keys
+        a["txn_seq"] = self.acc_txn()
+        a["type"] = self.types
+        if self.tables is not None:
+            a["table"] = self.tables
+        return a
+
+
+class DeviceEpoch:
+    """An epoch resident in HBM (torch tensors used as device buffers)."""
+
+    def __init__(self, epoch, device="cuda"):
+        import torch
+        self.n_txn = epoch.n_txn
+        self.n_acc = epoch.n_acc
+        self.keys = torch.from_numpy(epoch.keys.view(np.int64)).to(device)
+        self.types = torch.from_numpy(epoch.types).to(device)
+        self.acc_txn = torch.from_numpy(epoch.acc_txn().view(np.int32)).to(device)
+        self.tables = (torch.from_numpy(epoch.tables).to(device)
+                       if epoch.tables is not None else None)
+
+    @classmethod
+    def from_tensors(cls, keys, types, acc_txn, n_txn, tables=None):
+        self = cls.__new__(cls)
+        self.keys, self.types, self.acc_txn, self.tables = keys, types, acc_txn, tables
+        self.n_acc = int(keys.numel())
+        self.n_txn = int(n_txn)
+        return self
+
+    def desc(self):
+        return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
+                          self.tables.data_ptr() if self.tables is not None else None,
+                          self.n_acc, self.n_txn, 0)
+
+
+class CCEngine:
+    """One context = one GPU (one process per GPU)."""
+
+    def __init__(self, cc_alg, max_txn, max_acc, device=0, part_cnt=1, part_id=0, timing=False,
+                 workload=L.YCSB):
+        if isinstance(cc_alg, str):
+            cc_alg = L.CC_NAMES[cc_alg.upper()]
+        self.cc_alg = cc_alg
+        self.part_cnt, self.part_id = part_cnt, part_id
+        self.max_txn, self.max_acc = max_txn, max_acc
+        cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc,
+                       L.FLAG_TIMING if timing else 0, 0)
+        self._ctx = ctypes.c_void_p()
+        L.check(L.lib().dv_open(ctypes.byref(self._ctx), ctypes.byref(cfg)), "dv_open")
+
+    def close(self):
+        if self._ctx:
+            L.lib().dv_close(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream_ptr(self):
+        return L.lib().dv_stream(self._ctx)
+
+    def set_stream(self, stream):
+        """Run on an external hipStream_t (e.g. torch's current stream); None =
+        the context's own stream."""
+        L.check(L.lib().dv_set_stream(self._ctx, stream), "dv_set_stream")
+
+    # ---- storage (Workload::init_schema / init_table; IndexHash::index_insert)
+    def load_ycsb_partition(self, rows_per_part):
+        L.check(L.lib().dv_load_ycsb_partition(self._ctx, rows_per_part), "dv_load_ycsb_partition")
+
+    def create_table(self, table, capacity_rows, nbuckets, hash_kind=L.HASH_MOD):
+        L.check(L.lib().dv_create_table(self._ctx, table, capacity_rows, nbuckets, hash_kind),
+                "dv_create_table")
+
+    def load_table(self, table, keys, f0=None):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        f0 = None if f0 is None else np.ascontiguousarray(f0, dtype=np.uint64)
+        L.check(L.lib().dv_load_table(self._ctx, table, _ptr(keys), _ptr(f0), len(keys)),
+                "dv_load_table")
+
+    def read_table(self, first_row, n, table=0):
+        out = np.zeros(n, dtype=np.uint64)
+        L.check(L.lib().dv_read_table(self._ctx, table, first_row, n, _ptr(out)), "dv_read_table")
+        return out
+
+    def read_rows(self, keys, table=0):
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        out = np.zeros(len(keys), dtype=np.uint64)
+        L.check(L.lib().dv_read_rows(self._ctx, table, _ptr(keys), len(keys), _ptr(out)),
+                "dv_read_rows")
+        return out
+
+    # ---- one epoch from host buffers
+    def run_epoch(self, epoch, want_grant=False):
+        acc = epoch.to_access_array()
+        tb = np.ascontiguousarray(epoch.txn_begin, dtype=np.uint32)
+        commit = np.zeros(max(1, epoch.n_txn), dtype=np.uint8)
+        grant = np.zeros(max(1, epoch.n_acc), dtype=np.uint32) if want_grant else None
+        st = L.Stats()
+        L.check(L.lib().dv_epoch_run(self._ctx, _ptr(acc), epoch.n_acc, _ptr(tb), epoch.n_txn,
+                                     None, _ptr(commit), _ptr(grant), ctypes.byref(st)),
+                "dv_epoch_run")
+        return commit[:epoch.n_txn], (grant[:epoch.n_acc] if want_grant else None), st
+
+    # ---- one epoch already resident in HBM
+    def run_epoch_device(self, dep, d_commit=None, d_grant=None):
+        st = L.Stats()
+        desc = dep.desc()
+        L.check(L.lib().dv_epoch_run_device(self._ctx, ctypes.byref(desc), _ptr(d_commit),
+                                            _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
+        return st
+
+    # ---- staged form (multi-partition epochs)
+    def begin(self, dep, d_grant=None):
+        self._desc = dep.desc()
+        L.check(L.lib().dv_epoch_begin(self._ctx, ctypes.byref(self._desc), _ptr(d_grant)),
+                "dv_epoch_begin")
+
+    def round_local(self, d_verdict):
+        L.check(L.lib().dv_epoch_round_local(self._ctx, _ptr(d_verdict)), "dv_epoch_round_local")
+
+    def round_apply(self, d_verdict):
+        und = ctypes.c_uint32()
+        L.check(L.lib().dv_epoch_round_apply(self._ctx, _ptr(d_verdict), ctypes.byref(und)),
+                "dv_epoch_round_apply")
+        return und.value
+
+    def finish(self, d_commit=None):
+        st = L.Stats()
+        L.check(L.lib().dv_epoch_finish(self._ctx, _ptr(d_commit), ctypes.byref(st)),
+                "dv_epoch_finish")
+        return st

@@ -1,0 +1,136 @@
+"""Partitioned epochs across the GPUs of one node.
+
+One process per GPU; rank r owns partition r (PART_CNT == world size,
+GET_NODE_ID(part) == part, system/global.h:294).  Per epoch:
+
+1. every rank holds the accesses of its own client batch (its "home" txns),
+   grouped by owner rank = key % PART_CNT (YCSBWorkload::key_to_part,
+   benchmarks/ycsb_wl.cpp:69-74) -- the host does this split;
+2. one all-to-all moves each fragment to its owner -- it replaces RQRY
+   messages through msg_queue/nanomsg (ycsb_txn.cpp:160-175,
+   system/msg_queue.cpp, transport/transport.cpp:224-304);
+3. received fragments are concatenated in origin order, which *is* Calvin's
+   global lock order (epoch, origin node, position) (work_queue.cpp:105-151),
+   so the owner sorts them stably by row;
+4. NO_WAIT / WAIT_DIE / OCC: decision rounds; after each local round the
+   per-txn verdict bytes are combined with an all-reduce(MAX), which is the
+   vote combine of TxnManager::received_response (system/txn.cpp:544-554)
+   applied to every txn of the epoch at once; CALVIN needs no votes;
+5. every rank executes the committed accesses on its own rows.
+
+Decisions are identical to the single-thread E-schedule over the whole
+epoch, whatever the number of GPUs.
+
+The collectives go through torch.distributed: backend "nccl" is RCCL over
+xGMI on the GPU box; "gloo" runs the same protocol on CPU tensors in tests.
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .engine import Epoch
+
+
+def split_by_owner(epoch, txn_base, world):
+    """Host-side split of one origin batch into per-owner fragments.
+
+    Returns (keys, types, txn, counts): arrays ordered by owner rank and, inside
+    an owner, by (txn, request position); txn is the global sequence number
+    txn_base + local txn index."""
+    keys = epoch.keys
+    owner = (keys % np.uint64(world)).astype(np.int64)
+    order = np.argsort(owner, kind="stable")
+    txn = epoch.acc_txn().astype(np.int64) + txn_base
+    counts = np.bincount(owner, minlength=world)
+    return (keys[order], epoch.types[order], txn[order].astype(np.int32), counts)
+
+
+class PartitionedEpoch:
+    """One rank's outgoing fragments of one epoch, resident on `device`."""
+
+    def __init__(self, batch, rank, world, txns_per_rank, device):
+        k, t, x, counts = split_by_owner(batch, rank * txns_per_rank, world)
+        self.send_counts = [int(c) for c in counts]
+        self.keys = torch.from_numpy(k.view(np.int64)).to(device)
+        self.types = torch.from_numpy(t).to(device)
+        self.txn = torch.from_numpy(x).to(device)
+        self.n_txn_global = txns_per_rank * world
+
+
+class PartitionedRunner:
+    """Runs epochs over `engine`, a CC engine bound to this rank's partition
+    (CCEngine on the GPU; a test double on CPU)."""
+
+    def __init__(self, engine, world, rank, group=None, device="cuda"):
+        self.engine = engine
+        self.world, self.rank, self.group = world, rank, group
+        self.device = device
+
+    def exchange_counts(self, pe):
+        send = torch.tensor(pe.send_counts, dtype=torch.int64, device=self.device)
+        recv = torch.empty_like(send)
+        dist.all_to_all_single(recv, send, group=self.group)
+        return [int(c) for c in recv.cpu().tolist()]
+
+    def exchange(self, pe, recv_counts):
+        """All-to-all of the access fragments (keys, types, global txn)."""
+        n = sum(recv_counts)
+        out = []
+        for src, dt in ((pe.keys, torch.int64), (pe.types, torch.uint8), (pe.txn, torch.int32)):
+            dst = torch.empty(n, dtype=dt, device=self.device)
+            dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
+                                   input_split_sizes=pe.send_counts, group=self.group)
+            out.append(dst)
+        return out
+
+    def run(self, pe, recv_counts=None, commit=None):
+        """One partitioned epoch.  Returns (stats of this rank, rounds)."""
+        if recv_counts is None:
+            recv_counts = self.exchange_counts(pe)
+        keys, types, txn = self.exchange(pe, recv_counts)
+        n_txn = pe.n_txn_global
+        self.engine.begin_partition(keys, types, txn, n_txn)
+        rounds = 0
+        if self.engine.needs_votes:
+            verdict = torch.zeros((n_txn + 3) // 4 * 4, dtype=torch.uint8, device=self.device)
+            prev = n_txn + 1
+            while True:
+                self.engine.round_local(verdict)
+                dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=self.group)
+                rounds += 1
+                und = self.engine.round_apply(verdict)
+                if und == 0:
+                    break
+                if und >= prev:  # every round decides the lowest undecided txn
+                    raise RuntimeError(f"decision rounds stalled at {und} undecided txns")
+                prev = und
+        st = self.engine.finish(commit)
+        return st, rounds
+
+
+class EnginePartition:
+    """Gives CCEngine the partition interface PartitionedRunner drives.  The
+    engine is bound to torch's current stream (dv_set_stream), so its kernels,
+    the RCCL collectives and torch's own copies are ordered on one stream."""
+
+    def __init__(self, engine):
+        self.engine = engine
+        self.needs_votes = engine.cc_alg != 10  # CALVIN has no votes
+        engine.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def begin_partition(self, keys, types, txn, n_txn):
+        from .engine import DeviceEpoch
+        self._dep = DeviceEpoch.from_tensors(keys, types, txn, n_txn)
+        self.engine.begin(self._dep)
+
+    def round_local(self, verdict):
+        self.engine.round_local(verdict)
+
+    def round_apply(self, verdict):
+        return self.engine.round_apply(verdict)
+
+    def finish(self, commit=None):
+        return self.engine.finish(commit)
+
+
+__all__ = ["split_by_owner", "PartitionedEpoch", "PartitionedRunner", "EnginePartition", "Epoch"]

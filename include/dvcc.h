@@ -1,0 +1,201 @@
+/*
+ * dvcc.h -- C ABI of the MI355X batched concurrency-control engine.
+ *
+ * This is the drop-in boundary for Deneva's transaction-scheduling hot path.
+ * Plain pointers and sizes only; no exceptions cross it; every call returns
+ * DV_OK (0) or a negative DV_ERR_* code.  A context owns one HIP device, one
+ * stream and all device memory; it is not thread-safe (one host thread per
+ * context / GPU, like one CalvinLockThread per node).
+ *
+ * Which reference interface each entry point replaces (paths relative to the
+ * elrodrigues/deneva-plus tree):
+ *
+ *   dv_open / dv_close          row_t::init_manager (storage/row.cpp:54-74),
+ *                               Row_lock::init (concurrency_control/row_lock.cpp:24-44),
+ *                               Row_occ::init (row_occ.cpp:22-31), OptCC::init (occ.cpp:31-38)
+ *   dv_create_table /           Workload::init_schema (system/wl.cpp:31-149),
+ *   dv_load_table               IndexHash::init/index_insert (storage/index_hash.cpp:22-83),
+ *                               table_t::get_new_row (storage/table.cpp:43-54)
+ *   dv_load_ycsb_partition      YCSBWorkload::init_table_slice (benchmarks/ycsb_wl.cpp:144-203)
+ *   dv_epoch_run /              the per-epoch hot path:
+ *   dv_epoch_run_device           IndexHash::index_read (index_hash.cpp:137-153) via
+ *                                 TxnManager::index_read (system/txn.cpp:906-932);
+ *                                 Row_lock::lock_get / lock_release (row_lock.cpp:52-373)
+ *                                 for NO_WAIT, WAIT_DIE and CALVIN;
+ *                                 OptCC::validate / finish (occ.cpp:42-60, 116-294) and
+ *                                 Row_occ::access/validate/write (row_occ.cpp:33-79) for OCC;
+ *                                 Calvin's Sequencer::send_next_batch ->
+ *                                 QWorkQueue::sched_dequeue -> acquire_locks handoff
+ *                                 (sequencer.cpp:283-326, work_queue.cpp:105-151,
+ *                                 ycsb_txn.cpp:49-88);
+ *                                 YCSBTxnManager::run_ycsb_1 execution (ycsb_txn.cpp:227-254)
+ *   dv_epoch_begin /            the same path split at the points where a multi-node
+ *   dv_epoch_round_local /      Deneva exchanges RQRY/RPREPARE/RACK_PREP votes and
+ *   dv_epoch_round_apply /      combines them in TxnManager::received_response
+ *   dv_epoch_finish             (system/txn.cpp:544-554; worker_thread.cpp:277-451)
+ *   dv_read_rows /              row_t::get_value on the F0 prefix (storage/row.cpp:130-180)
+ *   dv_read_table
+ *   dv_ycsb_gen                 YCSBQueryGenerator::gen_requests_zipf
+ *                               (benchmarks/ycsb_query.cpp:29-38, 181-202, 303-376)
+ *
+ * Decisions follow SURVEY.md 8.0 ("E-schedule"): commit/abort of every txn and
+ * the final table state equal a single worker thread running the same epoch
+ * in sequence order with the reference's CC plugin.
+ */
+#ifndef DVCC_H
+#define DVCC_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes (the reference returns enum RC, system/global.h:236) */
+#define DV_OK 0
+#define DV_ERR_ARG (-1)           /* bad argument / capacity exceeded             */
+#define DV_ERR_HIP (-2)           /* HIP runtime error                            */
+#define DV_ERR_NOMEM (-3)         /* device allocation failed                     */
+#define DV_ERR_KEY_NOT_FOUND (-4) /* index probe missed (M_ASSERT_V, index_hash.cpp:225) */
+#define DV_ERR_DUP_ROW (-5)       /* 2PL/OCC txn touches one row twice (unsupported) */
+#define DV_ERR_NO_TABLE (-6)      /* table id not created / not loaded            */
+#define DV_ERR_STATE (-7)         /* call out of order (e.g. round before begin)  */
+#define DV_ERR_NO_DEVICE (-8)     /* no usable HIP device                         */
+#define DV_ERR_TXN_RANGE (-9)     /* an access names a txn >= n_txn, or txns unordered */
+
+/* CC_ALG values as in config.h */
+#define DV_NO_WAIT 1
+#define DV_WAIT_DIE 2
+#define DV_OCC 8
+#define DV_CALVIN 10
+
+/* WORKLOAD values as in config.h */
+#define DV_YCSB 1
+#define DV_TPCC 2
+
+/* access_t (system/global.h:287) */
+#define DV_RD 0
+#define DV_WR 1
+#define DV_SCAN 3
+
+/* index hash (storage/index_hash.h:86-92) */
+#define DV_HASH_YCSB 0 /* (key / part_cnt) % nbuckets */
+#define DV_HASH_MOD 1  /* key % nbuckets               */
+
+/* dv_config.flags */
+#define DV_FLAG_TIMING 1u /* record HIP-event timings per stage into dv_stats */
+
+typedef struct dv_ctx dv_ctx;
+
+typedef struct dv_config {
+    int32_t device;    /* HIP device ordinal                                  */
+    int32_t cc_alg;    /* DV_NO_WAIT / DV_WAIT_DIE / DV_OCC / DV_CALVIN       */
+    int32_t workload;  /* DV_YCSB (DV_TPCC reserved)                         */
+    uint32_t part_cnt; /* PART_CNT (config.h:14)                              */
+    uint32_t part_id;  /* partition owned by this context                     */
+    uint32_t max_txn;  /* capacity: txns per epoch (global sequence space)    */
+    uint64_t max_acc;  /* capacity: accesses per epoch handled by this context */
+    uint32_t flags;    /* DV_FLAG_*                                           */
+    uint32_t reserved;
+} dv_config;
+
+/* one request of one txn (ycsb_request, benchmarks/ycsb_query.h:35-50) */
+typedef struct dv_access {
+    uint64_t key;     /* primary key                                          */
+    uint32_t txn_seq; /* position of the txn in the epoch's sequence order    */
+    uint8_t type;     /* DV_RD / DV_WR / DV_SCAN                              */
+    uint8_t table;    /* table id                                             */
+    uint16_t flags;   /* reserved, 0                                          */
+} dv_access;
+
+/* a device-resident epoch (structure of arrays, all device pointers).
+ * Accesses are grouped by txn in sequence order: acc_txn is non-decreasing and
+ * a txn's accesses appear in its request order. */
+typedef struct dv_epoch_dev {
+    const uint64_t *keys;    /* [n_acc]                                     */
+    const uint8_t *types;    /* [n_acc] DV_RD / DV_WR / DV_SCAN             */
+    const uint32_t *acc_txn; /* [n_acc] txn sequence number of each access  */
+    const uint8_t *tables;   /* [n_acc] table ids, or NULL = all table 0    */
+    uint64_t n_acc;
+    uint32_t n_txn;          /* txns in the epoch (global sequence space)   */
+    uint32_t reserved;
+} dv_epoch_dev;
+
+typedef struct dv_stats {
+    uint64_t n_txn;
+    uint64_t n_acc;
+    uint64_t committed;   /* txn_cnt (system/txn.cpp:578)                        */
+    uint64_t aborted;     /* total_txn_abort_cnt (statistics/stats.cpp:447)     */
+    uint64_t write_cnt;   /* committed WR accesses executed                     */
+    uint64_t read_digest; /* sum over committed reads of mix64(v ^ mix64(txn<<32 ^ row)) */
+    uint32_t rounds;      /* decision rounds (0 for CALVIN)                     */
+    uint32_t sort_passes;
+    /* HIP-event timings (ms) when DV_FLAG_TIMING, else 0 */
+    float ms_total;
+    float ms_probe;
+    float ms_sort;
+    float ms_decide;
+    float ms_exec;
+    float ms_scatter;        /* sum over radix-scatter launches                */
+    uint32_t scatter_launches;
+    uint32_t reserved;
+} dv_stats;
+
+/* parameters of YCSBQueryGenerator (g_* globals, system/global.cpp:65-195) */
+typedef struct dv_ycsb_params {
+    uint64_t synth_table_size;
+    uint32_t part_cnt;
+    uint32_t req_per_query;
+    double zipf_theta;
+    double txn_write_perc;
+    double tup_write_perc;
+    uint32_t part_per_txn;
+    uint32_t strict_ppt;
+    double mpr; /* < 0: reference zipf generator; >= 0: MPR gate */
+} dv_ycsb_params;
+
+const char *dv_strerror(int code);
+int dv_device_count(int *count);
+
+int dv_open(dv_ctx **ctx, const dv_config *cfg);
+void dv_close(dv_ctx *ctx);
+void *dv_stream(dv_ctx *ctx); /* the hipStream_t the context launches on */
+/* launch on an external hipStream_t (e.g. the caller's framework stream) so the
+ * engine, the caller's copies and its RCCL collectives share one ordering;
+ * NULL restores the context's own stream */
+int dv_set_stream(dv_ctx *ctx, void *stream);
+
+/* tables: hot column = the 8-byte F0 prefix every YCSB txn reads/writes
+ * (ycsb_txn.cpp:227-254); bytes beyond it are never touched by the path (H3). */
+int dv_create_table(dv_ctx *ctx, uint32_t table, uint64_t capacity_rows, uint64_t nbuckets,
+                    uint32_t hash_kind);
+int dv_load_table(dv_ctx *ctx, uint32_t table, const uint64_t *keys, const uint64_t *f0,
+                  uint64_t n);
+int dv_load_ycsb_partition(dv_ctx *ctx, uint64_t rows_per_part); /* table 0 */
+int dv_read_rows(dv_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_t n, uint64_t *out_f0);
+int dv_read_table(dv_ctx *ctx, uint32_t table, uint64_t first_row, uint64_t n, uint64_t *out_f0);
+
+/* whole epoch from host buffers (H2D + run + D2H) */
+int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                 uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit,
+                 uint32_t *out_grant_group, dv_stats *st);
+/* whole epoch on a device-resident epoch; outputs are device pointers
+ * (d_grant_group only for DV_CALVIN, may be NULL) */
+int dv_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, uint8_t *d_commit,
+                        uint32_t *d_grant_group, dv_stats *st);
+
+/* staged form for partitioned (multi-GPU) epochs.  verdict vectors are device
+ * byte arrays of n_txn entries (rounded up to a multiple of 4); bit1 = abort,
+ * bit0 = wait; combine across partitions with an element-wise MAX. */
+int dv_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t *d_grant_group);
+int dv_epoch_round_local(dv_ctx *ctx, uint8_t *d_verdict);
+int dv_epoch_round_apply(dv_ctx *ctx, const uint8_t *d_verdict, uint32_t *undecided);
+int dv_epoch_finish(dv_ctx *ctx, uint8_t *d_commit, dv_stats *st);
+
+/* host-side epoch builder */
+int dv_ycsb_gen(const dv_ycsb_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                uint64_t *keys, uint8_t *types, uint32_t *txn_begin);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,695 @@
+/*
+ * oracle.c -- CPU restatement of Deneva's CC hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this; the product never does.  Every function cites the reference file:line
+ * (paths relative to the elrodrigues/deneva-plus tree) that it restates.
+ * Parity vs the reference binary is UNPINNED (no reference tests/fixtures exist
+ * and the reference cannot be built here); the oracle is pinned
+ * by hand-derived known-answer tests and literal-vs-indexed cross checks.
+ *
+ * Build: gcc -O2 -std=c11 -ffp-contract=off -fPIC -shared (oracle/Makefile).
+ * -ffp-contract=off keeps the zipf doubles identical to the reference's
+ * un-contracted expressions.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ myrand */
+/* system/helper.cpp:140-147: seed = (seed*1103515247 + 12345) % 2^63;
+ * return (seed / 65537) % RAND_MAX   (glibc RAND_MAX = 2147483647). */
+uint64_t or_myrand_next(uint64_t *seed) {
+    *seed = (*seed * 1103515247UL + 12345UL) % (1UL << 63);
+    return (*seed / 65537) % 2147483647UL;
+}
+
+/* -------------------------------------------------------------------- zipf */
+/* benchmarks/ycsb_query.cpp:181-186 -- note pow(1.0/i, theta), summed in order. */
+double or_zeta(uint64_t n, double theta) {
+    double sum = 0;
+    for (uint64_t i = 1; i <= n; i++) sum += pow(1.0 / i, theta);
+    return sum;
+}
+
+typedef struct {
+    uint64_t seed;
+    double zetan;         /* denom = zeta(the_n, theta)  (ycsb_query.cpp:35-36) */
+    double zeta_2_theta;  /* zeta(2, theta)              (ycsb_query.cpp:33)    */
+    double theta;
+} or_zipfgen;
+
+/* benchmarks/ycsb_query.cpp:188-202 */
+static uint64_t or_zipf(or_zipfgen *z, uint64_t n, double theta) {
+    double alpha = 1 / (1 - theta);
+    double zetan = z->zetan;
+    double eta = (1 - pow(2.0 / n, 1 - theta)) / (1 - z->zeta_2_theta / zetan);
+    double u = (double)(or_myrand_next(&z->seed) % 10000000) / 10000000;
+    double uz = u * zetan;
+    if (uz < 1) return 1;
+    if (uz < 1 + pow(0.5, theta)) return 2;
+    return 1 + (uint64_t)(n * pow(eta * u - eta + 1, alpha));
+}
+
+static int contains_u64(const uint64_t *a, uint32_t n, uint64_t v) {
+    for (uint32_t i = 0; i < n; i++)
+        if (a[i] == v) return 1;
+    return 0;
+}
+
+/* single-process cache of zeta(n, theta) (init-time work, ycsb_query.cpp:29-38) */
+static uint64_t zc_n = 0;
+static double zc_theta = -1, zc_val = 0;
+static double zeta_cached(uint64_t n, double theta) {
+    if (n != zc_n || theta != zc_theta) {
+        zc_val = or_zeta(n, theta);
+        zc_n = n;
+        zc_theta = theta;
+    }
+    return zc_val;
+}
+
+/* benchmarks/ycsb_query.cpp:303-376 (gen_requests_zipf), FIRST_PART_LOCAL=true
+ * (config.h), KEY_ORDER=false.  p->mpr >= 0 adds the MPR gate modelled on the
+ * HOT generator (ycsb_query.cpp:212-217, SURVEY 8.0 note): r_mpt is drawn
+ * first; a single-partition txn places every request on the home partition
+ * without a partition draw; a multi-partition txn draws partitions exactly as
+ * the reference does with part_limit in place of g_part_per_txn. */
+int or_ycsb_gen(const or_ycsb_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                uint64_t *keys, uint8_t *types, uint32_t *txn_begin) {
+    const uint32_t R = p->req_per_query;
+    const uint64_t table_size = p->synth_table_size / p->part_cnt;
+    if (R == 0 || R > 64 || table_size < 3 || home_part >= p->part_cnt) return -1;
+    or_zipfgen z;
+    z.seed = seed;                       /* mrand->init(seed)       (ycsb_query.cpp:31) */
+    z.theta = p->zipf_theta;
+    z.zeta_2_theta = or_zeta(2, p->zipf_theta);
+    z.zetan = zeta_cached(table_size - 1, p->zipf_theta);
+    const double txn_read_perc = 1.0 - p->txn_write_perc; /* global.cpp:86-89 */
+    const double tup_read_perc = 1.0 - p->tup_write_perc;
+    const int gate = p->mpr >= 0;
+    uint64_t all_keys[64];
+    uint64_t parts[64];
+    for (uint32_t t = 0; t < n_txn; t++) {
+        uint32_t nkeys = 0, nparts = 0;
+        uint32_t part_limit = p->part_per_txn;
+        if (gate) {
+            double r_mpt = (double)(or_myrand_next(&z.seed) % 10000) / 10000;
+            part_limit = (r_mpt < p->mpr) ? p->part_per_txn : 1;
+        }
+        double r_twr = (double)(or_myrand_next(&z.seed) % 10000) / 10000;
+        uint32_t rid = 0;
+        txn_begin[t] = t * R;
+        for (uint32_t i = 0; i < R; i++) {
+            double r = (double)(or_myrand_next(&z.seed) % 10000) / 10000;
+            uint64_t partition_id;
+            if (rid == 0) {
+                partition_id = home_part;
+            } else if (gate && part_limit == 1) {
+                partition_id = home_part;
+            } else {
+                partition_id = or_myrand_next(&z.seed) % p->part_cnt;
+                if (p->strict_ppt && part_limit <= p->part_cnt) {
+                    while ((nparts < part_limit && contains_u64(parts, nparts, partition_id)) ||
+                           (nparts == part_limit && !contains_u64(parts, nparts, partition_id)))
+                        partition_id = or_myrand_next(&z.seed) % p->part_cnt;
+                } else if (gate) {
+                    while (nparts == part_limit && !contains_u64(parts, nparts, partition_id))
+                        partition_id = or_myrand_next(&z.seed) % p->part_cnt;
+                }
+            }
+            uint8_t acctype = (r_twr < txn_read_perc || r < tup_read_perc) ? OR_RD : OR_WR;
+            uint64_t row_id = or_zipf(&z, table_size - 1, p->zipf_theta);
+            uint64_t primary_key = row_id * p->part_cnt + partition_id;
+            (void)(or_myrand_next(&z.seed) % (1 << 8)); /* req->value */
+            if (contains_u64(all_keys, nkeys, primary_key)) { /* duplicate: redo request */
+                i--;
+                continue;
+            }
+            all_keys[nkeys++] = primary_key;
+            if (!contains_u64(parts, nparts, partition_id)) parts[nparts++] = partition_id;
+            keys[(uint64_t)t * R + rid] = primary_key;
+            types[(uint64_t)t * R + rid] = acctype;
+            rid++;
+        }
+    }
+    txn_begin[n_txn] = n_txn * R;
+    return 0;
+}
+
+/* ------------------------------------------------------------------- index */
+#define NIL 0xFFFFFFFFu
+struct or_index {
+    uint64_t nbuckets;
+    uint32_t part_cnt;
+    int ycsb_hash;
+    uint64_t cap, nnodes, nitems;
+    uint32_t *first_node;   /* BucketHeader::first_node         */
+    uint64_t *node_key;     /* BucketNode::key                  */
+    uint32_t *node_next;    /* BucketNode::next                 */
+    uint32_t *node_items;   /* BucketNode::items (head of list) */
+    uint64_t *item_row;     /* itemid_t::location               */
+    uint32_t *item_next;    /* itemid_t::next                   */
+};
+
+or_index *or_index_create(uint64_t nbuckets, uint32_t part_cnt, int ycsb_hash, uint64_t cap) {
+    or_index *ix = (or_index *)calloc(1, sizeof(or_index));
+    ix->nbuckets = nbuckets;
+    ix->part_cnt = part_cnt ? part_cnt : 1;
+    ix->ycsb_hash = ycsb_hash;
+    ix->cap = cap;
+    ix->first_node = (uint32_t *)malloc(sizeof(uint32_t) * nbuckets);
+    memset(ix->first_node, 0xFF, sizeof(uint32_t) * nbuckets);
+    ix->node_key = (uint64_t *)malloc(sizeof(uint64_t) * cap);
+    ix->node_next = (uint32_t *)malloc(sizeof(uint32_t) * cap);
+    ix->node_items = (uint32_t *)malloc(sizeof(uint32_t) * cap);
+    ix->item_row = (uint64_t *)malloc(sizeof(uint64_t) * cap);
+    ix->item_next = (uint32_t *)malloc(sizeof(uint32_t) * cap);
+    return ix;
+}
+
+void or_index_free(or_index *ix) {
+    if (!ix) return;
+    free(ix->first_node);
+    free(ix->node_key);
+    free(ix->node_next);
+    free(ix->node_items);
+    free(ix->item_row);
+    free(ix->item_next);
+    free(ix);
+}
+
+/* storage/index_hash.h:86-92 */
+static uint64_t or_hash(const or_index *ix, uint64_t key) {
+    return ix->ycsb_hash ? (key / ix->part_cnt) % ix->nbuckets : key % ix->nbuckets;
+}
+
+/* storage/index_hash.cpp:69-83 + BucketHeader::insert_item 172-201: a new key is
+ * appended after the last node of the chain; a known key prepends the item. */
+int or_index_insert(or_index *ix, uint64_t key, uint64_t row) {
+    if (ix->nitems >= ix->cap) return -1;
+    uint64_t b = or_hash(ix, key);
+    uint32_t it = (uint32_t)ix->nitems++;
+    ix->item_row[it] = row;
+    ix->item_next[it] = NIL;
+    uint32_t cur = ix->first_node[b], prev = NIL;
+    while (cur != NIL) {
+        if (ix->node_key[cur] == key) break;
+        prev = cur;
+        cur = ix->node_next[cur];
+    }
+    if (cur == NIL) {
+        uint32_t nn = (uint32_t)ix->nnodes++;
+        ix->node_key[nn] = key;
+        ix->node_items[nn] = it;
+        if (prev != NIL) {
+            ix->node_next[nn] = ix->node_next[prev];
+            ix->node_next[prev] = nn;
+        } else {
+            ix->node_next[nn] = ix->first_node[b];
+            ix->first_node[b] = nn;
+        }
+    } else {
+        ix->item_next[it] = ix->node_items[cur];
+        ix->node_items[cur] = it;
+    }
+    return 0;
+}
+
+/* storage/index_hash.cpp:137-153 + BucketHeader::read_item 217-231
+ * (a missing key is fatal in the reference: M_ASSERT_V, line 225). */
+int or_index_read(const or_index *ix, uint64_t key, uint64_t *row) {
+    uint64_t b = or_hash(ix, key);
+    uint32_t cur = ix->first_node[b];
+    while (cur != NIL) {
+        if (ix->node_key[cur] == key) break;
+        cur = ix->node_next[cur];
+    }
+    if (cur == NIL) return -1;
+    *row = ix->item_row[ix->node_items[cur]];
+    return 0;
+}
+
+/* ---------------------------------------------------------------- YCSB row */
+/* ycsb_wl.cpp:173-186: set_value(0,&key,8) then set_value(fid,"hello",6) for
+ * every field: F0 bytes [0,6) = "hello\0", bytes [6,8) = bytes 6..7 of key. */
+uint64_t or_ycsb_f0_init(uint64_t key) {
+    unsigned char b[8];
+    memcpy(b, &key, 8);
+    memcpy(b, "hello", 6);
+    uint64_t v;
+    memcpy(&v, b, 8);
+    return v;
+}
+
+int or_ycsb_load(or_index *ix, uint64_t *f0, uint64_t rows_per_part, uint32_t part_cnt,
+                 uint32_t part_id) {
+    for (uint64_t r = 0; r < rows_per_part; r++) {
+        uint64_t key = r * part_cnt + part_id;
+        f0[r] = or_ycsb_f0_init(key);
+        if (or_index_insert(ix, key, r)) return -1;
+    }
+    return 0;
+}
+
+int or_index_insert_many(or_index *ix, const uint64_t *keys, const uint64_t *rows, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++)
+        if (or_index_insert(ix, keys[i], rows[i])) return -1;
+    return 0;
+}
+
+/* -------------------------------------------------------------- row lock */
+/* concurrency_control/row_lock.cpp:375-382 */
+int or_conflict_lock(int l1, int l2) {
+    if (l1 == OR_LOCK_NONE || l2 == OR_LOCK_NONE) return 0;
+    if (l1 == OR_LOCK_EX || l2 == OR_LOCK_EX) return 1;
+    return 0;
+}
+
+uint64_t or_mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+uint64_t or_table_digest(const uint64_t *f0, uint64_t n) {
+    uint64_t d = 0;
+    for (uint64_t i = 0; i < n; i++) d += or_mix64(f0[i] ^ or_mix64(i));
+    return d;
+}
+
+static uint64_t read_term(uint64_t value, uint32_t txn, uint64_t key) {
+    return or_mix64(value ^ or_mix64(((uint64_t)txn << 32) ^ key));
+}
+
+/* LockEntry (row_lock.h:20-26) with the grant group the Calvin FIFO put it in */
+typedef struct {
+    uint32_t txn;
+    uint8_t type;
+    uint32_t next;
+    uint32_t group;
+} or_entry;
+
+/* Row_lock state (row_lock.h:28-59); owners_size = 1 (row_lock.cpp:27) */
+typedef struct {
+    uint8_t *lock_type;
+    uint32_t *owner_cnt;
+    uint32_t *owners;       /* stack (STACK_PUSH) of entries */
+    uint32_t *wait_head, *wait_tail;
+    uint32_t *group;        /* grant groups started so far on the row */
+    or_entry *ent;
+    uint64_t nent;
+    const uint64_t *ts;     /* txn timestamps (WAIT_DIE) */
+} or_locks;
+
+static int locks_init(or_locks *L, uint64_t nrows, uint64_t cap) {
+    L->lock_type = (uint8_t *)malloc(nrows);
+    memset(L->lock_type, OR_LOCK_NONE, nrows);
+    L->owner_cnt = (uint32_t *)calloc(nrows, sizeof(uint32_t));
+    L->owners = (uint32_t *)malloc(nrows * sizeof(uint32_t));
+    L->wait_head = (uint32_t *)malloc(nrows * sizeof(uint32_t));
+    L->wait_tail = (uint32_t *)malloc(nrows * sizeof(uint32_t));
+    L->group = (uint32_t *)calloc(nrows, sizeof(uint32_t));
+    memset(L->owners, 0xFF, nrows * sizeof(uint32_t));
+    memset(L->wait_head, 0xFF, nrows * sizeof(uint32_t));
+    memset(L->wait_tail, 0xFF, nrows * sizeof(uint32_t));
+    L->ent = (or_entry *)malloc((cap + 1) * sizeof(or_entry));
+    L->nent = 0;
+    L->ts = NULL;
+    return (L->lock_type && L->owner_cnt && L->owners && L->wait_head && L->wait_tail &&
+            L->group && L->ent) ? 0 : -1;
+}
+
+static void locks_free(or_locks *L) {
+    free(L->lock_type);
+    free(L->owner_cnt);
+    free(L->owners);
+    free(L->wait_head);
+    free(L->wait_tail);
+    free(L->group);
+    free(L->ent);
+}
+
+static uint32_t new_entry(or_locks *L, uint32_t txn, uint8_t type) {
+    uint32_t e = (uint32_t)L->nent++;
+    L->ent[e].txn = txn;
+    L->ent[e].type = type;
+    L->ent[e].next = NIL;
+    L->ent[e].group = NIL;
+    return e;
+}
+
+/* grant an entry: STACK_PUSH(owners), owner_cnt++, lock_type = type
+ * (row_lock.cpp:171-197 and the promotion 318-358).  A grant that finds the
+ * lock free opens a new grant group; one that joins live owners shares it. */
+static void grant(or_locks *L, uint64_t r, uint32_t e, int track_owner) {
+    if (L->lock_type[r] == OR_LOCK_NONE) L->group[r]++;
+    L->ent[e].group = L->group[r] - 1;
+    if (track_owner) {
+        L->ent[e].next = L->owners[r];
+        L->owners[r] = e;
+    }
+    L->owner_cnt[r]++;
+    L->lock_type[r] = L->ent[e].type;
+}
+
+/* Row_lock::lock_get (row_lock.cpp:52-217).  Returns RC; *eout = entry. */
+static int lock_get(or_locks *L, int cc, uint64_t r, uint8_t type, uint32_t txn, uint32_t *eout) {
+    int conflict = or_conflict_lock(L->lock_type[r], type);              /* line 69 */
+    if (cc == OR_WAIT_DIE && !conflict) {                                  /* 73-77  */
+        uint32_t h = L->wait_head[r];
+        if (h != NIL && L->ts[txn] < L->ts[L->ent[h].txn]) conflict = 1;
+    }
+    if (cc == OR_CALVIN && !conflict) {                                    /* 78-81  */
+        if (L->wait_head[r] != NIL) conflict = 1;
+    }
+    if (conflict) {
+        if (cc == OR_NO_WAIT) return OR_ABORT;                             /* 86-90  */
+        if (cc == OR_WAIT_DIE) {                                           /* 91-151 */
+            int canwait = 1;
+            for (uint32_t en = L->owners[r]; en != NIL; en = L->ent[en].next)
+                if (L->ts[txn] > L->ts[L->ent[en].txn]) { canwait = 0; break; }
+            if (!canwait) return OR_ABORT;
+            return -100; /* a real wait never arises under the E-schedule */
+        }
+        /* CALVIN: FIFO append (152-170) */
+        uint32_t e = new_entry(L, txn, type);
+        if (L->wait_tail[r] == NIL) L->wait_head[r] = e;
+        else L->ent[L->wait_tail[r]].next = e;
+        L->wait_tail[r] = e;
+        *eout = e;
+        return OR_WAIT;
+    }
+    uint32_t e = new_entry(L, txn, type);
+    grant(L, r, e, cc != OR_NO_WAIT);                                      /* 171-197: NO_WAIT keeps no entry */
+    *eout = e;
+    return OR_RCOK;
+}
+
+/* Row_lock::lock_release (row_lock.cpp:220-373).  Promoted txns whose
+ * lock_ready_cnt reaches 0 are reported through ready_cb (restart_txn, 342-350). */
+static int lock_release(or_locks *L, int cc, uint64_t r, uint32_t txn, uint32_t *lr_cnt,
+                        uint32_t *ready, uint32_t *nready) {
+    if (cc == OR_NO_WAIT) {                                                /* 241-257 */
+        if (L->owner_cnt[r] == 0) return -1;
+        L->owner_cnt[r]--;
+        if (L->owner_cnt[r] == 0) L->lock_type[r] = OR_LOCK_NONE;
+    } else {                                                               /* 259-288 */
+        uint32_t en = L->owners[r], prev = NIL;
+        while (en != NIL && L->ent[en].txn != txn) {
+            prev = en;
+            en = L->ent[en].next;
+        }
+        if (en == NIL) return -1; /* assert(false) at line 290 */
+        if (prev != NIL) L->ent[prev].next = L->ent[en].next;
+        else L->owners[r] = L->ent[en].next;
+        L->owner_cnt[r]--;
+        if (L->owner_cnt[r] == 0) L->lock_type[r] = OR_LOCK_NONE;
+    }
+    /* promote compatible FIFO waiters (318-358) */
+    while (L->wait_head[r] != NIL &&
+           !or_conflict_lock(L->lock_type[r], L->ent[L->wait_head[r]].type)) {
+        uint32_t h = L->wait_head[r];
+        L->wait_head[r] = L->ent[h].next;
+        if (L->wait_head[r] == NIL) L->wait_tail[r] = NIL;
+        grant(L, r, h, cc != OR_NO_WAIT);
+        uint32_t wt = L->ent[h].txn;
+        if (--lr_cnt[wt] == 0) ready[(*nready)++] = wt;
+    }
+    return 0;
+}
+
+/* ---------------------------------------------------------- ready min-heap */
+typedef struct { uint32_t *a; uint32_t n; } heap_u32;
+static void heap_push(heap_u32 *h, uint32_t v) {
+    uint32_t i = h->n++;
+    h->a[i] = v;
+    while (i > 0) {
+        uint32_t p = (i - 1) / 2;
+        if (h->a[p] <= h->a[i]) break;
+        uint32_t t = h->a[p]; h->a[p] = h->a[i]; h->a[i] = t;
+        i = p;
+    }
+}
+static uint32_t heap_pop(heap_u32 *h) {
+    uint32_t top = h->a[0];
+    h->a[0] = h->a[--h->n];
+    uint32_t i = 0;
+    for (;;) {
+        uint32_t l = 2 * i + 1, r = l + 1, m = i;
+        if (l < h->n && h->a[l] < h->a[m]) m = l;
+        if (r < h->n && h->a[r] < h->a[m]) m = r;
+        if (m == i) break;
+        uint32_t t = h->a[m]; h->a[m] = h->a[i]; h->a[i] = t;
+        i = m;
+    }
+    return top;
+}
+
+/* ------------------------------------------------------------- the epoch */
+static int epoch_calvin(const uint64_t *keys, const uint64_t *rows, uint64_t *f0, uint64_t nrows, uint32_t n_txn,
+                        const uint32_t *tb, const uint8_t *types, uint8_t *out_commit,
+                        uint32_t *out_grant, or_epoch_stats *st) {
+    uint64_t n_acc = tb[n_txn];
+    or_locks L;
+    if (locks_init(&L, nrows, n_acc)) return -2;
+    uint32_t *lr = (uint32_t *)calloc(n_txn ? n_txn : 1, sizeof(uint32_t));
+    uint32_t *acc_ent = (uint32_t *)malloc((n_acc + 1) * sizeof(uint32_t));
+    uint32_t *acc_first = (uint32_t *)malloc((n_acc + 1) * sizeof(uint32_t)); /* calvin_locked_rows */
+    uint32_t *ready = (uint32_t *)malloc((n_txn + 1) * sizeof(uint32_t));
+    heap_u32 hp = {(uint32_t *)malloc((n_txn + 1) * sizeof(uint32_t)), 0};
+    int rc = 0;
+    /* Lock thread: acquire_locks in sequence order (ycsb_txn.cpp:49-88 and
+     * TxnManager::get_lock txn.cpp:778-788, dedup on calvin_locked_rows).  The
+     * whole epoch is sequenced before any txn executes. */
+    for (uint32_t t = 0; t < n_txn && !rc; t++) {
+        lr[t] = 1;                                   /* incr_lr() */
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++) {
+            uint64_t dup = NIL;
+            for (uint64_t b = tb[t]; b < a; b++)
+                if (acc_first[b] == b && rows[b] == rows[a]) { dup = b; break; }
+            if (dup != NIL) {
+                acc_first[a] = (uint32_t)dup;
+                acc_ent[a] = acc_ent[dup];
+                continue;
+            }
+            acc_first[a] = (uint32_t)a;
+            uint8_t lt = (types[a] == OR_RD || types[a] == OR_SCAN) ? OR_LOCK_SH : OR_LOCK_EX; /* row.cpp:190 */
+            uint32_t e;
+            int r = lock_get(&L, OR_CALVIN, rows[a], lt, t, &e);
+            acc_ent[a] = e;
+            if (r == OR_WAIT) lr[t]++;
+        }
+        if (--lr[t] == 0) heap_push(&hp, t);
+    }
+    /* Workers: run the lowest-sequence ready txn: LOC_RD then EXEC_WR
+     * (ycsb_txn.cpp:255-353), then calvin_wrapup releases calvin_locked_rows
+     * (txn.cpp:762-768 -> row.cpp:351-420 -> row_lock.cpp:220-373). */
+    uint64_t done = 0;
+    while (hp.n && !rc) {
+        uint32_t t = heap_pop(&hp);
+        done++;
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++)
+            if (types[a] == OR_RD) st->read_digest += read_term(f0[rows[a]], t, keys[a]);
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++)
+            if (types[a] == OR_WR) { f0[rows[a]] = 0; st->write_cnt++; }
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++) {
+            if (acc_first[a] != a) continue;
+            uint32_t nready = 0;
+            if (lock_release(&L, OR_CALVIN, rows[a], t, lr, ready, &nready)) { rc = -3; break; }
+            for (uint32_t k = 0; k < nready; k++) heap_push(&hp, ready[k]);
+        }
+        out_commit[t] = 1;
+    }
+    if (!rc && done != n_txn) rc = -4; /* a txn never got its locks */
+    if (!rc && out_grant)
+        for (uint64_t a = 0; a < n_acc; a++) out_grant[a] = L.ent[acc_ent[a]].group;
+    st->committed = done;
+    st->aborted = 0;
+    free(lr); free(acc_ent); free(acc_first); free(ready); free(hp.a);
+    locks_free(&L);
+    return rc;
+}
+
+/* NO_WAIT / WAIT_DIE under the E-schedule: access phase in sequence order,
+ * each txn runs to its end (get_row -> run_ycsb_1, ycsb_txn.cpp:211-254) or to
+ * its first Abort, after which cleanup releases in reverse access order and
+ * restores undo images (txn.cpp:700-776, row.cpp:365-370); survivors hold their
+ * locks until the commit phase, which releases them in sequence order. */
+static int epoch_2pl(int cc, const uint64_t *keys, const uint64_t *rows, uint64_t *f0, uint64_t nrows, uint32_t n_txn,
+                     const uint32_t *tb, const uint8_t *types, uint8_t *out_commit,
+                     or_epoch_stats *st) {
+    uint64_t n_acc = tb[n_txn];
+    or_locks L;
+    if (locks_init(&L, nrows, n_acc)) return -2;
+    uint64_t *ts = (uint64_t *)malloc((n_txn + 1) * sizeof(uint64_t));
+    /* WAIT_DIE: ts from the TS_CAS counter (manager.cpp:23-57) once per txn at
+     * first start, in sequence order (worker_thread.cpp:478-480) */
+    for (uint32_t t = 0; t < n_txn; t++) ts[t] = 1 + (uint64_t)t;
+    L.ts = ts;
+    uint64_t *undo = (uint64_t *)malloc((n_acc + 1) * sizeof(uint64_t));
+    uint64_t *rdval = (uint64_t *)malloc((n_acc + 1) * sizeof(uint64_t));
+    uint32_t dummy_lr = 0, dummy_ready[1], nready = 0;
+    int rc = 0;
+    for (uint32_t t = 0; t < n_txn && !rc; t++) {
+        uint64_t a, got = tb[t];
+        int abort = 0;
+        for (a = tb[t]; a < tb[t + 1]; a++) {
+            uint8_t lt = (types[a] == OR_RD || types[a] == OR_SCAN) ? OR_LOCK_SH : OR_LOCK_EX;
+            uint32_t e;
+            int r = lock_get(&L, cc, rows[a], lt, t, &e);
+            if (r == -100) { rc = -5; break; }
+            if (r == OR_ABORT) { abort = 1; break; }
+            got = a + 1;
+            if (types[a] == OR_WR) {             /* undo image (txn.cpp:820-841), then write 0 */
+                undo[a] = f0[rows[a]];
+                f0[rows[a]] = 0;
+            } else {
+                rdval[a] = f0[rows[a]];
+            }
+        }
+        if (rc) break;
+        if (abort) {
+            for (uint64_t b = got; b-- > tb[t];) {  /* cleanup: reverse order (txn.cpp:759-761) */
+                if (types[b] == OR_WR) f0[rows[b]] = undo[b]; /* XP restore (row.cpp:365-367) */
+                if (lock_release(&L, cc, rows[b], t, &dummy_lr, dummy_ready, &nready)) { rc = -3; break; }
+            }
+            out_commit[t] = 0;
+        } else {
+            out_commit[t] = 1;
+        }
+    }
+    /* commit phase in sequence order */
+    for (uint32_t t = 0; t < n_txn && !rc; t++) {
+        if (!out_commit[t]) { st->aborted++; continue; }
+        st->committed++;
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++) {
+            if (types[a] == OR_WR) st->write_cnt++;
+            else st->read_digest += read_term(rdval[a], t, keys[a]);
+        }
+        for (uint64_t b = tb[t + 1]; b-- > tb[t];)
+            if (lock_release(&L, cc, rows[b], t, &dummy_lr, dummy_ready, &nready)) { rc = -3; break; }
+    }
+    free(ts); free(undo); free(rdval);
+    locks_free(&L);
+    return rc;
+}
+
+/* OCC, PER_ROW_VALID=false (config.h): access phase (row_occ.cpp:33-52 copies
+ * every row), validation in sequence order (occ.cpp:116-239), finish for all
+ * after all validations (occ.cpp:248-294), commit installs the local copies
+ * (row.cpp:391-399 -> row_occ.cpp:66-73). */
+typedef struct { uint32_t txn; uint64_t tn; uint32_t n; uint64_t *rows; } or_set; /* set_ent occ.h:33-41 */
+
+static int test_valid(const or_set *s1, const uint64_t *rows2, uint32_t n2) { /* occ.cpp:319-327 */
+    for (uint32_t i = 0; i < s1->n; i++)
+        for (uint32_t j = 0; j < n2; j++)
+            if (s1->rows[i] == rows2[j]) return 0;
+    return 1;
+}
+
+static int epoch_occ(const uint64_t *keys, const uint64_t *rows, uint64_t *f0, uint64_t nrows, uint32_t n_txn,
+                     const uint32_t *tb, const uint8_t *types, uint8_t *out_commit,
+                     int literal, or_epoch_stats *st) {
+    uint64_t n_acc = tb[n_txn];
+    uint64_t tsc = 1;                                  /* glob_manager timestamp = 1 */
+    uint64_t *start_ts = (uint64_t *)malloc((n_txn + 1) * sizeof(uint64_t));
+    uint64_t *rdval = (uint64_t *)malloc((n_acc + 1) * sizeof(uint64_t));
+    int rc = 0;
+    /* access phase: start_ts per attempt (worker_thread.cpp:500-502), copy rows */
+    for (uint32_t t = 0; t < n_txn; t++) {
+        start_ts[t] = tsc++;
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++) rdval[a] = f0[rows[a]];
+    }
+    if (literal) {
+        or_set *wsets = (or_set *)calloc(n_txn + 1, sizeof(or_set));
+        uint32_t *active = (uint32_t *)malloc((n_txn + 1) * sizeof(uint32_t)); /* stack, top = end */
+        uint32_t active_len = 0;
+        uint64_t *rset = (uint64_t *)malloc((n_acc + 1) * sizeof(uint64_t));
+        for (uint32_t t = 0; t < n_txn; t++) {
+            /* get_rw_set (occ.cpp:296-317) */
+            or_set *ws = &wsets[t];
+            ws->txn = t;
+            ws->rows = (uint64_t *)malloc((tb[t + 1] - tb[t] + 1) * sizeof(uint64_t));
+            uint32_t nr = 0;
+            for (uint64_t a = tb[t]; a < tb[t + 1]; a++) {
+                if (types[a] == OR_WR) ws->rows[ws->n++] = rows[a];
+                else rset[nr++] = rows[a];
+            }
+            int readonly = ws->n == 0;
+            uint64_t finish_tn = tsc++;                /* get_ts (occ.cpp:140) */
+            uint32_t f_active_len = active_len;        /* snapshot (141-148)   */
+            int valid = 1;
+            /* history check (occ.cpp:167-180): history is only pushed in the
+             * finish phase, which follows every validation -> always empty here */
+            (void)finish_tn;
+            for (uint32_t i = 0; i < f_active_len && valid; i++) {   /* 185-199 */
+                const or_set *wact = &wsets[active[f_active_len - 1 - i]];
+                valid = test_valid(wact, rset, nr);
+                if (valid) valid = test_valid(wact, ws->rows, ws->n);
+            }
+            if (!readonly) active[active_len++] = t;   /* STACK_PUSH(active, wset) 149-152 */
+            if (!valid && !readonly) active_len--;    /* abort removes itself (219-234) */
+            out_commit[t] = (uint8_t)valid;
+        }
+        for (uint32_t t = 0; t < n_txn; t++) free(wsets[t].rows);
+        free(wsets); free(active); free(rset);
+    } else {
+        /* indexed restatement of the same predicate: the active set at txn t's
+         * validation holds exactly the write sets of earlier committed txns */
+        uint8_t *wr = (uint8_t *)calloc(nrows ? nrows : 1, 1);
+        for (uint32_t t = 0; t < n_txn; t++) {
+            int valid = 1;
+            for (uint64_t a = tb[t]; a < tb[t + 1] && valid; a++)
+                if (wr[rows[a]]) valid = 0;
+            out_commit[t] = (uint8_t)valid;
+            if (valid)
+                for (uint64_t a = tb[t]; a < tb[t + 1]; a++)
+                    if (types[a] == OR_WR) wr[rows[a]] = 1;
+        }
+        free(wr);
+    }
+    /* finish + cleanup in sequence order: committed writers install F0 = 0 */
+    for (uint32_t t = 0; t < n_txn; t++) {
+        if (!out_commit[t]) { st->aborted++; continue; }
+        st->committed++;
+        for (uint64_t a = tb[t]; a < tb[t + 1]; a++) {
+            if (types[a] == OR_WR) { f0[rows[a]] = 0; st->write_cnt++; }
+            else st->read_digest += read_term(rdval[a], t, keys[a]);
+        }
+    }
+    free(start_ts); free(rdval);
+    return rc;
+}
+
+int or_epoch_run(int cc_alg, const or_index *ix, uint64_t *f0, uint64_t nrows, uint32_t n_txn,
+                 const uint32_t *txn_begin, const uint64_t *keys, const uint8_t *types,
+                 uint8_t *out_commit, uint32_t *out_grant, int occ_literal, or_epoch_stats *st) {
+    memset(st, 0, sizeof(*st));
+    uint64_t n_acc = txn_begin[n_txn];
+    uint64_t *rows = (uint64_t *)malloc((n_acc + 1) * sizeof(uint64_t));
+    /* index probe per access (TxnManager::index_read txn.cpp:906-932) */
+    for (uint64_t a = 0; a < n_acc; a++) {
+        if (or_index_read(ix, keys[a], &rows[a]) || rows[a] >= nrows) { free(rows); return -1; }
+    }
+    int rc;
+    memset(out_commit, 0, n_txn);
+    switch (cc_alg) {
+    case OR_CALVIN:
+        rc = epoch_calvin(keys, rows, f0, nrows, n_txn, txn_begin, types, out_commit, out_grant, st);
+        break;
+    case OR_NO_WAIT:
+    case OR_WAIT_DIE:
+        rc = epoch_2pl(cc_alg, keys, rows, f0, nrows, n_txn, txn_begin, types, out_commit, st);
+        break;
+    case OR_OCC:
+        rc = epoch_occ(keys, rows, f0, nrows, n_txn, txn_begin, types, out_commit, occ_literal, st);
+        break;
+    default:
+        rc = -6;
+    }
+    free(rows);
+    return rc;
+}

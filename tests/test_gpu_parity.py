@@ -1,0 +1,201 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle on the
+same seeded epochs.  Integer work, so everything is bit-exact: per-txn commit
+bytes, Calvin grant groups, the final F0 column of every row, the committed
+read digest and the committed write count."""
+import numpy as np
+import pytest
+
+import _oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import dvcc  # noqa: E402
+from dvcc import CCEngine, DeviceEpoch, Epoch, YCSBQueryGenerator  # noqa: E402
+
+CCS = [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN]
+ORACLE_CC = {dvcc.NO_WAIT: O.NO_WAIT, dvcc.WAIT_DIE: O.WAIT_DIE, dvcc.OCC: O.OCC,
+             dvcc.CALVIN: O.CALVIN}
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a visible MI355X")
+    yield
+
+
+def _oracle_epoch(cc, tab, f0, e):
+    return O.epoch_run(ORACLE_CC[cc], tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types,
+                       want_grant=(cc == dvcc.CALVIN))
+
+
+def _gpu_epoch(eng, e, path):
+    want_grant = eng.cc_alg == dvcc.CALVIN
+    if path == "host":
+        return eng.run_epoch(e, want_grant=want_grant)
+    dep = DeviceEpoch(e)
+    d_commit = torch.zeros(max(1, e.n_txn), dtype=torch.uint8, device="cuda")
+    d_grant = (torch.zeros(max(1, e.n_acc), dtype=torch.int32, device="cuda")
+               if want_grant else None)
+    st = eng.run_epoch_device(dep, d_commit, d_grant)
+    c = d_commit.cpu().numpy()[:e.n_txn]
+    g = d_grant.cpu().numpy().view(np.uint32)[:e.n_acc] if want_grant else None
+    return c, g, st
+
+
+def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None):
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
+                   max_acc or max(1, max(e.n_acc for e in epochs)))
+    eng.load_ycsb_partition(rows)
+    assert (eng.read_table(0, rows) == f0).all()
+    for e in epochs:
+        c_ref, g_ref, st_ref = _oracle_epoch(cc, tab, f0, e)
+        c, g, st = _gpu_epoch(eng, e, path)
+        assert (c == c_ref).all(), f"commit mismatch: {int((c != c_ref).sum())} txns"
+        if cc == dvcc.CALVIN:
+            assert (g == g_ref).all(), f"grant mismatch: {int((g != g_ref).sum())}"
+        assert st.committed == st_ref.committed
+        assert st.aborted == st_ref.aborted
+        assert st.write_cnt == st_ref.write_cnt
+        assert st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == f0).all(), "table state mismatch"
+    eng.close()
+    return st
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_hand_scenario(cc):
+    txns = [[(1, 1)], [(1, 0)], [(2, 0), (3, 1)], [(2, 0)], [(2, 1)], [(3, 0)]]
+    keys = np.array([k for t in txns for k, _ in t], np.uint64)
+    types = np.array([ty for t in txns for _, ty in t], np.uint8)
+    tb = np.array([0] + list(np.cumsum([len(t) for t in txns])), np.uint32)
+    _check(cc, 8, [Epoch(keys, types, tb)])
+
+
+@pytest.mark.parametrize("path", ["device", "host"])
+@pytest.mark.parametrize("cc", CCS)
+def test_contended_epoch(cc, path):
+    g = YCSBQueryGenerator(1 << 12, zipf_theta=0.9)
+    _check(cc, 1 << 12, [g.gen(4096, 1234)], path=path)
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("n_txn,rows,theta", [(1, 1000, 0.9), (7, 1000, 0.6), (409, 999, 0.9),
+                                              (5000, 77777, 0.3), (20000, 1 << 16, 0.99)])
+def test_ragged_sizes(cc, n_txn, rows, theta):
+    g = YCSBQueryGenerator(rows, zipf_theta=theta, txn_write_perc=0.5, tup_write_perc=0.5)
+    _check(cc, rows, [g.gen(n_txn, 7 + n_txn)])
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_epochs_carry_table_state(cc):
+    g = YCSBQueryGenerator(1 << 14, zipf_theta=0.8)
+    _check(cc, 1 << 14, [g.gen(3000, s) for s in (1, 2, 3)])
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_medium_epoch(cc):
+    g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
+    _check(cc, 1 << 20, [g.gen(1 << 16, 99)])
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_empty_epoch(cc):
+    e = Epoch(np.zeros(0, np.uint64), np.zeros(0, np.uint8), np.zeros(1, np.uint32))
+    _check(cc, 16, [e], max_txn=4, max_acc=16)
+
+
+def test_missing_key_reports_error():
+    eng = CCEngine(dvcc.NO_WAIT, 4, 16)
+    eng.load_ycsb_partition(16)
+    e = Epoch(np.array([3, 1000], np.uint64), np.array([0, 1], np.uint8), np.array([0, 2], np.uint32))
+    with pytest.raises(dvcc.DvccError) as ex:
+        eng.run_epoch(e)
+    assert ex.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    # the context stays usable
+    e2 = Epoch(np.array([3], np.uint64), np.array([1], np.uint8), np.array([0, 1], np.uint32))
+    c, _, st = eng.run_epoch(e2)
+    assert c.tolist() == [1] and st.committed == 1
+
+
+def test_dup_row_rejected_for_2pl():
+    eng = CCEngine(dvcc.NO_WAIT, 4, 16)
+    eng.load_ycsb_partition(16)
+    e = Epoch(np.array([3, 3], np.uint64), np.array([0, 1], np.uint8), np.array([0, 2], np.uint32))
+    with pytest.raises(dvcc.DvccError) as ex:
+        eng.run_epoch(e)
+    assert ex.value.code == dvcc._lib.DV_ERR_DUP_ROW
+
+
+def test_calvin_repeat_access_keeps_first_lock_type():
+    # TxnManager::get_lock dedups on calvin_locked_rows (txn.cpp:778-788)
+    txns = [[(5, 0), (5, 1)], [(5, 0)], [(6, 1), (5, 1)], [(5, 0), (6, 0), (5, 0)]]
+    keys = np.array([k for t in txns for k, _ in t], np.uint64)
+    types = np.array([ty for t in txns for _, ty in t], np.uint8)
+    tb = np.array([0] + list(np.cumsum([len(t) for t in txns])), np.uint32)
+    e = Epoch(keys, types, tb)
+    tab = O.YcsbTable(8)
+    c_ref, g_ref, _ = O.epoch_run(O.CALVIN, tab.ix, tab.f0.copy(), 4, tb, keys, types, want_grant=True)
+    eng = CCEngine(dvcc.CALVIN, 4, 16)
+    eng.load_ycsb_partition(8)
+    c, g, _ = eng.run_epoch(e, want_grant=True)
+    assert (c == c_ref).all() and (g == g_ref).all()
+
+
+def test_chained_index_table():
+    # dv_load_table with key % nbuckets chains (index_hash.cpp:69-83, 217-231)
+    rows = 5000
+    rng = np.random.default_rng(3)
+    keys = rng.permutation(np.arange(rows, dtype=np.uint64) * 7 + 3)
+    f0 = rng.integers(1, 2**63, size=rows, dtype=np.uint64)
+    ix = O.MultiIndex(97, 1, 0, list(zip(keys.tolist(), range(rows))))
+    n_txn, R = 2000, 6
+    ak = keys[rng.integers(0, rows // 10, size=n_txn * R)]
+    at = rng.integers(0, 2, size=n_txn * R).astype(np.uint8)
+    # drop repeated keys inside a txn
+    for t in range(n_txn):
+        seen = set()
+        for j in range(R):
+            while int(ak[t * R + j]) in seen:
+                ak[t * R + j] = keys[rng.integers(0, rows)]
+            seen.add(int(ak[t * R + j]))
+    tb = (np.arange(n_txn + 1) * R).astype(np.uint32)
+    for cc in CCS:
+        ref_f0 = f0.copy()
+        c_ref, g_ref, st_ref = O.epoch_run(ORACLE_CC[cc], ix.ix, ref_f0, n_txn, tb, ak, at,
+                                           want_grant=cc == dvcc.CALVIN)
+        eng = CCEngine(cc, n_txn, n_txn * R)
+        eng.create_table(0, rows, 97, dvcc.HASH_MOD)
+        eng.load_table(0, keys, f0)
+        c, g, st = eng.run_epoch(Epoch(ak, at, tb), want_grant=cc == dvcc.CALVIN)
+        assert (c == c_ref).all()
+        if cc == dvcc.CALVIN:
+            assert (g == g_ref).all()
+        assert st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == ref_f0).all()
+        assert (eng.read_rows(keys[:100]) == ref_f0[:100]).all()
+        eng.close()
+
+
+# ---- BASELINE.json sizes (configs B, C, D at N=1), bit-exact against the oracle
+@pytest.mark.slow
+def test_config_b_calvin_full():
+    g = YCSBQueryGenerator(16_777_216, zipf_theta=0.6, txn_write_perc=1.0, tup_write_perc=0.5)
+    _check(dvcc.CALVIN, 16_777_216, [g.gen(65_536, dvcc.epoch_seed(0, 0))])
+
+
+@pytest.mark.slow
+def test_config_c_occ_full():
+    g = YCSBQueryGenerator(100_000_000, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    st = _check(dvcc.OCC, 100_000_000, [g.gen(1_048_576, dvcc.epoch_seed(0, 0))])
+    assert st.rounds > 1
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_config_d_single_partition_full(cc):
+    g = YCSBQueryGenerator(16_777_216, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    _check(cc, 16_777_216, [g.gen(1_048_576, dvcc.epoch_seed(0, 1))])
