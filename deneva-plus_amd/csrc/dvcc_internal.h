@@ -24,14 +24,18 @@ enum : uint8_t { V_WAIT = 1, V_ABORT = 2 };
 //   head: first access of a row segment; dup: repeat access of the same txn to
 //   the same row; bnd: Calvin grant-group boundary.
 constexpr uint32_t EL_WR = 1u, EL_HEAD = 2u, EL_DUP = 4u, EL_BND = 8u;
+// decision-round arrays reuse bit 3: the access is already OK (verdict pushed)
+constexpr uint32_t EL_DONE = 8u;
 constexpr uint32_t kMaxTxn = 1u << 28;
 
 // device counters block (zeroed per epoch)
 struct Counters {
-    uint32_t err;         // DV_ERR_* code (negated into positive bits) of the first failure
+    uint32_t err;         // ERRB_* bits of every failure seen
     uint32_t undecided;   // txns still undecided after the last round
     uint32_t committed;
     uint32_t pad0;
+    uint32_t nlive[2];    // live accesses of the current / next decision round
+    uint32_t pad1[2];
     unsigned long long write_cnt;
     unsigned long long read_digest;
 };
@@ -76,10 +80,19 @@ void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int ca
 void calvin_grant(hipStream_t s, const uint32_t *el, const uint32_t *vals, uint64_t n,
                   uint32_t *grant_out, uint8_t *ew, uint32_t *agg_f, uint32_t *agg_v,
                   uint32_t *carry);
-void round_local(hipStream_t s, int nowait, const uint32_t *el, uint64_t n, const uint8_t *status,
-                 uint8_t *verdict, uint32_t *agg_f, uint32_t *agg_v, uint32_t *carry);
-void launch_round_apply(hipStream_t s, uint8_t *status, uint8_t *verdict, uint32_t n_txn_pad4,
-                        Counters *ctr);
+// decision rounds (dvcc_rounds.hip)
+void rounds_epoch_init(hipStream_t s, const uint32_t *acc_txn, uint32_t n_acc, uint32_t n_txn_pad,
+                       uint32_t *need, uint8_t *abortf, Counters *ctr);
+void round_scan(hipStream_t s, int nowait, const uint32_t *el_in, uint32_t *el_out, uint32_t ub_in,
+                const uint32_t *n_in, uint32_t *n_out, const uint8_t *status, uint32_t *need,
+                uint8_t *abortf, uint32_t *agg_f, uint32_t *agg_v, uint32_t *agg_c, uint32_t *carry,
+                uint32_t *off, Counters *ctr);
+void round_settle(hipStream_t s, uint8_t *status, const uint32_t *need, const uint8_t *abortf,
+                  uint32_t n_txn_pad, Counters *ctr);
+void round_verdict(hipStream_t s, const uint8_t *status, const uint32_t *need, const uint8_t *abortf,
+                   uint32_t n_txn_pad, uint8_t *verdict);
+void round_apply(hipStream_t s, uint8_t *status, const uint8_t *verdict, uint32_t n_txn_pad,
+                 Counters *ctr);
 void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4,
                         uint8_t value);
 void launch_exec(hipStream_t s, int calvin, const uint64_t *pairs, const uint32_t *el,

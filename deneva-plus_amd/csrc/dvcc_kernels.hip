@@ -320,7 +320,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_prepare(const uint64_t *__restri
             }
         }
         if (dup && !calvin) set_err(ctr, ERRB_DUP);
-        el[i] = (txn << 4) | (bnd ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr;
+        el[i] = (txn << 4) | ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr;
     }
 }
 
@@ -341,13 +341,6 @@ struct SegPair {
     uint32_t v;
 };
 
-// OR of status bits: bit0 committed, bit1 undecided (any access); bit2
-// committed, bit3 undecided (WR accesses); bit4 = the element's own txn is
-// undecided (not used by the verdict).
-struct OpRound {
-    static constexpr uint32_t kId = 0;
-    __device__ static uint32_t comb(uint32_t a, uint32_t b) { return a | b; }
-};
 // Calvin: low 31 bits count grant-group boundaries, bit 31 = a WR access seen
 struct OpCalvin {
     static constexpr uint32_t kId = 0;
@@ -395,19 +388,6 @@ __device__ __forceinline__ int load_el(const uint32_t *__restrict__ el, uint64_t
     return cnt;
 }
 
-// value functors
-struct ValRound {
-    const uint8_t *status;
-    int nowait;
-    __device__ uint32_t operator()(uint32_t e) const {
-        const uint8_t s = status[e >> 4];
-        const uint32_t wr = e & EL_WR;
-        uint32_t v = 0;
-        if (s == ST_COMMIT) v = (nowait ? 1u : 0u) | (wr ? 4u : 0u);
-        else if (s == ST_UNDEC) v = (nowait ? 2u : 0u) | (wr ? 8u : 0u) | 16u;
-        return v;
-    }
-};
 struct ValCalvin {
     __device__ uint32_t operator()(uint32_t e) const {
         return ((e & EL_BND) ? 1u : 0u) | ((e & EL_WR) ? 0x80000000u : 0u);
@@ -473,18 +453,6 @@ __global__ __launch_bounds__(1024) void k_segscan_blocks(const uint32_t *__restr
 }
 
 // downsweep: per element exclusive value -> apply
-struct ApplyRound {
-    uint8_t *verdict;
-    int nowait;
-    __device__ void operator()(uint64_t /*i*/, uint32_t e, uint32_t excl, uint32_t v) const {
-        if (!(v & 16u)) return;  // own txn already decided
-        const uint32_t sel = (nowait && (e & EL_WR)) ? (excl & 3u) : ((excl >> 2) & 3u);
-        if (!sel) return;
-        const uint32_t code = (sel & 1u) ? V_ABORT : V_WAIT;
-        const uint32_t txn = e >> 4;
-        atomicOr(reinterpret_cast<uint32_t *>(verdict) + (txn >> 2), code << ((txn & 3u) * 8u));
-    }
-};
 struct ApplyCalvin {
     const uint32_t *vals;
     uint32_t *grant;
@@ -550,50 +518,6 @@ void calvin_grant(hipStream_t s, const uint32_t *el, const uint32_t *vals, uint6
                   uint32_t *grant_out, uint8_t *ew, uint32_t *agg_f, uint32_t *agg_v,
                   uint32_t *carry) {
     segscan<OpCalvin>(s, el, n, ValCalvin{}, ApplyCalvin{vals, grant_out, ew}, agg_f, agg_v, carry);
-}
-
-void round_local(hipStream_t s, int nowait, const uint32_t *el, uint64_t n, const uint8_t *status,
-                 uint8_t *verdict, uint32_t *agg_f, uint32_t *agg_v, uint32_t *carry) {
-    segscan<OpRound>(s, el, n, ValRound{status, nowait}, ApplyRound{verdict, nowait}, agg_f, agg_v,
-                     carry);
-}
-
-// --------------------------------------------------- per-txn round apply
-__global__ __launch_bounds__(kBlock) void k_round_apply(uint32_t *__restrict__ status4,
-                                                        uint32_t *__restrict__ verdict4, uint32_t nw,
-                                                        Counters *ctr) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t und = 0;
-    if (i < nw) {
-        uint32_t s = status4[i];
-        const uint32_t v = verdict4[i];
-        uint32_t ns = 0;
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-            uint32_t sb = (s >> (8 * b)) & 0xFFu;
-            const uint32_t vb = (v >> (8 * b)) & 0xFFu;
-            if (sb == ST_UNDEC) {
-                if (vb & V_ABORT) sb = ST_ABORT;
-                else if (vb & V_WAIT) { sb = ST_UNDEC; und++; }
-                else sb = ST_COMMIT;
-            }
-            ns |= sb << (8 * b);
-        }
-        status4[i] = ns;
-        verdict4[i] = 0;
-    }
-    // wave sum then one atomic per wave
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) und += __shfl_down(und, off, 64);
-    if ((threadIdx.x & 63) == 0 && und) atomicAdd(&ctr->undecided, und);
-}
-
-void launch_round_apply(hipStream_t s, uint8_t *status, uint8_t *verdict, uint32_t n_txn_pad4,
-                        Counters *ctr) {
-    const uint32_t nw = n_txn_pad4 / 4;
-    if (!nw) return;
-    k_round_apply<<<(nw + kBlock - 1) / kBlock, kBlock, 0, s>>>(
-        reinterpret_cast<uint32_t *>(status), reinterpret_cast<uint32_t *>(verdict), nw, ctr);
 }
 
 __global__ void k_status_init(uint8_t *status, uint32_t n_txn, uint32_t n_pad, uint8_t value) {

@@ -47,6 +47,10 @@ struct dv_ctx {
     uint8_t *ew = nullptr;
     uint32_t *counts = nullptr, *digit_tot = nullptr;
     uint32_t *agg_f = nullptr, *agg_v = nullptr, *carry = nullptr;
+    uint32_t *agg_c = nullptr, *off = nullptr;      // decision-round compaction
+    uint32_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
+    uint32_t *need = nullptr;                        // per txn: accesses not yet OK
+    uint8_t *abortf = nullptr;                       // per txn: an access aborted it
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
     Counters *h_ctr = nullptr;  // pinned host mirror
@@ -64,6 +68,7 @@ struct dv_ctx {
     uint32_t n_txn = 0, n_txn_pad = 0;
     int sorted = 0;
     uint32_t rounds = 0, sort_passes = 0;
+    uint32_t live_ub = 0;  // host-side upper bound of the next round's live accesses
 
     // timing
     hipEvent_t ev[32] = {};
@@ -72,6 +77,8 @@ struct dv_ctx {
 };
 
 namespace {
+
+constexpr int kRoundsPerSync = 2;
 
 inline void dfree(void *p) {
     if (p) (void)hipFree(p);
@@ -185,7 +192,7 @@ void dv_close(dv_ctx *c) {
         dfree(t.bstart);
     }
     void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->vals[0], c->vals[1], c->el,
-                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->status,
+                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->agg_c, c->off, c->rel[0], c->rel[1], c->need, c->abortf, c->status,
                     c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
                     c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
@@ -226,7 +233,15 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r) r = dalloc(&c->agg_f, nb);
     if (!r) r = dalloc(&c->agg_v, nb);
     if (!r) r = dalloc(&c->carry, nb);
+    if (!r) r = dalloc(&c->agg_c, nb);
+    if (!r) r = dalloc(&c->off, nb);
     if (!r) r = dalloc(&c->status, c->n_txn_cap_pad);
+    if (!r && cfg->cc_alg != DV_CALVIN) {
+        r = dalloc(&c->rel[0], A);
+        if (!r) r = dalloc(&c->rel[1], A);
+        if (!r) r = dalloc(&c->need, c->n_txn_cap_pad);
+        if (!r) r = dalloc(&c->abortf, c->n_txn_cap_pad);
+    }
     if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
     if (!r) r = dalloc(&c->ctr, 1);
     if (!r && cfg->cc_alg == DV_CALVIN) {
@@ -450,6 +465,10 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     if (calvin) {
         calvin_grant(c->stream, c->el, c->vals[c->sorted], ep->n_acc, d_grant, c->ew, c->agg_f,
                      c->agg_v, c->carry);
+    } else {
+        rounds_epoch_init(c->stream, ep->acc_txn, (uint32_t)ep->n_acc, c->n_txn_pad, c->need,
+                          c->abortf, c->ctr);
+        c->live_ub = (uint32_t)ep->n_acc;
     }
     rec(c, 3);
     HIPCHK(hipGetLastError());
@@ -457,32 +476,52 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     return DV_OK;
 }
 
-// one decision round on this partition's accesses: verdict bytes (wait/abort)
-// for every undecided txn that has an access here
-int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
-    if (!c || c->phase != 1) return DV_ERR_STATE;
-    if (c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
-    uint8_t *v = d_verdict ? d_verdict : c->verdict;
-    if (d_verdict) HIPCHK(hipMemsetAsync(v, 0, c->n_txn_pad, c->stream));
-    round_local(c->stream, c->cfg.cc_alg != DV_OCC, c->el, c->n_acc, c->status, v, c->agg_f,
-                c->agg_v, c->carry);
-    HIPCHK(hipGetLastError());
-    return DV_OK;
+namespace {
+
+// enqueue one decision round (scan + push + compaction); partitioned epochs
+// then write verdict bytes, single-GPU epochs settle statuses directly
+void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
+    const uint32_t r = c->rounds;
+    const uint32_t *in = r == 0 ? c->el : c->rel[(r - 1) & 1];
+    uint32_t *out = c->rel[r & 1];
+    round_scan(c->stream, c->cfg.cc_alg != DV_OCC, in, out, c->live_ub, &c->ctr->nlive[r & 1],
+               &c->ctr->nlive[(r + 1) & 1], c->status, c->need, c->abortf, c->agg_f, c->agg_v,
+               c->agg_c, c->carry, c->off, c->ctr);
+    if (settle) round_settle(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, c->ctr);
+    else round_verdict(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, d_verdict);
+    c->rounds++;
 }
 
-int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
-    if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
-    uint8_t *v = d_verdict ? const_cast<uint8_t *>(d_verdict) : c->verdict;
-    HIPCHK(hipMemsetAsync(&c->ctr->undecided, 0, sizeof(uint32_t), c->stream));
-    launch_round_apply(c->stream, c->status, v, c->n_txn_pad, c->ctr);
-    HIPCHK(hipGetLastError());
-    c->rounds++;
+// read the counters after the last enqueued round
+int round_sync(dv_ctx *c, uint32_t *undecided) {
     int r = sync_counters(c);
     if (r) return r;
     r = err_from_bits(c->h_ctr->err);
     if (r) { c->phase = 0; return r; }
+    c->live_ub = c->h_ctr->nlive[c->rounds & 1];  // input size of the next round
     if (undecided) *undecided = c->h_ctr->undecided;
     return DV_OK;
+}
+
+}  // namespace
+
+// one decision round on this partition's accesses; writes this partition's
+// verdict byte per txn (bit1 abort, bit0 wait) into d_verdict (NULL = internal)
+int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
+    if (!c || c->phase != 1) return DV_ERR_STATE;
+    if (c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
+    enqueue_round(c, d_verdict ? d_verdict : c->verdict, false);
+    HIPCHK(hipGetLastError());
+    return DV_OK;
+}
+
+// apply verdicts combined over all partitions (MAX); returns undecided txns
+int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
+    if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
+    if (c->rounds == 0) return DV_ERR_STATE;
+    round_apply(c->stream, c->status, d_verdict ? d_verdict : c->verdict, c->n_txn_pad, c->ctr);
+    HIPCHK(hipGetLastError());
+    return round_sync(c, undecided);
 }
 
 int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
@@ -533,13 +572,16 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     int r = dv_epoch_begin(c, ep, d_grant);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN) {
-        // rounds until every txn is decided; each round decides at least the
-        // lowest undecided txn, so the undecided count strictly falls
+        // rounds until every txn is decided.  Each round decides at least the
+        // lowest undecided txn, so the undecided count strictly falls between
+        // host syncs; rounds past the fixpoint are no-ops, so several rounds are
+        // enqueued per sync.
         uint32_t prev = c->n_txn + 1;
         for (;;) {
+            for (int k = 0; k < kRoundsPerSync; k++) enqueue_round(c, nullptr, true);
             uint32_t und = 0;
-            r = dv_epoch_round_local(c, nullptr);
-            if (!r) r = dv_epoch_round_apply(c, nullptr, &und);
+            r = hip_fail(hipGetLastError(), "round launch");
+            if (!r) r = round_sync(c, &und);
             if (!r && und >= prev) r = DV_ERR_STATE;  // no progress: internal error
             if (r) { c->phase = 0; return r; }
             if (und == 0) break;
