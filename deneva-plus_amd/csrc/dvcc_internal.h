@@ -60,12 +60,12 @@ struct Tables {
 };
 
 // error bits recorded by kernels
-enum : uint32_t { ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8 };
+enum : uint32_t { ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16 };
 
 // ---- launchers (dvcc_kernels.hip) ----
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  uint64_t *pairs, uint32_t *vals, Counters *ctr);
+                  uint64_t *pairs, uint32_t *vals, uint32_t *need, Counters *ctr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -81,12 +81,13 @@ void calvin_grant(hipStream_t s, const uint32_t *el, const uint32_t *vals, uint6
                   uint32_t *grant_out, uint8_t *ew, uint32_t *agg_f, uint32_t *agg_v,
                   uint32_t *carry);
 // decision rounds (dvcc_rounds.hip)
-void rounds_epoch_init(hipStream_t s, const uint32_t *acc_txn, uint32_t n_acc, uint32_t n_txn_pad,
-                       uint32_t *need, uint8_t *abortf, Counters *ctr);
-void round_scan(hipStream_t s, int nowait, const uint32_t *el_in, uint32_t *el_out, uint32_t ub_in,
-                const uint32_t *n_in, uint32_t *n_out, const uint8_t *status, uint32_t *need,
-                uint8_t *abortf, uint32_t *agg_f, uint32_t *agg_v, uint32_t *agg_c, uint32_t *carry,
-                uint32_t *off, Counters *ctr);
+constexpr uint32_t kTileCtrs = 1024;  // per-round tile tickets, reset every kTileCtrs rounds
+void rounds_epoch_init(hipStream_t s, uint32_t n_acc, uint32_t n_txn_pad, uint32_t *need,
+                       uint8_t *abortf, uint32_t *tile_ctr, Counters *ctr);
+void round_pass(hipStream_t s, bool first, int nowait, const uint32_t *el_in, uint32_t *el_out,
+                uint32_t ub_in, const uint32_t *n_in, uint32_t *n_out, const uint8_t *status,
+                uint32_t *need, uint8_t *abortf, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag,
+                Counters *ctr);
 void round_settle(hipStream_t s, uint8_t *status, const uint32_t *need, const uint8_t *abortf,
                   uint32_t n_txn_pad, Counters *ctr);
 void round_verdict(hipStream_t s, const uint8_t *status, const uint32_t *need, const uint8_t *abortf,

@@ -79,59 +79,84 @@ __device__ __forceinline__ uint64_t bucket_of(const TableDesc &t, uint64_t key) 
     return t.hash_kind == DV_HASH_YCSB ? (key / t.part_cnt) % t.nbuckets : key % t.nbuckets;
 }
 
-template <bool VALS>
+template <bool VALS, bool NEED>
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n,
                                                   uint32_t n_txn, uint64_t *__restrict__ pairs,
-                                                  uint32_t *__restrict__ vals, Counters *ctr) {
+                                                  uint32_t *__restrict__ vals,
+                                                  uint32_t *__restrict__ need, Counters *ctr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t key = keys[i];
-        const uint32_t tb = tables ? tables[i] : 0u;
-        uint32_t txn = acc_txn[i];
-        const uint32_t wr = types[i] == DV_WR ? 1u : 0u;
-        uint64_t row = 0;
-        if (tb >= tabs.n) {
-            set_err(ctr, ERRB_TABLE);
-        } else {
-            const TableDesc &t = tabs.t[tb];
-            const uint64_t b = bucket_of(t, key);
-            bool found = false;
-            if (t.bstart == nullptr) {                // YCSB: one key per bucket
-                const IxEntry e = t.ix[b];
-                if (e.key == key) { row = e.row; found = true; }
-            } else {                                  // chained bucket (read_item 217-231)
-                for (uint32_t j = t.bstart[b], end = t.bstart[b + 1]; j < end; j++) {
-                    const IxEntry e = t.ix[j];
-                    if (e.key == key) { row = e.row; found = true; break; }
+    const uint32_t lane = threadIdx.x & 63;
+    // block-uniform trip count so every lane takes part in the wave ballots
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
+        const uint64_t i = b0 + threadIdx.x;
+        const bool valid = i < n;
+        uint32_t txn = valid ? acc_txn[i] : 0xFFFFFFFFu;
+        if (valid) {
+            const uint64_t key = keys[i];
+            const uint32_t tb = tables ? tables[i] : 0u;
+            const uint32_t wr = types[i] == DV_WR ? 1u : 0u;
+            uint64_t row = 0;
+            if (tb >= tabs.n) {
+                set_err(ctr, ERRB_TABLE);
+            } else {
+                const TableDesc &t = tabs.t[tb];
+                const uint64_t bk = bucket_of(t, key);
+                bool found = false;
+                if (t.bstart == nullptr) {                // YCSB: one key per bucket
+                    const IxEntry e = t.ix[bk];
+                    if (e.key == key) { row = e.row; found = true; }
+                } else {                                  // chained bucket (read_item 217-231)
+                    for (uint32_t j = t.bstart[bk], end = t.bstart[bk + 1]; j < end; j++) {
+                        const IxEntry e = t.ix[j];
+                        if (e.key == key) { row = e.row; found = true; break; }
+                    }
                 }
+                if (!found) set_err(ctr, ERRB_KEY);
+                row += t.row_base;
             }
-            if (!found) set_err(ctr, ERRB_KEY);
-            row += t.row_base;
+            uint32_t t_ok = txn;
+            if (txn >= n_txn || (i > 0 && acc_txn[i - 1] > txn)) {
+                set_err(ctr, ERRB_TXN);
+                t_ok = 0;
+            }
+            pairs[i] = (row << 32) | ((uint64_t)t_ok << 1) | wr;
+            if (VALS) vals[i] = (uint32_t)i;
         }
-        if (txn >= n_txn || (i > 0 && acc_txn[i - 1] > txn)) {
-            set_err(ctr, ERRB_TXN);
-            txn = 0;
+        if (NEED) {
+            // need[t] = this partition's accesses of txn t: one atomic per run of
+            // equal txns inside the wave (acc_txn is non-decreasing)
+            const uint32_t tprev = __shfl_up(txn, 1, 64);
+            const bool start = valid && (lane == 0 || tprev != txn);
+            const uint64_t smask = __ballot(start);
+            const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
+            if (start && txn < n_txn) {
+                const uint64_t above = lane == 63 ? 0ull : ((smask >> (lane + 1)) << (lane + 1));
+                const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : nvalid;
+                atomicAdd(&need[txn], next - lane);
+            }
         }
-        pairs[i] = (row << 32) | ((uint64_t)txn << 1) | wr;
-        if (VALS) vals[i] = (uint32_t)i;
     }
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  uint64_t *pairs, uint32_t *vals, Counters *ctr) {
+                  uint64_t *pairs, uint32_t *vals, uint32_t *need, Counters *ctr) {
     if (n_acc == 0) return;
     uint64_t blocks = (n_acc + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
+    const uint32_t g = (uint32_t)blocks;
     if (vals)
-        k_probe<true><<<(uint32_t)blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc,
-                                                          n_txn, pairs, vals, ctr);
+        k_probe<true, false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
+                                                  pairs, vals, need, ctr);
+    else if (need)
+        k_probe<false, true><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
+                                                  pairs, vals, need, ctr);
     else
-        k_probe<false><<<(uint32_t)blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables,
-                                                           n_acc, n_txn, pairs, vals, ctr);
+        k_probe<false, false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
+                                                   pairs, vals, need, ctr);
 }
 
 // ------------------------------------------------------------- radix sort

@@ -100,6 +100,7 @@ struct Chunk {
     uint32_t umask;  // bit j: item j's txn is undecided
 };
 
+template <bool FIRST>
 __device__ __forceinline__ void eval_chunk(const uint32_t *__restrict__ el, uint32_t n, uint32_t first,
                                            const uint8_t *__restrict__ status, int nowait, Chunk &c) {
     uint32_t next;
@@ -115,7 +116,7 @@ __device__ __forceinline__ void eval_chunk(const uint32_t *__restrict__ el, uint
             if (j + 1 < c.cnt) nh = c.e[j + 1] & EL_HEAD;
             else if (c.cnt < kIPT) nh = 1u;
             else nh = next & EL_HEAD;
-            const uint8_t s = status[c.e[j] >> 4];
+            const uint8_t s = FIRST ? (uint8_t)ST_UNDEC : status[c.e[j] >> 4];
             c.umask |= (s == ST_UNDEC ? 1u : 0u) << j;
             c.v[j] = elem_value(c.e[j], nh, s, nowait);
             if (c.e[j] & EL_HEAD) c.agg = Seg{1u, c.v[j]};
@@ -127,120 +128,143 @@ __device__ __forceinline__ void eval_chunk(const uint32_t *__restrict__ el, uint
 
 }  // namespace
 
-// ---- K1: block aggregates (segmented OR + kept count)
-__global__ __launch_bounds__(kBlock) void k_round_reduce(const uint32_t *__restrict__ el_in,
-                                                         const uint32_t *__restrict__ n_in,
-                                                         const uint8_t *__restrict__ status, int nowait,
-                                                         uint32_t *__restrict__ agg_f,
-                                                         uint32_t *__restrict__ agg_v,
-                                                         uint32_t *__restrict__ agg_c) {
+// ---- one decision round in ONE pass: decoupled look-back segmented scan.
+// Tiles take tickets in launch order (atomicAdd), publish their aggregate as
+// one 8-byte descriptor (agent-scope atomic store: the data is the flag,
+// MI355X_MICROARCH.md "Valid forms", R2), and wave 0 of each tile folds its
+// predecessors' descriptors right-to-left until it meets an inclusive prefix.
+// A tile waits only on tiles with smaller tickets, which are already running,
+// so the pass always drains; every spin is bounded (ERRB_SPIN).
+//
+// descriptor: [63:39] tag (round id) [38:37] state (1 aggregate, 2 inclusive)
+//             [36] head seen [35:31] OR value [30:0] kept count
+namespace {
+constexpr uint64_t D_AGG = 1ull, D_INC = 2ull;
+__device__ __forceinline__ uint64_t desc_pack(uint32_t tag, uint64_t state, Seg s, uint32_t cnt) {
+    return ((uint64_t)tag << 39) | (state << 37) | ((uint64_t)(s.f & 1u) << 36) |
+           ((uint64_t)(s.v & 31u) << 31) | (uint64_t)(cnt & 0x7FFFFFFFu);
+}
+__device__ __forceinline__ uint32_t desc_tag(uint64_t d) { return (uint32_t)(d >> 39); }
+__device__ __forceinline__ uint32_t desc_state(uint64_t d) { return (uint32_t)(d >> 37) & 3u; }
+__device__ __forceinline__ Seg desc_seg(uint64_t d) {
+    return Seg{(uint32_t)(d >> 36) & 1u, (uint32_t)(d >> 31) & 31u};
+}
+__device__ __forceinline__ uint32_t desc_cnt(uint64_t d) { return (uint32_t)d & 0x7FFFFFFFu; }
+constexpr uint32_t kSpinLimit = 1u << 22;
+}  // namespace
+
+template <bool FIRST>
+__global__ __launch_bounds__(kBlock) void k_round_pass(
+    const uint32_t *__restrict__ el_in, const uint32_t *__restrict__ n_in,
+    const uint8_t *__restrict__ status, int nowait, uint32_t *__restrict__ el_out,
+    uint32_t *__restrict__ n_out, uint32_t *__restrict__ need, uint8_t *__restrict__ abortf,
+    uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
+    __shared__ uint32_t s_tile;
     __shared__ Seg wt[4];
     __shared__ uint32_t wc[4];
+    __shared__ Seg s_pre;
+    __shared__ uint32_t s_pos, s_tot;
     const uint32_t n = *n_in;
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if ((uint64_t)blockIdx.x * kTile >= n) {
-        if (tid == 0) { agg_f[blockIdx.x] = 0; agg_v[blockIdx.x] = 0; agg_c[blockIdx.x] = 0; }
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    if (tile >= ntiles) {
+        if (ntiles == 0 && tile == 0 && tid == 0) { *n_out = 0; ctr->undecided = 0; }
         return;
     }
     Chunk c;
-    eval_chunk(el_in, n, blockIdx.x * kTile + tid * kIPT, status, nowait, c);
+    eval_chunk<FIRST>(el_in, n, tile * kTile + tid * kIPT, status, nowait, c);
     const Seg inc = wave_incl(c.agg, lane);
     const uint32_t ks = wave_incl_sum(c.kept, lane);
     if (lane == 63) { wt[wave] = inc; wc[wave] = ks; }
     __syncthreads();
-    if (tid == 0) {
-        Seg t = wt[0];
-        for (int w = 1; w < 4; w++) t = seg_or(t, wt[w]);
-        agg_f[blockIdx.x] = t.f;
-        agg_v[blockIdx.x] = t.v;
-        agg_c[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+    if (wave == 0) {
+        Seg agg = wt[0];
+        uint32_t cnt = wc[0];
+        for (int w = 1; w < 4; w++) { agg = seg_or(agg, wt[w]); cnt += wc[w]; }
+        Seg pre{0u, 0u};
+        uint32_t pcnt = 0;
+        if (tile == 0) {
+            if (lane == 0)
+                __hip_atomic_store(&desc[0], desc_pack(tag, D_INC, agg, cnt), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            if (lane == 0)
+                __hip_atomic_store(&desc[tile], desc_pack(tag, D_AGG, agg, cnt), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            // look-back: lane k reads tile (j - k); fold nearest-first
+            int64_t j = (int64_t)tile - 1;
+            Seg acc{0u, 0u};  // covers (window start, tile)
+            uint32_t accc = 0;
+            bool done = false;
+            uint32_t spins = 0;
+            while (!done) {
+                const int64_t t = j - (int64_t)lane;
+                uint64_t d = 0;
+                bool ready = true;
+                if (t >= 0) {
+                    d = __hip_atomic_load(&desc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ready = desc_tag(d) == tag && desc_state(d) != 0;
+                }
+                if (!__all(ready)) {
+                    if (++spins > kSpinLimit) {
+                        if (lane == 0) atomicOr(&ctr->err, ERRB_SPIN);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                // lanes with t < 0 act as an inclusive identity
+                const uint64_t incmask = __ballot(t < 0 || desc_state(d) == D_INC);
+                const uint32_t stop = incmask ? (uint32_t)__builtin_ctzll(incmask) : 64u;
+                // fold lanes 0..stop (nearest first): acc = d_k o acc
+                for (uint32_t k = 0; k < 64 && k <= stop; k++) {
+                    const uint32_t lo = __shfl((uint32_t)d, (int)k, 64);
+                    const uint32_t hi = __shfl((uint32_t)(d >> 32), (int)k, 64);
+                    const int64_t tk = j - (int64_t)k;
+                    if (tk < 0) break;
+                    const uint64_t dk = ((uint64_t)hi << 32) | lo;
+                    acc = seg_or(desc_seg(dk), acc);
+                    accc += desc_cnt(dk);
+                }
+                if (stop < 64) done = true;
+                else j -= 64;
+            }
+            pre = acc;
+            pcnt = accc;
+            if (lane == 0)
+                __hip_atomic_store(&desc[tile], desc_pack(tag, D_INC, seg_or(pre, agg), pcnt + cnt),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (lane == 0) {
+            s_pre = pre;
+            s_pos = pcnt;
+            s_tot = pcnt + cnt;
+            if (tile == 0) ctr->undecided = 0;  // re-counted by this round's settle
+        }
     }
-}
-
-// ---- K2: scan of block aggregates -> carry-in value and output offset per block
-__global__ __launch_bounds__(1024) void k_round_blocks(const uint32_t *__restrict__ agg_f,
-                                                       const uint32_t *__restrict__ agg_v,
-                                                       const uint32_t *__restrict__ agg_c, uint32_t nb,
-                                                       uint32_t *__restrict__ carry,
-                                                       uint32_t *__restrict__ off, uint32_t *n_out,
-                                                       Counters *ctr) {
-    __shared__ Seg wt[16];
-    __shared__ uint32_t wc[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t per = (nb + 1023) / 1024;
-    const uint32_t lo = tid * per;
-    const uint32_t hi = lo + per < nb ? lo + per : nb;
-    Seg a{0u, 0u};
-    uint32_t cs = 0;
-    for (uint32_t i = lo; i < hi; i++) {
-        a = seg_or(a, Seg{agg_f[i], agg_v[i]});
-        cs += agg_c[i];
-    }
-    const Seg inc = wave_incl(a, lane);
-    const uint32_t ics = wave_incl_sum(cs, lane);
-    if (lane == 63) { wt[wave] = inc; wc[wave] = ics; }
+    __syncthreads();
     Seg ex;
     ex.f = __shfl_up(inc.f, 1, 64);
     ex.v = __shfl_up(inc.v, 1, 64);
     if (lane == 0) ex = Seg{0u, 0u};
-    uint32_t exs = ics - cs;
-    __syncthreads();
-    Seg pre{0u, 0u};
-    uint32_t pres = 0, tot = 0;
-    for (uint32_t w = 0; w < 16; w++) {
-        if (w < wave) { pre = seg_or(pre, wt[w]); pres += wc[w]; }
-        tot += wc[w];
-    }
-    Seg run = seg_or(pre, ex);
-    uint32_t pos = pres + exs;
-    for (uint32_t i = lo; i < hi; i++) {
-        carry[i] = run.v;
-        off[i] = pos;
-        run = seg_or(run, Seg{agg_f[i], agg_v[i]});
-        pos += agg_c[i];
-    }
-    if (tid == 0) {
-        *n_out = tot;
-        ctr->undecided = 0;  // re-counted by the settle kernel of this round
-    }
-}
-
-// ---- K3: downsweep -- verdict push (once per access) and compaction
-__global__ __launch_bounds__(kBlock) void k_round_down(
-    const uint32_t *__restrict__ el_in, const uint32_t *__restrict__ n_in,
-    const uint8_t *__restrict__ status, int nowait, const uint32_t *__restrict__ carry,
-    const uint32_t *__restrict__ off, uint32_t *__restrict__ el_out, uint32_t *__restrict__ need,
-    uint8_t *__restrict__ abortf) {
-    __shared__ Seg wt[4];
-    __shared__ uint32_t wc[4];
-    const uint32_t n = *n_in;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if ((uint64_t)blockIdx.x * kTile >= n) return;
-    Chunk c;
-    eval_chunk(el_in, n, blockIdx.x * kTile + tid * kIPT, status, nowait, c);
-    const Seg inc = wave_incl(c.agg, lane);
-    const uint32_t ks = wave_incl_sum(c.kept, lane);
-    if (lane == 63) { wt[wave] = inc; wc[wave] = ks; }
-    Seg ex;
-    ex.f = __shfl_up(inc.f, 1, 64);
-    ex.v = __shfl_up(inc.v, 1, 64);
-    if (lane == 0) ex = Seg{0u, 0u};
-    __syncthreads();
-    Seg pre{0u, carry[blockIdx.x]};
-    uint32_t pos = off[blockIdx.x] + ks - c.kept;
+    Seg pre = s_pre;
+    uint32_t pos = s_pos + ks - c.kept;
     for (uint32_t w = 0; w < wave; w++) {
         pre = seg_or(pre, wt[w]);
         pos += wc[w];
     }
     uint32_t run = seg_or(pre, ex).v;
 #pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        if (j < c.cnt) {
-            uint32_t e = c.e[j];
-            const uint32_t v = c.v[j];
+    for (int jj = 0; jj < kIPT; jj++) {
+        if (jj < c.cnt) {
+            uint32_t e = c.e[jj];
+            const uint32_t v = c.v[jj];
             const uint32_t excl = (e & EL_HEAD) ? 0u : run;
             const uint32_t txn = e >> 4;
-            if (((c.umask >> j) & 1u) && !(e & EL_DONE)) {
+            if (((c.umask >> jj) & 1u) && !(e & EL_DONE)) {
                 // NO_WAIT/WAIT_DIE: a WR conflicts with any earlier access, a RD
                 // with earlier WRs; OCC: any access with earlier committed writes
                 const uint32_t sel = (nowait && (e & EL_WR)) ? (excl & (B_CA | B_UA))
@@ -252,12 +276,12 @@ __global__ __launch_bounds__(kBlock) void k_round_down(
                     e |= EL_DONE;
                 }
             }
-            if (v & B_KEEP) {
+            if (v & B_KEEP)
                 el_out[pos++] = (txn << 4) | (e & (EL_DONE | EL_WR)) | ((excl & B_KEEP) ? 0u : EL_HEAD);
-            }
             run = (e & EL_HEAD) ? v : (run | v);
         }
     }
+    if (tile == ntiles - 1 && tid == 0) *n_out = s_tot;
 }
 
 // ---- K4: single-GPU settle -- status from the pushed verdicts, count undecided
@@ -351,43 +375,35 @@ __global__ __launch_bounds__(kBlock) void k_round_apply(uint32_t *__restrict__ s
     }
 }
 
-// ---- per-epoch init: need[t] = this partition's accesses of txn t
-//      (input order: acc_txn is non-decreasing), live count of round 0
-__global__ __launch_bounds__(kBlock) void k_need_init(const uint32_t *__restrict__ acc_txn, uint32_t n,
-                                                      uint32_t *__restrict__ need, Counters *ctr) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->nlive[0] = n;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t t = acc_txn[i];
-        if (i + 1 < n && acc_txn[i + 1] == t) continue;  // not the txn's last access
-        uint32_t s = i;
-        while (s > 0 && acc_txn[s - 1] == t) s--;
-        need[t] = i + 1 - s;
-    }
-}
+__global__ void k_round0_init(uint32_t n, Counters *ctr) { ctr->nlive[0] = n; }
 
 // ------------------------------------------------------------- launchers
 static uint32_t grid_for_txn_words(uint32_t nw) {
     uint32_t g = (nw + kBlock - 1) / kBlock;
-    return g < 1 ? 1 : (g > 512 ? 512 : g);
+    return g < 1 ? 1 : (g > 64 ? 64 : g);
 }
 
-void rounds_epoch_init(hipStream_t s, const uint32_t *acc_txn, uint32_t n_acc, uint32_t n_txn_pad,
-                       uint32_t *need, uint8_t *abortf, Counters *ctr) {
-    (void)hipMemsetAsync(need, 0, (size_t)(n_txn_pad ? n_txn_pad : 4) * 4, s);
+// per epoch: need[] is filled by the probe (one atomic per txn run), so only
+// the flags, the tile tickets and the round-0 live count are reset here
+void rounds_epoch_init(hipStream_t s, uint32_t n_acc, uint32_t n_txn_pad, uint32_t *need,
+                       uint8_t *abortf, uint32_t *tile_ctr, Counters *ctr) {
+    (void)need;
     (void)hipMemsetAsync(abortf, 0, n_txn_pad ? n_txn_pad : 4, s);
-    uint32_t g = (n_acc + kBlock - 1) / kBlock;
-    g = g < 1 ? 1 : (g > 4096 ? 4096 : g);
-    k_need_init<<<g, kBlock, 0, s>>>(acc_txn, n_acc, need, ctr);
+    (void)hipMemsetAsync(tile_ctr, 0, kTileCtrs * sizeof(uint32_t), s);
+    k_round0_init<<<1, 1, 0, s>>>(n_acc, ctr);
 }
 
-void round_scan(hipStream_t s, int nowait, const uint32_t *el_in, uint32_t *el_out, uint32_t ub_in,
-                const uint32_t *n_in, uint32_t *n_out, const uint8_t *status, uint32_t *need,
-                uint8_t *abortf, uint32_t *agg_f, uint32_t *agg_v, uint32_t *agg_c, uint32_t *carry,
-                uint32_t *off, Counters *ctr) {
+void round_pass(hipStream_t s, bool first, int nowait, const uint32_t *el_in, uint32_t *el_out,
+                uint32_t ub_in, const uint32_t *n_in, uint32_t *n_out, const uint8_t *status,
+                uint32_t *need, uint8_t *abortf, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag,
+                Counters *ctr) {
     const uint32_t nb = ub_in ? nblocks_for(ub_in) : 1;
-    k_round_reduce<<<nb, kBlock, 0, s>>>(el_in, n_in, status, nowait, agg_f, agg_v, agg_c);
-    k_round_blocks<<<1, 1024, 0, s>>>(agg_f, agg_v, agg_c, nb, carry, off, n_out, ctr);
-    k_round_down<<<nb, kBlock, 0, s>>>(el_in, n_in, status, nowait, carry, off, el_out, need, abortf);
+    if (first)
+        k_round_pass<true><<<nb, kBlock, 0, s>>>(el_in, n_in, status, nowait, el_out, n_out, need,
+                                                  abortf, desc, tile_ctr, tag, ctr);
+    else
+        k_round_pass<false><<<nb, kBlock, 0, s>>>(el_in, n_in, status, nowait, el_out, n_out, need,
+                                                   abortf, desc, tile_ctr, tag, ctr);
 }
 
 void round_settle(hipStream_t s, uint8_t *status, const uint32_t *need, const uint8_t *abortf,

@@ -51,6 +51,9 @@ struct dv_ctx {
     uint32_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
     uint32_t *need = nullptr;                        // per txn: accesses not yet OK
     uint8_t *abortf = nullptr;                       // per txn: an access aborted it
+    uint64_t *desc = nullptr;                        // look-back tile descriptors
+    uint32_t *tile_ctr = nullptr;                    // per-round tile tickets
+    uint32_t round_tag = 0;                          // descriptor tag of the last round
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
     Counters *h_ctr = nullptr;  // pinned host mirror
@@ -136,6 +139,7 @@ int err_from_bits(uint32_t b) {
     if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
     if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
     if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
+    if (b & ERRB_SPIN) return DV_ERR_HIP;
     return DV_OK;
 }
 
@@ -192,7 +196,7 @@ void dv_close(dv_ctx *c) {
         dfree(t.bstart);
     }
     void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->vals[0], c->vals[1], c->el,
-                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->agg_c, c->off, c->rel[0], c->rel[1], c->need, c->abortf, c->status,
+                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->agg_c, c->off, c->rel[0], c->rel[1], c->need, c->abortf, c->desc, c->tile_ctr, c->status,
                     c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
                     c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
@@ -241,6 +245,9 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
         if (!r) r = dalloc(&c->rel[1], A);
         if (!r) r = dalloc(&c->need, c->n_txn_cap_pad);
         if (!r) r = dalloc(&c->abortf, c->n_txn_cap_pad);
+        if (!r) r = dalloc(&c->desc, nb);
+        if (!r) r = dalloc(&c->tile_ctr, kTileCtrs);
+        if (!r) r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)nb * 8, c->stream), "memset");
     }
     if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
     if (!r) r = dalloc(&c->ctr, 1);
@@ -453,8 +460,10 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
     HIPCHK(hipMemsetAsync(c->verdict, 0, c->n_txn_pad ? c->n_txn_pad : 4, c->stream));
     launch_status_init(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC);
+    if (!calvin) HIPCHK(hipMemsetAsync(c->need, 0, (size_t)(c->n_txn_pad ? c->n_txn_pad : 4) * 4, c->stream));
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
-                 ep->n_txn, c->pairs[0], calvin ? c->vals[0] : nullptr, c->ctr);
+                 ep->n_txn, c->pairs[0], calvin ? c->vals[0] : nullptr, calvin ? nullptr : c->need,
+                 c->ctr);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
@@ -466,8 +475,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         calvin_grant(c->stream, c->el, c->vals[c->sorted], ep->n_acc, d_grant, c->ew, c->agg_f,
                      c->agg_v, c->carry);
     } else {
-        rounds_epoch_init(c->stream, ep->acc_txn, (uint32_t)ep->n_acc, c->n_txn_pad, c->need,
-                          c->abortf, c->ctr);
+        rounds_epoch_init(c->stream, (uint32_t)ep->n_acc, c->n_txn_pad, c->need, c->abortf,
+                          c->tile_ctr, c->ctr);
         c->live_ub = (uint32_t)ep->n_acc;
     }
     rec(c, 3);
@@ -484,9 +493,15 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     const uint32_t r = c->rounds;
     const uint32_t *in = r == 0 ? c->el : c->rel[(r - 1) & 1];
     uint32_t *out = c->rel[r & 1];
-    round_scan(c->stream, c->cfg.cc_alg != DV_OCC, in, out, c->live_ub, &c->ctr->nlive[r & 1],
-               &c->ctr->nlive[(r + 1) & 1], c->status, c->need, c->abortf, c->agg_f, c->agg_v,
-               c->agg_c, c->carry, c->off, c->ctr);
+    if (r > 0 && r % kTileCtrs == 0)
+        (void)hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream);
+    if (++c->round_tag >= (1u << 25)) {  // descriptor tags are 25 bits
+        (void)hipMemsetAsync(c->desc, 0, (size_t)nblocks_for(c->cfg.max_acc) * 8, c->stream);
+        c->round_tag = 1;
+    }
+    round_pass(c->stream, r == 0, c->cfg.cc_alg != DV_OCC, in, out, c->live_ub, &c->ctr->nlive[r & 1],
+               &c->ctr->nlive[(r + 1) & 1], c->status, c->need, c->abortf, c->desc,
+               &c->tile_ctr[r % kTileCtrs], c->round_tag, c->ctr);
     if (settle) round_settle(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, c->ctr);
     else round_verdict(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, d_verdict);
     c->rounds++;

@@ -1,0 +1,250 @@
+"""Partitioned (multi-GPU) epochs.
+
+CPU: the PartitionedRunner protocol (owner split, all-to-all of fragments in
+origin order, per-round verdict all-reduce MAX, termination) over gloo with
+world_size 2, driving a numpy restatement of one partition's decision round
+(test double); decisions must equal the single-node oracle E-schedule over the
+sequenced global epoch.
+
+GPU: two engine contexts on one device, each owning one partition, combined by
+an element-wise MAX of their verdict tensors -- the same combine RCCL performs
+across GPUs -- against the oracle; and the runner itself over a 1-rank
+process group.
+"""
+import os
+import socket
+import types
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _oracle as O
+import dvcc
+from dvcc.partitioned import PartitionedEpoch, PartitionedRunner, split_by_owner
+
+ORACLE_CC = {dvcc.NO_WAIT: O.NO_WAIT, dvcc.WAIT_DIE: O.WAIT_DIE, dvcc.OCC: O.OCC}
+
+
+class NumpyPartition:
+    """Test double: one partition's decision round in numpy (checker side)."""
+
+    needs_votes = True
+
+    def __init__(self, cc):
+        self.nowait = cc != dvcc.OCC
+
+    def begin_partition(self, keys, types_, txn, n_txn):
+        k = keys.numpy().view(np.uint64)
+        order = np.argsort(k, kind="stable")
+        self.k, self.w, self.t = k[order], types_.numpy()[order] == 1, txn.numpy()[order].astype(np.int64)
+        head = np.ones(len(self.k), bool)
+        head[1:] = self.k[1:] != self.k[:-1]
+        self.seg = np.cumsum(head) - 1
+        self.n_txn = n_txn
+        self.status = np.zeros(n_txn, np.int8)
+
+    def _first(self, mask):
+        n = len(self.k)
+        fp = np.full(self.seg[-1] + 1 if n else 1, n, np.int64)
+        np.minimum.at(fp, self.seg[mask], np.arange(n)[mask])
+        return fp[self.seg] < np.arange(n)
+
+    def round_local(self, verdict):
+        v = np.zeros(verdict.numel(), np.uint8)
+        if len(self.k):
+            s = self.status[self.t]
+            c, u, w = s == 1, s == 0, self.w
+            cw, uw = self._first(c & w), self._first(u & w)
+            if self.nowait:
+                ca, ua = self._first(c), self._first(u)
+                ab, wt = np.where(w, ca, cw), np.where(w, ua, uw)
+            else:
+                ab, wt = cw, uw
+            mine = u
+            np.maximum.at(v, self.t[mine & wt & ~ab], 1)
+            np.maximum.at(v, self.t[mine & ab], 2)
+        verdict.copy_(torch.from_numpy(v))
+
+    def round_apply(self, verdict):
+        v = verdict.numpy()[:self.n_txn]
+        und = self.status == 0
+        self.status[und & ((v & 2) != 0)] = 2
+        self.status[und & (v == 0)] = 1
+        return int((self.status == 0).sum())
+
+    def finish(self, commit=None):
+        if commit is not None:
+            commit[:self.n_txn] = torch.from_numpy((self.status == 1).astype(np.uint8))
+        return types.SimpleNamespace(committed=int((self.status == 1).sum()), n_txn=self.n_txn)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _global_setup(world, n_txn, rows_pp, mpr, seed0=3):
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9,
+                                  part_per_txn=2, strict_ppt=1, mpr=mpr)
+    batches = [gen.gen(n_txn, dvcc.epoch_seed(r, seed0), r) for r in range(world)]
+    return gen, batches
+
+
+def _oracle_global(cc, batches, world, rows_pp):
+    e = dvcc.sequence(batches)
+    n = rows_pp * world
+    tab = O.YcsbTable(n)  # part_cnt 1 view: row == key
+    f0 = tab.f0.copy()
+    c, _, st = O.epoch_run(ORACLE_CC[cc], tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types)
+    return c, st, f0
+
+
+def _gloo_worker(rank, world, port, cc, n_txn, rows_pp, mpr, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, batches = _global_setup(world, n_txn, rows_pp, mpr)
+        pe = PartitionedEpoch(batches[rank], rank, world, n_txn, "cpu")
+        runner = PartitionedRunner(NumpyPartition(cc), world, rank, device="cpu")
+        commit = torch.zeros(n_txn * world, dtype=torch.uint8)
+        st, rounds = runner.run(pe, commit=commit)
+        q.put((rank, commit.numpy().tobytes(), rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cc,mpr", [(dvcc.NO_WAIT, 0.3), (dvcc.OCC, 0.5), (dvcc.WAIT_DIE, 0.0),
+                                    (dvcc.NO_WAIT, 1.0)])
+def test_runner_protocol_gloo_world2(cc, mpr):
+    world, n_txn, rows_pp = 2, 600, 1 << 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, cc, n_txn, rows_pp, mpr, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, batches = _global_setup(world, n_txn, rows_pp, mpr)
+    c_ref, _, _ = _oracle_global(cc, batches, world, rows_pp)
+    for rank, buf, rounds in res:
+        got = np.frombuffer(buf, np.uint8)
+        assert (got == c_ref).all(), f"rank {rank}: {(got != c_ref).sum()} mismatches"
+        assert rounds >= 1
+
+
+def test_split_by_owner_orders_fragments():
+    e = dvcc.Epoch(np.array([5, 2, 7, 4, 9, 6], np.uint64), np.array([0, 1, 0, 1, 1, 0], np.uint8),
+                   np.array([0, 3, 6], np.uint32))
+    k, t, x, counts = split_by_owner(e, 100, 2)
+    assert counts.tolist() == [3, 3]
+    assert k.tolist() == [2, 4, 6, 5, 7, 9]     # owner 0 first, request order kept
+    assert x.tolist() == [100, 101, 101, 100, 100, 101]
+
+
+def test_sequence_is_origin_major():
+    _, batches = _global_setup(3, 50, 256, 0.5)
+    e = dvcc.sequence(batches)
+    assert e.n_txn == 150
+    assert (e.keys[:500] == batches[0].keys).all() and (e.keys[500:1000] == batches[1].keys).all()
+
+
+# ------------------------------------------------------------------- GPU
+def _gpu_two_partitions(cc, n_txn, rows_pp, mpr, world=2):
+    _, batches = _global_setup(world, n_txn, rows_pp, mpr, seed0=9)
+    c_ref, st_ref, f0_ref = _oracle_global(cc, batches, world, rows_pp)
+    # owner fragments, then each owner's input in origin order (the all-to-all)
+    frags = [split_by_owner(b, r * n_txn, world) for r, b in enumerate(batches)]
+    engines, deps = [], []
+    N = n_txn * world
+    for p in range(world):
+        ks, ts, xs = [], [], []
+        for k, t, x, counts in frags:
+            lo = int(counts[:p].sum())
+            hi = lo + int(counts[p])
+            ks.append(k[lo:hi]); ts.append(t[lo:hi]); xs.append(x[lo:hi])
+        k = np.concatenate(ks); t = np.concatenate(ts); x = np.concatenate(xs)
+        eng = dvcc.CCEngine(cc, N, max(16, len(k)), part_cnt=world, part_id=p)
+        eng.load_ycsb_partition(rows_pp)
+        dep = dvcc.DeviceEpoch.from_tensors(torch.from_numpy(k.view(np.int64)).cuda(),
+                                            torch.from_numpy(t).cuda(),
+                                            torch.from_numpy(x).cuda(), N)
+        eng.begin(dep)
+        engines.append(eng)
+        deps.append(dep)
+    rounds = 0
+    while True:
+        vs = []
+        for eng in engines:
+            v = torch.zeros((N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+            eng.round_local(v)
+            vs.append(v)
+        torch.cuda.synchronize()
+        comb = torch.stack(vs).max(dim=0).values.contiguous()
+        copies = [comb.clone() for _ in engines]
+        torch.cuda.synchronize()  # engines run on their own streams
+        und = [eng.round_apply(cp) for eng, cp in zip(engines, copies)]
+        rounds += 1
+        assert len(set(und)) == 1
+        if und[0] == 0:
+            break
+        assert rounds < N
+    digest = 0
+    for p, eng in enumerate(engines):
+        commit = torch.zeros(N, dtype=torch.uint8, device="cuda")
+        st = eng.finish(commit)
+        assert (commit.cpu().numpy() == c_ref).all()
+        digest = (digest + st.read_digest) % (1 << 64)
+        # partition p holds keys p, p+world, ...: oracle rows with the same keys
+        assert (eng.read_table(0, rows_pp) == f0_ref[p::world]).all()
+        eng.close()
+    assert digest == st_ref.read_digest
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC, dvcc.WAIT_DIE])
+@pytest.mark.parametrize("mpr", [0.0, 0.2, 1.0])
+def test_gpu_two_partition_engines(cc, mpr):
+    _gpu_two_partitions(cc, 3000, 1 << 12, mpr)
+
+
+@pytest.mark.gpu
+def test_gpu_four_partition_engines_large():
+    _gpu_two_partitions(dvcc.NO_WAIT, 50_000, 1 << 18, 0.3, world=4)
+
+
+@pytest.mark.gpu
+def test_gpu_runner_single_rank_process_group():
+    from dvcc.partitioned import EnginePartition
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    store = dist.HashStore()
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    try:
+        n_txn, rows = 20_000, 1 << 16
+        gen = dvcc.YCSBQueryGenerator(rows, zipf_theta=0.9)
+        e = gen.gen(n_txn, 5)
+        tab = O.YcsbTable(rows)
+        f0 = tab.f0.copy()
+        c_ref, _, st_ref = O.epoch_run(O.NO_WAIT, tab.ix, f0, n_txn, e.txn_begin, e.keys, e.types)
+        eng = dvcc.CCEngine(dvcc.NO_WAIT, n_txn, e.n_acc)
+        eng.load_ycsb_partition(rows)
+        runner = PartitionedRunner(EnginePartition(eng), 1, 0)
+        commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+        st, rounds = runner.run(PartitionedEpoch(e, 0, 1, n_txn, "cuda"), commit=commit)
+        assert (commit.cpu().numpy() == c_ref).all()
+        assert st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == f0).all()
+        eng.set_stream(None)
+        eng.close()
+    finally:
+        dist.destroy_process_group()
