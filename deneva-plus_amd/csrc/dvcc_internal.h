@@ -9,24 +9,39 @@
 namespace dvcc {
 
 constexpr int kBlock = 256;           // 4 waves of 64
-constexpr int kIPT = 16;              // items per thread in tiled kernels
-constexpr int kTile = kBlock * kIPT;  // 4096 elements per workgroup tile
+constexpr int kIPT = 16;              // items per thread in the radix kernels
+constexpr int kTile = kBlock * kIPT;  // 4096 keys per radix workgroup
 constexpr int kRadixBits = 8;
 constexpr int kRadix = 1 << kRadixBits;
 constexpr int kMaxTables = 8;
 
 // per-txn decision state (one byte per txn)
 enum : uint8_t { ST_UNDEC = 0, ST_COMMIT = 1, ST_ABORT = 2 };
-// verdict bits (combined across partitions by element-wise MAX)
+// partition verdict bits (combined across partitions by element-wise MAX)
 enum : uint8_t { V_WAIT = 1, V_ABORT = 2 };
 
-// sorted-element encoding: txn << 4 | bnd << 3 | dup << 2 | head << 1 | wr
-//   head: first access of a row segment; dup: repeat access of the same txn to
-//   the same row; bnd: Calvin grant-group boundary.
-constexpr uint32_t EL_WR = 1u, EL_HEAD = 2u, EL_DUP = 4u, EL_BND = 8u;
-// decision-round arrays reuse bit 3: the access is already OK (verdict pushed)
-constexpr uint32_t EL_DONE = 8u;
-constexpr uint32_t kMaxTxn = 1u << 28;
+// sort key of an access: row << 32 | txn << 8 | pos << 1 | wr
+//   pos = position of the access among its txn's accesses in this partition
+constexpr uint32_t kMaxTxn = 1u << 24;
+constexpr uint32_t kMaxPos = 1u << 7;
+constexpr uint64_t kMaxAcc = 1ull << 28;
+__host__ __device__ inline uint64_t pair_pack(uint64_t row, uint32_t txn, uint32_t pos, uint32_t wr) {
+    return (row << 32) | ((uint64_t)txn << 8) | ((uint64_t)pos << 1) | wr;
+}
+__host__ __device__ inline uint32_t pair_row(uint64_t p) { return (uint32_t)(p >> 32); }
+__host__ __device__ inline uint32_t pair_txn(uint64_t p) { return (uint32_t)(p >> 8) & 0xFFFFFFu; }
+__host__ __device__ inline uint32_t pair_pos(uint64_t p) { return (uint32_t)(p >> 1) & 0x7Fu; }
+
+// row-queue element (row order): txn << 32 | access << 4 | flags
+//   head: first access of a row queue; dup: repeat access of the same txn to
+//   the same row; bnd: Calvin grant-group boundary; done: decision rounds --
+//   the access is already OK.
+constexpr uint64_t EL_WR = 1u, EL_HEAD = 2u, EL_DUP = 4u, EL_BND = 8u, EL_DONE = 8u;
+__host__ __device__ inline uint32_t el_txn(uint64_t e) { return (uint32_t)(e >> 32); }
+__host__ __device__ inline uint32_t el_acc(uint64_t e) { return (uint32_t)(e >> 4) & 0x0FFFFFFFu; }
+__host__ __device__ inline uint64_t el_pack(uint32_t txn, uint32_t acc, uint64_t flags) {
+    return ((uint64_t)txn << 32) | ((uint64_t)acc << 4) | flags;
+}
 
 // device counters block (zeroed per epoch)
 struct Counters {
@@ -60,45 +75,57 @@ struct Tables {
 };
 
 // error bits recorded by kernels
-enum : uint32_t { ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16 };
+enum : uint32_t {
+    ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16, ERRB_BIG = 32
+};
 
-// ---- launchers (dvcc_kernels.hip) ----
+// ---- probe / queues (dvcc_kernels.hip)
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  uint64_t *pairs, uint32_t *vals, uint32_t *need, Counters *ctr);
+                  bool allow_dup, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
+                  Counters *ctr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
 // digit_tot: kRadix.  scatter_ev (optional): 2 events per pass for timing.
-int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint32_t *vals[2], uint64_t n, int key_bits,
-                    uint32_t *counts, uint32_t *digit_tot, hipEvent_t *scatter_ev);
+int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev);
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
-                        uint32_t *el, Counters *ctr);
+                        const uint32_t *tb_start, uint64_t *el, Counters *ctr);
 
-// segmented scans: block aggregates / carries live in agg_f, agg_v, carry (>= nblocks)
-void calvin_grant(hipStream_t s, const uint32_t *el, const uint32_t *vals, uint64_t n,
-                  uint32_t *grant_out, uint8_t *ew, uint32_t *agg_f, uint32_t *agg_v,
-                  uint32_t *carry);
-// decision rounds (dvcc_rounds.hip)
-constexpr uint32_t kTileCtrs = 1024;  // per-round tile tickets, reset every kTileCtrs rounds
-void rounds_epoch_init(hipStream_t s, uint32_t n_acc, uint32_t n_txn_pad, uint32_t *need,
-                       uint8_t *abortf, uint32_t *tile_ctr, Counters *ctr);
-void round_pass(hipStream_t s, bool first, int nowait, const uint32_t *el_in, uint32_t *el_out,
-                uint32_t ub_in, const uint32_t *n_in, uint32_t *n_out, const uint8_t *status,
-                uint32_t *need, uint8_t *abortf, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag,
-                Counters *ctr);
-void round_settle(hipStream_t s, uint8_t *status, const uint32_t *need, const uint8_t *abortf,
-                  uint32_t n_txn_pad, Counters *ctr);
-void round_verdict(hipStream_t s, const uint8_t *status, const uint32_t *need, const uint8_t *abortf,
-                   uint32_t n_txn_pad, uint8_t *verdict);
-void round_apply(hipStream_t s, uint8_t *status, const uint8_t *verdict, uint32_t n_txn_pad,
-                 Counters *ctr);
+// Calvin grant groups: one single-pass segmented scan over the row queues
+void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant_out, uint8_t *ew,
+                  uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr);
+
+// decision rounds (dvcc_rounds.hip): vb8 = per-access verdict (1 = permanently
+// OK, 2 = aborts its txn); [tb_start, tb_end) = a txn's accesses here.
+constexpr uint32_t kTileCtrs = 1024;  // tile tickets, reset every kTileCtrs passes
+struct RoundBufs {
+    const uint64_t *el0;     // round-0 elements (sorted, from seg_prepare)
+    uint64_t *rel[2];        // live elements, ping-pong
+    uint8_t *vb8;            // per access
+    uint8_t *status;         // per txn
+    const uint32_t *tb_start, *tb_end;
+    uint64_t *desc;
+    uint32_t *tile_ctr;
+    Counters *ctr;
+};
+void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc);
+void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
+                uint32_t tag, uint32_t ticket);
+// single GPU: settle statuses from the verdicts; partitioned: local verdict
+// bytes (bit1 abort, bit0 wait), then apply the MAX-combined verdicts
+void round_settle(hipStream_t s, const RoundBufs &b, uint32_t n_txn);
+void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict);
+void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_t *verdict);
+
+// ---- execution and outputs (dvcc_kernels.hip)
 void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4,
                         uint8_t value);
-void launch_exec(hipStream_t s, int calvin, const uint64_t *pairs, const uint32_t *el,
-                 const uint8_t *ew, uint64_t n, const uint8_t *status, uint64_t *f0,
-                 const uint64_t *pkey, Counters *ctr);
+void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
+                 uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
+                 Counters *ctr);
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
@@ -109,5 +136,6 @@ void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, uint64
                          uint8_t *types, uint32_t *acc_txn, uint8_t *tables);
 
 inline uint32_t nblocks_for(uint64_t n) { return (uint32_t)((n + kTile - 1) / kTile); }
+inline uint32_t rblocks_for(uint64_t n) { return (uint32_t)((n + kBlock * 8 - 1) / (kBlock * 8)); }
 
 }  // namespace dvcc

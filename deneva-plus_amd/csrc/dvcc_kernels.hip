@@ -2,140 +2,121 @@
 //
 // Epoch pipeline (DESIGN.md "Kernels"):
 //   k_probe         IndexHash::index_read (storage/index_hash.cpp:137-153) for every access,
-//                   emitting one packed u64 per access: row << 32 | txn << 1 | is_wr
-//   radix sort      stable LSD sort of those pairs by row (8-bit digits, wave64 ballot
+//                   emitting one packed u64 per access: row << 32 | txn << 8 | pos << 1 | wr
+//   radix sort      stable LSD sort of those keys by row (8-bit digits, wave64 ballot
 //                   multisplit ranks, LDS-staged coalesced scatter) -> per-row FIFO queues
 //                   in sequence order, i.e. the waiter/owner lists of Row_lock
 //                   (concurrency_control/row_lock.h:20-59) for the whole epoch at once
-//   k_seg_prepare   row-segment heads, same-txn repeats, Calvin grant-group boundaries
-//   segmented scans Calvin grant groups (row_lock.cpp:78-81,152-170,318-358) or one
-//                   decision round of NO_WAIT/WAIT_DIE lock_get (row_lock.cpp:69,86-90)
-//                   / OCC central_validate (occ.cpp:185-199, test_valid 319-327)
-//   k_round_apply   per-txn vote combine (TxnManager::received_response, txn.cpp:544-554)
-//   k_exec          run_ycsb_1 (benchmarks/ycsb_txn.cpp:227-254) for committed txns
+//   k_seg_prepare   queue heads, same-txn repeats, Calvin grant-group boundaries
+//   k_calvin_pass   Calvin grant groups (row_lock.cpp:78-81,152-170,318-358), single pass
+//   rounds          NO_WAIT / WAIT_DIE / OCC decisions (dvcc_rounds.hip)
+//   k_exec_*        run_ycsb_1 (benchmarks/ycsb_txn.cpp:227-254) for committed txns
 //
-// Every tiled kernel uses 256-thread workgroups (4 wave64s) and 4096-element
-// tiles; every cross-workgroup dependency goes through a kernel boundary (no
-// in-launch hand-offs), so no result depends on dispatch order or XCD placement.
-#include "dvcc_internal.h"
+// Cross-workgroup dependencies go through kernel boundaries, except the
+// decoupled look-back of the single-pass scans (dvcc_common.h), whose
+// protocol is independent of dispatch order and XCD placement.
+#include "dvcc_common.h"
 
 namespace dvcc {
-
-// ------------------------------------------------------------ wave helpers
-__device__ __forceinline__ uint32_t lane_id() {
-    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-}
-// number of set bits of `mask` below this lane
-__device__ __forceinline__ uint32_t mask_rank(uint64_t mask) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-// lanes of the wave holding the same 8-bit digit (restricted to `valid`)
-__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t valid) {
-    uint64_t peers = valid;
-#pragma unroll
-    for (int b = 0; b < kRadixBits; b++) {
-        const uint32_t bit = (d >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-    }
-    return peers;
-}
-
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
-    return z ^ (z >> 31);
-}
-
-// exclusive scan of one u32 per thread over a 256-thread block
-__device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *lds4,
-                                                        uint32_t *total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= (uint32_t)off) x += y;
-    }
-    if (lane == 63) lds4[wave] = x;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-        const uint32_t t = lds4[w];
-        if (w < (int)wave) pre += t;
-        tot += t;
-    }
-    __syncthreads();
-    if (total) *total = tot;
-    return pre + x - v;
-}
-
-__device__ __forceinline__ void set_err(Counters *ctr, uint32_t bit) { atomicOr(&ctr->err, bit); }
 
 // ------------------------------------------------------------------ probe
 __device__ __forceinline__ uint64_t bucket_of(const TableDesc &t, uint64_t key) {
     return t.hash_kind == DV_HASH_YCSB ? (key / t.part_cnt) % t.nbuckets : key % t.nbuckets;
 }
 
-template <bool VALS, bool NEED>
+__device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint64_t key, uint64_t &row,
+                                          Counters *ctr) {
+    if (tb >= tabs.n) {
+        set_err(ctr, ERRB_TABLE);
+        return false;
+    }
+    const TableDesc &t = tabs.t[tb];
+    const uint64_t bk = bucket_of(t, key);
+    bool found = false;
+    if (t.bstart == nullptr) {                // YCSB: one key per bucket
+        const IxEntry e = t.ix[bk];
+        if (e.key == key) { row = e.row; found = true; }
+    } else {                                  // chained bucket (read_item 217-231)
+        for (uint32_t j = t.bstart[bk], end = t.bstart[bk + 1]; j < end; j++) {
+            const IxEntry e = t.ix[j];
+            if (e.key == key) { row = e.row; found = true; break; }
+        }
+    }
+    if (!found) set_err(ctr, ERRB_KEY);
+    row += t.row_base;
+    return found;
+}
+
+// One access per lane (input order: a txn's accesses are contiguous).  Besides
+// the sort key it records the txn's access range [tb_start, tb_end) and the
+// access's position in it, and -- unless repeats are allowed (Calvin dedups
+// them, TxnManager::get_lock txn.cpp:778-788) -- flags a txn naming one row
+// twice.  Runs of one txn are found with wave ballots; a run that began in an
+// earlier wave is walked back in memory (at most one per wave).
+template <bool ALLOW_DUP>
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n,
                                                   uint32_t n_txn, uint64_t *__restrict__ pairs,
-                                                  uint32_t *__restrict__ vals,
-                                                  uint32_t *__restrict__ need, Counters *ctr) {
+                                                  uint32_t *__restrict__ tb_start,
+                                                  uint32_t *__restrict__ tb_end, Counters *ctr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t lane = threadIdx.x & 63;
     // block-uniform trip count so every lane takes part in the wave ballots
     for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
         const uint64_t i = b0 + threadIdx.x;
         const bool valid = i < n;
-        uint32_t txn = valid ? acc_txn[i] : 0xFFFFFFFFu;
+        uint32_t txn = 0xFFFFFFFFu, tb = 0, wr = 0;
+        uint64_t key = 0, row = 0;
+        bool bad_txn = false;
         if (valid) {
-            const uint64_t key = keys[i];
-            const uint32_t tb = tables ? tables[i] : 0u;
-            const uint32_t wr = types[i] == DV_WR ? 1u : 0u;
-            uint64_t row = 0;
-            if (tb >= tabs.n) {
-                set_err(ctr, ERRB_TABLE);
-            } else {
-                const TableDesc &t = tabs.t[tb];
-                const uint64_t bk = bucket_of(t, key);
-                bool found = false;
-                if (t.bstart == nullptr) {                // YCSB: one key per bucket
-                    const IxEntry e = t.ix[bk];
-                    if (e.key == key) { row = e.row; found = true; }
-                } else {                                  // chained bucket (read_item 217-231)
-                    for (uint32_t j = t.bstart[bk], end = t.bstart[bk + 1]; j < end; j++) {
-                        const IxEntry e = t.ix[j];
-                        if (e.key == key) { row = e.row; found = true; break; }
-                    }
-                }
-                if (!found) set_err(ctr, ERRB_KEY);
-                row += t.row_base;
-            }
-            uint32_t t_ok = txn;
-            if (txn >= n_txn || (i > 0 && acc_txn[i - 1] > txn)) {
-                set_err(ctr, ERRB_TXN);
-                t_ok = 0;
-            }
-            pairs[i] = (row << 32) | ((uint64_t)t_ok << 1) | wr;
-            if (VALS) vals[i] = (uint32_t)i;
+            txn = acc_txn[i];
+            key = keys[i];
+            tb = tables ? tables[i] : 0u;
+            wr = types[i] == DV_WR ? 1u : 0u;
+            probe_row(tabs, tb, key, row, ctr);
+            bad_txn = txn >= n_txn || (i > 0 && acc_txn[i - 1] > txn);
+            if (bad_txn) set_err(ctr, ERRB_TXN);
         }
-        if (NEED) {
-            // need[t] = this partition's accesses of txn t: one atomic per run of
-            // equal txns inside the wave (acc_txn is non-decreasing)
-            const uint32_t tprev = __shfl_up(txn, 1, 64);
-            const bool start = valid && (lane == 0 || tprev != txn);
-            const uint64_t smask = __ballot(start);
-            const uint32_t nvalid = (uint32_t)__popcll(__ballot(valid));
-            if (start && txn < n_txn) {
-                const uint64_t above = lane == 63 ? 0ull : ((smask >> (lane + 1)) << (lane + 1));
-                const uint32_t next = above ? (uint32_t)__builtin_ctzll(above) : nvalid;
-                atomicAdd(&need[txn], next - lane);
+        // runs of equal txn inside the wave
+        const uint32_t tprev = __shfl_up(txn, 1, 64);
+        const bool start = valid && (lane == 0 || tprev != txn);
+        const uint64_t smask = __ballot(start);
+        const uint64_t below = smask & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
+        const uint32_t run0 = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+        const uint32_t depth = valid ? lane - run0 : 0u;
+        bool dup = false;
+        if (!ALLOW_DUP) {
+            uint32_t maxd = depth;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                const uint32_t o = __shfl_xor(maxd, off, 64);
+                maxd = o > maxd ? o : maxd;
+            }
+            for (uint32_t d = 1; d <= maxd; d++) {
+                const uint64_t kp = __shfl_up(key, d, 64);
+                const uint32_t bp = __shfl_up(tb, d, 64);
+                if (d <= depth && kp == key && bp == tb) dup = true;
+            }
+        }
+        uint32_t before = 0;  // accesses of this txn in earlier waves
+        if (valid && run0 == 0 && i > (uint64_t)lane) {
+            for (uint64_t j = i - lane; j-- > 0;) {
+                if (acc_txn[j] != txn) break;
+                before++;
+                if (!ALLOW_DUP && keys[j] == key && (tables ? tables[j] : 0u) == tb) dup = true;
+            }
+        }
+        if (valid) {
+            if (dup) set_err(ctr, ERRB_DUP);
+            const uint32_t pos = depth + before;
+            if (pos >= kMaxPos) set_err(ctr, ERRB_BIG);
+            const uint32_t t_ok = bad_txn ? 0u : txn;
+            pairs[i] = pair_pack(row, t_ok, pos & (kMaxPos - 1), wr);
+            if (!bad_txn) {
+                if (pos == 0) tb_start[txn] = (uint32_t)i;
+                if (i + 1 == n || acc_txn[i + 1] != txn) tb_end[txn] = (uint32_t)(i + 1);
             }
         }
     }
@@ -143,20 +124,18 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  uint64_t *pairs, uint32_t *vals, uint32_t *need, Counters *ctr) {
+                  bool allow_dup, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
+                  Counters *ctr) {
     if (n_acc == 0) return;
     uint64_t blocks = (n_acc + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
     const uint32_t g = (uint32_t)blocks;
-    if (vals)
-        k_probe<true, false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
-                                                  pairs, vals, need, ctr);
-    else if (need)
-        k_probe<false, true><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
-                                                  pairs, vals, need, ctr);
+    if (allow_dup)
+        k_probe<true><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, pairs,
+                                           tb_start, tb_end, ctr);
     else
-        k_probe<false, false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
-                                                   pairs, vals, need, ctr);
+        k_probe<false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, pairs,
+                                            tb_start, tb_end, ctr);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -213,13 +192,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ co
     if (threadIdx.x == 0) digit_tot[blockIdx.x] = tot;
 }
 
-template <bool VALS>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(
-    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, const uint32_t *__restrict__ vin,
-    uint32_t *__restrict__ vout, uint64_t n, int shift, const uint32_t *__restrict__ counts,
+    const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n, int shift, const uint32_t *__restrict__ counts,
     const uint32_t *__restrict__ digit_tot, uint32_t nblocks) {
     __shared__ __attribute__((aligned(16))) uint64_t skeys[kTile];
-    __shared__ uint32_t svals[VALS ? kTile : 1];
     __shared__ uint32_t wc[4][kRadix];
     __shared__ uint32_t dstart[kRadix];
     __shared__ uint64_t gbase[kRadix];
@@ -239,13 +215,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
 
     const uint64_t base = tile0 + wave * (64 * kIPT);
     uint64_t k[kIPT];
-    uint32_t v[VALS ? kIPT : 1];
     uint32_t r[kIPT];
 #pragma unroll
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         k[j] = idx < n ? in[idx] : 0;
-        if (VALS) v[j] = idx < n ? vin[idx] : 0;
     }
 #pragma unroll
     for (int j = 0; j < kIPT; j++) {
@@ -278,7 +252,6 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
             const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
             const uint32_t pos = dstart[d] + wc[wave][d] + r[j];
             skeys[pos] = k[j];
-            if (VALS) svals[pos] = v[j];
         }
     }
     __syncthreads();
@@ -288,12 +261,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
         const uint32_t d = (uint32_t)(key >> shift) & (kRadix - 1);
         const uint64_t dst = gbase[d] + p;
         out[dst] = key;
-        if (VALS) vout[dst] = svals[p];
     }
 }
 
-int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint32_t *vals[2], uint64_t n, int key_bits,
-                    uint32_t *counts, uint32_t *digit_tot, hipEvent_t *scatter_ev) {
+int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
@@ -302,42 +274,39 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint32_t *vals[2], uint64
         k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb);
         k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot);
         if (scatter_ev) (void)hipEventRecord(scatter_ev[2 * pass], s);
-        if (vals)
-            k_radix_scatter<true><<<nb, kBlock, 0, s>>>(pairs[cur], pairs[cur ^ 1], vals[cur],
-                                                        vals[cur ^ 1], n, shift, counts, digit_tot, nb);
-        else
-            k_radix_scatter<false><<<nb, kBlock, 0, s>>>(pairs[cur], pairs[cur ^ 1], nullptr,
-                                                         nullptr, n, shift, counts, digit_tot, nb);
+        k_radix_scatter<<<nb, kBlock, 0, s>>>(pairs[cur], pairs[cur ^ 1], n, shift, counts, digit_tot,
+                                              nb);
         if (scatter_ev) (void)hipEventRecord(scatter_ev[2 * pass + 1], s);
         cur ^= 1;
     }
     return cur;
 }
 
-// ------------------------------------------------------- segment prepare
+// ------------------------------------------------------- queue elements
+// row-queue element of sorted position i: heads, same-txn repeats, Calvin
+// grant-group boundaries, and the access id tb_start[txn] + pos
 __global__ __launch_bounds__(kBlock) void k_seg_prepare(const uint64_t *__restrict__ pairs, uint64_t n,
-                                                        int calvin, uint32_t *__restrict__ el,
-                                                        Counters *ctr) {
+                                                        int calvin,
+                                                        const uint32_t *__restrict__ tb_start,
+                                                        uint64_t *__restrict__ el, Counters *ctr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t p = pairs[i];
-        const uint32_t row = (uint32_t)(p >> 32), txn = (uint32_t)(p >> 1) & 0x7FFFFFFFu;
+        const uint32_t row = pair_row(p), txn = pair_txn(p);
         const uint32_t wr = (uint32_t)p & 1u;
         uint32_t head = 1, dup = 0, bnd = 1;
         if (i > 0) {
             const uint64_t q = pairs[i - 1];
-            if ((uint32_t)(q >> 32) == row) {
+            if (pair_row(q) == row) {
                 head = 0;
-                if (((uint32_t)(q >> 1) & 0x7FFFFFFFu) == txn) dup = 1;
-                // previous queue entry's lock type: a repeat access keeps the lock
+                if (pair_txn(q) == txn) dup = 1;
+                // lock type of the previous queue entry: a repeat access keeps the
                 // type of its txn's first access to the row (TxnManager::get_lock,
                 // system/txn.cpp:778-788)
                 uint64_t e = i - 1;
                 while (e > 0) {
                     const uint64_t qq = pairs[e - 1];
-                    if ((uint32_t)(qq >> 32) != row ||
-                        ((uint32_t)(qq >> 1) & 0x7FFFFFFFu) != ((uint32_t)(pairs[e] >> 1) & 0x7FFFFFFFu))
-                        break;
+                    if (pair_row(qq) != row || pair_txn(qq) != pair_txn(pairs[e])) break;
                     e--;
                 }
                 const uint32_t prev_entry_wr = (uint32_t)pairs[e] & 1u;
@@ -345,206 +314,95 @@ __global__ __launch_bounds__(kBlock) void k_seg_prepare(const uint64_t *__restri
             }
         }
         if (dup && !calvin) set_err(ctr, ERRB_DUP);
-        el[i] = (txn << 4) | ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr;
+        const uint32_t acc = tb_start[txn] + pair_pos(p);
+        el[i] = el_pack(txn, acc,
+                        ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr);
     }
 }
 
-void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin, uint32_t *el,
-                        Counters *ctr) {
+void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
+                        const uint32_t *tb_start, uint64_t *el, Counters *ctr) {
     if (n == 0) return;
     uint64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 8192) blocks = 8192;
-    k_seg_prepare<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, n, calvin, el, ctr);
+    k_seg_prepare<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, n, calvin, tb_start, el, ctr);
 }
 
-// ----------------------------------------------------- segmented scans
-// A scan element is (head, value).  The segmented operator
-//   (f1,v1) o (f2,v2) = (f1|f2, f2 ? v2 : comb(v1,v2))
-// is associative; the exclusive value at a head is the identity.
-struct SegPair {
-    uint32_t f;
-    uint32_t v;
-};
-
-// Calvin: low 31 bits count grant-group boundaries, bit 31 = a WR access seen
-struct OpCalvin {
-    static constexpr uint32_t kId = 0;
-    __device__ static uint32_t comb(uint32_t a, uint32_t b) {
-        return ((a & 0x7FFFFFFFu) + (b & 0x7FFFFFFFu)) | ((a | b) & 0x80000000u);
-    }
-};
-
-template <class Op>
-__device__ __forceinline__ SegPair seg_comb(SegPair a, SegPair b) {
-    return SegPair{a.f | b.f, b.f ? b.v : Op::comb(a.v, b.v)};
-}
-
-template <class Op>
-__device__ __forceinline__ SegPair wave_incl_scan(SegPair p, uint32_t lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        SegPair o;
-        o.f = __shfl_up(p.f, off, 64);
-        o.v = __shfl_up(p.v, off, 64);
-        if (lane >= (uint32_t)off) p = seg_comb<Op>(o, p);
-    }
-    return p;
-}
-
-// load this thread's kIPT consecutive elements of a tile (blocked arrangement)
-__device__ __forceinline__ int load_el(const uint32_t *__restrict__ el, uint64_t n, uint64_t first,
-                                       uint32_t (&e)[kIPT]) {
-    if (first + kIPT <= n) {
-        const uint4 *p = reinterpret_cast<const uint4 *>(el + first);
-#pragma unroll
-        for (int q = 0; q < kIPT / 4; q++) {
-            const uint4 x = p[q];
-            e[4 * q] = x.x; e[4 * q + 1] = x.y; e[4 * q + 2] = x.z; e[4 * q + 3] = x.w;
-        }
-        return kIPT;
-    }
-    int cnt = 0;
-#pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        const bool ok = first + j < n;
-        e[j] = ok ? el[first + j] : EL_HEAD;
-        cnt += ok;
-    }
-    return cnt;
-}
-
-struct ValCalvin {
-    __device__ uint32_t operator()(uint32_t e) const {
-        return ((e & EL_BND) ? 1u : 0u) | ((e & EL_WR) ? 0x80000000u : 0u);
-    }
-};
-
-template <class Op, class Val>
-__global__ __launch_bounds__(kBlock) void k_segscan_reduce(const uint32_t *__restrict__ el, uint64_t n,
-                                                           Val val, uint32_t *__restrict__ agg_f,
-                                                           uint32_t *__restrict__ agg_v) {
-    __shared__ SegPair wt[4];
+// ------------------------------------------------------- Calvin grants
+// Per row queue (sequence order), a request is granted together with the
+// requests in front of it when they are all shared: grant groups are maximal
+// runs of SH requests, each EX alone (CALVIN lock_get queues behind any
+// waiter, row_lock.cpp:78-81, 152-170; lock_release promotes compatible FIFO
+// waiters, 318-358).  grant group = (boundaries so far in the queue) - 1, one
+// OpSeg scan; ew = a WR of an earlier txn precedes the access in its queue
+// (its read sees that write under the serial order).
+__global__ __launch_bounds__(kBlock) void k_calvin_pass(const uint64_t *__restrict__ el, uint32_t n,
+                                                        uint32_t *__restrict__ grant,
+                                                        uint8_t *__restrict__ ew, uint64_t *desc,
+                                                        uint32_t *tile_ctr, uint32_t tag,
+                                                        Counters *ctr) {
+    __shared__ uint64_t s_el[kRTile + kRTile / kRIPT];
+    __shared__ uint64_t s_next;
+    __shared__ uint32_t s_tile;
+    __shared__ Agg wt[4];
+    __shared__ Agg s_pre;
+    const uint32_t ntiles = (n + kRTile - 1) / kRTile;
+    if (blockIdx.x >= ntiles) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t first = (uint64_t)blockIdx.x * kTile + (uint64_t)tid * kIPT;
-    uint32_t e[kIPT];
-    const int cnt = first < n ? load_el(el, n, first, e) : 0;
-    SegPair a{0u, Op::kId};
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t base = tile * kRTile;
+    const uint32_t tile_n = n - base < (uint32_t)kRTile ? n - base : (uint32_t)kRTile;
+    load_tile64(el, base, tile_n, n, s_el, &s_next);
+    __syncthreads();
+    const uint32_t first = tid * kRIPT;
+    const int cnt = first >= tile_n ? 0 : (tile_n - first < (uint32_t)kRIPT ? (int)(tile_n - first) : kRIPT);
+    uint64_t e[kRIPT];
+    Agg a{0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < kIPT; j++) {
+    for (int j = 0; j < kRIPT; j++) {
+        e[j] = j < cnt ? s_el[rpad(first + j)] : (uint64_t)EL_HEAD;
         if (j < cnt) {
-            const uint32_t v = val(e[j]);
-            if (e[j] & EL_HEAD) { a.f = 1; a.v = v; }
-            else a.v = Op::comb(a.v, v);
+            const Agg x{(uint32_t)((e[j] & EL_HEAD) != 0), (uint32_t)(e[j] & EL_WR),
+                        (uint32_t)((e[j] & EL_BND) != 0)};
+            a = OpSeg::comb(a, x);
         }
     }
-    SegPair inc = wave_incl_scan<Op>(a, lane);
+    const Agg inc = wave_incl<OpSeg>(a, lane);
     if (lane == 63) wt[wave] = inc;
     __syncthreads();
-    if (tid == 0) {
-        SegPair t = wt[0];
-        for (int w = 1; w < 4; w++) t = seg_comb<Op>(t, wt[w]);
-        agg_f[blockIdx.x] = t.f;
-        agg_v[blockIdx.x] = t.v;
+    if (wave == 0) {
+        Agg bagg = wt[0];
+        for (int w = 1; w < 4; w++) bagg = OpSeg::comb(bagg, wt[w]);
+        const Agg pre = look_back<OpSeg>(desc, tile, tag, bagg, lane, ctr);
+        if (lane == 0) s_pre = pre;
     }
-}
-
-// exclusive segmented scan of the block aggregates (one workgroup of 1024)
-template <class Op>
-__global__ __launch_bounds__(1024) void k_segscan_blocks(const uint32_t *__restrict__ agg_f,
-                                                         const uint32_t *__restrict__ agg_v,
-                                                         uint32_t nb, uint32_t *__restrict__ carry) {
-    __shared__ SegPair wt[16];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t per = (nb + 1023) / 1024;
-    const uint32_t lo = tid * per;
-    uint32_t hi = lo + per;
-    if (hi > nb) hi = nb;
-    SegPair a{0u, Op::kId};
-    for (uint32_t i = lo; i < hi; i++) a = seg_comb<Op>(a, SegPair{agg_f[i], agg_v[i]});
-    SegPair inc = wave_incl_scan<Op>(a, lane);
-    if (lane == 63) wt[wave] = inc;
-    SegPair ex;
-    ex.f = __shfl_up(inc.f, 1, 64);
-    ex.v = __shfl_up(inc.v, 1, 64);
-    if (lane == 0) ex = SegPair{0u, Op::kId};
     __syncthreads();
-    SegPair pre{0u, Op::kId};
-    for (uint32_t w = 0; w < wave; w++) pre = seg_comb<Op>(pre, wt[w]);
-    SegPair run = seg_comb<Op>(pre, ex);
-    for (uint32_t i = lo; i < hi; i++) {
-        carry[i] = run.v;
-        run = seg_comb<Op>(run, SegPair{agg_f[i], agg_v[i]});
-    }
-}
-
-// downsweep: per element exclusive value -> apply
-struct ApplyCalvin {
-    const uint32_t *vals;
-    uint32_t *grant;
-    uint8_t *ew;
-    __device__ void operator()(uint64_t i, uint32_t e, uint32_t excl, uint32_t v) const {
-        const uint32_t inc = OpCalvin::comb(excl, v);
-        if (grant) grant[vals[i]] = (inc & 0x7FFFFFFFu) - 1u;
-        ew[i] = (uint8_t)(((e & EL_HEAD) ? 0u : (excl >> 31)) & 1u);
-    }
-};
-
-template <class Op, class Val, class Apply>
-__global__ __launch_bounds__(kBlock) void k_segscan_down(const uint32_t *__restrict__ el, uint64_t n,
-                                                         Val val, const uint32_t *__restrict__ agg_f,
-                                                         const uint32_t *__restrict__ carry,
-                                                         Apply apply) {
-    __shared__ SegPair wt[4];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t first = (uint64_t)blockIdx.x * kTile + (uint64_t)tid * kIPT;
-    uint32_t e[kIPT], v[kIPT];
-    const int cnt = first < n ? load_el(el, n, first, e) : 0;
-    SegPair a{0u, Op::kId};
+    Agg run = s_pre;
+    for (uint32_t w = 0; w < wave; w++) run = OpSeg::comb(run, wt[w]);
+    run = OpSeg::comb(run, wave_excl_from_incl<OpSeg>(inc, lane));
 #pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        v[j] = 0;
+    for (int j = 0; j < kRIPT; j++) {
         if (j < cnt) {
-            v[j] = val(e[j]);
-            if (e[j] & EL_HEAD) { a.f = 1; a.v = v[j]; }
-            else a.v = Op::comb(a.v, v[j]);
-        }
-    }
-    SegPair inc = wave_incl_scan<Op>(a, lane);
-    if (lane == 63) wt[wave] = inc;
-    SegPair ex;
-    ex.f = __shfl_up(inc.f, 1, 64);
-    ex.v = __shfl_up(inc.v, 1, 64);
-    if (lane == 0) ex = SegPair{0u, Op::kId};
-    __syncthreads();
-    SegPair pre{0u, carry[blockIdx.x]};
-    for (uint32_t w = 0; w < wave; w++) pre = seg_comb<Op>(pre, wt[w]);
-    uint32_t run = seg_comb<Op>(pre, ex).v;
-#pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        if (j < cnt) {
-            const uint32_t excl = (e[j] & EL_HEAD) ? Op::kId : run;
-            apply(first + j, e[j], excl, v[j]);
-            run = (e[j] & EL_HEAD) ? v[j] : Op::comb(run, v[j]);
+            const bool head = (e[j] & EL_HEAD) != 0;
+            const uint32_t bnd = (e[j] & EL_BND) ? 1u : 0u;
+            const uint32_t incl = (head ? 0u : run.c) + bnd;
+            if (grant) grant[el_acc(e[j])] = incl - 1u;
+            ew[base + first + j] = (uint8_t)(head ? 0u : (run.v & 1u));
+            run = OpSeg::comb(run, Agg{head ? 1u : 0u, (uint32_t)(e[j] & EL_WR), bnd});
         }
     }
 }
 
-template <class Op, class Val, class Apply>
-static void segscan(hipStream_t s, const uint32_t *el, uint64_t n, Val val, Apply apply,
-                    uint32_t *agg_f, uint32_t *agg_v, uint32_t *carry) {
+void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant_out, uint8_t *ew,
+                  uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
     if (n == 0) return;
-    const uint32_t nb = nblocks_for(n);
-    k_segscan_reduce<Op, Val><<<nb, kBlock, 0, s>>>(el, n, val, agg_f, agg_v);
-    k_segscan_blocks<Op><<<1, 1024, 0, s>>>(agg_f, agg_v, nb, carry);
-    k_segscan_down<Op, Val, Apply><<<nb, kBlock, 0, s>>>(el, n, val, agg_f, carry, apply);
+    const uint32_t nb = (uint32_t)((n + kRTile - 1) / kRTile);
+    k_calvin_pass<<<nb, kBlock, 0, s>>>(el, (uint32_t)n, grant_out, ew, desc, tile_ctr, tag, ctr);
 }
 
-void calvin_grant(hipStream_t s, const uint32_t *el, const uint32_t *vals, uint64_t n,
-                  uint32_t *grant_out, uint8_t *ew, uint32_t *agg_f, uint32_t *agg_v,
-                  uint32_t *carry) {
-    segscan<OpCalvin>(s, el, n, ValCalvin{}, ApplyCalvin{vals, grant_out, ew}, agg_f, agg_v, carry);
-}
-
+// ---------------------------------------------------------------- status
 __global__ void k_status_init(uint8_t *status, uint32_t n_txn, uint32_t n_pad, uint8_t value) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n_pad) status[i] = i < n_txn ? value : (uint8_t)ST_ABORT;
@@ -561,9 +419,10 @@ void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // run_ycsb_1 (ycsb_txn.cpp:227-254) for committed txns: a RD loads the 8-byte
 // F0 prefix, a WR stores 0.  Reads see the epoch's initial image unless an
 // earlier WR of another txn precedes them in the row queue (Calvin only; under
-// NO_WAIT/OCC a committed reader never follows a committed writer).
+// NO_WAIT/OCC a committed reader never follows a committed writer).  Reads
+// run before writes (two launches) so every read sees the pre-epoch image.
 __global__ __launch_bounds__(kBlock) void k_exec_reads(const uint64_t *__restrict__ pairs,
-                                                       const uint32_t *__restrict__ el,
+                                                       const uint64_t *__restrict__ el,
                                                        const uint8_t *__restrict__ ew, uint64_t n,
                                                        const uint8_t *__restrict__ status,
                                                        const uint64_t *__restrict__ f0,
@@ -573,11 +432,11 @@ __global__ __launch_bounds__(kBlock) void k_exec_reads(const uint64_t *__restric
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long dig = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t e = el[i];
+        const uint64_t e = el[i];
         if (e & EL_WR) continue;
-        const uint32_t txn = e >> 4;
+        const uint32_t txn = el_txn(e);
         if (status[txn] != ST_COMMIT) continue;
-        const uint64_t row = pairs[i] >> 32;
+        const uint64_t row = pair_row(pairs[i]);
         const uint64_t val = (ew && ew[i]) ? 0ull : f0[row];
         dig += mix64(val ^ mix64(((uint64_t)txn << 32) ^ pkey[row]));
     }
@@ -592,17 +451,17 @@ __global__ __launch_bounds__(kBlock) void k_exec_reads(const uint64_t *__restric
 }
 
 __global__ __launch_bounds__(kBlock) void k_exec_writes(const uint64_t *__restrict__ pairs,
-                                                        const uint32_t *__restrict__ el, uint64_t n,
+                                                        const uint64_t *__restrict__ el, uint64_t n,
                                                         const uint8_t *__restrict__ status,
                                                         uint64_t *__restrict__ f0, Counters *ctr) {
     __shared__ uint32_t part[4];
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     uint32_t cnt = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t e = el[i];
+        const uint64_t e = el[i];
         if (!(e & EL_WR)) continue;
-        if (status[e >> 4] != ST_COMMIT) continue;
-        f0[pairs[i] >> 32] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+        if (status[el_txn(e)] != ST_COMMIT) continue;
+        f0[pair_row(pairs[i])] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
         cnt++;
     }
 #pragma unroll
@@ -615,14 +474,13 @@ __global__ __launch_bounds__(kBlock) void k_exec_writes(const uint64_t *__restri
     }
 }
 
-void launch_exec(hipStream_t s, int calvin, const uint64_t *pairs, const uint32_t *el,
-                 const uint8_t *ew, uint64_t n, const uint8_t *status, uint64_t *f0,
-                 const uint64_t *pkey, Counters *ctr) {
+void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
+                 uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
+                 Counters *ctr) {
     if (n == 0) return;
     uint64_t blocks = (n + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
-    k_exec_reads<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, calvin ? ew : nullptr, n, status, f0,
-                                                     pkey, ctr);
+    k_exec_reads<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
     k_exec_writes<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, n, status, f0, ctr);
 }
 
@@ -677,23 +535,9 @@ void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,
                               const uint64_t *f0, uint64_t *out, Counters *ctr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const TableDesc &t = tabs.t[table];
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t key = keys[i];
-        const uint64_t b = bucket_of(t, key);
-        bool found = false;
         uint64_t row = 0;
-        if (t.bstart == nullptr) {
-            const IxEntry e = t.ix[b];
-            if (e.key == key) { row = e.row; found = true; }
-        } else {
-            for (uint32_t j = t.bstart[b], end = t.bstart[b + 1]; j < end; j++) {
-                const IxEntry e = t.ix[j];
-                if (e.key == key) { row = e.row; found = true; break; }
-            }
-        }
-        if (!found) { set_err(ctr, ERRB_KEY); out[i] = 0; continue; }
-        out[i] = f0[t.row_base + row];
+        out[i] = probe_row(tabs, table, keys[i], row, ctr) ? f0[row] : 0ull;
     }
 }
 

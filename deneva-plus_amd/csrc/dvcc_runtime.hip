@@ -14,7 +14,7 @@
 #include <new>
 #include <vector>
 
-#include "dvcc_internal.h"
+#include "dvcc_common.h"
 
 using namespace dvcc;
 
@@ -42,18 +42,16 @@ struct dv_ctx {
 
     // workspace (capacities from cfg)
     uint64_t *pairs[2] = {nullptr, nullptr};
-    uint32_t *vals[2] = {nullptr, nullptr};
-    uint32_t *el = nullptr;
+    uint64_t *el = nullptr;                          // row-queue elements (sorted)
     uint8_t *ew = nullptr;
     uint32_t *counts = nullptr, *digit_tot = nullptr;
-    uint32_t *agg_f = nullptr, *agg_v = nullptr, *carry = nullptr;
-    uint32_t *agg_c = nullptr, *off = nullptr;      // decision-round compaction
-    uint32_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
-    uint32_t *need = nullptr;                        // per txn: accesses not yet OK
-    uint8_t *abortf = nullptr;                       // per txn: an access aborted it
+    uint64_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
+    uint8_t *vb8 = nullptr;                          // per access: verdict
+    uint32_t *tb_start = nullptr, *tb_end = nullptr; // per txn: its access range
     uint64_t *desc = nullptr;                        // look-back tile descriptors
-    uint32_t *tile_ctr = nullptr;                    // per-round tile tickets
-    uint32_t round_tag = 0;                          // descriptor tag of the last round
+    uint32_t *tile_ctr = nullptr;                    // tile tickets, one per single-pass launch
+    uint32_t round_tag = 0;                          // descriptor tag of the last pass
+    uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
     Counters *h_ctr = nullptr;  // pinned host mirror
@@ -115,6 +113,38 @@ int bits_for(uint64_t n) {  // bits needed to represent values in [0, n)
     int b = 0;
     while (b < 64 && (1ull << b) < n) b++;
     return b;
+}
+
+RoundBufs round_bufs(dv_ctx *c) {
+    RoundBufs b;
+    b.el0 = c->el;
+    b.rel[0] = c->rel[0];
+    b.rel[1] = c->rel[1];
+    b.vb8 = c->vb8;
+    b.status = c->status;
+    b.tb_start = c->tb_start;
+    b.tb_end = c->tb_end;
+    b.desc = c->desc;
+    b.tile_ctr = c->tile_ctr;
+    b.ctr = c->ctr;
+    return b;
+}
+
+// descriptor tag of the next single-pass launch (tags are kTagBits wide)
+uint32_t next_tag(dv_ctx *c) {
+    if (++c->round_tag >= (1u << 25)) {
+        (void)hipMemsetAsync(c->desc, 0, (size_t)((c->cfg.max_acc + kRTile - 1) / kRTile) * 8,
+                             c->stream);
+        c->round_tag = 1;
+    }
+    return c->round_tag;
+}
+
+// a zeroed tile-ticket counter for the next single-pass launch
+uint32_t *next_ticket(dv_ctx *c) {
+    if (c->ticket > 0 && c->ticket % kTileCtrs == 0)
+        (void)hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream);
+    return &c->tile_ctr[c->ticket++ % kTileCtrs];
 }
 
 Tables make_tables(dv_ctx *c) {
@@ -195,8 +225,8 @@ void dv_close(dv_ctx *c) {
         dfree(t.ix);
         dfree(t.bstart);
     }
-    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->vals[0], c->vals[1], c->el,
-                    c->ew, c->counts, c->digit_tot, c->agg_f, c->agg_v, c->carry, c->agg_c, c->off, c->rel[0], c->rel[1], c->need, c->abortf, c->desc, c->tile_ctr, c->status,
+    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el,
+                    c->ew, c->counts, c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tb_start, c->tb_end, c->desc, c->tile_ctr, c->status,
                     c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
                     c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
@@ -214,7 +244,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
         cfg->cc_alg != DV_CALVIN)
         return DV_ERR_ARG;
     if (cfg->max_txn == 0 || cfg->max_txn > kMaxTxn || cfg->max_acc == 0 ||
-        cfg->max_acc > 0x7FFFFFFFull || cfg->part_cnt == 0 || cfg->part_id >= cfg->part_cnt)
+        cfg->max_acc > kMaxAcc || cfg->part_cnt == 0 || cfg->part_id >= cfg->part_cnt)
         return DV_ERR_ARG;
     int ndev = 0;
     if (dv_device_count(&ndev) != DV_OK || cfg->device < 0 || cfg->device >= ndev)
@@ -234,28 +264,21 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r) r = dalloc(&c->el, A);
     if (!r) r = dalloc(&c->counts, (uint64_t)kRadix * nb);
     if (!r) r = dalloc(&c->digit_tot, kRadix);
-    if (!r) r = dalloc(&c->agg_f, nb);
-    if (!r) r = dalloc(&c->agg_v, nb);
-    if (!r) r = dalloc(&c->carry, nb);
-    if (!r) r = dalloc(&c->agg_c, nb);
-    if (!r) r = dalloc(&c->off, nb);
     if (!r) r = dalloc(&c->status, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->ctr, 1);
+    const uint32_t rnb = (uint32_t)((A + kRTile - 1) / kRTile);  // single-pass tiles
+    if (!r) r = dalloc(&c->tb_start, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->tb_end, c->n_txn_cap_pad);
+    if (!r) r = dalloc(&c->desc, rnb);
+    if (!r) r = dalloc(&c->tile_ctr, kTileCtrs);
+    if (!r) r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)rnb * 8, c->stream), "memset");
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = dalloc(&c->rel[0], A);
         if (!r) r = dalloc(&c->rel[1], A);
-        if (!r) r = dalloc(&c->need, c->n_txn_cap_pad);
-        if (!r) r = dalloc(&c->abortf, c->n_txn_cap_pad);
-        if (!r) r = dalloc(&c->desc, nb);
-        if (!r) r = dalloc(&c->tile_ctr, kTileCtrs);
-        if (!r) r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)nb * 8, c->stream), "memset");
+        if (!r) r = dalloc(&c->vb8, A);
     }
-    if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
-    if (!r) r = dalloc(&c->ctr, 1);
-    if (!r && cfg->cc_alg == DV_CALVIN) {
-        r = dalloc(&c->vals[0], A);
-        if (!r) r = dalloc(&c->vals[1], A);
-        if (!r) r = dalloc(&c->ew, A);
-    }
+    if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->ew, A);
     if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)),
                          "hipHostMalloc");
     if (!r && timing(c)) {
@@ -273,12 +296,13 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
 }
 
 void *dv_stream(dv_ctx *c) { return c ? (void *)c->stream : nullptr; }
+void *dv_own_stream(dv_ctx *c) { return c ? (void *)c->own_stream : nullptr; }
 
 int dv_set_stream(dv_ctx *c, void *stream) {
     if (!c) return DV_ERR_ARG;
     if (c->phase != 0) return DV_ERR_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
-    c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own_stream;
+    c->stream = reinterpret_cast<hipStream_t>(stream);
     return DV_OK;
 }
 
@@ -460,23 +484,28 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
     HIPCHK(hipMemsetAsync(c->verdict, 0, c->n_txn_pad ? c->n_txn_pad : 4, c->stream));
     launch_status_init(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC);
-    if (!calvin) HIPCHK(hipMemsetAsync(c->need, 0, (size_t)(c->n_txn_pad ? c->n_txn_pad : 4) * 4, c->stream));
+    {  // txns without accesses here keep an empty range
+        const size_t tb_bytes = (size_t)(c->n_txn_pad ? c->n_txn_pad : 4) * 4;
+        HIPCHK(hipMemsetAsync(c->tb_start, 0, tb_bytes, c->stream));
+        HIPCHK(hipMemsetAsync(c->tb_end, 0, tb_bytes, c->stream));
+    }
+    HIPCHK(hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream));
+    c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
-                 ep->n_txn, c->pairs[0], calvin ? c->vals[0] : nullptr, calvin ? nullptr : c->need,
-                 c->ctr);
+                 ep->n_txn, calvin, c->pairs[0], c->tb_start, c->tb_end, c->ctr);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
-    c->sorted = radix_sort_rows(c->stream, c->pairs, calvin ? c->vals : nullptr, ep->n_acc, key_bits,
-                                c->counts, c->digit_tot, timing(c) ? c->sev : nullptr);
-    launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, calvin ? 1 : 0, c->el, c->ctr);
+    c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
+                                timing(c) ? c->sev : nullptr);
+    launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, calvin ? 1 : 0, c->tb_start, c->el,
+                       c->ctr);
     rec(c, 2);
     if (calvin) {
-        calvin_grant(c->stream, c->el, c->vals[c->sorted], ep->n_acc, d_grant, c->ew, c->agg_f,
-                     c->agg_v, c->carry);
+        const uint32_t tag = next_tag(c);
+        calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
-        rounds_epoch_init(c->stream, (uint32_t)ep->n_acc, c->n_txn_pad, c->need, c->abortf,
-                          c->tile_ctr, c->ctr);
+        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc);
         c->live_ub = (uint32_t)ep->n_acc;
     }
     rec(c, 3);
@@ -491,19 +520,13 @@ namespace {
 // then write verdict bytes, single-GPU epochs settle statuses directly
 void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     const uint32_t r = c->rounds;
-    const uint32_t *in = r == 0 ? c->el : c->rel[(r - 1) & 1];
-    uint32_t *out = c->rel[r & 1];
-    if (r > 0 && r % kTileCtrs == 0)
-        (void)hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream);
-    if (++c->round_tag >= (1u << 25)) {  // descriptor tags are 25 bits
-        (void)hipMemsetAsync(c->desc, 0, (size_t)nblocks_for(c->cfg.max_acc) * 8, c->stream);
-        c->round_tag = 1;
-    }
-    round_pass(c->stream, r == 0, c->cfg.cc_alg != DV_OCC, in, out, c->live_ub, &c->ctr->nlive[r & 1],
-               &c->ctr->nlive[(r + 1) & 1], c->status, c->need, c->abortf, c->desc,
-               &c->tile_ctr[r % kTileCtrs], c->round_tag, c->ctr);
-    if (settle) round_settle(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, c->ctr);
-    else round_verdict(c->stream, c->status, c->need, c->abortf, c->n_txn_pad, d_verdict);
+    const uint32_t tag = next_tag(c);
+    uint32_t *tc = next_ticket(c);
+    const RoundBufs b = round_bufs(c);
+    round_pass(c->stream, b, r, c->cfg.cc_alg != DV_OCC, c->live_ub, tag,
+               (uint32_t)(tc - c->tile_ctr));
+    if (settle) round_settle(c->stream, b, c->n_txn);
+    else round_verdict(c->stream, b, c->n_txn, d_verdict);
     c->rounds++;
 }
 
@@ -534,7 +557,7 @@ int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
 int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
     if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
     if (c->rounds == 0) return DV_ERR_STATE;
-    round_apply(c->stream, c->status, d_verdict ? d_verdict : c->verdict, c->n_txn_pad, c->ctr);
+    round_apply(c->stream, round_bufs(c), c->n_txn, d_verdict ? d_verdict : c->verdict);
     HIPCHK(hipGetLastError());
     return round_sync(c, undecided);
 }
@@ -543,7 +566,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     if (!c || c->phase != 1) return DV_ERR_STATE;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     rec(c, 4);
-    launch_exec(c->stream, calvin ? 1 : 0, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status,
+    launch_exec(c->stream, c->pairs[c->sorted], c->el, calvin ? c->ew : nullptr, c->n_acc, c->status,
                 c->f0, c->pkey, c->ctr);
     launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
     rec(c, 5);

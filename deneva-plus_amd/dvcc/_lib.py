@@ -8,7 +8,7 @@ import ctypes
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "build", "libdvcc.so")
+LIB_PATH = os.environ.get("DVCC_LIB") or os.path.join(PKG_DIR, "build", "libdvcc.so")
 
 DV_OK = 0
 DV_ERR_ARG = -1
@@ -86,6 +86,7 @@ SIGNATURES = [
     ("dv_open", ctypes.c_int, [_P(_vp), _P(Config)]),
     ("dv_close", None, [_vp]),
     ("dv_stream", _vp, [_vp]),
+    ("dv_own_stream", _vp, [_vp]),
     ("dv_set_stream", ctypes.c_int, [_vp, _vp]),
     ("dv_create_table", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_uint32]),

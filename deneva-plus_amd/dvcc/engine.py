@@ -114,8 +114,11 @@ class CCEngine:
         return L.lib().dv_stream(self._ctx)
 
     def set_stream(self, stream):
-        """Run on an external hipStream_t (e.g. torch's current stream); None =
-        the context's own stream."""
+        """Run on the hipStream_t handle `stream` (an int such as
+        torch.cuda.current_stream().cuda_stream; 0 is the default stream);
+        None returns to the context's own stream."""
+        if stream is None:
+            stream = L.lib().dv_own_stream(self._ctx)
         L.check(L.lib().dv_set_stream(self._ctx, stream), "dv_set_stream")
 
     # ---- storage (Workload::init_schema / init_table; IndexHash::index_insert)

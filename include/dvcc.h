@@ -158,10 +158,12 @@ int dv_device_count(int *count);
 
 int dv_open(dv_ctx **ctx, const dv_config *cfg);
 void dv_close(dv_ctx *ctx);
-void *dv_stream(dv_ctx *ctx); /* the hipStream_t the context launches on */
-/* launch on an external hipStream_t (e.g. the caller's framework stream) so the
- * engine, the caller's copies and its RCCL collectives share one ordering;
- * NULL restores the context's own stream */
+void *dv_stream(dv_ctx *ctx);     /* the hipStream_t the context launches on */
+void *dv_own_stream(dv_ctx *ctx); /* the stream dv_open created              */
+/* launch on `stream` exactly as given (NULL = the HIP default stream), e.g. the
+ * caller's framework stream, so the engine, the caller's copies and its RCCL
+ * collectives share one ordering; dv_set_stream(ctx, dv_own_stream(ctx))
+ * returns to the context's own stream */
 int dv_set_stream(dv_ctx *ctx, void *stream);
 
 /* tables: hot column = the 8-byte F0 prefix every YCSB txn reads/writes
