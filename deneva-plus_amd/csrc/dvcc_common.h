@@ -154,7 +154,12 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
             d = __hip_atomic_load(&desc[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ready = desc_tag(d) == tag && desc_state(d) != 0;
         }
-        if (!__all(ready)) {
+        // only the descriptors up to the nearest inclusive one are needed
+        // (t < 0 acts as one); later ones may still be unpublished
+        const uint64_t incmask = __ballot(ready && (t < 0 || desc_state(d) == D_INC));
+        const uint32_t stop = incmask ? (uint32_t)__builtin_ctzll(incmask) : 64u;
+        const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
+        if (__ballot(!ready) & need) {
             if (++spins > kSpinLimit) {
                 if (lane == 0) set_err(ctr, ERRB_SPIN);
                 break;
@@ -162,9 +167,6 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
             __builtin_amdgcn_s_sleep(1);
             continue;
         }
-        // fold lanes nearest-first up to the first inclusive one (t < 0 acts as one)
-        const uint64_t incmask = __ballot(t < 0 || desc_state(d) == D_INC);
-        const uint32_t stop = incmask ? (uint32_t)__builtin_ctzll(incmask) : 64u;
         for (uint32_t k = 0; k < 64 && k <= stop; k++) {
             const uint32_t lo = __shfl((uint32_t)d, (int)k, 64);
             const uint32_t hi = __shfl((uint32_t)(d >> 32), (int)k, 64);
@@ -183,8 +185,8 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
 // ---- tiles of 64-bit row-queue elements staged through LDS ----------------
 // kRIPT consecutive elements per thread; the LDS image pads one slot per
 // kRIPT so each lane's ds_read_b64 run is bank-conflict free.
-constexpr int kRIPT = 8;
-constexpr int kRTile = kBlock * kRIPT;  // 2048 elements per workgroup
+constexpr int kRIPT = 16;
+constexpr int kRTile = kBlock * kRIPT;  // 4096 elements per workgroup
 __device__ __forceinline__ uint32_t rpad(uint32_t j) { return j + j / kRIPT; }
 
 // coalesced load of elements [base, base + tile_n) into s (padded) and the

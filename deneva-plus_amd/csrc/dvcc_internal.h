@@ -48,9 +48,10 @@ struct Counters {
     uint32_t err;         // ERRB_* bits of every failure seen
     uint32_t undecided;   // txns still undecided after the last round
     uint32_t committed;
-    uint32_t pad0;
+    uint32_t pad1;
     uint32_t nlive[2];    // live accesses of the current / next decision round
-    uint32_t pad1[2];
+    uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
+    uint32_t pad0[2];
     unsigned long long write_cnt;
     unsigned long long read_digest;
 };
@@ -106,17 +107,29 @@ struct RoundBufs {
     uint64_t *rel[2];        // live elements, ping-pong
     uint8_t *vb8;            // per access
     uint8_t *status;         // per txn
+    uint32_t *ulist[2];      // undecided txns, ping-pong (single-GPU settle)
     const uint32_t *tb_start, *tb_end;
     uint64_t *desc;
     uint32_t *tile_ctr;
     Counters *ctr;
 };
+// Host-mapped progress record: the pass of round r (r >= 1) publishes the
+// outcome of round r - 1 so the host can follow the rounds without
+// synchronising the stream.  Each word is one 64-bit store, so round and
+// undecided count are always consistent; nlive may lag (still an upper bound).
+struct RoundPub {
+    unsigned long long ru;  // rounds settled << 32 | undecided txns
+    unsigned long long le;  // live accesses << 32 | error bits
+};
 void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc);
+// settle = single GPU (the following settle compacts the undecided list; a
+// pass whose round starts with no undecided txn is a no-op)
 void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
-                uint32_t tag, uint32_t ticket);
-// single GPU: settle statuses from the verdicts; partitioned: local verdict
-// bytes (bit1 abort, bit0 wait), then apply the MAX-combined verdicts
-void round_settle(hipStream_t s, const RoundBufs &b, uint32_t n_txn);
+                uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub);
+// single GPU: settle statuses from the verdicts, walking the undecided-txn
+// list (ub = upper bound of its length); partitioned: local verdict bytes
+// (bit1 abort, bit0 wait), then apply the MAX-combined verdicts
+void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub);
 void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict);
 void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_t *verdict);
 
@@ -136,6 +149,5 @@ void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, uint64
                          uint8_t *types, uint32_t *acc_txn, uint8_t *tables);
 
 inline uint32_t nblocks_for(uint64_t n) { return (uint32_t)((n + kTile - 1) / kTile); }
-inline uint32_t rblocks_for(uint64_t n) { return (uint32_t)((n + kBlock * 8 - 1) / (kBlock * 8)); }
 
 }  // namespace dvcc

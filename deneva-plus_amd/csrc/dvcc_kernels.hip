@@ -47,13 +47,14 @@ __device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint6
     return found;
 }
 
-// One access per lane (input order: a txn's accesses are contiguous).  Besides
-// the sort key it records the txn's access range [tb_start, tb_end) and the
-// access's position in it, and -- unless repeats are allowed (Calvin dedups
-// them, TxnManager::get_lock txn.cpp:778-788) -- flags a txn naming one row
-// twice.  Runs of one txn are found with wave ballots; a run that began in an
-// earlier wave is walked back in memory (at most one per wave).
-template <bool ALLOW_DUP>
+// Input order: a txn's accesses are contiguous.  Each thread takes kPV
+// consecutive accesses (vector loads, kPV independent index probes in
+// flight).  Besides the sort key it records each txn's access range
+// [tb_start, tb_end) and every access's position in it: the start of the run
+// of equal txns is a max-scan of run-start indices over the wave; a run that
+// began in an earlier wave is walked back in memory (at most one per wave).
+// Repeated rows inside a txn are detected later, in row order (seg_prepare).
+constexpr int kPV = 4;
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
@@ -61,63 +62,109 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t n_txn, uint64_t *__restrict__ pairs,
                                                   uint32_t *__restrict__ tb_start,
                                                   uint32_t *__restrict__ tb_end, Counters *ctr) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint32_t lane = threadIdx.x & 63;
-    // block-uniform trip count so every lane takes part in the wave ballots
-    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < n; b0 += stride) {
-        const uint64_t i = b0 + threadIdx.x;
-        const bool valid = i < n;
-        uint32_t txn = 0xFFFFFFFFu, tb = 0, wr = 0;
-        uint64_t key = 0, row = 0;
-        bool bad_txn = false;
-        if (valid) {
-            txn = acc_txn[i];
-            key = keys[i];
-            tb = tables ? tables[i] : 0u;
-            wr = types[i] == DV_WR ? 1u : 0u;
-            probe_row(tabs, tb, key, row, ctr);
-            bad_txn = txn >= n_txn || (i > 0 && acc_txn[i - 1] > txn);
-            if (bad_txn) set_err(ctr, ERRB_TXN);
-        }
-        // runs of equal txn inside the wave
-        const uint32_t tprev = __shfl_up(txn, 1, 64);
-        const bool start = valid && (lane == 0 || tprev != txn);
-        const uint64_t smask = __ballot(start);
-        const uint64_t below = smask & (lane == 63 ? ~0ull : ((2ull << lane) - 1));
-        const uint32_t run0 = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
-        const uint32_t depth = valid ? lane - run0 : 0u;
-        bool dup = false;
-        if (!ALLOW_DUP) {
-            uint32_t maxd = depth;
+    const uint64_t per_block = (uint64_t)kBlock * kPV;
+    const uint64_t stride = (uint64_t)gridDim.x * per_block;
+    // block-uniform trip count so every lane takes part in the wave scans
+    for (uint64_t b0 = (uint64_t)blockIdx.x * per_block; b0 < n; b0 += stride) {
+        const uint64_t wave0 = b0 + (threadIdx.x & ~63u) * kPV;   // first access of this wave
+        const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPV;       // first access of this thread
+        uint32_t txn[kPV], wr[kPV], tb[kPV];
+        uint64_t key[kPV], row[kPV];
+        if (i0 + kPV <= n) {
+            const uint4 t4 = *reinterpret_cast<const uint4 *>(acc_txn + i0);
+            txn[0] = t4.x; txn[1] = t4.y; txn[2] = t4.z; txn[3] = t4.w;
+            const ulonglong2 k0 = *reinterpret_cast<const ulonglong2 *>(keys + i0);
+            const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + 2);
+            key[0] = k0.x; key[1] = k0.y; key[2] = k1.x; key[3] = k1.y;
+            const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0);
+            const uint32_t tt = tables ? *reinterpret_cast<const uint32_t *>(tables + i0) : 0u;
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                const uint32_t o = __shfl_xor(maxd, off, 64);
-                maxd = o > maxd ? o : maxd;
+            for (int j = 0; j < kPV; j++) {
+                wr[j] = ((ty >> (8 * j)) & 0xFFu) == DV_WR ? 1u : 0u;
+                tb[j] = (tt >> (8 * j)) & 0xFFu;
             }
-            for (uint32_t d = 1; d <= maxd; d++) {
-                const uint64_t kp = __shfl_up(key, d, 64);
-                const uint32_t bp = __shfl_up(tb, d, 64);
-                if (d <= depth && kp == key && bp == tb) dup = true;
-            }
-        }
-        uint32_t before = 0;  // accesses of this txn in earlier waves
-        if (valid && run0 == 0 && i > (uint64_t)lane) {
-            for (uint64_t j = i - lane; j-- > 0;) {
-                if (acc_txn[j] != txn) break;
-                before++;
-                if (!ALLOW_DUP && keys[j] == key && (tables ? tables[j] : 0u) == tb) dup = true;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPV; j++) {
+                const bool ok = i0 + j < n;
+                txn[j] = ok ? acc_txn[i0 + j] : 0xFFFFFFFFu;
+                key[j] = ok ? keys[i0 + j] : 0ull;
+                wr[j] = ok && types[i0 + j] == DV_WR ? 1u : 0u;
+                tb[j] = ok && tables ? tables[i0 + j] : 0u;
             }
         }
-        if (valid) {
-            if (dup) set_err(ctr, ERRB_DUP);
-            const uint32_t pos = depth + before;
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            row[j] = 0;
+            if (i0 + j < n) {
+#ifdef DVCC_EXP_NO_INDEX
+                row[j] = key[j];
+#else
+                probe_row(tabs, tb[j], key[j], row[j], ctr);
+#endif
+            }
+        }
+        // run starts and their max-scan
+        uint32_t prev = __shfl_up(txn[kPV - 1], 1, 64);
+        if (lane == 0) prev = wave0 > 0 && wave0 - 1 < n ? acc_txn[wave0 - 1] : 0xFFFFFFFEu;
+        uint64_t st[kPV];
+        uint64_t mx = 0;
+        bool bad = false;
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            const uint32_t pt = j == 0 ? prev : txn[j - 1];
+            const bool valid = i0 + j < n;
+            const bool start = valid && (i0 + j == 0 || pt != txn[j]);
+            if (valid && (txn[j] >= n_txn || (i0 + j > 0 && pt > txn[j] && pt != 0xFFFFFFFEu))) bad = true;
+            mx = start ? i0 + j + 1 : mx;  // +1: 0 means "no start yet"
+            st[j] = mx;
+        }
+        uint64_t inc = mx;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint64_t o = __shfl_up(inc, off, 64);
+            if (lane >= (uint32_t)off && o > inc) inc = o;
+        }
+        uint64_t ex = __shfl_up(inc, 1, 64);
+        if (lane == 0) ex = 0;
+        // the wave's first run may have begun before the wave
+        uint64_t carry = 0;
+        if (lane == 0 && wave0 > 0 && wave0 < n && acc_txn[wave0 - 1] == txn[0]) {
+            uint64_t j = wave0 - 1;
+            while (j > 0 && acc_txn[j - 1] == txn[0]) j--;
+            carry = j + 1;
+        }
+        carry = __shfl(carry, 0, 64);
+        if (ex == 0) ex = carry;
+        const uint32_t nxt_lane = __shfl_down(txn[0], 1, 64);
+        const uint64_t in_last = i0 + kPV;
+        uint32_t nxt_last = lane == 63 ? (in_last < n ? acc_txn[in_last] : 0xFFFFFFFFu) : nxt_lane;
+        if (i0 + kPV > n) nxt_last = 0xFFFFFFFFu;
+        if (bad) set_err(ctr, ERRB_TXN);
+        uint64_t out[kPV];
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            const uint64_t i = i0 + j;
+            out[j] = 0;
+            if (i >= n) continue;
+            const uint64_t start = (st[j] ? st[j] : ex) - 1;
+            const uint32_t pos = (uint32_t)(i - start);
             if (pos >= kMaxPos) set_err(ctr, ERRB_BIG);
-            const uint32_t t_ok = bad_txn ? 0u : txn;
-            pairs[i] = pair_pack(row, t_ok, pos & (kMaxPos - 1), wr);
-            if (!bad_txn) {
-                if (pos == 0) tb_start[txn] = (uint32_t)i;
-                if (i + 1 == n || acc_txn[i + 1] != txn) tb_end[txn] = (uint32_t)(i + 1);
+            const uint32_t t = txn[j] < n_txn ? txn[j] : 0u;
+            out[j] = pair_pack(row[j], t, pos & (kMaxPos - 1), wr[j]);
+            if (txn[j] < n_txn) {
+                if (pos == 0) tb_start[t] = (uint32_t)i;
+                const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
+                if (i + 1 == n || nt != txn[j]) tb_end[t] = (uint32_t)(i + 1);
             }
+        }
+        if (i0 + kPV <= n) {
+            *reinterpret_cast<ulonglong2 *>(pairs + i0) = ulonglong2{out[0], out[1]};
+            *reinterpret_cast<ulonglong2 *>(pairs + i0 + 2) = ulonglong2{out[2], out[3]};
+        } else {
+            for (int j = 0; j < kPV; j++)
+                if (i0 + j < n) pairs[i0 + j] = out[j];
         }
     }
 }
@@ -126,16 +173,12 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   bool allow_dup, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   Counters *ctr) {
+    (void)allow_dup;  // repeats are classified in row order (k_seg_prepare)
     if (n_acc == 0) return;
-    uint64_t blocks = (n_acc + kBlock - 1) / kBlock;
-    if (blocks > 8192) blocks = 8192;
-    const uint32_t g = (uint32_t)blocks;
-    if (allow_dup)
-        k_probe<true><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, pairs,
-                                           tb_start, tb_end, ctr);
-    else
-        k_probe<false><<<g, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, pairs,
-                                            tb_start, tb_end, ctr);
+    uint64_t blocks = (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
+    if (blocks > 4096) blocks = 4096;
+    k_probe<<<(uint32_t)blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
+                                                pairs, tb_start, tb_end, ctr);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -283,48 +326,84 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
 }
 
 // ------------------------------------------------------- queue elements
-// row-queue element of sorted position i: heads, same-txn repeats, Calvin
-// grant-group boundaries, and the access id tb_start[txn] + pos
+// Row-queue element of sorted position i: queue heads, repeats of one txn on
+// one row (an error for 2PL/OCC; Calvin merges them into one lock request),
+// Calvin grant-group boundaries, and the access id tb_start[txn] + pos.
+// kPV consecutive keys per thread, vector loads and stores.
+__device__ __forceinline__ uint32_t prev_entry_wr(const uint64_t *__restrict__ pairs, uint64_t e) {
+    // lock type of the queue entry ending at e: a repeat access keeps the type
+    // of its txn's first access to the row (TxnManager::get_lock, txn.cpp:778-788)
+    const uint64_t pe = pairs[e];
+    while (e > 0) {
+        const uint64_t qq = pairs[e - 1];
+        if (pair_row(qq) != pair_row(pe) || pair_txn(qq) != pair_txn(pe)) break;
+        e--;
+    }
+    return (uint32_t)pairs[e] & 1u;
+}
+
 __global__ __launch_bounds__(kBlock) void k_seg_prepare(const uint64_t *__restrict__ pairs, uint64_t n,
                                                         int calvin,
                                                         const uint32_t *__restrict__ tb_start,
                                                         uint64_t *__restrict__ el, Counters *ctr) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t p = pairs[i];
-        const uint32_t row = pair_row(p), txn = pair_txn(p);
-        const uint32_t wr = (uint32_t)p & 1u;
-        uint32_t head = 1, dup = 0, bnd = 1;
-        if (i > 0) {
-            const uint64_t q = pairs[i - 1];
-            if (pair_row(q) == row) {
-                head = 0;
-                if (pair_txn(q) == txn) dup = 1;
-                // lock type of the previous queue entry: a repeat access keeps the
-                // type of its txn's first access to the row (TxnManager::get_lock,
-                // system/txn.cpp:778-788)
-                uint64_t e = i - 1;
-                while (e > 0) {
-                    const uint64_t qq = pairs[e - 1];
-                    if (pair_row(qq) != row || pair_txn(qq) != pair_txn(pairs[e])) break;
-                    e--;
-                }
-                const uint32_t prev_entry_wr = (uint32_t)pairs[e] & 1u;
-                bnd = dup ? 0u : ((wr | prev_entry_wr) ? 1u : 0u);
-            }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t per_block = (uint64_t)kBlock * kPV;
+    const uint64_t stride = (uint64_t)gridDim.x * per_block;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * per_block; b0 < n; b0 += stride) {
+        const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPV;
+        uint64_t p[kPV];
+        if (i0 + kPV <= n) {
+            const ulonglong2 a0 = *reinterpret_cast<const ulonglong2 *>(pairs + i0);
+            const ulonglong2 a1 = *reinterpret_cast<const ulonglong2 *>(pairs + i0 + 2);
+            p[0] = a0.x; p[1] = a0.y; p[2] = a1.x; p[3] = a1.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPV; j++) p[j] = i0 + j < n ? pairs[i0 + j] : ~0ull;
         }
-        if (dup && !calvin) set_err(ctr, ERRB_DUP);
-        const uint32_t acc = tb_start[txn] + pair_pos(p);
-        el[i] = el_pack(txn, acc,
-                        ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr);
+        uint64_t q = __shfl_up(p[kPV - 1], 1, 64);
+        if (lane == 0) q = i0 > 0 && i0 - 1 < n ? pairs[i0 - 1] : ~0ull;
+        uint32_t acc[kPV];
+#pragma unroll
+        for (int j = 0; j < kPV; j++) acc[j] = i0 + j < n ? tb_start[pair_txn(p[j])] + pair_pos(p[j]) : 0u;
+        uint64_t out[kPV];
+        bool dup_err = false;
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            const uint64_t i = i0 + j;
+            const uint64_t pj = p[j];
+            const uint64_t pq = j == 0 ? q : p[j - 1];
+            const uint32_t wr = (uint32_t)pj & 1u;
+            uint32_t head = 1, dup = 0, bnd = 1;
+            if (i > 0 && pair_row(pq) == pair_row(pj)) {
+                head = 0;
+                dup = pair_txn(pq) == pair_txn(pj);
+                if (calvin) {
+                    uint32_t pwr = (uint32_t)pq & 1u;
+                    if (i >= 2 && pair_txn(pairs[i - 2]) == pair_txn(pq) && pair_row(pairs[i - 2]) == pair_row(pq))
+                        pwr = prev_entry_wr(pairs, i - 1);  // the previous entry is itself a repeat run
+                    bnd = dup ? 0u : ((wr | pwr) ? 1u : 0u);
+                }
+            }
+            dup_err |= dup && !calvin && i < n;
+            out[j] = el_pack(pair_txn(pj), acc[j],
+                             ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr);
+        }
+        if (dup_err) set_err(ctr, ERRB_DUP);
+        if (i0 + kPV <= n) {
+            *reinterpret_cast<ulonglong2 *>(el + i0) = ulonglong2{out[0], out[1]};
+            *reinterpret_cast<ulonglong2 *>(el + i0 + 2) = ulonglong2{out[2], out[3]};
+        } else {
+            for (int j = 0; j < kPV; j++)
+                if (i0 + j < n) el[i0 + j] = out[j];
+        }
     }
 }
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
                         const uint32_t *tb_start, uint64_t *el, Counters *ctr) {
     if (n == 0) return;
-    uint64_t blocks = (n + kBlock - 1) / kBlock;
-    if (blocks > 8192) blocks = 8192;
+    uint64_t blocks = (n + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
+    if (blocks > 4096) blocks = 4096;
     k_seg_prepare<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, n, calvin, tb_start, el, ctr);
 }
 
@@ -421,56 +500,54 @@ void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // earlier WR of another txn precedes them in the row queue (Calvin only; under
 // NO_WAIT/OCC a committed reader never follows a committed writer).  Reads
 // run before writes (two launches) so every read sees the pre-epoch image.
-__global__ __launch_bounds__(kBlock) void k_exec_reads(const uint64_t *__restrict__ pairs,
-                                                       const uint64_t *__restrict__ el,
-                                                       const uint8_t *__restrict__ ew, uint64_t n,
-                                                       const uint8_t *__restrict__ status,
-                                                       const uint64_t *__restrict__ f0,
-                                                       const uint64_t *__restrict__ pkey,
-                                                       Counters *ctr) {
+template <bool WRITES>
+__global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pairs,
+                                                 const uint64_t *__restrict__ el,
+                                                 const uint8_t *__restrict__ ew, uint64_t n,
+                                                 const uint8_t *__restrict__ status,
+                                                 uint64_t *__restrict__ f0,
+                                                 const uint64_t *__restrict__ pkey, Counters *ctr) {
     __shared__ unsigned long long part[4];
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    unsigned long long dig = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t e = el[i];
-        if (e & EL_WR) continue;
-        const uint32_t txn = el_txn(e);
-        if (status[txn] != ST_COMMIT) continue;
-        const uint64_t row = pair_row(pairs[i]);
-        const uint64_t val = (ew && ew[i]) ? 0ull : f0[row];
-        dig += mix64(val ^ mix64(((uint64_t)txn << 32) ^ pkey[row]));
+    const uint64_t per_block = (uint64_t)kBlock * kPV;
+    const uint64_t stride = (uint64_t)gridDim.x * per_block;
+    unsigned long long acc = 0;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * per_block + (uint64_t)threadIdx.x * kPV; i0 < n;
+         i0 += stride) {
+        uint64_t e[kPV];
+        if (i0 + kPV <= n) {
+            const ulonglong2 a0 = *reinterpret_cast<const ulonglong2 *>(el + i0);
+            const ulonglong2 a1 = *reinterpret_cast<const ulonglong2 *>(el + i0 + 2);
+            e[0] = a0.x; e[1] = a0.y; e[2] = a1.x; e[3] = a1.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPV; j++) e[j] = i0 + j < n ? el[i0 + j] : (WRITES ? 0ull : EL_WR);
+        }
+        uint8_t st[kPV];
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            const bool mine = i0 + j < n && (((e[j] & EL_WR) != 0) == WRITES);
+            st[j] = mine ? status[el_txn(e[j])] : (uint8_t)ST_ABORT;
+        }
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            if (st[j] != ST_COMMIT) continue;
+            const uint64_t row = pair_row(pairs[i0 + j]);
+            if (WRITES) {
+                f0[row] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+                acc++;
+            } else {
+                const uint64_t val = (ew && ew[i0 + j]) ? 0ull : f0[row];
+                acc += mix64(val ^ mix64(((uint64_t)el_txn(e[j]) << 32) ^ pkey[row]));
+            }
+        }
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) dig += __shfl_down(dig, off, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = dig;
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&ctr->read_digest, t);
-    }
-}
-
-__global__ __launch_bounds__(kBlock) void k_exec_writes(const uint64_t *__restrict__ pairs,
-                                                        const uint64_t *__restrict__ el, uint64_t n,
-                                                        const uint8_t *__restrict__ status,
-                                                        uint64_t *__restrict__ f0, Counters *ctr) {
-    __shared__ uint32_t part[4];
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    uint32_t cnt = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t e = el[i];
-        if (!(e & EL_WR)) continue;
-        if (status[el_txn(e)] != ST_COMMIT) continue;
-        f0[pair_row(pairs[i])] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
-        cnt++;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&ctr->write_cnt, (unsigned long long)t);
+        if (t) atomicAdd(WRITES ? &ctr->write_cnt : &ctr->read_digest, t);
     }
 }
 
@@ -478,21 +555,37 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
                  Counters *ctr) {
     if (n == 0) return;
-    uint64_t blocks = (n + kBlock - 1) / kBlock;
-    if (blocks > 4096) blocks = 4096;
-    k_exec_reads<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
-    k_exec_writes<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, n, status, f0, ctr);
+    uint64_t blocks = (n + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
+    if (blocks > 2048) blocks = 2048;
+    k_exec<false><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
+    k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
 }
 
 __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict__ status, uint32_t n,
                                                        uint8_t *__restrict__ out, Counters *ctr) {
     __shared__ uint32_t part[4];
-    const uint32_t stride = gridDim.x * blockDim.x;
     uint32_t cnt = 0;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint32_t c = status[i] == ST_COMMIT ? 1u : 0u;
-        if (out) out[i] = (uint8_t)c;
-        cnt += c;
+    // 16 txns per thread per step
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u; i0 < n;
+         i0 += gridDim.x * blockDim.x * 16u) {
+        if (i0 + 16 <= n && ((uintptr_t)out & 15u) == 0) {
+            uint4 s4 = *reinterpret_cast<const uint4 *>(status + i0);
+            uint32_t w[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                // byte == ST_COMMIT (1) -> 1, else 0 (statuses are 0, 1 or 2)
+                const uint32_t c = w[q] & ~(w[q] >> 1) & 0x01010101u;
+                cnt += __popc(c);
+                w[q] = c;
+            }
+            if (out) *reinterpret_cast<uint4 *>(out + i0) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+            for (uint32_t i = i0; i < n; i++) {
+                const uint32_t c = status[i] == ST_COMMIT ? 1u : 0u;
+                if (out) out[i] = (uint8_t)c;
+                cnt += c;
+            }
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
@@ -507,8 +600,8 @@ __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr) {
     if (!n_txn) return;
-    uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
-    if (blocks > 2048) blocks = 2048;
+    uint32_t blocks = (n_txn + kBlock * 16 - 1) / (kBlock * 16);
+    if (blocks > 1024) blocks = 1024;
     k_commit_out<<<blocks, kBlock, 0, s>>>(status, n_txn, d_commit, ctr);
 }
 

@@ -9,8 +9,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <new>
 #include <vector>
 
@@ -47,6 +49,7 @@ struct dv_ctx {
     uint32_t *counts = nullptr, *digit_tot = nullptr;
     uint64_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
     uint8_t *vb8 = nullptr;                          // per access: verdict
+    uint32_t *ulist[2] = {nullptr, nullptr};         // undecided txns, ping-pong
     uint32_t *tb_start = nullptr, *tb_end = nullptr; // per txn: its access range
     uint64_t *desc = nullptr;                        // look-back tile descriptors
     uint32_t *tile_ctr = nullptr;                    // tile tickets, one per single-pass launch
@@ -70,6 +73,10 @@ struct dv_ctx {
     int sorted = 0;
     uint32_t rounds = 0, sort_passes = 0;
     uint32_t live_ub = 0;  // host-side upper bound of the next round's live accesses
+    uint32_t und_ub = 0;   // host-side upper bound of the undecided-txn list
+    RoundPub *h_pub = nullptr;  // host-mapped round progress (single-GPU rounds)
+    RoundPub *d_pub = nullptr;  // its device address
+    uint32_t rounds_real = 0;   // rounds until every txn was decided
 
     // timing
     hipEvent_t ev[32] = {};
@@ -78,8 +85,6 @@ struct dv_ctx {
 };
 
 namespace {
-
-constexpr int kRoundsPerSync = 2;
 
 inline void dfree(void *p) {
     if (p) (void)hipFree(p);
@@ -122,6 +127,8 @@ RoundBufs round_bufs(dv_ctx *c) {
     b.rel[1] = c->rel[1];
     b.vb8 = c->vb8;
     b.status = c->status;
+    b.ulist[0] = c->ulist[0];
+    b.ulist[1] = c->ulist[1];
     b.tb_start = c->tb_start;
     b.tb_end = c->tb_end;
     b.desc = c->desc;
@@ -226,11 +233,12 @@ void dv_close(dv_ctx *c) {
         dfree(t.bstart);
     }
     void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el,
-                    c->ew, c->counts, c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tb_start, c->tb_end, c->desc, c->tile_ctr, c->status,
+                    c->ew, c->counts, c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr, c->status,
                     c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
                     c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
+    if (c->h_pub) (void)hipHostFree(c->h_pub);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : c->sev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -276,11 +284,21 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = dalloc(&c->rel[0], A);
         if (!r) r = dalloc(&c->rel[1], A);
-        if (!r) r = dalloc(&c->vb8, A);
+        if (!r) r = dalloc(&c->vb8, A + 16);  // dword reads may run 3 B past the end
+        if (!r) r = dalloc(&c->ulist[0], T);
+        if (!r) r = dalloc(&c->ulist[1], T);
     }
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->ew, A);
     if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)),
                          "hipHostMalloc");
+    if (!r && cfg->cc_alg != DV_CALVIN) {
+        r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_pub), sizeof(RoundPub),
+                                   hipHostMallocMapped | hipHostMallocCoherent),
+                     "hipHostMalloc");
+        if (!r) r = hip_fail(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_pub), c->h_pub, 0),
+                             "hipHostGetDevicePointer");
+        if (!r) std::memset(c->h_pub, 0, sizeof(RoundPub));
+    }
     if (!r && timing(c)) {
         for (auto &e : c->ev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
         for (auto &e : c->sev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
@@ -479,6 +497,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->n_txn = ep->n_txn;
     c->n_txn_pad = (ep->n_txn + 3u) & ~3u;
     c->rounds = 0;
+    c->rounds_real = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
@@ -507,6 +526,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     } else {
         rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc);
         c->live_ub = (uint32_t)ep->n_acc;
+        c->und_ub = ep->n_txn;
     }
     rec(c, 3);
     HIPCHK(hipGetLastError());
@@ -524,20 +544,23 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     uint32_t *tc = next_ticket(c);
     const RoundBufs b = round_bufs(c);
     round_pass(c->stream, b, r, c->cfg.cc_alg != DV_OCC, c->live_ub, tag,
-               (uint32_t)(tc - c->tile_ctr));
-    if (settle) round_settle(c->stream, b, c->n_txn);
+               (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr);
+    if (settle) round_settle(c->stream, b, r, c->n_txn, c->und_ub);
     else round_verdict(c->stream, b, c->n_txn, d_verdict);
     c->rounds++;
 }
 
 // read the counters after the last enqueued round
-int round_sync(dv_ctx *c, uint32_t *undecided) {
+// (settle: single-GPU rounds, the undecided count is the list length)
+int round_sync(dv_ctx *c, uint32_t *undecided, bool settle) {
     int r = sync_counters(c);
     if (r) return r;
     r = err_from_bits(c->h_ctr->err);
     if (r) { c->phase = 0; return r; }
     c->live_ub = c->h_ctr->nlive[c->rounds & 1];  // input size of the next round
-    if (undecided) *undecided = c->h_ctr->undecided;
+    const uint32_t und = settle ? c->h_ctr->nund[c->rounds & 1] : c->h_ctr->undecided;
+    c->und_ub = und;
+    if (undecided) *undecided = und;
     return DV_OK;
 }
 
@@ -559,7 +582,7 @@ int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecide
     if (c->rounds == 0) return DV_ERR_STATE;
     round_apply(c->stream, round_bufs(c), c->n_txn, d_verdict ? d_verdict : c->verdict);
     HIPCHK(hipGetLastError());
-    return round_sync(c, undecided);
+    return round_sync(c, undecided, false);
 }
 
 int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
@@ -584,7 +607,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         st->aborted = c->n_txn - c->h_ctr->committed;
         st->write_cnt = c->h_ctr->write_cnt;
         st->read_digest = c->h_ctr->read_digest;
-        st->rounds = c->rounds;
+        st->rounds = calvin ? 0 : (c->rounds_real ? c->rounds_real : c->rounds);
         st->sort_passes = c->sort_passes;
         if (timing(c)) {
             st->ms_probe = elapsed(c, 0, 1);
@@ -605,26 +628,78 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     return DV_OK;
 }
 
+namespace {
+
+// Single-GPU decision rounds, pipelined: kRoundsAhead rounds stay queued
+// while the host follows the published progress record (no stream sync).
+// Each round decides at least the lowest undecided txn, so the undecided
+// count strictly falls from one observed round to the next; rounds queued
+// past the fixpoint are no-ops.
+constexpr uint32_t kRoundsAhead = 2;
+
+// rounds settled so far (and the undecided count after the last of them)
+inline uint32_t pub_round(const dv_ctx *c, uint32_t *und) {
+    const unsigned long long ru = __atomic_load_n(&c->h_pub->ru, __ATOMIC_ACQUIRE);
+    if (und) *und = (uint32_t)ru;
+    return (uint32_t)(ru >> 32);
+}
+
+int wait_published(dv_ctx *c, uint32_t target) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0;; i++) {
+        if (pub_round(c, nullptr) >= target) return DV_OK;
+        if ((i & 255) == 255) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess)  // drained: the record must be there now
+                return pub_round(c, nullptr) >= target ? DV_OK : DV_ERR_STATE;
+            if (q != hipErrorNotReady) return hip_fail(q, "round stream");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// Rounds are published by the NEXT round's pass, so kRoundsAhead >= 2 keeps
+// the round the host waits for always enqueued.
+int run_rounds(dv_ctx *c) {
+    __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
+    uint32_t prev = c->n_txn + 1, seen = 0;
+    for (;;) {
+        while (c->rounds < seen + kRoundsAhead + 1) enqueue_round(c, nullptr, true);
+        int r = hip_fail(hipGetLastError(), "round launch");
+        if (!r) r = wait_published(c, seen + 1);
+        if (r) {
+            (void)hipStreamSynchronize(c->stream);
+            return r;
+        }
+        uint32_t und = 0;
+        seen = pub_round(c, &und);
+        const unsigned long long le = __atomic_load_n(&c->h_pub->le, __ATOMIC_ACQUIRE);
+        r = err_from_bits((uint32_t)le);
+        if (!r && und != 0 && und >= prev) r = DV_ERR_STATE;  // no progress: internal error
+        if (r) {
+            (void)hipStreamSynchronize(c->stream);
+            return r;
+        }
+        if (und == 0) {
+            c->rounds_real = seen;
+            return DV_OK;
+        }
+        prev = und;
+        c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));  // bounds for rounds not yet enqueued
+        c->und_ub = und;
+    }
+}
+
+}  // namespace
+
 int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, uint32_t *d_grant,
                         dv_stats *st) {
     int r = dv_epoch_begin(c, ep, d_grant);
     if (r) return r;
-    if (c->cfg.cc_alg != DV_CALVIN) {
-        // rounds until every txn is decided.  Each round decides at least the
-        // lowest undecided txn, so the undecided count strictly falls between
-        // host syncs; rounds past the fixpoint are no-ops, so several rounds are
-        // enqueued per sync.
-        uint32_t prev = c->n_txn + 1;
-        for (;;) {
-            for (int k = 0; k < kRoundsPerSync; k++) enqueue_round(c, nullptr, true);
-            uint32_t und = 0;
-            r = hip_fail(hipGetLastError(), "round launch");
-            if (!r) r = round_sync(c, &und);
-            if (!r && und >= prev) r = DV_ERR_STATE;  // no progress: internal error
-            if (r) { c->phase = 0; return r; }
-            if (und == 0) break;
-            prev = und;
-        }
+    if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
+        r = run_rounds(c);
+        if (r) { c->phase = 0; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
 }

@@ -199,3 +199,14 @@ def test_config_c_occ_full():
 def test_config_d_single_partition_full(cc):
     g = YCSBQueryGenerator(16_777_216, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
     _check(cc, 16_777_216, [g.gen(1_048_576, dvcc.epoch_seed(0, 1))])
+
+
+@pytest.mark.parametrize("rows,req,theta", [(64, 4, 0.5), (1 << 14, 8, 0.95), (1 << 12, 16, 0.99)])
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_many_rounds(cc, rows, req, theta):
+    """Long decision chains: the pipelined round loop (rounds queued ahead of
+    the host, no-op rounds past the fixpoint) over many rounds."""
+    gen = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=req)
+    epochs = [gen.gen(20_000, 300 + k) for k in range(2)]
+    st = _check(cc, rows, epochs)
+    assert st.rounds >= 2
