@@ -200,6 +200,9 @@ def main():
                           for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")},
         "gen_seconds": t_gen,
     }
+    if world == 1:
+        live, und = eng.round_log()
+        out["round_log_last_epoch"] = {"live": live, "undecided": und}
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(epochs, rows, cc_name, a.cpu_seconds)
     if rank == 0:

@@ -13,12 +13,15 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
-OUT = os.path.join(PKG, "build")
+# DVCC_BUILD_DIR / DVCC_DEFINES: experiment variants (tools/exp_pass.py) only
+OUT = os.environ.get("DVCC_BUILD_DIR") or os.path.join(PKG, "build")
+DEFINES = os.environ.get("DVCC_DEFINES", "").split()
 LIB = os.path.join(OUT, "libdvcc.so")
 INCLUDE = os.path.join(ROOT, "include")
 ARCH = os.environ.get("DVCC_OFFLOAD_ARCH", "gfx950")
 
-HEADERS = [os.path.join(INCLUDE, "dvcc.h"), os.path.join(CSRC, "dvcc_internal.h")]
+HEADERS = [os.path.join(INCLUDE, "dvcc.h"), os.path.join(CSRC, "dvcc_internal.h"),
+           os.path.join(CSRC, "dvcc_common.h")]
 HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_runtime.hip"]
 CPP_SRCS = ["ycsb_gen.cpp"]
 
@@ -44,7 +47,7 @@ def build(force=False, verbose_resources=False):
         objs.append(obj)
         if force or _newer(obj, [src] + HEADERS):
             cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                   "-I", INCLUDE, "-I", CSRC, "-c", src, "-o", obj]
+                   "-I", INCLUDE, "-I", CSRC, "-c", src, "-o", obj] + DEFINES
             if verbose_resources:
                 cmd.insert(1, "-Rpass-analysis=kernel-resource-usage")
             _run(cmd)

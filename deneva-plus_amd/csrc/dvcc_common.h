@@ -190,10 +190,10 @@ constexpr int kRTile = kBlock * kRIPT;  // 4096 elements per workgroup
 __device__ __forceinline__ uint32_t rpad(uint32_t j) { return j + j / kRIPT; }
 
 // coalesced load of elements [base, base + tile_n) into s (padded) and the
-// element after the tile into *s_next (EL_HEAD past the end)
+// element after the tile into *s_next (`past_end` past the end)
 __device__ __forceinline__ void load_tile64(const uint64_t *__restrict__ src, uint32_t base,
                                             uint32_t tile_n, uint32_t n, uint64_t *s,
-                                            uint64_t *s_next) {
+                                            uint64_t *s_next, uint64_t past_end = EL_HEAD) {
     const uint32_t tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < kRIPT / 2; q++) {
@@ -206,7 +206,7 @@ __device__ __forceinline__ void load_tile64(const uint64_t *__restrict__ src, ui
             s[rpad(j)] = src[base + j];
         }
     }
-    if (tid == 0) *s_next = base + tile_n < n ? src[base + tile_n] : (uint64_t)EL_HEAD;
+    if (tid == 0) *s_next = base + tile_n < n ? src[base + tile_n] : past_end;
 }
 
 }  // namespace dvcc

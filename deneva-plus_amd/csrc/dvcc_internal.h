@@ -32,29 +32,47 @@ __host__ __device__ inline uint32_t pair_row(uint64_t p) { return (uint32_t)(p >
 __host__ __device__ inline uint32_t pair_txn(uint64_t p) { return (uint32_t)(p >> 8) & 0xFFFFFFu; }
 __host__ __device__ inline uint32_t pair_pos(uint64_t p) { return (uint32_t)(p >> 1) & 0x7Fu; }
 
-// row-queue element (row order): txn << 32 | access << 4 | flags
+// row-queue element (row order): txn << 32 | id << 4 | flags
+//   id: Calvin -- the access id (index into the epoch's access arrays);
+//       decision rounds -- the access's position in its txn (verdict byte
+//       vb8[txn << slog | pos]).
 //   head: first access of a row queue; dup: repeat access of the same txn to
 //   the same row; bnd: Calvin grant-group boundary; done: decision rounds --
 //   the access is already OK.
 constexpr uint64_t EL_WR = 1u, EL_HEAD = 2u, EL_DUP = 4u, EL_BND = 8u, EL_DONE = 8u;
 __host__ __device__ inline uint32_t el_txn(uint64_t e) { return (uint32_t)(e >> 32); }
 __host__ __device__ inline uint32_t el_acc(uint64_t e) { return (uint32_t)(e >> 4) & 0x0FFFFFFFu; }
+__host__ __device__ inline uint32_t el_pos(uint64_t e) { return (uint32_t)(e >> 4) & (kMaxPos - 1); }
 __host__ __device__ inline uint64_t el_pack(uint32_t txn, uint32_t acc, uint64_t flags) {
     return ((uint64_t)txn << 32) | ((uint64_t)acc << 4) | flags;
 }
+// row of an access for the txn-major execution: row | wr << 31
+constexpr uint32_t AR_WR = 0x80000000u;
+constexpr uint64_t kMaxRows = 0x7FFFFFFFull;
 
-// device counters block (zeroed per epoch)
+// device counters block (zeroed per epoch).  Sums that every workgroup adds
+// to go to one of kSlots line-separated slots (slot = block % kSlots): one
+// device-scope atomic word saturates at ~88 adds/us (MI355X_MICROARCH.md,
+// "dequeue"), so 4096 blocks on one word would cost ~50 us.  The host adds
+// the slots up.
+constexpr int kRoundLog = 64;
+constexpr int kSlots = 32;
+struct alignas(128) CtrSlot {
+    unsigned long long read_digest;
+    unsigned long long write_cnt;
+    uint32_t committed;
+    uint32_t undecided;   // partitioned rounds: txns still undecided after apply
+};
 struct Counters {
     uint32_t err;         // ERRB_* bits of every failure seen
-    uint32_t undecided;   // txns still undecided after the last round
-    uint32_t committed;
-    uint32_t pad1;
+    uint32_t pad1[3];
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
-    uint32_t pad0[2];
-    unsigned long long write_cnt;
-    unsigned long long read_digest;
+    uint32_t log_live[kRoundLog];  // per round: live accesses entering it
+    uint32_t log_und[kRoundLog];   // per round: undecided txns before it
+    CtrSlot slot[kSlots];
 };
+__device__ inline CtrSlot &my_slot(Counters *ctr) { return ctr->slot[blockIdx.x & (kSlots - 1)]; }
 
 struct IxEntry {
     uint64_t key;
@@ -81,10 +99,13 @@ enum : uint32_t {
 };
 
 // ---- probe / queues (dvcc_kernels.hip)
+// pairs: sort keys; tb_start/tb_end: each txn's access range; tlen (optional):
+// its access count; acc_row (optional): row | wr << 31 per access.  An access
+// at position >= 1 << slog in its txn is an error (ERRB_BIG).
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  bool allow_dup, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  Counters *ctr);
+                  uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -100,15 +121,18 @@ void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant
                   uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr);
 
 // decision rounds (dvcc_rounds.hip): vb8 = per-access verdict (1 = permanently
-// OK, 2 = aborts its txn); [tb_start, tb_end) = a txn's accesses here.
+// OK, 2 = aborts its txn) at vb8[txn << slog | pos]; tlen[txn] = the txn's
+// accesses on this partition.
 constexpr uint32_t kTileCtrs = 1024;  // tile tickets, reset every kTileCtrs passes
 struct RoundBufs {
-    const uint64_t *el0;     // round-0 elements (sorted, from seg_prepare)
-    uint64_t *rel[2];        // live elements, ping-pong
-    uint8_t *vb8;            // per access
+    const uint64_t *pairs0;  // round-0 input: the row-sorted pairs
+    void *rel[2];            // live elements (32- or 64-bit), ping-pong
+    bool el32;               // 32-bit round elements (round_el32)
+    uint8_t *vb8;            // per access, txn-strided
+    uint32_t slog;           // log2 of the per-txn stride of vb8
     uint8_t *status;         // per txn
+    const uint8_t *tlen;     // per txn
     uint32_t *ulist[2];      // undecided txns, ping-pong (single-GPU settle)
-    const uint32_t *tb_start, *tb_end;
     uint64_t *desc;
     uint32_t *tile_ctr;
     Counters *ctr;
@@ -120,8 +144,10 @@ struct RoundBufs {
 struct RoundPub {
     unsigned long long ru;  // rounds settled << 32 | undecided txns
     unsigned long long le;  // live accesses << 32 | error bits
+    unsigned long long tl;  // tail launched at round r0 but the live set did not
+                            // fit: r0 << 32 | 1 (the rounds resume from r0)
 };
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc);
+void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn_pad);
 // settle = single GPU (the following settle compacts the undecided list; a
 // pass whose round starts with no undecided txn is a no-op)
 void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
@@ -132,13 +158,27 @@ void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, u
 void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub);
 void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict);
 void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_t *verdict);
+// single GPU: all remaining rounds from round r0 >= 1 in one single-workgroup
+// launch; publishes the final round and 0 undecided (0xFFFFFFFF on failure)
+// through pub, or declines (pub->tl) and does nothing when the live accesses
+// or undecided txns entering round r0 exceed tail_cap()
+constexpr int kTailThreads = 1024;
+void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, RoundPub *pub);
+uint32_t tail_cap(bool el32);  // live accesses the tail holds in LDS
+// round elements ((txn << slog | pos) << 3 | flags) fit 32 bits
+bool round_el32(uint32_t n_txn, uint32_t slog);
 
 // ---- execution and outputs (dvcc_kernels.hip)
 void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4,
                         uint8_t value);
+// Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
                  Counters *ctr);
+// NO_WAIT / WAIT_DIE / OCC: in txn order over the committed txns
+void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+                     const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
+                     const uint64_t *pkey, bool fused, Counters *ctr);
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,

@@ -59,9 +59,12 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n,
-                                                  uint32_t n_txn, uint64_t *__restrict__ pairs,
+                                                  uint32_t n_txn, uint32_t slog,
+                                                  uint64_t *__restrict__ pairs,
                                                   uint32_t *__restrict__ tb_start,
-                                                  uint32_t *__restrict__ tb_end, Counters *ctr) {
+                                                  uint32_t *__restrict__ tb_end,
+                                                  uint8_t *__restrict__ tlen,
+                                                  uint32_t *__restrict__ acc_row, Counters *ctr) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t per_block = (uint64_t)kBlock * kPV;
     const uint64_t stride = (uint64_t)gridDim.x * per_block;
@@ -150,13 +153,27 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
             if (i >= n) continue;
             const uint64_t start = (st[j] ? st[j] : ex) - 1;
             const uint32_t pos = (uint32_t)(i - start);
-            if (pos >= kMaxPos) set_err(ctr, ERRB_BIG);
+            if (pos >> slog) set_err(ctr, ERRB_BIG);
             const uint32_t t = txn[j] < n_txn ? txn[j] : 0u;
             out[j] = pair_pack(row[j], t, pos & (kMaxPos - 1), wr[j]);
             if (txn[j] < n_txn) {
                 if (pos == 0) tb_start[t] = (uint32_t)i;
                 const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
-                if (i + 1 == n || nt != txn[j]) tb_end[t] = (uint32_t)(i + 1);
+                if (i + 1 == n || nt != txn[j]) {
+                    tb_end[t] = (uint32_t)(i + 1);
+                    if (tlen) tlen[t] = (uint8_t)(pos + 1);
+                }
+            }
+        }
+        if (acc_row) {
+            uint32_t ar[kPV];
+#pragma unroll
+            for (int j = 0; j < kPV; j++) ar[j] = (uint32_t)row[j] | (wr[j] ? AR_WR : 0u);
+            if (i0 + kPV <= n) {
+                *reinterpret_cast<uint4 *>(acc_row + i0) = uint4{ar[0], ar[1], ar[2], ar[3]};
+            } else {
+                for (int j = 0; j < kPV; j++)
+                    if (i0 + j < n) acc_row[i0 + j] = ar[j];
             }
         }
         if (i0 + kPV <= n) {
@@ -171,14 +188,13 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
-                  bool allow_dup, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  Counters *ctr) {
-    (void)allow_dup;  // repeats are classified in row order (k_seg_prepare)
+                  uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr) {
     if (n_acc == 0) return;
     uint64_t blocks = (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     if (blocks > 4096) blocks = 4096;
     k_probe<<<(uint32_t)blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
-                                                pairs, tb_start, tb_end, ctr);
+                                                slog, pairs, tb_start, tb_end, tlen, acc_row, ctr);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -547,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pa
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(WRITES ? &ctr->write_cnt : &ctr->read_digest, t);
+        if (t) atomicAdd(WRITES ? &my_slot(ctr).write_cnt : &my_slot(ctr).read_digest, t);
     }
 }
 
@@ -559,6 +575,89 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
     if (blocks > 2048) blocks = 2048;
     k_exec<false><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
     k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
+}
+
+// NO_WAIT / WAIT_DIE / OCC: run_ycsb_1 for the committed txns only, in txn
+// order (acc_row from the probe), one thread per txn with its accesses'
+// loads issued together.  A committed reader never sees a committed writer's
+// value here (2PL: the two conflict, so one launch does both; OCC: reads
+// happen in the access phase, occ.cpp:116-294, so the reads run in a launch
+// before the writes).
+enum : int { EX_READS = 1, EX_WRITES = 2 };
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict__ tb_start,
+                                                     const uint32_t *__restrict__ tb_end,
+                                                     const uint32_t *__restrict__ acc_row,
+                                                     uint32_t n_txn,
+                                                     const uint8_t *__restrict__ status,
+                                                     uint64_t *__restrict__ f0,
+                                                     const uint64_t *__restrict__ pkey,
+                                                     Counters *ctr) {
+    __shared__ unsigned long long part[2][4];
+    unsigned long long dig = 0, wcnt = 0;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
+        if (status[t] != ST_COMMIT) continue;
+        const uint32_t a0 = tb_start[t], len = tb_end[t] - a0;
+        for (uint32_t c = 0; c < len; c += 16) {
+            uint32_t ar[16];
+#pragma unroll
+            for (int k = 0; k < 16; k++) ar[k] = c + k < len ? acc_row[a0 + c + k] : 0xFFFFFFFFu;
+            if (MODE & EX_READS) {
+                uint64_t val[16], pk[16];
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    const bool rd = !(ar[k] & AR_WR);
+                    val[k] = rd ? f0[ar[k]] : 0ull;
+                    pk[k] = rd ? pkey[ar[k]] : 0ull;
+                }
+#pragma unroll
+                for (int k = 0; k < 16; k++)
+                    if (!(ar[k] & AR_WR)) dig += mix64(val[k] ^ mix64(((uint64_t)t << 32) ^ pk[k]));
+            }
+            if (MODE & EX_WRITES) {
+#pragma unroll
+                for (int k = 0; k < 16; k++) {
+                    if (ar[k] != 0xFFFFFFFFu && (ar[k] & AR_WR)) {
+                        f0[ar[k] & ~AR_WR] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+                        wcnt++;
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        dig += __shfl_down(dig, off, 64);
+        wcnt += __shfl_down(wcnt, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        part[0][threadIdx.x >> 6] = dig;
+        part[1][threadIdx.x >> 6] = wcnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long d = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+        const unsigned long long w = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+        if (d) atomicAdd(&my_slot(ctr).read_digest, d);
+        if (w) atomicAdd(&my_slot(ctr).write_cnt, w);
+    }
+}
+
+void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+                     const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
+                     const uint64_t *pkey, bool fused, Counters *ctr) {
+    if (n_txn == 0) return;
+    uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
+    if (blocks > 4096) blocks = 4096;
+    if (fused) {
+        k_exec_txn<EX_READS | EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn,
+                                                                  status, f0, pkey, ctr);
+    } else {
+        k_exec_txn<EX_READS><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
+                                                       pkey, ctr);
+        k_exec_txn<EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
+                                                        pkey, ctr);
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict__ status, uint32_t n,
@@ -593,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&ctr->committed, t);
+        if (t) atomicAdd(&my_slot(ctr).committed, t);
     }
 }
 

@@ -15,13 +15,19 @@
 // A txn commits once all its accesses are OK.  The lowest undecided txn always
 // decides, so rounds terminate; zipf 0.9 epochs of 1M txns take ~20.
 //
-// Layout: a round element is one access (txn << 32 | access << 4 | flags) in
-// row order.  An access reads its txn's status byte (1 B per txn: L2-resident)
-// and writes its own verdict byte vb8[access]; a txn then reads its contiguous
-// access range [tb_start, tb_end) -- plain loads and stores, no atomics.
-// The round pass compacts away accesses of aborted txns and accesses alone in
-// their row queue, stages tiles through LDS for coalesced loads and stores, and
-// is a single launch (decoupled look-back scan, below).
+// Layout.  A round element is one access in row order,
+//     e = ((txn << slog | pos) << 3) | done << 2 | head << 1 | wr
+// with pos = its position in the txn: e >> 3 indexes the access's verdict byte
+// vb8[txn << slog | pos], and a txn reads its 1 << slog verdict bytes with one
+// 16-byte load per 16 accesses.  Elements are 32-bit when the txn, position
+// and flag bits fit (1M txns of <= 16 accesses: 27 bits), else 64-bit.  An
+// access reads its txn's status byte (1 B per txn: L2-resident); aborts go
+// straight to that byte, OKs to the verdict byte -- plain loads and stores,
+// no atomics.  Each pass compacts away what the next round does not need,
+// stages tiles through LDS for coalesced loads and stores, and is a single
+// launch (decoupled look-back scan, dvcc_common.h).  Round 0 reads the
+// row-sorted pairs directly.  Once the live set fits in LDS, one
+// single-workgroup launch runs every remaining round (k_round_tail).
 #include "dvcc_common.h"
 
 namespace dvcc {
@@ -32,105 +38,280 @@ namespace {
 // 8 undecided (WR accesses), 16 = the access is kept for the next round
 constexpr uint32_t B_CA = 1u, B_UA = 2u, B_CW = 4u, B_UW = 8u, B_KEEP = 16u;
 constexpr uint8_t VB_OK = 1, VB_ABORT = 2;
+constexpr uint32_t F_WR = 1u, F_HEAD = 2u, F_DONE = 4u;
 
-// per-element scan value from its txn's status; an access alone in its row
-// queue and the accesses of aborted txns are not kept
-__device__ __forceinline__ uint32_t elem_value(uint64_t e, bool next_head, uint8_t s, int nowait) {
-    const bool single = (e & EL_HEAD) && next_head;
-    const bool wr = (e & EL_WR) != 0;
-    if (s == ST_COMMIT) return (nowait ? B_CA : 0u) | (wr ? B_CW : 0u) | (single ? 0u : B_KEEP);
-    if (s == ST_UNDEC) return (nowait ? B_UA : 0u) | (wr ? B_UW : 0u) | (single ? 0u : B_KEEP);
+template <class E>
+__device__ __forceinline__ uint32_t r_txn(E e, uint32_t slog) {
+    return (uint32_t)(e >> (slog + 3));
+}
+
+// per-element scan value (without B_KEEP) from its txn's status: aborted
+// txns block nobody
+template <class E>
+__device__ __forceinline__ uint32_t elem_value(E e, uint8_t s, int nowait) {
+    const bool wr = (e & F_WR) != 0;
+    if (s == ST_COMMIT) return (nowait ? B_CA : 0u) | (wr ? B_CW : 0u);
+    if (s == ST_UNDEC) return (nowait ? B_UA : 0u) | (wr ? B_UW : 0u);
     return 0u;
 }
 
 // verdict of a live access of an undecided txn from the OR of the scan values
-// in front of it in its row queue
-__device__ __forceinline__ uint64_t decide_elem(uint64_t e, uint32_t excl, int nowait,
-                                                uint8_t *__restrict__ vb8) {
-    if (e & EL_DONE) return e;
+// in front of it in its row queue.  An abort is a final fact about the whole
+// txn, so it goes straight to the txn's status byte (readers of that byte in
+// this same pass may or may not see it yet -- either view is a true fact, and
+// the greedy outcome is unique); an OK is recorded per access for the settle.
+template <class E>
+__device__ __forceinline__ E decide_elem(E e, uint32_t excl, int nowait, uint8_t *__restrict__ vb8,
+                                         uint32_t slog, uint8_t *status) {
+    if (e & F_DONE) return e;
     // NO_WAIT/WAIT_DIE: a WR conflicts with any earlier access, a RD with
     // earlier WRs; OCC: any access with earlier committed writes
-    const uint32_t sel = (nowait && (e & EL_WR)) ? (excl & (B_CA | B_UA)) : ((excl >> 2) & (B_CA | B_UA));
+    const uint32_t sel = (nowait && (e & F_WR)) ? (excl & (B_CA | B_UA)) : ((excl >> 2) & (B_CA | B_UA));
     if (sel & B_CA) {
-#ifndef DVCC_EXP_NO_VB
-        vb8[el_acc(e)] = VB_ABORT;  // Abort (row_lock.cpp:86-90 / occ.cpp:219-234)
-#endif
+        status[r_txn(e, slog)] = ST_ABORT;  // Abort (row_lock.cpp:86-90 / occ.cpp:219-234)
     } else if (!(sel & B_UA)) {
-#ifndef DVCC_EXP_NO_VB
-        vb8[el_acc(e)] = VB_OK;     // granted / validated: permanently OK
-#endif
-        e |= EL_DONE;
+        vb8[e >> 3] = VB_OK;  // granted / validated: permanently OK
+        e |= F_DONE;
     }
     return e;
+}
+
+// reverse segmented OR (right to left; f = a queue ends inside the span,
+// v = some element of the span's first queue piece still needs a verdict)
+struct RAgg {
+    uint32_t f, v;
+};
+__device__ __forceinline__ RAgg rcomb(RAgg near, RAgg far) {
+    return RAgg{near.f | far.f, near.f ? near.v : (near.v | far.v)};
+}
+__device__ __forceinline__ RAgg wave_incl_rev(RAgg p, uint32_t lane) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        RAgg o;
+        o.f = __shfl_down(p.f, off, 64);
+        o.v = __shfl_down(p.v, off, 64);
+        if (lane + off < 64) p = rcomb(p, o);
+    }
+    return p;
+}
+
+// Which elements survive into the next round: an element of an undecided
+// txn that still waits (needy), and a potential blocker (committed or
+// undecided txn) followed in its queue by a needy element.  Each thread holds
+// IPT consecutive elements; nhm bit j = the element after j starts a queue.
+// `far` describes what follows the last thread's chunk.  Returns keep bits.
+template <int IPT, int WAVES>
+__device__ __forceinline__ uint32_t keep_bits(int cnt, uint32_t nhm, uint32_t needy, uint32_t blk,
+                                              RAgg *rw, RAgg far, uint32_t lane, uint32_t wave) {
+    const uint32_t valid = cnt >= 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
+    RAgg x{1u, 0u};
+    if (cnt > 0) {
+        const uint32_t cuts = nhm & valid;
+        x.f = cuts != 0;
+        const uint32_t upto = cuts ? ((2u << __builtin_ctz(cuts)) - 1u) : valid;
+        x.v = (needy & upto) != 0;
+    }
+    const RAgg inc_r = wave_incl_rev(x, lane);
+    if (lane == 0) rw[wave] = inc_r;
+    RAgg ex_r;
+    ex_r.f = __shfl_down(inc_r.f, 1, 64);
+    ex_r.v = __shfl_down(inc_r.v, 1, 64);
+    if (lane == 63) ex_r = RAgg{0u, 0u};
+    __syncthreads();
+    for (int w = WAVES - 1; w > (int)wave; w--) far = rcomb(rw[w], far);
+    uint32_t r = rcomb(ex_r, far).v;  // needy after my last element, same queue
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = IPT - 1; j >= 0; j--) {
+        if (j < cnt) {
+            const uint32_t after = ((nhm >> j) & 1u) ? 0u : r;
+            const uint32_t nd = (needy >> j) & 1u;
+            keep |= (((blk >> j) & 1u) & (nd | after)) << j;
+            r = after | nd;
+        }
+    }
+    return keep;
 }
 
 }  // namespace
 
 // ---- one tile of a decision round (single-pass OpPlain scan: v = status
 //      bits OR-ed along the row queue, c = kept accesses -> compaction offset)
+// Tile geometry follows the input width: 512 threads x 16 32-bit elements, or
+// 256 threads x 16 64-bit elements (round 0's pairs, or 64-bit elements);
+// 16 elements per thread, the LDS image padded one slot per 16.
+template <class EIn>
+struct Geo {
+    static constexpr int kThreads = sizeof(EIn) == 4 ? 512 : 256;
+    static constexpr int kMinWaves = sizeof(EIn) == 4 ? 4 : 3;  // per SIMD: <= 128 / 168 VGPRs
+    static constexpr int kWaves = kThreads / 64;
+    static constexpr int kIPT = 16;
+    static constexpr uint32_t kTile = kThreads * kIPT;
+};
+__device__ __forceinline__ uint32_t pad16(uint32_t j) { return j + (j >> 4); }
+
+template <class EIn>
 struct TileLds {
-    uint64_t el[kRTile + kRTile / kRIPT];  // input tile, then the compacted output
-    uint64_t next;
-    Agg wt[4];
+    EIn el[Geo<EIn>::kTile + Geo<EIn>::kTile / 16];  // input tile, then the compacted output
+    EIn next;
+    uint64_t prev;
+    Agg wt[Geo<EIn>::kWaves];
+    RAgg rw[Geo<EIn>::kWaves];
     Agg pre;
     uint32_t tot;
 };
 
-template <bool FIRST>
-__device__ __forceinline__ void round_tile(TileLds &sh, uint32_t tile, uint32_t n, uint32_t ntiles,
-                                           const uint64_t *__restrict__ el_in,
-                                           uint64_t *__restrict__ el_out, uint32_t *__restrict__ n_out,
-                                           const uint8_t *__restrict__ status,
-                                           uint8_t *__restrict__ vb8, int nowait, uint64_t *desc,
-                                           uint32_t tag, uint32_t *und_reset, Counters *ctr) {
+// coalesced 16-byte loads of [base, base + tile_n) into the padded LDS image
+template <class EIn>
+__device__ __forceinline__ void load_tile(const EIn *__restrict__ src, uint32_t base, uint32_t tile_n,
+                                          uint32_t n, EIn *s, EIn *s_next, EIn past_end) {
+    constexpr int V = 16 / sizeof(EIn);
+    constexpr int T = Geo<EIn>::kThreads;
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < Geo<EIn>::kIPT / V; q++) {
+        const uint32_t j = (q * T + tid) * V;
+        if (j + V <= tile_n) {
+            if constexpr (V == 2) {
+                const ulonglong2 x = *reinterpret_cast<const ulonglong2 *>(src + base + j);
+                s[pad16(j)] = x.x;
+                s[pad16(j + 1)] = x.y;
+            } else {
+                const uint4 x = *reinterpret_cast<const uint4 *>(src + base + j);
+                s[pad16(j)] = x.x;
+                s[pad16(j + 1)] = x.y;
+                s[pad16(j + 2)] = x.z;
+                s[pad16(j + 3)] = x.w;
+            }
+        } else {
+            for (int k = 0; k < V; k++)
+                if (j + k < tile_n) s[pad16(j + k)] = src[base + j + k];
+        }
+    }
+    if (tid == 0) *s_next = base + tile_n < n ? src[base + tile_n] : past_end;
+}
+
+// Round 0 reads the row-sorted pairs (row << 32 | txn << 8 | pos << 1 | wr)
+// directly: queue heads and repeats come from the row of the neighbouring
+// pair, and every txn is undecided (no status gather).  Later rounds read the
+// compacted elements of the previous round.
+template <bool FIRST, class EIn, class E>
+__device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint32_t n, uint32_t ntiles,
+                                           const EIn *__restrict__ el_in, E *__restrict__ el_out,
+                                           uint32_t *__restrict__ n_out, uint8_t *status,
+                                           uint8_t *__restrict__ vb8, uint32_t slog, int nowait,
+                                           uint64_t *desc, uint32_t tag, uint32_t *und_reset,
+                                           Counters *ctr);
+
+// the undecided count the following settle (single GPU: list length) or apply
+// (partitioned: slot sums) recounts
+__device__ __forceinline__ void reset_und(uint32_t *und_reset, Counters *ctr) {
+    if (und_reset) *und_reset = 0;
+    else for (int k = 0; k < kSlots; k++) ctr->slot[k].undecided = 0;
+}
+
+template <bool FIRST, class EIn, class E>
+__device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint32_t n, uint32_t ntiles,
+                                           const EIn *__restrict__ el_in, E *__restrict__ el_out,
+                                           uint32_t *__restrict__ n_out, uint8_t *status,
+                                           uint8_t *__restrict__ vb8, uint32_t slog, int nowait,
+                                           uint64_t *desc, uint32_t tag, uint32_t *und_reset,
+                                           Counters *ctr) {
+    using G = Geo<EIn>;
+    constexpr int IPT = G::kIPT;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t base = tile * kRTile;
-    const uint32_t tile_n = n - base < (uint32_t)kRTile ? n - base : (uint32_t)kRTile;
-    load_tile64(el_in, base, tile_n, n, sh.el, &sh.next);
+    const uint32_t base = tile * G::kTile;
+    const uint32_t tile_n = n - base < G::kTile ? n - base : G::kTile;
+    load_tile<EIn>(el_in, base, tile_n, n, sh.el, &sh.next, FIRST ? (EIn)~0ull : (EIn)F_HEAD);
+    if (FIRST && tid == 0) sh.prev = base > 0 ? (uint64_t)el_in[base - 1] : ~0ull;
     __syncthreads();
 
-    const uint32_t first = tid * kRIPT;
-    const int cnt = first >= tile_n ? 0 : (tile_n - first < (uint32_t)kRIPT ? (int)(tile_n - first) : kRIPT);
-    uint64_t e[kRIPT];
-    uint32_t v[kRIPT];
+    const uint32_t first = tid * IPT;
+    const int cnt = first >= tile_n ? 0 : (tile_n - first < (uint32_t)IPT ? (int)(tile_n - first) : IPT);
+    E e[IPT];
+    uint32_t v[IPT];
+    uint32_t nhm = 0;  // bit j: the element after e[j] starts a new queue
+    if constexpr (FIRST) {
+        uint64_t pp = first == 0 ? sh.prev : (uint64_t)sh.el[pad16(first - 1)];
+        const uint64_t pn = first + IPT < tile_n ? (uint64_t)sh.el[pad16(first + IPT)] : (uint64_t)sh.next;
+        bool dup = false;
+        uint64_t p[IPT];
 #pragma unroll
-    for (int j = 0; j < kRIPT; j++) e[j] = j < cnt ? sh.el[rpad(first + j)] : (uint64_t)EL_HEAD;
-    const uint64_t nxt = first + kRIPT < tile_n ? sh.el[rpad(first + kRIPT)] : sh.next;
-    uint64_t *s_out = sh.el;  // reused for the output once every lane holds its elements
-    Agg a{0u, 0u, 0u};
-    uint32_t umask = 0;
+        for (int j = 0; j < IPT; j++) p[j] = j < cnt ? (uint64_t)sh.el[pad16(first + j)] : ~0ull;
 #pragma unroll
-    for (int j = 0; j < kRIPT; j++) {
-        v[j] = 0;
-        if (j < cnt) {
-            const bool nh = j + 1 < cnt ? (e[j + 1] & EL_HEAD) != 0
-                                        : (cnt < kRIPT ? true : (nxt & EL_HEAD) != 0);
-#ifdef DVCC_EXP_NO_GATHER
-            const uint8_t s = (uint8_t)ST_UNDEC;
-#else
-            const uint8_t s = FIRST ? (uint8_t)ST_UNDEC : status[el_txn(e[j])];
-#endif
-            umask |= (s == ST_UNDEC ? 1u : 0u) << j;
-            v[j] = elem_value(e[j], nh, s, nowait);
-            a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & EL_HEAD) != 0), v[j],
-                                     (v[j] & B_KEEP) ? 1u : 0u});
+        for (int j = 0; j < IPT; j++) {
+            e[j] = (E)F_HEAD;
+            if (j < cnt) {
+                const bool head = pair_row(pp) != pair_row(p[j]);
+                dup |= !head && pair_txn(pp) == pair_txn(p[j]);
+                const uint64_t id = ((uint64_t)pair_txn(p[j]) << slog) | pair_pos(p[j]);
+                e[j] = (E)((id << 3) | (head ? F_HEAD : 0u) | (uint32_t)(p[j] & 1u));
+                const uint64_t q = j + 1 < cnt ? p[j + 1] : (cnt < IPT ? ~0ull : pn);
+                nhm |= (pair_row(q) != pair_row(p[j]) ? 1u : 0u) << j;
+                pp = p[j];
+            }
         }
+        if (dup) set_err(ctr, ERRB_DUP);  // a 2PL/OCC txn locks one row twice
+    } else {
+        // branch-free: first + j < kTile, so the padded index stays inside the image
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            const E x = (E)sh.el[pad16(first + j)];
+            e[j] = j < cnt ? x : (E)F_HEAD;
+        }
+        const E nxt = first + IPT < tile_n ? (E)sh.el[pad16(first + IPT)] : (E)sh.next;
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            const bool nh = j + 1 < cnt ? (e[j + 1] & F_HEAD) != 0
+                                        : (cnt < IPT ? true : (nxt & F_HEAD) != 0);
+            nhm |= (nh ? 1u : 0u) << j;
+        }
+    }
+    // branch-free over all IPT slots (a padding slot reads txn 0's status and
+    // is masked out), so the compiler keeps e[] and v[] in plain registers
+    uint32_t umask = 0, needy = 0, blk = 0;
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+        const bool valid = j < cnt;
+#ifdef DVCC_EXP_NO_GATHER
+        const uint8_t s = valid ? (uint8_t)ST_UNDEC : (uint8_t)ST_ABORT;
+#else
+        const uint8_t s0 = FIRST ? (uint8_t)ST_UNDEC : status[r_txn(e[j], slog)];
+        const uint8_t s = valid ? s0 : (uint8_t)ST_ABORT;
+#endif
+        umask |= (s == ST_UNDEC ? 1u : 0u) << j;
+        needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
+        const bool single = (e[j] & F_HEAD) && ((nhm >> j) & 1u);
+        blk |= (s != ST_ABORT && !single ? 1u : 0u) << j;
+        v[j] = elem_value(e[j], s, nowait);
+    }
+    // round 0: every element is needy; later: a queue running past the tile's
+    // end is assumed to be followed by a needy element
+    const uint32_t keep = FIRST ? blk
+                                : keep_bits<IPT, G::kWaves>(cnt, nhm, needy, blk, sh.rw, RAgg{1u, 1u},
+                                                            lane, wave);
+    Agg a{0u, 0u, 0u};
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+        v[j] |= ((keep >> j) & 1u) ? B_KEEP : 0u;
+        const Agg x{(uint32_t)((e[j] & F_HEAD) != 0), v[j], (keep >> j) & 1u};
+        if (j < cnt) a = OpPlain::comb(a, x);
     }
     const Agg inc = wave_incl<OpPlain>(a, lane);
     if (lane == 63) sh.wt[wave] = inc;
     __syncthreads();
     if (wave == 0) {
         Agg bagg = sh.wt[0];
-        for (int w = 1; w < 4; w++) bagg = OpPlain::comb(bagg, sh.wt[w]);
+        for (int w = 1; w < G::kWaves; w++) bagg = OpPlain::comb(bagg, sh.wt[w]);
 #ifdef DVCC_EXP_NO_LOOKBACK
-        const Agg pre{0u, 0u, tile * (uint32_t)kRTile};
+        const Agg pre{0u, 0u, tile * G::kTile};
 #else
         const Agg pre = look_back<OpPlain>(desc, tile, tag, bagg, lane, ctr);
 #endif
         if (lane == 0) {
             sh.pre = pre;
             sh.tot = bagg.c;
-            if (tile == 0) *und_reset = 0;  // re-counted by this round's settle
+            if (tile == 0) reset_und(und_reset, ctr);  // re-counted by this round's settle / apply
         }
     }
     __syncthreads();
@@ -139,50 +320,59 @@ __device__ __forceinline__ void round_tile(TileLds &sh, uint32_t tile, uint32_t 
     const Agg lex = wave_excl_from_incl<OpPlain>(inc, lane);
     uint32_t lpos = wpre.c + lex.c;                                   // block-local slot
     uint32_t run = OpPlain::comb(OpPlain::comb(sh.pre, wpre), lex).v;  // OR since queue head
+    E *s_out = reinterpret_cast<E *>(sh.el);  // every lane holds its elements: reuse the tile
+    // padding slots have umask and keep bits clear: no branch on cnt needed
 #pragma unroll
-    for (int j = 0; j < kRIPT; j++) {
-        if (j < cnt) {
-            uint64_t ej = e[j];
-            const uint32_t vj = v[j];
-            const bool head = (ej & EL_HEAD) != 0;
-            const uint32_t excl = head ? 0u : run;
-            if ((umask >> j) & 1u) ej = decide_elem(ej, excl, nowait, vb8);
-            if (vj & B_KEEP)
-                s_out[lpos++] = (ej & ~(uint64_t)EL_HEAD) | ((excl & B_KEEP) ? 0u : EL_HEAD);
-            run = head ? vj : (run | vj);
-        }
+    for (int j = 0; j < IPT; j++) {
+        E ej = e[j];
+        const uint32_t vj = v[j];
+        const bool head = (ej & F_HEAD) != 0;
+        const uint32_t excl = head ? 0u : run;
+#ifndef DVCC_EXP_NO_DECIDE
+        if ((umask >> j) & 1u) ej = decide_elem(ej, excl, nowait, vb8, slog, status);
+#endif
+        if (vj & B_KEEP) s_out[lpos++] = (E)((ej & ~(E)F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD));
+        run = head ? vj : (run | vj);
     }
     __syncthreads();
     // coalesced write-out of the compacted tile
     const uint32_t tot = sh.tot, gpos = sh.pre.c;
-    for (uint32_t k = tid; k < tot; k += kBlock) el_out[gpos + k] = s_out[k];
+    for (uint32_t k = tid; k < tot; k += G::kThreads) el_out[gpos + k] = s_out[k];
     if (tile == ntiles - 1 && tid == 0) *n_out = gpos + tot;
     __syncthreads();  // the LDS tile is free again
 }
 
 // one decision round, one launch; tiles are taken by ticket so that a tile
 // only ever waits on tiles already running
-template <bool FIRST>
-__global__ __launch_bounds__(kBlock) void k_round_pass(
-    const uint64_t *__restrict__ el_in, const uint32_t *__restrict__ n_in,
-    uint64_t *__restrict__ el_out, uint32_t *__restrict__ n_out, const uint8_t *__restrict__ status,
-    uint8_t *__restrict__ vb8, int nowait, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag,
-    uint32_t *und_reset, const uint32_t *und_in, uint32_t round, RoundPub *pub, Counters *ctr) {
-    __shared__ TileLds sh;
+template <bool FIRST, class EIn, class E>
+__global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_round_pass(
+    const EIn *__restrict__ el_in, const uint32_t *__restrict__ n_in, E *__restrict__ el_out,
+    uint32_t *__restrict__ n_out, uint8_t *status, uint8_t *__restrict__ vb8, uint32_t slog,
+    int nowait, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, uint32_t *und_reset,
+    const uint32_t *und_in, uint32_t round, RoundPub *pub, Counters *ctr) {
+    __shared__ TileLds<EIn> sh;
     __shared__ uint32_t s_tile;
     const uint32_t n_live = *n_in;
     const uint32_t und = und_in ? *und_in : 1u;
     const uint32_t n = und ? n_live : 0u;  // nothing left to decide: no-op
-    const uint32_t ntiles = (n + kRTile - 1) / kRTile;
+    const uint32_t ntiles = (n + Geo<EIn>::kTile - 1) / Geo<EIn>::kTile;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && round < (uint32_t)kRoundLog && (und || round == 0)) {
+        ctr->log_live[round] = n_live;
+        ctr->log_und[round] = und_in ? und : 0u;
+    }
     // one thread publishes the outcome of the previous round to the host
     const bool publisher = pub && threadIdx.x == 0 && blockIdx.x == (ntiles ? ntiles - 1 : 0);
     if (blockIdx.x >= ntiles) {  // spare blocks of a stale upper bound: no ticket
-        if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) { *n_out = 0; *und_reset = 0; }
+        if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) { *n_out = 0; reset_und(und_reset, ctr); }
     } else {
+#ifdef DVCC_EXP_TICKET_BLOCKIDX
+        if (threadIdx.x == 0) s_tile = blockIdx.x;
+#else
         if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
+#endif
         __syncthreads();
-        round_tile<FIRST>(sh, s_tile, n, ntiles, el_in, el_out, n_out, status, vb8, nowait, desc, tag,
-                          und_reset, ctr);
+        round_tile<FIRST, EIn, E>(sh, s_tile, n, ntiles, el_in, el_out, n_out, status, vb8, slog,
+                                  nowait, desc, tag, und_reset, ctr);
     }
     if (publisher) {
         __hip_atomic_store(&pub->le, ((unsigned long long)n_live << 32) | ctr->err, __ATOMIC_RELAXED,
@@ -193,16 +383,19 @@ __global__ __launch_bounds__(kBlock) void k_round_pass(
 }
 
 // ---- per-txn settle (single GPU): new status from its accesses' verdicts
-__device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ vb8, uint32_t a0, uint32_t a1) {
+// The verdict bytes of txn t are vb8[t << slog, (t << slog) + len): one
+// 16-byte load per 16 accesses (slog >= 4).
+__device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, uint32_t len) {
     uint32_t any_abort = 0, all_ok = 1;
-    for (uint32_t w = a0 & ~3u; w < a1; w += 4) {  // aligned dwords over [a0, a1)
-        const uint32_t x = *reinterpret_cast<const uint32_t *>(vb8 + w);
+    for (uint32_t w = 0; w < len; w += 16) {
+        const uint4 x4 = *reinterpret_cast<const uint4 *>(v + w);
+        const uint32_t x[4] = {x4.x, x4.y, x4.z, x4.w};
 #pragma unroll
-        for (uint32_t b = 0; b < 4; b++) {
-            if (w + b < a0 || w + b >= a1) continue;
-            const uint32_t vb = (x >> (8 * b)) & 0xFFu;
-            any_abort |= vb == VB_ABORT;
-            all_ok &= vb == VB_OK;
+        for (uint32_t q = 0; q < 4; q++) {
+            const int nb = (int)len - (int)(w + 4 * q);
+            const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
+            any_abort |= x[q] & 0x02020202u & m;
+            all_ok &= (x[q] & m) == (0x01010101u & m);
         }
     }
     return any_abort ? V_ABORT : (all_ok ? 0 : V_WAIT);
@@ -216,7 +409,7 @@ __device__ __forceinline__ void block_count(uint32_t und, Counters *ctr) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&ctr->undecided, t);
+        if (t) atomicAdd(&my_slot(ctr).undecided, t);
     }
 }
 
@@ -226,9 +419,10 @@ __device__ __forceinline__ void block_count(uint32_t und, Counters *ctr) {
 constexpr uint32_t kSettleIPT = 4, kSettleChunk = kBlock * kSettleIPT;
 
 __device__ __forceinline__ bool settle_txn(uint8_t *__restrict__ status, const uint8_t *__restrict__ vb8,
-                                           const uint32_t *__restrict__ tb_start,
-                                           const uint32_t *__restrict__ tb_end, uint32_t t) {
-    const uint8_t v = txn_verdict(vb8, tb_start[t], tb_end[t]);
+                                           uint32_t slog, const uint8_t *__restrict__ tlen,
+                                           uint32_t t) {
+    if (status[t] != ST_UNDEC) return false;  // aborted by the pass
+    const uint8_t v = txn_verdict(vb8 + ((size_t)t << slog), tlen[t]);
     if (v & V_ABORT) status[t] = ST_ABORT;
     else if (!(v & V_WAIT)) status[t] = ST_COMMIT;
     return (v & (V_ABORT | V_WAIT)) == V_WAIT;
@@ -243,9 +437,8 @@ struct SettleLds {
 template <bool FIRST>
 __device__ __forceinline__ void settle_chunk(SettleLds &sh, uint32_t lo, uint32_t n,
                                              uint8_t *__restrict__ status,
-                                             const uint8_t *__restrict__ vb8,
-                                             const uint32_t *__restrict__ tb_start,
-                                             const uint32_t *__restrict__ tb_end,
+                                             const uint8_t *__restrict__ vb8, uint32_t slog,
+                                             const uint8_t *__restrict__ tlen,
                                              const uint32_t *__restrict__ list_in,
                                              uint32_t *__restrict__ list_out,
                                              uint32_t *__restrict__ n_out) {
@@ -259,7 +452,7 @@ __device__ __forceinline__ void settle_chunk(SettleLds &sh, uint32_t lo, uint32_
         bool keep = false;
         if (i < n) {
             t = FIRST ? i : list_in[i];
-            keep = settle_txn(status, vb8, tb_start, tb_end, t);
+            keep = settle_txn(status, vb8, slog, tlen, t);
         }
         const uint64_t m = __ballot(keep);
         uint32_t wb = 0;
@@ -277,26 +470,28 @@ __device__ __forceinline__ void settle_chunk(SettleLds &sh, uint32_t lo, uint32_
 
 template <bool FIRST>
 __global__ __launch_bounds__(kBlock) void k_round_settle(
-    uint8_t *__restrict__ status, const uint8_t *__restrict__ vb8,
-    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
-    const uint32_t *__restrict__ list_in, const uint32_t *__restrict__ n_in, uint32_t n_txn,
-    uint32_t *__restrict__ list_out, uint32_t *__restrict__ n_out) {
+    uint8_t *__restrict__ status, const uint8_t *__restrict__ vb8, uint32_t slog,
+    const uint8_t *__restrict__ tlen, const uint32_t *__restrict__ list_in,
+    const uint32_t *__restrict__ n_in, uint32_t n_txn, uint32_t *__restrict__ list_out,
+    uint32_t *__restrict__ n_out) {
     __shared__ SettleLds sh;
     const uint32_t n = FIRST ? n_txn : *n_in;
     const uint32_t lo = blockIdx.x * kSettleChunk;
     if (lo >= n) return;
-    settle_chunk<FIRST>(sh, lo, n, status, vb8, tb_start, tb_end, list_in, list_out, n_out);
+    settle_chunk<FIRST>(sh, lo, n, status, vb8, slog, tlen, list_in, list_out, n_out);
 }
 
 // ---- partitioned: this partition's verdict byte per txn (bit1 abort, bit0
 //      wait), combined across partitions by an element-wise MAX
 __global__ __launch_bounds__(kBlock) void k_round_verdict(const uint8_t *__restrict__ status,
                                                           const uint8_t *__restrict__ vb8,
-                                                          const uint32_t *__restrict__ tb_start,
-                                                          const uint32_t *__restrict__ tb_end,
+                                                          uint32_t slog,
+                                                          const uint8_t *__restrict__ tlen,
                                                           uint32_t n_txn, uint8_t *__restrict__ verdict) {
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x)
-        verdict[t] = status[t] == ST_UNDEC ? txn_verdict(vb8, tb_start[t], tb_end[t]) : 0;
+        verdict[t] = status[t] == ST_UNDEC   ? txn_verdict(vb8 + ((size_t)t << slog), tlen[t])
+                     : status[t] == ST_ABORT ? (uint8_t)V_ABORT  // possibly aborted by this pass
+                                             : (uint8_t)0;
 }
 
 // ---- partitioned: apply the combined verdicts
@@ -314,6 +509,162 @@ __global__ __launch_bounds__(kBlock) void k_round_apply(uint8_t *__restrict__ st
     block_count(und, ctr);
 }
 
+
+// ---- the tail: every remaining round in ONE single-workgroup launch --------
+// Once the live set fits in LDS, a pass + settle pair costs two launches and
+// ~20 us of latency for a few thousand elements.  k_round_tail runs the same
+// round -- status gather, reverse (dead-element) and forward segmented scans,
+// decisions, compaction, settle -- on one CU with __syncthreads as the only
+// barrier, until no txn is undecided.  The lowest undecided txn decides in
+// every round, so the loop ends; a round without progress is an error.
+template <class E>
+struct TailGeo {
+    static constexpr int kIPT = sizeof(E) == 4 ? 16 : 12;
+    static constexpr uint32_t kCap = (uint32_t)kTailThreads * kIPT;  // 16384 / 12288
+};
+constexpr int kTailWaves = kTailThreads / 64;
+
+template <class E>
+struct TailLds {
+    E el[TailGeo<E>::kCap];
+    uint32_t ul[TailGeo<E>::kCap];
+    Agg wt[kTailWaves];
+    RAgg rw[kTailWaves];
+    uint32_t ucnt;
+};
+
+template <class E>
+__global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32_t r0, int nowait,
+                                                             RoundPub *pub) {
+    constexpr int IPT = TailGeo<E>::kIPT;
+    __shared__ TailLds<E> sh;
+    Counters *ctr = b.ctr;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t slog = b.slog;
+    uint32_t n = ctr->nlive[r0 & 1];
+    uint32_t U = ctr->nund[r0 & 1];
+    uint32_t round = r0;
+    bool ok = r0 > 0 && n <= TailGeo<E>::kCap && U <= TailGeo<E>::kCap;
+    if (!ok) {  // decline: the host resumes the multi-workgroup rounds at r0
+        if (tid == 0 && pub)
+            __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+    }
+    {
+        const E *src = reinterpret_cast<const E *>(b.rel[(r0 - 1) & 1]);
+        const uint32_t *lsrc = b.ulist[r0 & 1];
+        for (uint32_t i = tid; i < n; i += kTailThreads) sh.el[i] = src[i];
+        for (uint32_t i = tid; i < U; i += kTailThreads) sh.ul[i] = lsrc[i];
+    }
+    __syncthreads();
+    while (ok && U > 0) {
+        if (tid == 0 && round < (uint32_t)kRoundLog) {
+            ctr->log_live[round] = n;
+            ctr->log_und[round] = U;
+        }
+        // ---- pass: my chunk of k consecutive elements
+        const uint32_t k = (n + kTailThreads - 1) / kTailThreads;
+        const uint32_t first = tid * k;
+        const int cnt = first >= n ? 0 : (int)(n - first < k ? n - first : k);
+        E e[IPT];
+        uint32_t v[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; j++) e[j] = j < cnt ? sh.el[first + j] : (E)F_HEAD;
+        const E nxt = first + (uint32_t)cnt < n ? sh.el[first + cnt] : (E)F_HEAD;
+        uint32_t nhm = 0, umask = 0, needy = 0, blk = 0;
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            v[j] = 0;
+            if (j < cnt) {
+                const bool nh = j + 1 < cnt ? (e[j + 1] & F_HEAD) != 0 : (nxt & F_HEAD) != 0;
+                nhm |= (nh ? 1u : 0u) << j;
+                const uint8_t s = b.status[r_txn(e[j], slog)];
+                umask |= (s == ST_UNDEC ? 1u : 0u) << j;
+                needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
+                const bool single = (e[j] & F_HEAD) && nh;
+                blk |= (s != ST_ABORT && !single ? 1u : 0u) << j;
+                v[j] = elem_value(e[j], s, nowait);
+            }
+        }
+        // the whole live set is here: nothing follows the end
+        const uint32_t keep = keep_bits<IPT, kTailWaves>(cnt, nhm, needy, blk, sh.rw, RAgg{1u, 0u},
+                                                         lane, wave);
+        Agg a{0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            if (j < cnt) {
+                if ((keep >> j) & 1u) v[j] |= B_KEEP;
+                a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & F_HEAD) != 0), v[j], (keep >> j) & 1u});
+            }
+        }
+        const Agg inc = wave_incl<OpPlain>(a, lane);
+        if (lane == 63) sh.wt[wave] = inc;
+        __syncthreads();
+        Agg wpre{0u, 0u, 0u}, total{0u, 0u, 0u};
+        for (int w = 0; w < kTailWaves; w++) {
+            if (w < (int)wave) wpre = OpPlain::comb(wpre, sh.wt[w]);
+            total = OpPlain::comb(total, sh.wt[w]);
+        }
+        const Agg lex = wave_excl_from_incl<OpPlain>(inc, lane);
+        const Agg pre = OpPlain::comb(wpre, lex);
+        uint32_t lpos = pre.c, run = pre.v;
+        // every thread read its elements before the first barrier: write in place
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            if (j < cnt) {
+                E ej = e[j];
+                const bool head = (ej & F_HEAD) != 0;
+                const uint32_t excl = head ? 0u : run;
+                if ((umask >> j) & 1u) ej = decide_elem(ej, excl, nowait, b.vb8, slog, b.status);
+                if (v[j] & B_KEEP)
+                    sh.el[lpos++] = (E)((ej & ~(E)F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD));
+                run = head ? v[j] : (run | v[j]);
+            }
+        }
+        if (tid == 0) sh.ucnt = 0;
+        __syncthreads();  // verdict and status stores are visible to the workgroup
+        // ---- settle: the undecided list, compacted in place
+        uint32_t tl[IPT];
+        uint32_t km = 0;
+#pragma unroll
+        for (int q = 0; q < IPT; q++) {
+            const uint32_t i = q * kTailThreads + tid;
+            tl[q] = 0;
+            if (i < U) {
+                tl[q] = sh.ul[i];
+                km |= (settle_txn(b.status, b.vb8, slog, b.tlen, tl[q]) ? 1u : 0u) << q;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < IPT; q++) {
+            const bool kp = (km >> q) & 1u;
+            const uint64_t m = __ballot(kp);
+            uint32_t wb = 0;
+            if (lane == 0 && m) wb = atomicAdd(&sh.ucnt, (uint32_t)__builtin_popcountll(m));
+            wb = __shfl(wb, 0, 64);
+            if (kp) sh.ul[wb + mask_rank(m)] = tl[q];
+        }
+        __syncthreads();
+        const uint32_t U2 = sh.ucnt;
+        round++;
+        if (U2 >= U) {  // the lowest undecided txn must have decided
+            if (tid == 0) set_err(ctr, ERRB_SPIN);
+            ok = false;
+        }
+        U = U2;
+        n = total.c;
+        __syncthreads();  // sh.ucnt is reset by the next round
+    }
+    if (tid == 0 && pub) {
+        __hip_atomic_store(&pub->le, ((unsigned long long)n << 32) | ctr->err, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&pub->ru, ((unsigned long long)round << 32) | (ok ? U : 0xFFFFFFFFu),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 __global__ void k_round0_init(uint32_t n, Counters *ctr) { ctr->nlive[0] = n; }
 
 // ------------------------------------------------------------- launchers
@@ -322,27 +673,52 @@ static uint32_t txn_grid(uint32_t n_txn) {
     return g < 1 ? 1 : (g > 1024 ? 1024 : g);
 }
 
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc) {
-    (void)hipMemsetAsync(b.vb8, 0, n_acc ? n_acc : 1, s);
+bool round_el32(uint32_t n_txn, uint32_t slog) {
+    uint32_t tb = 0;
+    while (tb < 32 && (1ull << tb) < (uint64_t)n_txn) tb++;
+    return tb + slog + 3 <= 32;
+}
+
+uint32_t tail_cap(bool el32) { return el32 ? TailGeo<uint32_t>::kCap : TailGeo<uint64_t>::kCap; }
+
+void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn_pad) {
+    (void)hipMemsetAsync(b.vb8, 0, n_txn_pad ? ((size_t)n_txn_pad << b.slog) : 16, s);
     k_round0_init<<<1, 1, 0, s>>>(n_acc, b.ctr);
+}
+
+template <class E>
+static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
+                         uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub) {
+    E *out = reinterpret_cast<E *>(b.rel[round & 1]);
+    const uint32_t *n_in = &b.ctr->nlive[round & 1];
+    uint32_t *n_out = &b.ctr->nlive[(round + 1) & 1];
+    uint32_t *tc = &b.tile_ctr[ticket % kTileCtrs];
+    uint32_t *und = settle ? &b.ctr->nund[(round + 1) & 1] : nullptr;
+    const uint32_t *und_in = settle && round > 0 ? &b.ctr->nund[round & 1] : nullptr;
+    if (round == 0) {
+        using G = Geo<uint64_t>;
+        const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
+        k_round_pass<true, uint64_t, E><<<nb, G::kThreads, 0, s>>>(
+            b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait, b.desc, tc, tag, und, nullptr,
+            round, nullptr, b.ctr);
+    } else {
+        using G = Geo<E>;
+        const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
+        k_round_pass<false, E, E><<<nb, G::kThreads, 0, s>>>(
+            reinterpret_cast<const E *>(b.rel[(round - 1) & 1]), n_in, out, n_out, b.status, b.vb8,
+            b.slog, nowait, b.desc, tc, tag, und, und_in, round, pub, b.ctr);
+    }
 }
 
 void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
                 uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub) {
-    const uint32_t nb = ub_in ? (uint32_t)((ub_in + kRTile - 1) / kRTile) : 1;
-    const uint64_t *in = round == 0 ? b.el0 : b.rel[(round - 1) & 1];
-    uint64_t *out = b.rel[round & 1];
-    const uint32_t *n_in = &b.ctr->nlive[round & 1];
-    uint32_t *n_out = &b.ctr->nlive[(round + 1) & 1];
-    uint32_t *tc = &b.tile_ctr[ticket % kTileCtrs];
-    uint32_t *und = settle ? &b.ctr->nund[(round + 1) & 1] : &b.ctr->undecided;
-    const uint32_t *und_in = settle && round > 0 ? &b.ctr->nund[round & 1] : nullptr;
-    if (round == 0)
-        k_round_pass<true><<<nb, kBlock, 0, s>>>(in, n_in, out, n_out, b.status, b.vb8, nowait, b.desc,
-                                                  tc, tag, und, nullptr, round, nullptr, b.ctr);
-    else
-        k_round_pass<false><<<nb, kBlock, 0, s>>>(in, n_in, out, n_out, b.status, b.vb8, nowait,
-                                                   b.desc, tc, tag, und, und_in, round, pub, b.ctr);
+    if (b.el32) round_pass_t<uint32_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub);
+    else round_pass_t<uint64_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub);
+}
+
+void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, RoundPub *pub) {
+    if (b.el32) k_round_tail<uint32_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
+    else k_round_tail<uint64_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
 }
 
 void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub) {
@@ -350,17 +726,17 @@ void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_
     const uint32_t nb = n ? (n + kSettleChunk - 1) / kSettleChunk : 1;
     uint32_t *n_out = &b.ctr->nund[(round + 1) & 1];
     if (round == 0)
-        k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.tb_start, b.tb_end, nullptr,
-                                                   nullptr, n_txn, b.ulist[1], n_out);
+        k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, nullptr, nullptr,
+                                                   n_txn, b.ulist[1], n_out);
     else
-        k_round_settle<false><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.tb_start, b.tb_end,
-                                                    b.ulist[round & 1], &b.ctr->nund[round & 1], n_txn,
-                                                    b.ulist[(round + 1) & 1], n_out);
+        k_round_settle<false><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
+                                                    b.ulist[round & 1], &b.ctr->nund[round & 1],
+                                                    n_txn, b.ulist[(round + 1) & 1], n_out);
 }
 
 void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict) {
     if (!n_txn) return;
-    k_round_verdict<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, b.vb8, b.tb_start, b.tb_end, n_txn,
+    k_round_verdict<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, n_txn,
                                                       verdict);
 }
 

@@ -48,7 +48,12 @@ struct dv_ctx {
     uint8_t *ew = nullptr;
     uint32_t *counts = nullptr, *digit_tot = nullptr;
     uint64_t *rel[2] = {nullptr, nullptr};           // live accesses, ping-pong
-    uint8_t *vb8 = nullptr;                          // per access: verdict
+    uint8_t *vb8 = nullptr;                          // per access: verdict, txn-strided
+    uint64_t vb8_cap = 0;                            // bytes
+    uint32_t slog = 4;                               // log2 of vb8's per-txn stride
+    bool el32 = false;                               // 32-bit round elements this epoch
+    uint8_t *tlen = nullptr;                         // per txn: accesses here
+    uint32_t *acc_row = nullptr;                     // per access: row | wr << 31
     uint32_t *ulist[2] = {nullptr, nullptr};         // undecided txns, ping-pong
     uint32_t *tb_start = nullptr, *tb_end = nullptr; // per txn: its access range
     uint64_t *desc = nullptr;                        // look-back tile descriptors
@@ -122,15 +127,16 @@ int bits_for(uint64_t n) {  // bits needed to represent values in [0, n)
 
 RoundBufs round_bufs(dv_ctx *c) {
     RoundBufs b;
-    b.el0 = c->el;
+    b.pairs0 = c->pairs[c->sorted];
     b.rel[0] = c->rel[0];
     b.rel[1] = c->rel[1];
+    b.el32 = c->el32;
     b.vb8 = c->vb8;
+    b.slog = c->slog;
     b.status = c->status;
+    b.tlen = c->tlen;
     b.ulist[0] = c->ulist[0];
     b.ulist[1] = c->ulist[1];
-    b.tb_start = c->tb_start;
-    b.tb_end = c->tb_end;
     b.desc = c->desc;
     b.tile_ctr = c->tile_ctr;
     b.ctr = c->ctr;
@@ -232,10 +238,11 @@ void dv_close(dv_ctx *c) {
         dfree(t.ix);
         dfree(t.bstart);
     }
-    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el,
-                    c->ew, c->counts, c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr, c->status,
-                    c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types, c->d_tables,
-                    c->d_commit, c->d_txn, c->d_grant};
+    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
+                    c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tlen, c->acc_row,
+                    c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
+                    c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
+                    c->d_tables, c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
@@ -269,7 +276,6 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     const uint32_t nb = nblocks_for(A);
     if (!r) r = dalloc(&c->pairs[0], A);
     if (!r) r = dalloc(&c->pairs[1], A);
-    if (!r) r = dalloc(&c->el, A);
     if (!r) r = dalloc(&c->counts, (uint64_t)kRadix * nb);
     if (!r) r = dalloc(&c->digit_tot, kRadix);
     if (!r) r = dalloc(&c->status, c->n_txn_cap_pad);
@@ -284,10 +290,15 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = dalloc(&c->rel[0], A);
         if (!r) r = dalloc(&c->rel[1], A);
-        if (!r) r = dalloc(&c->vb8, A + 16);  // dword reads may run 3 B past the end
+        if (!r) r = dalloc(&c->tlen, c->n_txn_cap_pad);
+        if (!r) r = dalloc(&c->acc_row, A);
         if (!r) r = dalloc(&c->ulist[0], T);
         if (!r) r = dalloc(&c->ulist[1], T);
+        // verdict bytes: 16 per txn; grown on demand for longer txns (dv_epoch_begin)
+        c->vb8_cap = (uint64_t)c->n_txn_cap_pad << 4;
+        if (!r) r = dalloc(&c->vb8, c->vb8_cap);
     }
+    if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->el, A);
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->ew, A);
     if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)),
                          "hipHostMalloc");
@@ -332,7 +343,7 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
         return DV_ERR_ARG;
     HostTable &t = c->tab[table];
     if (t.created) return DV_ERR_STATE;
-    if (c->total_rows + capacity_rows > 0xFFFFFFFFull) return DV_ERR_ARG;
+    if (c->total_rows + capacity_rows > kMaxRows) return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     // grow the global hot column / primary-key arrays (load-time only)
     const uint64_t new_total = c->total_rows + capacity_rows;
@@ -492,7 +503,26 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     if (!any) return DV_ERR_NO_TABLE;
     HIPCHK(hipSetDevice(c->cfg.device));
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
-    if (ep->n_txn > kMaxTxn) return DV_ERR_ARG;
+    if (ep->n_txn > kMaxTxn || ep->max_txn_acc > kMaxPos) return DV_ERR_ARG;
+    // verdict-byte stride: 1 << slog >= the longest txn (16 at least)
+    uint32_t slog = 7;
+    if (!calvin) {
+        const uint32_t hint = ep->max_txn_acc ? ep->max_txn_acc : kMaxPos;
+        slog = 4;
+        while ((1u << slog) < hint) slog++;
+        const uint64_t need = (uint64_t)((ep->n_txn + 3u) & ~3u) << slog;
+        if (need > c->vb8_cap) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            dfree(c->vb8);
+            c->vb8 = nullptr;
+            c->vb8_cap = 0;
+            int r = dalloc(&c->vb8, need);
+            if (r) return r;
+            c->vb8_cap = need;
+        }
+        c->slog = slog;
+        c->el32 = round_el32(ep->n_txn, slog) && !(c->cfg.flags & DV_FLAG_EL64);
+    }
     c->n_acc = ep->n_acc;
     c->n_txn = ep->n_txn;
     c->n_txn_pad = (ep->n_txn + 3u) & ~3u;
@@ -507,24 +537,26 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         const size_t tb_bytes = (size_t)(c->n_txn_pad ? c->n_txn_pad : 4) * 4;
         HIPCHK(hipMemsetAsync(c->tb_start, 0, tb_bytes, c->stream));
         HIPCHK(hipMemsetAsync(c->tb_end, 0, tb_bytes, c->stream));
+        if (!calvin) HIPCHK(hipMemsetAsync(c->tlen, 0, tb_bytes / 4, c->stream));
     }
     HIPCHK(hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream));
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
-                 ep->n_txn, calvin, c->pairs[0], c->tb_start, c->tb_end, c->ctr);
+                 ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
+                 calvin ? nullptr : c->acc_row, c->ctr);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
                                 timing(c) ? c->sev : nullptr);
-    launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, calvin ? 1 : 0, c->tb_start, c->el,
-                       c->ctr);
+    if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
+        launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
     if (calvin) {
         const uint32_t tag = next_tag(c);
         calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
-        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc);
+        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, c->n_txn_pad);
         c->live_ub = (uint32_t)ep->n_acc;
         c->und_ub = ep->n_txn;
     }
@@ -558,7 +590,9 @@ int round_sync(dv_ctx *c, uint32_t *undecided, bool settle) {
     r = err_from_bits(c->h_ctr->err);
     if (r) { c->phase = 0; return r; }
     c->live_ub = c->h_ctr->nlive[c->rounds & 1];  // input size of the next round
-    const uint32_t und = settle ? c->h_ctr->nund[c->rounds & 1] : c->h_ctr->undecided;
+    uint32_t und = 0;
+    if (settle) und = c->h_ctr->nund[c->rounds & 1];
+    else for (const CtrSlot &sl : c->h_ctr->slot) und += sl.undecided;
     c->und_ub = und;
     if (undecided) *undecided = und;
     return DV_OK;
@@ -589,8 +623,12 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     if (!c || c->phase != 1) return DV_ERR_STATE;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     rec(c, 4);
-    launch_exec(c->stream, c->pairs[c->sorted], c->el, calvin ? c->ew : nullptr, c->n_acc, c->status,
-                c->f0, c->pkey, c->ctr);
+    if (calvin)
+        launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey,
+                    c->ctr);
+    else
+        launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0,
+                        c->pkey, c->cfg.cc_alg != DV_OCC, c->ctr);
     launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
     rec(c, 5);
     HIPCHK(hipGetLastError());
@@ -603,10 +641,16 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         std::memset(st, 0, sizeof(*st));
         st->n_txn = c->n_txn;
         st->n_acc = c->n_acc;
-        st->committed = c->h_ctr->committed;
-        st->aborted = c->n_txn - c->h_ctr->committed;
-        st->write_cnt = c->h_ctr->write_cnt;
-        st->read_digest = c->h_ctr->read_digest;
+        uint64_t committed = 0, wcnt = 0, dig = 0;
+        for (const CtrSlot &sl : c->h_ctr->slot) {
+            committed += sl.committed;
+            wcnt += sl.write_cnt;
+            dig += sl.read_digest;
+        }
+        st->committed = committed;
+        st->aborted = c->n_txn - committed;
+        st->write_cnt = wcnt;
+        st->read_digest = dig;
         st->rounds = calvin ? 0 : (c->rounds_real ? c->rounds_real : c->rounds);
         st->sort_passes = c->sort_passes;
         if (timing(c)) {
@@ -644,14 +688,23 @@ inline uint32_t pub_round(const dv_ctx *c, uint32_t *und) {
     return (uint32_t)(ru >> 32);
 }
 
-int wait_published(dv_ctx *c, uint32_t target) {
+// returns DV_OK, kTailDeclined when the tail launched at round tail_r0
+// declined, or an error
+constexpr int kTailDeclined = 1;
+int wait_published(dv_ctx *c, uint32_t target, uint32_t tail_r0) {
     const auto t0 = std::chrono::steady_clock::now();
+    const unsigned long long declined = ((unsigned long long)tail_r0 << 32) | 1u;
     for (uint64_t i = 0;; i++) {
         if (pub_round(c, nullptr) >= target) return DV_OK;
+        if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined) return kTailDeclined;
         if ((i & 255) == 255) {
             const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess)  // drained: the record must be there now
-                return pub_round(c, nullptr) >= target ? DV_OK : DV_ERR_STATE;
+            if (q == hipSuccess) {  // drained: the record must be there now
+                if (pub_round(c, nullptr) >= target) return DV_OK;
+                if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined)
+                    return kTailDeclined;
+                return DV_ERR_STATE;
+            }
             if (q != hipErrorNotReady) return hip_fail(q, "round stream");
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
         }
@@ -661,13 +714,29 @@ int wait_published(dv_ctx *c, uint32_t target) {
 
 // Rounds are published by the NEXT round's pass, so kRoundsAhead >= 2 keeps
 // the round the host waits for always enqueued.
+// Once the published live count and undecided count fit the tail kernel's
+// LDS, the remaining rounds run in one single-workgroup launch (round_tail).
+// The rounds queued ahead lag the published count by about two rounds, so the
+// tail is first tried at kTailTry (the live set shrinks ~2x per round pair
+// once it is that small); if it declines, the next try waits for a published
+// count that fits outright.
+constexpr uint32_t kTailTryFactor = 4;
 int run_rounds(dv_ctx *c) {
     __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
+    __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
     uint32_t prev = c->n_txn + 1, seen = 0;
+    uint32_t tail_r0 = 0;             // round the pending tail launch starts at (0: none)
+    const uint32_t cap = tail_cap(c->el32);
+    uint32_t tail_limit = kTailTryFactor * cap;  // published live count that triggers a try
     for (;;) {
-        while (c->rounds < seen + kRoundsAhead + 1) enqueue_round(c, nullptr, true);
+        while (!tail_r0 && c->rounds < seen + kRoundsAhead + 1) enqueue_round(c, nullptr, true);
         int r = hip_fail(hipGetLastError(), "round launch");
-        if (!r) r = wait_published(c, seen + 1);
+        if (!r) r = wait_published(c, seen + 1, tail_r0);
+        if (r == kTailDeclined) {
+            tail_r0 = 0;
+            tail_limit = cap;
+            continue;
+        }
         if (r) {
             (void)hipStreamSynchronize(c->stream);
             return r;
@@ -683,11 +752,16 @@ int run_rounds(dv_ctx *c) {
         }
         if (und == 0) {
             c->rounds_real = seen;
+            c->rounds = std::max(c->rounds, seen);
             return DV_OK;
         }
         prev = und;
         c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));  // bounds for rounds not yet enqueued
         c->und_ub = und;
+        if (!tail_r0 && !(c->cfg.flags & DV_FLAG_NO_TAIL) && c->live_ub <= tail_limit) {
+            tail_r0 = c->rounds;
+            round_tail(c->stream, round_bufs(c), tail_r0, c->cfg.cc_alg != DV_OCC, c->d_pub);
+        }
     }
 }
 
@@ -704,17 +778,33 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     return dv_epoch_finish(c, d_commit, st);
 }
 
+int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {
+    if (!c || !c->h_ctr) return 0;
+    uint32_t n = c->rounds < (uint32_t)kRoundLog ? c->rounds : (uint32_t)kRoundLog;
+    if (n > cap) n = cap;
+    for (uint32_t r = 0; r < n; r++) {
+        if (live) live[r] = c->h_ctr->log_live[r];
+        if (undecided) undecided[r] = c->h_ctr->log_und[r];
+    }
+    return (int)n;
+}
+
 int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                  uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
                  dv_stats *st) {
     (void)ts;  // decisions follow sequence order; TS_CAS timestamps are monotone in it
     if (!c || (n_acc && !acc) || !out_commit) return DV_ERR_ARG;
     if (n_acc > c->cfg.max_acc || n_txn > c->cfg.max_txn) return DV_ERR_ARG;
+    uint32_t max_len = 0;
     if (txn_begin) {  // CSR form must agree with acc[].txn_seq
         if (txn_begin[0] != 0 || txn_begin[n_txn] != n_acc) return DV_ERR_ARG;
-        for (uint32_t t = 0; t < n_txn; t++)
+        for (uint32_t t = 0; t < n_txn; t++) {
+            if (txn_begin[t + 1] < txn_begin[t]) return DV_ERR_ARG;
+            max_len = std::max(max_len, txn_begin[t + 1] - txn_begin[t]);
             for (uint64_t a = txn_begin[t]; a < txn_begin[t + 1]; a++)
                 if (acc[a].txn_seq != t) return DV_ERR_TXN_RANGE;
+        }
+        if (max_len > kMaxPos) return DV_ERR_ARG;
     }
     HIPCHK(hipSetDevice(c->cfg.device));
     int r = DV_OK;
@@ -741,6 +831,7 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
     ep.tables = c->d_tables;
     ep.n_acc = n_acc;
     ep.n_txn = n_txn;
+    ep.max_txn_acc = max_len;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
     if (r) return r;

@@ -28,6 +28,8 @@ YCSB, TPCC = 1, 2
 RD, WR, SCAN = 0, 1, 3
 HASH_YCSB, HASH_MOD = 0, 1
 FLAG_TIMING = 1
+FLAG_NO_TAIL = 2
+FLAG_EL64 = 4
 
 
 class DvccError(RuntimeError):
@@ -52,7 +54,7 @@ class Access(ctypes.Structure):
 class EpochDev(ctypes.Structure):
     _fields_ = [("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("acc_txn", ctypes.c_void_p),
                 ("tables", ctypes.c_void_p), ("n_acc", ctypes.c_uint64), ("n_txn", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("max_txn_acc", ctypes.c_uint32)]
 
 
 class Stats(ctypes.Structure):
@@ -101,6 +103,7 @@ SIGNATURES = [
     ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),
     ("dv_epoch_finish", ctypes.c_int, [_vp, _vp, _P(Stats)]),
+    ("dv_round_log", ctypes.c_int, [_vp, _P(ctypes.c_uint32), _P(ctypes.c_uint32), ctypes.c_uint32]),
     ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_uint32, _vp, _vp, _vp]),
 ]

@@ -41,6 +41,9 @@ class Epoch:
     def n_acc(self):
         return int(self.txn_begin[-1])
 
+    def max_txn_acc(self):
+        return int(np.diff(self.txn_begin.astype(np.int64)).max()) if self.n_txn else 0
+
     def acc_txn(self):
         counts = np.diff(self.txn_begin.astype(np.int64))
         return np.repeat(np.arange(self.n_txn, dtype=np.uint32), counts)
@@ -63,6 +66,7 @@ class DeviceEpoch:
         import torch
         self.n_txn = epoch.n_txn
         self.n_acc = epoch.n_acc
+        self.max_txn_acc = epoch.max_txn_acc()
         self.keys = torch.from_numpy(epoch.keys.view(np.int64)).to(device)
         self.types = torch.from_numpy(epoch.types).to(device)
         self.acc_txn = torch.from_numpy(epoch.acc_txn().view(np.int32)).to(device)
@@ -70,31 +74,38 @@ class DeviceEpoch:
                        if epoch.tables is not None else None)
 
     @classmethod
-    def from_tensors(cls, keys, types, acc_txn, n_txn, tables=None):
+    def from_tensors(cls, keys, types, acc_txn, n_txn, tables=None, max_txn_acc=0):
+        """max_txn_acc: bound on one txn's accesses (0 = unknown, the engine
+        then assumes the 128-access maximum)."""
         self = cls.__new__(cls)
         self.keys, self.types, self.acc_txn, self.tables = keys, types, acc_txn, tables
         self.n_acc = int(keys.numel())
         self.n_txn = int(n_txn)
+        self.max_txn_acc = int(max_txn_acc)
         return self
 
     def desc(self):
         return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
                           self.tables.data_ptr() if self.tables is not None else None,
-                          self.n_acc, self.n_txn, 0)
+                          self.n_acc, self.n_txn, self.max_txn_acc)
 
 
 class CCEngine:
     """One context = one GPU (one process per GPU)."""
 
     def __init__(self, cc_alg, max_txn, max_acc, device=0, part_cnt=1, part_id=0, timing=False,
-                 workload=L.YCSB):
+                 workload=L.YCSB, tail=True, el64=False):
+        """tail=False keeps every decision round in the multi-workgroup pass
+        (no single-workgroup tail kernel); el64=True forces 64-bit round
+        elements.  Decisions are the same either way (testing knobs)."""
         if isinstance(cc_alg, str):
             cc_alg = L.CC_NAMES[cc_alg.upper()]
         self.cc_alg = cc_alg
         self.part_cnt, self.part_id = part_cnt, part_id
         self.max_txn, self.max_acc = max_txn, max_acc
-        cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc,
-                       L.FLAG_TIMING if timing else 0, 0)
+        flags = ((L.FLAG_TIMING if timing else 0) | (0 if tail else L.FLAG_NO_TAIL)
+                 | (L.FLAG_EL64 if el64 else 0))
+        cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc, flags, 0)
         self._ctx = ctypes.c_void_p()
         L.check(L.lib().dv_open(ctypes.byref(self._ctx), ctypes.byref(cfg)), "dv_open")
 
@@ -166,6 +177,14 @@ class CCEngine:
         L.check(L.lib().dv_epoch_run_device(self._ctx, ctypes.byref(desc), _ptr(d_commit),
                                             _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
         return st
+
+    def round_log(self):
+        """(live accesses entering, undecided txns before) per decision round
+        of the last epoch."""
+        live = (ctypes.c_uint32 * 64)()
+        und = (ctypes.c_uint32 * 64)()
+        n = L.lib().dv_round_log(self._ctx, live, und, 64)
+        return list(live[:n]), list(und[:n])
 
     # ---- staged form (multi-partition epochs)
     def begin(self, dep, d_grant=None):

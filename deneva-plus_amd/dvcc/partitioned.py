@@ -55,6 +55,7 @@ class PartitionedEpoch:
         self.types = torch.from_numpy(t).to(device)
         self.txn = torch.from_numpy(x).to(device)
         self.n_txn_global = txns_per_rank * world
+        self.max_txn_acc = batch.max_txn_acc()
 
 
 class PartitionedRunner:
@@ -89,7 +90,7 @@ class PartitionedRunner:
             recv_counts = self.exchange_counts(pe)
         keys, types, txn = self.exchange(pe, recv_counts)
         n_txn = pe.n_txn_global
-        self.engine.begin_partition(keys, types, txn, n_txn)
+        self.engine.begin_partition(keys, types, txn, n_txn, max_txn_acc=pe.max_txn_acc)
         rounds = 0
         if self.engine.needs_votes:
             verdict = torch.zeros((n_txn + 3) // 4 * 4, dtype=torch.uint8, device=self.device)
@@ -118,9 +119,9 @@ class EnginePartition:
         self.needs_votes = engine.cc_alg != 10  # CALVIN has no votes
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
 
-    def begin_partition(self, keys, types, txn, n_txn):
+    def begin_partition(self, keys, types, txn, n_txn, max_txn_acc=0):
         from .engine import DeviceEpoch
-        self._dep = DeviceEpoch.from_tensors(keys, types, txn, n_txn)
+        self._dep = DeviceEpoch.from_tensors(keys, types, txn, n_txn, max_txn_acc=max_txn_acc)
         self.engine.begin(self._dep)
 
     def round_local(self, verdict):

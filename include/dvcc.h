@@ -82,7 +82,10 @@ extern "C" {
 #define DV_HASH_MOD 1  /* key % nbuckets               */
 
 /* dv_config.flags */
-#define DV_FLAG_TIMING 1u /* record HIP-event timings per stage into dv_stats */
+#define DV_FLAG_TIMING 1u  /* record HIP-event timings per stage into dv_stats */
+#define DV_FLAG_NO_TAIL 2u /* never finish the decision rounds in the single-
+                              workgroup tail kernel (testing) */
+#define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
 
 typedef struct dv_ctx dv_ctx;
 
@@ -117,7 +120,9 @@ typedef struct dv_epoch_dev {
     const uint8_t *tables;   /* [n_acc] table ids, or NULL = all table 0    */
     uint64_t n_acc;
     uint32_t n_txn;          /* txns in the epoch (global sequence space)   */
-    uint32_t reserved;
+    uint32_t max_txn_acc;    /* upper bound on one txn's accesses in this
+                                epoch (e.g. REQ_PER_QUERY); 0 = unknown
+                                (<= 128 is always required)                 */
 } dv_epoch_dev;
 
 typedef struct dv_stats {
@@ -192,6 +197,11 @@ int dv_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t *d_grant_group)
 int dv_epoch_round_local(dv_ctx *ctx, uint8_t *d_verdict);
 int dv_epoch_round_apply(dv_ctx *ctx, const uint8_t *d_verdict, uint32_t *undecided);
 int dv_epoch_finish(dv_ctx *ctx, uint8_t *d_commit, dv_stats *st);
+
+/* diagnostics: per decision round of the last finished epoch, the live
+ * accesses entering the round and the undecided txns before it; returns the
+ * number of rounds logged (at most cap, and at most 64) */
+int dv_round_log(dv_ctx *ctx, uint32_t *live, uint32_t *undecided, uint32_t cap);
 
 /* host-side epoch builder */
 int dv_ycsb_gen(const dv_ycsb_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,

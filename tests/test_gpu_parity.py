@@ -44,11 +44,11 @@ def _gpu_epoch(eng, e, path):
     return c, g, st
 
 
-def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None):
+def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False):
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
-                   max_acc or max(1, max(e.n_acc for e in epochs)))
+                   max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64)
     eng.load_ycsb_partition(rows)
     assert (eng.read_table(0, rows) == f0).all()
     for e in epochs:
@@ -201,12 +201,26 @@ def test_config_d_single_partition_full(cc):
     _check(cc, 16_777_216, [g.gen(1_048_576, dvcc.epoch_seed(0, 1))])
 
 
+@pytest.mark.parametrize("tail,el64", [(True, False), (False, False), (True, True), (False, True)])
 @pytest.mark.parametrize("rows,req,theta", [(64, 4, 0.5), (1 << 14, 8, 0.95), (1 << 12, 16, 0.99)])
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
-def test_many_rounds(cc, rows, req, theta):
+def test_many_rounds(cc, rows, req, theta, tail, el64):
     """Long decision chains: the pipelined round loop (rounds queued ahead of
-    the host, no-op rounds past the fixpoint) over many rounds."""
+    the host, no-op rounds past the fixpoint) over many rounds, with and
+    without the single-workgroup tail kernel."""
     gen = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=req)
     epochs = [gen.gen(20_000, 300 + k) for k in range(2)]
-    st = _check(cc, rows, epochs)
+    st = _check(cc, rows, epochs, tail=tail, el64=el64)
     assert st.rounds >= 2
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+def test_medium_epoch_without_tail(cc):
+    g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
+    _check(cc, 1 << 20, [g.gen(1 << 16, 98)], tail=False)
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_medium_epoch_el64(cc):
+    g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
+    _check(cc, 1 << 20, [g.gen(1 << 16, 97)], el64=True)

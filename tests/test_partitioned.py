@@ -36,7 +36,7 @@ class NumpyPartition:
     def __init__(self, cc):
         self.nowait = cc != dvcc.OCC
 
-    def begin_partition(self, keys, types_, txn, n_txn):
+    def begin_partition(self, keys, types_, txn, n_txn, max_txn_acc=0):
         k = keys.numpy().view(np.uint64)
         order = np.argsort(k, kind="stable")
         self.k, self.w, self.t = k[order], types_.numpy()[order] == 1, txn.numpy()[order].astype(np.int64)
