@@ -33,6 +33,8 @@ from dvcc.partitioned import EnginePartition, PartitionedEpoch, PartitionedRunne
 METRIC = "committed txns/sec (node) YCSB zipf0.9 at 1/2/4/8 GPUs; abort-set bit-exact"
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_ACCESS = 67        # algorithmic bytes per access
+SCAN_BYTES = 9               # SURVEY.md 8d per access: scan read 8 B + conflict flag write 1 B
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_round_pass.json")  # tools/pmc_summary.py
 
 CONFIGS = {
     # name: rows per partition, txns per GPU-epoch, zipf theta, description
@@ -154,11 +156,23 @@ def main():
     txns = sum(s.n_txn for s in stats)
     acc_local = sum(s.n_acc for s in stats)
     value = committed / el
+    # dominant kernel: the decision-round pass (k_round_pass), timed with HIP
+    # events on the engine's stream around every launch of the timed steps
+    launches = sum(s.pass_launches for s in stats)
+    pass_ms = sum(s.ms_pass for s in stats)
+    pass_live = sum(s.pass_live for s in stats)
+    avg_ms = pass_ms / max(1, launches)
+    bytes_per_launch = SCAN_BYTES * pass_live / max(1, launches)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        pmc = json.load(open(PMC_SUMMARY))
+        if pmc.get("config") == a.config and pmc.get("cc") == cc_name and pmc.get("n_gpus") == world:
+            traffic = pmc["hbm_bytes_per_launch"]
     sc_ms = [s.ms_scatter / max(1, s.scatter_launches) for s in stats if s.scatter_launches]
     sc_avg = float(np.mean(sc_ms)) if sc_ms else 0.0
     n_acc_step = acc_local / max(1, len(stats))
-    scatter_bytes = n_acc_step * 16  # one radix pass: read + write of one packed u64 per access
-    achieved = scatter_bytes / (sc_avg * 1e-3) / 1e9 if sc_avg > 0 else 0.0
+    scatter_gbps = n_acc_step * 16 / (sc_avg * 1e-3) / 1e9 if sc_avg > 0 else 0.0
     epoch_gbps = (txns / el) * (BYTES_PER_ACCESS * R + 1) / 1e9
     out = {
         "metric": METRIC,
@@ -181,16 +195,22 @@ def main():
             "distinct_epochs": n_epochs,
         },
         "roofline": {
-            "kernel": "k_radix_scatter",
+            "kernel": "k_round_pass",
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": None,
-            "bytes_per_launch": scatter_bytes,
-            "avg_launch_ms": sc_avg,
+            "traffic": traffic,
+            "bytes_per_launch": bytes_per_launch,
+            "avg_launch_ms": avg_ms,
+            "launches": launches,
+            "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d scan read "
+                                 "8 B + flag 1 B) x live accesses the launch reads",
+            "traffic_source": PMC_SUMMARY if traffic is not None else None,
         },
+        "sort": {"kernel": "k_radix_scatter", "avg_launch_ms": sc_avg, "achieved_GBps": scatter_gbps,
+                 "keys_per_s": n_acc_step / (sc_avg * 1e-3) if sc_avg > 0 else 0.0},
         "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1, "achieved_GBps": epoch_gbps,
                            "frac": epoch_gbps / HBM_PEAK_GBPS},
         "abort_rate": 1.0 - committed / max(1, txns),

@@ -65,7 +65,9 @@ struct alignas(128) CtrSlot {
 };
 struct Counters {
     uint32_t err;         // ERRB_* bits of every failure seen
-    uint32_t pad1[3];
+    uint32_t pad2;
+    uint32_t async_iters;     // most iterations any asynchronous workgroup ran
+    uint32_t pad1;
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
     uint32_t log_live[kRoundLog];  // per round: live accesses entering it
@@ -150,8 +152,10 @@ struct RoundPub {
 void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn_pad);
 // settle = single GPU (the following settle compacts the undecided list; a
 // pass whose round starts with no undecided txn is a no-op)
+// ev0/ev1 (optional): recorded by the pass's own dispatch (hipExtLaunchKernel)
 void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
-                uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub);
+                uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub, hipEvent_t ev0,
+                hipEvent_t ev1);
 // single GPU: settle statuses from the verdicts, walking the undecided-txn
 // list (ub = upper bound of its length); partitioned: local verdict bytes
 // (bit1 abort, bit0 wait), then apply the MAX-combined verdicts
@@ -165,6 +169,17 @@ void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_
 constexpr int kTailThreads = 1024;
 void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, RoundPub *pub);
 uint32_t tail_cap(bool el32);  // live accesses the tail holds in LDS
+// single GPU, 32-bit elements: every remaining decision from round r0 >= 1 in
+// one multi-workgroup launch without grid barriers, then the status bytes of
+// every txn (undecided leftovers -- an error -- counted in the slots'
+// `undecided`); carry: kAsyncGroups words of scratch.  Needs the live
+// accesses entering round r0 <= async_try_limit().
+constexpr uint32_t kAsyncGroups = 512;
+// tword: one 32-bit fact word per txn (scratch, n_txn words)
+void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G,
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn);
+uint32_t async_groups(int device);  // co-resident workgroups (<= kAsyncGroups; 0: unusable)
+uint32_t async_try_limit(uint32_t G);
 // round elements ((txn << slog | pos) << 3 | flags) fit 32 bits
 bool round_el32(uint32_t n_txn, uint32_t slog);
 

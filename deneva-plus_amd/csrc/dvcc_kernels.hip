@@ -15,6 +15,8 @@
 // Cross-workgroup dependencies go through kernel boundaries, except the
 // decoupled look-back of the single-pass scans (dvcc_common.h), whose
 // protocol is independent of dispatch order and XCD placement.
+#include <hip/hip_ext.h>
+
 #include "dvcc_common.h"
 
 namespace dvcc {
@@ -332,10 +334,12 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
         const int shift = 32 + bit;
         k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb);
         k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot);
-        if (scatter_ev) (void)hipEventRecord(scatter_ev[2 * pass], s);
-        k_radix_scatter<<<nb, kBlock, 0, s>>>(pairs[cur], pairs[cur ^ 1], n, shift, counts, digit_tot,
-                                              nb);
-        if (scatter_ev) (void)hipEventRecord(scatter_ev[2 * pass + 1], s);
+        // timing: events recorded by the dispatch itself (no extra packets)
+        hipExtLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kBlock), 0, s,
+                              scatter_ev ? scatter_ev[2 * pass] : nullptr,
+                              scatter_ev ? scatter_ev[2 * pass + 1] : nullptr, 0,
+                              (const uint64_t *)pairs[cur], pairs[cur ^ 1], n, shift,
+                              (const uint32_t *)counts, (const uint32_t *)digit_tot, nb);
         cur ^= 1;
     }
     return cur;

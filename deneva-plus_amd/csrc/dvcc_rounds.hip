@@ -28,6 +28,8 @@
 // launch (decoupled look-back scan, dvcc_common.h).  Round 0 reads the
 // row-sorted pairs directly.  Once the live set fits in LDS, one
 // single-workgroup launch runs every remaining round (k_round_tail).
+#include <hip/hip_ext.h>
+
 #include "dvcc_common.h"
 
 namespace dvcc {
@@ -104,7 +106,7 @@ template <int IPT, int WAVES>
 __device__ __forceinline__ uint32_t keep_bits(int cnt, uint32_t nhm, uint32_t needy, uint32_t blk,
                                               RAgg *rw, RAgg far, uint32_t lane, uint32_t wave) {
     const uint32_t valid = cnt >= 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
-    RAgg x{1u, 0u};
+    RAgg x{0u, 0u};  // a thread past the end is transparent: `far` reaches the last element
     if (cnt > 0) {
         const uint32_t cuts = nhm & valid;
         x.f = cuts != 0;
@@ -665,6 +667,221 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
     }
 }
 
+// ---- asynchronous rounds: every remaining decision in one multi-workgroup
+//      launch, without grid barriers
+// Once the live set fits the workgroups' LDS, each workgroup takes an equal
+// contiguous slice of the row-ordered elements and iterates on its own: read
+// the status of its elements' txns, scan its queues, decide, publish the
+// facts, compact.  A txn's status is a monotone fact (undecided, then
+// committed or aborted), so any mix of fresh and stale reads of the facts
+// other workgroups publish yields only true decisions, and the greedy's
+// fixpoint is unique: the outcome equals the round-synchronous one.  A txn's
+// facts are one 32-bit word -- status | OK count << 8 | accesses << 16 -- set
+// with device-scope atomics and read with agent-scope atomic loads, so they
+// cross CUs and XCDs inside the launch and one load tells committed (count ==
+// accesses), aborted or undecided.
+// A row queue may run across slices: each workgroup publishes, every
+// iteration, the OR of the scan values of the queue its slice ends in (its
+// carry word); the next workgroup reads it as the value in front of its first
+// element.  Carries are built from monotone facts and start fully
+// pessimistic, so a stale carry only delays decisions.  The slice's last
+// element is never dropped while its queue runs on, so the carry always
+// describes that queue.  A workgroup leaves
+// once no element of an undecided txn remains in its slice and its carry no
+// longer holds an undecided blocker; the lowest undecided txn can always
+// decide, so every workgroup leaves (bounded spin: ERRB_SPIN).
+constexpr int kAsyncThreads = 512;
+constexpr int kAsyncWaves = kAsyncThreads / 64;
+constexpr int kAsyncIPT = 24;
+constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
+constexpr uint32_t kAsyncMaxIters = 1u << 18;
+constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP;  // "undecided blockers in front"
+
+constexpr uint32_t TW_OK = 1u << 8;  // one more access OK
+
+__device__ __forceinline__ uint8_t word_status(uint32_t w) {
+    const uint32_t s = w & 0xFFu;
+    if (s != ST_UNDEC) return (uint8_t)s;
+    return ((w >> 8) & 0xFFu) == (w >> 16) ? (uint8_t)ST_COMMIT : (uint8_t)ST_UNDEC;
+}
+// the status fact of txn t
+__device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t) {
+    return word_status(__hip_atomic_load(tword + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// the words from the synchronous rounds' state (status byte, OK verdict
+// bytes), and every carry word pessimistic
+__global__ __launch_bounds__(kBlock) void k_async_words(const uint8_t *__restrict__ status,
+                                                        const uint8_t *__restrict__ vb8, uint32_t slog,
+                                                        const uint8_t *__restrict__ tlen, uint32_t n_txn,
+                                                        uint32_t *__restrict__ tword,
+                                                        uint32_t *__restrict__ carry, uint32_t G) {
+    const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint32_t g = i0; g < G; g += gridDim.x * blockDim.x) carry[g] = kCarryInit;
+    for (uint32_t t = i0; t < n_txn; t += gridDim.x * blockDim.x) {
+        const uint32_t len = tlen[t];
+        uint32_t ok = 0;
+        const uint8_t s = status[t];
+        if (s == ST_UNDEC) {
+            for (uint32_t w = 0; w < len; w += 16) {
+                const uint4 x4 = *reinterpret_cast<const uint4 *>(vb8 + ((size_t)t << slog) + w);
+                const uint32_t x[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++) {
+                    const int nb = (int)len - (int)(w + 4 * q);
+                    const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
+                    ok += __popc(x[q] & 0x01010101u & m);
+                }
+            }
+        }
+        tword[t] = s | (ok << 8) | (len << 16);
+    }
+}
+
+__global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
+                                                               const uint32_t *n_in, uint32_t *tword,
+                                                               uint32_t *carry, int nowait,
+                                                               uint32_t max_iters) {
+    constexpr int IPT = kAsyncIPT;
+    __shared__ uint32_t sel[kAsyncCap];
+    __shared__ RAgg rw[kAsyncWaves];
+    __shared__ Agg wt[kAsyncWaves];
+    // per-iteration counters, double-buffered by iteration parity: slot p is
+    // reset during the iteration before it is used, after every thread has
+    // read it for the iteration before that
+    __shared__ uint32_t s_needy[2], s_moved[2];
+    Counters *ctr = b.ctr;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
+    const uint32_t n_all = *n_in;
+    const uint32_t lo = (uint32_t)((uint64_t)g * n_all / G), hi = (uint32_t)((uint64_t)(g + 1) * n_all / G);
+    uint32_t n = hi - lo;
+    if (n > kAsyncCap) {  // the host launches only when every slice fits
+        if (tid == 0) set_err(ctr, ERRB_BIG);
+        return;
+    }
+    // does a queue run in from the previous slice / out into the next one?
+    const bool cont_in = lo > 0 && lo < n_all && !(src[lo] & F_HEAD);
+    const bool cont_out = hi < n_all && !(src[hi] & F_HEAD);
+    for (uint32_t i = tid; i < n; i += kAsyncThreads) sel[i] = src[lo + i] & ~(i == 0 && cont_in ? F_HEAD : 0u);
+    if (tid == 0) s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
+    __syncthreads();
+    uint32_t it = 0;
+    for (; it < max_iters; it++) {
+        const uint32_t p = it & 1u;
+        const uint32_t cin = cont_in ? __hip_atomic_load(carry + g - 1, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                                     : 0u;
+        const uint32_t k = (n + kAsyncThreads - 1) / kAsyncThreads;
+        const uint32_t first = tid * k;
+        const int cnt = first >= n ? 0 : (int)(n - first < k ? n - first : k);
+        uint32_t e[IPT], v[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; j++) e[j] = j < cnt ? sel[first + j] : F_HEAD;
+        const uint32_t nxt = first + (uint32_t)cnt < n ? sel[first + cnt] : (cont_out ? 0u : F_HEAD);
+        uint32_t nhm = 0, umask = 0, needy = 0, blk = 0;
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            v[j] = 0;
+            if (j < cnt) {
+                const bool nh = j + 1 < cnt ? (e[j + 1] & F_HEAD) != 0 : (nxt & F_HEAD) != 0;
+                nhm |= (nh ? 1u : 0u) << j;
+                const uint8_t s = fact_status(tword, r_txn(e[j], slog));
+                umask |= (s == ST_UNDEC ? 1u : 0u) << j;
+                needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
+                const bool single = (e[j] & F_HEAD) && nh;
+                blk |= (s != ST_ABORT && !single ? 1u : 0u) << j;
+                v[j] = elem_value(e[j], s, nowait);
+            }
+        }
+        // a queue running into the next slice is assumed to be followed by a
+        // needy element there (keep_bits holds a barrier: every thread is done
+        // with slot p ^ 1 of the previous iteration)
+        uint32_t keep = keep_bits<IPT, kAsyncWaves>(cnt, nhm, needy, blk, rw,
+                                                    RAgg{1u, cont_out ? 1u : 0u}, lane, wave);
+        // ... and the slice's last element anchors that queue here: it is kept
+        // whatever its txn, so the carry is always the OR of that queue (were
+        // the queue's elements all dropped, the last head would be an
+        // earlier queue's)
+        if (cont_out && cnt > 0 && first + (uint32_t)cnt == n) keep |= 1u << (cnt - 1);
+        if (tid == 0) { s_needy[p ^ 1u] = 0; s_moved[p ^ 1u] = 0; }
+        if (needy) atomicAdd(&s_needy[p], (uint32_t)__builtin_popcount(needy));
+        Agg a{0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            if (j < cnt) {
+                if ((keep >> j) & 1u) v[j] |= B_KEEP;
+                a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & F_HEAD) != 0), v[j], (keep >> j) & 1u});
+            }
+        }
+        const Agg inc = wave_incl<OpPlain>(a, lane);
+        if (lane == 63) wt[wave] = inc;
+        __syncthreads();
+        Agg wpre{0u, cin, 0u}, total{0u, cin, 0u};  // the carry is in front of the slice
+        for (int w = 0; w < kAsyncWaves; w++) {
+            if (w < (int)wave) wpre = OpPlain::comb(wpre, wt[w]);
+            total = OpPlain::comb(total, wt[w]);
+        }
+        const Agg pre = OpPlain::comb(wpre, wave_excl_from_incl<OpPlain>(inc, lane));
+        uint32_t lpos = pre.c, run = pre.v, moved = 0;
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            if (j < cnt) {
+                uint32_t ej = e[j];
+                const bool head = (ej & F_HEAD) != 0;
+                const uint32_t excl = head ? 0u : run;
+                if (((umask >> j) & 1u) && !(ej & F_DONE)) {
+                    const uint32_t sl = (nowait && (ej & F_WR)) ? (excl & (B_CA | B_UA))
+                                                                : ((excl >> 2) & (B_CA | B_UA));
+                    if (sl & B_CA) {  // Abort (row_lock.cpp:86-90 / occ.cpp:219-234)
+                        atomicOr(tword + r_txn(ej, slog), (uint32_t)ST_ABORT);
+                        moved = 1;
+                    } else if (!(sl & B_UA)) {  // permanently OK
+                        atomicAdd(tword + r_txn(ej, slog), TW_OK);
+                        ej |= F_DONE;
+                        moved = 1;
+                    }
+                }
+                // the slice's first element never becomes a head when a queue
+                // runs in: what is in front of it arrives through the carry
+                if (v[j] & B_KEEP) sel[lpos++] = (ej & ~F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD);
+                run = head ? v[j] : (run | v[j]);
+            }
+        }
+        if (moved) s_moved[p] = 1;
+        // what the next slice has in front of it: the OR since the last head
+        const uint32_t cout = total.v;
+        if (cont_out && tid == 0)
+            __hip_atomic_store(carry + g, cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        n = total.c;
+        __syncthreads();
+        if (s_needy[p] == 0 && (!cont_out || !(cout & (B_UA | B_UW)))) break;  // nothing left to learn
+        // nothing decided here: the facts this slice waits for come from other
+        // workgroups -- back off before reading them again
+        if (!s_moved[p]) __builtin_amdgcn_s_sleep(8);
+    }
+    if (tid == 0) {
+        if (it >= max_iters) set_err(ctr, ERRB_SPIN);
+        atomicMax(&ctr->async_iters, it);
+    }
+}
+
+// after the asynchronous rounds: the status bytes from the words (a declined
+// launch leaves undecided txns; their OKs are recomputed by the rounds that
+// resume) and the count of txns left undecided
+__global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__ status,
+                                                           const uint32_t *__restrict__ tword,
+                                                           uint32_t n_txn, Counters *ctr) {
+    uint32_t und = 0;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
+        const uint8_t s = word_status(tword[t]);
+        status[t] = s;
+        und += s == ST_UNDEC ? 1u : 0u;
+    }
+    if (und) atomicAdd(&my_slot(ctr).undecided, und);
+}
+
+
 __global__ void k_round0_init(uint32_t n, Counters *ctr) { ctr->nlive[0] = n; }
 
 // ------------------------------------------------------------- launchers
@@ -688,7 +905,8 @@ void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32
 
 template <class E>
 static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
-                         uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub) {
+                         uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub, hipEvent_t ev0,
+                         hipEvent_t ev1) {
     E *out = reinterpret_cast<E *>(b.rel[round & 1]);
     const uint32_t *n_in = &b.ctr->nlive[round & 1];
     uint32_t *n_out = &b.ctr->nlive[(round + 1) & 1];
@@ -698,28 +916,56 @@ static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int 
     if (round == 0) {
         using G = Geo<uint64_t>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
-        k_round_pass<true, uint64_t, E><<<nb, G::kThreads, 0, s>>>(
-            b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait, b.desc, tc, tag, und, nullptr,
-            round, nullptr, b.ctr);
+        hipExtLaunchKernelGGL(k_round_pass<true, uint64_t, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0,
+                              ev1, 0, b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait,
+                              b.desc, tc, tag, und, (const uint32_t *)nullptr, round,
+                              (RoundPub *)nullptr, b.ctr);
     } else {
         using G = Geo<E>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
-        k_round_pass<false, E, E><<<nb, G::kThreads, 0, s>>>(
-            reinterpret_cast<const E *>(b.rel[(round - 1) & 1]), n_in, out, n_out, b.status, b.vb8,
-            b.slog, nowait, b.desc, tc, tag, und, und_in, round, pub, b.ctr);
+        hipExtLaunchKernelGGL(k_round_pass<false, E, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0, ev1, 0,
+                              reinterpret_cast<const E *>(b.rel[(round - 1) & 1]), n_in, out, n_out,
+                              b.status, b.vb8, b.slog, nowait, b.desc, tc, tag, und, und_in, round,
+                              pub, b.ctr);
     }
 }
 
 void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
-                uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub) {
-    if (b.el32) round_pass_t<uint32_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub);
-    else round_pass_t<uint64_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub);
+                uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub, hipEvent_t ev0,
+                hipEvent_t ev1) {
+    if (b.el32) round_pass_t<uint32_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub, ev0, ev1);
+    else round_pass_t<uint64_t>(s, b, round, nowait, ub_in, tag, ticket, settle, pub, ev0, ev1);
 }
 
 void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, RoundPub *pub) {
     if (b.el32) k_round_tail<uint32_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
     else k_round_tail<uint64_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
 }
+
+void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G,
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
+    k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
+                                                                    n_txn, tword, carry, G);
+    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, &b.ctr->nlive[r0 & 1], tword, carry, nowait,
+                                              kAsyncMaxIters);
+    if (n_txn) k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, b.ctr);
+}
+
+// Every workgroup of the asynchronous launch must be resident at once (one
+// may wait for facts only another produces): at most what the occupancy
+// calculator admits on every CU of the device.
+uint32_t async_groups(int device) {
+    int cus = 0, per = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_round_async, kAsyncThreads, 0) !=
+            hipSuccess)
+        return 0;
+    const uint64_t g = (uint64_t)cus * (uint64_t)per;
+    return (uint32_t)(g < kAsyncGroups ? g : kAsyncGroups);
+}
+
+uint32_t async_try_limit(uint32_t G) { return G * kAsyncCap; }
 
 void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub) {
     const uint32_t n = round == 0 ? n_txn : (ub < n_txn ? ub : n_txn);

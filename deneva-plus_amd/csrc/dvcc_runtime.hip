@@ -58,6 +58,9 @@ struct dv_ctx {
     uint32_t *tb_start = nullptr, *tb_end = nullptr; // per txn: its access range
     uint64_t *desc = nullptr;                        // look-back tile descriptors
     uint32_t *tile_ctr = nullptr;                    // tile tickets, one per single-pass launch
+    uint32_t *abounds = nullptr;                     // asynchronous-round slice carries
+    uint32_t *tword = nullptr;                       // asynchronous-round txn fact words
+    uint32_t async_g = 0;                            // its workgroups (all co-resident)
     uint32_t round_tag = 0;                          // descriptor tag of the last pass
     uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
@@ -86,6 +89,8 @@ struct dv_ctx {
     // timing
     hipEvent_t ev[32] = {};
     hipEvent_t sev[16] = {};
+    hipEvent_t pev[2 * kRoundLog] = {};  // around each decision-round pass
+    uint32_t passes = 0;                 // pass launches this epoch
     float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
 };
 
@@ -241,6 +246,7 @@ void dv_close(dv_ctx *c) {
     void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
                     c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tlen, c->acc_row,
                     c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
+                    c->abounds, c->tword,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
@@ -248,6 +254,7 @@ void dv_close(dv_ctx *c) {
     if (c->h_pub) (void)hipHostFree(c->h_pub);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : c->sev) if (e) (void)hipEventDestroy(e);
+    for (auto &e : c->pev) if (e) (void)hipEventDestroy(e);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -294,6 +301,9 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
         if (!r) r = dalloc(&c->acc_row, A);
         if (!r) r = dalloc(&c->ulist[0], T);
         if (!r) r = dalloc(&c->ulist[1], T);
+        if (!r) r = dalloc(&c->abounds, kAsyncGroups);
+        if (!r) r = dalloc(&c->tword, c->n_txn_cap_pad);
+        if (!r) c->async_g = async_groups(cfg->device);
         // verdict bytes: 16 per txn; grown on demand for longer txns (dv_epoch_begin)
         c->vb8_cap = (uint64_t)c->n_txn_cap_pad << 4;
         if (!r) r = dalloc(&c->vb8, c->vb8_cap);
@@ -313,6 +323,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r && timing(c)) {
         for (auto &e : c->ev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
         for (auto &e : c->sev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
+        for (auto &e : c->pev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
     }
     if (!r) r = hip_fail(hipMemsetAsync(c->verdict, 0, c->n_txn_cap_pad, c->stream), "memset");
     if (!r) r = hip_fail(hipStreamSynchronize(c->stream), "sync");
@@ -528,6 +539,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->n_txn_pad = (ep->n_txn + 3u) & ~3u;
     c->rounds = 0;
     c->rounds_real = 0;
+    c->passes = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
@@ -575,8 +587,13 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     const uint32_t tag = next_tag(c);
     uint32_t *tc = next_ticket(c);
     const RoundBufs b = round_bufs(c);
+    // timing: the pass's own dispatch records its events (hipExtLaunchKernel),
+    // no extra packets in the stream
+    const bool t = timing(c) && c->passes < (uint32_t)kRoundLog;
     round_pass(c->stream, b, r, c->cfg.cc_alg != DV_OCC, c->live_ub, tag,
-               (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr);
+               (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr,
+               t ? c->pev[2 * c->passes] : nullptr, t ? c->pev[2 * c->passes + 1] : nullptr);
+    c->passes++;
     if (settle) round_settle(c->stream, b, r, c->n_txn, c->und_ub);
     else round_verdict(c->stream, b, c->n_txn, d_verdict);
     c->rounds++;
@@ -667,6 +684,18 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             }
             st->ms_scatter = s;
             st->scatter_launches = c->n_acc ? c->sort_passes : 0;
+            const uint32_t np = std::min(c->passes, (uint32_t)kRoundLog);
+            float sp = 0;
+            uint64_t live = 0;
+            for (uint32_t p = 0; p < np; p++) {
+                float m = 0;
+                (void)hipEventElapsedTime(&m, c->pev[2 * p], c->pev[2 * p + 1]);
+                sp += m;
+                live += c->h_ctr->log_live[p];  // 0 for a no-op pass past the fixpoint
+            }
+            st->pass_launches = np;
+            st->ms_pass = sp;
+            st->pass_live = live;
         }
     }
     return DV_OK;
@@ -728,6 +757,7 @@ int run_rounds(dv_ctx *c) {
     uint32_t tail_r0 = 0;             // round the pending tail launch starts at (0: none)
     const uint32_t cap = tail_cap(c->el32);
     uint32_t tail_limit = kTailTryFactor * cap;  // published live count that triggers a try
+    bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     for (;;) {
         while (!tail_r0 && c->rounds < seen + kRoundsAhead + 1) enqueue_round(c, nullptr, true);
         int r = hip_fail(hipGetLastError(), "round launch");
@@ -758,6 +788,21 @@ int run_rounds(dv_ctx *c) {
         prev = und;
         c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));  // bounds for rounds not yet enqueued
         c->und_ub = und;
+        if (async && !tail_r0 && c->live_ub <= async_try_limit(c->async_g)) {
+            // every remaining decision in one asynchronous launch (round_async)
+            const uint32_t r0 = c->rounds;
+            round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, c->abounds,
+                        c->tword, c->n_txn);
+            r = sync_counters(c);
+            if (!r) r = err_from_bits(c->h_ctr->err);
+            if (r) return r;
+            uint32_t left = 0;
+            for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
+            if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
+            c->rounds_real = r0 + c->h_ctr->async_iters;
+            c->rounds = std::max(c->rounds, r0);
+            return DV_OK;
+        }
         if (!tail_r0 && !(c->cfg.flags & DV_FLAG_NO_TAIL) && c->live_ub <= tail_limit) {
             tail_r0 = c->rounds;
             round_tail(c->stream, round_bufs(c), tail_r0, c->cfg.cc_alg != DV_OCC, c->d_pub);

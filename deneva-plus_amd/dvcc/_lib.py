@@ -30,6 +30,7 @@ HASH_YCSB, HASH_MOD = 0, 1
 FLAG_TIMING = 1
 FLAG_NO_TAIL = 2
 FLAG_EL64 = 4
+FLAG_NO_ASYNC = 8
 
 
 class DvccError(RuntimeError):
@@ -65,7 +66,9 @@ class Stats(ctypes.Structure):
                 ("ms_total", ctypes.c_float), ("ms_probe", ctypes.c_float),
                 ("ms_sort", ctypes.c_float), ("ms_decide", ctypes.c_float),
                 ("ms_exec", ctypes.c_float), ("ms_scatter", ctypes.c_float),
-                ("scatter_launches", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("scatter_launches", ctypes.c_uint32), ("pass_launches", ctypes.c_uint32),
+                ("ms_pass", ctypes.c_float), ("reserved", ctypes.c_uint32),
+                ("pass_live", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}

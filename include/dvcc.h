@@ -86,6 +86,8 @@ extern "C" {
 #define DV_FLAG_NO_TAIL 2u /* never finish the decision rounds in the single-
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
+#define DV_FLAG_NO_ASYNC 8u /* never finish the decision rounds in the
+                               asynchronous multi-workgroup kernel (testing) */
 
 typedef struct dv_ctx dv_ctx;
 
@@ -142,7 +144,10 @@ typedef struct dv_stats {
     float ms_exec;
     float ms_scatter;        /* sum over radix-scatter launches                */
     uint32_t scatter_launches;
+    uint32_t pass_launches;  /* decision-round pass launches (k_round_pass)    */
+    float ms_pass;           /* sum over those launches                        */
     uint32_t reserved;
+    uint64_t pass_live;      /* live accesses those launches read, summed      */
 } dv_stats;
 
 /* parameters of YCSBQueryGenerator (g_* globals, system/global.cpp:65-195) */

@@ -42,6 +42,7 @@ def test_struct_layouts_match_header():
     assert ctypes.sizeof(_lib.Config) == 40
     assert ctypes.sizeof(_lib.EpochDev) == 48
     assert ctypes.sizeof(_lib.YcsbParams) == 56
+    assert ctypes.sizeof(_lib.Stats) == 104
 
 
 def test_strerror():

@@ -44,11 +44,13 @@ def _gpu_epoch(eng, e, path):
     return c, g, st
 
 
-def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False):
+def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False,
+           asynchronous=True):
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
-                   max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64)
+                   max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64,
+                   asynchronous=asynchronous)
     eng.load_ycsb_partition(rows)
     assert (eng.read_table(0, rows) == f0).all()
     for e in epochs:
@@ -201,23 +203,31 @@ def test_config_d_single_partition_full(cc):
     _check(cc, 16_777_216, [g.gen(1_048_576, dvcc.epoch_seed(0, 1))])
 
 
-@pytest.mark.parametrize("tail,el64", [(True, False), (False, False), (True, True), (False, True)])
+@pytest.mark.parametrize("tail,el64,asyn", [(True, False, True), (True, False, False),
+                                            (False, False, False), (True, True, True),
+                                            (False, True, True)])
 @pytest.mark.parametrize("rows,req,theta", [(64, 4, 0.5), (1 << 14, 8, 0.95), (1 << 12, 16, 0.99)])
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
-def test_many_rounds(cc, rows, req, theta, tail, el64):
+def test_many_rounds(cc, rows, req, theta, tail, el64, asyn):
     """Long decision chains: the pipelined round loop (rounds queued ahead of
     the host, no-op rounds past the fixpoint) over many rounds, with and
     without the single-workgroup tail kernel."""
     gen = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=req)
     epochs = [gen.gen(20_000, 300 + k) for k in range(2)]
-    st = _check(cc, rows, epochs, tail=tail, el64=el64)
+    st = _check(cc, rows, epochs, tail=tail, el64=el64, asynchronous=asyn)
     assert st.rounds >= 2
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
 def test_medium_epoch_without_tail(cc):
     g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
-    _check(cc, 1 << 20, [g.gen(1 << 16, 98)], tail=False)
+    _check(cc, 1 << 20, [g.gen(1 << 16, 98)], tail=False, asynchronous=False)
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+def test_medium_epoch_tail_only(cc):
+    g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
+    _check(cc, 1 << 20, [g.gen(1 << 16, 96)], asynchronous=False)
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
