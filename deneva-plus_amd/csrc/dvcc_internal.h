@@ -148,8 +148,14 @@ struct RoundPub {
     unsigned long long le;  // live accesses << 32 | error bits
     unsigned long long tl;  // tail launched at round r0 but the live set did not
                             // fit: r0 << 32 | 1 (the rounds resume from r0)
+    // partitioned rounds: undecided txns after round r, at [r % kPubLog]
+    // (written before ru publishes r + 1), so every rank reads the count of
+    // the same round however far its stream has run ahead
+    static constexpr uint32_t kPubLog = 64;
+    unsigned int und_log[kPubLog];
 };
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn_pad);
+void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
+                       uint32_t n_txn_pad);
 // settle = single GPU (the following settle compacts the undecided list; a
 // pass whose round starts with no undecided txn is a no-op)
 // ev0/ev1 (optional): recorded by the pass's own dispatch (hipExtLaunchKernel)
@@ -157,11 +163,15 @@ void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, u
                 uint32_t tag, uint32_t ticket, bool settle, RoundPub *pub, hipEvent_t ev0,
                 hipEvent_t ev1);
 // single GPU: settle statuses from the verdicts, walking the undecided-txn
-// list (ub = upper bound of its length); partitioned: local verdict bytes
-// (bit1 abort, bit0 wait), then apply the MAX-combined verdicts
+// list (ub = upper bound of its length)
 void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub);
-void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict);
-void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_t *verdict);
+// partitioned: this partition's verdict byte (bit1 abort, bit0 wait) for every
+// entry of round `round`'s undecided list, in list order (ub: bound of the
+// list length); then apply the MAX-combined bytes, compact the list for the
+// next round (same order on every rank) and publish (round + 1, its length)
+void list_verdict(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, uint8_t *verdict);
+void list_apply(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, const uint8_t *verdict,
+                uint32_t tag, uint32_t *tile_ctr, RoundPub *pub);
 // single GPU: all remaining rounds from round r0 >= 1 in one single-workgroup
 // launch; publishes the final round and 0 undecided (0xFFFFFFFF on failure)
 // through pub, or declines (pub->tl) and does nothing when the live accesses

@@ -483,32 +483,109 @@ __global__ __launch_bounds__(kBlock) void k_round_settle(
     settle_chunk<FIRST>(sh, lo, n, status, vb8, slog, tlen, list_in, list_out, n_out);
 }
 
-// ---- partitioned: this partition's verdict byte per txn (bit1 abort, bit0
-//      wait), combined across partitions by an element-wise MAX
-__global__ __launch_bounds__(kBlock) void k_round_verdict(const uint8_t *__restrict__ status,
-                                                          const uint8_t *__restrict__ vb8,
-                                                          uint32_t slog,
-                                                          const uint8_t *__restrict__ tlen,
-                                                          uint32_t n_txn, uint8_t *__restrict__ verdict) {
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x)
-        verdict[t] = status[t] == ST_UNDEC   ? txn_verdict(vb8 + ((size_t)t << slog), tlen[t])
-                     : status[t] == ST_ABORT ? (uint8_t)V_ABORT  // possibly aborted by this pass
-                                             : (uint8_t)0;
+// ---- partitioned rounds over the undecided-txn list -----------------------
+// Every partition holds the same statuses after each apply, so the list of
+// undecided txns (ascending, compacted by a deterministic scan) is the same
+// on every rank: verdict bytes travel for list entries only, in list order,
+// and the all-reduce shrinks with the undecided set (1M txns: 1 MB in round
+// 0, a few KB by the tail) instead of n_txn bytes every round.
+// list = nullptr: round 0, the list is every txn.
+__global__ __launch_bounds__(kBlock) void k_list_verdict(const uint32_t *__restrict__ list,
+                                                         const uint32_t *__restrict__ n_list,
+                                                         const uint8_t *__restrict__ status,
+                                                         const uint8_t *__restrict__ vb8, uint32_t slog,
+                                                         const uint8_t *__restrict__ tlen,
+                                                         uint8_t *__restrict__ verdict) {
+    const uint32_t U = *n_list;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < U; i += gridDim.x * blockDim.x) {
+        const uint32_t t = list ? list[i] : i;
+        const uint8_t s = status[t];
+        // a local abort (this round's pass) is final everywhere; an undecided
+        // txn reports its local accesses' verdict
+        verdict[i] = s == ST_ABORT ? (uint8_t)V_ABORT
+                                   : (s == ST_UNDEC ? txn_verdict(vb8 + ((size_t)t << slog), tlen[t]) : 0);
+    }
 }
 
-// ---- partitioned: apply the combined verdicts
-__global__ __launch_bounds__(kBlock) void k_round_apply(uint8_t *__restrict__ status,
-                                                        const uint8_t *__restrict__ verdict,
-                                                        uint32_t n_txn, Counters *ctr) {
-    uint32_t und = 0;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
-        if (status[t] != ST_UNDEC) continue;
-        const uint8_t v = verdict[t];
-        if (v & V_ABORT) status[t] = ST_ABORT;
-        else if (v & V_WAIT) und++;
-        else status[t] = ST_COMMIT;
+// apply the MAX-combined verdicts, compact the list (order kept: decoupled
+// look-back over kRTile-entry tiles) and publish the undecided count
+__global__ __launch_bounds__(kBlock) void k_list_apply(
+    const uint32_t *__restrict__ list, const uint32_t *__restrict__ n_list,
+    const uint8_t *__restrict__ verdict, uint8_t *__restrict__ status, uint32_t *__restrict__ list_out,
+    uint32_t *__restrict__ n_out, const uint32_t *__restrict__ n_live_next, uint64_t *desc,
+    uint32_t *tile_ctr, uint32_t tag, uint32_t round, RoundPub *pub, Counters *ctr) {
+    __shared__ Agg wt[4];
+    __shared__ Agg s_pre;
+    __shared__ uint32_t s_tile;
+    const uint32_t U = *n_list;
+    const uint32_t ntiles = (U + kRTile - 1) / kRTile;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (blockIdx.x >= ntiles) {
+        if (ntiles == 0 && blockIdx.x == 0 && tid == 0) {
+            *n_out = 0;
+            if (pub) {
+                __hip_atomic_store(&pub->und_log[round % RoundPub::kPubLog], 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+                __threadfence_system();
+                __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                __hip_atomic_store(&pub->ru, (unsigned long long)(round + 1) << 32, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        return;
     }
-    block_count(und, ctr);
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile, base = tile * kRTile;
+    // kRIPT consecutive entries per thread
+    uint32_t keepm = 0, tl[kRIPT];
+    const uint32_t first = base + tid * kRIPT;
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++) {
+        const uint32_t i = first + j;
+        tl[j] = 0;
+        if (i < U) {
+            const uint32_t t = list ? list[i] : i;
+            tl[j] = t;
+            const uint8_t v = verdict[i];
+            if (status[t] == ST_UNDEC) {
+                if (v & V_ABORT) status[t] = ST_ABORT;
+                else if (!(v & V_WAIT)) status[t] = ST_COMMIT;
+                else keepm |= 1u << j;
+            }
+        }
+    }
+    const Agg inc = wave_incl<OpPlain>(Agg{0u, 0u, (uint32_t)__builtin_popcount(keepm)}, lane);
+    if (lane == 63) wt[wave] = inc;
+    __syncthreads();
+    if (wave == 0) {
+        Agg bagg = wt[0];
+        for (int w = 1; w < 4; w++) bagg = OpPlain::comb(bagg, wt[w]);
+        const Agg pre = look_back<OpPlain>(desc, tile, tag, bagg, lane, ctr);
+        if (lane == 0) s_pre = pre;
+    }
+    __syncthreads();
+    uint32_t pos = s_pre.c;
+    for (uint32_t w = 0; w < wave; w++) pos += wt[w].c;
+    pos += wave_excl_from_incl<OpPlain>(inc, lane).c;
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++)
+        if ((keepm >> j) & 1u) list_out[pos++] = tl[j];
+    if (tile == ntiles - 1 && tid == 0) {
+        uint32_t tot = s_pre.c;
+        for (int w = 0; w < 4; w++) tot += wt[w].c;
+        *n_out = tot;
+        if (pub) {
+            __hip_atomic_store(&pub->und_log[round % RoundPub::kPubLog], tot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+            __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pub->ru, ((unsigned long long)(round + 1) << 32) | tot, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
 }
 
 
@@ -882,7 +959,10 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
 }
 
 
-__global__ void k_round0_init(uint32_t n, Counters *ctr) { ctr->nlive[0] = n; }
+__global__ void k_round0_init(uint32_t n, uint32_t n_txn, Counters *ctr) {
+    ctr->nlive[0] = n;
+    ctr->nund[0] = n_txn;  // partitioned rounds: round 0's list is every txn
+}
 
 // ------------------------------------------------------------- launchers
 static uint32_t txn_grid(uint32_t n_txn) {
@@ -898,9 +978,10 @@ bool round_el32(uint32_t n_txn, uint32_t slog) {
 
 uint32_t tail_cap(bool el32) { return el32 ? TailGeo<uint32_t>::kCap : TailGeo<uint64_t>::kCap; }
 
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn_pad) {
+void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
+                       uint32_t n_txn_pad) {
     (void)hipMemsetAsync(b.vb8, 0, n_txn_pad ? ((size_t)n_txn_pad << b.slog) : 16, s);
-    k_round0_init<<<1, 1, 0, s>>>(n_acc, b.ctr);
+    k_round0_init<<<1, 1, 0, s>>>(n_acc, n_txn, b.ctr);
 }
 
 template <class E>
@@ -912,7 +993,9 @@ static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int 
     uint32_t *n_out = &b.ctr->nlive[(round + 1) & 1];
     uint32_t *tc = &b.tile_ctr[ticket % kTileCtrs];
     uint32_t *und = settle ? &b.ctr->nund[(round + 1) & 1] : nullptr;
-    const uint32_t *und_in = settle && round > 0 ? &b.ctr->nund[round & 1] : nullptr;
+    // the pass is a no-op once no txn is undecided: single GPU, the settle's
+    // list; partitioned, the list the applies keep
+    const uint32_t *und_in = !settle || round > 0 ? &b.ctr->nund[round & 1] : nullptr;
     if (round == 0) {
         using G = Geo<uint64_t>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
@@ -980,15 +1063,20 @@ void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_
                                                     n_txn, b.ulist[(round + 1) & 1], n_out);
 }
 
-void round_verdict(hipStream_t s, const RoundBufs &b, uint32_t n_txn, uint8_t *verdict) {
-    if (!n_txn) return;
-    k_round_verdict<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, n_txn,
-                                                      verdict);
+void list_verdict(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, uint8_t *verdict) {
+    const uint32_t *list = round == 0 ? nullptr : b.ulist[round & 1];
+    k_list_verdict<<<txn_grid(ub), kBlock, 0, s>>>(list, &b.ctr->nund[round & 1], b.status, b.vb8,
+                                                  b.slog, b.tlen, verdict);
 }
 
-void round_apply(hipStream_t s, const RoundBufs &b, uint32_t n_txn, const uint8_t *verdict) {
-    if (!n_txn) return;
-    k_round_apply<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, verdict, n_txn, b.ctr);
+void list_apply(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, const uint8_t *verdict,
+                uint32_t tag, uint32_t *tile_ctr, RoundPub *pub) {
+    const uint32_t *list = round == 0 ? nullptr : b.ulist[round & 1];
+    const uint32_t nb = ub ? (ub + kRTile - 1) / kRTile : 1;
+    k_list_apply<<<nb, kBlock, 0, s>>>(list, &b.ctr->nund[round & 1], verdict, b.status,
+                                       b.ulist[(round + 1) & 1], &b.ctr->nund[(round + 1) & 1],
+                                       &b.ctr->nlive[(round + 1) & 1], b.desc, tile_ctr, tag, round, pub,
+                                       b.ctr);
 }
 
 }  // namespace dvcc

@@ -91,6 +91,7 @@ struct dv_ctx {
     hipEvent_t sev[16] = {};
     hipEvent_t pev[2 * kRoundLog] = {};  // around each decision-round pass
     uint32_t passes = 0;                 // pass launches this epoch
+    uint32_t applied = 0;                // partitioned rounds applied this epoch
     float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
 };
 
@@ -540,6 +541,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->rounds = 0;
     c->rounds_real = 0;
     c->passes = 0;
+    c->applied = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
@@ -568,7 +570,9 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         const uint32_t tag = next_tag(c);
         calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
-        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, c->n_txn_pad);
+        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, ep->n_txn, c->n_txn_pad);
+        __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
+        __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
         c->live_ub = (uint32_t)ep->n_acc;
         c->und_ub = ep->n_txn;
     }
@@ -595,7 +599,7 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
                t ? c->pev[2 * c->passes] : nullptr, t ? c->pev[2 * c->passes + 1] : nullptr);
     c->passes++;
     if (settle) round_settle(c->stream, b, r, c->n_txn, c->und_ub);
-    else round_verdict(c->stream, b, c->n_txn, d_verdict);
+    else list_verdict(c->stream, b, r, c->und_ub, d_verdict);
     c->rounds++;
 }
 
@@ -617,6 +621,45 @@ int round_sync(dv_ctx *c, uint32_t *undecided, bool settle) {
 
 }  // namespace
 
+namespace {
+
+// rounds settled so far (and the undecided count after the last of them)
+inline uint32_t pub_round(const dv_ctx *c, uint32_t *und) {
+    const unsigned long long ru = __atomic_load_n(&c->h_pub->ru, __ATOMIC_ACQUIRE);
+    if (und) *und = (uint32_t)ru;
+    return (uint32_t)(ru >> 32);
+}
+
+// returns DV_OK, kTailDeclined when the tail launched at round tail_r0
+// declined, or an error
+constexpr int kTailDeclined = 1;
+int wait_published(dv_ctx *c, uint32_t target, uint32_t tail_r0) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const unsigned long long declined = ((unsigned long long)tail_r0 << 32) | 1u;
+    for (uint64_t i = 0;; i++) {
+        if (pub_round(c, nullptr) >= target) return DV_OK;
+        if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined) return kTailDeclined;
+        if ((i & 255) == 255) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {  // drained: the record must be there now
+                if (pub_round(c, nullptr) >= target) return DV_OK;
+                if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined)
+                    return kTailDeclined;
+                return DV_ERR_STATE;
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "round stream");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// Rounds are published by the NEXT round's pass, so kRoundsAhead >= 2 keeps
+// the round the host waits for always enqueued.
+// Once the published live count and undecided count fit the tail kernel's
+// LDS, the remaining rounds run in one single-workgroup launch (round_tail).
+}  // namespace
+
 // one decision round on this partition's accesses; writes this partition's
 // verdict byte per txn (bit1 abort, bit0 wait) into d_verdict (NULL = internal)
 int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
@@ -630,10 +673,41 @@ int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
 // apply verdicts combined over all partitions (MAX); returns undecided txns
 int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
     if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
-    if (c->rounds == 0) return DV_ERR_STATE;
-    round_apply(c->stream, round_bufs(c), c->n_txn, d_verdict ? d_verdict : c->verdict);
+    if (c->rounds == 0 || c->applied >= c->rounds) return DV_ERR_STATE;
+    const uint32_t tag = next_tag(c);
+    list_apply(c->stream, round_bufs(c), c->applied, c->und_ub, d_verdict ? d_verdict : c->verdict, tag,
+               next_ticket(c), c->d_pub);
     HIPCHK(hipGetLastError());
-    return round_sync(c, undecided, false);
+    c->applied++;
+    if (!undecided) return DV_OK;  // asynchronous: dv_epoch_round_wait reads the outcome
+    return dv_epoch_round_wait(c, c->applied - 1, undecided);
+}
+
+int dv_epoch_round_wait(dv_ctx *c, uint32_t round, uint32_t *undecided) {
+    if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN || round >= c->applied) return DV_ERR_STATE;
+    // the count log keeps the last kPubLog rounds enqueued
+    if (c->applied - round > RoundPub::kPubLog) return DV_ERR_STATE;
+    int r = wait_published(c, round + 1, 0);
+    if (r) {
+        (void)hipStreamSynchronize(c->stream);
+        c->phase = 0;
+        return r;
+    }
+    const uint32_t seen = pub_round(c, nullptr);
+    const uint32_t und = __atomic_load_n(&c->h_pub->und_log[round % RoundPub::kPubLog], __ATOMIC_ACQUIRE);
+    const unsigned long long le = __atomic_load_n(&c->h_pub->le, __ATOMIC_ACQUIRE);
+    r = err_from_bits((uint32_t)le);
+    if (r) {
+        (void)hipStreamSynchronize(c->stream);
+        c->phase = 0;
+        return r;
+    }
+    // bounds for the rounds enqueued from now on
+    c->und_ub = std::min(c->und_ub, und);
+    c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));
+    if (seen > c->rounds_real) c->rounds_real = seen;
+    if (undecided) *undecided = und;
+    return DV_OK;
 }
 
 int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
@@ -710,41 +784,6 @@ namespace {
 // past the fixpoint are no-ops.
 constexpr uint32_t kRoundsAhead = 2;
 
-// rounds settled so far (and the undecided count after the last of them)
-inline uint32_t pub_round(const dv_ctx *c, uint32_t *und) {
-    const unsigned long long ru = __atomic_load_n(&c->h_pub->ru, __ATOMIC_ACQUIRE);
-    if (und) *und = (uint32_t)ru;
-    return (uint32_t)(ru >> 32);
-}
-
-// returns DV_OK, kTailDeclined when the tail launched at round tail_r0
-// declined, or an error
-constexpr int kTailDeclined = 1;
-int wait_published(dv_ctx *c, uint32_t target, uint32_t tail_r0) {
-    const auto t0 = std::chrono::steady_clock::now();
-    const unsigned long long declined = ((unsigned long long)tail_r0 << 32) | 1u;
-    for (uint64_t i = 0;; i++) {
-        if (pub_round(c, nullptr) >= target) return DV_OK;
-        if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined) return kTailDeclined;
-        if ((i & 255) == 255) {
-            const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess) {  // drained: the record must be there now
-                if (pub_round(c, nullptr) >= target) return DV_OK;
-                if (tail_r0 && __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE) == declined)
-                    return kTailDeclined;
-                return DV_ERR_STATE;
-            }
-            if (q != hipErrorNotReady) return hip_fail(q, "round stream");
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
-        }
-        __builtin_ia32_pause();
-    }
-}
-
-// Rounds are published by the NEXT round's pass, so kRoundsAhead >= 2 keeps
-// the round the host waits for always enqueued.
-// Once the published live count and undecided count fit the tail kernel's
-// LDS, the remaining rounds run in one single-workgroup launch (round_tail).
 // The rounds queued ahead lag the published count by about two rounds, so the
 // tail is first tried at kTailTry (the live set shrinks ~2x per round pair
 // once it is that small); if it declines, the next try waits for a published

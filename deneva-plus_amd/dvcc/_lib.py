@@ -105,6 +105,7 @@ SIGNATURES = [
     ("dv_epoch_begin", ctypes.c_int, [_vp, _P(EpochDev), _vp]),
     ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),
+    ("dv_epoch_round_wait", ctypes.c_int, [_vp, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("dv_epoch_finish", ctypes.c_int, [_vp, _vp, _P(Stats)]),
     ("dv_round_log", ctypes.c_int, [_vp, _P(ctypes.c_uint32), _P(ctypes.c_uint32), ctypes.c_uint32]),
     ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,

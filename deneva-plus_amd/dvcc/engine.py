@@ -197,10 +197,19 @@ class CCEngine:
     def round_local(self, d_verdict):
         L.check(L.lib().dv_epoch_round_local(self._ctx, _ptr(d_verdict)), "dv_epoch_round_local")
 
-    def round_apply(self, d_verdict):
+    def round_apply(self, d_verdict, wait=True):
+        """Applies the combined verdicts; wait=False only enqueues the apply
+        (read its outcome with round_wait)."""
         und = ctypes.c_uint32()
-        L.check(L.lib().dv_epoch_round_apply(self._ctx, _ptr(d_verdict), ctypes.byref(und)),
+        L.check(L.lib().dv_epoch_round_apply(self._ctx, _ptr(d_verdict),
+                                             ctypes.byref(und) if wait else None),
                 "dv_epoch_round_apply")
+        return und.value if wait else None
+
+    def round_wait(self, r):
+        """Undecided txns after round r (or after a later, already applied one)."""
+        und = ctypes.c_uint32()
+        L.check(L.lib().dv_epoch_round_wait(self._ctx, r, ctypes.byref(und)), "dv_epoch_round_wait")
         return und.value
 
     def finish(self, d_commit=None):

@@ -13,9 +13,15 @@ GET_NODE_ID(part) == part, system/global.h:294).  Per epoch:
    global lock order (epoch, origin node, position) (work_queue.cpp:105-151),
    so the owner sorts them stably by row;
 4. NO_WAIT / WAIT_DIE / OCC: decision rounds; after each local round the
-   per-txn verdict bytes are combined with an all-reduce(MAX), which is the
-   vote combine of TxnManager::received_response (system/txn.cpp:544-554)
-   applied to every txn of the epoch at once; CALVIN needs no votes;
+   verdict bytes of the still-undecided txns are combined with an
+   all-reduce(MAX), which is the vote combine of TxnManager::received_response
+   (system/txn.cpp:544-554) applied to every open txn of the epoch at once;
+   CALVIN needs no votes.  Every rank holds the same statuses, hence the same
+   ascending list of undecided txns: the bytes travel in list order, so the
+   all-reduce shrinks with the list.  The host runs LAG rounds ahead of the
+   outcomes it reads (rounds past the fixpoint are no-ops), sizing each
+   all-reduce by the list length of LAG - 1 rounds earlier -- the same number
+   on every rank;
 5. every rank executes the committed accesses on its own rows.
 
 Decisions are identical to the single-thread E-schedule over the whole
@@ -62,6 +68,8 @@ class PartitionedRunner:
     """Runs epochs over `engine`, a CC engine bound to this rank's partition
     (CCEngine on the GPU; a test double on CPU)."""
 
+    LAG = 2  # rounds enqueued ahead of the outcome the host reads
+
     def __init__(self, engine, world, rank, group=None, device="cuda"):
         self.engine = engine
         self.world, self.rank, self.group = world, rank, group
@@ -94,17 +102,20 @@ class PartitionedRunner:
         rounds = 0
         if self.engine.needs_votes:
             verdict = torch.zeros((n_txn + 3) // 4 * 4, dtype=torch.uint8, device=self.device)
-            prev = n_txn + 1
-            while True:
+            counts = [n_txn]  # counts[k]: list length entering round k (known rounds)
+            r = 0
+            while counts[-1] > 0:
+                # round r's list is no longer than the last one known
                 self.engine.round_local(verdict)
-                dist.all_reduce(verdict, op=dist.ReduceOp.MAX, group=self.group)
-                rounds += 1
-                und = self.engine.round_apply(verdict)
-                if und == 0:
-                    break
-                if und >= prev:  # every round decides the lowest undecided txn
-                    raise RuntimeError(f"decision rounds stalled at {und} undecided txns")
-                prev = und
+                dist.all_reduce(verdict[:counts[-1]], op=dist.ReduceOp.MAX, group=self.group)
+                self.engine.round_apply(verdict, wait=False)
+                r += 1
+                if r >= self.LAG:
+                    und = self.engine.round_wait(r - self.LAG)
+                    if und >= counts[-1] > 0:  # every round decides the lowest undecided txn
+                        raise RuntimeError(f"decision rounds stalled at {und} undecided txns")
+                    counts.append(und)
+            rounds = len(counts) - 1
         st = self.engine.finish(commit)
         return st, rounds
 
@@ -127,8 +138,11 @@ class EnginePartition:
     def round_local(self, verdict):
         self.engine.round_local(verdict)
 
-    def round_apply(self, verdict):
-        return self.engine.round_apply(verdict)
+    def round_apply(self, verdict, wait=True):
+        return self.engine.round_apply(verdict, wait=wait)
+
+    def round_wait(self, r):
+        return self.engine.round_wait(r)
 
     def finish(self, commit=None):
         return self.engine.finish(commit)

@@ -195,12 +195,24 @@ int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32
 int dv_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, uint8_t *d_commit,
                         uint32_t *d_grant_group, dv_stats *st);
 
-/* staged form for partitioned (multi-GPU) epochs.  verdict vectors are device
- * byte arrays of n_txn entries (rounded up to a multiple of 4); bit1 = abort,
- * bit0 = wait; combine across partitions with an element-wise MAX. */
+/* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
+ * same txn statuses after each round, hence the same list of undecided txns
+ * (ascending).  dv_epoch_round_local writes this partition's verdict byte for
+ * every list entry, in list order, into d_verdict (a device byte array of
+ * n_txn entries, rounded up to a multiple of 4; bit1 = abort, bit0 = wait);
+ * combine the first U bytes across partitions with an element-wise MAX (U =
+ * the list length; any bound on it works, bytes past U are ignored) and hand
+ * the result to dv_epoch_round_apply.  Round 0's list is every txn; the list
+ * of round r + 1 has the length dv_epoch_round_wait(r) reports.
+ * dv_epoch_round_apply with undecided == NULL only enqueues the apply, so
+ * rounds can be queued ahead of their outcome (rounds past the fixpoint are
+ * no-ops); dv_epoch_round_wait(r) waits for round r's apply and reports the
+ * undecided count after it (or after a later round, if that one is already
+ * done -- never larger). */
 int dv_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t *d_grant_group);
 int dv_epoch_round_local(dv_ctx *ctx, uint8_t *d_verdict);
 int dv_epoch_round_apply(dv_ctx *ctx, const uint8_t *d_verdict, uint32_t *undecided);
+int dv_epoch_round_wait(dv_ctx *ctx, uint32_t round, uint32_t *undecided);
 int dv_epoch_finish(dv_ctx *ctx, uint8_t *d_commit, dv_stats *st);
 
 /* diagnostics: per decision round of the last finished epoch, the live

@@ -45,6 +45,8 @@ class NumpyPartition:
         self.seg = np.cumsum(head) - 1
         self.n_txn = n_txn
         self.status = np.zeros(n_txn, np.int8)
+        self.ulist = np.arange(n_txn)  # undecided txns, ascending
+        self.log = []                  # undecided count after each applied round
 
     def _first(self, mask):
         n = len(self.k)
@@ -66,14 +68,22 @@ class NumpyPartition:
             mine = u
             np.maximum.at(v, self.t[mine & wt & ~ab], 1)
             np.maximum.at(v, self.t[mine & ab], 2)
-        verdict.copy_(torch.from_numpy(v))
+        # list order: entry i is txn ulist[i]; bytes past the list are junk
+        out = np.full(verdict.numel(), 0xEE, np.uint8)
+        out[:len(self.ulist)] = v[self.ulist]
+        verdict.copy_(torch.from_numpy(out))
 
-    def round_apply(self, verdict):
-        v = verdict.numpy()[:self.n_txn]
-        und = self.status == 0
-        self.status[und & ((v & 2) != 0)] = 2
-        self.status[und & (v == 0)] = 1
-        return int((self.status == 0).sum())
+    def round_apply(self, verdict, wait=True):
+        v = verdict.numpy()[:len(self.ulist)]
+        lst = self.ulist
+        self.status[lst[(v & 2) != 0]] = 2
+        self.status[lst[v == 0]] = 1
+        self.ulist = lst[self.status[lst] == 0]
+        self.log.append(len(self.ulist))
+        return self.log[-1] if wait else None
+
+    def round_wait(self, r):
+        return self.log[r]
 
     def finish(self, commit=None):
         if commit is not None:
