@@ -216,6 +216,8 @@ def main():
         "abort_rate": 1.0 - committed / max(1, txns),
         "decided_txns_per_s": txns / el,
         "rounds_mean": float(np.mean([s.rounds for s in stats])),
+        "async_tries": {"launches": int(sum(s.async_launches for s in stats)),
+                        "declined": int(sum(s.async_declined for s in stats)), "epochs": len(stats)},
         "stage_ms_mean": {k: float(np.mean([getattr(s, k) for s in stats]))
                           for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")},
         "gen_seconds": t_gen,

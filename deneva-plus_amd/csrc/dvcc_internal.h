@@ -65,9 +65,10 @@ struct alignas(128) CtrSlot {
 };
 struct Counters {
     uint32_t err;         // ERRB_* bits of every failure seen
-    uint32_t pad2;
+    uint32_t async_go;        // the last asynchronous try: 1 ran, 2 declined, 0 nothing to do
     uint32_t async_iters;     // most iterations any asynchronous workgroup ran
-    uint32_t pad1;
+    uint32_t async_r0;        // round the accepted asynchronous launch started at (0: none)
+    uint32_t async_declined;  // asynchronous tries that found the live set too large
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
     uint32_t log_live[kRoundLog];  // per round: live accesses entering it
@@ -182,12 +183,17 @@ uint32_t tail_cap(bool el32);  // live accesses the tail holds in LDS
 // single GPU, 32-bit elements: every remaining decision from round r0 >= 1 in
 // one multi-workgroup launch without grid barriers, then the status bytes of
 // every txn (undecided leftovers -- an error -- counted in the slots'
-// `undecided`); carry: kAsyncGroups words of scratch.  Needs the live
-// accesses entering round r0 <= async_try_limit().
+// `undecided`); carry: kAsyncGroups words of scratch.  The launch is a try,
+// decided on the device: it runs when some txn is undecided, no earlier try
+// ran, and the live accesses entering round r0 are at most `thresh` (and fit
+// its workgroups, async_try_limit()); then it zeroes round r0's undecided
+// count, so the passes queued behind it are no-ops that publish "0
+// undecided".  A try that finds the live set too large changes nothing and
+// publishes pub->tl = r0 << 32 | 2 (declined); the rounds go on.
 constexpr uint32_t kAsyncGroups = 512;
 // tword: one 32-bit fact word per txn (scratch, n_txn words)
-void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G,
-                 uint32_t *carry, uint32_t *tword, uint32_t n_txn);
+void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub);
 uint32_t async_groups(int device);  // co-resident workgroups (<= kAsyncGroups; 0: unusable)
 uint32_t async_try_limit(uint32_t G);
 // round elements ((txn << slog | pos) << 3 | flags) fit 32 bits

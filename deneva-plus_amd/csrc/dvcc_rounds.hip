@@ -102,15 +102,17 @@ __device__ __forceinline__ RAgg wave_incl_rev(RAgg p, uint32_t lane) {
 // undecided txn) followed in its queue by a needy element.  Each thread holds
 // IPT consecutive elements; nhm bit j = the element after j starts a queue.
 // `far` describes what follows the last thread's chunk.  Returns keep bits.
-template <int IPT, int WAVES>
-__device__ __forceinline__ uint32_t keep_bits(int cnt, uint32_t nhm, uint32_t needy, uint32_t blk,
-                                              RAgg *rw, RAgg far, uint32_t lane, uint32_t wave) {
-    const uint32_t valid = cnt >= 32 ? 0xFFFFFFFFu : ((1u << cnt) - 1u);
+template <int IPT, int WAVES, class M = uint32_t>
+__device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw, RAgg far, uint32_t lane,
+                                       uint32_t wave) {
+    constexpr int kBits = 8 * (int)sizeof(M);
+    const M valid = cnt >= kBits ? ~(M)0 : (((M)1 << cnt) - 1);
     RAgg x{0u, 0u};  // a thread past the end is transparent: `far` reaches the last element
     if (cnt > 0) {
-        const uint32_t cuts = nhm & valid;
+        const M cuts = nhm & valid;
         x.f = cuts != 0;
-        const uint32_t upto = cuts ? ((2u << __builtin_ctz(cuts)) - 1u) : valid;
+        const int c0 = sizeof(M) == 8 ? __builtin_ctzll((uint64_t)cuts) : __builtin_ctz((uint32_t)cuts);
+        const M upto = cuts ? (c0 + 1 >= kBits ? ~(M)0 : (((M)2 << c0) - 1)) : valid;
         x.v = (needy & upto) != 0;
     }
     const RAgg inc_r = wave_incl_rev(x, lane);
@@ -122,13 +124,13 @@ __device__ __forceinline__ uint32_t keep_bits(int cnt, uint32_t nhm, uint32_t ne
     __syncthreads();
     for (int w = WAVES - 1; w > (int)wave; w--) far = rcomb(rw[w], far);
     uint32_t r = rcomb(ex_r, far).v;  // needy after my last element, same queue
-    uint32_t keep = 0;
+    M keep = 0;
 #pragma unroll
     for (int j = IPT - 1; j >= 0; j--) {
         if (j < cnt) {
             const uint32_t after = ((nhm >> j) & 1u) ? 0u : r;
-            const uint32_t nd = (needy >> j) & 1u;
-            keep |= (((blk >> j) & 1u) & (nd | after)) << j;
+            const uint32_t nd = (uint32_t)(needy >> j) & 1u;
+            keep |= (M)(((uint32_t)(blk >> j) & 1u) & (nd | after)) << j;
             r = after | nd;
         }
     }
@@ -401,18 +403,6 @@ __device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, ui
         }
     }
     return any_abort ? V_ABORT : (all_ok ? 0 : V_WAIT);
-}
-
-__device__ __forceinline__ void block_count(uint32_t und, Counters *ctr) {
-    __shared__ uint32_t part[4];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) und += __shfl_down(und, off, 64);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = und;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t t = part[0] + part[1] + part[2] + part[3];
-        if (t) atomicAdd(&my_slot(ctr).undecided, t);
-    }
 }
 
 // Walks the undecided-txn list (round 0: every txn) and writes the survivors
@@ -769,7 +759,13 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
 // decide, so every workgroup leaves (bounded spin: ERRB_SPIN).
 constexpr int kAsyncThreads = 512;
 constexpr int kAsyncWaves = kAsyncThreads / 64;
-constexpr int kAsyncIPT = 24;
+// 28 elements per thread (128 VGPRs, two workgroups per CU): 7.3M live
+// accesses chip-wide.  Measured on a 1M-txn zipf-0.9 epoch, the launch pays
+// off once the live set has halved: from round 1 (9.2M live) it took 570 us,
+// more than the synchronous rounds it replaces -- every iteration re-reads
+// the facts of every live access, and while the queues are long a slice
+// iterates many times per round's worth of progress.
+constexpr int kAsyncIPT = 28;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
 constexpr uint32_t kAsyncMaxIters = 1u << 18;
 constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP;  // "undecided blockers in front"
@@ -786,13 +782,27 @@ __device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t
     return word_status(__hip_atomic_load(tword + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
+// the try's verdict from its inputs, which no kernel of the try changes:
+// 1 run, 2 declined (the live set exceeds thresh or does not fit the
+// workgroups -- equal slices, the largest holds ceil(n / G)), 0 nothing to
+// do (no txn undecided, or an earlier try ran)
+__device__ __forceinline__ uint32_t async_gate(const Counters *ctr, uint32_t r0, uint32_t G,
+                                               uint32_t thresh) {
+    if (ctr->async_r0 != 0 || ctr->nund[r0 & 1] == 0) return 0u;
+    const uint32_t n_all = ctr->nlive[r0 & 1];
+    return n_all <= thresh && ((uint64_t)n_all + G - 1) / G <= kAsyncCap ? 1u : 2u;
+}
+
 // the words from the synchronous rounds' state (status byte, OK verdict
 // bytes), and every carry word pessimistic
 __global__ __launch_bounds__(kBlock) void k_async_words(const uint8_t *__restrict__ status,
                                                         const uint8_t *__restrict__ vb8, uint32_t slog,
                                                         const uint8_t *__restrict__ tlen, uint32_t n_txn,
                                                         uint32_t *__restrict__ tword,
-                                                        uint32_t *__restrict__ carry, uint32_t G) {
+                                                        uint32_t *__restrict__ carry, uint32_t G,
+                                                        uint32_t thresh, uint32_t r0,
+                                                        const Counters *__restrict__ ctr) {
+    if (async_gate(ctr, r0, G, thresh) != 1u) return;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t g = i0; g < G; g += gridDim.x * blockDim.x) carry[g] = kCarryInit;
     for (uint32_t t = i0; t < n_txn; t += gridDim.x * blockDim.x) {
@@ -815,11 +825,19 @@ __global__ __launch_bounds__(kBlock) void k_async_words(const uint8_t *__restric
     }
 }
 
+// per-element scan value from the element and its txn's status bits
+__device__ __forceinline__ uint32_t async_value(uint32_t e, bool undec, bool abort, int nowait) {
+    if (abort) return 0u;
+    const bool wr = (e & F_WR) != 0;
+    return undec ? ((nowait ? B_UA : 0u) | (wr ? B_UW : 0u)) : ((nowait ? B_CA : 0u) | (wr ? B_CW : 0u));
+}
+
 __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
-                                                               const uint32_t *n_in, uint32_t *tword,
-                                                               uint32_t *carry, int nowait,
-                                                               uint32_t max_iters) {
+                                                               uint32_t r0, uint32_t thresh,
+                                                               uint32_t *tword, uint32_t *carry,
+                                                               int nowait, uint32_t max_iters) {
     constexpr int IPT = kAsyncIPT;
+    using M = uint32_t;  // per-thread element bit masks
     __shared__ uint32_t sel[kAsyncCap];
     __shared__ RAgg rw[kAsyncWaves];
     __shared__ Agg wt[kAsyncWaves];
@@ -830,13 +848,12 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     Counters *ctr = b.ctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
-    const uint32_t n_all = *n_in;
+    const uint32_t go = async_gate(ctr, r0, G, thresh);
+    if (g == 0 && tid == 0) ctr->async_go = go;  // for the finalize (the gate's inputs change there)
+    if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
+    const uint32_t n_all = ctr->nlive[r0 & 1];
     const uint32_t lo = (uint32_t)((uint64_t)g * n_all / G), hi = (uint32_t)((uint64_t)(g + 1) * n_all / G);
     uint32_t n = hi - lo;
-    if (n > kAsyncCap) {  // the host launches only when every slice fits
-        if (tid == 0) set_err(ctr, ERRB_BIG);
-        return;
-    }
     // does a queue run in from the previous slice / out into the next one?
     const bool cont_in = lo > 0 && lo < n_all && !(src[lo] & F_HEAD);
     const bool cont_out = hi < n_all && !(src[hi] & F_HEAD);
@@ -852,43 +869,44 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         const uint32_t k = (n + kAsyncThreads - 1) / kAsyncThreads;
         const uint32_t first = tid * k;
         const int cnt = first >= n ? 0 : (int)(n - first < k ? n - first : k);
-        uint32_t e[IPT], v[IPT];
+        uint32_t e[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; j++) e[j] = j < cnt ? sel[first + j] : F_HEAD;
         const uint32_t nxt = first + (uint32_t)cnt < n ? sel[first + cnt] : (cont_out ? 0u : F_HEAD);
-        uint32_t nhm = 0, umask = 0, needy = 0, blk = 0;
+        M nhm = 0, umask = 0, amask = 0, needy = 0, blk = 0;
 #pragma unroll
         for (int j = 0; j < IPT; j++) {
-            v[j] = 0;
             if (j < cnt) {
                 const bool nh = j + 1 < cnt ? (e[j + 1] & F_HEAD) != 0 : (nxt & F_HEAD) != 0;
-                nhm |= (nh ? 1u : 0u) << j;
+                nhm |= (M)(nh ? 1u : 0u) << j;
                 const uint8_t s = fact_status(tword, r_txn(e[j], slog));
-                umask |= (s == ST_UNDEC ? 1u : 0u) << j;
-                needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
+                umask |= (M)(s == ST_UNDEC ? 1u : 0u) << j;
+                amask |= (M)(s == ST_ABORT ? 1u : 0u) << j;
+                needy |= (M)(s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
                 const bool single = (e[j] & F_HEAD) && nh;
-                blk |= (s != ST_ABORT && !single ? 1u : 0u) << j;
-                v[j] = elem_value(e[j], s, nowait);
+                blk |= (M)(s != ST_ABORT && !single ? 1u : 0u) << j;
             }
         }
         // a queue running into the next slice is assumed to be followed by a
         // needy element there (keep_bits holds a barrier: every thread is done
         // with slot p ^ 1 of the previous iteration)
-        uint32_t keep = keep_bits<IPT, kAsyncWaves>(cnt, nhm, needy, blk, rw,
-                                                    RAgg{1u, cont_out ? 1u : 0u}, lane, wave);
+        M keep = keep_bits<IPT, kAsyncWaves, M>(cnt, nhm, needy, blk, rw, RAgg{1u, cont_out ? 1u : 0u},
+                                                lane, wave);
         // ... and the slice's last element anchors that queue here: it is kept
         // whatever its txn, so the carry is always the OR of that queue (were
         // the queue's elements all dropped, the last head would be an
         // earlier queue's)
-        if (cont_out && cnt > 0 && first + (uint32_t)cnt == n) keep |= 1u << (cnt - 1);
+        if (cont_out && cnt > 0 && first + (uint32_t)cnt == n) keep |= (M)1 << (cnt - 1);
         if (tid == 0) { s_needy[p ^ 1u] = 0; s_moved[p ^ 1u] = 0; }
-        if (needy) atomicAdd(&s_needy[p], (uint32_t)__builtin_popcount(needy));
+        if (needy) atomicAdd(&s_needy[p], (uint32_t)__popcll(needy));
         Agg a{0u, 0u, 0u};
 #pragma unroll
         for (int j = 0; j < IPT; j++) {
             if (j < cnt) {
-                if ((keep >> j) & 1u) v[j] |= B_KEEP;
-                a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & F_HEAD) != 0), v[j], (keep >> j) & 1u});
+                const uint32_t kj = (uint32_t)(keep >> j) & 1u;
+                const uint32_t vj = async_value(e[j], (umask >> j) & 1u, (amask >> j) & 1u, nowait) |
+                                    (kj ? B_KEEP : 0u);
+                a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & F_HEAD) != 0), vj, kj});
             }
         }
         const Agg inc = wave_incl<OpPlain>(a, lane);
@@ -907,6 +925,9 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
                 uint32_t ej = e[j];
                 const bool head = (ej & F_HEAD) != 0;
                 const uint32_t excl = head ? 0u : run;
+                const uint32_t kj = (uint32_t)(keep >> j) & 1u;
+                const uint32_t vj = async_value(ej, (umask >> j) & 1u, (amask >> j) & 1u, nowait) |
+                                    (kj ? B_KEEP : 0u);
                 if (((umask >> j) & 1u) && !(ej & F_DONE)) {
                     const uint32_t sl = (nowait && (ej & F_WR)) ? (excl & (B_CA | B_UA))
                                                                 : ((excl >> 2) & (B_CA | B_UA));
@@ -921,8 +942,8 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
                 }
                 // the slice's first element never becomes a head when a queue
                 // runs in: what is in front of it arrives through the carry
-                if (v[j] & B_KEEP) sel[lpos++] = (ej & ~F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD);
-                run = head ? v[j] : (run | v[j]);
+                if (kj) sel[lpos++] = (ej & ~F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD);
+                run = head ? vj : (run | vj);
             }
         }
         if (moved) s_moved[p] = 1;
@@ -943,12 +964,27 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     }
 }
 
-// after the asynchronous rounds: the status bytes from the words (a declined
-// launch leaves undecided txns; their OKs are recomputed by the rounds that
-// resume) and the count of txns left undecided
+// after the asynchronous rounds: the status bytes from the words and the
+// count of txns left undecided (an error).  A declined launch changes nothing
+// and says so through pub->tl = r0 << 32 | 2.
 __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__ status,
                                                            const uint32_t *__restrict__ tword,
-                                                           uint32_t n_txn, Counters *ctr) {
+                                                           uint32_t n_txn, uint32_t r0, RoundPub *pub,
+                                                           Counters *ctr) {
+    const uint32_t go = ctr->async_go;
+    if (go != 1u) {
+        if (go == 2u && blockIdx.x == 0 && threadIdx.x == 0) {
+            ctr->async_declined++;
+            if (pub)
+                __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 2u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctr->async_r0 = r0;
+        ctr->nund[r0 & 1] = 0;  // the passes queued behind the try are no-ops
+    }
     uint32_t und = 0;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
         const uint8_t s = word_status(tword[t]);
@@ -1025,14 +1061,14 @@ void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, Roun
     else k_round_tail<uint64_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
 }
 
-void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G,
-                 uint32_t *carry, uint32_t *tword, uint32_t n_txn) {
+void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
     k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
-                                                                    n_txn, tword, carry, G);
-    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, &b.ctr->nlive[r0 & 1], tword, carry, nowait,
-                                              kAsyncMaxIters);
-    if (n_txn) k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, b.ctr);
+                                                                    n_txn, tword, carry, G, thresh, r0,
+                                                                    b.ctr);
+    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, kAsyncMaxIters);
+    k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, r0, pub, b.ctr);
 }
 
 // Every workgroup of the asynchronous launch must be resident at once (one

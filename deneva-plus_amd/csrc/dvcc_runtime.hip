@@ -92,6 +92,8 @@ struct dv_ctx {
     hipEvent_t pev[2 * kRoundLog] = {};  // around each decision-round pass
     uint32_t passes = 0;                 // pass launches this epoch
     uint32_t applied = 0;                // partitioned rounds applied this epoch
+    uint32_t async_launched = 0;         // asynchronous-round tries this epoch
+    uint32_t async_hint = 0;             // round the last epoch's asynchronous launch ran at
     float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
 };
 
@@ -542,6 +544,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->rounds_real = 0;
     c->passes = 0;
     c->applied = 0;
+    c->async_launched = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
@@ -601,22 +604,6 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     if (settle) round_settle(c->stream, b, r, c->n_txn, c->und_ub);
     else list_verdict(c->stream, b, r, c->und_ub, d_verdict);
     c->rounds++;
-}
-
-// read the counters after the last enqueued round
-// (settle: single-GPU rounds, the undecided count is the list length)
-int round_sync(dv_ctx *c, uint32_t *undecided, bool settle) {
-    int r = sync_counters(c);
-    if (r) return r;
-    r = err_from_bits(c->h_ctr->err);
-    if (r) { c->phase = 0; return r; }
-    c->live_ub = c->h_ctr->nlive[c->rounds & 1];  // input size of the next round
-    uint32_t und = 0;
-    if (settle) und = c->h_ctr->nund[c->rounds & 1];
-    else for (const CtrSlot &sl : c->h_ctr->slot) und += sl.undecided;
-    c->und_ub = und;
-    if (undecided) *undecided = und;
-    return DV_OK;
 }
 
 }  // namespace
@@ -728,6 +715,13 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     if (r) return r;
     r = err_from_bits(c->h_ctr->err);
     if (r) return r;
+    if (!calvin && c->h_ctr->async_r0) {  // an asynchronous launch decided the rest
+        uint32_t left = 0;
+        for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
+        if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
+        c->rounds_real = c->h_ctr->async_r0 + c->h_ctr->async_iters;
+    }
+    c->async_hint = calvin ? c->async_hint : c->h_ctr->async_r0;
     if (st) {
         std::memset(st, 0, sizeof(*st));
         st->n_txn = c->n_txn;
@@ -744,6 +738,8 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         st->read_digest = dig;
         st->rounds = calvin ? 0 : (c->rounds_real ? c->rounds_real : c->rounds);
         st->sort_passes = c->sort_passes;
+        st->async_launches = (uint16_t)std::min(c->async_launched, 0xFFFFu);
+        st->async_declined = (uint16_t)std::min(c->h_ctr->async_declined, 0xFFFFu);
         if (timing(c)) {
             st->ms_probe = elapsed(c, 0, 1);
             st->ms_sort = elapsed(c, 1, 2);
@@ -789,6 +785,31 @@ constexpr uint32_t kRoundsAhead = 2;
 // once it is that small); if it declines, the next try waits for a published
 // count that fits outright.
 constexpr uint32_t kTailTryFactor = 4;
+
+// The asynchronous launch (round_async) takes over once the published live
+// count is at most kAsyncLiveFrac of the epoch's accesses (and fits its
+// workgroups); the passes already queued behind it become no-ops.  Launching
+// earlier does not pay: every asynchronous iteration re-reads the facts of
+// its whole slice, so while the live set is large it costs more than the
+// synchronous rounds it replaces (1M-txn zipf-0.9 epoch: 570 us from round
+// 1, 240 us from round 3, 153 us from round 5 after 107 us of rounds 3-4).
+// The launch is a device-decided try (round_async), so speculative tries
+// queued behind passes are possible (kAsyncSpeculate); they lost ~40 us of
+// empty launches and no-op passes for ~20 us gained, and are off.
+constexpr double kAsyncLiveFrac = 0.5;
+constexpr bool kAsyncSpeculate = false;
+
+uint32_t async_thresh(dv_ctx *c) {
+    const uint64_t frac = (uint64_t)(kAsyncLiveFrac * (double)c->n_acc);
+    return (uint32_t)std::min<uint64_t>(frac, async_try_limit(c->async_g));
+}
+
+void async_try(dv_ctx *c, uint32_t r0) {
+    c->async_launched++;
+    round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, async_thresh(c),
+                c->abounds, c->tword, c->n_txn, c->d_pub);
+}
+
 int run_rounds(dv_ctx *c) {
     __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
@@ -796,9 +817,14 @@ int run_rounds(dv_ctx *c) {
     uint32_t tail_r0 = 0;             // round the pending tail launch starts at (0: none)
     const uint32_t cap = tail_cap(c->el32);
     uint32_t tail_limit = kTailTryFactor * cap;  // published live count that triggers a try
-    bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
+    const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
+    // speculative tries start one round before the previous epoch's launch
+    const uint32_t try_from = !kAsyncSpeculate ? ~0u : (c->async_hint > 1 ? c->async_hint - 1 : 1);
     for (;;) {
-        while (!tail_r0 && c->rounds < seen + kRoundsAhead + 1) enqueue_round(c, nullptr, true);
+        while (!tail_r0 && c->rounds < seen + kRoundsAhead + 1) {
+            enqueue_round(c, nullptr, true);
+            if (async && c->rounds >= try_from) async_try(c, c->rounds);
+        }
         int r = hip_fail(hipGetLastError(), "round launch");
         if (!r) r = wait_published(c, seen + 1, tail_r0);
         if (r == kTailDeclined) {
@@ -819,7 +845,7 @@ int run_rounds(dv_ctx *c) {
             (void)hipStreamSynchronize(c->stream);
             return r;
         }
-        if (und == 0) {
+        if (und == 0) {  // (after an asynchronous launch: dv_epoch_finish counts its rounds)
             c->rounds_real = seen;
             c->rounds = std::max(c->rounds, seen);
             return DV_OK;
@@ -827,20 +853,17 @@ int run_rounds(dv_ctx *c) {
         prev = und;
         c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));  // bounds for rounds not yet enqueued
         c->und_ub = und;
-        if (async && !tail_r0 && c->live_ub <= async_try_limit(c->async_g)) {
-            // every remaining decision in one asynchronous launch (round_async)
-            const uint32_t r0 = c->rounds;
-            round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, c->abounds,
-                        c->tword, c->n_txn);
+        if (async && !tail_r0 && c->live_ub <= async_thresh(c)) {
+            // the try behind the last queued pass qualifies (unless an
+            // earlier one ran): wait for it and the no-op passes behind it
+            if (c->rounds < try_from) async_try(c, c->rounds);
             r = sync_counters(c);
             if (!r) r = err_from_bits(c->h_ctr->err);
-            if (r) return r;
-            uint32_t left = 0;
-            for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
-            if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
-            c->rounds_real = r0 + c->h_ctr->async_iters;
-            c->rounds = std::max(c->rounds, r0);
-            return DV_OK;
+            if (!r && c->h_ctr->async_go == 2u) r = DV_ERR_STATE;  // cannot happen: the count fits
+            if (r || c->h_ctr->async_r0) return r;
+            // nothing left to decide by round c->rounds: the passes have
+            // published it (or the next one will)
+            continue;
         }
         if (!tail_r0 && !(c->cfg.flags & DV_FLAG_NO_TAIL) && c->live_ub <= tail_limit) {
             tail_r0 = c->rounds;

@@ -67,7 +67,8 @@ class Stats(ctypes.Structure):
                 ("ms_sort", ctypes.c_float), ("ms_decide", ctypes.c_float),
                 ("ms_exec", ctypes.c_float), ("ms_scatter", ctypes.c_float),
                 ("scatter_launches", ctypes.c_uint32), ("pass_launches", ctypes.c_uint32),
-                ("ms_pass", ctypes.c_float), ("reserved", ctypes.c_uint32),
+                ("ms_pass", ctypes.c_float), ("async_launches", ctypes.c_uint16),
+                ("async_declined", ctypes.c_uint16),
                 ("pass_live", ctypes.c_uint64)]
 
     def as_dict(self):

@@ -146,7 +146,8 @@ typedef struct dv_stats {
     uint32_t scatter_launches;
     uint32_t pass_launches;  /* decision-round pass launches (k_round_pass)    */
     float ms_pass;           /* sum over those launches                        */
-    uint32_t reserved;
+    uint16_t async_launches; /* asynchronous-round launches (accepted or not)  */
+    uint16_t async_declined; /* ... that found the live set too large          */
     uint64_t pass_live;      /* live accesses those launches read, summed      */
 } dv_stats;
 

@@ -1,11 +1,9 @@
 set -e
-T=gpurun_out/exp1
+# experiment variants: tools/gpu_exp.sh <tag> <variant>...  (exp_build/<variant>/libdvcc.so)
+T=gpurun_out/$1
+shift
 mkdir -p $T
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $T/pytest.log 2>&1 || { tail -40 $T/pytest.log; exit 1; }
-tail -1 $T/pytest.log
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > $T/bench.json 2> $T/bench.err
-head -c 600 $T/bench.json; echo
-for n in base tick nolb nogather nodecide all; do
-  DVCC_LIB=$PWD/exp_build/$n/libdvcc.so timeout -k 10 120 rocprofv3 --kernel-trace -f csv -T -d $T/$n -o run -- python3 tools/exp_pass.py > $T/$n.log 2>&1
-  tail -1 $T/$n.log
+for n in "$@"; do
+  DVCC_LIB=$PWD/exp_build/$n/libdvcc.so timeout -k 10 120 python3 -u bench.py --no-cpu-baseline --steps 10 > $T/$n.json 2> $T/$n.err
+  python3 -c "import json,sys; d=json.load(open('$T/$n.json')); print('$n', round(d['ms_per_step'],4), d['stage_ms_mean'])"
 done
