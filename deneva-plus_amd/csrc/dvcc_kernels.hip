@@ -218,14 +218,22 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
         const uint64_t idx = base + j * 64 + lane;
         k[j] = idx < n ? in[idx] : 0;
     }
+    // counts only: one LDS atomic per key into the wave's own histogram (the
+    // ballot multisplit that ranks keys in the scatter costs 8 ballots each)
+    // (a step whose keys all share one digit -- hot rows, high digits of
+    // small row ids -- adds once instead of 64 times to one LDS word)
 #pragma unroll
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
         const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
         const uint64_t vmask = __ballot(valid);
-        const uint64_t peers = match_digit(d, vmask);
-        if (valid && lane == (uint32_t)__builtin_ctzll(peers)) wc[wave][d] += (uint32_t)__popcll(peers);
+        if (__ballot(valid && d == d0) == vmask) {
+            if (lane == 0) wc[wave][d0] += (uint32_t)__popcll(vmask);
+        } else if (valid) {
+            atomicAdd(&wc[wave][d], 1u);
+        }
     }
     __syncthreads();
     for (uint32_t d = tid; d < kRadix; d += kBlock)
