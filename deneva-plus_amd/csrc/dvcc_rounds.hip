@@ -141,15 +141,32 @@ __device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw,
 
 // ---- one tile of a decision round (single-pass OpPlain scan: v = status
 //      bits OR-ed along the row queue, c = kept accesses -> compaction offset)
-// Tile geometry follows the input width: 512 threads x 16 32-bit elements, or
-// 256 threads x 16 64-bit elements (round 0's pairs, or 64-bit elements);
-// 16 elements per thread, the LDS image padded one slot per 16.
+// Tile geometry follows the input width: 1024 threads x 16 32-bit elements,
+// or 512 threads x 16 64-bit elements (round 0's pairs, or 64-bit elements);
+// 16 elements per thread, the LDS image padded one slot per 16.  Large tiles
+// keep the look-back short: the tiles dispatched together all publish their
+// aggregates at about the same time and each walks back to the nearest
+// inclusive prefix, 64 descriptors per step (config D: 16K/8K-element tiles
+// took 2.5 % less epoch time than 8K/4K, 4K/4K took 3 % more).
+// DVCC_EXP_* override the geometry for experiments (tools/gpu_exp.sh).
+#ifndef DVCC_EXP_T32
+#define DVCC_EXP_T32 1024
+#endif
+#ifndef DVCC_EXP_IPT
+#define DVCC_EXP_IPT 16
+#endif
+#ifndef DVCC_EXP_MW32
+#define DVCC_EXP_MW32 4
+#endif
+#ifndef DVCC_EXP_T64
+#define DVCC_EXP_T64 512
+#endif
 template <class EIn>
 struct Geo {
-    static constexpr int kThreads = sizeof(EIn) == 4 ? 512 : 256;
-    static constexpr int kMinWaves = sizeof(EIn) == 4 ? 4 : 3;  // per SIMD: <= 128 / 168 VGPRs
+    static constexpr int kThreads = sizeof(EIn) == 4 ? DVCC_EXP_T32 : DVCC_EXP_T64;
+    static constexpr int kMinWaves = sizeof(EIn) == 4 ? DVCC_EXP_MW32 : 3;  // per SIMD: <= 128 / 168 VGPRs
     static constexpr int kWaves = kThreads / 64;
-    static constexpr int kIPT = 16;
+    static constexpr int kIPT = sizeof(EIn) == 4 ? DVCC_EXP_IPT : 16;
     static constexpr uint32_t kTile = kThreads * kIPT;
 };
 __device__ __forceinline__ uint32_t pad16(uint32_t j) { return j + (j >> 4); }
