@@ -35,7 +35,9 @@ __device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint6
     const TableDesc &t = tabs.t[tb];
     const uint64_t bk = bucket_of(t, key);
     bool found = false;
-    if (t.bstart == nullptr) {                // YCSB: one key per bucket
+    if (t.pkey != nullptr) {                  // direct map, local row = bucket
+        if (t.pkey[bk] == key) { row = bk; found = true; }
+    } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
         const IxEntry e = t.ix[bk];
         if (e.key == key) { row = e.row; found = true; }
     } else {                                  // chained bucket (read_item 217-231)
@@ -719,21 +721,21 @@ void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uin
 // ------------------------------------------------------------- loaders
 // YCSBWorkload::init_table_slice (ycsb_wl.cpp:144-203) for one partition:
 // local row r holds key r*P + part; F0 = "hello\0" + key bytes 6..7 (H3);
-// YCSB bucket (key/P) % rows == r, so the index is a direct map.
+// YCSB bucket (key/P) % rows == r, so the index is a direct map with local
+// row == bucket: an implicit-row map over the pkey column (TableDesc::pkey).
 __global__ void k_ycsb_load(uint64_t rows, uint32_t part_cnt, uint32_t part_id, uint64_t *f0,
-                            uint64_t *pkey, IxEntry *ix) {
+                            uint64_t *pkey) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
         const uint64_t key = r * part_cnt + part_id;
         f0[r] = 0x00006F6C6C6568ull | (key & 0xFFFF000000000000ull);
         pkey[r] = key;
-        ix[r] = IxEntry{key, r};
     }
 }
 
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
-                      uint64_t *f0, uint64_t *pkey, IxEntry *ix) {
-    k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey, ix);
+                      uint64_t *f0, uint64_t *pkey) {
+    k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey);
 }
 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,

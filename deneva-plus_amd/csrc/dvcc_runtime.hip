@@ -24,6 +24,7 @@ namespace {
 
 struct HostTable {
     bool created = false, loaded = false;
+    bool implicit_rows = false;  // direct map with local row == bucket: probes read pkey
     uint64_t cap_rows = 0, n_rows = 0, nbuckets = 0, row_base = 0;
     uint32_t hash_kind = DV_HASH_YCSB;
     IxEntry *ix = nullptr;      // device
@@ -176,6 +177,7 @@ Tables make_tables(dv_ctx *c) {
         if (!h.created) continue;
         t.n = i + 1;
         t.t[i].ix = h.ix;
+        t.t[i].pkey = h.implicit_rows ? c->pkey + h.row_base : nullptr;
         t.t[i].bstart = h.bstart;
         t.t[i].nbuckets = h.nbuckets ? h.nbuckets : 1;
         t.t[i].row_base = h.row_base;
@@ -426,13 +428,17 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
     dfree(t.bstart);
     t.ix = nullptr;
     t.bstart = nullptr;
-    int r = dalloc(&t.ix, direct ? nb : (n ? n : 1));
+    // keys in bucket order: row b is in bucket b, the pkey column is the index
+    bool implicit = direct;
+    for (uint64_t b = 0; b < nb && implicit; b++) implicit = ent[cnt[b]].row == b;
+    t.implicit_rows = implicit;
+    int r = implicit ? DV_OK : dalloc(&t.ix, direct ? nb : (n ? n : 1));
     if (r) return r;
-    if (direct) {
+    if (direct && !implicit) {
         std::vector<IxEntry> d(nb);
         for (uint64_t b = 0; b < nb; b++) d[b] = ent[cnt[b]];
         HIPCHK(hipMemcpy(t.ix, d.data(), nb * sizeof(IxEntry), hipMemcpyHostToDevice));
-    } else {
+    } else if (!direct) {
         r = dalloc(&t.bstart, nb + 1);
         if (r) return r;
         if (n) HIPCHK(hipMemcpy(t.ix, ent.data(), n * sizeof(IxEntry), hipMemcpyHostToDevice));
@@ -459,11 +465,11 @@ int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
     HIPCHK(hipSetDevice(c->cfg.device));
     dfree(t.ix);
     dfree(t.bstart);
+    t.ix = nullptr;
     t.bstart = nullptr;
-    int r = dalloc(&t.ix, rows_per_part);
-    if (r) return r;
+    t.implicit_rows = true;  // row r holds key r * P + part, in bucket r
     launch_ycsb_load(c->stream, rows_per_part, c->cfg.part_cnt, c->cfg.part_id, c->f0 + t.row_base,
-                     c->pkey + t.row_base, t.ix);
+                     c->pkey + t.row_base);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     t.n_rows = rows_per_part;
