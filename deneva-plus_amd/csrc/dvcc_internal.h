@@ -206,8 +206,11 @@ uint32_t async_try_limit(uint32_t G);
 bool round_el32(uint32_t n_txn, uint32_t slog);
 
 // ---- execution and outputs (dvcc_kernels.hip)
-void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4,
-                        uint8_t value);
+// per-epoch reset: counters, tile tickets, status (value; padding aborted),
+// access ranges and counts
+void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
+                        uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
+                        Counters *ctr);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,

@@ -512,16 +512,37 @@ void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant
 }
 
 // ---------------------------------------------------------------- status
-__global__ void k_status_init(uint8_t *status, uint32_t n_txn, uint32_t n_pad, uint8_t value) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n_pad) status[i] = i < n_txn ? value : (uint8_t)ST_ABORT;
+// Per-epoch state in one launch (instead of a fill per buffer): the counters
+// block and tile tickets (block 0), every txn's status byte (padding txns
+// aborted), and its access range / count (txns without accesses here keep an
+// empty range).
+__global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ status, uint32_t n_txn,
+                                                        uint32_t n_pad, uint8_t value,
+                                                        uint32_t *__restrict__ tb_start,
+                                                        uint32_t *__restrict__ tb_end,
+                                                        uint8_t *__restrict__ tlen,
+                                                        uint32_t *__restrict__ tile_ctr, Counters *ctr) {
+    if (blockIdx.x == 0) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(ctr);
+        for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) w[i] = 0;
+        for (uint32_t i = threadIdx.x; i < kTileCtrs; i += kBlock) tile_ctr[i] = 0;
+    }
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
+        status[i] = i < n_txn ? value : (uint8_t)ST_ABORT;
+        tb_start[i] = 0;
+        tb_end[i] = 0;
+        if (tlen) tlen[i] = 0;
+    }
 }
 
-void launch_status_init(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4,
-                        uint8_t value) {
-    if (!n_txn_pad4) return;
-    k_status_init<<<(n_txn_pad4 + kBlock - 1) / kBlock, kBlock, 0, s>>>(status, n_txn, n_txn_pad4,
-                                                                        value);
+void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
+                        uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
+                        Counters *ctr) {
+    uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
+    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
+                                       ctr);
 }
 
 // ---------------------------------------------------------------- execute

@@ -1012,9 +1012,18 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
 }
 
 
-__global__ void k_round0_init(uint32_t n, uint32_t n_txn, Counters *ctr) {
-    ctr->nlive[0] = n;
-    ctr->nund[0] = n_txn;  // partitioned rounds: round 0's list is every txn
+// round 0's counts, and every txn's verdict bytes cleared (16-byte stores,
+// 1 << slog bytes per txn)
+__global__ __launch_bounds__(kBlock) void k_round0_init(uint32_t n, uint32_t n_txn, uint32_t n_pad,
+                                                        uint4 *__restrict__ vb8, uint32_t slog,
+                                                        Counters *ctr) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctr->nlive[0] = n;
+        ctr->nund[0] = n_txn;  // partitioned rounds: round 0's list is every txn
+    }
+    const uint64_t words = (uint64_t)n_pad << (slog - 4);
+    for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
+        vb8[i] = uint4{0u, 0u, 0u, 0u};
 }
 
 // ------------------------------------------------------------- launchers
@@ -1033,8 +1042,8 @@ uint32_t tail_cap(bool el32) { return el32 ? TailGeo<uint32_t>::kCap : TailGeo<u
 
 void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
                        uint32_t n_txn_pad) {
-    (void)hipMemsetAsync(b.vb8, 0, n_txn_pad ? ((size_t)n_txn_pad << b.slog) : 16, s);
-    k_round0_init<<<1, 1, 0, s>>>(n_acc, n_txn, b.ctr);
+    k_round0_init<<<txn_grid(n_txn_pad << (b.slog - 4)), kBlock, 0, s>>>(
+        n_acc, n_txn, n_txn_pad, reinterpret_cast<uint4 *>(b.vb8), b.slog, b.ctr);
 }
 
 template <class E>

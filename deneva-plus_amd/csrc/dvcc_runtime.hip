@@ -553,16 +553,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->async_launched = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
-    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
-    HIPCHK(hipMemsetAsync(c->verdict, 0, c->n_txn_pad ? c->n_txn_pad : 4, c->stream));
-    launch_status_init(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC);
-    {  // txns without accesses here keep an empty range
-        const size_t tb_bytes = (size_t)(c->n_txn_pad ? c->n_txn_pad : 4) * 4;
-        HIPCHK(hipMemsetAsync(c->tb_start, 0, tb_bytes, c->stream));
-        HIPCHK(hipMemsetAsync(c->tb_end, 0, tb_bytes, c->stream));
-        if (!calvin) HIPCHK(hipMemsetAsync(c->tlen, 0, tb_bytes / 4, c->stream));
-    }
-    HIPCHK(hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream));
+    launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
+                       c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, c->ctr);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,

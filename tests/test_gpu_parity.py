@@ -182,6 +182,45 @@ def test_chained_index_table():
         eng.close()
 
 
+@pytest.mark.parametrize("order", ["bucket", "shuffled"])
+def test_direct_index_table(order):
+    """dv_load_table with one key per bucket: keys loaded in bucket order give
+    an implicit-row map (probes read the primary-key column), shuffled keys a
+    {key, row} entry per bucket.  Same decisions, table and digests either
+    way, and a key that is not in the table is reported."""
+    rows = 4096
+    rng = np.random.default_rng(11)
+    keys = np.arange(rows, dtype=np.uint64) + np.uint64(5 * rows)  # key % rows: distinct buckets
+    if order == "shuffled":
+        keys = rng.permutation(keys)
+    f0 = rng.integers(1, 2**63, size=rows, dtype=np.uint64)
+    ix = O.MultiIndex(rows, 1, 0, list(zip(keys.tolist(), range(rows))))
+    n_txn, R = 1500, 8
+    ak = np.empty(n_txn * R, np.uint64)
+    for t in range(n_txn):
+        ak[t * R:(t + 1) * R] = keys[rng.choice(rows // 4, size=R, replace=False)]
+    at = rng.integers(0, 2, size=n_txn * R).astype(np.uint8)
+    tb = (np.arange(n_txn + 1) * R).astype(np.uint32)
+    for cc in CCS:
+        ref_f0 = f0.copy()
+        c_ref, g_ref, st_ref = O.epoch_run(ORACLE_CC[cc], ix.ix, ref_f0, n_txn, tb, ak, at,
+                                           want_grant=cc == dvcc.CALVIN)
+        eng = CCEngine(cc, n_txn, n_txn * R)
+        eng.create_table(0, rows, rows, dvcc.HASH_MOD)
+        eng.load_table(0, keys, f0)
+        c, g, st = eng.run_epoch(Epoch(ak, at, tb), want_grant=cc == dvcc.CALVIN)
+        assert (c == c_ref).all()
+        if cc == dvcc.CALVIN:
+            assert (g == g_ref).all()
+        assert st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == ref_f0).all()
+        missing = ak.copy()
+        missing[7] = np.uint64(3 * rows + 1)  # bucket 1 holds another key
+        with pytest.raises(dvcc.DvccError):
+            eng.run_epoch(Epoch(missing, at, tb))
+        eng.close()
+
+
 # ---- BASELINE.json sizes (configs B, C, D at N=1), bit-exact against the oracle
 @pytest.mark.slow
 def test_config_b_calvin_full():
