@@ -94,6 +94,7 @@ struct dv_ctx {
     uint32_t passes = 0;                 // pass launches this epoch
     uint32_t applied = 0;                // partitioned rounds applied this epoch
     uint32_t async_launched = 0;         // asynchronous-round tries this epoch
+    bool async_unconfirmed = false;      // the rounds ended in a try nobody waited for
     uint32_t async_hint = 0;             // round the last epoch's asynchronous launch ran at
     float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
 };
@@ -551,6 +552,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->passes = 0;
     c->applied = 0;
     c->async_launched = 0;
+    c->async_unconfirmed = false;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
@@ -718,6 +720,14 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
         if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
         c->rounds_real = c->h_ctr->async_r0 + c->h_ctr->async_iters;
+    } else if (c->async_unconfirmed) {
+        // the last try found nothing left to decide (a declined one would
+        // leave txns undecided: cannot happen, its live count fitted)
+        if (c->h_ctr->async_go == 2u) return DV_ERR_STATE;
+        uint32_t r_end = 0;  // the passes decided everything: the last round with undecided txns
+        for (uint32_t k = 0; k < std::min(c->rounds, (uint32_t)kRoundLog); k++)
+            if (c->h_ctr->log_und[k]) r_end = k + 1;
+        c->rounds_real = std::max(r_end, 1u);
     }
     c->async_hint = calvin ? c->async_hint : c->h_ctr->async_r0;
     if (st) {
@@ -852,16 +862,13 @@ int run_rounds(dv_ctx *c) {
         c->live_ub = std::min(c->live_ub, (uint32_t)(le >> 32));  // bounds for rounds not yet enqueued
         c->und_ub = und;
         if (async && !tail_r0 && c->live_ub <= async_thresh(c)) {
-            // the try behind the last queued pass qualifies (unless an
-            // earlier one ran): wait for it and the no-op passes behind it
+            // the try behind the last queued pass qualifies: it decides the
+            // rest, or finds nothing left (an earlier try ran, or the passes
+            // finished).  No wait here: dv_epoch_finish queues the execution
+            // behind it and checks the outcome with the counters.
             if (c->rounds < try_from) async_try(c, c->rounds);
-            r = sync_counters(c);
-            if (!r) r = err_from_bits(c->h_ctr->err);
-            if (!r && c->h_ctr->async_go == 2u) r = DV_ERR_STATE;  // cannot happen: the count fits
-            if (r || c->h_ctr->async_r0) return r;
-            // nothing left to decide by round c->rounds: the passes have
-            // published it (or the next one will)
-            continue;
+            c->async_unconfirmed = true;
+            return DV_OK;
         }
         if (!tail_r0 && !(c->cfg.flags & DV_FLAG_NO_TAIL) && c->live_ub <= tail_limit) {
             tail_r0 = c->rounds;
