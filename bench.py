@@ -207,7 +207,7 @@ def main():
             "launches": launches,
             "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d scan read "
                                  "8 B + flag 1 B) x live accesses the launch reads",
-            "traffic_source": PMC_SUMMARY if traffic is not None else None,
+            "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic is not None else None,
         },
         "sort": {"kernel": "k_radix_scatter", "avg_launch_ms": sc_avg, "achieved_GBps": scatter_gbps,
                  "keys_per_s": n_acc_step / (sc_avg * 1e-3) if sc_avg > 0 else 0.0},
