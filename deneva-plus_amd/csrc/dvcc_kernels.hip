@@ -612,12 +612,14 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
     k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
 }
 
-// NO_WAIT / WAIT_DIE / OCC: run_ycsb_1 for the committed txns only, in txn
-// order (acc_row from the probe), one thread per txn with its accesses'
-// loads issued together.  A committed reader never sees a committed writer's
-// value here (2PL: the two conflict, so one launch does both; OCC: reads
-// happen in the access phase, occ.cpp:116-294, so the reads run in a launch
-// before the writes).
+// NO_WAIT / WAIT_DIE / OCC: run_ycsb_1 for the committed txns only (acc_row
+// from the probe).  A committed reader never sees a committed writer's value
+// here (2PL: the two conflict, so one launch does both; OCC: reads happen in
+// the access phase, occ.cpp:116-294, so the reads run in a launch before the
+// writes).  Each wave takes 64 consecutive txns and spreads the accesses of
+// its committed ones over its lanes (a prefix sum of their lengths): at a
+// ~2 % commit rate a thread per txn left most lanes idle behind a few serial
+// access loops, and at high commit rates this keeps every lane busy.
 enum : int { EX_READS = 1, EX_WRITES = 2 };
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict__ tb_start,
@@ -629,34 +631,43 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      const uint64_t *__restrict__ pkey,
                                                      Counters *ctr) {
     __shared__ unsigned long long part[2][4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long dig = 0, wcnt = 0;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
-        if (status[t] != ST_COMMIT) continue;
-        const uint32_t a0 = tb_start[t], len = tb_end[t] - a0;
-        for (uint32_t c = 0; c < len; c += 16) {
-            uint32_t ar[16];
+    const uint32_t step = gridDim.x * (kBlock / 64) * 64;
+    for (uint32_t base = (blockIdx.x * (kBlock / 64) + wave) * 64; base < n_txn; base += step) {
+        const uint32_t t = base + lane;
+        const bool com = t < n_txn && status[t] == ST_COMMIT;
+        if (__ballot(com) == 0) continue;
+        const uint32_t a0 = com ? tb_start[t] : 0u;
+        const uint32_t len = com ? tb_end[t] - a0 : 0u;
+        uint32_t incl = len;  // inclusive prefix of the lengths over the wave
 #pragma unroll
-            for (int k = 0; k < 16; k++) ar[k] = c + k < len ? acc_row[a0 + c + k] : 0xFFFFFFFFu;
-            if (MODE & EX_READS) {
-                uint64_t val[16], pk[16];
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (lane >= (uint32_t)off) incl += o;
+        }
+        const uint32_t pre = incl - len, total = __shfl(incl, 63, 64);
+        // wave-uniform trip count: the shuffles below read every lane
+        for (uint32_t g0 = 0; g0 < total; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            // the last lane whose prefix is <= g owns access g (empty lanes
+            // share the next lane's prefix and lose to it)
+            uint32_t src = 0;
 #pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    const bool rd = !(ar[k] & AR_WR);
-                    val[k] = rd ? f0[ar[k]] : 0ull;
-                    pk[k] = rd ? pkey[ar[k]] : 0ull;
-                }
-#pragma unroll
-                for (int k = 0; k < 16; k++)
-                    if (!(ar[k] & AR_WR)) dig += mix64(val[k] ^ mix64(((uint64_t)t << 32) ^ pk[k]));
+            for (uint32_t w = 32; w > 0; w >>= 1) {
+                const uint32_t cand = src + w;
+                const uint32_t pv = __shfl(pre, (int)(cand & 63u), 64);
+                if (cand < 64 && pv <= g) src = cand;
             }
-            if (MODE & EX_WRITES) {
-#pragma unroll
-                for (int k = 0; k < 16; k++) {
-                    if (ar[k] != 0xFFFFFFFFu && (ar[k] & AR_WR)) {
-                        f0[ar[k] & ~AR_WR] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
-                        wcnt++;
-                    }
-                }
+            const uint32_t sa0 = __shfl(a0, (int)src, 64), spre = __shfl(pre, (int)src, 64);
+            if (g >= total) continue;
+            const uint32_t tt = base + src;
+            const uint32_t ar = acc_row[sa0 + (g - spre)];
+            if ((MODE & EX_READS) && !(ar & AR_WR))
+                dig += mix64(f0[ar] ^ mix64(((uint64_t)tt << 32) ^ pkey[ar]));
+            if ((MODE & EX_WRITES) && (ar & AR_WR)) {
+                f0[ar & ~AR_WR] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+                wcnt++;
             }
         }
     }
@@ -665,9 +676,9 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
         dig += __shfl_down(dig, off, 64);
         wcnt += __shfl_down(wcnt, off, 64);
     }
-    if ((threadIdx.x & 63) == 0) {
-        part[0][threadIdx.x >> 6] = dig;
-        part[1][threadIdx.x >> 6] = wcnt;
+    if (lane == 0) {
+        part[0][wave] = dig;
+        part[1][wave] = wcnt;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
