@@ -198,6 +198,8 @@ int err_from_bits(uint32_t b) {
 }
 
 bool timing(dv_ctx *c) { return (c->cfg.flags & DV_FLAG_TIMING) != 0; }
+// dispatch timestamps of the scatter and pass launches (hipExtLaunchKernelGGL)
+bool ktiming(dv_ctx *c) { return (c->cfg.flags & (DV_FLAG_TIMING | DV_FLAG_KERNEL_TIMING)) != 0; }
 
 void rec(dv_ctx *c, int i) {
     if (timing(c)) (void)hipEventRecord(c->ev[i], c->stream);
@@ -326,7 +328,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
                              "hipHostGetDevicePointer");
         if (!r) std::memset(c->h_pub, 0, sizeof(RoundPub));
     }
-    if (!r && timing(c)) {
+    if (!r && ktiming(c)) {
         for (auto &e : c->ev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
         for (auto &e : c->sev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
         for (auto &e : c->pev) if (!r) r = hip_fail(hipEventCreate(&e), "hipEventCreate");
@@ -349,6 +351,20 @@ int dv_set_stream(dv_ctx *c, void *stream) {
     if (c->phase != 0) return DV_ERR_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->stream = reinterpret_cast<hipStream_t>(stream);
+    return DV_OK;
+}
+
+int dv_set_timing(dv_ctx *c, uint32_t flags) {
+    if (!c) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    constexpr uint32_t kBits = DV_FLAG_TIMING | DV_FLAG_KERNEL_TIMING;
+    c->cfg.flags = (c->cfg.flags & ~kBits) | (flags & kBits);
+    if (ktiming(c) && !c->ev[0]) {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+        for (auto &e : c->sev) HIPCHK(hipEventCreate(&e));
+        for (auto &e : c->pev) HIPCHK(hipEventCreate(&e));
+    }
     return DV_OK;
 }
 
@@ -565,7 +581,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
-                                timing(c) ? c->sev : nullptr);
+                                ktiming(c) ? c->sev : nullptr);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
@@ -596,7 +612,7 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
     const RoundBufs b = round_bufs(c);
     // timing: the pass's own dispatch records its events (hipExtLaunchKernel),
     // no extra packets in the stream
-    const bool t = timing(c) && c->passes < (uint32_t)kRoundLog;
+    const bool t = ktiming(c) && c->passes < (uint32_t)kRoundLog;
     round_pass(c->stream, b, r, c->cfg.cc_alg != DV_OCC, c->live_ub, tag,
                (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr,
                t ? c->pev[2 * c->passes] : nullptr, t ? c->pev[2 * c->passes + 1] : nullptr);
@@ -754,6 +770,8 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             st->ms_decide = elapsed(c, 2, 4);
             st->ms_exec = elapsed(c, 4, 5);
             st->ms_total = elapsed(c, 0, 5);
+        }
+        if (ktiming(c)) {
             float s = 0;
             for (uint32_t p = 0; p < c->sort_passes && p < 8; p++) {
                 float m = 0;

@@ -31,6 +31,7 @@ FLAG_TIMING = 1
 FLAG_NO_TAIL = 2
 FLAG_EL64 = 4
 FLAG_NO_ASYNC = 8
+FLAG_KERNEL_TIMING = 16
 
 
 class DvccError(RuntimeError):
@@ -94,6 +95,7 @@ SIGNATURES = [
     ("dv_stream", _vp, [_vp]),
     ("dv_own_stream", _vp, [_vp]),
     ("dv_set_stream", ctypes.c_int, [_vp, _vp]),
+    ("dv_set_timing", ctypes.c_int, [_vp, ctypes.c_uint32]),
     ("dv_create_table", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_uint32]),
     ("dv_load_table", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64]),

@@ -105,7 +105,10 @@ class CCEngine:
         self.cc_alg = cc_alg
         self.part_cnt, self.part_id = part_cnt, part_id
         self.max_txn, self.max_acc = max_txn, max_acc
-        flags = ((L.FLAG_TIMING if timing else 0) | (0 if tail else L.FLAG_NO_TAIL)
+        # timing: True = per-stage events, "kernel" = only the scatter / pass
+        # launches' own dispatch timestamps (no marker packets between kernels)
+        tflag = L.FLAG_KERNEL_TIMING if timing == "kernel" else (L.FLAG_TIMING if timing else 0)
+        flags = (tflag | (0 if tail else L.FLAG_NO_TAIL)
                  | (L.FLAG_EL64 if el64 else 0) | (0 if asynchronous else L.FLAG_NO_ASYNC))
         cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc, flags, 0)
         self._ctx = ctypes.c_void_p()
@@ -133,6 +136,12 @@ class CCEngine:
         if stream is None:
             stream = L.lib().dv_own_stream(self._ctx)
         L.check(L.lib().dv_set_stream(self._ctx, stream), "dv_set_stream")
+
+    def set_timing(self, timing):
+        """Between epochs: True = per-stage events, "kernel" = only the scatter
+        and pass launches' dispatch timestamps, False = none."""
+        flag = L.FLAG_KERNEL_TIMING if timing == "kernel" else (L.FLAG_TIMING if timing else 0)
+        L.check(L.lib().dv_set_timing(self._ctx, flag), "dv_set_timing")
 
     # ---- storage (Workload::init_schema / init_table; IndexHash::index_insert)
     def load_ycsb_partition(self, rows_per_part):

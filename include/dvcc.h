@@ -82,7 +82,11 @@ extern "C" {
 #define DV_HASH_MOD 1  /* key % nbuckets               */
 
 /* dv_config.flags */
-#define DV_FLAG_TIMING 1u  /* record HIP-event timings per stage into dv_stats */
+#define DV_FLAG_TIMING 1u  /* record HIP-event timings per stage into dv_stats
+                              (implies DV_FLAG_KERNEL_TIMING)                */
+#define DV_FLAG_KERNEL_TIMING 16u /* only the sort-scatter and round-pass
+                              launches' own dispatch timestamps (ms_scatter,
+                              ms_pass): no marker packets between kernels   */
 #define DV_FLAG_NO_TAIL 2u /* never finish the decision rounds in the single-
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
@@ -176,6 +180,11 @@ void *dv_own_stream(dv_ctx *ctx); /* the stream dv_open created              */
  * collectives share one ordering; dv_set_stream(ctx, dv_own_stream(ctx))
  * returns to the context's own stream */
 int dv_set_stream(dv_ctx *ctx, void *stream);
+/* switch timing between epochs: flags' DV_FLAG_TIMING / DV_FLAG_KERNEL_TIMING
+ * bits replace the context's (the other flags are kept).  Event timing costs
+ * launch latency (a marker packet per stage, dispatch timestamps per launch:
+ * ~70 us per 1M-txn epoch), so a caller measures with it on and runs without. */
+int dv_set_timing(dv_ctx *ctx, uint32_t flags);
 
 /* tables: hot column = the 8-byte F0 prefix every YCSB txn reads/writes
  * (ycsb_txn.cpp:227-254); bytes beyond it are never touched by the path (H3). */
