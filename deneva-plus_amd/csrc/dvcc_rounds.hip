@@ -764,16 +764,19 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
 // with device-scope atomics and read with agent-scope atomic loads, so they
 // cross CUs and XCDs inside the launch and one load tells committed (count ==
 // accesses), aborted or undecided.
-// A row queue may run across slices: each workgroup publishes, every
-// iteration, the OR of the scan values of the queue its slice ends in (its
-// carry word); the next workgroup reads it as the value in front of its first
-// element.  Carries are built from monotone facts and start fully
-// pessimistic, so a stale carry only delays decisions.  The slice's last
-// element is never dropped while its queue runs on, so the carry always
-// describes that queue.  A workgroup leaves
-// once no element of an undecided txn remains in its slice and its carry no
-// longer holds an undecided blocker; the lowest undecided txn can always
-// decide, so every workgroup leaves (bounded spin: ERRB_SPIN).
+// A row queue may run across slices (a zipf-hot row spans dozens): each
+// workgroup publishes, every iteration, its carry word -- the OR of the scan
+// values after its last queue head (the whole slice if it holds no head) and
+// a has-head bit.  A workgroup whose first queue runs in takes the value in
+// front of it by walking the carries back, 64 at a time, to the nearest slice
+// holding a head: a fact reaches the far end of a long queue in one
+// iteration, not one slice per iteration.  Carries are built from monotone
+// facts and start fully pessimistic (with a head, so walks stop there), so a
+// stale carry only delays decisions.  The slice's last element is never
+// dropped while its queue runs on, so a carry always describes that queue.
+// A workgroup leaves once no element of an undecided txn remains in its slice
+// and its carry no longer holds an undecided blocker; the lowest undecided
+// txn can always decide, so every workgroup leaves (bounded spin: ERRB_SPIN).
 constexpr int kAsyncThreads = 512;
 constexpr int kAsyncWaves = kAsyncThreads / 64;
 // 28 elements per thread (128 VGPRs, two workgroups per CU): 7.3M live
@@ -785,7 +788,8 @@ constexpr int kAsyncWaves = kAsyncThreads / 64;
 constexpr int kAsyncIPT = 28;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
 constexpr uint32_t kAsyncMaxIters = 1u << 18;
-constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP;  // "undecided blockers in front"
+constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
+constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
 
 constexpr uint32_t TW_OK = 1u << 8;  // one more access OK
 
@@ -861,7 +865,7 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     // per-iteration counters, double-buffered by iteration parity: slot p is
     // reset during the iteration before it is used, after every thread has
     // read it for the iteration before that
-    __shared__ uint32_t s_needy[2], s_moved[2];
+    __shared__ uint32_t s_needy[2], s_moved[2], s_cin;
     Counters *ctr = b.ctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
@@ -880,9 +884,25 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     uint32_t it = 0;
     for (; it < max_iters; it++) {
         const uint32_t p = it & 1u;
-        const uint32_t cin = cont_in ? __hip_atomic_load(carry + g - 1, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                                     : 0u;
+        // the value in front of the slice: carries back to the nearest head
+        // (read by wave 0 here, taken from LDS after keep_bits' barrier)
+        if (cont_in && wave == 0) {
+            uint32_t acc = 0;
+            for (int64_t j0 = (int64_t)g - 1;; j0 -= 64) {
+                const int64_t j = j0 - (int64_t)lane;
+                const uint32_t w = j >= 0 ? __hip_atomic_load(carry + j, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : kCarryHead;  // (slice 0 starts with a head)
+                const uint64_t hm = __ballot((w & kCarryHead) != 0);
+                const uint32_t stop = hm ? (uint32_t)__builtin_ctzll(hm) : 64u;
+                uint32_t v = lane <= stop ? (w & ~kCarryHead) : 0u;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
+                acc |= v;
+                if (hm) break;
+            }
+            if (lane == 0) s_cin = acc;
+        }
         const uint32_t k = (n + kAsyncThreads - 1) / kAsyncThreads;
         const uint32_t first = tid * k;
         const int cnt = first >= n ? 0 : (int)(n - first < k ? n - first : k);
@@ -929,10 +949,12 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         const Agg inc = wave_incl<OpPlain>(a, lane);
         if (lane == 63) wt[wave] = inc;
         __syncthreads();
-        Agg wpre{0u, cin, 0u}, total{0u, cin, 0u};  // the carry is in front of the slice
+        const uint32_t cin = cont_in ? s_cin : 0u;
+        // wpre: the carry is in front of the slice; own: the slice alone
+        Agg wpre{0u, cin, 0u}, own{0u, 0u, 0u};
         for (int w = 0; w < kAsyncWaves; w++) {
             if (w < (int)wave) wpre = OpPlain::comb(wpre, wt[w]);
-            total = OpPlain::comb(total, wt[w]);
+            own = OpPlain::comb(own, wt[w]);
         }
         const Agg pre = OpPlain::comb(wpre, wave_excl_from_incl<OpPlain>(inc, lane));
         uint32_t lpos = pre.c, run = pre.v, moved = 0;
@@ -964,11 +986,12 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
             }
         }
         if (moved) s_moved[p] = 1;
-        // what the next slice has in front of it: the OR since the last head
-        const uint32_t cout = total.v;
+        // the carry word: the OR since the slice's last head (or over all of
+        // it) and whether it holds a head; later slices walk back to it
+        const uint32_t cout = own.v | (own.f ? kCarryHead : 0u);
         if (cont_out && tid == 0)
             __hip_atomic_store(carry + g, cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        n = total.c;
+        n = own.c;
         __syncthreads();
         if (s_needy[p] == 0 && (!cont_out || !(cout & (B_UA | B_UW)))) break;  // nothing left to learn
         // nothing decided here: the facts this slice waits for come from other
