@@ -95,6 +95,27 @@ def cpu_baseline(epochs, rows, cc_name, seconds):
                       f"restatement of the reference CC, not the reference binary"}
 
 
+def e2e_host_leg(eng, epochs, k):
+    """SURVEY.md 8(d)'s second reading: dv_epoch_run from host buffers, so
+    the H2D copy of the 16-B access records is inside the time (pinned host
+    memory, as a caller that batches epochs would hold them).  Never `value`."""
+    bufs = []
+    for e in epochs:
+        acc = torch.from_numpy(e.to_access_array().view(np.uint8)).pin_memory()
+        tb = torch.from_numpy(np.ascontiguousarray(e.txn_begin, dtype=np.uint32)).pin_memory()
+        bufs.append((acc, tb, e.n_acc, e.n_txn))
+    commit = torch.zeros(max(b[3] for b in bufs), dtype=torch.uint8).pin_memory()
+    eng.run_epoch_host(*bufs[0], commit)  # staging buffers allocated outside the timing
+    t0 = time.perf_counter()
+    committed = 0
+    for i in range(k):
+        committed += eng.run_epoch_host(*bufs[i % len(bufs)], commit).committed
+    el = time.perf_counter() - t0
+    return {"committed_per_s": committed / el, "ms_per_epoch": el / k * 1e3, "epochs": k,
+            "bytes_h2d_per_epoch": int(bufs[0][0].numel()),
+            "note": "dv_epoch_run: H2D of the access records + the same device path"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,6 +276,7 @@ def main():
     if world == 1:
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
+        out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(epochs, rows, cc_name, a.cpu_seconds)
     if rank == 0:

@@ -1,0 +1,149 @@
+// dvcc_carry.hip -- abort carry-over into the next epoch.
+//
+// The reference retries an aborted txn: WorkerThread::abort (worker_thread.cpp:
+// 160-172) hands its id to AbortQueue::enqueue, which holds it for a penalty
+// and re-enqueues it as RTXN with its query unchanged (abort_queue.cpp:26-82).
+// Here the penalty is one epoch: after an epoch is decided, the accesses of
+// its aborted txns are compacted on the device, in sequence order and
+// renumbered from 0, to open the next epoch ahead of the new txns -- they are
+// older, so they keep their priority (WAIT_DIE keeps a restarted txn's
+// timestamp).  Three launches: per-block counts, one scan of the block
+// counts, then every carried txn copies its accesses.
+#include "dvcc_common.h"
+
+namespace dvcc {
+
+constexpr uint32_t kCarryTpb = kBlock * 4;  // txns per block: 4 per thread
+
+__device__ __forceinline__ bool carried(const uint8_t *status, uint32_t t) {
+    return status[t] != ST_COMMIT;  // aborted (nothing is undecided after the rounds)
+}
+
+// per block: aborted txns and their accesses
+__global__ __launch_bounds__(kBlock) void k_carry_count(const uint8_t *__restrict__ status,
+                                                        const uint32_t *__restrict__ tb_start,
+                                                        const uint32_t *__restrict__ tb_end,
+                                                        uint32_t n_txn, uint32_t *__restrict__ bt,
+                                                        uint32_t *__restrict__ ba) {
+    __shared__ uint32_t lds4[4];
+    uint32_t nt = 0, na = 0;
+    const uint32_t t0 = blockIdx.x * kCarryTpb + threadIdx.x * 4;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t t = t0 + k;
+        if (t < n_txn && carried(status, t)) {
+            nt++;
+            na += tb_end[t] - tb_start[t];
+        }
+    }
+    uint32_t tt = 0, ta = 0;
+    (void)block_excl_scan256(nt, lds4, &tt);
+    (void)block_excl_scan256(na, lds4, &ta);
+    if (threadIdx.x == 0) {
+        bt[blockIdx.x] = tt;
+        ba[blockIdx.x] = ta;
+    }
+}
+
+// one block: exclusive scans of the block counts, in place
+__global__ __launch_bounds__(kBlock) void k_carry_scan(uint32_t *__restrict__ bt, uint32_t *__restrict__ ba,
+                                                       uint32_t nb) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t per = (nb + kBlock - 1) / kBlock;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+    uint32_t st = 0, sa = 0;
+    for (uint32_t i = lo; i < hi; i++) {
+        st += bt[i];
+        sa += ba[i];
+    }
+    uint32_t pt = block_excl_scan256(st, lds4, nullptr);
+    uint32_t pa = block_excl_scan256(sa, lds4, nullptr);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t vt = bt[i], va = ba[i];
+        bt[i] = pt;
+        ba[i] = pa;
+        pt += vt;
+        pa += va;
+    }
+}
+
+// every carried txn with a new id below max_txn copies its accesses; the last
+// one reports the carried epoch's size (tot[0] txns, tot[1] accesses)
+__global__ __launch_bounds__(kBlock) void k_carry_copy(
+    const uint8_t *__restrict__ status, const uint32_t *__restrict__ tb_start,
+    const uint32_t *__restrict__ tb_end, uint32_t n_txn, const uint32_t *__restrict__ bt,
+    const uint32_t *__restrict__ ba, uint32_t max_txn, const uint64_t *__restrict__ keys,
+    const uint8_t *__restrict__ types, const uint8_t *__restrict__ tables, uint64_t *__restrict__ okeys,
+    uint8_t *__restrict__ otypes, uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
+    uint32_t *__restrict__ tot) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t t0 = blockIdx.x * kCarryTpb + threadIdx.x * 4;
+    uint32_t nt = 0, na = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t t = t0 + k;
+        if (t < n_txn && carried(status, t)) {
+            nt++;
+            na += tb_end[t] - tb_start[t];
+        }
+    }
+    uint32_t id = bt[blockIdx.x] + block_excl_scan256(nt, lds4, nullptr);
+    uint32_t pos = ba[blockIdx.x] + block_excl_scan256(na, lds4, nullptr);
+    const uint32_t total_txn = tot[2];  // carried txns before the cap (k_carry_scan's grand total)
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t t = t0 + k;
+        if (t >= n_txn || !carried(status, t)) continue;
+        const uint32_t a0 = tb_start[t], len = tb_end[t] - a0;
+        if (id < max_txn) {
+            for (uint32_t j = 0; j < len; j++) {
+                okeys[pos + j] = keys[a0 + j];
+                otypes[pos + j] = types[a0 + j];
+                otxn[pos + j] = id;
+                if (tables) otables[pos + j] = tables[a0 + j];
+            }
+            const uint32_t last = total_txn < max_txn ? total_txn : max_txn;
+            if (id + 1 == last) {
+                tot[0] = last;
+                tot[1] = pos + len;
+            }
+        }
+        id++;
+        pos += len;
+    }
+}
+
+// tot[2] = carried txns before the cap: the last block's exclusive prefix plus
+// its own count; tot[0..1] cleared for k_carry_copy
+__global__ void k_carry_total(const uint8_t *__restrict__ status, uint32_t n_txn, const uint32_t *bt,
+                              uint32_t nb, uint32_t *tot) {
+    uint32_t c = 0;
+    for (uint32_t t = (nb - 1) * kCarryTpb + threadIdx.x; t < n_txn; t += blockDim.x)
+        c += carried(status, t) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (threadIdx.x == 0) {
+        tot[0] = 0;
+        tot[1] = 0;
+        tot[2] = bt[nb - 1] + c;
+    }
+}
+
+uint32_t carry_blocks(uint32_t n_txn) { return n_txn ? (n_txn + kCarryTpb - 1) / kCarryTpb : 0; }
+
+void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                  uint32_t n_txn, uint32_t max_txn, const uint64_t *keys, const uint8_t *types,
+                  const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
+                  uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot) {
+    const uint32_t nb = carry_blocks(n_txn);
+    if (!nb) {
+        (void)hipMemsetAsync(tot, 0, 3 * sizeof(uint32_t), s);
+        return;
+    }
+    k_carry_count<<<nb, kBlock, 0, s>>>(status, tb_start, tb_end, n_txn, bt, ba);
+    k_carry_scan<<<1, kBlock, 0, s>>>(bt, ba, nb);
+    k_carry_total<<<1, 64, 0, s>>>(status, n_txn, bt, nb, tot);
+    k_carry_copy<<<nb, kBlock, 0, s>>>(status, tb_start, tb_end, n_txn, bt, ba, max_txn, keys, types, tables,
+                                       okeys, otypes, otxn, otables, tot);
+}
+
+}  // namespace dvcc

@@ -206,6 +206,16 @@ uint32_t async_try_limit(uint32_t G);
 bool round_el32(uint32_t n_txn, uint32_t slog);
 
 // ---- execution and outputs (dvcc_kernels.hip)
+// abort carry-over (dvcc_carry.hip): the accesses of the txns whose status is
+// not committed, in sequence order and renumbered from 0, capped at max_txn
+// txns, into o*; tot (3 words, device) = carried txns, their accesses, and the
+// carried txns before the cap.  bt/ba: carry_blocks(n_txn) words each.
+uint32_t carry_blocks(uint32_t n_txn);
+void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                  uint32_t n_txn, uint32_t max_txn, const uint64_t *keys, const uint8_t *types,
+                  const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
+                  uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot);
+
 // per-epoch reset: counters, tile tickets, status (value; padding aborted),
 // access ranges and counts
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,

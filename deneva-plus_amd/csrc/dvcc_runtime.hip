@@ -62,6 +62,9 @@ struct dv_ctx {
     uint32_t *abounds = nullptr;                     // asynchronous-round slice carries
     uint32_t *tword = nullptr;                       // asynchronous-round txn fact words
     uint32_t async_g = 0;                            // its workgroups (all co-resident)
+    uint32_t *carry_b = nullptr;                     // abort carry-over: block counts (2 x carry_nb)
+    uint32_t carry_nb = 0;
+    uint32_t *carry_tot = nullptr;                   // its totals (3 words)
     uint32_t round_tag = 0;                          // descriptor tag of the last pass
     uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
@@ -254,7 +257,7 @@ void dv_close(dv_ctx *c) {
     void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
                     c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tlen, c->acc_row,
                     c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
-                    c->abounds, c->tword,
+                    c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant};
     for (void *b : bufs) dfree(b);
@@ -351,6 +354,39 @@ int dv_set_stream(dv_ctx *c, void *stream) {
     if (c->phase != 0) return DV_ERR_STATE;
     HIPCHK(hipStreamSynchronize(c->stream));
     c->stream = reinterpret_cast<hipStream_t>(stream);
+    return DV_OK;
+}
+
+int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch_dev *out) {
+    if (!c || !ep || !out) return DV_ERR_ARG;
+    if (c->phase != 0 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
+    if (ep->n_txn != c->n_txn || ep->n_acc != c->n_acc) return DV_ERR_STATE;  // not the last epoch
+    if (ep->n_acc && (!out->keys || !out->types || !out->acc_txn || (ep->tables && !out->tables)))
+        return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const uint32_t nb = carry_blocks(ep->n_txn);
+    if (nb > c->carry_nb || !c->carry_tot) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(c->carry_b);
+        c->carry_b = nullptr;
+        c->carry_nb = 0;
+        int r = dalloc(&c->carry_b, 2ull * (nb ? nb : 1));
+        if (!r && !c->carry_tot) r = dalloc(&c->carry_tot, 3);
+        if (r) return r;
+        c->carry_nb = nb ? nb : 1;
+    }
+    launch_carry(c->stream, c->status, c->tb_start, c->tb_end, ep->n_txn, max_txn, ep->keys, ep->types,
+                 ep->tables, const_cast<uint64_t *>(out->keys), const_cast<uint8_t *>(out->types),
+                 const_cast<uint32_t *>(out->acc_txn),
+                 ep->tables ? const_cast<uint8_t *>(out->tables) : nullptr,
+                 c->carry_b, c->carry_b + c->carry_nb, c->carry_tot);
+    HIPCHK(hipGetLastError());
+    uint32_t tot[3] = {0, 0, 0};
+    HIPCHK(hipMemcpyAsync(tot, c->carry_tot, sizeof(tot), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    out->n_txn = tot[0];
+    out->n_acc = tot[1];
+    out->max_txn_acc = ep->max_txn_acc;
     return DV_OK;
 }
 

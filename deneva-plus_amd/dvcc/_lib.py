@@ -106,6 +106,7 @@ SIGNATURES = [
                                     _P(Stats)]),
     ("dv_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _P(Stats)]),
     ("dv_epoch_begin", ctypes.c_int, [_vp, _P(EpochDev), _vp]),
+    ("dv_epoch_carry", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(EpochDev)]),
     ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),
     ("dv_epoch_round_wait", ctypes.c_int, [_vp, ctypes.c_uint32, _P(ctypes.c_uint32)]),

@@ -84,6 +84,21 @@ class DeviceEpoch:
         self.max_txn_acc = int(max_txn_acc)
         return self
 
+    @classmethod
+    def concat(cls, first, second):
+        """`first`'s txns, then `second`'s (renumbered after them): the next
+        epoch of the abort carry-over, carried txns ahead of the new ones."""
+        import torch
+        tabs = None
+        if first.tables is not None or second.tables is not None:
+            tabs = torch.cat([t.tables if t.tables is not None
+                              else torch.zeros_like(t.types) for t in (first, second)])
+        return cls.from_tensors(torch.cat([first.keys, second.keys]),
+                                torch.cat([first.types, second.types]),
+                                torch.cat([first.acc_txn, second.acc_txn + first.n_txn]),
+                                first.n_txn + second.n_txn, tables=tabs,
+                                max_txn_acc=max(first.max_txn_acc, second.max_txn_acc))
+
     def desc(self):
         return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
                           self.tables.data_ptr() if self.tables is not None else None,
@@ -181,6 +196,15 @@ class CCEngine:
                 "dv_epoch_run")
         return commit[:epoch.n_txn], (grant[:epoch.n_acc] if want_grant else None), st
 
+    def run_epoch_host(self, acc, tb, n_acc, n_txn, commit):
+        """dv_epoch_run on prebuilt host buffers (any objects _ptr accepts:
+        numpy arrays or pinned torch tensors): 16-B access records, txn_begin,
+        and the commit-byte output.  Returns the stats."""
+        st = L.Stats()
+        L.check(L.lib().dv_epoch_run(self._ctx, _ptr(acc), n_acc, _ptr(tb), n_txn, None, _ptr(commit),
+                                     None, ctypes.byref(st)), "dv_epoch_run")
+        return st
+
     # ---- one epoch already resident in HBM
     def run_epoch_device(self, dep, d_commit=None, d_grant=None):
         st = L.Stats()
@@ -188,6 +212,25 @@ class CCEngine:
         L.check(L.lib().dv_epoch_run_device(self._ctx, ctypes.byref(desc), _ptr(d_commit),
                                             _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
         return st
+
+    def carry(self, dep, max_txn=None):
+        """Abort carry-over: a DeviceEpoch of the last epoch's (`dep`'s)
+        aborted txns, in sequence order, at most max_txn of them."""
+        import torch
+        dev = dep.keys.device
+        keys = torch.empty(max(1, dep.n_acc), dtype=torch.int64, device=dev)
+        types = torch.empty(max(1, dep.n_acc), dtype=torch.uint8, device=dev)
+        txn = torch.empty(max(1, dep.n_acc), dtype=torch.int32, device=dev)
+        tabs = torch.empty(max(1, dep.n_acc), dtype=torch.uint8, device=dev) if dep.tables is not None else None
+        out = L.EpochDev(keys.data_ptr(), types.data_ptr(), txn.data_ptr(),
+                         tabs.data_ptr() if tabs is not None else None, 0, 0, 0)
+        cap = dep.n_txn if max_txn is None else max_txn
+        L.check(L.lib().dv_epoch_carry(self._ctx, ctypes.byref(dep.desc()), cap, ctypes.byref(out)),
+                "dv_epoch_carry")
+        n = int(out.n_acc)
+        return DeviceEpoch.from_tensors(keys[:n], types[:n], txn[:n], int(out.n_txn),
+                                        tables=tabs[:n] if tabs is not None else None,
+                                        max_txn_acc=int(out.max_txn_acc))
 
     def round_log(self):
         """(live accesses entering, undecided txns before) per decision round

@@ -205,6 +205,20 @@ int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32
 int dv_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, uint8_t *d_commit,
                         uint32_t *d_grant_group, dv_stats *st);
 
+/* abort carry-over: the reference retries an aborted txn with
+ * its query unchanged after a penalty (WorkerThread::abort,
+ * worker_thread.cpp:160-172 -> AbortQueue::enqueue/process,
+ * abort_queue.cpp:26-82).  After dv_epoch_run_device / dv_epoch_finish of
+ * `ep` (single GPU, not CALVIN; the context still holds its decisions),
+ * writes the accesses of its aborted txns -- in sequence order, renumbered
+ * 0..C-1, C = min(aborted, max_txn) -- into out->keys / types / acc_txn
+ * (/ tables when ep->tables is set): device arrays with room for ep->n_acc
+ * accesses.  Sets out->n_txn = C, out->n_acc, out->max_txn_acc.  The caller
+ * opens the next epoch with them, ahead of its new txns (the penalty is one
+ * epoch; they keep their priority, as WAIT_DIE keeps a restarted txn's
+ * timestamp). */
+int dv_epoch_carry(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch_dev *out);
+
 /* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
  * same txn statuses after each round, hence the same list of undecided txns
  * (ascending).  dv_epoch_round_local writes this partition's verdict byte for
