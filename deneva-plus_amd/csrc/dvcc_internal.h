@@ -235,8 +235,8 @@ void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t 
                       uint64_t *f0, uint64_t *pkey);
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
                         uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr);
-void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, uint64_t *keys,
-                         uint8_t *types, uint32_t *acc_txn, uint8_t *tables);
+void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
+                         uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables, uint32_t *err);
 
 inline uint32_t nblocks_for(uint64_t n) { return (uint32_t)((n + kTile - 1) / kTile); }
 

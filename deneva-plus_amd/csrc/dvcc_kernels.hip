@@ -785,22 +785,28 @@ void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const
     k_gather_rows<<<1024, kBlock, 0, s>>>(tabs, table, keys, n, f0, out, ctr);
 }
 
-__global__ void k_split_access(const dv_access *acc, uint64_t n, uint64_t *keys, uint8_t *types,
-                               uint32_t *acc_txn, uint8_t *tables) {
+// host records -> the epoch's arrays; with txn_begin (CSR), every record's
+// txn_seq must own its index (ERRB_TXN otherwise)
+__global__ void k_split_access(const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
+                               uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables,
+                               uint32_t *err) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    bool bad = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const dv_access a = acc[i];
         keys[i] = a.key;
         types[i] = a.type;
         acc_txn[i] = a.txn_seq;
         tables[i] = a.table;
+        if (tb) bad |= a.txn_seq >= n_txn || i < tb[a.txn_seq] || i >= tb[a.txn_seq + 1];
     }
+    if (bad) atomicOr(err, ERRB_TXN);
 }
 
-void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, uint64_t *keys,
-                         uint8_t *types, uint32_t *acc_txn, uint8_t *tables) {
+void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
+                         uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables, uint32_t *err) {
     if (!n) return;
-    k_split_access<<<2048, kBlock, 0, s>>>(acc, n, keys, types, acc_txn, tables);
+    k_split_access<<<2048, kBlock, 0, s>>>(acc, n, tb, n_txn, keys, types, acc_txn, tables, err);
 }
 
 }  // namespace dvcc

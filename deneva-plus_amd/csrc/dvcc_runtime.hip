@@ -77,6 +77,8 @@ struct dv_ctx {
     uint64_t *d_keys = nullptr;
     uint8_t *d_types = nullptr, *d_tables = nullptr, *d_commit = nullptr;
     uint32_t *d_txn = nullptr, *d_grant = nullptr;
+    uint32_t *d_tb = nullptr;         // txn_begin
+    uint32_t *split_err = nullptr;    // the record check's error bits (begin clears the counters)
 
     // epoch state
     int phase = 0;  // 0 idle, 1 begun
@@ -259,7 +261,7 @@ void dv_close(dv_ctx *c) {
                     c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
-                    c->d_tables, c->d_commit, c->d_txn, c->d_grant};
+                    c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
@@ -962,13 +964,11 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
     if (!c || (n_acc && !acc) || !out_commit) return DV_ERR_ARG;
     if (n_acc > c->cfg.max_acc || n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     uint32_t max_len = 0;
-    if (txn_begin) {  // CSR form must agree with acc[].txn_seq
+    if (txn_begin) {  // CSR form: checked here per txn, against acc[].txn_seq on the device
         if (txn_begin[0] != 0 || txn_begin[n_txn] != n_acc) return DV_ERR_ARG;
         for (uint32_t t = 0; t < n_txn; t++) {
             if (txn_begin[t + 1] < txn_begin[t]) return DV_ERR_ARG;
             max_len = std::max(max_len, txn_begin[t + 1] - txn_begin[t]);
-            for (uint64_t a = txn_begin[t]; a < txn_begin[t + 1]; a++)
-                if (acc[a].txn_seq != t) return DV_ERR_TXN_RANGE;
         }
         if (max_len > kMaxPos) return DV_ERR_ARG;
     }
@@ -983,12 +983,19 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
         if (!r) r = dalloc(&c->d_txn, A);
         if (!r) r = dalloc(&c->d_commit, c->cfg.max_txn);
         if (!r && c->cfg.cc_alg == DV_CALVIN) r = dalloc(&c->d_grant, A);
+        if (!r) r = dalloc(&c->d_tb, (uint64_t)c->cfg.max_txn + 1);
+        if (!r) r = dalloc(&c->split_err, 1);
         if (r) return r;
     }
     if (n_acc) {
         HIPCHK(hipMemcpyAsync(c->d_acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice,
                               c->stream));
-        launch_split_access(c->stream, c->d_acc, n_acc, c->d_keys, c->d_types, c->d_txn, c->d_tables);
+        if (txn_begin)
+            HIPCHK(hipMemcpyAsync(c->d_tb, txn_begin, ((size_t)n_txn + 1) * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemsetAsync(c->split_err, 0, sizeof(uint32_t), c->stream));
+        launch_split_access(c->stream, c->d_acc, n_acc, txn_begin ? c->d_tb : nullptr, n_txn, c->d_keys,
+                            c->d_types, c->d_txn, c->d_tables, c->split_err);
     }
     dv_epoch_dev ep{};
     ep.keys = c->d_keys;
@@ -1001,6 +1008,11 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
     if (r) return r;
+    if (n_acc && txn_begin) {  // a record outside its txn's CSR range
+        uint32_t bad = 0;
+        HIPCHK(hipMemcpy(&bad, c->split_err, sizeof(bad), hipMemcpyDeviceToHost));
+        if (bad) return DV_ERR_TXN_RANGE;
+    }
     if (n_txn)
         HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
     if (calvin && out_grant && n_acc)

@@ -182,6 +182,24 @@ def test_chained_index_table():
         eng.close()
 
 
+def test_host_records_must_match_txn_begin():
+    """dv_epoch_run checks every record's txn_seq against the CSR txn_begin
+    (on the device); a record placed in another txn's range is rejected."""
+    g = YCSBQueryGenerator(1 << 12, zipf_theta=0.6)
+    e = g.gen(500, 5)
+    eng = CCEngine(dvcc.NO_WAIT, 500, 5000)
+    eng.load_ycsb_partition(1 << 12)
+    acc = e.to_access_array()
+    tb = np.ascontiguousarray(e.txn_begin, dtype=np.uint32)
+    commit = np.zeros(500, np.uint8)
+    st = eng.run_epoch_host(acc, tb, e.n_acc, e.n_txn, commit)
+    assert st.n_txn == 500
+    acc["txn_seq"][int(tb[7])] = 8  # first access of txn 7 claims txn 8
+    with pytest.raises(dvcc.DvccError):
+        eng.run_epoch_host(acc, tb, e.n_acc, e.n_txn, commit)
+    eng.close()
+
+
 @pytest.mark.parametrize("order", ["bucket", "shuffled"])
 def test_direct_index_table(order):
     """dv_load_table with one key per bucket: keys loaded in bucket order give
