@@ -81,6 +81,9 @@ def lib():
                                    ctypes.c_uint32, u32p, u64p, u8p, u8p, u32p, ctypes.c_int,
                                    P(EpochStats)]
         L.or_epoch_run.restype = ctypes.c_int
+        L.or_mt_epoch_run.argtypes = [ctypes.c_void_p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint32, u32p,
+                                      u64p, u8p, ctypes.c_int, u64p, u64p]
+        L.or_mt_epoch_run.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -141,6 +144,18 @@ class MultiIndex:
             lib().or_index_free(self.ix)
         except Exception:
             pass
+
+
+def mt_epoch_run(ix, f0, lock, n_txn, tb, keys, types, threads):
+    """SURVEY.md 8(d)(ii) baseline: Deneva-style multi-threaded NO_WAIT
+    (oracle/mt_engine.c).  lock: uint32 zeros, one per row.  Returns
+    (committed, read digest); its aborts depend on the interleaving."""
+    c, d = ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib().or_mt_epoch_run(ix, _p(f0, ctypes.c_uint64), _p(lock, ctypes.c_uint32), len(f0), n_txn,
+                               _p(tb, ctypes.c_uint32), _p(keys, ctypes.c_uint64), _p(types, ctypes.c_uint8),
+                               threads, ctypes.byref(c), ctypes.byref(d))
+    assert rc == 0, rc
+    return c.value, d.value
 
 
 def epoch_run(cc, ix, f0, n_txn, tb, keys, types, want_grant=False, occ_literal=False):

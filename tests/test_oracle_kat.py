@@ -279,3 +279,23 @@ def test_empty_epoch():
     c, g, st = O.epoch_run(O.CALVIN, tab.ix, tab.f0.copy(), 0, np.zeros(1, np.uint32),
                            np.zeros(1, np.uint64), np.zeros(1, np.uint8), want_grant=True)
     assert st.committed == 0 and len(c) == 0
+
+
+def test_mt_baseline_engine():
+    """SURVEY.md 8(d)(ii) CPU baseline: one worker runs txns one at a time, so
+    nothing conflicts and everything commits; several workers under zipf 0.9
+    abort some txns, and every lock is free again at the end."""
+    rows, n = 1 << 12, 4000
+    p = O.ycsb_params(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    keys, types, tb = O.ycsb_gen(p, 11, 0, n)
+    for threads in (1, 4):
+        tab = O.YcsbTable(rows)
+        f0 = tab.f0.copy()
+        lock = np.zeros(rows, np.uint32)
+        committed, _ = O.mt_epoch_run(tab.ix, f0, lock, n, tb, keys, types, threads)
+        assert not lock.any()
+        if threads == 1:
+            assert committed == n
+            assert (f0[keys[types == O.WR].astype(np.int64)] == 0).all()
+        else:
+            assert 0 < committed <= n
