@@ -22,7 +22,7 @@ ARCH = os.environ.get("DVCC_OFFLOAD_ARCH", "gfx950")
 
 HEADERS = [os.path.join(INCLUDE, "dvcc.h"), os.path.join(CSRC, "dvcc_internal.h"),
            os.path.join(CSRC, "dvcc_common.h")]
-HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_carry.hip", "dvcc_runtime.hip"]
+HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_carry.hip", "dvcc_comm.hip", "dvcc_runtime.hip"]
 CPP_SRCS = ["ycsb_gen.cpp"]
 
 
@@ -59,7 +59,8 @@ def build(force=False, verbose_resources=False):
             _run(["g++", "-O2", "-std=c++17", "-fPIC", "-ffp-contract=off", "-I", INCLUDE,
                   "-c", src, "-o", obj])
     if force or _newer(LIB, objs):
-        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs)
+        _run(["hipcc", f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+             + ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"])
     return LIB
 
 

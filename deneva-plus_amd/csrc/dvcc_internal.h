@@ -206,6 +206,15 @@ uint32_t async_try_limit(uint32_t G);
 bool round_el32(uint32_t n_txn, uint32_t slog);
 
 // ---- execution and outputs (dvcc_kernels.hip)
+// ---- runtime accessors for the RCCL driver (dvcc_comm.hip)
+struct DvComm;  // defined in dvcc_comm.hip
+}  // namespace dvcc
+dvcc::DvComm *&ctx_comm(dv_ctx *c);
+hipStream_t ctx_stream(dv_ctx *c);
+const dv_config &ctx_config(dv_ctx *c);
+void comm_free(dvcc::DvComm *m);
+namespace dvcc {
+
 // abort carry-over (dvcc_carry.hip): the accesses of the txns whose status is
 // not committed, in sequence order and renumbered from 0, capped at max_txn
 // txns, into o*; tot (3 words, device) = carried txns, their accesses, and the

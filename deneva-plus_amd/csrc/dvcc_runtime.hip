@@ -65,6 +65,7 @@ struct dv_ctx {
     uint32_t *carry_b = nullptr;                     // abort carry-over: block counts (2 x carry_nb)
     uint32_t carry_nb = 0;
     uint32_t *carry_tot = nullptr;                   // its totals (3 words)
+    DvComm *comm = nullptr;                          // RCCL communicator (dv_comm_init)
     uint32_t round_tag = 0;                          // descriptor tag of the last pass
     uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
@@ -224,6 +225,10 @@ int sync_counters(dv_ctx *c) {
 
 }  // namespace
 
+DvComm *&ctx_comm(dv_ctx *c) { return c->comm; }
+hipStream_t ctx_stream(dv_ctx *c) { return c->stream; }
+const dv_config &ctx_config(dv_ctx *c) { return c->cfg; }
+
 extern "C" {
 
 const char *dv_strerror(int code) {
@@ -252,6 +257,8 @@ int dv_device_count(int *count) {
 void dv_close(dv_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    comm_free(c->comm);
+    c->comm = nullptr;
     for (auto &t : c->tab) {
         dfree(t.ix);
         dfree(t.bstart);

@@ -25,6 +25,14 @@ def _ptr(a):
     return ctypes.c_void_p(int(a.data_ptr()))  # torch tensor (device memory)
 
 
+def comm_unique_id():
+    """A fresh RCCL unique id (128 bytes) for dv_comm_init; make it on rank 0
+    and hand it to the other ranks."""
+    buf = ctypes.create_string_buffer(128)
+    L.check(L.lib().dv_comm_unique_id(buf), "dv_comm_unique_id")
+    return buf.raw
+
+
 @dataclass
 class Epoch:
     """One host-side epoch in sequence order."""
@@ -211,6 +219,20 @@ class CCEngine:
         desc = dep.desc()
         L.check(L.lib().dv_epoch_run_device(self._ctx, ctypes.byref(desc), _ptr(d_commit),
                                             _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
+        return st
+
+    # ---- partitioned epochs over RCCL from the engine (dv_comm_init)
+    def comm_init(self, unique_id, nranks, rank):
+        """unique_id: the 128 bytes comm_unique_id() returned on rank 0."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        L.check(L.lib().dv_comm_init(self._ctx, buf, nranks, rank), "dv_comm_init")
+
+    def run_epoch_part(self, home, txns_per_rank, d_commit=None):
+        """One partitioned epoch from this rank's client batch (DeviceEpoch,
+        txn ids local); d_commit: nranks * txns_per_rank device bytes."""
+        st = L.Stats()
+        L.check(L.lib().dv_epoch_run_part(self._ctx, ctypes.byref(home.desc()), txns_per_rank,
+                                          _ptr(d_commit), ctypes.byref(st)), "dv_epoch_run_part")
         return st
 
     def carry(self, dep, max_txn=None):

@@ -219,6 +219,22 @@ int dv_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, uint8_t *d_commit,
  * timestamp). */
 int dv_epoch_carry(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch_dev *out);
 
+/* RCCL from the engine: one process per GPU, rank r
+ * owns partition r (the context's part_cnt / part_id must equal nranks /
+ * rank).  Rank 0 makes the id (128 bytes) and the caller hands it to every
+ * rank (ncclGetUniqueId / ncclCommInitRank).  dv_epoch_run_part runs a whole
+ * partitioned epoch from this rank's client batch `home` (txn ids 0..n_txn-1,
+ * global sequence number rank * txns_per_rank + id): split by owner = key %
+ * nranks on the device, one all-to-all of the access records, decision
+ * rounds closed by all-reduce(MAX) of the undecided txns' verdict bytes
+ * (queued two rounds ahead), execution of this rank's rows.  d_commit: device
+ * bytes, one per global txn (nranks * txns_per_rank).  Same decisions as
+ * deneva-plus_amd/dvcc/partitioned.py over torch.distributed. */
+int dv_comm_unique_id(void *id_out);
+int dv_comm_init(dv_ctx *ctx, const void *unique_id, int nranks, int rank);
+int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
+                      dv_stats *st);
+
 /* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
  * same txn statuses after each round, hence the same list of undecided txns
  * (ascending).  dv_epoch_round_local writes this partition's verdict byte for

@@ -258,3 +258,33 @@ def test_gpu_runner_single_rank_process_group():
         eng.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC, dvcc.CALVIN])
+def test_rccl_engine_driver_single_rank(cc):
+    """dv_comm_init + dv_epoch_run_part (RCCL called from the engine) on a
+    one-rank communicator: the owner split, all-to-all, list all-reduces and
+    lagged rounds run for real and must decide exactly as the single-GPU
+    path and the oracle.  (More ranks need more GPUs: the Python driver's
+    protocol, which this mirrors, is covered with gloo above.)"""
+    import torch
+    rows, n_txn = 1 << 14, 6000
+    gen = dvcc.YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    e = gen.gen(n_txn, dvcc.epoch_seed(0, 3))
+    ref = dvcc.CCEngine(cc, n_txn, e.n_acc)
+    ref.load_ycsb_partition(rows)
+    c_ref = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    st_ref = ref.run_epoch_device(dvcc.DeviceEpoch(e), c_ref)
+    eng = dvcc.CCEngine(cc, n_txn, e.n_acc, part_cnt=1, part_id=0)
+    eng.load_ycsb_partition(rows)
+    eng.comm_init(dvcc.comm_unique_id(), 1, 0)
+    c = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    for _ in range(2):  # the communicator and buffers are reused across epochs
+        eng.load_ycsb_partition(rows)
+        st = eng.run_epoch_part(dvcc.DeviceEpoch(e), n_txn, c)
+        assert torch.equal(c, c_ref)
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt)
+    eng.close()
+    ref.close()
