@@ -131,7 +131,11 @@ __device__ __forceinline__ Agg desc_agg(uint64_t d) {
 }
 
 // called by ALL lanes of wave 0 of the tile; returns the tile's exclusive prefix
-template <class Op>
+// and publishes its inclusive one.  HEAD: only the OR value in front of the
+// tile -- the walk stops at the nearest tile holding a queue head (usually the
+// one before), nothing inclusive is published, and only .v of the result is
+// the prefix's; a second, full call follows.
+template <class Op, bool HEAD = false>
 __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, uint32_t lane,
                          Counters *ctr) {
     Agg pre{0u, 0u, 0u};
@@ -156,7 +160,8 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
         }
         // only the descriptors up to the nearest inclusive one are needed
         // (t < 0 acts as one); later ones may still be unpublished
-        const uint64_t incmask = __ballot(ready && (t < 0 || desc_state(d) == D_INC));
+        const uint64_t incmask =
+            __ballot(ready && (t < 0 || desc_state(d) == D_INC || (HEAD && desc_agg(d).f)));
         const uint32_t stop = incmask ? (uint32_t)__builtin_ctzll(incmask) : 64u;
         const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
         if (__ballot(!ready) & need) {
@@ -176,6 +181,7 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
         if (stop < 64) break;
         j -= 64;
     }
+    if (HEAD) return pre;
     if (lane == 0)
         __hip_atomic_store(&desc[tile], desc_pack(tag, D_INC, Op::comb(pre, agg)), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);

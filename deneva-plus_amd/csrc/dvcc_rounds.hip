@@ -178,8 +178,9 @@ struct TileLds {
     uint64_t prev;
     Agg wt[Geo<EIn>::kWaves];
     RAgg rw[Geo<EIn>::kWaves];
-    Agg pre;
+    Agg pre;        // .v: the OR value in front of the tile
     uint32_t tot;
+    uint32_t gpos;  // the tile's output offset (count prefix)
 };
 
 // coalesced 16-byte loads of [base, base + tile_n) into the padded LDS image
@@ -321,21 +322,34 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     const Agg inc = wave_incl<OpPlain>(a, lane);
     if (lane == 63) sh.wt[wave] = inc;
     __syncthreads();
+    // The decisions need only the OR in front of the tile (a walk back to the
+    // nearest tile holding a head); the output offset needs the full count
+    // prefix.  Wave 0 fetches the first, releases the other waves to decide,
+    // then walks on for the second while they work.
+    Agg bagg{0u, 0u, 0u};
     if (wave == 0) {
-        Agg bagg = sh.wt[0];
+        bagg = sh.wt[0];
         for (int w = 1; w < G::kWaves; w++) bagg = OpPlain::comb(bagg, sh.wt[w]);
 #ifdef DVCC_EXP_NO_LOOKBACK
         const Agg pre{0u, 0u, tile * G::kTile};
 #else
-        const Agg pre = look_back<OpPlain>(desc, tile, tag, bagg, lane, ctr);
+        const Agg pre = look_back<OpPlain, true>(desc, tile, tag, bagg, lane, ctr);
 #endif
         if (lane == 0) {
-            sh.pre = pre;
+            sh.pre = Agg{pre.f, pre.v, 0u};
             sh.tot = bagg.c;
             if (tile == 0) reset_und(und_reset, ctr);  // re-counted by this round's settle / apply
         }
     }
     __syncthreads();
+    if (wave == 0) {
+#ifdef DVCC_EXP_NO_LOOKBACK
+        const uint32_t gpos = tile * G::kTile;
+#else
+        const uint32_t gpos = look_back<OpPlain>(desc, tile, tag, bagg, lane, ctr).c;
+#endif
+        if (lane == 0) sh.gpos = gpos;
+    }
     Agg wpre{0u, 0u, 0u};  // this wave's prefix within the tile
     for (uint32_t w = 0; w < wave; w++) wpre = OpPlain::comb(wpre, sh.wt[w]);
     const Agg lex = wave_excl_from_incl<OpPlain>(inc, lane);
@@ -357,7 +371,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     }
     __syncthreads();
     // coalesced write-out of the compacted tile
-    const uint32_t tot = sh.tot, gpos = sh.pre.c;
+    const uint32_t tot = sh.tot, gpos = sh.gpos;
     for (uint32_t k = tid; k < tot; k += G::kThreads) el_out[gpos + k] = s_out[k];
     if (tile == ntiles - 1 && tid == 0) *n_out = gpos + tot;
     __syncthreads();  // the LDS tile is free again
