@@ -126,6 +126,44 @@ def cpu_baseline_mt(epochs, rows, seconds):
                       "restatement of the reference CC, not the reference binary"}
 
 
+def closed_loop_leg(eng, gen, n_txn, k, d_commit):
+    """Closed loop with retries: every epoch holds n_txn
+    txns, the previous epoch's aborted ones first (dv_epoch_carry), new ones
+    from a pre-generated pool filling the rest.  Committed txns/s over k
+    epochs, the carry-over and epoch assembly included."""
+    pool_n = 2 * n_txn  # new txns are drawn in order, wrapping around
+    pool = gen.gen(pool_n, dvcc.epoch_seed(0, 999))
+    dpool = dvcc.DeviceEpoch(pool)
+    tb = pool.txn_begin.astype(np.int64)
+    nxt = 0
+
+    def fresh(m):
+        nonlocal nxt
+        if nxt + m > pool_n:
+            nxt = 0
+        a, b = int(tb[nxt]), int(tb[nxt + m])
+        d = dvcc.DeviceEpoch.from_tensors(dpool.keys[a:b], dpool.types[a:b], dpool.acc_txn[a:b] - nxt, m,
+                                          max_txn_acc=dpool.max_txn_acc)
+        nxt += m
+        return d
+
+    cur = fresh(n_txn)
+    eng.run_epoch_device(cur, d_commit)  # warm: the first epoch has nothing carried
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    committed = carried = 0
+    for _ in range(k):
+        c = eng.carry(cur, n_txn)
+        carried += c.n_txn
+        cur = dvcc.DeviceEpoch.concat(c, fresh(n_txn - c.n_txn)) if c.n_txn < n_txn else c
+        committed += eng.run_epoch_device(cur, d_commit).committed
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return {"committed_per_s": committed / el, "ms_per_epoch": el / k * 1e3, "epochs": k,
+            "carried_per_epoch": carried / k,
+            "note": "aborted txns retried in the next epoch ahead of new ones (one-epoch penalty)"}
+
+
 def e2e_host_leg(eng, epochs, k):
     """SURVEY.md 8(d)'s second reading: dv_epoch_run from host buffers, so
     the H2D copy of the 16-B access records is inside the time (pinned host
@@ -308,6 +346,7 @@ def main():
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
+        out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn, min(a.steps, 10), d_commit)
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         # the single-thread E-schedule port (decision-identical) and, for
         # NO_WAIT, the multi-threaded engine, which is then the baseline

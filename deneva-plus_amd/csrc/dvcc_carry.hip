@@ -13,7 +13,7 @@
 
 namespace dvcc {
 
-constexpr uint32_t kCarryTpb = kBlock * 4;  // txns per block: 4 per thread
+constexpr uint32_t kCarryTpb = kBlock;  // txns per block: one per thread
 
 __device__ __forceinline__ bool carried(const uint8_t *status, uint32_t t) {
     return status[t] != ST_COMMIT;  // aborted (nothing is undecided after the rounds)
@@ -26,16 +26,9 @@ __global__ __launch_bounds__(kBlock) void k_carry_count(const uint8_t *__restric
                                                         uint32_t n_txn, uint32_t *__restrict__ bt,
                                                         uint32_t *__restrict__ ba) {
     __shared__ uint32_t lds4[4];
-    uint32_t nt = 0, na = 0;
-    const uint32_t t0 = blockIdx.x * kCarryTpb + threadIdx.x * 4;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t t = t0 + k;
-        if (t < n_txn && carried(status, t)) {
-            nt++;
-            na += tb_end[t] - tb_start[t];
-        }
-    }
+    const uint32_t t = blockIdx.x * kCarryTpb + threadIdx.x;
+    const bool cr = t < n_txn && carried(status, t);
+    const uint32_t nt = cr ? 1u : 0u, na = cr ? tb_end[t] - tb_start[t] : 0u;
     uint32_t tt = 0, ta = 0;
     (void)block_excl_scan256(nt, lds4, &tt);
     (void)block_excl_scan256(na, lds4, &ta);
@@ -67,8 +60,11 @@ __global__ __launch_bounds__(kBlock) void k_carry_scan(uint32_t *__restrict__ bt
     }
 }
 
-// every carried txn with a new id below max_txn copies its accesses; the last
-// one reports the carried epoch's size (tot[0] txns, tot[1] accesses)
+// every carried txn with a new id below max_txn is copied; the last one
+// reports the carried epoch's size (tot[0] txns, tot[1] accesses).  A wave
+// holds 64 consecutive txns, whose carried accesses are contiguous in the
+// output: its lanes copy them together (a prefix sum of the lengths picks
+// each access's txn), so reads and writes are coalesced.
 __global__ __launch_bounds__(kBlock) void k_carry_copy(
     const uint8_t *__restrict__ status, const uint32_t *__restrict__ tb_start,
     const uint32_t *__restrict__ tb_end, uint32_t n_txn, const uint32_t *__restrict__ bt,
@@ -77,38 +73,48 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
     uint8_t *__restrict__ otypes, uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
     uint32_t *__restrict__ tot) {
     __shared__ uint32_t lds4[4];
-    const uint32_t t0 = blockIdx.x * kCarryTpb + threadIdx.x * 4;
-    uint32_t nt = 0, na = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t t = t0 + k;
-        if (t < n_txn && carried(status, t)) {
-            nt++;
-            na += tb_end[t] - tb_start[t];
-        }
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t t = blockIdx.x * kCarryTpb + threadIdx.x;
+    const bool cr = t < n_txn && carried(status, t);
+    const uint32_t a0 = cr ? tb_start[t] : 0u;
+    uint32_t len = cr ? tb_end[t] - a0 : 0u;
+    const uint32_t id = bt[blockIdx.x] + block_excl_scan256(cr ? 1u : 0u, lds4, nullptr);
+    const uint32_t pos = ba[blockIdx.x] + block_excl_scan256(len, lds4, nullptr);
+    const uint32_t total_txn = tot[2];  // carried txns before the cap (k_carry_total)
+    const uint32_t last = total_txn < max_txn ? total_txn : max_txn;
+    if (cr && id < max_txn && id + 1 == last) {
+        tot[0] = last;
+        tot[1] = pos + len;
     }
-    uint32_t id = bt[blockIdx.x] + block_excl_scan256(nt, lds4, nullptr);
-    uint32_t pos = ba[blockIdx.x] + block_excl_scan256(na, lds4, nullptr);
-    const uint32_t total_txn = tot[2];  // carried txns before the cap (k_carry_scan's grand total)
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t t = t0 + k;
-        if (t >= n_txn || !carried(status, t)) continue;
-        const uint32_t a0 = tb_start[t], len = tb_end[t] - a0;
-        if (id < max_txn) {
-            for (uint32_t j = 0; j < len; j++) {
-                okeys[pos + j] = keys[a0 + j];
-                otypes[pos + j] = types[a0 + j];
-                otxn[pos + j] = id;
-                if (tables) otables[pos + j] = tables[a0 + j];
-            }
-            const uint32_t last = total_txn < max_txn ? total_txn : max_txn;
-            if (id + 1 == last) {
-                tot[0] = last;
-                tot[1] = pos + len;
-            }
+    if (!cr || id >= max_txn) len = 0;  // (ids grow with t: the cap cuts a suffix)
+    uint32_t incl = len;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(incl, off, 64);
+        if (lane >= (uint32_t)off) incl += o;
+    }
+    const uint32_t pre = incl - len, wtot = __shfl(incl, 63, 64);
+    // the wave's first carried access goes where its first carried txn's does
+    const uint64_t first = __ballot(len != 0);
+    if (!first) return;
+    const uint32_t wpos = __shfl(pos, (int)__builtin_ctzll(first), 64);
+    for (uint32_t g0 = 0; g0 < wtot; g0 += 64) {  // wave-uniform trips: shuffles read every lane
+        const uint32_t g = g0 + lane;
+        uint32_t src = 0;
+#pragma unroll
+        for (uint32_t w = 32; w > 0; w >>= 1) {
+            const uint32_t cand = src + w;
+            const uint32_t pv = __shfl(pre, (int)(cand & 63u), 64);
+            if (cand < 64 && pv <= g) src = cand;
         }
-        id++;
-        pos += len;
+        const uint32_t sa0 = __shfl(a0, (int)src, 64), spre = __shfl(pre, (int)src, 64);
+        const uint32_t sid = __shfl(id, (int)src, 64);
+        if (g >= wtot) continue;
+        const uint32_t in = sa0 + (g - spre), o = wpos + g;
+        okeys[o] = keys[in];
+        otypes[o] = types[in];
+        otxn[o] = sid;
+        if (tables) otables[o] = tables[in];
     }
 }
 

@@ -291,3 +291,23 @@ def test_medium_epoch_tail_only(cc):
 def test_medium_epoch_el64(cc):
     g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
     _check(cc, 1 << 20, [g.gen(1 << 16, 97)], el64=True)
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_randomized_sweep(case):
+    """Seeded random configurations across sizes, request counts, skew, write
+    mixes, CC algorithms and the decision-path knobs (tail kernel, 64-bit
+    elements, asynchronous rounds), each bit-exact against the oracle over two
+    consecutive epochs (table state carried)."""
+    rng = np.random.default_rng(1000 + case)
+    R = int(rng.integers(1, 17))
+    rows = int(rng.integers(max(R, 16), 1 << 16))
+    n_txn = int(rng.integers(1, 8000))
+    theta = float(rng.choice([0.0, 0.3, 0.6, 0.9, 0.99]))
+    cc = CCS[case % len(CCS)]
+    g = YCSBQueryGenerator(rows, req_per_query=R, zipf_theta=theta,
+                           txn_write_perc=float(rng.choice([0.0, 0.5, 1.0])),
+                           tup_write_perc=float(rng.choice([0.1, 0.5, 0.9])))
+    knobs = dict(tail=bool(rng.integers(0, 2)), el64=bool(rng.integers(0, 2)),
+                 asynchronous=bool(rng.integers(0, 2)))
+    _check(cc, rows, [g.gen(n_txn, 77 + case), g.gen(n_txn, 78 + case)], **knobs)
