@@ -166,7 +166,10 @@ __device__ Agg look_back(uint64_t *desc, uint32_t tile, uint32_t tag, Agg agg, u
         const uint64_t need = stop >= 63 ? ~0ull : ((2ull << stop) - 1);
         if (__ballot(!ready) & need) {
             if (++spins > kSpinLimit) {
-                if (lane == 0) set_err(ctr, ERRB_SPIN);
+                if (lane == 0) {
+                    set_err(ctr, ERRB_SPIN);
+                    atomicMax(&ctr->spin_site, 1u);
+                }
                 break;
             }
             __builtin_amdgcn_s_sleep(1);

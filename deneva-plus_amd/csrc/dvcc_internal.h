@@ -69,6 +69,7 @@ struct Counters {
     uint32_t async_iters;     // most iterations any asynchronous workgroup ran
     uint32_t async_r0;        // round the accepted asynchronous launch started at (0: none)
     uint32_t async_declined;  // asynchronous tries that found the live set too large
+    uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
     uint32_t log_live[kRoundLog];  // per round: live accesses entering it

@@ -750,7 +750,10 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
         const uint32_t U2 = sh.ucnt;
         round++;
         if (U2 >= U) {  // the lowest undecided txn must have decided
-            if (tid == 0) set_err(ctr, ERRB_SPIN);
+            if (tid == 0) {
+                set_err(ctr, ERRB_SPIN);
+                atomicMax(&ctr->spin_site, 3u);
+            }
             ok = false;
         }
         U = U2;
@@ -1013,7 +1016,10 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         if (!s_moved[p]) __builtin_amdgcn_s_sleep(8);
     }
     if (tid == 0) {
-        if (it >= max_iters) set_err(ctr, ERRB_SPIN);
+        if (it >= max_iters) {
+            set_err(ctr, ERRB_SPIN);
+            atomicMax(&ctr->spin_site, 2u);
+        }
         atomicMax(&ctr->async_iters, it);
     }
 }

@@ -775,7 +775,12 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     c->phase = 0;
     if (r) return r;
     r = err_from_bits(c->h_ctr->err);
-    if (r) return r;
+    if (r) {
+        if (c->h_ctr->err & ERRB_SPIN)
+            std::fprintf(stderr, "dvcc: a bounded wait ran out (site %u: 1 look-back, 2 asynchronous rounds, "
+                         "3 tail)\n", c->h_ctr->spin_site);
+        return r;
+    }
     if (!calvin && c->h_ctr->async_r0) {  // an asynchronous launch decided the rest
         uint32_t left = 0;
         for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
