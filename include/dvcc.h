@@ -91,7 +91,13 @@ extern "C" {
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
 #define DV_FLAG_NO_ASYNC 8u /* never finish the decision rounds in the
-                               asynchronous multi-workgroup kernel (testing) */
+                               asynchronous multi-workgroup kernel.  That
+                               kernel needs every workgroup of its launch
+                               resident at once, so it assumes the GPU to
+                               itself: contexts that run epochs concurrently
+                               on one GPU (threads or processes) set this
+                               flag, or two such launches can each hold half
+                               the CUs until their bounded wait runs out */
 
 typedef struct dv_ctx dv_ctx;
 
