@@ -17,6 +17,7 @@
 #include <vector>
 
 #include "dvcc_common.h"
+#include "dvcc_tpcc.h"
 
 using namespace dvcc;
 
@@ -42,6 +43,18 @@ struct dv_ctx {
     uint64_t total_rows = 0;
     uint64_t *f0 = nullptr;    // hot column, global row id
     uint64_t *pkey = nullptr;  // primary key per row (row_t::get_primary_key)
+    uint64_t *col1 = nullptr, *col2 = nullptr;  // DV_TPCC: state columns 1 and 2
+
+    // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
+    // execution scratch, and the operation words / o_id output of this epoch
+    uint64_t *tp_keys = nullptr;
+    uint8_t *tp_tables = nullptr;
+    uint32_t *tp_flag = nullptr, *tp_scan = nullptr, *tp_dhead = nullptr;
+    void *tp_tmp = nullptr;
+    size_t tp_tmp_bytes = 0;
+    uint64_t tp_dhead_cap = 0;
+    const uint64_t *tp_args = nullptr;
+    uint64_t *tp_oid = nullptr;
 
     // workspace (capacities from cfg)
     uint64_t *pairs[2] = {nullptr, nullptr};
@@ -268,7 +281,9 @@ void dv_close(dv_ctx *c) {
                     c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
-                    c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err};
+                    c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
+                    c->col1, c->col2, c->tp_keys, c->tp_tables, c->tp_flag, c->tp_scan, c->tp_dhead,
+                    c->tp_tmp};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
@@ -285,6 +300,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (cfg->cc_alg != DV_NO_WAIT && cfg->cc_alg != DV_WAIT_DIE && cfg->cc_alg != DV_OCC &&
         cfg->cc_alg != DV_CALVIN)
         return DV_ERR_ARG;
+    if (cfg->workload != DV_YCSB && cfg->workload != DV_TPCC) return DV_ERR_ARG;
     if (cfg->max_txn == 0 || cfg->max_txn > kMaxTxn || cfg->max_acc == 0 ||
         cfg->max_acc > kMaxAcc || cfg->part_cnt == 0 || cfg->part_id >= cfg->part_cnt)
         return DV_ERR_ARG;
@@ -425,21 +441,36 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     HIPCHK(hipSetDevice(c->cfg.device));
     // grow the global hot column / primary-key arrays (load-time only)
     const uint64_t new_total = c->total_rows + capacity_rows;
-    uint64_t *nf0 = nullptr, *npk = nullptr;
+    const bool cols = c->cfg.workload == DV_TPCC;
+    uint64_t *nf0 = nullptr, *npk = nullptr, *nc1 = nullptr, *nc2 = nullptr;
     int r = dalloc(&nf0, new_total);
     if (!r) r = dalloc(&npk, new_total);
-    if (r) { dfree(nf0); return r; }
+    if (!r && cols) r = dalloc(&nc1, new_total);
+    if (!r && cols) r = dalloc(&nc2, new_total);
+    if (r) { dfree(nf0); dfree(npk); dfree(nc1); return r; }
     if (c->total_rows) {
         HIPCHK(hipMemcpyAsync(nf0, c->f0, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(npk, c->pkey, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        if (cols) {
+            HIPCHK(hipMemcpyAsync(nc1, c->col1, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(nc2, c->col2, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        }
     }
     HIPCHK(hipMemsetAsync(nf0 + c->total_rows, 0, capacity_rows * 8, c->stream));
     HIPCHK(hipMemsetAsync(npk + c->total_rows, 0xFF, capacity_rows * 8, c->stream));
+    if (cols) {
+        HIPCHK(hipMemsetAsync(nc1 + c->total_rows, 0, capacity_rows * 8, c->stream));
+        HIPCHK(hipMemsetAsync(nc2 + c->total_rows, 0, capacity_rows * 8, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     dfree(c->f0);
     dfree(c->pkey);
+    dfree(c->col1);
+    dfree(c->col2);
     c->f0 = nf0;
     c->pkey = npk;
+    c->col1 = nc1;
+    c->col2 = nc2;
     t.created = true;
     t.cap_rows = capacity_rows;
     t.row_base = c->total_rows;
@@ -570,6 +601,53 @@ int dv_read_table(dv_ctx *c, uint32_t table, uint64_t first_row, uint64_t n, uin
     HIPCHK(hipMemcpyAsync(out_f0, c->f0 + t.row_base + first_row, n * 8, hipMemcpyDeviceToHost,
                           c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+// ---------------------------------------------------------------- TPC-C tables
+int dv_load_table_cols(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_t *col0,
+                       const uint64_t *col1, const uint64_t *col2, uint64_t n) {
+    if (!c || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
+    int r = dv_load_table(c, table, keys, col0, n);
+    if (r || !n) return r;
+    const HostTable &t = c->tab[table];
+    if (col1) HIPCHK(hipMemcpy(c->col1 + t.row_base, col1, n * 8, hipMemcpyHostToDevice));
+    if (col2) HIPCHK(hipMemcpy(c->col2 + t.row_base, col2, n * 8, hipMemcpyHostToDevice));
+    return DV_OK;
+}
+
+int dv_read_table_col(dv_ctx *c, uint32_t table, uint32_t col, uint64_t first_row, uint64_t n,
+                      uint64_t *out) {
+    if (!c || col > 2 || (col && c->cfg.workload != DV_TPCC)) return DV_ERR_ARG;
+    if (col == 0) return dv_read_table(c, table, first_row, n, out);
+    if (table >= kMaxTables || (n && !out)) return DV_ERR_ARG;
+    const HostTable &t = c->tab[table];
+    if (!t.created) return DV_ERR_NO_TABLE;
+    if (first_row + n > t.cap_rows) return DV_ERR_ARG;
+    if (!n) return DV_OK;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const uint64_t *src = (col == 1 ? c->col1 : c->col2) + t.row_base + first_row;
+    HIPCHK(hipMemcpyAsync(out, src, n * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+// TPCCWorkload::init (tpcc_wl.cpp:95-200): the six tables of this context's
+// partition, chained IndexHash tables with one bucket per row (key % rows)
+int dv_tpcc_load(dv_ctx *c, const dv_tpcc_params *p, uint64_t seed) {
+    if (!c || !p || c->cfg.workload != DV_TPCC || p->part_cnt != c->cfg.part_cnt) return DV_ERR_ARG;
+    const uint32_t part = c->cfg.part_id;
+    for (uint32_t tb = DV_TPCC_WAREHOUSE; tb <= DV_TPCC_CUST_LAST; tb++) {
+        uint64_t n = 0;
+        int r = dv_tpcc_table_rows(p, part, tb, &n);
+        if (r) return r;
+        const uint64_t cap = n ? n : 1;
+        std::vector<uint64_t> k(cap), a(cap), b(cap), d(cap);
+        r = dv_tpcc_table(p, seed, part, tb, k.data(), a.data(), b.data(), d.data());
+        if (!r) r = dv_create_table(c, tb, cap, cap, DV_HASH_MOD);
+        if (!r) r = dv_load_table_cols(c, tb, k.data(), a.data(), b.data(), d.data(), n);
+        if (r) return r;
+    }
     return DV_OK;
 }
 
@@ -762,7 +840,30 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     if (!c || c->phase != 1) return DV_ERR_STATE;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     rec(c, 4);
-    if (calvin)
+    if (c->cfg.workload == DV_TPCC) {
+        if (!c->tp_args) { c->phase = 0; return DV_ERR_STATE; }  // only through dv_tpcc_epoch_run_device
+        const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
+        TpccExec x{};
+        x.pairs = c->pairs[c->sorted];
+        x.n = c->n_acc;
+        x.status = c->status;
+        x.tb_start = c->tb_start;
+        x.args = c->tp_args;
+        x.c0 = c->f0;
+        x.c1 = c->col1;
+        x.c2 = c->col2;
+        x.flag = c->tp_flag;
+        x.scan = c->tp_scan;
+        x.dhead = c->tp_dhead;
+        x.dist_base = dt.row_base;
+        x.dist_rows = dt.created ? dt.cap_rows : 0;
+        x.scan_tmp = c->tp_tmp;
+        x.scan_tmp_bytes = c->tp_tmp_bytes;
+        x.oid = c->tp_oid;
+        x.ctr = c->ctr;
+        if (c->tp_oid) HIPCHK(hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream));
+        launch_tpcc_exec(c->stream, x);
+    } else if (calvin)
         launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey,
                     c->ctr);
     else
@@ -956,6 +1057,57 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
         if (r) { c->phase = 0; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
+}
+
+// One TPC-C epoch: the last-name lookups resolve into a scratch copy of the
+// epoch, which then runs the generic path; dv_epoch_finish executes the
+// committed txns' TPC-C operations (dvcc_tpcc.hip).
+int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint8_t *d_commit,
+                             uint64_t *d_oid, dv_stats *st) {
+    if (!c || !ep || !d_args || (ep->n_acc && !ep->tables) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
+    if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    const uint64_t A = c->cfg.max_acc;
+    int r = DV_OK;
+    if (!c->tp_keys) {
+        r = dalloc(&c->tp_keys, A);
+        if (!r) r = dalloc(&c->tp_tables, A);
+        if (!r) r = dalloc(&c->tp_flag, A);
+        if (!r) r = dalloc(&c->tp_scan, A);
+        if (!r) {
+            c->tp_tmp_bytes = tpcc_scan_bytes(A);
+            r = dalloc(reinterpret_cast<uint8_t **>(&c->tp_tmp), c->tp_tmp_bytes ? c->tp_tmp_bytes : 1);
+        }
+        if (r) return r;
+    }
+    const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
+    const uint64_t drows = dt.created ? dt.cap_rows : 1;
+    if (c->tp_dhead_cap < drows) {
+        dfree(c->tp_dhead);
+        c->tp_dhead = nullptr;
+        r = dalloc(&c->tp_dhead, drows);
+        if (r) return r;
+        c->tp_dhead_cap = drows;
+    }
+    // the resolve kernel reports into the counters that dv_epoch_begin clears:
+    // run it, check, then start the epoch
+    HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(uint32_t), c->stream));
+    launch_tpcc_resolve(c->stream, make_tables(c), ep->keys, ep->tables, ep->n_acc, c->f0, c->tp_keys,
+                        c->tp_tables, c->ctr);
+    uint32_t err = 0;
+    HIPCHK(hipMemcpyAsync(&err, c->ctr, sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    r = err_from_bits(err);
+    if (r) return r;
+    dv_epoch_dev e = *ep;
+    e.keys = c->tp_keys;
+    e.tables = c->tp_tables;
+    c->tp_args = d_args;
+    c->tp_oid = d_oid;
+    r = dv_epoch_run_device(c, &e, d_commit, nullptr, st);
+    c->tp_args = nullptr;
+    c->tp_oid = nullptr;
+    return r;
 }
 
 int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {

@@ -1,0 +1,211 @@
+// dvcc_tpcc.hip -- TPC-C on the epoch path (config E), gfx950.
+//
+// Two pieces around the generic probe -> sort -> decide pipeline:
+//
+// k_tpcc_resolve   Payment's customer-by-last-name lookup (run_payment_4,
+//                  tpcc_txn.cpp:600-626): index_read on i_customer_last
+//                  returns the item list of the key, newest insert first
+//                  (BucketHeader::insert_item prepends, index_hash.cpp:
+//                  197-200), and the txn takes element floor(n/2) (`mid`
+//                  advances on every second element).  The chained index keeps
+//                  equal keys grouped newest first (dv_load_table), so the
+//                  lookup counts the key's entries and takes the middle one;
+//                  its payload (col 0) is the customer's primary key.  The
+//                  access is rewritten to CUSTOMER/custKey in the engine's
+//                  scratch copy of the epoch.
+//
+// execution        run_payment_1/3/5 and new_order_5/9 (tpcc_txn.cpp:530-933)
+//                  for committed txns, over the row-sorted pairs so that every
+//                  row's accesses are visited in sequence order (CALVIN: all
+//                  txns commit and a row's updates apply serially in that
+//                  order; NO_WAIT / WAIT_DIE / OCC: a written row has at most
+//                  one committed accessor that writes it).
+//   - Additive updates (W_YTD, D_YTD, C_BALANCE, C_YTD_PAYMENT, C_PAYMENT_CNT,
+//     S_YTD, S_ORDER_CNT) are integer-valued: every partial sum is an integer
+//     below 2^53, so device-scope atomic adds give the serial result exactly
+//     in any order.  C_PAYMENT_CNT is loaded as the integer 1 and read as a
+//     double (a denormal): denormal + 1.0 rounds to 1.0 either way.
+//   - D_NEXT_O_ID: o_id of a NewOrder = D_NEXT_O_ID + 1 + (committed NewOrders
+//     before it in the district's queue), an exclusive scan of flags over the
+//     sorted pairs minus the scan value at the queue head; then the district
+//     word grows by its count.
+//   - S_QUANTITY is piecewise (s > q + 10 ? s - q : s - q + 91): the queue
+//     head walks its stock row's queue in order (stock queues are short: the
+//     NURand(8191) item choice spreads over max_items x warehouses rows).
+#include <hipcub/hipcub.hpp>
+
+#include "dvcc_internal.h"
+#include "dvcc_common.h"
+#include "dvcc_tpcc.h"
+
+namespace dvcc {
+
+namespace {
+
+constexpr uint64_t kOpMask = (1ull << 56) - 1;
+
+__device__ __forceinline__ uint64_t bucket_of_t(const TableDesc &t, uint64_t key) {
+    return t.hash_kind == DV_HASH_YCSB ? (key / t.part_cnt) % t.nbuckets : key % t.nbuckets;
+}
+
+__global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint64_t *__restrict__ keys,
+                                                         const uint8_t *__restrict__ tables, uint64_t n,
+                                                         const uint64_t *__restrict__ col0,
+                                                         uint64_t *__restrict__ okeys,
+                                                         uint8_t *__restrict__ otables, Counters *ctr) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        uint64_t key = keys[i];
+        uint8_t tb = tables[i];
+        if (tb == DV_TPCC_CUST_LAST) {
+            if (tb >= tabs.n) {
+                set_err(ctr, ERRB_TABLE);
+            } else {
+                const TableDesc &t = tabs.t[tb];
+                const uint64_t bk = bucket_of_t(t, key);
+                uint64_t row = ~0ull;
+                if (t.pkey != nullptr) {
+                    if (t.pkey[bk] == key) row = bk;
+                } else if (t.bstart == nullptr) {
+                    if (t.ix[bk].key == key) row = t.ix[bk].row;
+                } else {
+                    const uint32_t lo = t.bstart[bk], hi = t.bstart[bk + 1];
+                    uint32_t cnt = 0, first = hi;
+                    for (uint32_t j = lo; j < hi; j++) {
+                        if (t.ix[j].key == key) {
+                            if (first == hi) first = j;
+                            cnt++;
+                        }
+                    }
+                    // equal keys are contiguous: the floor(cnt/2)-th of the list
+                    if (cnt) row = t.ix[first + cnt / 2].row;
+                }
+                if (row == ~0ull) {
+                    set_err(ctr, ERRB_KEY);
+                    key = ~0ull;
+                } else {
+                    key = col0[t.row_base + row];
+                }
+                tb = DV_TPCC_CUSTOMER;
+            }
+        }
+        okeys[i] = key;
+        otables[i] = tb;
+    }
+}
+
+// pass 1: additive updates, stock queues, NewOrder flags, district queue heads
+__global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restrict__ pairs, uint64_t n,
+                                                       const uint8_t *__restrict__ status,
+                                                       const uint32_t *__restrict__ tb_start,
+                                                       const uint64_t *__restrict__ args, uint64_t *c0,
+                                                       uint64_t *c1, uint64_t *c2, uint32_t *__restrict__ flag,
+                                                       uint32_t *__restrict__ dhead, uint64_t dist_base,
+                                                       uint64_t dist_rows, Counters *ctr) {
+    unsigned long long wcnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t p = pairs[i];
+        const uint32_t row = pair_row(p), txn = pair_txn(p);
+        const bool com = status[txn] == ST_COMMIT;
+        const uint64_t w = args[tb_start[txn] + pair_pos(p)];
+        const uint32_t op = (uint32_t)(w >> 56);
+        const uint64_t v = w & kOpMask;
+        const bool head = i == 0 || pair_row(pairs[i - 1]) != row;
+        flag[i] = com && op == DV_TOP_NO_DIST ? 1u : 0u;
+        if (head && row >= dist_base && row < dist_base + dist_rows) dhead[row - dist_base] = (uint32_t)i;
+        if (com && (p & 1)) wcnt++;
+        if (com) {
+            switch (op) {
+            case DV_TOP_PAY_WH:    // W_YTD += h_amount (run_payment_1)
+            case DV_TOP_PAY_DIST:  // D_YTD += h_amount (run_payment_3)
+                atomicAdd(reinterpret_cast<double *>(c0 + row), (double)v);
+                break;
+            case DV_TOP_PAY_CUST:  // run_payment_5
+                atomicAdd(reinterpret_cast<double *>(c0 + row), -(double)v);
+                atomicAdd(reinterpret_cast<double *>(c1 + row), (double)v);
+                atomicAdd(reinterpret_cast<double *>(c2 + row), 1.0);
+                break;
+            default:
+                break;
+            }
+        }
+        if (head && op == DV_TOP_NO_STOCK) {  // new_order_9 in queue order
+            uint64_t s = c0[row];
+            int64_t ytd = (int64_t)c1[row], ocnt = (int64_t)c2[row];
+            bool any = false;
+            for (uint64_t j = i; j < n; j++) {
+                const uint64_t q = pairs[j];
+                if (pair_row(q) != row) break;
+                const uint32_t t = pair_txn(q);
+                if (status[t] != ST_COMMIT) continue;
+                const uint64_t qty = args[tb_start[t] + pair_pos(q)] & kOpMask;
+                ytd += (int64_t)qty;
+                ocnt += 1;
+                s = s > qty + 10 ? s - qty : s - qty + 91;
+                any = true;
+            }
+            if (any) {
+                c0[row] = s;
+                c1[row] = (uint64_t)ytd;
+                c2[row] = (uint64_t)ocnt;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) wcnt += __shfl_down(wcnt, off, 64);
+    if ((threadIdx.x & 63) == 0 && wcnt) atomicAdd(&my_slot(ctr).write_cnt, wcnt);
+}
+
+// pass 2: o_id of every committed NewOrder (new_order_5: ++D_NEXT_O_ID)
+__global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict__ pairs, uint64_t n,
+                                                     const uint32_t *__restrict__ flag,
+                                                     const uint32_t *__restrict__ scan,
+                                                     const uint32_t *__restrict__ dhead, uint64_t dist_base,
+                                                     const uint64_t *__restrict__ c1, uint64_t *__restrict__ oid) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        if (!flag[i]) continue;
+        const uint64_t p = pairs[i];
+        const uint32_t row = pair_row(p);
+        const uint32_t rank = scan[i] - scan[dhead[row - dist_base]];
+        if (oid) oid[pair_txn(p)] = c1[row] + 1 + rank;
+    }
+}
+
+// pass 3: D_NEXT_O_ID += committed NewOrders of the district
+__global__ __launch_bounds__(kBlock) void k_tpcc_next_oid(const uint64_t *__restrict__ pairs, uint64_t n,
+                                                          const uint32_t *__restrict__ flag, uint64_t *c1) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        if (flag[i]) atomicAdd(reinterpret_cast<unsigned long long *>(c1 + pair_row(pairs[i])), 1ull);
+}
+
+uint32_t grid_for(uint64_t n) {
+    uint64_t g = (n + kBlock - 1) / kBlock;
+    return (uint32_t)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace
+
+void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *tables,
+                         uint64_t n, const uint64_t *col0, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
+    if (n == 0) return;
+    k_tpcc_resolve<<<grid_for(n), kBlock, 0, s>>>(tabs, keys, tables, n, col0, okeys, otables, ctr);
+}
+
+size_t tpcc_scan_bytes(uint64_t n) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (int)(n ? n : 1));
+    return bytes;
+}
+
+void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
+    if (x.n == 0) return;
+    const uint32_t g = grid_for(x.n);
+    k_tpcc_apply<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2, x.flag,
+                                      x.dhead, x.dist_base, x.dist_rows, x.ctr);
+    size_t bytes = x.scan_tmp_bytes;
+    (void)hipcub::DeviceScan::ExclusiveSum(x.scan_tmp, bytes, x.flag, x.scan, (int)x.n, s);
+    k_tpcc_oid<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.flag, x.scan, x.dhead, x.dist_base, x.c1, x.oid);
+    k_tpcc_next_oid<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.flag, x.c1);
+}
+
+}  // namespace dvcc

@@ -84,6 +84,18 @@ class YcsbParams(ctypes.Structure):
                 ("mpr", ctypes.c_double)]
 
 
+class TpccParams(ctypes.Structure):
+    _fields_ = [("num_wh", ctypes.c_uint32), ("dist_per_wh", ctypes.c_uint32),
+                ("cust_per_dist", ctypes.c_uint32), ("max_items", ctypes.c_uint32),
+                ("max_items_per_txn", ctypes.c_uint32), ("part_cnt", ctypes.c_uint32),
+                ("part_per_txn", ctypes.c_uint32), ("wh_update", ctypes.c_uint32),
+                ("perc_payment", ctypes.c_double), ("mpr", ctypes.c_double)]
+
+
+# TPC-C table ids and operation words (include/dvcc.h)
+T_WAREHOUSE, T_DISTRICT, T_CUSTOMER, T_ITEM, T_STOCK, T_CUST_LAST = 0, 1, 2, 3, 4, 5
+TOP_NONE, TOP_PAY_WH, TOP_PAY_DIST, TOP_PAY_CUST, TOP_NO_DIST, TOP_NO_STOCK = 0, 1, 2, 3, 4, 5
+
 # every symbol include/dvcc.h declares: (name, restype, argtypes)
 _P = ctypes.POINTER
 _vp = ctypes.c_void_p
@@ -117,6 +129,17 @@ SIGNATURES = [
     ("dv_round_log", ctypes.c_int, [_vp, _P(ctypes.c_uint32), _P(ctypes.c_uint32), ctypes.c_uint32]),
     ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_uint32, _vp, _vp, _vp]),
+    ("dv_tpcc_table_rows", ctypes.c_int, [_P(TpccParams), ctypes.c_uint32, ctypes.c_uint32,
+                                          _P(ctypes.c_uint64)]),
+    ("dv_tpcc_load", ctypes.c_int, [_vp, _P(TpccParams), ctypes.c_uint64]),
+    ("dv_tpcc_table", ctypes.c_int, [_P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                     _vp, _vp, _vp, _vp]),
+    ("dv_tpcc_gen", ctypes.c_int, [_P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                   _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("dv_load_table_cols", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_uint64]),
+    ("dv_read_table_col", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
+                                         ctypes.c_uint64, _vp]),
+    ("dv_tpcc_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _vp, _P(Stats)]),
 ]
 
 _lib = None

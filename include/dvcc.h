@@ -37,6 +37,19 @@
  *   dv_read_table
  *   dv_ycsb_gen                 YCSBQueryGenerator::gen_requests_zipf
  *                               (benchmarks/ycsb_query.cpp:29-38, 181-202, 303-376)
+ *   dv_tpcc_load                TPCCWorkload::init / init_tab_* (benchmarks/tpcc_wl.cpp:95-420)
+ *                               with the secondary index i_customer_last
+ *   dv_tpcc_gen                 TPCCQueryGenerator::create_query / gen_payment /
+ *                               gen_new_order (benchmarks/tpcc_query.cpp:26-263) and the
+ *                               access lists of TPCCTxnManager::acquire_locks /
+ *                               run_txn_state (tpcc_txn.cpp:117-244, 500-933)
+ *   dv_tpcc_epoch_run_device    the hot path for TPC-C: the customer-by-last-name
+ *                               index_read + mid selection (tpcc_txn.cpp:600-626),
+ *                               then dv_epoch_run_device's probe/lock/validate, then
+ *                               run_payment_1/3/5 and new_order_5/9 (tpcc_txn.cpp:530-933)
+ *                               for the committed txns
+ *   dv_load_table_cols /        row_t::set_value / get_value on the mutated TPC-C
+ *   dv_read_table_col           columns (storage/row.cpp:95-180)
  *
  * Decisions follow SURVEY.md 8.0 ("E-schedule"): commit/abort of every txn and
  * the final table state equal a single worker thread running the same epoch
@@ -70,7 +83,7 @@ extern "C" {
 
 /* WORKLOAD values as in config.h */
 #define DV_YCSB 1
-#define DV_TPCC 2
+#define DV_TPCC 2 /* contexts keep three 8-byte state columns per row (col 0 = the F0 column) */
 
 /* access_t (system/global.h:287) */
 #define DV_RD 0
@@ -269,6 +282,76 @@ int dv_round_log(dv_ctx *ctx, uint32_t *live, uint32_t *undecided, uint32_t cap)
 /* host-side epoch builder */
 int dv_ycsb_gen(const dv_ycsb_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
                 uint64_t *keys, uint8_t *types, uint32_t *txn_begin);
+
+/* ---------------------------------------------------------------- TPC-C (config E)
+ * Table ids of this engine (the reference's TPCCTable enum, config.h:200-208,
+ * also numbers the insert-only tables; the engine keeps the five tables txns
+ * lock plus the i_customer_last secondary index). */
+#define DV_TPCC_WAREHOUSE 0
+#define DV_TPCC_DISTRICT 1
+#define DV_TPCC_CUSTOMER 2
+#define DV_TPCC_ITEM 3
+#define DV_TPCC_STOCK 4
+#define DV_TPCC_CUST_LAST 5 /* key custNPKey (tpcc_helper.cpp:35-43); col 0 = custKey of the row */
+
+/* mutated columns (8-byte words, H4: 4-byte integer parameters zero-extended)
+ *   WAREHOUSE  col0 W_YTD (double)          col1 W_TAX (double)
+ *   DISTRICT   col0 D_YTD (double)          col1 D_NEXT_O_ID (int64)   col2 D_TAX (double)
+ *   CUSTOMER   col0 C_BALANCE (double)      col1 C_YTD_PAYMENT (double)
+ *              col2 C_PAYMENT_CNT (loaded as the integer 1, read and written as a double:
+ *                   run_payment_5, tpcc_txn.cpp:640-647)
+ *   ITEM       col0 I_PRICE (int64)
+ *   STOCK      col0 S_QUANTITY (uint64)     col1 S_YTD (int64)         col2 S_ORDER_CNT (int64) */
+
+/* per-access operation word of a TPC-C epoch: op << 56 | operand */
+#define DV_TOP_NONE 0      /* a read whose value no output depends on                  */
+#define DV_TOP_PAY_WH 1    /* W_YTD += h_amount                 (run_payment_1)        */
+#define DV_TOP_PAY_DIST 2  /* D_YTD += h_amount                 (run_payment_3)        */
+#define DV_TOP_PAY_CUST 3  /* C_BALANCE -= h, C_YTD_PAYMENT += h, C_PAYMENT_CNT += 1
+                              (run_payment_5)                                          */
+#define DV_TOP_NO_DIST 4   /* o_id = ++D_NEXT_O_ID              (new_order_5)          */
+#define DV_TOP_NO_STOCK 5  /* S_QUANTITY piecewise, S_YTD += q, S_ORDER_CNT += 1
+                              (new_order_9); operand = ol_quantity                     */
+
+typedef struct dv_tpcc_params {
+    uint32_t num_wh;            /* NUM_WH                                    */
+    uint32_t dist_per_wh;       /* DIST_PER_WH (10)                          */
+    uint32_t cust_per_dist;     /* g_cust_per_dist (>= 1000, tpcc_wl.cpp)    */
+    uint32_t max_items;         /* g_max_items                               */
+    uint32_t max_items_per_txn; /* MAX_ITEMS_PER_TXN (15)                    */
+    uint32_t part_cnt;          /* PART_CNT; wh_to_part(w) = (w-1) % part_cnt */
+    uint32_t part_per_txn;      /* g_part_per_txn                            */
+    uint32_t wh_update;         /* WH_UPDATE: Payment writes the warehouse   */
+    double perc_payment;        /* PERC_PAYMENT                              */
+    double mpr;                 /* g_mpr                                     */
+} dv_tpcc_params;
+
+/* rows of each table held by partition part_id (order of dv_tpcc_load) */
+int dv_tpcc_table_rows(const dv_tpcc_params *p, uint32_t part_id, uint32_t table, uint64_t *rows);
+/* seeded sequential loader for the context's partition (hazard H7: the
+ * reference loads with 8 threads sharing glibc rand()); creates and loads the
+ * six tables.  The context must be opened with workload DV_TPCC. */
+int dv_tpcc_load(dv_ctx *ctx, const dv_tpcc_params *p, uint64_t seed);
+/* host side of the same loader: keys and columns of one table (NULL = skip) */
+int dv_tpcc_table(const dv_tpcc_params *p, uint64_t seed, uint32_t part_id, uint32_t table,
+                  uint64_t *keys, uint64_t *col0, uint64_t *col1, uint64_t *col2);
+/* epoch builder: n_txn queries from a glibc-rand stream seeded with `seed`;
+ * accesses in run_txn_state order.  Capacity: n_txn * (3 + 2 * max_items_per_txn).
+ * txn_type (optional): 1 Payment, 2 NewOrder. */
+int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args,
+                uint32_t *txn_begin, uint8_t *txn_type);
+
+/* multi-column tables (DV_TPCC contexts) */
+int dv_load_table_cols(dv_ctx *ctx, uint32_t table, const uint64_t *keys, const uint64_t *col0,
+                       const uint64_t *col1, const uint64_t *col2, uint64_t n);
+int dv_read_table_col(dv_ctx *ctx, uint32_t table, uint32_t col, uint64_t first_row, uint64_t n,
+                      uint64_t *out);
+/* one TPC-C epoch on the device: ep->tables required; d_args[n_acc] operation
+ * words; d_oid[n_txn] (may be NULL) receives o_id of every committed NewOrder
+ * whose district is local (0 otherwise) */
+int dv_tpcc_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args,
+                             uint8_t *d_commit, uint64_t *d_oid, dv_stats *st);
 
 #ifdef __cplusplus
 }

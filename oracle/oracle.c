@@ -232,6 +232,27 @@ int or_index_read(const or_index *ix, uint64_t key, uint64_t *row) {
     return 0;
 }
 
+/* TPCCTxnManager::run_payment_4 by last name (benchmarks/tpcc_txn.cpp:600-626):
+ * walk the key's item list, `mid` advancing on every second element */
+int or_index_read_mid(const or_index *ix, uint64_t key, uint64_t *row) {
+    uint64_t b = or_hash(ix, key);
+    uint32_t cur = ix->first_node[b];
+    while (cur != NIL) {
+        if (ix->node_key[cur] == key) break;
+        cur = ix->node_next[cur];
+    }
+    if (cur == NIL) return -1;
+    uint32_t it = ix->node_items[cur], mid = it;
+    int cnt = 0;
+    while (it != NIL) {
+        cnt++;
+        it = ix->item_next[it];
+        if (cnt % 2 == 0) mid = ix->item_next[mid];
+    }
+    *row = ix->item_row[mid];
+    return 0;
+}
+
 /* ---------------------------------------------------------------- YCSB row */
 /* ycsb_wl.cpp:173-186: set_value(0,&key,8) then set_value(fid,"hello",6) for
  * every field: F0 bytes [0,6) = "hello\0", bytes [6,8) = bytes 6..7 of key. */
@@ -691,5 +712,31 @@ int or_epoch_run(int cc_alg, const or_index *ix, uint64_t *f0, uint64_t nrows, u
         rc = -6;
     }
     free(rows);
+    return rc;
+}
+
+/* decisions only, on pre-resolved global row ids (TPC-C: several tables) */
+int or_epoch_decide(int cc_alg, const uint64_t *rows, uint64_t nrows, uint32_t n_txn,
+                    const uint32_t *txn_begin, const uint8_t *types, uint8_t *out_commit,
+                    uint32_t *out_grant, or_epoch_stats *st) {
+    memset(st, 0, sizeof(*st));
+    uint64_t *scratch = (uint64_t *)calloc(nrows ? nrows : 1, sizeof(uint64_t));
+    int rc;
+    memset(out_commit, 0, n_txn);
+    switch (cc_alg) {
+    case OR_CALVIN:
+        rc = epoch_calvin(rows, rows, scratch, nrows, n_txn, txn_begin, types, out_commit, out_grant, st);
+        break;
+    case OR_NO_WAIT:
+    case OR_WAIT_DIE:
+        rc = epoch_2pl(cc_alg, rows, rows, scratch, nrows, n_txn, txn_begin, types, out_commit, st);
+        break;
+    case OR_OCC:
+        rc = epoch_occ(rows, rows, scratch, nrows, n_txn, txn_begin, types, out_commit, 0, st);
+        break;
+    default:
+        rc = -6;
+    }
+    free(scratch);
     return rc;
 }

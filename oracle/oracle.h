@@ -62,6 +62,10 @@ void      or_index_free(or_index *ix);
 int       or_index_insert(or_index *ix, uint64_t key, uint64_t row);    /* index_hash.cpp:69-83, 172-201 */
 int       or_index_read(const or_index *ix, uint64_t key, uint64_t *row); /* index_hash.cpp:137-153, 217-231 */
 
+/* run_payment_4's last-name lookup: element floor(n/2) of the key's item list
+ * (tpcc_txn.cpp:600-626) */
+int       or_index_read_mid(const or_index *ix, uint64_t key, uint64_t *row);
+
 /* ---- YCSB table F0 prefix (ycsb_wl.cpp:144-203, row.cpp:107-115; hazard H3) ---- */
 uint64_t or_ycsb_f0_init(uint64_t key);
 /* init_table_slice (ycsb_wl.cpp:144-203) for one partition: keys part_id,
@@ -92,6 +96,38 @@ int or_epoch_run(int cc_alg, const or_index *ix, uint64_t *f0, uint64_t nrows,
                  uint32_t n_txn, const uint32_t *txn_begin, const uint64_t *keys,
                  const uint8_t *types, uint8_t *out_commit, uint32_t *out_grant,
                  int occ_literal, or_epoch_stats *st);
+
+/* decisions only, on pre-resolved row ids (stats: committed / aborted / write_cnt) */
+int or_epoch_decide(int cc_alg, const uint64_t *rows, uint64_t nrows, uint32_t n_txn,
+                    const uint32_t *txn_begin, const uint8_t *types, uint8_t *out_commit,
+                    uint32_t *out_grant, or_epoch_stats *st);
+
+/* ---- TPC-C (tpcc.c) ---- */
+typedef struct { int32_t st[31]; int f, r; } or_grand;   /* glibc random_r TYPE_3 state */
+void     or_grand_seed(or_grand *g, uint32_t seed);      /* srandom_r */
+uint32_t or_grand_next(or_grand *g);                     /* random_r  */
+
+typedef struct {
+    uint32_t num_wh, dist_per_wh, cust_per_dist, max_items, max_items_per_txn;
+    uint32_t part_cnt, part_per_txn, wh_update;
+    double perc_payment, mpr;
+} or_tpcc_params;
+enum { OR_T_WH = 0, OR_T_DIST = 1, OR_T_CUST = 2, OR_T_ITEM = 3, OR_T_STOCK = 4, OR_T_CLAST = 5 };
+typedef struct or_tpcc_db or_tpcc_db;
+or_tpcc_db *or_tpcc_load(const or_tpcc_params *p, uint64_t seed, uint32_t part_id);
+void     or_tpcc_free(or_tpcc_db *db);
+uint64_t or_tpcc_rows(const or_tpcc_db *db, uint32_t table);
+/* keys and the three state columns of a table (NULL = skip) */
+int or_tpcc_table(const or_tpcc_db *db, uint32_t table, uint64_t *keys, uint64_t *c0, uint64_t *c1,
+                  uint64_t *c2);
+int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args, uint32_t *txn_begin,
+                uint8_t *txn_type);
+/* one epoch: decisions (E-schedule) then the committed txns' TPC-C operations
+ * in sequence order; out_oid[t] = o_id of a committed NewOrder, else 0 */
+int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *txn_begin,
+                  const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
+                  const uint64_t *args, uint8_t *out_commit, uint64_t *out_oid, or_epoch_stats *st);
 
 uint64_t or_mix64(uint64_t z);
 uint64_t or_table_digest(const uint64_t *f0, uint64_t n);

@@ -84,8 +84,100 @@ def lib():
         L.or_mt_epoch_run.argtypes = [ctypes.c_void_p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint32, u32p,
                                       u64p, u8p, ctypes.c_int, u64p, u64p]
         L.or_mt_epoch_run.restype = ctypes.c_int
+        L.or_index_read_mid.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u64p]
+        L.or_index_read_mid.restype = ctypes.c_int
+        L.or_grand_seed.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.or_grand_next.argtypes = [ctypes.c_void_p]
+        L.or_grand_next.restype = ctypes.c_uint32
+        L.or_tpcc_load.argtypes = [P(TpccParams), ctypes.c_uint64, ctypes.c_uint32]
+        L.or_tpcc_load.restype = ctypes.c_void_p
+        L.or_tpcc_free.argtypes = [ctypes.c_void_p]
+        L.or_tpcc_rows.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        L.or_tpcc_rows.restype = ctypes.c_uint64
+        L.or_tpcc_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u64p, u64p, u64p, u64p]
+        L.or_tpcc_table.restype = ctypes.c_int
+        L.or_tpcc_gen.argtypes = [P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                  u64p, u8p, u8p, u64p, u32p, u8p]
+        L.or_tpcc_gen.restype = ctypes.c_int
+        L.or_tpcc_epoch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, u32p, u64p, u8p, u8p,
+                                    u64p, u8p, u64p, P(EpochStats)]
+        L.or_tpcc_epoch.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+class TpccParams(ctypes.Structure):
+    _fields_ = [("num_wh", ctypes.c_uint32), ("dist_per_wh", ctypes.c_uint32),
+                ("cust_per_dist", ctypes.c_uint32), ("max_items", ctypes.c_uint32),
+                ("max_items_per_txn", ctypes.c_uint32), ("part_cnt", ctypes.c_uint32),
+                ("part_per_txn", ctypes.c_uint32), ("wh_update", ctypes.c_uint32),
+                ("perc_payment", ctypes.c_double), ("mpr", ctypes.c_double)]
+
+
+def tpcc_params(num_wh, dist_per_wh=10, cust_per_dist=3000, max_items=100000, max_items_per_txn=15,
+                part_cnt=1, part_per_txn=2, wh_update=1, perc_payment=0.5, mpr=1.0):
+    return TpccParams(num_wh, dist_per_wh, cust_per_dist, max_items, max_items_per_txn, part_cnt,
+                      part_per_txn, wh_update, perc_payment, mpr)
+
+
+class GlibcRand:
+    """oracle restatement of glibc srand()/rand() (random_r TYPE_3)."""
+
+    def __init__(self, seed):
+        self.buf = ctypes.create_string_buffer(31 * 4 + 8)
+        lib().or_grand_seed(self.buf, seed)
+
+    def next(self):
+        return lib().or_grand_next(self.buf)
+
+
+def tpcc_gen(p, n_txn, seed, home_part=0):
+    cap = n_txn * (3 + 2 * p.max_items_per_txn)
+    keys = np.zeros(cap, dtype=np.uint64)
+    types = np.zeros(cap, dtype=np.uint8)
+    tables = np.zeros(cap, dtype=np.uint8)
+    args = np.zeros(cap, dtype=np.uint64)
+    tb = np.zeros(n_txn + 1, dtype=np.uint32)
+    tt = np.zeros(max(1, n_txn), dtype=np.uint8)
+    assert lib().or_tpcc_gen(ctypes.byref(p), seed, home_part, n_txn, _p(keys, ctypes.c_uint64),
+                             _p(types, ctypes.c_uint8), _p(tables, ctypes.c_uint8),
+                             _p(args, ctypes.c_uint64), _p(tb, ctypes.c_uint32), _p(tt, ctypes.c_uint8)) == 0
+    n = int(tb[-1])
+    return keys[:n].copy(), types[:n].copy(), tables[:n].copy(), args[:n].copy(), tb, tt[:n_txn]
+
+
+class TpccDB:
+    """Oracle TPC-C partition (oracle/tpcc.c)."""
+
+    def __init__(self, p, seed, part_id=0):
+        self.p = p
+        self.db = lib().or_tpcc_load(ctypes.byref(p), seed, part_id)
+        assert self.db
+
+    def table(self, t):
+        n = lib().or_tpcc_rows(self.db, t)
+        out = [np.zeros(n, dtype=np.uint64) for _ in range(4)]
+        assert lib().or_tpcc_table(self.db, t, *[_p(a, ctypes.c_uint64) for a in out]) == 0
+        return out
+
+    def epoch(self, cc, keys, types, tables, args, tb):
+        n_txn = len(tb) - 1
+        commit = np.zeros(max(1, n_txn), dtype=np.uint8)
+        oid = np.zeros(max(1, n_txn), dtype=np.uint64)
+        st = EpochStats()
+        rc = lib().or_tpcc_epoch(self.db, cc, n_txn, _p(tb, ctypes.c_uint32), _p(keys, ctypes.c_uint64),
+                                 _p(types, ctypes.c_uint8), _p(tables, ctypes.c_uint8),
+                                 _p(args, ctypes.c_uint64), _p(commit, ctypes.c_uint8),
+                                 _p(oid, ctypes.c_uint64), ctypes.byref(st))
+        if rc != 0:
+            raise RuntimeError(f"oracle tpcc epoch failed rc={rc}")
+        return commit[:n_txn], oid[:n_txn], st
+
+    def __del__(self):
+        try:
+            lib().or_tpcc_free(self.db)
+        except Exception:
+            pass
 
 
 def _p(a, t):
