@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
+    ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
+    ap.add_argument("--tpcc-txns", type=int, default=65536, help="txns per TPC-C epoch")
     ap.add_argument("--timing", choices=["full", "kernel", "off"], default="off",
                     help="engine timing inside the timed region: per-stage events, only the "
                          "scatter/pass dispatch timestamps, or none (default: the timed region "
@@ -124,6 +127,69 @@ def cpu_baseline_mt(epochs, rows, seconds):
                       f"threads) over {i} epoch(s) of {epochs[0].n_txn} txns of the bench workload, "
                       f"{txns} txns in {el:.1f} s, abort rate {1 - committed / max(1, txns):.3f}; "
                       "restatement of the reference CC, not the reference binary"}
+
+
+def tpcc_bytes_per_txn(e):
+    """SURVEY.md 8(d) algorithmic bytes of one TPC-C epoch: 67 B per access,
+    plus execution and inserts -- Payment 160 B (3 row updates + HISTORY),
+    NewOrder 148 B per order line (stock update + ORDER_LINE; ORDER/NEW_ORDER
+    and the district counted in the 592 + 888 B of a 10-line order)."""
+    n = np.diff(e.txn_begin.astype(np.int64))
+    pay = e.txn_type == 1
+    per = np.where(pay, 67 * n + 160, 67 * n + 148 * ((n - 3) // 2))
+    return int(per.sum())
+
+
+def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
+    """Config E on one GPU: TPC-C Payment + NewOrder (PERC_PAYMENT 0.5, MPR 1.0,
+    remote customer 15 %, remote item 1 %), this GPU's share of 256
+    warehouses (32), full item / customer counts; a step = one epoch of
+    --tpcc-txns txns through last-name lookup -> probe -> sort -> decide ->
+    execute, epochs resident in HBM.  Beside it the oracle (single thread)
+    on one of the same epochs."""
+    from dvcc import tpcc as T
+    p = T.tpcc_params(a.tpcc_wh)
+    n_txn = a.tpcc_txns
+    eps = [T.gen(p, n_txn, dvcc.epoch_seed(0, e)) for e in range(2)]
+    out = {"workload": f"TPC-C config E share: {a.tpcc_wh} warehouses/GPU, {n_txn}-txn epochs, "
+                       "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
+           "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
+    for cc_name in cc_names:
+        eng = T.TpccEngine(cc_name, p, n_txn, seed=1)
+        dev = [T.device_epoch(e) for e in eps]
+        d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+        d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
+        k = max(a.steps, 5)
+        for i in range(a.warmup):
+            eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        sts = [eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid) for i in range(k)]
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        committed = sum(s.committed for s in sts)
+        byts = sum(tpcc_bytes_per_txn(eps[i % 2]) for i in range(k))
+        out[cc_name] = {"committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el,
+                        "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_txn),
+                        "epochs": k, "epoch_roofline": {"achieved_GBps": byts / el / 1e9,
+                                                        "frac": byts / el / 1e9 / HBM_PEAK_GBPS}}
+        eng.close()
+    if not a.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import _oracle as O
+        po = O.tpcc_params(a.tpcc_wh)
+        e = eps[0]
+        for cc_name in cc_names:
+            db = O.TpccDB(po, 1)
+            cc = {"WAIT_DIE": O.WAIT_DIE, "CALVIN": O.CALVIN, "NO_WAIT": O.NO_WAIT, "OCC": O.OCC}[cc_name]
+            t0 = time.perf_counter()
+            commit, _, st = db.epoch(cc, e.keys, e.types, e.tables, e.args, e.txn_begin)
+            el = time.perf_counter() - t0
+            out[cc_name]["cpu_baseline"] = {
+                "value": st.committed / el, "unit": "committed txns/s", "cores": 1, "kind": "port",
+                "sample": f"oracle (tpcc.c, E-schedule {cc_name}) on 1 epoch of {n_txn} txns of this "
+                          f"workload in {el:.2f} s on 1 host core; restatement, not the reference binary"}
+    return out
 
 
 def closed_loop_leg(eng, gen, n_txn, k, d_commit):
@@ -356,6 +422,8 @@ def main():
             out["cpu_baseline_single_thread"] = single
         else:
             out["cpu_baseline"] = single
+    if world == 1 and not a.no_tpcc:
+        out["tpcc"] = tpcc_leg(a)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -52,14 +52,12 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
                                                          const uint8_t *__restrict__ tables, uint64_t n,
                                                          const uint64_t *__restrict__ col0,
                                                          uint64_t *__restrict__ okeys,
-                                                         uint8_t *__restrict__ otables, Counters *ctr) {
+                                                         uint8_t *__restrict__ otables) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
         uint64_t key = keys[i];
         uint8_t tb = tables[i];
         if (tb == DV_TPCC_CUST_LAST) {
-            if (tb >= tabs.n) {
-                set_err(ctr, ERRB_TABLE);
-            } else {
+            if (tb < tabs.n) {  // else the probe reports the missing table
                 const TableDesc &t = tabs.t[tb];
                 const uint64_t bk = bucket_of_t(t, key);
                 uint64_t row = ~0ull;
@@ -79,12 +77,8 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
                     // equal keys are contiguous: the floor(cnt/2)-th of the list
                     if (cnt) row = t.ix[first + cnt / 2].row;
                 }
-                if (row == ~0ull) {
-                    set_err(ctr, ERRB_KEY);
-                    key = ~0ull;
-                } else {
-                    key = col0[t.row_base + row];
-                }
+                // no customer of that name: key ~0 misses in the probe (DV_ERR_KEY_NOT_FOUND)
+                key = row == ~0ull ? ~0ull : col0[t.row_base + row];
                 tb = DV_TPCC_CUSTOMER;
             }
         }
@@ -93,7 +87,12 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
     }
 }
 
-// pass 1: additive updates, stock queues, NewOrder flags, district queue heads
+// pass 1: additive updates, stock queues, NewOrder flags, district queue heads.
+// Each wave takes 64 consecutive sorted accesses; the additive contributions
+// of a row's run inside the wave are summed by a segmented shuffle reduction
+// (rows are contiguous in sort order) and the run's first lane issues one
+// atomic per column: a hot row (CALVIN: every Payment of a warehouse) takes
+// one same-address atomic per wave instead of one per access.
 __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restrict__ pairs, uint64_t n,
                                                        const uint8_t *__restrict__ status,
                                                        const uint32_t *__restrict__ tb_start,
@@ -101,32 +100,50 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                                                        uint64_t *c1, uint64_t *c2, uint32_t *__restrict__ flag,
                                                        uint32_t *__restrict__ dhead, uint64_t dist_base,
                                                        uint64_t dist_rows, Counters *ctr) {
+    const uint32_t lane = threadIdx.x & 63;
     unsigned long long wcnt = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t p = pairs[i];
-        const uint32_t row = pair_row(p), txn = pair_txn(p);
-        const bool com = status[txn] == ST_COMMIT;
-        const uint64_t w = args[tb_start[txn] + pair_pos(p)];
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t i = base + lane;
+        const bool valid = i < n;
+        const uint64_t p = valid ? pairs[i] : ~0ull;
+        const uint32_t row = valid ? pair_row(p) : 0xFFFFFFFFu, txn = pair_txn(p);
+        const bool com = valid && status[txn] == ST_COMMIT;
+        const uint64_t w = valid ? args[tb_start[txn] + pair_pos(p)] : 0ull;
         const uint32_t op = (uint32_t)(w >> 56);
         const uint64_t v = w & kOpMask;
-        const bool head = i == 0 || pair_row(pairs[i - 1]) != row;
-        flag[i] = com && op == DV_TOP_NO_DIST ? 1u : 0u;
+        const uint32_t prow = __shfl_up(row, 1, 64);
+        const bool head = valid && (i == 0 || (lane ? prow : pair_row(pairs[i - 1])) != row);
+        if (valid) flag[i] = com && op == DV_TOP_NO_DIST ? 1u : 0u;
         if (head && row >= dist_base && row < dist_base + dist_rows) dhead[row - dist_base] = (uint32_t)i;
         if (com && (p & 1)) wcnt++;
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0;
         if (com) {
-            switch (op) {
-            case DV_TOP_PAY_WH:    // W_YTD += h_amount (run_payment_1)
-            case DV_TOP_PAY_DIST:  // D_YTD += h_amount (run_payment_3)
-                atomicAdd(reinterpret_cast<double *>(c0 + row), (double)v);
-                break;
-            case DV_TOP_PAY_CUST:  // run_payment_5
-                atomicAdd(reinterpret_cast<double *>(c0 + row), -(double)v);
-                atomicAdd(reinterpret_cast<double *>(c1 + row), (double)v);
-                atomicAdd(reinterpret_cast<double *>(c2 + row), 1.0);
-                break;
-            default:
-                break;
+            if (op == DV_TOP_PAY_WH || op == DV_TOP_PAY_DIST) {  // W_YTD / D_YTD += h (run_payment_1/3)
+                a0 = (double)v;
+            } else if (op == DV_TOP_PAY_CUST) {  // run_payment_5
+                a0 = -(double)v;
+                a1 = (double)v;
+                a2 = 1.0;
             }
+        }
+        // suffix sums over the row's run inside the wave (integer-valued: exact)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const double o0 = __shfl_down(a0, off, 64), o1 = __shfl_down(a1, off, 64),
+                         o2 = __shfl_down(a2, off, 64);
+            const uint32_t orow = __shfl_down(row, off, 64);
+            if (lane + off < 64 && orow == row) {
+                a0 += o0;
+                a1 += o1;
+                a2 += o2;
+            }
+        }
+        const bool run_first = valid && (lane == 0 || prow != row);
+        if (run_first) {
+            if (a0 != 0.0) atomicAdd(reinterpret_cast<double *>(c0 + row), a0);
+            if (a1 != 0.0) atomicAdd(reinterpret_cast<double *>(c1 + row), a1);
+            if (a2 != 0.0) atomicAdd(reinterpret_cast<double *>(c2 + row), a2);
         }
         if (head && op == DV_TOP_NO_STOCK) {  // new_order_9 in queue order
             uint64_t s = c0[row];
@@ -152,7 +169,7 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) wcnt += __shfl_down(wcnt, off, 64);
-    if ((threadIdx.x & 63) == 0 && wcnt) atomicAdd(&my_slot(ctr).write_cnt, wcnt);
+    if (lane == 0 && wcnt) atomicAdd(&my_slot(ctr).write_cnt, wcnt);
 }
 
 // pass 2: o_id of every committed NewOrder (new_order_5: ++D_NEXT_O_ID)
@@ -170,11 +187,28 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
     }
 }
 
-// pass 3: D_NEXT_O_ID += committed NewOrders of the district
+// pass 3: D_NEXT_O_ID += committed NewOrders of the district (one atomic per
+// row run of a wave, as in pass 1)
 __global__ __launch_bounds__(kBlock) void k_tpcc_next_oid(const uint64_t *__restrict__ pairs, uint64_t n,
                                                           const uint32_t *__restrict__ flag, uint64_t *c1) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-        if (flag[i]) atomicAdd(reinterpret_cast<unsigned long long *>(c1 + pair_row(pairs[i])), 1ull);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); base < n; base += stride) {
+        const uint64_t i = base + lane;
+        const uint32_t f = i < n ? flag[i] : 0u;
+        if (__ballot(f != 0) == 0) continue;
+        const uint32_t row = i < n ? pair_row(pairs[i]) : 0xFFFFFFFFu;
+        uint32_t cnt = f;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_down(cnt, off, 64);
+            const uint32_t orow = __shfl_down(row, off, 64);
+            if (lane + off < 64 && orow == row) cnt += o;
+        }
+        const uint32_t prow = __shfl_up(row, 1, 64);
+        if (i < n && (lane == 0 || prow != row) && cnt)
+            atomicAdd(reinterpret_cast<unsigned long long *>(c1 + row), (unsigned long long)cnt);
+    }
 }
 
 uint32_t grid_for(uint64_t n) {
@@ -187,7 +221,8 @@ uint32_t grid_for(uint64_t n) {
 void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *tables,
                          uint64_t n, const uint64_t *col0, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
     if (n == 0) return;
-    k_tpcc_resolve<<<grid_for(n), kBlock, 0, s>>>(tabs, keys, tables, n, col0, okeys, otables, ctr);
+    (void)ctr;
+    k_tpcc_resolve<<<grid_for(n), kBlock, 0, s>>>(tabs, keys, tables, n, col0, okeys, otables);
 }
 
 size_t tpcc_scan_bytes(uint64_t n) {
