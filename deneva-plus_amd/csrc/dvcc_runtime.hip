@@ -863,6 +863,8 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         x.ctr = c->ctr;
         if (c->tp_oid) HIPCHK(hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream));
         launch_tpcc_exec(c->stream, x);
+        c->tp_args = nullptr;  // per epoch (dv_tpcc_epoch_begin)
+        c->tp_oid = nullptr;
     } else if (calvin)
         launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey,
                     c->ctr);
@@ -1059,12 +1061,11 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     return dv_epoch_finish(c, d_commit, st);
 }
 
-// One TPC-C epoch: the last-name lookups resolve into a scratch copy of the
+// TPC-C epochs: the last-name lookups resolve into a scratch copy of the
 // epoch, which then runs the generic path; dv_epoch_finish executes the
 // committed txns' TPC-C operations (dvcc_tpcc.hip).
-int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint8_t *d_commit,
-                             uint64_t *d_oid, dv_stats *st) {
-    if (!c || !ep || !d_args || (ep->n_acc && !ep->tables) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
+int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint64_t *d_oid) {
+    if (!c || !ep || (ep->n_acc && (!d_args || !ep->tables)) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     const uint64_t A = c->cfg.max_acc;
@@ -1096,12 +1097,23 @@ int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *
     dv_epoch_dev e = *ep;
     e.keys = c->tp_keys;
     e.tables = c->tp_tables;
-    c->tp_args = d_args;
+    static const uint64_t kNoArgs = 0;
+    c->tp_args = d_args ? d_args : &kNoArgs;  // an empty partition still finishes
     c->tp_oid = d_oid;
-    r = dv_epoch_run_device(c, &e, d_commit, nullptr, st);
-    c->tp_args = nullptr;
-    c->tp_oid = nullptr;
+    r = dv_epoch_begin(c, &e, nullptr);
+    if (r) c->tp_args = c->tp_oid = nullptr;
     return r;
+}
+
+int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint8_t *d_commit,
+                             uint64_t *d_oid, dv_stats *st) {
+    int r = dv_tpcc_epoch_begin(c, ep, d_args, d_oid);
+    if (r) return r;
+    if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
+        r = run_rounds(c);
+        if (r) { c->phase = 0; c->tp_args = nullptr; c->tp_oid = nullptr; return r; }
+    }
+    return dv_epoch_finish(c, d_commit, st);
 }
 
 int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {

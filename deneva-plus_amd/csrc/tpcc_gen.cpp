@@ -191,13 +191,17 @@ extern "C" int dv_tpcc_table(const dv_tpcc_params *p, uint64_t seed, uint32_t pa
 
 extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
                            uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args,
-                           uint32_t *txn_begin, uint8_t *txn_type) {
+                           uint32_t *txn_begin, uint8_t *txn_type, uint8_t *owner) {
     if (!valid(p) || home_part >= p->part_cnt || !keys || !types || !tables || !args || !txn_begin)
         return DV_ERR_ARG;
     const Keys K{p->dist_per_wh, p->cust_per_dist, p->max_items};
     TpccRand R((uint32_t)seed);
     uint64_t n = 0;
-    auto acc = [&](uint8_t table, uint64_t key, uint8_t type, uint64_t op, uint64_t v) {
+    // owner: the partition whose node runs the access (acquire_locks tests
+    // GET_NODE_ID(wh_to_part(...)) per access; ITEM goes with its supply
+    // warehouse's stock access, tpcc_txn.cpp:210-240)
+    auto acc = [&](uint8_t table, uint64_t key, uint8_t type, uint64_t op, uint64_t v, uint64_t wh) {
+        if (owner) owner[n] = (uint8_t)wh_to_part(p, wh);
         keys[n] = key;
         types[n] = type;
         tables[n] = table;
@@ -234,14 +238,14 @@ extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home
             }
             // run_payment_0..5 (tpcc_txn.cpp:500-660): WH, DIST, CUST
             acc(DV_TPCC_WAREHOUSE, w, p->wh_update ? DV_WR : DV_RD, p->wh_update ? DV_TOP_PAY_WH : DV_TOP_NONE,
-                h_amount);
-            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_PAY_DIST, h_amount);
+                h_amount, w);
+            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_PAY_DIST, h_amount, w);
             if (y <= 60) {  // by last name: index_read(i_customer_last) + mid (600-626)
                 const std::string last = last_name(R.NURand(255, 0, 999));
-                acc(DV_TPCC_CUST_LAST, K.cust_np(last, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount);
+                acc(DV_TPCC_CUST_LAST, K.cust_np(last, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount, c_w);
             } else {
                 const uint64_t c = R.NURand(1023, 1, p->cust_per_dist);
-                acc(DV_TPCC_CUSTOMER, K.cust(c, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount);
+                acc(DV_TPCC_CUSTOMER, K.cust(c, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount, c_w);
             }
         } else {
             if (txn_type) txn_type[t] = 2;
@@ -254,9 +258,9 @@ extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home
             const double r_mpr = (double)(R.raw() % 10000) / 10000;
             const uint64_t part_limit = r_mpr < p->mpr ? p->part_per_txn : 1;
             // new_order_0..5 (tpcc_txn.cpp:663-800): WH RD, CUST RD, DIST WR
-            acc(DV_TPCC_WAREHOUSE, w, DV_RD, DV_TOP_NONE, 0);
-            acc(DV_TPCC_CUSTOMER, K.cust(c, d, w), DV_RD, DV_TOP_NONE, 0);
-            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_NO_DIST, 0);
+            acc(DV_TPCC_WAREHOUSE, w, DV_RD, DV_TOP_NONE, 0, w);
+            acc(DV_TPCC_CUSTOMER, K.cust(c, d, w), DV_RD, DV_TOP_NONE, 0, w);
+            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_NO_DIST, 0, w);
             std::set<uint64_t> ids;
             for (uint64_t k = 0; k < ol_cnt; k++) {
                 uint64_t i_id;
@@ -274,8 +278,8 @@ extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home
                     while (parts.count(wh_to_part(p, sw = R.URand(1, p->num_wh))) == 0) {}
                 }
                 // new_order_6..9 (tpcc_txn.cpp:801-933): ITEM RD, STOCK WR
-                acc(DV_TPCC_ITEM, i_id, DV_RD, DV_TOP_NONE, 0);
-                acc(DV_TPCC_STOCK, K.stock(i_id, sw), DV_WR, DV_TOP_NO_STOCK, qty);
+                acc(DV_TPCC_ITEM, i_id, DV_RD, DV_TOP_NONE, 0, sw);
+                acc(DV_TPCC_STOCK, K.stock(i_id, sw), DV_WR, DV_TOP_NO_STOCK, qty, sw);
             }
         }
     }

@@ -37,22 +37,33 @@ import torch.distributed as dist
 from .engine import Epoch
 
 
+def owner_order(epoch, world):
+    """Owner rank of every access and the stable order grouping them by owner.
+    YCSB: key % PART_CNT (ycsb_wl.cpp:69-74); TPC-C epochs carry the owner
+    (wh_to_part of the access's warehouse, tpcc_helper.cpp:161-164)."""
+    own = getattr(epoch, "owner", None)
+    if own is not None:
+        owner = own.astype(np.int64)
+    else:
+        owner = (epoch.keys % np.uint64(world)).astype(np.int64)
+    return owner, np.argsort(owner, kind="stable")
+
+
 def split_by_owner(epoch, txn_base, world):
     """Host-side split of one origin batch into per-owner fragments.
 
     Returns (keys, types, txn, counts): arrays ordered by owner rank and, inside
     an owner, by (txn, request position); txn is the global sequence number
     txn_base + local txn index."""
-    keys = epoch.keys
-    owner = (keys % np.uint64(world)).astype(np.int64)
-    order = np.argsort(owner, kind="stable")
+    owner, order = owner_order(epoch, world)
     txn = epoch.acc_txn().astype(np.int64) + txn_base
     counts = np.bincount(owner, minlength=world)
-    return (keys[order], epoch.types[order], txn[order].astype(np.int32), counts)
+    return (epoch.keys[order], epoch.types[order], txn[order].astype(np.int32), counts)
 
 
 class PartitionedEpoch:
-    """One rank's outgoing fragments of one epoch, resident on `device`."""
+    """One rank's outgoing fragments of one epoch, resident on `device`.
+    TPC-C epochs also carry each access's table and operation word."""
 
     def __init__(self, batch, rank, world, txns_per_rank, device):
         k, t, x, counts = split_by_owner(batch, rank * txns_per_rank, world)
@@ -60,6 +71,11 @@ class PartitionedEpoch:
         self.keys = torch.from_numpy(k.view(np.int64)).to(device)
         self.types = torch.from_numpy(t).to(device)
         self.txn = torch.from_numpy(x).to(device)
+        self.tables = self.args = None
+        if getattr(batch, "args", None) is not None:
+            _, order = owner_order(batch, world)
+            self.tables = torch.from_numpy(batch.tables[order]).to(device)
+            self.args = torch.from_numpy(batch.args[order].view(np.int64)).to(device)
         self.n_txn_global = txns_per_rank * world
         self.max_txn_acc = batch.max_txn_acc()
 
@@ -82,10 +98,14 @@ class PartitionedRunner:
         return [int(c) for c in recv.cpu().tolist()]
 
     def exchange(self, pe, recv_counts):
-        """All-to-all of the access fragments (keys, types, global txn)."""
+        """All-to-all of the access fragments (keys, types, global txn; TPC-C:
+        tables and operation words too)."""
         n = sum(recv_counts)
         out = []
-        for src, dt in ((pe.keys, torch.int64), (pe.types, torch.uint8), (pe.txn, torch.int32)):
+        cols = [(pe.keys, torch.int64), (pe.types, torch.uint8), (pe.txn, torch.int32)]
+        if pe.args is not None:
+            cols += [(pe.tables, torch.uint8), (pe.args, torch.int64)]
+        for src, dt in cols:
             dst = torch.empty(n, dtype=dt, device=self.device)
             dist.all_to_all_single(dst, src, output_split_sizes=recv_counts,
                                    input_split_sizes=pe.send_counts, group=self.group)
@@ -96,9 +116,10 @@ class PartitionedRunner:
         """One partitioned epoch.  Returns (stats of this rank, rounds)."""
         if recv_counts is None:
             recv_counts = self.exchange_counts(pe)
-        keys, types, txn = self.exchange(pe, recv_counts)
+        cols = self.exchange(pe, recv_counts)
         n_txn = pe.n_txn_global
-        self.engine.begin_partition(keys, types, txn, n_txn, max_txn_acc=pe.max_txn_acc)
+        extra = {"tables": cols[3], "args": cols[4]} if len(cols) > 3 else {}
+        self.engine.begin_partition(*cols[:3], n_txn, max_txn_acc=pe.max_txn_acc, **extra)
         rounds = 0
         if self.engine.needs_votes:
             verdict = torch.zeros((n_txn + 3) // 4 * 4, dtype=torch.uint8, device=self.device)
@@ -130,10 +151,17 @@ class EnginePartition:
         self.needs_votes = engine.cc_alg != 10  # CALVIN has no votes
         engine.set_stream(torch.cuda.current_stream().cuda_stream)
 
-    def begin_partition(self, keys, types, txn, n_txn, max_txn_acc=0):
+    def begin_partition(self, keys, types, txn, n_txn, max_txn_acc=0, tables=None, args=None):
+        """TPC-C (args given): dv_tpcc_epoch_begin; the o_id of committed
+        NewOrders whose district is on this partition land in self.oid."""
         from .engine import DeviceEpoch
-        self._dep = DeviceEpoch.from_tensors(keys, types, txn, n_txn, max_txn_acc=max_txn_acc)
-        self.engine.begin(self._dep)
+        self._dep = DeviceEpoch.from_tensors(keys, types, txn, n_txn, tables=tables, max_txn_acc=max_txn_acc)
+        if args is not None:
+            self.oid = torch.zeros(max(1, n_txn), dtype=torch.int64, device=keys.device)
+            self._args = args
+            self.engine.begin_tpcc(self._dep, args, self.oid)
+        else:
+            self.engine.begin(self._dep)
 
     def round_local(self, verdict):
         self.engine.round_local(verdict)
@@ -148,4 +176,4 @@ class EnginePartition:
         return self.engine.finish(commit)
 
 
-__all__ = ["split_by_owner", "PartitionedEpoch", "PartitionedRunner", "EnginePartition", "Epoch"]
+__all__ = ["owner_order", "split_by_owner", "PartitionedEpoch", "PartitionedRunner", "EnginePartition", "Epoch"]

@@ -30,6 +30,7 @@ def tpcc_params(num_wh, dist_per_wh=10, cust_per_dist=3000, max_items=100000, ma
 class TpccEpoch(Epoch):
     args: np.ndarray = None      # uint64 [n_acc] op << 56 | operand
     txn_type: np.ndarray = None  # uint8 [n_txn] 1 Payment, 2 NewOrder
+    owner: np.ndarray = None     # uint8 [n_acc] partition that runs the access
 
 
 def table_rows(p, table, part_id=0):
@@ -55,10 +56,12 @@ def gen(p, n_txn, seed, home_part=0):
     args = np.zeros(cap, dtype=np.uint64)
     tb = np.zeros(n_txn + 1, dtype=np.uint32)
     tt = np.zeros(n_txn, dtype=np.uint8)
+    own = np.zeros(cap, dtype=np.uint8)
     L.check(L.lib().dv_tpcc_gen(ctypes.byref(p), seed, home_part, n_txn, _ptr(keys), _ptr(types),
-                                _ptr(tables), _ptr(args), _ptr(tb), _ptr(tt)), "dv_tpcc_gen")
+                                _ptr(tables), _ptr(args), _ptr(tb), _ptr(tt), _ptr(own)), "dv_tpcc_gen")
     n = int(tb[-1])
-    return TpccEpoch(keys[:n].copy(), types[:n].copy(), tb, tables[:n].copy(), args[:n].copy(), tt)
+    return TpccEpoch(keys[:n].copy(), types[:n].copy(), tb, tables[:n].copy(), args[:n].copy(), tt,
+                     own[:n].copy())
 
 
 class TpccEngine(CCEngine):
@@ -77,6 +80,13 @@ class TpccEngine(CCEngine):
         out = np.zeros(n, dtype=np.uint64)
         L.check(L.lib().dv_read_table_col(self._ctx, table_id, col, first, n, _ptr(out)), "dv_read_table_col")
         return out
+
+    def begin_tpcc(self, dep, d_args, d_oid=None):
+        """Staged form (partitioned epochs): rounds and finish as CCEngine's."""
+        self._desc = dep.desc()
+        self._keep = (d_args, d_oid)  # alive until finish
+        L.check(L.lib().dv_tpcc_epoch_begin(self._ctx, ctypes.byref(self._desc), _ptr(d_args), _ptr(d_oid)),
+                "dv_tpcc_epoch_begin")
 
     def run_tpcc_epoch_device(self, dep, d_args, d_commit, d_oid=None):
         st = L.Stats()

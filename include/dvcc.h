@@ -337,10 +337,12 @@ int dv_tpcc_table(const dv_tpcc_params *p, uint64_t seed, uint32_t part_id, uint
                   uint64_t *keys, uint64_t *col0, uint64_t *col1, uint64_t *col2);
 /* epoch builder: n_txn queries from a glibc-rand stream seeded with `seed`;
  * accesses in run_txn_state order.  Capacity: n_txn * (3 + 2 * max_items_per_txn).
- * txn_type (optional): 1 Payment, 2 NewOrder. */
+ * txn_type (optional): 1 Payment, 2 NewOrder.  owner (optional): the partition
+ * that runs each access (wh_to_part of its warehouse; ITEM reads go with the
+ * supply warehouse, as acquire_locks does, tpcc_txn.cpp:210-240). */
 int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
                 uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args,
-                uint32_t *txn_begin, uint8_t *txn_type);
+                uint32_t *txn_begin, uint8_t *txn_type, uint8_t *owner);
 
 /* multi-column tables (DV_TPCC contexts) */
 int dv_load_table_cols(dv_ctx *ctx, uint32_t table, const uint64_t *keys, const uint64_t *col0,
@@ -352,6 +354,11 @@ int dv_read_table_col(dv_ctx *ctx, uint32_t table, uint32_t col, uint64_t first_
  * whose district is local (0 otherwise) */
 int dv_tpcc_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args,
                              uint8_t *d_commit, uint64_t *d_oid, dv_stats *st);
+/* staged form for partitioned epochs: dv_epoch_begin of a TPC-C epoch (this
+ * partition's accesses); then the rounds, and dv_epoch_finish executes the
+ * committed txns' operations on this partition's rows.  d_args / d_oid must
+ * stay valid until dv_epoch_finish. */
+int dv_tpcc_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args, uint64_t *d_oid);
 
 #ifdef __cplusplus
 }

@@ -122,7 +122,7 @@ int or_tpcc_table(const or_tpcc_db *db, uint32_t table, uint64_t *keys, uint64_t
                   uint64_t *c2);
 int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
                 uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args, uint32_t *txn_begin,
-                uint8_t *txn_type);
+                uint8_t *txn_type, uint8_t *owner);
 /* one epoch: decisions (E-schedule) then the committed txns' TPC-C operations
  * in sequence order; out_oid[t] = o_id of a committed NewOrder, else 0 */
 int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *txn_begin,

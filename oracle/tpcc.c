@@ -197,11 +197,11 @@ enum { OP_NONE = 0, OP_PAY_WH = 1, OP_PAY_DIST = 2, OP_PAY_CUST = 3, OP_NO_DIST 
 
 int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
                 uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args, uint32_t *txn_begin,
-                uint8_t *txn_type) {
+                uint8_t *txn_type, uint8_t *owner) {
     trand R;
     t_init(&R, seed);
     uint64_t n = 0;
-#define ACC(tb, k, ty, op, v) do { keys[n] = (k); types[n] = (ty); tables[n] = (tb); \
+#define ACC(tb, k, ty, op, v, wh) do { if (owner) owner[n] = (uint8_t)wh_part(p, (wh)); keys[n] = (k); types[n] = (ty); tables[n] = (tb); \
                                    args[n] = ((uint64_t)(op) << 56) | (v); n++; } while (0)
     for (uint32_t t = 0; t < n_txn; t++) {
         txn_begin[t] = (uint32_t)n;
@@ -226,15 +226,15 @@ int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint
                     c_w_id = w;
                 }
             }
-            ACC(OR_T_WH, w, p->wh_update ? OR_WR : OR_RD, p->wh_update ? OP_PAY_WH : OP_NONE, h_amount);
-            ACC(OR_T_DIST, k_dist(p, d_id, w), OR_WR, OP_PAY_DIST, h_amount);
+            ACC(OR_T_WH, w, p->wh_update ? OR_WR : OR_RD, p->wh_update ? OP_PAY_WH : OP_NONE, h_amount, w);
+            ACC(OR_T_DIST, k_dist(p, d_id, w), OR_WR, OP_PAY_DIST, h_amount, w);
             if (y <= 60) {
                 char last[32];
                 lastname(t_nurand(&R, 255, 0, 999), last);
-                ACC(OR_T_CLAST, k_custnp(p, last, c_d_id, c_w_id), OR_WR, OP_PAY_CUST, h_amount);
+                ACC(OR_T_CLAST, k_custnp(p, last, c_d_id, c_w_id), OR_WR, OP_PAY_CUST, h_amount, c_w_id);
             } else {
                 uint64_t c_id = t_nurand(&R, 1023, 1, p->cust_per_dist);
-                ACC(OR_T_CUST, k_cust(p, c_id, c_d_id, c_w_id), OR_WR, OP_PAY_CUST, h_amount);
+                ACC(OR_T_CUST, k_cust(p, c_id, c_d_id, c_w_id), OR_WR, OP_PAY_CUST, h_amount, c_w_id);
             }
         } else {                                               /* gen_new_order */
             if (txn_type) txn_type[t] = 2;
@@ -247,9 +247,9 @@ int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint
             parts[nparts++] = wh_part(p, w);
             double r_mpr = (double)(or_grand_next(&R.g) % 10000) / 10000;
             uint64_t part_limit = r_mpr < p->mpr ? p->part_per_txn : 1;
-            ACC(OR_T_WH, w, OR_RD, OP_NONE, 0);
-            ACC(OR_T_CUST, k_cust(p, c_id, d_id, w), OR_RD, OP_NONE, 0);
-            ACC(OR_T_DIST, k_dist(p, d_id, w), OR_WR, OP_NO_DIST, 0);
+            ACC(OR_T_WH, w, OR_RD, OP_NONE, 0, w);
+            ACC(OR_T_CUST, k_cust(p, c_id, d_id, w), OR_RD, OP_NONE, 0, w);
+            ACC(OR_T_DIST, k_dist(p, d_id, w), OR_WR, OP_NO_DIST, 0, w);
             uint64_t ids[64];
             for (uint64_t k = 0; k < ol_cnt; k++) {
                 uint64_t i_id;
@@ -280,8 +280,8 @@ int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint
                         if (have) break;
                     }
                 }
-                ACC(OR_T_ITEM, i_id, OR_RD, OP_NONE, 0);
-                ACC(OR_T_STOCK, k_stock(p, i_id, sw), OR_WR, OP_NO_STOCK, qty);
+                ACC(OR_T_ITEM, i_id, OR_RD, OP_NONE, 0, sw);
+                ACC(OR_T_STOCK, k_stock(p, i_id, sw), OR_WR, OP_NO_STOCK, qty, sw);
             }
         }
     }

@@ -97,7 +97,7 @@ def lib():
         L.or_tpcc_table.argtypes = [ctypes.c_void_p, ctypes.c_uint32, u64p, u64p, u64p, u64p]
         L.or_tpcc_table.restype = ctypes.c_int
         L.or_tpcc_gen.argtypes = [P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
-                                  u64p, u8p, u8p, u64p, u32p, u8p]
+                                  u64p, u8p, u8p, u64p, u32p, u8p, u8p]
         L.or_tpcc_gen.restype = ctypes.c_int
         L.or_tpcc_epoch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, u32p, u64p, u8p, u8p,
                                     u64p, u8p, u64p, P(EpochStats)]
@@ -139,11 +139,13 @@ def tpcc_gen(p, n_txn, seed, home_part=0):
     args = np.zeros(cap, dtype=np.uint64)
     tb = np.zeros(n_txn + 1, dtype=np.uint32)
     tt = np.zeros(max(1, n_txn), dtype=np.uint8)
+    own = np.zeros(cap, dtype=np.uint8)
     assert lib().or_tpcc_gen(ctypes.byref(p), seed, home_part, n_txn, _p(keys, ctypes.c_uint64),
                              _p(types, ctypes.c_uint8), _p(tables, ctypes.c_uint8),
-                             _p(args, ctypes.c_uint64), _p(tb, ctypes.c_uint32), _p(tt, ctypes.c_uint8)) == 0
+                             _p(args, ctypes.c_uint64), _p(tb, ctypes.c_uint32), _p(tt, ctypes.c_uint8),
+                             _p(own, ctypes.c_uint8)) == 0
     n = int(tb[-1])
-    return keys[:n].copy(), types[:n].copy(), tables[:n].copy(), args[:n].copy(), tb, tt[:n_txn]
+    return keys[:n].copy(), types[:n].copy(), tables[:n].copy(), args[:n].copy(), tb, tt[:n_txn], own[:n].copy()
 
 
 class TpccDB:

@@ -142,7 +142,7 @@ def test_product_gen_matches_oracle(dv, nw, parts, home):
         pp = dv.tpcc_params(nw, cust_per_dist=1000, max_items=2000, part_cnt=parts)
         a = O.tpcc_gen(po, 2000, seed, home)
         e = dv.gen(pp, 2000, seed, home)
-        for x, y in zip(a[:5], [e.keys, e.types, e.tables, e.args, e.txn_begin]):
+        for x, y in zip(a[:5] + a[6:], [e.keys, e.types, e.tables, e.args, e.txn_begin, e.owner]):
             assert (x == y).all()
         assert (a[5] == e.txn_type).all()
 

@@ -100,3 +100,109 @@ def test_tpcc_missing_last_name():
         assert ei.value.code == -4
     finally:
         eng.close()
+
+
+def _global(batches):
+    """Origin batches -> one epoch in Calvin's global order (rank-major)."""
+    keys = np.concatenate([b.keys for b in batches])
+    types = np.concatenate([b.types for b in batches])
+    tables = np.concatenate([b.tables for b in batches])
+    args = np.concatenate([b.args for b in batches])
+    sizes = np.concatenate([np.diff(b.txn_begin.astype(np.int64)) for b in batches])
+    tb = np.zeros(len(sizes) + 1, np.uint32)
+    tb[1:] = np.cumsum(sizes)
+    return keys, types, tables, args, tb
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("world", [2, 4])
+def test_tpcc_partitioned_engines(cc, world):
+    """config E's layout on one GPU: `world` contexts, each the partition of
+    its warehouses ((w-1) % PART_CNT, ITEM replicated); fragments routed by
+    owner in origin order, verdicts combined by MAX (the all-reduce) -- equal
+    to the single-thread E-schedule over the whole epoch."""
+    from dvcc.partitioned import split_by_owner, owner_order
+    n_txn = 1500
+    kw = dict(num_wh=2 * world, cust_per_dist=1000, max_items=2000, part_cnt=world, part_per_txn=2, mpr=1.0)
+    pp = T.tpcc_params(**kw)
+    batches = [T.gen(pp, n_txn, 40 + r, home_part=r) for r in range(world)]
+    kw1 = dict(kw, part_cnt=1)
+    db = O.TpccDB(O.tpcc_params(**kw1), 5)
+    c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], *_global(batches))
+    N = n_txn * world
+    engines, parts = [], []
+    for p in range(world):
+        ks, ts, xs, tbs, ags = [], [], [], [], []
+        for r, b in enumerate(batches):
+            k, t, x, counts = split_by_owner(b, r * n_txn, world)
+            _, order = owner_order(b, world)
+            lo = int(counts[:p].sum()); hi = lo + int(counts[p])
+            ks.append(k[lo:hi]); ts.append(t[lo:hi]); xs.append(x[lo:hi])
+            tbs.append(b.tables[order][lo:hi]); ags.append(b.args[order][lo:hi])
+        k = np.concatenate(ks); t = np.concatenate(ts); x = np.concatenate(xs)
+        eng = T.TpccEngine(cc, pp, N, part_id=p, seed=5)
+        dep = dvcc.DeviceEpoch.from_tensors(torch.from_numpy(k.view(np.int64)).cuda(), torch.from_numpy(t).cuda(),
+                                            torch.from_numpy(x).cuda(), N,
+                                            tables=torch.from_numpy(np.concatenate(tbs)).cuda(), max_txn_acc=33)
+        args = torch.from_numpy(np.concatenate(ags).view(np.int64)).cuda()
+        oid = torch.zeros(N, dtype=torch.int64, device="cuda")
+        eng.begin_tpcc(dep, args, oid)
+        engines.append(eng)
+        parts.append((dep, args, oid))
+    if cc != dvcc.CALVIN:
+        for _ in range(N + 1):
+            vs = []
+            for eng in engines:
+                v = torch.zeros((N + 3) // 4 * 4, dtype=torch.uint8, device="cuda")
+                eng.round_local(v)
+                vs.append(v)
+            torch.cuda.synchronize()
+            comb = torch.stack(vs).max(dim=0).values.contiguous()
+            copies = [comb.clone() for _ in engines]
+            torch.cuda.synchronize()
+            und = [eng.round_apply(cp) for eng, cp in zip(engines, copies)]
+            assert len(set(und)) == 1
+            if und[0] == 0:
+                break
+    oid_sum = np.zeros(N, np.uint64)
+    committed = 0
+    for p, eng in enumerate(engines):
+        commit = torch.zeros(N, dtype=torch.uint8, device="cuda")
+        st = eng.finish(commit)
+        committed += st.committed
+        assert (commit.cpu().numpy() == c_ref).all(), p
+        oid_sum += parts[p][2].cpu().numpy().view(np.uint64)
+        for tid in range(5):
+            ref = db.table(tid)
+            mine = np.isin(ref[0], T.table(pp, 5, tid, p)[0])
+            for col in range(3):
+                assert (eng.read_col(tid, col) == ref[1 + col][mine]).all(), (p, tid, col)
+        eng.close()
+    assert (oid_sum == o_ref).all()
+
+
+@pytest.mark.parametrize("cc", [dvcc.WAIT_DIE, dvcc.CALVIN])
+def test_tpcc_runner_single_rank_rccl(cc):
+    """The torch.distributed driver (RCCL) over a TPC-C engine, one rank."""
+    import torch.distributed as dist
+    from dvcc.partitioned import EnginePartition, PartitionedEpoch, PartitionedRunner
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1)
+    try:
+        po, pp = _params("small")
+        db = O.TpccDB(po, 5)
+        eng = T.TpccEngine(cc, pp, 3000, seed=5)
+        e = T.gen(pp, 3000, 21)
+        c_ref, o_ref, _ = db.epoch(ORACLE_CC[cc], e.keys, e.types, e.tables, e.args, e.txn_begin)
+        part = EnginePartition(eng)
+        runner = PartitionedRunner(part, 1, 0)
+        commit = torch.zeros(3000, dtype=torch.uint8, device="cuda")
+        runner.run(PartitionedEpoch(e, 0, 1, 3000, "cuda"), commit=commit)
+        assert (commit.cpu().numpy() == c_ref).all()
+        assert (part.oid.cpu().numpy().view(np.uint64)[:3000] == o_ref).all()
+        _check_tables(eng, db, pp)
+        eng.set_stream(None)
+        eng.close()
+    finally:
+        dist.destroy_process_group()
