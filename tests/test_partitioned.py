@@ -288,3 +288,87 @@ def test_rccl_engine_driver_single_rank(cc):
                                                                st_ref.write_cnt)
     eng.close()
     ref.close()
+
+
+class NumpyTpccPartition(NumpyPartition):
+    """Test double for TPC-C fragments: the last-name lookup (mid of the
+    newest-first list, tpcc_txn.cpp:600-626) on the host, then rows keyed by
+    (table, key); checks each access arrived with its own table and operation."""
+
+    def __init__(self, cc, pp, seed, expect):
+        super().__init__(cc)
+        from dvcc import tpcc as T
+        k, cust, _, _ = T.table(pp, seed, T.L.T_CUST_LAST, 0)
+        lists = {}
+        for a, c in zip(k.tolist(), cust.tolist()):
+            lists.setdefault(a, []).insert(0, c)  # insert_item prepends
+        self.mid = {a: v[len(v) // 2] for a, v in lists.items()}
+        self.expect = expect
+
+    def begin_partition(self, keys, types_, txn, n_txn, max_txn_acc=0, tables=None, args=None):
+        k = keys.numpy().view(np.uint64).copy()
+        tb = tables.numpy().copy()
+        for i in np.flatnonzero(tb == 5):
+            k[i] = self.mid[int(k[i])]
+            tb[i] = 2
+        trip = set(zip(txn.numpy().tolist(), keys.numpy().view(np.uint64).tolist(), tables.numpy().tolist(),
+                       args.numpy().view(np.uint64).tolist()))
+        assert trip <= self.expect
+        rows = torch.from_numpy((k * np.uint64(8) + tb.astype(np.uint64)).view(np.int64))
+        super().begin_partition(rows, types_, txn, n_txn, max_txn_acc)
+
+
+def _tpcc_setup(world, n_txn):
+    from dvcc import tpcc as T
+    kw = dict(num_wh=2 * world, cust_per_dist=1000, max_items=2000, part_cnt=world)
+    pp = T.tpcc_params(**kw)
+    batches = [T.gen(pp, n_txn, 60 + r, home_part=r) for r in range(world)]
+    return kw, pp, batches
+
+
+def _tpcc_gloo_worker(rank, world, port, cc, n_txn, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kw, pp, batches = _tpcc_setup(world, n_txn)
+        expect = set()
+        for r, b in enumerate(batches):
+            expect |= set(zip((b.acc_txn().astype(np.int64) + r * n_txn).tolist(), b.keys.tolist(),
+                              b.tables.tolist(), b.args.tolist()))
+        pe = PartitionedEpoch(batches[rank], rank, world, n_txn, "cpu")
+        runner = PartitionedRunner(NumpyTpccPartition(cc, dvcc.tpcc.tpcc_params(**dict(kw, part_cnt=1)), 5, expect),
+                                   world, rank, device="cpu")
+        commit = torch.zeros(n_txn * world, dtype=torch.uint8)
+        runner.run(pe, commit=commit)
+        q.put((rank, commit.numpy().tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_tpcc_runner_protocol_gloo_world2(cc):
+    """TPC-C fragments (with tables and operation words) through the runner
+    over gloo, world 2: decisions equal the global oracle E-schedule."""
+    import dvcc.tpcc  # noqa: F401
+    world, n_txn = 2, 400
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tpcc_gloo_worker, args=(r, world, port, cc, n_txn, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    kw, pp, batches = _tpcc_setup(world, n_txn)
+    db = O.TpccDB(O.tpcc_params(**dict(kw, part_cnt=1)), 5)
+    keys = np.concatenate([b.keys for b in batches])
+    sizes = np.concatenate([np.diff(b.txn_begin.astype(np.int64)) for b in batches])
+    tb = np.zeros(len(sizes) + 1, np.uint32)
+    tb[1:] = np.cumsum(sizes)
+    c_ref, _, _ = db.epoch(ORACLE_CC[cc], keys, np.concatenate([b.types for b in batches]),
+                           np.concatenate([b.tables for b in batches]), np.concatenate([b.args for b in batches]), tb)
+    assert 0 < c_ref.sum() < len(c_ref)
+    for rank, buf in res:
+        assert (np.frombuffer(buf, np.uint8) == c_ref).all(), rank
