@@ -152,6 +152,28 @@ class CCEngine:
     def stream_ptr(self):
         return L.lib().dv_stream(self._ctx)
 
+    def _after_torch(self):
+        """Orders the engine's stream after the work torch has queued on its
+        current stream: device epochs built by torch kernels (cat, slices,
+        arithmetic) are inputs of the next launch, and the context's own
+        stream is non-blocking, so without this wait it can read them early
+        (no host synchronisation: an event record + stream wait)."""
+        import sys
+        torch = sys.modules.get("torch")
+        if torch is None or not torch.cuda.is_initialized():
+            return
+        cur = torch.cuda.current_stream()
+        sp = self.stream_ptr or 0
+        if sp == cur.cuda_stream:
+            return
+        if getattr(self, "_ev", None) is None:
+            self._ev = torch.cuda.Event()
+            self._ext = torch.cuda.ExternalStream(sp)
+        elif self._ext.cuda_stream != sp:
+            self._ext = torch.cuda.ExternalStream(sp)
+        self._ev.record(cur)
+        self._ext.wait_event(self._ev)
+
     def set_stream(self, stream):
         """Run on the hipStream_t handle `stream` (an int such as
         torch.cuda.current_stream().cuda_stream; 0 is the default stream);
@@ -216,6 +238,7 @@ class CCEngine:
     # ---- one epoch already resident in HBM
     def run_epoch_device(self, dep, d_commit=None, d_grant=None):
         st = L.Stats()
+        self._after_torch()
         desc = dep.desc()
         L.check(L.lib().dv_epoch_run_device(self._ctx, ctypes.byref(desc), _ptr(d_commit),
                                             _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
@@ -230,6 +253,7 @@ class CCEngine:
     def run_epoch_part(self, home, txns_per_rank, d_commit=None):
         """One partitioned epoch from this rank's client batch (DeviceEpoch,
         txn ids local); d_commit: nranks * txns_per_rank device bytes."""
+        self._after_torch()
         st = L.Stats()
         L.check(L.lib().dv_epoch_run_part(self._ctx, ctypes.byref(home.desc()), txns_per_rank,
                                           _ptr(d_commit), ctypes.byref(st)), "dv_epoch_run_part")
@@ -247,6 +271,7 @@ class CCEngine:
         out = L.EpochDev(keys.data_ptr(), types.data_ptr(), txn.data_ptr(),
                          tabs.data_ptr() if tabs is not None else None, 0, 0, 0)
         cap = dep.n_txn if max_txn is None else max_txn
+        self._after_torch()
         L.check(L.lib().dv_epoch_carry(self._ctx, ctypes.byref(dep.desc()), cap, ctypes.byref(out)),
                 "dv_epoch_carry")
         n = int(out.n_acc)
@@ -264,6 +289,7 @@ class CCEngine:
 
     # ---- staged form (multi-partition epochs)
     def begin(self, dep, d_grant=None):
+        self._after_torch()
         self._desc = dep.desc()
         L.check(L.lib().dv_epoch_begin(self._ctx, ctypes.byref(self._desc), _ptr(d_grant)),
                 "dv_epoch_begin")

@@ -83,12 +83,14 @@ class TpccEngine(CCEngine):
 
     def begin_tpcc(self, dep, d_args, d_oid=None):
         """Staged form (partitioned epochs): rounds and finish as CCEngine's."""
+        self._after_torch()
         self._desc = dep.desc()
         self._keep = (d_args, d_oid)  # alive until finish
         L.check(L.lib().dv_tpcc_epoch_begin(self._ctx, ctypes.byref(self._desc), _ptr(d_args), _ptr(d_oid)),
                 "dv_tpcc_epoch_begin")
 
     def run_tpcc_epoch_device(self, dep, d_args, d_commit, d_oid=None):
+        self._after_torch()
         st = L.Stats()
         L.check(L.lib().dv_tpcc_epoch_run_device(self._ctx, ctypes.byref(dep.desc()), _ptr(d_args),
                                                  _ptr(d_commit), _ptr(d_oid), ctypes.byref(st)),
