@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
+    ap.add_argument("--tpcc-only", action="store_true", help="run and print only the TPC-C leg (profiling)")
     ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
     ap.add_argument("--tpcc-txns", type=int, default=65536, help="txns per TPC-C epoch")
     ap.add_argument("--timing", choices=["full", "kernel", "off"], default="off",
@@ -263,6 +264,9 @@ def main():
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if a.tpcc_only:
+        print(json.dumps({"tpcc": tpcc_leg(a)}), flush=True)
+        return
     cc_name = a.cc.upper()
     rows, n_txn, theta, desc = CONFIGS[a.config]
     R = 10
