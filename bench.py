@@ -426,6 +426,10 @@ def main():
             out["cpu_baseline_single_thread"] = single
         else:
             out["cpu_baseline"] = single
+    if rank == 0:  # Deneva's [summary] line (stats.cpp:425-500) for scripts/helper.py, on stderr
+        from dvcc.stats import summary_line
+        out["deneva_summary"] = summary_line(el, stats)
+        print(out["deneva_summary"], file=sys.stderr, flush=True)
     if world == 1 and not a.no_tpcc:
         out["tpcc"] = tpcc_leg(a)
     if rank == 0:
