@@ -3,6 +3,7 @@ rand(), hand-derived known answers from tpcc_helper.cpp / tpcc_txn.cpp, and
 the product's host-side loader and epoch builder (libdvcc, no GPU needed)
 against the oracle's restatement."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -173,3 +174,37 @@ def test_generator_mix(dv):
     first = e.txn_begin[:-1][pay]
     by_name = (e.tables[first + 2] == 5).mean()
     assert abs(by_name - 0.6) < 0.03
+
+
+GOLDEN_TPCC = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "tpcc")
+
+
+def _golden_names():
+    return sorted(f[:-4] for f in os.listdir(GOLDEN_TPCC) if f.endswith(".npz"))
+
+
+def test_tpcc_golden_set_complete():
+    from golden.make_golden_tpcc import CASES
+    assert sorted(CASES) == _golden_names()
+
+
+@pytest.mark.parametrize("name", _golden_names())
+def test_oracle_reproduces_tpcc_golden(name):
+    from golden.make_golden_tpcc import make
+    with np.load(os.path.join(GOLDEN_TPCC, name + ".npz")) as z:
+        g = {k: z[k] for k in z.files}
+    m = make(name)
+    assert sorted(g) == sorted(m)
+    for k in g:
+        assert np.array_equal(g[k], m[k]), k
+
+
+@pytest.mark.parametrize("name", _golden_names())
+def test_product_generator_matches_tpcc_golden(dv, name):
+    from golden.make_golden_tpcc import CASES, PARAMS
+    cc, n_txn, seed, perc = CASES[name]
+    e = dv.gen(dv.tpcc_params(perc_payment=perc, **PARAMS), n_txn, seed)
+    with np.load(os.path.join(GOLDEN_TPCC, name + ".npz")) as z:
+        for k, v in (("keys", e.keys), ("types", e.types), ("tables", e.tables), ("args", e.args),
+                     ("txn_begin", e.txn_begin)):
+            assert np.array_equal(z[k], v), k

@@ -206,3 +206,27 @@ def test_tpcc_runner_single_rank_rccl(cc):
         eng.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in __import__("os").listdir(
+    __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "tpcc")) if f.endswith(".npz")))
+def test_engine_matches_tpcc_golden(name):
+    import os
+    from golden.make_golden_tpcc import CASES, LOAD_SEED, PARAMS
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", "tpcc", name + ".npz")) as z:
+        g = {k: z[k] for k in z.files}
+    cc = {O.NO_WAIT: dvcc.NO_WAIT, O.WAIT_DIE: dvcc.WAIT_DIE, O.OCC: dvcc.OCC, O.CALVIN: dvcc.CALVIN}[int(g["cc"])]
+    pp = T.tpcc_params(perc_payment=float(g["perc"]), **PARAMS)
+    e = T.TpccEpoch(g["keys"], g["types"], g["txn_begin"], g["tables"], g["args"])
+    eng = T.TpccEngine(cc, pp, e.n_txn, seed=LOAD_SEED)
+    try:
+        before = [[eng.read_col(t, c) for c in range(3)] for t in range(5)]
+        c, o, st = _run(eng, e)
+        assert np.array_equal(c, g["commit"]) and np.array_equal(o, g["oid"])
+        assert (st.committed, st.aborted, st.write_cnt) == tuple(int(x) for x in g["stats"])
+        for t in range(5):
+            after = np.stack([eng.read_col(t, col) for col in range(3)], 1)
+            rows = np.flatnonzero((after != np.stack(before[t], 1)).any(1))
+            assert np.array_equal(rows, g[f"rows_{t}"]) and np.array_equal(after[rows], g[f"vals_{t}"]), t
+    finally:
+        eng.close()
