@@ -109,19 +109,20 @@ enum : uint32_t {
 };
 
 // ---- probe / queues (dvcc_kernels.hip)
+// counts: the first radix pass's per-tile digit counts (k_radix_hist layout)
 // pairs: sort keys; tb_start/tb_end: each txn's access range; tlen (optional):
 // its access count; acc_row (optional): row | wr << 31 per access.  An access
 // at position >= 1 << slog in its txn is an error (ERRB_BIG).
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr);
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
 // digit_tot: kRadix.  scatter_ev (optional): 2 events per pass for timing.
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev);
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done);
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
                         const uint32_t *tb_start, uint64_t *el, Counters *ctr);

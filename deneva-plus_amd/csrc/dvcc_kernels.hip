@@ -68,12 +68,20 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t *__restrict__ tb_start,
                                                   uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen,
-                                                  uint32_t *__restrict__ acc_row, Counters *ctr) {
-    const uint32_t lane = threadIdx.x & 63;
+                                                  uint32_t *__restrict__ acc_row, Counters *ctr,
+                                                  uint32_t *__restrict__ counts, uint32_t ntiles) {
+    // The first radix pass's histogram (digit = row bits [0, 8)) is counted
+    // here, per 4096-access sort tile, so the sort skips that k_radix_hist
+    // launch and its 8-byte-per-access re-read of the pairs.
+    __shared__ uint32_t wc[4][kRadix];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t per_block = (uint64_t)kBlock * kPV;
-    const uint64_t stride = (uint64_t)gridDim.x * per_block;
+    static_assert(kTile % (kBlock * kPV) == 0, "probe chunks tile the sort tiles");
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t d = threadIdx.x; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
+    __syncthreads();
     // block-uniform trip count so every lane takes part in the wave scans
-    for (uint64_t b0 = (uint64_t)blockIdx.x * per_block; b0 < n; b0 += stride) {
+    for (uint64_t b0 = (uint64_t)tile * kTile; b0 < n && b0 < (uint64_t)(tile + 1) * kTile; b0 += per_block) {
         const uint64_t wave0 = b0 + (threadIdx.x & ~63u) * kPV;   // first access of this wave
         const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPV;       // first access of this thread
         uint32_t txn[kPV], wr[kPV], tb[kPV];
@@ -187,18 +195,37 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
             for (int j = 0; j < kPV; j++)
                 if (i0 + j < n) pairs[i0 + j] = out[j];
         }
+        // digit-0 counts of the emitted pairs (as k_radix_hist: a step whose
+        // keys share one digit adds once)
+#pragma unroll
+        for (int j = 0; j < kPV; j++) {
+            const bool valid = i0 + j < n;
+            const uint32_t d = (uint32_t)row[j] & (kRadix - 1);
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            const uint64_t vmask = __ballot(valid);
+            if (__ballot(valid && d == d0) == vmask) {
+                if (lane == 0) wc[wave][d0] += (uint32_t)__popcll(vmask);
+            } else if (valid) {
+                atomicAdd(&wc[wave][d], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < kRadix; d += kBlock)
+        counts[(uint64_t)d * ntiles + tile] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+    __syncthreads();
     }
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr) {
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts) {
     if (n_acc == 0) return;
-    uint64_t blocks = (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
-    if (blocks > 4096) blocks = 4096;
-    k_probe<<<(uint32_t)blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn,
-                                                slog, pairs, tb_start, tb_end, tlen, acc_row, ctr);
+    const uint32_t ntiles = nblocks_for(n_acc);
+    const uint32_t blocks = ntiles > 4096 ? 4096u : ntiles;
+    k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
+                                      tb_end, tlen, acc_row, ctr, counts, ntiles);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -336,13 +363,13 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
 }
 
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev) {
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb);
+        if (pass > 0 || !hist0_done) k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb);
         k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot);
         // timing: events recorded by the dispatch itself (no extra packets)
         hipExtLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kBlock), 0, s,
