@@ -93,6 +93,7 @@ struct dv_ctx {
     uint32_t *d_txn = nullptr, *d_grant = nullptr;
     uint32_t *d_tb = nullptr;         // txn_begin
     uint32_t *split_err = nullptr;    // the record check's error bits (begin clears the counters)
+    uint64_t *d_args = nullptr, *d_oid = nullptr;  // dv_tpcc_epoch_run staging
 
     // epoch state
     int phase = 0;  // 0 idle, 1 begun
@@ -282,7 +283,7 @@ void dv_close(dv_ctx *c) {
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
-                    c->col1, c->col2, c->tp_keys, c->tp_tables, c->tp_flag, c->tp_scan, c->tp_dhead,
+                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_flag, c->tp_scan, c->tp_dhead,
                     c->tp_tmp};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
@@ -1127,11 +1128,14 @@ int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {
     return (int)n;
 }
 
-int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
-                 uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
-                 dv_stats *st) {
-    (void)ts;  // decisions follow sequence order; TS_CAS timestamps are monotone in it
-    if (!c || (n_acc && !acc) || !out_commit) return DV_ERR_ARG;
+}  // extern "C"
+
+namespace {
+// host buffers -> the context's device epoch (H2D of the 16-B records, then
+// split into SoA on the device, checked against txn_begin there)
+int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                     uint32_t n_txn, dv_epoch_dev *ep) {
+    if (!c || (n_acc && !acc)) return DV_ERR_ARG;
     if (n_acc > c->cfg.max_acc || n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     uint32_t max_len = 0;
     if (txn_begin) {  // CSR form: checked here per txn, against acc[].txn_seq on the device
@@ -1167,26 +1171,69 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
         launch_split_access(c->stream, c->d_acc, n_acc, txn_begin ? c->d_tb : nullptr, n_txn, c->d_keys,
                             c->d_types, c->d_txn, c->d_tables, c->split_err);
     }
-    dv_epoch_dev ep{};
-    ep.keys = c->d_keys;
-    ep.types = c->d_types;
-    ep.acc_txn = c->d_txn;
-    ep.tables = c->d_tables;
-    ep.n_acc = n_acc;
-    ep.n_txn = n_txn;
-    ep.max_txn_acc = max_len;
-    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
-    r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
-    if (r) return r;
+    *ep = dv_epoch_dev{};
+    ep->keys = c->d_keys;
+    ep->types = c->d_types;
+    ep->acc_txn = c->d_txn;
+    ep->tables = c->d_tables;
+    ep->n_acc = n_acc;
+    ep->n_txn = n_txn;
+    ep->max_txn_acc = max_len;
+    return DV_OK;
+}
+
+int staged_range_error(dv_ctx *c, uint64_t n_acc, const uint32_t *txn_begin) {
     if (n_acc && txn_begin) {  // a record outside its txn's CSR range
         uint32_t bad = 0;
         HIPCHK(hipMemcpy(&bad, c->split_err, sizeof(bad), hipMemcpyDeviceToHost));
         if (bad) return DV_ERR_TXN_RANGE;
     }
+    return DV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                 uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
+                 dv_stats *st) {
+    (void)ts;  // decisions follow sequence order; TS_CAS timestamps are monotone in it
+    if (!out_commit) return DV_ERR_ARG;
+    dv_epoch_dev ep;
+    int r = stage_host_epoch(c, acc, n_acc, txn_begin, n_txn, &ep);
+    if (r) return r;
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
+    if (!r) r = staged_range_error(c, n_acc, txn_begin);
+    if (r) return r;
     if (n_txn)
         HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
     if (calvin && out_grant && n_acc)
         HIPCHK(hipMemcpyAsync(out_grant, c->d_grant, n_acc * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+int dv_tpcc_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                      uint32_t n_txn, const uint64_t *args, uint8_t *out_commit, uint64_t *out_oid,
+                      dv_stats *st) {
+    if (!out_commit || (n_acc && !args)) return DV_ERR_ARG;
+    dv_epoch_dev ep;
+    int r = stage_host_epoch(c, acc, n_acc, txn_begin, n_txn, &ep);
+    if (r) return r;
+    if (!c->d_args) {
+        r = dalloc(&c->d_args, c->cfg.max_acc);
+        if (!r) r = dalloc(&c->d_oid, c->cfg.max_txn);
+        if (r) return r;
+    }
+    if (n_acc) HIPCHK(hipMemcpyAsync(c->d_args, args, n_acc * 8, hipMemcpyHostToDevice, c->stream));
+    r = dv_tpcc_epoch_run_device(c, &ep, c->d_args, c->d_commit, c->d_oid, st);
+    if (!r) r = staged_range_error(c, n_acc, txn_begin);
+    if (r) return r;
+    if (n_txn) {
+        HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
+        if (out_oid) HIPCHK(hipMemcpyAsync(out_oid, c->d_oid, (size_t)n_txn * 8, hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     return DV_OK;
 }

@@ -137,6 +137,8 @@ SIGNATURES = [
     ("dv_tpcc_gen", ctypes.c_int, [_P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                    _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("dv_tpcc_epoch_begin", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp]),
+    ("dv_tpcc_epoch_run", ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32, _vp, _vp, _vp,
+                                         _P(Stats)]),
     ("dv_load_table_cols", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, ctypes.c_uint64]),
     ("dv_read_table_col", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                          ctypes.c_uint64, _vp]),

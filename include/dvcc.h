@@ -354,6 +354,11 @@ int dv_read_table_col(dv_ctx *ctx, uint32_t table, uint32_t col, uint64_t first_
  * whose district is local (0 otherwise) */
 int dv_tpcc_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args,
                              uint8_t *d_commit, uint64_t *d_oid, dv_stats *st);
+/* the same from host buffers (H2D + run + D2H; records as dv_epoch_run);
+ * out_oid (may be NULL): n_txn words */
+int dv_tpcc_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                      uint32_t n_txn, const uint64_t *args, uint8_t *out_commit, uint64_t *out_oid,
+                      dv_stats *st);
 /* staged form for partitioned epochs: dv_epoch_begin of a TPC-C epoch (this
  * partition's accesses); then the rounds, and dv_epoch_finish executes the
  * committed txns' operations on this partition's rows.  d_args / d_oid must
