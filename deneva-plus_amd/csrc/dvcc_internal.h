@@ -109,7 +109,10 @@ enum : uint32_t {
 };
 
 // ---- probe / queues (dvcc_kernels.hip)
-// counts: the first radix pass's per-tile digit counts (k_radix_hist layout)
+// counts (optional): the first radix pass's per-tile digit counts (k_radix_hist
+// layout); worth it from kProbeHistTiles sort tiles up (below that a block per
+// tile leaves CUs idle)
+constexpr uint32_t kProbeHistTiles = 1024;
 // pairs: sort keys; tb_start/tb_end: each txn's access range; tlen (optional):
 // its access count; acc_row (optional): row | wr << 31 per access.  An access
 // at position >= 1 << slog in its txn is an error (ERRB_BIG).

@@ -77,11 +77,17 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t per_block = (uint64_t)kBlock * kPV;
     static_assert(kTile % (kBlock * kPV) == 0, "probe chunks tile the sort tiles");
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    for (uint32_t d = threadIdx.x; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
-    __syncthreads();
+    // work unit of a block: a whole sort tile when counting, else one chunk
+    // (small epochs keep one chunk per block so the launch fills the GPU)
+    const uint64_t unit = counts ? (uint64_t)kTile : per_block;
+    const uint64_t nunits = (n + unit - 1) / unit;
+    for (uint64_t tile = blockIdx.x; tile < nunits; tile += gridDim.x) {
+    if (counts) {
+        for (uint32_t d = threadIdx.x; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
+        __syncthreads();
+    }
     // block-uniform trip count so every lane takes part in the wave scans
-    for (uint64_t b0 = (uint64_t)tile * kTile; b0 < n && b0 < (uint64_t)(tile + 1) * kTile; b0 += per_block) {
+    for (uint64_t b0 = tile * unit; b0 < n && b0 < (tile + 1) * unit; b0 += per_block) {
         const uint64_t wave0 = b0 + (threadIdx.x & ~63u) * kPV;   // first access of this wave
         const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPV;       // first access of this thread
         uint32_t txn[kPV], wr[kPV], tb[kPV];
@@ -197,6 +203,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
         }
         // digit-0 counts of the emitted pairs (as k_radix_hist: a step whose
         // keys share one digit adds once)
+        if (counts) {
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             const bool valid = i0 + j < n;
@@ -209,11 +216,14 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                 atomicAdd(&wc[wave][d], 1u);
             }
         }
+        }
     }
-    __syncthreads();
-    for (uint32_t d = threadIdx.x; d < kRadix; d += kBlock)
-        counts[(uint64_t)d * ntiles + tile] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
-    __syncthreads();
+    if (counts) {
+        __syncthreads();
+        for (uint32_t d = threadIdx.x; d < kRadix; d += kBlock)
+            counts[(uint64_t)d * ntiles + tile] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+        __syncthreads();
+    }
     }
 }
 
@@ -223,7 +233,8 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
-    const uint32_t blocks = ntiles > 4096 ? 4096u : ntiles;
+    const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
+    const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
                                       tb_end, tlen, acc_row, ctr, counts, ntiles);
 }

@@ -698,14 +698,15 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
                        c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, c->ctr);
     c->ticket = 0;
+    const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
-                 calvin ? nullptr : c->acc_row, c->ctr, c->counts);
+                 calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
-                                ktiming(c) ? c->sev : nullptr, true);
+                                ktiming(c) ? c->sev : nullptr, fuse_hist);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
