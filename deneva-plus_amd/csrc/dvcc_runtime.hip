@@ -980,8 +980,12 @@ constexpr uint32_t kTailTryFactor = 4;
 constexpr double kAsyncLiveFrac = 0.5;
 constexpr bool kAsyncSpeculate = false;
 
+// Small epochs (TPC-C's 65K txns): the slices are a few elements per thread,
+// so an asynchronous iteration is cheap and the launch pays from round 1.
+constexpr uint64_t kAsyncSmallAcc = 2u << 20;
+
 uint32_t async_thresh(dv_ctx *c) {
-    const uint64_t frac = (uint64_t)(kAsyncLiveFrac * (double)c->n_acc);
+    const uint64_t frac = c->n_acc <= kAsyncSmallAcc ? c->n_acc : (uint64_t)(kAsyncLiveFrac * (double)c->n_acc);
     return (uint32_t)std::min<uint64_t>(frac, async_try_limit(c->async_g));
 }
 
