@@ -114,8 +114,10 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
         const uint64_t v = w & kOpMask;
         const uint32_t prow = __shfl_up(row, 1, 64);
         const bool head = valid && (i == 0 || (lane ? prow : pair_row(pairs[i - 1])) != row);
-        if (valid) flag[i] = com && op == DV_TOP_NO_DIST ? 1u : 0u;
-        if (head && row >= dist_base && row < dist_base + dist_rows) dhead[row - dist_base] = (uint32_t)i;
+        const bool dist_row = row >= dist_base && row < dist_base + dist_rows;
+        // o_id only for DISTRICT rows (an operation word naming another table is ignored)
+        if (valid) flag[i] = com && op == DV_TOP_NO_DIST && dist_row ? 1u : 0u;
+        if (head && dist_row) dhead[row - dist_base] = (uint32_t)i;
         if (com && (p & 1)) wcnt++;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
         if (com) {
