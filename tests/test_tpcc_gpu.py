@@ -115,7 +115,7 @@ def _global(batches):
 
 
 @pytest.mark.parametrize("cc", CCS)
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_tpcc_partitioned_engines(cc, world):
     """config E's layout on one GPU: `world` contexts, each the partition of
     its warehouses ((w-1) % PART_CNT, ITEM replicated); fragments routed by
