@@ -59,6 +59,7 @@ __device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint6
 // began in an earlier wave is walked back in memory (at most one per wave).
 // Repeated rows inside a txn are detected later, in row order (seg_prepare).
 constexpr int kPV = 4;
+template <bool HIST>
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
@@ -79,15 +80,11 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
     static_assert(kTile % (kBlock * kPV) == 0, "probe chunks tile the sort tiles");
     // work unit of a block: a whole sort tile when counting, else one chunk
     // (small epochs keep one chunk per block so the launch fills the GPU)
-    const uint64_t unit = counts ? (uint64_t)kTile : per_block;
+    const uint64_t unit = HIST ? (uint64_t)kTile : per_block;
     const uint64_t nunits = (n + unit - 1) / unit;
-    for (uint64_t tile = blockIdx.x; tile < nunits; tile += gridDim.x) {
-    if (counts) {
-        for (uint32_t d = threadIdx.x; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
-        __syncthreads();
-    }
-    // block-uniform trip count so every lane takes part in the wave scans
-    for (uint64_t b0 = tile * unit; b0 < n && b0 < (tile + 1) * unit; b0 += per_block) {
+    // one 1024-access chunk starting at b0 (block-uniform, so every lane
+    // takes part in the wave scans)
+    auto chunk = [&](const uint64_t b0) {
         const uint64_t wave0 = b0 + (threadIdx.x & ~63u) * kPV;   // first access of this wave
         const uint64_t i0 = b0 + (uint64_t)threadIdx.x * kPV;       // first access of this thread
         uint32_t txn[kPV], wr[kPV], tb[kPV];
@@ -203,7 +200,7 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
         }
         // digit-0 counts of the emitted pairs (as k_radix_hist: a step whose
         // keys share one digit adds once)
-        if (counts) {
+        if (HIST) {
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             const bool valid = i0 + j < n;
@@ -217,13 +214,20 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
             }
         }
         }
+    };
+    if (!HIST) {
+        for (uint64_t b0 = (uint64_t)blockIdx.x * per_block; b0 < n; b0 += (uint64_t)gridDim.x * per_block)
+            chunk(b0);
+        return;
     }
-    if (counts) {
+    for (uint64_t tile = blockIdx.x; tile < nunits; tile += gridDim.x) {
+        for (uint32_t d = threadIdx.x; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
+        __syncthreads();
+        for (uint64_t b0 = tile * unit; b0 < n && b0 < (tile + 1) * unit; b0 += per_block) chunk(b0);
         __syncthreads();
         for (uint32_t d = threadIdx.x; d < kRadix; d += kBlock)
             counts[(uint64_t)d * ntiles + tile] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
         __syncthreads();
-    }
     }
 }
 
@@ -235,8 +239,12 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     const uint32_t ntiles = nblocks_for(n_acc);
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
-    k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
-                                      tb_end, tlen, acc_row, ctr, counts, ntiles);
+    if (counts)
+        k_probe<true><<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
+                                                tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
+    else
+        k_probe<false><<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
+                                                 tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
 }
 
 // ------------------------------------------------------------- radix sort
