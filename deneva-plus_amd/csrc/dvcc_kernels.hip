@@ -19,6 +19,10 @@
 
 #include "dvcc_common.h"
 
+#ifndef DVCC_PROBE_HIST_WAVES
+#define DVCC_PROBE_HIST_WAVES 6
+#endif
+
 namespace dvcc {
 
 // ------------------------------------------------------------------ probe
@@ -60,7 +64,7 @@ __device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint6
 // Repeated rows inside a txn are detected later, in row order (seg_prepare).
 constexpr int kPV = 4;
 template <bool HIST>
-__global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
+__device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *__restrict__ keys,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n,
@@ -231,6 +235,28 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
     }
 }
 
+// the fused-histogram variant needs more registers: capped at 6 waves per SIMD
+__global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
+                                                  const uint8_t *__restrict__ types,
+                                                  const uint32_t *__restrict__ acc_txn,
+                                                  const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
+                                                  uint32_t slog, uint64_t *__restrict__ pairs,
+                                                  uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
+                                                  uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
+                                                  Counters *ctr) {
+    probe_body<false>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
+                      ctr, nullptr, 0);
+}
+__global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
+    Tables tabs, const uint64_t *__restrict__ keys, const uint8_t *__restrict__ types,
+    const uint32_t *__restrict__ acc_txn, const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
+    uint32_t slog, uint64_t *__restrict__ pairs, uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
+    uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
+    uint32_t ntiles) {
+    probe_body<true>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
+                     ctr, counts, ntiles);
+}
+
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
@@ -240,11 +266,11 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     if (counts)
-        k_probe<true><<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
-                                                tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
+        k_probe_hist<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
+                                               tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
     else
-        k_probe<false><<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
-                                                 tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
+        k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
+                                          tb_end, tlen, acc_row, ctr);
 }
 
 // ------------------------------------------------------------- radix sort
