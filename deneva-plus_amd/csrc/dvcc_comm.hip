@@ -25,7 +25,9 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdio>
+#include <mutex>
 #include <cstring>
 #include <vector>
 
@@ -117,8 +119,38 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
     }
 }
 
+// flags word of the argument vote (element-wise MAX across ranks)
+constexpr uint32_t kVoteBadArg = 1u, kVoteOverflow = 2u;
+
+// the received record count exceeds this context's capacity: a vote, so every
+// rank leaves together (xvote[1] |= kVoteOverflow)
+__global__ void k_recv_check(const uint64_t *__restrict__ recvc, uint32_t P, uint64_t cap,
+                             uint32_t *__restrict__ xvote) {
+    if (threadIdx.x != 0) return;
+    uint64_t n = 0;
+    for (uint32_t o = 0; o < P; o++) n += recvc[o];
+    if (n > cap) xvote[1] |= kVoteOverflow;
+}
+
+// ---- in-process group: element-wise MAX of the P ranks' buffers
+constexpr int kMaxLocalRanks = 16;
+template <class T>
+struct PeerPtrs {
+    const T *p[kMaxLocalRanks];
+};
+template <class T>
+__global__ __launch_bounds__(kBlock) void k_max_reduce(PeerPtrs<T> in, int P, T *__restrict__ out, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        T v = in.p[0][i];
+        for (int q = 1; q < P; q++) v = in.p[q][i] > v ? in.p[q][i] : v;
+        out[i] = v;
+    }
+}
+
+struct Xport;  // the collectives of one rank (below)
+
 struct DvComm {
-    ncclComm_t comm = nullptr;
+    Xport *x = nullptr;
     int nranks = 0, rank = 0;
     uint64_t acc_cap = 0;  // capacity of the record / SoA buffers
     uint32_t nb_cap = 0, txn_cap = 0;
@@ -127,7 +159,8 @@ struct DvComm {
     uint8_t *types = nullptr, *tables = nullptr, *verdict = nullptr;
     uint32_t *txn = nullptr, *counts = nullptr, *tot = nullptr, *err = nullptr;
     uint64_t *xcnt = nullptr;  // [2 * nranks]: send counts, received counts
-    uint32_t *xmax = nullptr;  // longest txn, all-reduced
+    uint32_t *xvote = nullptr; // [2]: longest txn, argument flags -- all-reduced (MAX)
+    uint32_t *gerr = nullptr;  // input-error bits, all-reduced (MAX)
 };
 
 }  // namespace dvcc
@@ -157,24 +190,173 @@ int alloc(T **p, uint64_t n) {
     return hip_fail2(hipMalloc(reinterpret_cast<void **>(p), sizeof(T) * (n ? n : 1)), "hipMalloc");
 }
 
+}  // namespace
+
+// The four collectives of the partitioned epoch, issued on the context's
+// stream in the same order by every rank.  RCCL between processes (one per
+// GPU, over xGMI) is the product; the in-process group runs the same driver
+// for P contexts in one process -- several partitions on one GPU -- so the
+// multi-rank protocol is tested on a one-GPU box.
+struct dvcc::Xport {
+    virtual ~Xport() = default;
+    // one u64 to every peer, one from every peer
+    virtual int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) = 0;
+    // bytes: send segment [sd[q], sd[q] + sc[q]) to peer q, receive rc[q] at rd[q]
+    virtual int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv,
+                            const size_t *rc, const size_t *rd, hipStream_t s) = 0;
+    // in place, element-wise MAX
+    virtual int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) = 0;
+    virtual int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) = 0;
+};
+
+namespace {
+
+struct RcclXport final : Xport {
+    ncclComm_t comm = nullptr;
+    int P = 0;
+    ~RcclXport() override {
+        if (comm) (void)ncclCommDestroy(comm);
+    }
+    int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) override {
+        return nccl_fail(ncclAllToAll(send, recv, 1, ncclUint64, comm, s), "ncclAllToAll");
+    }
+    int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv, const size_t *rc,
+                    const size_t *rd, hipStream_t s) override {
+        return nccl_fail(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint8, comm, s), "ncclAllToAllv");
+    }
+    int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override {
+        return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, comm, s), "ncclAllReduce");
+    }
+    int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override {
+        return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint8, ncclMax, comm, s), "ncclAllReduce");
+    }
+};
+
+// P ranks in one process, each driven by its own host thread.  A collective:
+// every rank publishes its buffers and an event behind the data on its
+// stream; host barrier; every rank makes its stream wait for the peers'
+// events and pulls (device copies, or a MAX kernel into private scratch);
+// it records a second event; host barrier; every rank waits for all
+// second events -- no peer still reads its buffers -- before it writes the
+// result in place or goes on.
+struct LocalGroup {
+    int P = 0;
+    int refs = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t gen = 0;
+    struct Slot {
+        const uint8_t *send = nullptr;
+        const size_t *sd = nullptr;
+        hipEvent_t ready = nullptr, done = nullptr;
+    };
+    std::vector<Slot> slot;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == P) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+struct LocalXport final : Xport {
+    LocalGroup *g = nullptr;
+    int r = 0;
+    uint8_t *scratch = nullptr;  // all-reduce result before it goes in place
+    uint64_t scratch_cap = 0;
+    ~LocalXport() override {
+        if (scratch) (void)hipFree(scratch);
+        LocalGroup::Slot &me = g->slot[r];
+        if (me.ready) (void)hipEventDestroy(me.ready);
+        if (me.done) (void)hipEventDestroy(me.done);
+        bool last = false;
+        {
+            std::lock_guard<std::mutex> lk(g->mu);
+            last = --g->refs == 0;
+        }
+        if (last) delete g;
+    }
+    int publish(const uint8_t *send, const size_t *sd, hipStream_t s) {
+        g->slot[r].send = send;
+        g->slot[r].sd = sd;
+        CHK(hip_fail2(hipEventRecord(g->slot[r].ready, s), "hipEventRecord"));
+        g->barrier();
+        for (int q = 0; q < g->P; q++) CHK(hip_fail2(hipStreamWaitEvent(s, g->slot[q].ready, 0), "wait"));
+        return DV_OK;
+    }
+    int retire(hipStream_t s) {
+        CHK(hip_fail2(hipEventRecord(g->slot[r].done, s), "hipEventRecord"));
+        g->barrier();
+        for (int q = 0; q < g->P; q++) CHK(hip_fail2(hipStreamWaitEvent(s, g->slot[q].done, 0), "wait"));
+        g->barrier();  // every rank has queued its waits before any event is recorded again
+        return DV_OK;
+    }
+    int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) override {
+        CHK(publish(reinterpret_cast<const uint8_t *>(send), nullptr, s));
+        for (int q = 0; q < g->P; q++)
+            CHK(hip_fail2(hipMemcpyAsync(recv + q, reinterpret_cast<const uint64_t *>(g->slot[q].send) + r, 8,
+                                         hipMemcpyDeviceToDevice, s), "copy"));
+        return retire(s);
+    }
+    int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv, const size_t *rc,
+                    const size_t *rd, hipStream_t s) override {
+        (void)sc;
+        CHK(publish(send, sd, s));
+        for (int q = 0; q < g->P; q++)
+            if (rc[q])
+                CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], g->slot[q].send + g->slot[q].sd[r], rc[q],
+                                             hipMemcpyDeviceToDevice, s), "copy"));
+        return retire(s);
+    }
+    template <class T>
+    int max_t(T *buf, uint64_t n, hipStream_t s) {
+        if (n * sizeof(T) > scratch_cap) {
+            CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+            if (scratch) (void)hipFree(scratch);
+            scratch = nullptr;
+            scratch_cap = 0;
+            CHK(alloc(&scratch, n * sizeof(T)));
+            scratch_cap = n * sizeof(T);
+        }
+        CHK(publish(reinterpret_cast<const uint8_t *>(buf), nullptr, s));
+        PeerPtrs<T> in{};
+        for (int q = 0; q < g->P; q++) in.p[q] = reinterpret_cast<const T *>(g->slot[q].send);
+        if (n) {
+            const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
+            k_max_reduce<T><<<(uint32_t)blocks, kBlock, 0, s>>>(in, g->P, reinterpret_cast<T *>(scratch), n);
+            CHK(hip_fail2(hipGetLastError(), "k_max_reduce"));
+        }
+        CHK(retire(s));
+        if (n) CHK(hip_fail2(hipMemcpyAsync(buf, scratch, n * sizeof(T), hipMemcpyDeviceToDevice, s), "copy"));
+        return DV_OK;
+    }
+    int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+};
+
 void free_bufs(DvComm *m) {
     void *b[] = {m->send, m->recv, m->keys, m->types, m->tables, m->verdict, m->txn,
-                 m->counts, m->tot, m->err, m->xcnt, m->xmax};
+                 m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
     m->keys = nullptr;
     m->types = m->tables = m->verdict = nullptr;
-    m->txn = m->counts = m->tot = m->err = m->xmax = nullptr;
+    m->txn = m->counts = m->tot = m->err = m->xvote = m->gerr = nullptr;
     m->xcnt = nullptr;
 }
 
-int reserve(DvComm *m, uint64_t acc, uint32_t nb, uint32_t txn) {
-    if (acc <= m->acc_cap && nb <= m->nb_cap && txn <= m->txn_cap && m->xcnt) return DV_OK;
-    free_bufs(m);
-    acc = std::max(acc, m->acc_cap);
-    nb = std::max(nb, m->nb_cap);
-    txn = std::max(txn, m->txn_cap);
+// every buffer an epoch of this context can need, sized once (dv_comm_init):
+// an allocation that fails inside an epoch would leave one rank outside the
+// collectives the others enter
+int reserve(DvComm *m, uint64_t acc, uint32_t txn) {
+    const uint32_t nb = nblocks_for(acc ? acc : 1);
     const uint32_t P = (uint32_t)m->nranks;
     CHK(alloc(&m->send, acc));
     CHK(alloc(&m->recv, acc));
@@ -187,7 +369,8 @@ int reserve(DvComm *m, uint64_t acc, uint32_t nb, uint32_t txn) {
     CHK(alloc(&m->tot, P));
     CHK(alloc(&m->err, 1));
     CHK(alloc(&m->xcnt, 2ull * P));
-    CHK(alloc(&m->xmax, 1));
+    CHK(alloc(&m->xvote, 2));
+    CHK(alloc(&m->gerr, 1));
     m->acc_cap = acc;
     m->nb_cap = nb;
     m->txn_cap = txn;
@@ -199,7 +382,7 @@ int reserve(DvComm *m, uint64_t acc, uint32_t nb, uint32_t txn) {
 void comm_free(DvComm *m) {
     if (!m) return;
     free_bufs(m);
-    if (m->comm) (void)ncclCommDestroy(m->comm);
+    delete m->x;
     delete m;
 }
 
@@ -225,57 +408,110 @@ int dv_comm_init(dv_ctx *c, const void *unique_id, int nranks, int rank) {
     slot->rank = rank;
     ncclUniqueId id;
     std::memcpy(&id, unique_id, sizeof(id));
-    int r = nccl_fail(ncclCommInitRank(&slot->comm, nranks, id, rank), "ncclCommInitRank");
+    RcclXport *x = new RcclXport();
+    x->P = nranks;
+    slot->x = x;
+    int r = nccl_fail(ncclCommInitRank(&x->comm, nranks, id, rank), "ncclCommInitRank");
+    if (r) x->comm = nullptr;
+    if (!r) r = reserve(slot, cfg.max_acc, cfg.max_txn);
     if (r) {
-        slot->comm = nullptr;
         comm_free(slot);
         slot = nullptr;
     }
     return r;
 }
 
+int dv_comm_init_local(dv_ctx **ctxs, int nranks) {
+    if (!ctxs || nranks < 1 || nranks > kMaxLocalRanks) return DV_ERR_ARG;
+    for (int q = 0; q < nranks; q++) {
+        if (!ctxs[q]) return DV_ERR_ARG;
+        const dv_config &cfg = ctx_config(ctxs[q]);
+        if ((int)cfg.part_cnt != nranks || (int)cfg.part_id != q) return DV_ERR_ARG;
+    }
+    LocalGroup *g = new LocalGroup();
+    g->P = nranks;
+    g->slot.resize(nranks);
+    int r = DV_OK;
+    for (int q = 0; q < nranks && !r; q++) {
+        dv_ctx *c = ctxs[q];
+        r = hip_fail2(hipSetDevice(ctx_config(c).device), "hipSetDevice");
+        if (!r) r = hip_fail2(hipEventCreateWithFlags(&g->slot[q].ready, hipEventDisableTiming), "event");
+        if (!r) r = hip_fail2(hipEventCreateWithFlags(&g->slot[q].done, hipEventDisableTiming), "event");
+        if (r) break;
+        DvComm *&slot = ctx_comm(c);
+        comm_free(slot);
+        slot = new DvComm();
+        slot->nranks = nranks;
+        slot->rank = q;
+        LocalXport *x = new LocalXport();
+        x->g = g;
+        x->r = q;
+        g->refs++;
+        slot->x = x;
+        r = reserve(slot, ctx_config(c).max_acc, ctx_config(c).max_txn);
+    }
+    if (g->refs == 0) {  // nothing handed out
+        for (auto &sl : g->slot) {
+            if (sl.ready) (void)hipEventDestroy(sl.ready);
+            if (sl.done) (void)hipEventDestroy(sl.done);
+        }
+        delete g;
+    }
+    return r;
+}
+
 int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st) {
-    if (!c || !home || (home->n_acc && (!home->keys || !home->types || !home->acc_txn))) return DV_ERR_ARG;
+    // No rank may leave between collectives on its own: arguments are voted
+    // on with the other ranks before anything depends on them, input errors
+    // found by the probe are combined before the rounds (every rank then
+    // reports the error at the same round), and the round loop's own exits
+    // depend only on combined verdicts, identical on every rank.  Only a
+    // missing context or communicator returns at once (no rank of this
+    // communicator can have entered a collective of it).
+    if (!c) return DV_ERR_ARG;
     DvComm *m = ctx_comm(c);
     if (!m) return DV_ERR_STATE;
-    if (home->n_txn > txns_per_rank) return DV_ERR_ARG;
     const dv_config &cfg = ctx_config(c);
     const uint32_t P = (uint32_t)m->nranks;
     const uint64_t n_txn64 = (uint64_t)txns_per_rank * P;
-    if (n_txn64 > cfg.max_txn) return DV_ERR_ARG;
-    const uint32_t n_txn = (uint32_t)n_txn64;
+    const bool bad = !home || (home->n_acc && (!home->keys || !home->types || !home->acc_txn)) ||
+                     home->n_txn > txns_per_rank || n_txn64 > cfg.max_txn || n_txn64 > m->txn_cap ||
+                     home->n_acc > m->acc_cap || !ctx_has_tables(c);
+    const uint32_t n_txn = bad ? 0u : (uint32_t)n_txn64;
+    const uint64_t n_home = bad ? 0 : home->n_acc;
     hipStream_t s = ctx_stream(c);
-    const uint32_t nb = home->n_acc ? (uint32_t)((home->n_acc + kTile - 1) / kTile) : 1;
-    CHK(reserve(m, std::max<uint64_t>(home->n_acc, cfg.max_acc), nb, n_txn));
+    const uint32_t nb = n_home ? nblocks_for(n_home) : 1;
 
-    // 1. split the batch by owner
-    if (home->n_acc) {
-        k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, home->n_acc, P, m->counts, nb);
+    // 1. split the batch by owner (a bad rank sends nothing)
+    if (n_home) {
+        k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, n_home, P, m->counts, nb);
         k_owner_scan<<<P, kBlock, 0, s>>>(m->counts, nb, m->tot);
-        k_owner_scatter<<<nb, kBlock, 0, s>>>(home->keys, home->types, home->acc_txn, home->n_acc, P,
+        k_owner_scatter<<<nb, kBlock, 0, s>>>(home->keys, home->types, home->acc_txn, n_home, P,
                                              (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb,
                                              m->send);
     } else {
         CHK(hip_fail2(hipMemsetAsync(m->tot, 0, P * sizeof(uint32_t), s), "memset"));
     }
     CHK(hip_fail2(hipGetLastError(), "owner split"));
-    // 2. counts, then the records
+    // 2. counts, the argument vote (longest txn, flags), then the records
     std::vector<uint32_t> tot(P);
     CHK(hip_fail2(hipMemcpyAsync(tot.data(), m->tot, P * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
     std::vector<uint64_t> sendc(P), recvc(P);
     for (uint32_t o = 0; o < P; o++) sendc[o] = tot[o];
     CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
-    CHK(nccl_fail(ncclAllToAll(m->xcnt, m->xcnt + P, 1, ncclUint64, m->comm, s), "ncclAllToAll"));
+    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
     // the longest txn anywhere sets the verdict-byte stride on every rank
-    const uint32_t mx = home->max_txn_acc ? home->max_txn_acc : kMaxPos;
-    CHK(hip_fail2(hipMemcpyAsync(m->xmax, &mx, 4, hipMemcpyHostToDevice, s), "H2D"));
-    CHK(nccl_fail(ncclAllReduce(m->xmax, m->xmax, 1, ncclUint32, ncclMax, m->comm, s), "ncclAllReduce"));
-    uint32_t gmax = 0;
+    const uint32_t vote[2] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u};
+    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
+    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, m->acc_cap), m->xvote);
+    CHK(m->x->max_u32(m->xvote, 2, s));
+    uint32_t gvote[2] = {0, 0};
     CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipMemcpyAsync(&gmax, m->xmax, 4, hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments or capacity were bad
     std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
     uint64_t n_recv = 0, so = 0;
     for (uint32_t o = 0; o < P; o++) {
@@ -286,15 +522,14 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
         rd[o] = n_recv * sizeof(dv_access);
         n_recv += recvc[o];
     }
-    if (n_recv > cfg.max_acc) return DV_ERR_ARG;
-    CHK(nccl_fail(ncclAllToAllv(m->send, sc.data(), sd.data(), m->recv, rc.data(), rd.data(), ncclUint8,
-                                m->comm, s),
-                  "ncclAllToAllv"));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->send), sc.data(), sd.data(),
+                          reinterpret_cast<uint8_t *>(m->recv), rc.data(), rd.data(), s));
     CHK(hip_fail2(hipMemsetAsync(m->err, 0, 4, s), "memset"));
     launch_split_access(s, m->recv, n_recv, nullptr, n_txn, m->keys, m->types, m->txn, m->tables, m->err);
     CHK(hip_fail2(hipGetLastError(), "unpack"));
 
-    // 3. the partition's epoch: rounds closed by list all-reduces
+    // 3. the partition's epoch: input errors combined, then the rounds closed
+    //    by list all-reduces
     dv_epoch_dev ep{};
     ep.keys = m->keys;
     ep.types = m->types;
@@ -302,26 +537,31 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
     ep.tables = nullptr;
     ep.n_acc = n_recv;
     ep.n_txn = n_txn;
-    ep.max_txn_acc = std::min<uint32_t>(gmax, kMaxPos);
+    ep.max_txn_acc = std::min<uint32_t>(gvote[0], kMaxPos);
     CHK(dv_epoch_begin(c, &ep, nullptr));
+    CHK(dv_epoch_errors_local(c, m->gerr));
+    CHK(m->x->max_u32(m->gerr, 1, s));
+    CHK(dv_epoch_errors_combined(c, m->gerr));
     if (cfg.cc_alg != DV_CALVIN) {
         constexpr uint32_t kLag = 2;  // rounds queued ahead of the outcome read
         std::vector<uint32_t> counts{n_txn};  // list length entering each known round
         uint32_t r = 0;
         while (counts.back() > 0) {
             CHK(dv_epoch_round_local(c, m->verdict));
-            CHK(nccl_fail(ncclAllReduce(m->verdict, m->verdict, counts.back(), ncclUint8, ncclMax, m->comm, s),
-                          "ncclAllReduce"));
+            CHK(m->x->max_u8(m->verdict, counts.back(), s));
             CHK(dv_epoch_round_apply(c, m->verdict, nullptr));
             if (++r >= kLag) {
                 uint32_t und = 0;
+                // an input error anywhere: every rank returns it here, at the same round
                 CHK(dv_epoch_round_wait(c, r - kLag, &und));
+                // the combined verdicts are the same on every rank, so is und
                 if (und != 0 && und >= counts.back()) return DV_ERR_STATE;  // every round decides one
                 counts.push_back(und);
             }
         }
     }
-    // 4. execute and report
+    // 4. execute and report (CALVIN: a rejected epoch executes nothing, and
+    //    every rank reports the combined error)
     return dv_epoch_finish(c, d_commit, st);
 }
 

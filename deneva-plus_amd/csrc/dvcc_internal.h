@@ -65,10 +65,15 @@ struct alignas(128) CtrSlot {
 };
 struct Counters {
     uint32_t err;         // ERRB_* bits of every failure seen
+    uint32_t peer_err;    // partitioned epochs: the input-error bits of every partition (MAX-combined)
+    uint32_t halt;        // 1: the asynchronous rounds yielded undecided txns; execution waits for the
+                          // synchronous rounds the host resumes (dv_epoch_finish)
     uint32_t async_go;        // the last asynchronous try: 1 ran, 2 declined, 0 nothing to do
     uint32_t async_iters;     // most iterations any asynchronous workgroup ran
     uint32_t async_r0;        // round the accepted asynchronous launch started at (0: none)
     uint32_t async_declined;  // asynchronous tries that found the live set too large
+    uint32_t async_yields;    // asynchronous launches whose workgroups yielded (no more tries this epoch)
+    uint32_t calvin_dups;     // CALVIN: some txn touches a row twice (k_calvin_dup_fix)
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
@@ -107,6 +112,15 @@ struct Tables {
 enum : uint32_t {
     ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16, ERRB_BIG = 32
 };
+// errors in the epoch's input, all found by the probe (or the host-record
+// check before it): once one is set -- on this partition or, for partitioned
+// epochs, on any (Counters::peer_err) -- the decision rounds are no-ops and
+// no execution kernel touches the tables, so a rejected epoch leaves them as
+// they were
+constexpr uint32_t ERRB_INPUT = ERRB_KEY | ERRB_DUP | ERRB_TXN | ERRB_TABLE | ERRB_BIG;
+__device__ __forceinline__ uint32_t input_err(const Counters *ctr) {
+    return (ctr->err | ctr->peer_err) & ERRB_INPUT;
+}
 
 // ---- probe / queues (dvcc_kernels.hip)
 // counts (optional): the first radix pass's per-tile digit counts (k_radix_hist
@@ -202,9 +216,13 @@ uint32_t tail_cap(bool el32);  // live accesses the tail holds in LDS
 // undecided".  A try that finds the live set too large changes nothing and
 // publishes pub->tl = r0 << 32 | 2 (declined); the rounds go on.
 constexpr uint32_t kAsyncGroups = 512;
-// tword: one 32-bit fact word per txn (scratch, n_txn words)
+// tword: one 32-bit fact word per txn (scratch, n_txn words).  A workgroup
+// yields after max_iters iterations or idle_ticks wall-clock ticks without a
+// decision; if any did, the finalize sets Counters::halt and publishes
+// pub->tl = r0 << 32 | 3 instead of closing the rounds (the host resumes them).
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
-                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub);
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
+                 uint64_t idle_ticks);
 uint32_t async_groups(int device);  // co-resident workgroups (<= kAsyncGroups; 0: unusable)
 uint32_t async_try_limit(uint32_t G);
 // round elements ((txn << slog | pos) << 3 | flags) fit 32 bits
@@ -217,6 +235,7 @@ struct DvComm;  // defined in dvcc_comm.hip
 dvcc::DvComm *&ctx_comm(dv_ctx *c);
 hipStream_t ctx_stream(dv_ctx *c);
 const dv_config &ctx_config(dv_ctx *c);
+bool ctx_has_tables(dv_ctx *c);  // some table is loaded (dv_epoch_begin's precondition)
 void comm_free(dvcc::DvComm *m);
 namespace dvcc {
 
@@ -230,11 +249,11 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
                   const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
                   uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot);
 
-// per-epoch reset: counters, tile tickets, status (value; padding aborted),
-// access ranges and counts
+// per-epoch reset: counters (err = *err_seed when given), tile tickets,
+// status (value; padding aborted), access ranges and counts
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        Counters *ctr);
+                        const uint32_t *err_seed, Counters *ctr);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,

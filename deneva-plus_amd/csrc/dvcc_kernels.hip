@@ -172,15 +172,20 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             if (i >= n) continue;
             const uint64_t start = (st[j] ? st[j] : ex) - 1;
             const uint32_t pos = (uint32_t)(i - start);
-            if (pos >> slog) set_err(ctr, ERRB_BIG);
+            // a txn longer than the epoch's declared bound (1 << slog verdict
+            // bytes per txn): an input error; positions and lengths are clamped
+            // so every later index stays inside its txn's slot (the epoch is
+            // rejected before anything executes, input_err)
+            const bool big = (pos >> slog) != 0;
+            if (big) set_err(ctr, ERRB_BIG);
             const uint32_t t = txn[j] < n_txn ? txn[j] : 0u;
-            out[j] = pair_pack(row[j], t, pos & (kMaxPos - 1), wr[j]);
+            out[j] = pair_pack(row[j], t, big ? 0u : pos, wr[j]);
             if (txn[j] < n_txn) {
                 if (pos == 0) tb_start[t] = (uint32_t)i;
                 const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
                 if (i + 1 == n || nt != txn[j]) {
                     tb_end[t] = (uint32_t)(i + 1);
-                    if (tlen) tlen[t] = (uint8_t)(pos + 1);
+                    if (tlen) tlen[t] = (uint8_t)(big ? (1u << slog) : pos + 1);
                 }
             }
         }
@@ -486,11 +491,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_prepare(const uint64_t *__restri
                     bnd = dup ? 0u : ((wr | pwr) ? 1u : 0u);
                 }
             }
-            dup_err |= dup && !calvin && i < n;
+            dup_err |= dup && i < n;
             out[j] = el_pack(pair_txn(pj), acc[j],
                              ((calvin && bnd) ? EL_BND : 0u) | (dup ? EL_DUP : 0u) | (head ? EL_HEAD : 0u) | wr);
         }
-        if (dup_err) set_err(ctr, ERRB_DUP);
+        if (dup_err) {
+            if (calvin) ctr->calvin_dups = 1u;  // k_calvin_dup_fix has work
+            else set_err(ctr, ERRB_DUP);
+        }
         if (i0 + kPV <= n) {
             *reinterpret_cast<ulonglong2 *>(el + i0) = ulonglong2{out[0], out[1]};
             *reinterpret_cast<ulonglong2 *>(el + i0 + 2) = ulonglong2{out[2], out[3]};
@@ -576,11 +584,29 @@ __global__ __launch_bounds__(kBlock) void k_calvin_pass(const uint64_t *__restri
     }
 }
 
+// A txn that touches a row several times reads it before any of its own
+// writes (run_calvin_txn: the reads, then the writes, ycsb_txn.cpp:327-353),
+// so a repeat access's "earlier WR" flag is its group's first access's:
+// own writes in front of it do not count.  Only launched work when
+// k_seg_prepare saw a repeat.
+__global__ __launch_bounds__(kBlock) void k_calvin_dup_fix(const uint64_t *__restrict__ el, uint64_t n,
+                                                           uint8_t *__restrict__ ew, const Counters *ctr) {
+    if (!ctr->calvin_dups) return;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        if (!(el[i] & EL_DUP)) continue;
+        uint64_t j = i;
+        while (j > 0 && (el[j] & EL_DUP)) j--;
+        ew[i] = ew[j];
+    }
+}
+
 void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant_out, uint8_t *ew,
                   uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
     if (n == 0) return;
     const uint32_t nb = (uint32_t)((n + kRTile - 1) / kRTile);
     k_calvin_pass<<<nb, kBlock, 0, s>>>(el, (uint32_t)n, grant_out, ew, desc, tile_ctr, tag, ctr);
+    const uint64_t fb = (n + kBlock - 1) / kBlock;
+    k_calvin_dup_fix<<<(uint32_t)(fb > 1024 ? 1024 : fb), kBlock, 0, s>>>(el, n, ew, ctr);
 }
 
 // ---------------------------------------------------------------- status
@@ -593,11 +619,15 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         uint32_t *__restrict__ tb_start,
                                                         uint32_t *__restrict__ tb_end,
                                                         uint8_t *__restrict__ tlen,
-                                                        uint32_t *__restrict__ tile_ctr, Counters *ctr) {
+                                                        uint32_t *__restrict__ tile_ctr,
+                                                        const uint32_t *__restrict__ err_seed, Counters *ctr) {
     if (blockIdx.x == 0) {
         uint32_t *w = reinterpret_cast<uint32_t *>(ctr);
         for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) w[i] = 0;
         for (uint32_t i = threadIdx.x; i < kTileCtrs; i += kBlock) tile_ctr[i] = 0;
+        __syncthreads();
+        // errors found before the epoch began (the host-record check)
+        if (threadIdx.x == 0 && err_seed) ctr->err = *err_seed;
     }
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
@@ -610,11 +640,11 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        Counters *ctr) {
+                        const uint32_t *err_seed, Counters *ctr) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
-                                       ctr);
+                                       err_seed, ctr);
 }
 
 // ---------------------------------------------------------------- execute
@@ -631,6 +661,7 @@ __global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pa
                                                  uint64_t *__restrict__ f0,
                                                  const uint64_t *__restrict__ pkey, Counters *ctr) {
     __shared__ unsigned long long part[4];
+    if (input_err(ctr)) return;  // a rejected epoch changes no row
     const uint64_t per_block = (uint64_t)kBlock * kPV;
     const uint64_t stride = (uint64_t)gridDim.x * per_block;
     unsigned long long acc = 0;
@@ -703,6 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      const uint64_t *__restrict__ pkey,
                                                      Counters *ctr) {
     __shared__ unsigned long long part[2][4];
+    if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     unsigned long long dig = 0, wcnt = 0;
     const uint32_t step = gridDim.x * (kBlock / 64) * 64;
@@ -781,6 +813,7 @@ void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb
 __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict__ status, uint32_t n,
                                                        uint8_t *__restrict__ out, Counters *ctr) {
     __shared__ uint32_t part[4];
+    if (ctr->halt) return;  // the rounds resume first (dv_epoch_finish)
     uint32_t cnt = 0;
     // 16 txns per thread per step
     for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u; i0 < n;

@@ -253,10 +253,10 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     E e[IPT];
     uint32_t v[IPT];
     uint32_t nhm = 0;  // bit j: the element after e[j] starts a new queue
+    uint32_t tmask = 0;  // bit j: a repeat access of its txn to the row (transparent)
     if constexpr (FIRST) {
         uint64_t pp = first == 0 ? sh.prev : (uint64_t)sh.el[pad16(first - 1)];
         const uint64_t pn = first + IPT < tile_n ? (uint64_t)sh.el[pad16(first + IPT)] : (uint64_t)sh.next;
-        bool dup = false;
         uint64_t p[IPT];
 #pragma unroll
         for (int j = 0; j < IPT; j++) p[j] = j < cnt ? (uint64_t)sh.el[pad16(first + j)] : ~0ull;
@@ -265,15 +265,38 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
             e[j] = (E)F_HEAD;
             if (j < cnt) {
                 const bool head = pair_row(pp) != pair_row(p[j]);
-                dup |= !head && pair_txn(pp) == pair_txn(p[j]);
-                const uint64_t id = ((uint64_t)pair_txn(p[j]) << slog) | pair_pos(p[j]);
-                e[j] = (E)((id << 3) | (head ? F_HEAD : 0u) | (uint32_t)(p[j] & 1u));
                 const uint64_t q = j + 1 < cnt ? p[j + 1] : (cnt < IPT ? ~0ull : pn);
+                // A txn that touches one row several times (same row and txn:
+                // adjacent in row order).  The repeats are transparent -- OK
+                // at once, no value in the scan, dropped -- and the group's
+                // first access stands for all of them with the OR of their
+                // types: OCC puts the row in the txn's write set if any access
+                // writes it (occ.cpp:296-317; a txn never validates against
+                // itself, 185-199).  NO_WAIT / WAIT_DIE re-lock the row through
+                // get_row (txn.cpp:790-803), which conflicts with the txn's own
+                // lock unless both are shared (row_lock.cpp:69): NO_WAIT aborts
+                // (86-90); WAIT_DIE, whose reference asserts here
+                // (row_lock.cpp:106), is given the same outcome -- a txn cannot
+                // wait for itself, so it dies (hazard H9).
+                const bool rep = !head && pair_txn(pp) == pair_txn(p[j]);
+                uint32_t wr = (uint32_t)(p[j] & 1u);
+                const uint64_t id = ((uint64_t)pair_txn(p[j]) << slog) | pair_pos(p[j]);
+                if (rep) {
+                    tmask |= 1u << j;
+                    vb8[id] = VB_OK;
+                    if (nowait && ((p[j] | pp) & 1u)) status[pair_txn(p[j])] = ST_ABORT;
+                } else if ((q >> 8) == (p[j] >> 8)) {  // the first of a group: OR of its types
+                    for (uint32_t k = base + first + j + 1; k < n && !wr; k++) {
+                        const uint64_t x = (uint64_t)el_in[k];
+                        if ((x >> 8) != (p[j] >> 8)) break;
+                        wr |= (uint32_t)(x & 1u);
+                    }
+                }
+                e[j] = (E)((id << 3) | (head ? F_HEAD : 0u) | (rep ? F_DONE : 0u) | wr);
                 nhm |= (pair_row(q) != pair_row(p[j]) ? 1u : 0u) << j;
                 pp = p[j];
             }
         }
-        if (dup) set_err(ctr, ERRB_DUP);  // a 2PL/OCC txn locks one row twice
     } else {
         // branch-free: first + j < kTile, so the padded index stays inside the image
 #pragma unroll
@@ -304,8 +327,9 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
         umask |= (s == ST_UNDEC ? 1u : 0u) << j;
         needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
         const bool single = (e[j] & F_HEAD) && ((nhm >> j) & 1u);
-        blk |= (s != ST_ABORT && !single ? 1u : 0u) << j;
-        v[j] = elem_value(e[j], s, nowait);
+        const bool transparent = FIRST && ((tmask >> j) & 1u);
+        blk |= (s != ST_ABORT && !single && !transparent ? 1u : 0u) << j;
+        v[j] = transparent ? 0u : elem_value(e[j], s, nowait);
     }
     // round 0: every element is needy; later: a queue running past the tile's
     // end is assumed to be followed by a needy element
@@ -389,7 +413,8 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
     __shared__ uint32_t s_tile;
     const uint32_t n_live = *n_in;
     const uint32_t und = und_in ? *und_in : 1u;
-    const uint32_t n = und ? n_live : 0u;  // nothing left to decide: no-op
+    // nothing left to decide, or a rejected epoch: no-op
+    const uint32_t n = und && !input_err(ctr) ? n_live : 0u;
     const uint32_t ntiles = (n + Geo<EIn>::kTile - 1) / Geo<EIn>::kTile;
     if (blockIdx.x == 0 && threadIdx.x == 0 && round < (uint32_t)kRoundLog && (und || round == 0)) {
         ctr->log_live[round] = n_live;
@@ -410,8 +435,8 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
                                   nowait, desc, tag, und_reset, ctr);
     }
     if (publisher) {
-        __hip_atomic_store(&pub->le, ((unsigned long long)n_live << 32) | ctr->err, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&pub->le, ((unsigned long long)n_live << 32) | ctr->err | ctr->peer_err,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(&pub->ru, ((unsigned long long)round << 32) | und, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -548,7 +573,7 @@ __global__ __launch_bounds__(kBlock) void k_list_apply(
                 __hip_atomic_store(&pub->und_log[round % RoundPub::kPubLog], 0u, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
                 __threadfence_system();
-                __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err,
+                __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err | ctr->peer_err,
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 __hip_atomic_store(&pub->ru, (unsigned long long)(round + 1) << 32, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_SYSTEM);
@@ -601,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_list_apply(
             __hip_atomic_store(&pub->und_log[round % RoundPub::kPubLog], tot, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
             __threadfence_system();
-            __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err,
+            __hip_atomic_store(&pub->le, ((unsigned long long)*n_live_next << 32) | ctr->err | ctr->peer_err,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&pub->ru, ((unsigned long long)(round + 1) << 32) | tot, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -644,7 +669,7 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
     uint32_t n = ctr->nlive[r0 & 1];
     uint32_t U = ctr->nund[r0 & 1];
     uint32_t round = r0;
-    bool ok = r0 > 0 && n <= TailGeo<E>::kCap && U <= TailGeo<E>::kCap;
+    bool ok = r0 > 0 && n <= TailGeo<E>::kCap && U <= TailGeo<E>::kCap && !input_err(ctr);
     if (!ok) {  // decline: the host resumes the multi-workgroup rounds at r0
         if (tid == 0 && pub)
             __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 1u, __ATOMIC_RELAXED,
@@ -792,8 +817,15 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
 // stale carry only delays decisions.  The slice's last element is never
 // dropped while its queue runs on, so a carry always describes that queue.
 // A workgroup leaves once no element of an undecided txn remains in its slice
-// and its carry no longer holds an undecided blocker; the lowest undecided
-// txn can always decide, so every workgroup leaves (bounded spin: ERRB_SPIN).
+// and its carry no longer holds an undecided blocker.  That needs every
+// workgroup resident at once: a workgroup waiting for facts only a
+// non-resident one can produce (a co-running kernel holding CUs) would never
+// learn them.  So a workgroup also leaves -- yields -- after `idle` wall-clock
+// ticks without deciding anything, or after `max_iters` iterations: the facts
+// it published stay true, the finalize turns them into status bytes and halts
+// execution (Counters::halt), and the host resumes the synchronous rounds from
+// the element array the launch started from (dv_epoch_finish).  Facts are
+// monotone, so that array plus the newer statuses is a valid round state.
 constexpr int kAsyncThreads = 512;
 constexpr int kAsyncWaves = kAsyncThreads / 64;
 // 28 elements per thread (128 VGPRs, two workgroups per CU): 7.3M live
@@ -804,7 +836,6 @@ constexpr int kAsyncWaves = kAsyncThreads / 64;
 // iterates many times per round's worth of progress.
 constexpr int kAsyncIPT = 28;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
-constexpr uint32_t kAsyncMaxIters = 1u << 18;
 constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
 constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
 
@@ -826,7 +857,7 @@ __device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t
 // do (no txn undecided, or an earlier try ran)
 __device__ __forceinline__ uint32_t async_gate(const Counters *ctr, uint32_t r0, uint32_t G,
                                                uint32_t thresh) {
-    if (ctr->async_r0 != 0 || ctr->nund[r0 & 1] == 0) return 0u;
+    if (ctr->async_r0 != 0 || ctr->async_yields != 0 || ctr->nund[r0 & 1] == 0 || input_err(ctr)) return 0u;
     const uint32_t n_all = ctr->nlive[r0 & 1];
     return n_all <= thresh && ((uint64_t)n_all + G - 1) / G <= kAsyncCap ? 1u : 2u;
 }
@@ -873,7 +904,8 @@ __device__ __forceinline__ uint32_t async_value(uint32_t e, bool undec, bool abo
 __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
                                                                uint32_t r0, uint32_t thresh,
                                                                uint32_t *tword, uint32_t *carry,
-                                                               int nowait, uint32_t max_iters) {
+                                                               int nowait, uint32_t max_iters,
+                                                               uint64_t idle) {
     constexpr int IPT = kAsyncIPT;
     using M = uint32_t;  // per-thread element bit masks
     __shared__ uint32_t sel[kAsyncCap];
@@ -882,7 +914,7 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     // per-iteration counters, double-buffered by iteration parity: slot p is
     // reset during the iteration before it is used, after every thread has
     // read it for the iteration before that
-    __shared__ uint32_t s_needy[2], s_moved[2], s_cin;
+    __shared__ uint32_t s_needy[2], s_moved[2], s_cin, s_quit;
     Counters *ctr = b.ctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
@@ -899,6 +931,8 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     if (tid == 0) s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
     __syncthreads();
     uint32_t it = 0;
+    bool yielded = true;                  // cleared when the slice has nothing left to learn
+    uint64_t last_move = wall_clock64();  // thread 0's: the last iteration that decided something
     for (; it < max_iters; it++) {
         const uint32_t p = it & 1u;
         // the value in front of the slice: carries back to the nearest head
@@ -1010,16 +1044,25 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
             __hip_atomic_store(carry + g, cout, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         n = own.c;
         __syncthreads();
-        if (s_needy[p] == 0 && (!cont_out || !(cout & (B_UA | B_UW)))) break;  // nothing left to learn
+        if (s_needy[p] == 0 && (!cont_out || !(cout & (B_UA | B_UW)))) {  // nothing left to learn
+            yielded = false;
+            break;
+        }
         // nothing decided here: the facts this slice waits for come from other
-        // workgroups -- back off before reading them again
+        // workgroups -- back off before reading them again, and yield once
+        // they have not come for `idle` ticks (their producer may not be
+        // resident).  Thread 0's clock decides for the workgroup.
+        if (tid == 0) {
+            const uint64_t now = wall_clock64();
+            if (s_moved[p]) last_move = now;
+            s_quit = now - last_move > idle;
+        }
+        __syncthreads();
+        if (s_quit) break;
         if (!s_moved[p]) __builtin_amdgcn_s_sleep(8);
     }
     if (tid == 0) {
-        if (it >= max_iters) {
-            set_err(ctr, ERRB_SPIN);
-            atomicMax(&ctr->spin_site, 2u);
-        }
+        if (yielded) ctr->halt = 1u;  // the finalize hands the rest to the synchronous rounds
         atomicMax(&ctr->async_iters, it);
     }
 }
@@ -1041,9 +1084,20 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
         }
         return;
     }
+    const bool yielded = ctr->halt != 0;  // some workgroup left undecided txns behind
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctr->async_r0 = r0;
-        ctr->nund[r0 & 1] = 0;  // the passes queued behind the try are no-ops
+        if (yielded) {
+            // no further tries this epoch; the round state of r0 stays as it
+            // was (nund, the element array), so the host's synchronous rounds
+            // resume from it with these statuses
+            ctr->async_yields++;
+            if (pub)
+                __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 3u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            ctr->async_r0 = r0;
+            ctr->nund[r0 & 1] = 0;  // the passes queued behind the try are no-ops
+        }
     }
     uint32_t und = 0;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
@@ -1051,7 +1105,7 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
         status[t] = s;
         und += s == ST_UNDEC ? 1u : 0u;
     }
-    if (und) atomicAdd(&my_slot(ctr).undecided, und);
+    if (und && !yielded) atomicAdd(&my_slot(ctr).undecided, und);
 }
 
 
@@ -1131,12 +1185,13 @@ void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, Roun
 }
 
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
-                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub) {
+                 uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
+                 uint64_t idle_ticks) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
     k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
                                                                     b.ctr);
-    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, kAsyncMaxIters);
+    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
     k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, r0, pub, b.ctr);
 }
 

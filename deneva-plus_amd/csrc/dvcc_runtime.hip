@@ -49,10 +49,8 @@ struct dv_ctx {
     // execution scratch, and the operation words / o_id output of this epoch
     uint64_t *tp_keys = nullptr;
     uint8_t *tp_tables = nullptr;
-    uint32_t *tp_flag = nullptr, *tp_scan = nullptr, *tp_dhead = nullptr;
-    void *tp_tmp = nullptr;
-    size_t tp_tmp_bytes = 0;
-    uint64_t tp_dhead_cap = 0;
+    uint64_t *tp_dsnap = nullptr;  // per district row: D_NEXT_O_ID before the epoch
+    uint64_t tp_dsnap_cap = 0;
     const uint64_t *tp_args = nullptr;
     uint64_t *tp_oid = nullptr;
 
@@ -106,6 +104,12 @@ struct dv_ctx {
     RoundPub *h_pub = nullptr;  // host-mapped round progress (single-GPU rounds)
     RoundPub *d_pub = nullptr;  // its device address
     uint32_t rounds_real = 0;   // rounds until every txn was decided
+    const uint32_t *err_seed = nullptr;  // dv_epoch_run: the record check's bits, for the next begin
+    // asynchronous rounds: a workgroup yields after this many iterations, or
+    // this many wall-clock ticks without a decision (dv_set_async_limits)
+    uint32_t async_max_iters = 1u << 18;
+    uint64_t async_idle_ticks = 0;
+    uint64_t wall_khz = 100000;  // hipDeviceAttributeWallClockRate
 
     // timing
     hipEvent_t ev[32] = {};
@@ -212,10 +216,15 @@ int err_from_bits(uint32_t b) {
     if (b & ERRB_TABLE) return DV_ERR_NO_TABLE;
     if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
     if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
+    if (b & ERRB_BIG) return DV_ERR_ARG;  // a txn longer than the epoch's max_txn_acc
     if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
     if (b & ERRB_SPIN) return DV_ERR_HIP;
     return DV_OK;
 }
+
+// idle time after which an asynchronous workgroup yields: the
+// whole asynchronous phase of a config-D epoch takes ~130 us
+constexpr uint64_t kAsyncIdleUs = 200;
 
 bool timing(dv_ctx *c) { return (c->cfg.flags & DV_FLAG_TIMING) != 0; }
 // dispatch timestamps of the scatter and pass launches (hipExtLaunchKernelGGL)
@@ -242,6 +251,11 @@ int sync_counters(dv_ctx *c) {
 DvComm *&ctx_comm(dv_ctx *c) { return c->comm; }
 hipStream_t ctx_stream(dv_ctx *c) { return c->stream; }
 const dv_config &ctx_config(dv_ctx *c) { return c->cfg; }
+bool ctx_has_tables(dv_ctx *c) {
+    for (const auto &t : c->tab)
+        if (t.loaded) return true;
+    return false;
+}
 
 extern "C" {
 
@@ -283,8 +297,7 @@ void dv_close(dv_ctx *c) {
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
-                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_flag, c->tp_scan, c->tp_dhead,
-                    c->tp_tmp};
+                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
@@ -341,6 +354,10 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
         if (!r) r = dalloc(&c->abounds, kAsyncGroups);
         if (!r) r = dalloc(&c->tword, c->n_txn_cap_pad);
         if (!r) c->async_g = async_groups(cfg->device);
+        int khz = 0;
+        if (!r && hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) == hipSuccess && khz > 0)
+            c->wall_khz = (uint64_t)khz;
+        c->async_idle_ticks = kAsyncIdleUs * c->wall_khz / 1000;
         // verdict bytes: 16 per txn; grown on demand for longer txns (dv_epoch_begin)
         c->vb8_cap = (uint64_t)c->n_txn_cap_pad << 4;
         if (!r) r = dalloc(&c->vb8, c->vb8_cap);
@@ -657,6 +674,8 @@ int dv_tpcc_load(dv_ctx *c, const dv_tpcc_params *p, uint64_t seed) {
 // (the lock thread's whole job for the epoch, calvin_thread.cpp:40-100).
 int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     if (!c || !ep) return DV_ERR_ARG;
+    const uint32_t *err_seed = c->err_seed;  // only for the epoch dv_epoch_run staged just now
+    c->err_seed = nullptr;
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     if (ep->n_acc && (!ep->keys || !ep->types || !ep->acc_txn)) return DV_ERR_ARG;
     bool any = false;
@@ -696,7 +715,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
-                       c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, c->ctr);
+                       c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr);
     c->ticket = 0;
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
@@ -838,12 +857,14 @@ int dv_epoch_round_wait(dv_ctx *c, uint32_t round, uint32_t *undecided) {
     return DV_OK;
 }
 
-int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
-    if (!c || c->phase != 1) return DV_ERR_STATE;
-    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
-    rec(c, 4);
+namespace {
+int run_rounds(dv_ctx *c, bool resume);
+
+// the execution of the committed txns and the commit bytes (every execution
+// kernel is a no-op for a rejected epoch, input_err, and while the rounds
+// are halted, Counters::halt)
+void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
     if (c->cfg.workload == DV_TPCC) {
-        if (!c->tp_args) { c->phase = 0; return DV_ERR_STATE; }  // only through dv_tpcc_epoch_run_device
         const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
         TpccExec x{};
         x.pairs = c->pairs[c->sorted];
@@ -854,36 +875,63 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         x.c0 = c->f0;
         x.c1 = c->col1;
         x.c2 = c->col2;
-        x.flag = c->tp_flag;
-        x.scan = c->tp_scan;
-        x.dhead = c->tp_dhead;
+        x.dsnap = c->tp_dsnap;
         x.dist_base = dt.row_base;
         x.dist_rows = dt.created ? dt.cap_rows : 0;
-        x.scan_tmp = c->tp_tmp;
-        x.scan_tmp_bytes = c->tp_tmp_bytes;
+        x.desc = c->desc;
+        x.tag = next_tag(c);
+        x.tile_ctr = next_ticket(c);
         x.oid = c->tp_oid;
         x.ctr = c->ctr;
-        if (c->tp_oid) HIPCHK(hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream));
+        if (c->tp_oid) (void)hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream);
         launch_tpcc_exec(c->stream, x);
-        c->tp_args = nullptr;  // per epoch (dv_tpcc_epoch_begin)
-        c->tp_oid = nullptr;
-    } else if (calvin)
+    } else if (c->cfg.cc_alg == DV_CALVIN) {
         launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey,
                     c->ctr);
-    else
+    } else {
         launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0,
                         c->pkey, c->cfg.cc_alg != DV_OCC, c->ctr);
+    }
     launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
+}
+}  // namespace
+
+int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
+    if (!c || c->phase != 1) return DV_ERR_STATE;
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    if (c->cfg.workload == DV_TPCC && !c->tp_args) {  // only through dv_tpcc_epoch_begin
+        c->phase = 0;
+        return DV_ERR_STATE;
+    }
+    rec(c, 4);
+    enqueue_exec(c, d_commit);
     rec(c, 5);
-    HIPCHK(hipGetLastError());
-    int r = sync_counters(c);
+    int r = hip_fail(hipGetLastError(), "execution launch");
+    if (!r) r = sync_counters(c);
+    if (!r && !calvin && c->h_ctr->halt) {
+        // the asynchronous rounds yielded (a workgroup waited too long for
+        // facts, e.g. while another kernel held CUs): the execution above was
+        // a no-op; finish the rounds synchronously, then execute
+        r = hip_fail(hipMemsetAsync(&c->ctr->halt, 0, sizeof(uint32_t), c->stream), "memset");
+        c->async_unconfirmed = false;
+        if (!r) r = run_rounds(c, true);
+        if (!r) {
+            rec(c, 4);
+            enqueue_exec(c, d_commit);
+            rec(c, 5);
+            r = hip_fail(hipGetLastError(), "execution launch");
+        }
+        if (!r) r = sync_counters(c);
+    }
     c->phase = 0;
+    c->tp_args = nullptr;  // per epoch (dv_tpcc_epoch_begin)
+    c->tp_oid = nullptr;
     if (r) return r;
-    r = err_from_bits(c->h_ctr->err);
+    r = err_from_bits(c->h_ctr->err | c->h_ctr->peer_err);
     if (r) {
         if (c->h_ctr->err & ERRB_SPIN)
-            std::fprintf(stderr, "dvcc: a bounded wait ran out (site %u: 1 look-back, 2 asynchronous rounds, "
-                         "3 tail)\n", c->h_ctr->spin_site);
+            std::fprintf(stderr, "dvcc: a bounded wait ran out (site %u: 1 look-back, 3 tail)\n",
+                         c->h_ctr->spin_site);
         return r;
     }
     if (!calvin && c->h_ctr->async_r0) {  // an asynchronous launch decided the rest
@@ -919,6 +967,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         st->sort_passes = c->sort_passes;
         st->async_launches = (uint16_t)std::min(c->async_launched, 0xFFFFu);
         st->async_declined = (uint16_t)std::min(c->h_ctr->async_declined, 0xFFFFu);
+        st->async_yields = c->h_ctr->async_yields;
         if (timing(c)) {
             st->ms_probe = elapsed(c, 0, 1);
             st->ms_sort = elapsed(c, 1, 2);
@@ -992,17 +1041,19 @@ uint32_t async_thresh(dv_ctx *c) {
 void async_try(dv_ctx *c, uint32_t r0) {
     c->async_launched++;
     round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, async_thresh(c),
-                c->abounds, c->tword, c->n_txn, c->d_pub);
+                c->abounds, c->tword, c->n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks);
 }
 
-int run_rounds(dv_ctx *c) {
-    __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
+// resume: continue after an asynchronous launch that yielded (dv_epoch_finish)
+// from the round it started at, without further asynchronous tries
+int run_rounds(dv_ctx *c, bool resume) {
+    if (!resume) __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
-    uint32_t prev = c->n_txn + 1, seen = 0;
+    uint32_t prev = c->n_txn + 1, seen = resume ? pub_round(c, nullptr) : 0;
     uint32_t tail_r0 = 0;             // round the pending tail launch starts at (0: none)
     const uint32_t cap = tail_cap(c->el32);
     uint32_t tail_limit = kTailTryFactor * cap;  // published live count that triggers a try
-    const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
+    const bool async = !resume && c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     // speculative tries start one round before the previous epoch's launch
     const uint32_t try_from = !kAsyncSpeculate ? ~0u : (c->async_hint > 1 ? c->async_hint - 1 : 1);
     for (;;) {
@@ -1061,7 +1112,7 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     int r = dv_epoch_begin(c, ep, d_grant);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
-        r = run_rounds(c);
+        r = run_rounds(c, false);
         if (r) { c->phase = 0; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
@@ -1079,22 +1130,16 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
     if (!c->tp_keys) {
         r = dalloc(&c->tp_keys, A);
         if (!r) r = dalloc(&c->tp_tables, A);
-        if (!r) r = dalloc(&c->tp_flag, A);
-        if (!r) r = dalloc(&c->tp_scan, A);
-        if (!r) {
-            c->tp_tmp_bytes = tpcc_scan_bytes(A);
-            r = dalloc(reinterpret_cast<uint8_t **>(&c->tp_tmp), c->tp_tmp_bytes ? c->tp_tmp_bytes : 1);
-        }
         if (r) return r;
     }
     const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
     const uint64_t drows = dt.created ? dt.cap_rows : 1;
-    if (c->tp_dhead_cap < drows) {
-        dfree(c->tp_dhead);
-        c->tp_dhead = nullptr;
-        r = dalloc(&c->tp_dhead, drows);
+    if (c->tp_dsnap_cap < drows) {
+        dfree(c->tp_dsnap);
+        c->tp_dsnap = nullptr;
+        r = dalloc(&c->tp_dsnap, drows);
         if (r) return r;
-        c->tp_dhead_cap = drows;
+        c->tp_dsnap_cap = drows;
     }
     // no host wait: a last name without customers resolves to key ~0, which
     // the probe of dv_epoch_begin then reports as DV_ERR_KEY_NOT_FOUND
@@ -1116,10 +1161,34 @@ int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *
     int r = dv_tpcc_epoch_begin(c, ep, d_args, d_oid);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
-        r = run_rounds(c);
+        r = run_rounds(c, false);
         if (r) { c->phase = 0; c->tp_args = nullptr; c->tp_oid = nullptr; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
+}
+
+int dv_set_async_limits(dv_ctx *c, uint32_t max_iters, uint32_t idle_us) {
+    if (!c) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    c->async_max_iters = max_iters ? max_iters : (1u << 18);
+    c->async_idle_ticks = (uint64_t)(idle_us ? idle_us : kAsyncIdleUs) * c->wall_khz / 1000;
+    return DV_OK;
+}
+
+// partitioned epochs: every partition must learn of an input error found on
+// any of them before the rounds, so that all leave at the same collective
+int dv_epoch_errors_local(dv_ctx *c, uint32_t *d_word) {
+    if (!c || !d_word) return DV_ERR_ARG;
+    if (c->phase != 1) return DV_ERR_STATE;
+    HIPCHK(hipMemcpyAsync(d_word, &c->ctr->err, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    return DV_OK;
+}
+
+int dv_epoch_errors_combined(dv_ctx *c, const uint32_t *d_word) {
+    if (!c || !d_word) return DV_ERR_ARG;
+    if (c->phase != 1) return DV_ERR_STATE;
+    HIPCHK(hipMemcpyAsync(&c->ctr->peer_err, d_word, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+    return DV_OK;
 }
 
 int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {
@@ -1175,6 +1244,7 @@ int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint
         HIPCHK(hipMemsetAsync(c->split_err, 0, sizeof(uint32_t), c->stream));
         launch_split_access(c->stream, c->d_acc, n_acc, txn_begin ? c->d_tb : nullptr, n_txn, c->d_keys,
                             c->d_types, c->d_txn, c->d_tables, c->split_err);
+        c->err_seed = c->split_err;  // the epoch starts with the record check's verdict (input_err)
     }
     *ep = dv_epoch_dev{};
     ep->keys = c->d_keys;
@@ -1187,14 +1257,6 @@ int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint
     return DV_OK;
 }
 
-int staged_range_error(dv_ctx *c, uint64_t n_acc, const uint32_t *txn_begin) {
-    if (n_acc && txn_begin) {  // a record outside its txn's CSR range
-        uint32_t bad = 0;
-        HIPCHK(hipMemcpy(&bad, c->split_err, sizeof(bad), hipMemcpyDeviceToHost));
-        if (bad) return DV_ERR_TXN_RANGE;
-    }
-    return DV_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -1202,14 +1264,22 @@ extern "C" {
 int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                  uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
                  dv_stats *st) {
-    (void)ts;  // decisions follow sequence order; TS_CAS timestamps are monotone in it
-    if (!out_commit) return DV_ERR_ARG;
+    if (!c || !out_commit) return DV_ERR_ARG;
+    // WAIT_DIE: decisions follow sequence order, which equals timestamp order
+    // when ts rises with it (TS_CAS, manager.cpp:52-57, taken in sequence
+    // order; a retried txn keeps its ts and is sequenced first,
+    // worker_thread.cpp:478-480).  Otherwise the reference would make txns
+    // wait (row_lock.cpp:119-147): not supported, rejected.  NO_WAIT and
+    // CALVIN never read ts; OCC's start_ts only feeds the history check,
+    // which is empty under central validation.
+    if (ts && c->cfg.cc_alg == DV_WAIT_DIE)
+        for (uint32_t t = 1; t < n_txn; t++)
+            if (ts[t] <= ts[t - 1]) return DV_ERR_ARG;
     dv_epoch_dev ep;
     int r = stage_host_epoch(c, acc, n_acc, txn_begin, n_txn, &ep);
     if (r) return r;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
-    if (!r) r = staged_range_error(c, n_acc, txn_begin);
     if (r) return r;
     if (n_txn)
         HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
@@ -1233,7 +1303,6 @@ int dv_tpcc_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uin
     }
     if (n_acc) HIPCHK(hipMemcpyAsync(c->d_args, args, n_acc * 8, hipMemcpyHostToDevice, c->stream));
     r = dv_tpcc_epoch_run_device(c, &ep, c->d_args, c->d_commit, c->d_oid, st);
-    if (!r) r = staged_range_error(c, n_acc, txn_begin);
     if (r) return r;
     if (n_txn) {
         HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));

@@ -15,15 +15,15 @@ struct TpccExec {
     const uint32_t *tb_start;  // per txn: first access
     const uint64_t *args;      // per access: op << 56 | operand
     uint64_t *c0, *c1, *c2;    // state columns (global row id)
-    uint32_t *flag, *scan;     // per access scratch
-    uint32_t *dhead;           // per district row: index of its queue head
+    uint64_t *dsnap;           // per district row: D_NEXT_O_ID before the epoch (scratch)
     uint64_t dist_base, dist_rows;
-    void *scan_tmp;
-    size_t scan_tmp_bytes;
+    uint64_t *desc;            // look-back descriptors (>= n / kRTile), tagged
+    uint32_t tag;
+    uint32_t *tile_ctr;        // a zeroed tile ticket
     uint64_t *oid;             // per txn (may be null)
     Counters *ctr;
 };
-size_t tpcc_scan_bytes(uint64_t n);
+// two launches: updates + D_NEXT_O_ID snapshots, then the o_id numbering
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x);
 
 }  // namespace dvcc

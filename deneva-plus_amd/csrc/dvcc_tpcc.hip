@@ -26,14 +26,13 @@
 //     in any order.  C_PAYMENT_CNT is loaded as the integer 1 and read as a
 //     double (a denormal): denormal + 1.0 rounds to 1.0 either way.
 //   - D_NEXT_O_ID: o_id of a NewOrder = D_NEXT_O_ID + 1 + (committed NewOrders
-//     before it in the district's queue), an exclusive scan of flags over the
-//     sorted pairs minus the scan value at the queue head; then the district
-//     word grows by its count.
+//     before it in the district's queue): the apply pass snapshots D_NEXT_O_ID
+//     at each district queue's head, then one single-pass segmented count
+//     (decoupled look-back, dvcc_common.h) numbers the committed NewOrders of
+//     every queue and the queue's last element stores the grown word.
 //   - S_QUANTITY is piecewise (s > q + 10 ? s - q : s - q + 91): the queue
 //     head walks its stock row's queue in order (stock queues are short: the
 //     NURand(8191) item choice spreads over max_items x warehouses rows).
-#include <hipcub/hipcub.hpp>
-
 #include "dvcc_internal.h"
 #include "dvcc_common.h"
 #include "dvcc_tpcc.h"
@@ -87,7 +86,8 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
     }
 }
 
-// pass 1: additive updates, stock queues, NewOrder flags, district queue heads.
+// pass 1: additive updates, stock queues, D_NEXT_O_ID snapshots at the
+// district queue heads.
 // Each wave takes 64 consecutive sorted accesses; the additive contributions
 // of a row's run inside the wave are summed by a segmented shuffle reduction
 // (rows are contiguous in sort order) and the run's first lane issues one
@@ -97,9 +97,9 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                                                        const uint8_t *__restrict__ status,
                                                        const uint32_t *__restrict__ tb_start,
                                                        const uint64_t *__restrict__ args, uint64_t *c0,
-                                                       uint64_t *c1, uint64_t *c2, uint32_t *__restrict__ flag,
-                                                       uint32_t *__restrict__ dhead, uint64_t dist_base,
-                                                       uint64_t dist_rows, Counters *ctr) {
+                                                       uint64_t *c1, uint64_t *c2, uint64_t *__restrict__ dsnap,
+                                                       uint64_t dist_base, uint64_t dist_rows, Counters *ctr) {
+    if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
     const uint32_t lane = threadIdx.x & 63;
     unsigned long long wcnt = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
@@ -115,9 +115,7 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
         const uint32_t prow = __shfl_up(row, 1, 64);
         const bool head = valid && (i == 0 || (lane ? prow : pair_row(pairs[i - 1])) != row);
         const bool dist_row = row >= dist_base && row < dist_base + dist_rows;
-        // o_id only for DISTRICT rows (an operation word naming another table is ignored)
-        if (valid) flag[i] = com && op == DV_TOP_NO_DIST && dist_row ? 1u : 0u;
-        if (head && dist_row) dhead[row - dist_base] = (uint32_t)i;
+        if (head && dist_row) dsnap[row - dist_base] = c1[row];  // D_NEXT_O_ID before the epoch
         if (com && (p & 1)) wcnt++;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
         if (com) {
@@ -174,42 +172,87 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
     if (lane == 0 && wcnt) atomicAdd(&my_slot(ctr).write_cnt, wcnt);
 }
 
-// pass 2: o_id of every committed NewOrder (new_order_5: ++D_NEXT_O_ID)
-__global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict__ pairs, uint64_t n,
-                                                     const uint32_t *__restrict__ flag,
-                                                     const uint32_t *__restrict__ scan,
-                                                     const uint32_t *__restrict__ dhead, uint64_t dist_base,
-                                                     const uint64_t *__restrict__ c1, uint64_t *__restrict__ oid) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        if (!flag[i]) continue;
-        const uint64_t p = pairs[i];
-        const uint32_t row = pair_row(p);
-        const uint32_t rank = scan[i] - scan[dhead[row - dist_base]];
-        if (oid) oid[pair_txn(p)] = c1[row] + 1 + rank;
-    }
-}
-
-// pass 3: D_NEXT_O_ID += committed NewOrders of the district (one atomic per
-// row run of a wave, as in pass 1)
-__global__ __launch_bounds__(kBlock) void k_tpcc_next_oid(const uint64_t *__restrict__ pairs, uint64_t n,
-                                                          const uint32_t *__restrict__ flag, uint64_t *c1) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t base = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); base < n; base += stride) {
-        const uint64_t i = base + lane;
-        const uint32_t f = i < n ? flag[i] : 0u;
-        if (__ballot(f != 0) == 0) continue;
-        const uint32_t row = i < n ? pair_row(pairs[i]) : 0xFFFFFFFFu;
-        uint32_t cnt = f;
+// pass 2: o_id of every committed NewOrder (new_order_5: o_id = ++D_NEXT_O_ID,
+// in sequence order per district) -- an OpSeg count over the row queues (head
+// = f, committed NewOrder on a DISTRICT row = c), one launch: tiles of kRTile
+// sorted accesses taken by ticket, decoupled look-back across tiles.  o_id =
+// snapshot + inclusive count; the queue's last element stores D_NEXT_O_ID =
+// snapshot + its inclusive count (one writer per row, no atomics).  An
+// operation word naming another table is ignored.
+__global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict__ pairs, uint32_t n,
+                                                     const uint8_t *__restrict__ status,
+                                                     const uint32_t *__restrict__ tb_start,
+                                                     const uint64_t *__restrict__ args,
+                                                     const uint64_t *__restrict__ dsnap, uint64_t dist_base,
+                                                     uint64_t dist_rows, uint64_t *__restrict__ c1,
+                                                     uint64_t *__restrict__ oid, uint64_t *desc,
+                                                     uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
+    __shared__ uint64_t s_el[kRTile + kRTile / kRIPT];
+    __shared__ uint64_t s_next, s_prev;
+    __shared__ uint32_t s_tile;
+    __shared__ Agg wt[4];
+    __shared__ Agg s_pre;
+    const uint32_t ntiles = (n + kRTile - 1) / kRTile;
+    if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile, base = tile * kRTile;
+    const uint32_t tile_n = n - base < (uint32_t)kRTile ? n - base : (uint32_t)kRTile;
+    load_tile64(pairs, base, tile_n, n, s_el, &s_next, ~0ull);
+    if (tid == 0) s_prev = base ? pairs[base - 1] : ~0ull;
+    __syncthreads();
+    const uint32_t first = tid * kRIPT;
+    const int cnt = first >= tile_n ? 0 : (tile_n - first < (uint32_t)kRIPT ? (int)(tile_n - first) : kRIPT);
+    uint64_t e[kRIPT];
+    uint32_t flags = 0, heads = 0;
+    Agg a{0u, 0u, 0u};
+    uint64_t pp = first == 0 ? s_prev : s_el[rpad(first - 1)];
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t o = __shfl_down(cnt, off, 64);
-            const uint32_t orow = __shfl_down(row, off, 64);
-            if (lane + off < 64 && orow == row) cnt += o;
+    for (int j = 0; j < kRIPT; j++) {
+        e[j] = j < cnt ? s_el[rpad(first + j)] : ~0ull;
+        if (j < cnt) {
+            const uint32_t row = pair_row(e[j]);
+            const bool head = pair_row(pp) != row;
+            bool f = false;
+            if (row >= dist_base && row < dist_base + dist_rows) {
+                const uint32_t t = pair_txn(e[j]);
+                f = status[t] == ST_COMMIT &&
+                    (uint32_t)(args[tb_start[t] + pair_pos(e[j])] >> 56) == DV_TOP_NO_DIST;
+            }
+            flags |= (f ? 1u : 0u) << j;
+            heads |= (head ? 1u : 0u) << j;
+            a = OpSeg::comb(a, Agg{head ? 1u : 0u, 0u, f ? 1u : 0u});
+            pp = e[j];
         }
-        const uint32_t prow = __shfl_up(row, 1, 64);
-        if (i < n && (lane == 0 || prow != row) && cnt)
-            atomicAdd(reinterpret_cast<unsigned long long *>(c1 + row), (unsigned long long)cnt);
+    }
+    const uint64_t nxt = first + kRIPT < tile_n ? s_el[rpad(first + kRIPT)] : s_next;
+    const Agg inc = wave_incl<OpSeg>(a, lane);
+    if (lane == 63) wt[wave] = inc;
+    __syncthreads();
+    if (wave == 0) {
+        Agg bagg = wt[0];
+        for (int w = 1; w < 4; w++) bagg = OpSeg::comb(bagg, wt[w]);
+        const Agg pre = look_back<OpSeg>(desc, tile, tag, bagg, lane, ctr);
+        if (lane == 0) s_pre = pre;
+    }
+    __syncthreads();
+    Agg run = s_pre;
+    for (uint32_t w = 0; w < wave; w++) run = OpSeg::comb(run, wt[w]);
+    run = OpSeg::comb(run, wave_excl_from_incl<OpSeg>(inc, lane));
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++) {
+        if (j < cnt) {
+            const uint32_t f = (flags >> j) & 1u;
+            run = OpSeg::comb(run, Agg{(heads >> j) & 1u, 0u, f});  // inclusive count since the head
+            const uint32_t row = pair_row(e[j]);
+            if (row >= dist_base && row < dist_base + dist_rows) {
+                const uint64_t snap = dsnap[row - dist_base];
+                if (f && oid) oid[pair_txn(e[j])] = snap + run.c;
+                const uint64_t q = j + 1 < cnt ? e[j + 1] : (j + 1 < kRIPT ? ~0ull : nxt);
+                if (pair_row(q) != row && run.c) c1[row] = snap + run.c;  // the queue's last element
+            }
+        }
     }
 }
 
@@ -227,22 +270,13 @@ void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys
     k_tpcc_resolve<<<grid_for(n), kBlock, 0, s>>>(tabs, keys, tables, n, col0, okeys, otables);
 }
 
-size_t tpcc_scan_bytes(uint64_t n) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (int)(n ? n : 1));
-    return bytes;
-}
-
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
     if (x.n == 0) return;
-    const uint32_t g = grid_for(x.n);
-    k_tpcc_apply<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2, x.flag,
-                                      x.dhead, x.dist_base, x.dist_rows, x.ctr);
-    size_t bytes = x.scan_tmp_bytes;
-    (void)hipcub::DeviceScan::ExclusiveSum(x.scan_tmp, bytes, x.flag, x.scan, (int)x.n, s);
-    k_tpcc_oid<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.flag, x.scan, x.dhead, x.dist_base, x.c1, x.oid);
-    k_tpcc_next_oid<<<g, kBlock, 0, s>>>(x.pairs, x.n, x.flag, x.c1);
+    k_tpcc_apply<<<grid_for(x.n), kBlock, 0, s>>>(x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2,
+                                                  x.dsnap, x.dist_base, x.dist_rows, x.ctr);
+    const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
+    k_tpcc_oid<<<ntiles, kBlock, 0, s>>>(x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
+                                         x.dist_base, x.dist_rows, x.c1, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
 }
 
 }  // namespace dvcc

@@ -70,7 +70,8 @@ class Stats(ctypes.Structure):
                 ("scatter_launches", ctypes.c_uint32), ("pass_launches", ctypes.c_uint32),
                 ("ms_pass", ctypes.c_float), ("async_launches", ctypes.c_uint16),
                 ("async_declined", ctypes.c_uint16),
-                ("pass_live", ctypes.c_uint64)]
+                ("pass_live", ctypes.c_uint64), ("async_yields", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
@@ -121,12 +122,16 @@ SIGNATURES = [
     ("dv_epoch_carry", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(EpochDev)]),
     ("dv_comm_unique_id", ctypes.c_int, [_vp]),
     ("dv_comm_init", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
+    ("dv_comm_init_local", ctypes.c_int, [_P(_vp), ctypes.c_int]),
     ("dv_epoch_run_part", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _vp, _P(Stats)]),
     ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),
     ("dv_epoch_round_wait", ctypes.c_int, [_vp, ctypes.c_uint32, _P(ctypes.c_uint32)]),
     ("dv_epoch_finish", ctypes.c_int, [_vp, _vp, _P(Stats)]),
     ("dv_round_log", ctypes.c_int, [_vp, _P(ctypes.c_uint32), _P(ctypes.c_uint32), ctypes.c_uint32]),
+    ("dv_epoch_errors_local", ctypes.c_int, [_vp, _vp]),
+    ("dv_epoch_errors_combined", ctypes.c_int, [_vp, _vp]),
+    ("dv_set_async_limits", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
     ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_uint32, _vp, _vp, _vp]),
     ("dv_tpcc_table_rows", ctypes.c_int, [_P(TpccParams), ctypes.c_uint32, ctypes.c_uint32,

@@ -182,6 +182,11 @@ class CCEngine:
             stream = L.lib().dv_own_stream(self._ctx)
         L.check(L.lib().dv_set_stream(self._ctx, stream), "dv_set_stream")
 
+    def set_async_limits(self, max_iters=0, idle_us=0):
+        """Asynchronous rounds: a workgroup yields after max_iters iterations
+        or idle_us without a decision (0 = defaults); testing knob."""
+        L.check(L.lib().dv_set_async_limits(self._ctx, max_iters, idle_us), "dv_set_async_limits")
+
     def set_timing(self, timing):
         """Between epochs: True = per-stage events, "kernel" = only the scatter
         and pass launches' dispatch timestamps, False = none."""
@@ -250,6 +255,14 @@ class CCEngine:
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         L.check(L.lib().dv_comm_init(self._ctx, buf, nranks, rank), "dv_comm_init")
 
+    @staticmethod
+    def comm_init_local(engines):
+        """Partitioned epochs among engines of this process (engine q owns
+        partition q), e.g. several partitions on one GPU: drive each engine's
+        run_epoch_part from its own thread."""
+        arr = (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
+        L.check(L.lib().dv_comm_init_local(arr, len(engines)), "dv_comm_init_local")
+
     def run_epoch_part(self, home, txns_per_rank, d_commit=None):
         """One partitioned epoch from this rank's client batch (DeviceEpoch,
         txn ids local); d_commit: nranks * txns_per_rank device bytes."""
@@ -311,6 +324,16 @@ class CCEngine:
         und = ctypes.c_uint32()
         L.check(L.lib().dv_epoch_round_wait(self._ctx, r, ctypes.byref(und)), "dv_epoch_round_wait")
         return und.value
+
+    def errors_local(self, d_word):
+        """Partitioned epochs: enqueue this partition's input-error bits into
+        the device int32 tensor d_word (combine with MAX across ranks)."""
+        L.check(L.lib().dv_epoch_errors_local(self._ctx, _ptr(d_word)), "dv_epoch_errors_local")
+
+    def errors_combined(self, d_word):
+        """... and hand the combined word back: an error anywhere rejects the
+        epoch on every partition, at the same round."""
+        L.check(L.lib().dv_epoch_errors_combined(self._ctx, _ptr(d_word)), "dv_epoch_errors_combined")
 
     def finish(self, d_commit=None):
         st = L.Stats()

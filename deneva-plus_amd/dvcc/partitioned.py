@@ -24,6 +24,13 @@ GET_NODE_ID(part) == part, system/global.h:294).  Per epoch:
    on every rank;
 5. every rank executes the committed accesses on its own rows.
 
+Errors are collective: after the probe, one all-reduce(MAX) of every
+partition's input-error bits (missing key, bad txn order, ...) makes every
+rank treat the epoch as rejected, so all of them raise at the same round --
+none is left waiting in a collective the others never reach.  The round loop's
+other exits (stalled rounds) depend only on the combined verdicts, which are
+identical on every rank.
+
 Decisions are identical to the single-thread E-schedule over the whole
 epoch, whatever the number of GPUs.
 
@@ -120,6 +127,10 @@ class PartitionedRunner:
         n_txn = pe.n_txn_global
         extra = {"tables": cols[3], "args": cols[4]} if len(cols) > 3 else {}
         self.engine.begin_partition(*cols[:3], n_txn, max_txn_acc=pe.max_txn_acc, **extra)
+        err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.engine.errors_local(err)
+        dist.all_reduce(err, op=dist.ReduceOp.MAX, group=self.group)
+        self.engine.errors_combined(err)
         rounds = 0
         if self.engine.needs_votes:
             verdict = torch.zeros((n_txn + 3) // 4 * 4, dtype=torch.uint8, device=self.device)
@@ -162,6 +173,12 @@ class EnginePartition:
             self.engine.begin_tpcc(self._dep, args, self.oid)
         else:
             self.engine.begin(self._dep)
+
+    def errors_local(self, word):
+        self.engine.errors_local(word)
+
+    def errors_combined(self, word):
+        self.engine.errors_combined(word)
 
     def round_local(self, verdict):
         self.engine.round_local(verdict)

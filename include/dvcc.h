@@ -65,11 +65,14 @@ extern "C" {
 
 /* status codes (the reference returns enum RC, system/global.h:236) */
 #define DV_OK 0
-#define DV_ERR_ARG (-1)           /* bad argument / capacity exceeded             */
+#define DV_ERR_ARG (-1)           /* bad argument / capacity exceeded (also: a txn
+                                     longer than the epoch's max_txn_acc, a WAIT_DIE
+                                     ts array not rising in sequence order)       */
 #define DV_ERR_HIP (-2)           /* HIP runtime error                            */
 #define DV_ERR_NOMEM (-3)         /* device allocation failed                     */
 #define DV_ERR_KEY_NOT_FOUND (-4) /* index probe missed (M_ASSERT_V, index_hash.cpp:225) */
-#define DV_ERR_DUP_ROW (-5)       /* 2PL/OCC txn touches one row twice (unsupported) */
+#define DV_ERR_DUP_ROW (-5)       /* reserved (repeated rows in a txn are supported:
+                                     dvcc_rounds.hip, round 0)                    */
 #define DV_ERR_NO_TABLE (-6)      /* table id not created / not loaded            */
 #define DV_ERR_STATE (-7)         /* call out of order (e.g. round before begin)  */
 #define DV_ERR_NO_DEVICE (-8)     /* no usable HIP device                         */
@@ -172,6 +175,9 @@ typedef struct dv_stats {
     uint16_t async_launches; /* asynchronous-round launches (accepted or not)  */
     uint16_t async_declined; /* ... that found the live set too large          */
     uint64_t pass_live;      /* live accesses those launches read, summed      */
+    uint32_t async_yields;   /* asynchronous launches that yielded: the rounds
+                                were finished synchronously (dv_set_async_limits) */
+    uint32_t reserved;
 } dv_stats;
 
 /* parameters of YCSBQueryGenerator (g_* globals, system/global.cpp:65-195) */
@@ -215,7 +221,14 @@ int dv_load_ycsb_partition(dv_ctx *ctx, uint64_t rows_per_part); /* table 0 */
 int dv_read_rows(dv_ctx *ctx, uint32_t table, const uint64_t *keys, uint64_t n, uint64_t *out_f0);
 int dv_read_table(dv_ctx *ctx, uint32_t table, uint64_t first_row, uint64_t n, uint64_t *out_f0);
 
-/* whole epoch from host buffers (H2D + run + D2H) */
+/* whole epoch from host buffers (H2D + run + D2H).  ts (may be NULL): one
+ * timestamp per txn; WAIT_DIE requires it to rise strictly in sequence order
+ * (DV_ERR_ARG otherwise: the reference would make txns wait, row_lock.cpp:
+ * 119-147); the other algorithms' decisions do not depend on it.  A txn that
+ * touches one row several times: CALVIN locks it once with the first access's
+ * type (txn.cpp:778-788); OCC puts it in the write set if any access writes
+ * it; NO_WAIT / WAIT_DIE abort the txn unless every access to the row reads
+ * (its own lock conflicts, row_lock.cpp:69, 86-90). */
 int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                  uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit,
                  uint32_t *out_grant_group, dv_stats *st);
@@ -251,6 +264,12 @@ int dv_epoch_carry(dv_ctx *ctx, const dv_epoch_dev *ep, uint32_t max_txn, dv_epo
  * deneva-plus_amd/dvcc/partitioned.py over torch.distributed. */
 int dv_comm_unique_id(void *id_out);
 int dv_comm_init(dv_ctx *ctx, const void *unique_id, int nranks, int rank);
+/* the same partitioned epochs for nranks (<= 16) contexts of ONE process --
+ * e.g. several partitions on one GPU: ctxs[q] owns partition q; the
+ * collectives become device copies between the contexts' streams and a host
+ * barrier, so each context must be driven by its own host thread
+ * (dv_epoch_run_part called concurrently).  Same protocol, same decisions. */
+int dv_comm_init_local(dv_ctx **ctxs, int nranks);
 int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st);
 
@@ -273,6 +292,22 @@ int dv_epoch_round_local(dv_ctx *ctx, uint8_t *d_verdict);
 int dv_epoch_round_apply(dv_ctx *ctx, const uint8_t *d_verdict, uint32_t *undecided);
 int dv_epoch_round_wait(dv_ctx *ctx, uint32_t round, uint32_t *undecided);
 int dv_epoch_finish(dv_ctx *ctx, uint8_t *d_commit, dv_stats *st);
+
+/* partitioned epochs, between dv_epoch_begin and the first round: enqueue a
+ * copy of this partition's input-error bits (probe: missing key, bad txn
+ * order, ...) into the device word d_word; combine the words of all
+ * partitions with MAX and hand the result to dv_epoch_errors_combined.  Every
+ * partition then treats the epoch as rejected -- rounds are no-ops, each
+ * round's outcome reports the error, nothing executes -- so all ranks leave
+ * the round loop at the same collective with the same verdict. */
+int dv_epoch_errors_local(dv_ctx *ctx, uint32_t *d_word);
+int dv_epoch_errors_combined(dv_ctx *ctx, const uint32_t *d_word);
+
+/* asynchronous decision rounds: a workgroup yields after max_iters iterations
+ * or idle_us microseconds without a decision (0 = defaults: 2^18, 200 us);
+ * the rounds are then finished synchronously (same decisions).  Between
+ * epochs; lower values are a testing knob. */
+int dv_set_async_limits(dv_ctx *ctx, uint32_t max_iters, uint32_t idle_us);
 
 /* diagnostics: per decision round of the last finished epoch, the live
  * accesses entering the round and the undecided txns before it; returns the

@@ -389,9 +389,13 @@ static int lock_get(or_locks *L, int cc, uint64_t r, uint8_t type, uint32_t txn,
     if (conflict) {
         if (cc == OR_NO_WAIT) return OR_ABORT;                             /* 86-90  */
         if (cc == OR_WAIT_DIE) {                                           /* 91-151 */
+            /* hazard H9: a txn re-locking a row it owns in a
+             * conflicting mode meets itself among the owners, where the
+             * reference asserts (line 106); it cannot wait for itself, so it
+             * dies -- the NO_WAIT outcome (86-90) */
             int canwait = 1;
             for (uint32_t en = L->owners[r]; en != NIL; en = L->ent[en].next)
-                if (L->ts[txn] > L->ts[L->ent[en].txn]) { canwait = 0; break; }
+                if (L->ent[en].txn == txn || L->ts[txn] > L->ts[L->ent[en].txn]) { canwait = 0; break; }
             if (!canwait) return OR_ABORT;
             return -100; /* a real wait never arises under the E-schedule */
         }

@@ -36,13 +36,28 @@ def test_library_exports_every_declared_symbol():
     assert set(_declared_symbols()) == bound
 
 
-def test_struct_layouts_match_header():
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirrors against the header itself, compiled by gcc."""
+    import subprocess
     from dvcc import _lib
-    assert ctypes.sizeof(_lib.Access) == 16
-    assert ctypes.sizeof(_lib.Config) == 40
-    assert ctypes.sizeof(_lib.EpochDev) == 48
-    assert ctypes.sizeof(_lib.YcsbParams) == 56
-    assert ctypes.sizeof(_lib.Stats) == 104
+    structs = {"dv_access": _lib.Access, "dv_config": _lib.Config, "dv_epoch_dev": _lib.EpochDev,
+               "dv_ycsb_params": _lib.YcsbParams, "dv_stats": _lib.Stats, "dv_tpcc_params": _lib.TpccParams}
+    src = tmp_path / "sz.c"
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dvcc.h"', "int main(void) {"]
+    for name, cls in structs.items():
+        lines.append(f'printf("{name} %zu\\n", sizeof({name}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{name}.{f} %zu\\n", offsetof({name}, {f}));')
+    lines.append("return 0; }")
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "sz"
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    subprocess.check_call(["gcc", "-I", inc, str(src), "-o", str(exe)])
+    got = dict(line.split() for line in subprocess.check_output([str(exe)]).decode().splitlines())
+    for name, cls in structs.items():
+        assert int(got[name]) == ctypes.sizeof(cls), name
+        for f, _ in cls._fields_:
+            assert int(got[f"{name}.{f}"]) == getattr(cls, f).offset, f"{name}.{f}"
 
 
 def test_strerror():

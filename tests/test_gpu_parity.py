@@ -123,13 +123,142 @@ def test_missing_key_reports_error():
     assert c.tolist() == [1] and st.committed == 1
 
 
-def test_dup_row_rejected_for_2pl():
-    eng = CCEngine(dvcc.NO_WAIT, 4, 16)
-    eng.load_ycsb_partition(16)
-    e = Epoch(np.array([3, 3], np.uint64), np.array([0, 1], np.uint8), np.array([0, 2], np.uint32))
+def _epoch_of(txns):
+    keys = np.array([k for t in txns for k, _ in t], np.uint64)
+    types = np.array([ty for t in txns for _, ty in t], np.uint8)
+    tb = np.array([0] + list(np.cumsum([len(t) for t in txns])), np.uint32)
+    return Epoch(keys, types, tb)
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_repeated_rows_hand(cc):
+    """A txn touching one row several times: NO_WAIT /
+    WAIT_DIE abort it unless every access to the row reads (its own lock
+    conflicts, row_lock.cpp:69, 86-90); OCC puts the row in its write set if
+    any access writes it; CALVIN locks it once (txn.cpp:778-788)."""
+    txns = [[(1, 0), (1, 0)], [(2, 0), (2, 1)], [(3, 1), (3, 0)], [(2, 0)], [(3, 0), (4, 1), (3, 0)]]
+    _check(cc, 8, [_epoch_of(txns)])
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("rows,R,theta", [(64, 6, 0.5), (1 << 12, 10, 0.9), (1 << 14, 16, 0.99)])
+def test_repeated_rows_random(cc, rows, R, theta):
+    """Keys drawn with replacement inside a txn (the YCSB generator never
+    repeats one), over several epochs and all decision-path knobs."""
+    rng = np.random.default_rng(rows + R)
+    epochs = []
+    for k in range(2):
+        n_txn = 3000
+        lens = rng.integers(1, R + 1, size=n_txn)
+        tb = np.zeros(n_txn + 1, np.uint32)
+        tb[1:] = np.cumsum(lens)
+        n = int(tb[-1])
+        hot = max(4, rows // 64)
+        keys = np.where(rng.random(n) < theta, rng.integers(0, hot, size=n), rng.integers(0, rows, size=n))
+        # force a repeat in about a third of the txns
+        for t in range(0, n_txn, 3):
+            a, b = int(tb[t]), int(tb[t + 1])
+            if b - a >= 2:
+                keys[b - 1] = keys[a]
+        types = (rng.random(n) < 0.5).astype(np.uint8)
+        epochs.append(Epoch(keys.astype(np.uint64), types, tb))
+    for knobs in (dict(), dict(asynchronous=False), dict(tail=False, asynchronous=False), dict(el64=True)):
+        _check(cc, rows, epochs, **knobs)
+
+
+def test_txn_longer_than_declared_bound_is_rejected():
+    """max_txn_acc under-declared (ERRB_BIG): the epoch fails with DV_ERR_ARG
+    before anything executes, and the context stays usable."""
+    rows = 64
+    e = _epoch_of([[(k, 1) for k in range(20)], [(30, 1)]])
+    for cc in (dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC):  # CALVIN: any length <= 128
+        eng = CCEngine(cc, 4, 64)
+        eng.load_ycsb_partition(rows)
+        before = eng.read_table(0, rows)
+        dep = DeviceEpoch(e)
+        dep.max_txn_acc = 16  # the first txn has 20 accesses
+        with pytest.raises(dvcc.DvccError) as ex:
+            eng.run_epoch_device(dep, torch.zeros(4, dtype=torch.uint8, device="cuda"))
+        assert ex.value.code == dvcc._lib.DV_ERR_ARG
+        assert (eng.read_table(0, rows) == before).all(), "a rejected epoch changed the table"
+        c, _, st = eng.run_epoch(e)
+        assert st.committed == 2
+        eng.close()
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_rejected_epoch_leaves_table_unchanged(cc):
+    """A missing key (and, from host buffers, a record outside its txn's range)
+    rejects the whole epoch before execution: no row changes, for every CC
+    (CALVIN has no rounds in between, so the gate is on the execution)."""
+    rows = 64
+    eng = CCEngine(cc, 8, 64)
+    eng.load_ycsb_partition(rows)
+    before = eng.read_table(0, rows)
+    bad = _epoch_of([[(1, 1), (2, 1)], [(3, 1), (1000, 1)], [(5, 1)]])
     with pytest.raises(dvcc.DvccError) as ex:
-        eng.run_epoch(e)
-    assert ex.value.code == dvcc._lib.DV_ERR_DUP_ROW
+        eng.run_epoch(bad)
+    assert ex.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    assert (eng.read_table(0, rows) == before).all()
+    good = _epoch_of([[(1, 1), (2, 1)], [(3, 1), (4, 1)], [(5, 1)]])
+    acc = good.to_access_array()
+    acc["txn_seq"][2] = 0  # the first access of txn 1 claims txn 0
+    commit = np.zeros(3, np.uint8)
+    with pytest.raises(dvcc.DvccError) as ex:
+        eng.run_epoch_host(acc, np.ascontiguousarray(good.txn_begin), good.n_acc, good.n_txn, commit)
+    assert ex.value.code == dvcc._lib.DV_ERR_TXN_RANGE
+    assert (eng.read_table(0, rows) == before).all()
+    c, _, st = eng.run_epoch(good)
+    assert st.committed == 3 and st.write_cnt == 5
+    eng.close()
+
+
+def test_wait_die_timestamps_must_rise_in_sequence_order():
+    """dv_epoch_run's ts: WAIT_DIE decisions equal sequence order only when ts
+    rises with it (otherwise the reference waits, row_lock.cpp:119-147)."""
+    import ctypes
+    e = _epoch_of([[(1, 1)], [(1, 0)], [(2, 1)]])
+    eng = CCEngine(dvcc.WAIT_DIE, 4, 16)
+    eng.load_ycsb_partition(8)
+    acc = e.to_access_array()
+    tb = np.ascontiguousarray(e.txn_begin)
+    commit = np.zeros(3, np.uint8)
+    st = dvcc._lib.Stats()
+    L = dvcc._lib.lib()
+    for ts, ok in (([5, 9, 12], True), ([5, 5, 12], False), ([9, 5, 12], False)):
+        t = np.array(ts, np.uint64)
+        rc = L.dv_epoch_run(eng._ctx, acc.ctypes.data, e.n_acc, tb.ctypes.data, 3, t.ctypes.data,
+                            commit.ctypes.data, None, ctypes.byref(st))
+        assert (rc == 0) == ok, (ts, rc)
+        if ok:
+            assert commit.tolist() == [1, 0, 1]
+    eng.close()
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+@pytest.mark.parametrize("max_iters", [1, 3])
+def test_async_rounds_yield_and_resume(cc, max_iters):
+    """Forward progress of the asynchronous rounds: workgroups forced to yield
+    after max_iters iterations; the host resumes the synchronous rounds from
+    the launch's input state and decisions stay bit-exact."""
+    rows = 1 << 20
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    epochs = [g.gen(1 << 16, 95), g.gen(1 << 16, 94)]
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, 1 << 16, max(e.n_acc for e in epochs))
+    eng.load_ycsb_partition(rows)
+    eng.set_async_limits(max_iters, 0)
+    yields = 0
+    for e in epochs:
+        c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+        c, _, st = _gpu_epoch(eng, e, "device")
+        assert (c == c_ref).all()
+        assert st.read_digest == st_ref.read_digest and st.write_cnt == st_ref.write_cnt
+        assert (eng.read_table(0, rows) == f0).all()
+        yields += st.async_yields
+    assert yields > 0, "no asynchronous launch yielded"
+    eng.close()
 
 
 def test_calvin_repeat_access_keeps_first_lock_type():

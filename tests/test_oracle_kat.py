@@ -267,6 +267,48 @@ def test_no_wait_greedy_predicate():
             surv.append(i)
 
 
+# A txn touching one row twice.  Hand-derived from the text:
+# 2PL re-locks through get_row (txn.cpp:790-803); conflict_lock(SH, SH) is
+# free, anything with EX conflicts with the txn's own lock (row_lock.cpp:69):
+# NO_WAIT aborts (86-90), WAIT_DIE dies (the reference asserts at 106).  OCC
+# never validates a txn against itself (occ.cpp:185-199): the row is in its
+# write set if any access writes it.
+REP = [[(A, R_), (A, R_)],          # T0: shared twice -> commits
+       [(B, R_), (B, W_)],          # T1: SH then EX on its own row
+       [(C, W_), (C, R_)],          # T2: EX then SH
+       [(B, R_)],                   # T3: reads b
+       [(C, R_), (4, W_), (C, R_)]]  # T4: c twice (shared), writes d
+
+
+def test_repeated_rows_2pl():
+    for cc in (O.NO_WAIT, O.WAIT_DIE):
+        c, _, st, f0 = _run(cc, REP)
+        # T1 and T2 abort on themselves; T3 then finds b free; T4 too
+        assert c.tolist() == [1, 0, 0, 1, 1], cc
+        assert st.write_cnt == 1 and f0[4] == 0 and f0[B] != 0 and f0[C] != 0
+
+
+def test_repeated_rows_occ():
+    for lit in (False, True):
+        c, _, st, f0 = _run(O.OCC, REP, literal=lit)
+        # T1 and T2 commit (b, c in their write sets); T3 reads b -> aborts;
+        # T4 reads c -> aborts
+        assert c.tolist() == [1, 1, 1, 0, 0], lit
+        assert st.write_cnt == 2 and f0[B] == 0 and f0[C] == 0
+
+
+def test_repeated_rows_occ_reads_see_the_epoch_image():
+    # OCC reads in the access phase (row_occ.cpp:38-46): T0's read of a after its
+    # own write of a still sees the initial value
+    keys, types, tb = _epoch([[(A, W_), (A, R_)]])
+    tab = O.YcsbTable(8)
+    f0 = tab.f0.copy()
+    init = int(f0[A])
+    _, _, st = O.epoch_run(O.OCC, tab.ix, f0, 1, tb, keys, types)
+    mix = O.lib().or_mix64
+    assert st.read_digest == mix(init ^ mix((0 << 32) ^ A)) and f0[A] == 0
+
+
 def test_missing_key_is_an_error():
     keys, types, tb = _epoch([[(100, R_)]])
     tab = O.YcsbTable(8)

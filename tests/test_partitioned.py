@@ -33,11 +33,14 @@ class NumpyPartition:
 
     needs_votes = True
 
-    def __init__(self, cc):
+    def __init__(self, cc, nkeys=None):
         self.nowait = cc != dvcc.OCC
+        self.nkeys = nkeys  # keys >= nkeys are missing from the index
 
     def begin_partition(self, keys, types_, txn, n_txn, max_txn_acc=0):
         k = keys.numpy().view(np.uint64)
+        self.err = int(self.nkeys is not None and bool((k >= self.nkeys).any()))  # ERRB_KEY
+        self.peer = 0
         order = np.argsort(k, kind="stable")
         self.k, self.w, self.t = k[order], types_.numpy()[order] == 1, txn.numpy()[order].astype(np.int64)
         head = np.ones(len(self.k), bool)
@@ -73,6 +76,12 @@ class NumpyPartition:
         out[:len(self.ulist)] = v[self.ulist]
         verdict.copy_(torch.from_numpy(out))
 
+    def errors_local(self, word):
+        word.fill_(self.err)
+
+    def errors_combined(self, word):
+        self.peer = int(word.item())
+
     def round_apply(self, verdict, wait=True):
         v = verdict.numpy()[:len(self.ulist)]
         lst = self.ulist
@@ -83,6 +92,8 @@ class NumpyPartition:
         return self.log[-1] if wait else None
 
     def round_wait(self, r):
+        if self.err | self.peer:  # the engine reports the rejected epoch at the first round it reads
+            raise dvcc.DvccError(dvcc._lib.DV_ERR_KEY_NOT_FOUND, "dv_epoch_round_wait")
         return self.log[r]
 
     def finish(self, commit=None):
@@ -288,6 +299,167 @@ def test_rccl_engine_driver_single_rank(cc):
                                                                st_ref.write_cnt)
     eng.close()
     ref.close()
+
+
+def _gloo_error_worker(rank, world, port, cc, n_txn, rows_pp, bad_rank, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, batches = _global_setup(world, n_txn, rows_pp, 0.5)
+        b = batches[rank]
+        if rank == bad_rank:  # a key no partition holds (IndexHash::index_read miss)
+            b.keys = b.keys.copy()
+            b.keys[7] = np.uint64(rows_pp * world * 4 + 1)
+        pe = PartitionedEpoch(b, rank, world, n_txn, "cpu")
+        runner = PartitionedRunner(NumpyPartition(cc, nkeys=rows_pp * world), world, rank, device="cpu")
+        try:
+            runner.run(pe, commit=torch.zeros(n_txn * world, dtype=torch.uint8))
+            q.put((rank, "ok"))
+        except dvcc.DvccError as ex:
+            q.put((rank, ex.code))
+        # the group still works: every rank left the round loop together
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        q.put((rank, int(t.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cc,bad_rank", [(dvcc.NO_WAIT, 1), (dvcc.OCC, 0)])
+def test_runner_error_is_collective_gloo_world2(cc, bad_rank):
+    """A missing key on one rank: every rank raises the same error from the
+    same round, and the process group is still in step afterwards (no rank
+    left behind in a collective)."""
+    world, n_txn, rows_pp = 2, 300, 1 << 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_error_worker, args=(r, world, port, cc, n_txn, rows_pp, bad_rank, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(2 * world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    codes = sorted(v for _, v in res)
+    assert codes == sorted([dvcc._lib.DV_ERR_KEY_NOT_FOUND] * world + [world] * world), res
+
+
+# ---- the engine's own partitioned driver (dv_epoch_run_part) with P ranks in
+# one process: P contexts on one GPU, one host thread each, the in-process
+# transport in place of RCCL (dv_comm_init_local) -- the same C++ protocol
+# the bench runs over RCCL with one process per GPU.
+def _run_group(engines, homes, n_txn):
+    """run_epoch_part on every engine concurrently; (commit bytes, stats) or
+    the exception, per rank."""
+    import threading
+    world = len(engines)
+    out = [None] * world
+
+    def body(r):
+        try:
+            d = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+            st = engines[r].run_epoch_part(homes[r], n_txn, d)
+            out[r] = (d.cpu().numpy(), st)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a rank hung in the partitioned epoch"
+    return out
+
+
+def _engine_group(cc, world, rows_pp, n_txn, R=10):
+    engines = []
+    for p in range(world):
+        eng = dvcc.CCEngine(cc, n_txn * world, max(64, int(n_txn * world * R * 1.2 / world) + 4096),
+                            part_cnt=world, part_id=p)
+        eng.load_ycsb_partition(rows_pp)
+        engines.append(eng)
+    dvcc.CCEngine.comm_init_local(engines)
+    return engines
+
+
+def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9):
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
+    engines = _engine_group(cc, world, rows_pp, n_txn)
+    tab = O.YcsbTable(rows_pp * world)  # one-partition view: row == key
+    f0 = tab.f0.copy()
+    for k in range(epochs):
+        batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 20 + k), r) for r in range(world)]
+        e = dvcc.sequence(batches)
+        c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, e.n_txn, e.txn_begin, e.keys,
+                                       e.types)
+        res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], n_txn)
+        digest = writes = 0
+        for r, x in enumerate(res):
+            assert not isinstance(x, Exception), f"rank {r}: {x}"
+            c, st = x
+            assert (c == c_ref).all(), f"rank {r}: {(c != c_ref).sum()} mismatches"
+            assert st.committed == st_ref.committed
+            digest = (digest + st.read_digest) % (1 << 64)
+            writes += st.write_cnt
+        assert digest == st_ref.read_digest and writes == st_ref.write_cnt
+        for p, eng in enumerate(engines):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+    for eng in engines:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+@pytest.mark.parametrize("mpr", [0.1, 0.5])
+def test_engine_driver_8_partitions(cc, mpr):
+    """SURVEY config D's protocol at 8 partitions: owner split, all-to-all of
+    the records, list-ordered verdict MAX per round, execution per partition
+    -- decisions, digests and every partition's rows equal the one-partition
+    oracle E-schedule over the sequenced global epoch."""
+    _check_group(cc, 8, 1 << 14, 4000, mpr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_engine_driver_other_widths(world):
+    _check_group(dvcc.NO_WAIT, world, 1 << 13, 3000, 0.3, theta=0.99)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("cc,mpr", [(dvcc.NO_WAIT, 0.1), (dvcc.OCC, 0.5)])
+def test_config_d_8_partitions_full(cc, mpr):
+    """Config D as written: 16,777,216 rows per partition, a 1,048,576-txn
+    epoch in total (131,072 per rank), zipf 0.9, 8 partitions."""
+    _check_group(cc, 8, 16_777_216, 131_072, mpr, epochs=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.CALVIN])
+def test_engine_driver_error_is_collective(cc):
+    """A missing key on one rank: every rank returns DV_ERR_KEY_NOT_FOUND
+    (none hangs in a collective), no table changes, and the group runs the
+    next epoch normally."""
+    world, rows_pp, n_txn = 4, 1 << 12, 1000
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(cc, world, rows_pp, n_txn)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 5), r) for r in range(world)]
+    bad = [dvcc.Epoch(b.keys.copy(), b.types, b.txn_begin) for b in batches]
+    bad[2].keys[11] = np.uint64(rows_pp * world * 3 + 2)
+    res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in bad], n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, x)
+    for eng, b in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b).all()
+    res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], n_txn)
+    assert all(not isinstance(x, Exception) for x in res), res
+    for eng in engines:
+        eng.close()
 
 
 class NumpyTpccPartition(NumpyPartition):
