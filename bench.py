@@ -1,17 +1,24 @@
 """Benchmark: committed txns/sec of the batched CC engine on YCSB (BASELINE.json).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--cc NO_WAIT|WAIT_DIE|OCC|CALVIN]
-                    [--config D|C|B] [--mpr 0.1]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+                    [--config D|C|B] [--mpr 0.1] [--mpr-sweep 0,0.1,0.2,0.3,0.4,0.5]
 
 A step is one epoch through the hot path (probe -> sort -> decide -> execute)
-with its accesses already resident in HBM.  Default workload (config D of
-SURVEY.md 8d, the headline "YCSB zipf 0.9 at 1/2/4/8 GPUs"): 16,777,216 rows
-and 1,048,576 txns per GPU per epoch, 10 requests/txn, zipf 0.9, 50 % of the
-accesses writes (TXN_WRITE_PERC 1.0, TUP_WRITE_PERC 0.5), NO_WAIT.  With N>1,
-rank r owns partition r and multi-partition txns (MPR gate, 2 partitions)
-exchange fragments by all-to-all and votes by all-reduce (RCCL over xGMI).
-Weak scaling: rows and txns per GPU are fixed.  Rank 0 prints one JSON line.
+with its accesses already resident in HBM.  Default workload: config D of
+SURVEY.md 8(d), the headline "YCSB zipf 0.9 at 1/2/4/8 GPUs" -- 16,777,216
+rows per partition, an epoch of 1,048,576 txns IN TOTAL (1,048,576 / N per
+GPU), 10 requests/txn, zipf 0.9, 50 % of the accesses writes (TXN_WRITE_PERC
+1.0, TUP_WRITE_PERC 0.5), NO_WAIT.
+
+--gpus N > 1 starts its own N rank processes (torch.distributed.run) when no
+launcher did; one process per GPU, rank r owns partition r, and every epoch
+runs through the engine's own RCCL driver (dv_comm_init + dv_epoch_run_part:
+one all-to-allv of 16-byte access records, then decision rounds closed by
+all-reduce(MAX) of the undecided txns' verdict bytes, all on the engine's
+stream).  Multi-partition txns follow the MPR gate (2 partitions).  Beside
+the headline (strong scaling: the epoch is fixed) the line carries the
+weak-scaling run (1,048,576 txns per GPU) and the MPR sweep of config D.
+Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -28,7 +35,6 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 import dvcc  # noqa: E402
-from dvcc.partitioned import EnginePartition, PartitionedEpoch, PartitionedRunner  # noqa: E402
 
 METRIC = "committed txns/sec (node) YCSB zipf0.9 at 1/2/4/8 GPUs; abort-set bit-exact"
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -38,11 +44,12 @@ TIMING = {"full": True, "kernel": "kernel", "off": False}
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_round_pass.json")  # tools/pmc_summary.py
 
 CONFIGS = {
-    # name: rows per partition, txns per GPU-epoch, zipf theta, description
-    "D": (16_777_216, 1_048_576, 0.9, "YCSB config D: 16,777,216 rows/partition, 1,048,576-txn epoch/GPU"),
+    # name: rows per partition, txns per epoch (in total, over all GPUs), zipf theta, description
+    "D": (16_777_216, 1_048_576, 0.9, "YCSB config D: 16,777,216 rows/partition, 1,048,576-txn epoch in total"),
     "C": (100_000_000, 1_048_576, 0.9, "YCSB config C: 100,000,000 rows, 1,048,576-txn epoch"),
     "B": (16_777_216, 65_536, 0.6, "YCSB config B: 16,777,216 rows, 65,536-txn epoch"),
 }
+CPU_SHARE = 16  # host threads the GPU box gives one GPU's job (nproc shows the whole machine)
 
 
 def parse():
@@ -52,7 +59,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cc", default="NO_WAIT")
     ap.add_argument("--config", default="D")
-    ap.add_argument("--mpr", type=float, default=0.1)
+    ap.add_argument("--mpr", type=float, default=0.1, help="N>1: multi-partition txn ratio of the headline")
+    ap.add_argument("--mpr-sweep", default="0,0.1,0.2,0.3,0.4,0.5",
+                    help="N>1: config D's MPR values, each a short extra run ('' = none)")
+    ap.add_argument("--no-weak", action="store_true", help="N>1: skip the 1,048,576-txn-per-GPU run")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -102,12 +112,14 @@ def cpu_baseline(epochs, rows, cc_name, seconds):
 def cpu_baseline_mt(epochs, rows, seconds):
     """a Deneva-style multi-threaded NO_WAIT engine
     (oracle/mt_engine.c: per-row lock words, index probe, run_ycsb_1, no
-    retry) on the host cores the box gives this job (at most 16), same
+    retry) on every host core the box gives this job -- its CPU share for
+    one GPU, CPU_SHARE threads; nproc reports the whole machine -- same
     epochs.  Its aborts depend on the interleaving (THREAD_CNT txns in
     flight), not the E-schedule's 1M; a throughput reference only."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
-    threads = max(1, min(16, os.cpu_count() or 1))
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = max(1, min(CPU_SHARE, avail))
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     lock = np.zeros(rows, np.uint32)
@@ -124,8 +136,10 @@ def cpu_baseline_mt(epochs, rows, seconds):
         if el >= seconds:
             break
     return {"value": committed / el, "unit": "committed txns/s", "cores": threads, "kind": "port",
+            "nproc": os.cpu_count(), "affinity": avail,
             "sample": f"Deneva-style multi-threaded NO_WAIT engine (per-row lock words, {threads} "
-                      f"threads) over {i} epoch(s) of {epochs[0].n_txn} txns of the bench workload, "
+                      f"threads = the box's CPU share for one GPU; nproc {os.cpu_count()}, affinity {avail}) "
+                      f"over {i} epoch(s) of {epochs[0].n_txn} txns of the bench workload, "
                       f"{txns} txns in {el:.1f} s, abort rate {1 - committed / max(1, txns):.3f}; "
                       "restatement of the reference CC, not the reference binary"}
 
@@ -252,61 +266,31 @@ def e2e_host_leg(eng, epochs, k):
             "note": "dv_epoch_run: H2D of the access records + the same device path"}
 
 
-def main():
-    a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        a.gpus = world if world > 1 else a.gpus
-    if a.gpus > 1 and world == 1:
-        raise SystemExit("--gpus N>1 must be launched with torch.distributed.run")
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    if a.tpcc_only:
-        print(json.dumps({"tpcc": tpcc_leg(a)}), flush=True)
-        return
-    cc_name = a.cc.upper()
-    rows, n_txn, theta, desc = CONFIGS[a.config]
-    R = 10
-    mpr = a.mpr if world > 1 else -1.0  # N=1: the reference zipf generator, unmodified
-    gen = dvcc.YCSBQueryGenerator(rows * world, part_cnt=world, req_per_query=R, zipf_theta=theta,
-                                  txn_write_perc=1.0, tup_write_perc=0.5,
-                                  part_per_txn=min(2, world), strict_ppt=1, mpr=mpr)
-    n_epochs = max(1, min(a.epochs, a.steps + a.warmup))
-    t_gen = time.perf_counter()
-    epochs = gen_epochs(gen, n_txn, rank, n_epochs)
-    t_gen = time.perf_counter() - t_gen
+def launch_ranks(a):
+    """--gpus N > 1 without a launcher: run this script as N rank processes
+    under torch.distributed.run (one per GPU) as a child, and return its exit
+    status.  Nothing in this process has touched the GPU."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
 
-    if world == 1:
-        eng = dvcc.CCEngine(cc_name, n_txn, n_txn * R, device=local_rank, timing=TIMING[a.timing])
-        eng.load_ycsb_partition(rows)
-        deps = [dvcc.DeviceEpoch(e) for e in epochs]
-        d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
 
-        def step(i):
-            return eng.run_epoch_device(deps[i % n_epochs], d_commit)
-    else:
-        max_acc = int(n_txn * R * 1.5) + 4096
-        eng = dvcc.CCEngine(cc_name, n_txn * world, max_acc, device=local_rank, part_cnt=world,
-                            part_id=rank, timing=TIMING[a.timing])
-        eng.load_ycsb_partition(rows)
-        runner = PartitionedRunner(EnginePartition(eng), world, rank)
-        pes = [PartitionedEpoch(e, rank, world, n_txn, "cuda") for e in epochs]
-        d_commit = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
-
-        def step(i):
-            st, _ = runner.run(pes[i % n_epochs], commit=d_commit)
-            return st
-
-    for i in range(a.warmup):
-        step(i)
+def timed(step, first, warmup, steps, world):
+    """W untimed steps, then exactly K steps between barrier + synchronize
+    on both sides; the slowest rank's time."""
+    for i in range(warmup):
+        step(first + i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step(a.warmup + i) for i in range(a.steps)]
+    stats = [step(first + warmup + i) for i in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -315,14 +299,52 @@ def main():
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    return stats, el
 
-    # Measurement legs after the timed region, on the same epochs and stream:
-    # event timing adds launch latency (dispatch timestamps ~6 us per timed
-    # launch, stage markers more), so the timed region runs without it unless
-    # --timing asks.  Roofline: the pass / scatter launches' own dispatch
-    # timestamps over as many epochs as the timed region; stages: a few
-    # epochs with per-stage events.
-    nxt = a.warmup + a.steps
+
+def pmc_traffic(a, cc_name, world):
+    """HBM bytes per k_round_pass launch from the committed PMC summary, only
+    if it was measured on these sources, this config and GPU count."""
+    if not os.path.exists(PMC_SUMMARY):
+        return None, "no PMC summary"
+    pmc = json.load(open(PMC_SUMMARY))
+    want = {"config": a.config, "cc": cc_name, "n_gpus": world, "src_hash": dvcc._lib.source_hash()}
+    stale = {k: (pmc.get(k), v) for k, v in want.items() if pmc.get(k) != v}
+    if stale:
+        return None, f"PMC summary does not match this run: {stale}"
+    return pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
+
+
+def roofline(kstats, a, cc_name, world):
+    """The dominant kernel, k_round_pass: algorithmic bytes per launch (9 B per
+    live access) / its average duration from the launches' own
+    dispatch timestamps on the engine's stream."""
+    launches = sum(s.pass_launches for s in kstats)
+    pass_ms = sum(s.ms_pass for s in kstats)
+    pass_live = sum(s.pass_live for s in kstats)
+    avg_ms = pass_ms / max(1, launches)
+    bytes_per_launch = SCAN_BYTES * pass_live / max(1, launches)
+    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+    traffic, src = pmc_traffic(a, cc_name, world)
+    return {
+        "kernel": "k_round_pass", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
+        "avg_launch_ms": avg_ms, "launches": launches,
+        "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d scan read "
+                             "8 B + flag 1 B) x live accesses the launch reads",
+        "traffic_source": src,
+        "timed_by": ("dispatch timestamps of every pass launch in the timed region"
+                     if a.timing != "off" else
+                     f"dispatch timestamps of every pass launch over {len(kstats)} epochs run "
+                     "right after the timed region (same epochs, same stream)"),
+    }
+
+
+def measure_legs(a, eng, step, nxt, stats):
+    """Event-timed legs after the timed region, on the same epochs and stream:
+    event timing adds launch latency (dispatch timestamps ~6 us per timed
+    launch, stage markers more), so the timed region runs without it unless
+    --timing asks.  Returns (kernel-timed stats, stage-timed stats)."""
     if a.timing == "off":
         eng.set_timing("kernel")
         kstats = [step(nxt + i) for i in range(a.steps)]
@@ -335,88 +357,177 @@ def main():
     else:
         sstats = stats
     eng.set_timing(False)
+    return kstats, sstats
 
-    # commits are global (every rank holds the same decision vector): count once
+
+def stage_summary(stats, sstats, kstats, el, R):
     committed = sum(s.committed for s in stats)
     txns = sum(s.n_txn for s in stats)
     acc_local = sum(s.n_acc for s in stats)
-    value = committed / el
-    # dominant kernel: the decision-round pass (k_round_pass), timed by its
-    # launches' own dispatch timestamps (HIP events) on the engine's stream
-    launches = sum(s.pass_launches for s in kstats)
-    pass_ms = sum(s.ms_pass for s in kstats)
-    pass_live = sum(s.pass_live for s in kstats)
-    avg_ms = pass_ms / max(1, launches)
-    bytes_per_launch = SCAN_BYTES * pass_live / max(1, launches)
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic = None
-    if os.path.exists(PMC_SUMMARY):
-        pmc = json.load(open(PMC_SUMMARY))
-        if pmc.get("config") == a.config and pmc.get("cc") == cc_name and pmc.get("n_gpus") == world:
-            traffic = pmc["hbm_bytes_per_launch"]
     sc_ms = [s.ms_scatter / max(1, s.scatter_launches) for s in kstats if s.scatter_launches]
     sc_avg = float(np.mean(sc_ms)) if sc_ms else 0.0
     n_acc_step = acc_local / max(1, len(stats))
     scatter_gbps = n_acc_step * 16 / (sc_avg * 1e-3) / 1e9 if sc_avg > 0 else 0.0
     epoch_gbps = (txns / el) * (BYTES_PER_ACCESS * R + 1) / 1e9
+    stage = {k: float(np.mean([getattr(s, k) for s in sstats]))
+             for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")}
+    # SURVEY.md 8(d) counts every stage once: the scan stage's 9 B per access
+    # over the whole decide stage (rounds are overhead, not algorithmic)
+    dec = stage["ms_decide"]
+    scan_stage_gbps = n_acc_step * SCAN_BYTES / (dec * 1e-3) / 1e9 if dec > 0 else 0.0
+    return {
+        "sort": {"kernel": "k_radix_scatter", "avg_launch_ms": sc_avg, "achieved_GBps": scatter_gbps,
+                 "keys_per_s": n_acc_step / (sc_avg * 1e-3) if sc_avg > 0 else 0.0},
+        "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1, "achieved_GBps": epoch_gbps,
+                           "frac": epoch_gbps / HBM_PEAK_GBPS},
+        "decide_stage_roofline": {"bytes": f"{SCAN_BYTES} B per access of this partition, counted once "
+                                           "(SURVEY.md 8d: rounds are overhead)",
+                                  "achieved_GBps": scan_stage_gbps, "frac": scan_stage_gbps / HBM_PEAK_GBPS},
+        "abort_rate": 1.0 - committed / max(1, txns),
+        "decided_txns_per_s": txns / el,
+        "rounds_mean": float(np.mean([s.rounds for s in stats])),
+        "async_tries": {"launches": int(sum(s.async_launches for s in stats)),
+                        "declined": int(sum(s.async_declined for s in stats)),
+                        "yields": int(sum(s.async_yields for s in stats)), "epochs": len(stats)},
+        "stage_ms_mean": stage,
+    }
+
+
+class PartitionedBench:
+    """One rank of a partitioned run: the engine bound to partition `rank`,
+    its RCCL communicator (dv_comm_init) and device-resident home batches."""
+
+    def __init__(self, a, cc_name, rows, world, rank, local_rank, max_txn_rank, R):
+        self.a, self.world, self.rank, self.R = a, world, rank, R
+        # received accesses: this rank's share of every origin's batch (keys
+        # spread evenly by key % PART_CNT; multi-partition txns add ~MPR / 2)
+        cap = int(max_txn_rank * R * 1.4) + 65536
+        self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
+                                 part_id=rank, timing=TIMING[a.timing])
+        self.eng.load_ycsb_partition(rows)
+        uid = [dvcc.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        self.eng.comm_init(uid[0], world, rank)
+        self.rows = rows
+        self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
+
+    def epochs(self, n_txn_rank, mpr, theta, count):
+        gen = dvcc.YCSBQueryGenerator(self.rows * self.world, part_cnt=self.world, req_per_query=self.R,
+                                      zipf_theta=theta, txn_write_perc=1.0, tup_write_perc=0.5,
+                                      part_per_txn=2, strict_ppt=1, mpr=mpr)
+        host = gen_epochs(gen, n_txn_rank, self.rank, count)
+        return [dvcc.DeviceEpoch(e) for e in host]
+
+    def stepper(self, deps, n_txn_rank):
+        def step(i):
+            return self.eng.run_epoch_part(deps[i % len(deps)], n_txn_rank, self.d_commit)
+        return step
+
+
+def main():
+    a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(a))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    a.gpus = world
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    if a.tpcc_only:
+        print(json.dumps({"tpcc": tpcc_leg(a)}), flush=True)
+        return
+    cc_name = a.cc.upper()
+    rows, n_txn_total, theta, desc = CONFIGS[a.config]
+    R = 10
+    n_txn_rank = n_txn_total // world
+    mpr = a.mpr if world > 1 else -1.0  # N=1: the reference zipf generator, unmodified
+    n_epochs = max(1, min(a.epochs, a.steps + a.warmup))
+    t_gen = time.perf_counter()
+    extra = {}
+    if world == 1:
+        gen = dvcc.YCSBQueryGenerator(rows, part_cnt=1, req_per_query=R, zipf_theta=theta,
+                                      txn_write_perc=1.0, tup_write_perc=0.5, part_per_txn=1, strict_ppt=1,
+                                      mpr=mpr)
+        epochs = gen_epochs(gen, n_txn_total, 0, n_epochs)
+        t_gen = time.perf_counter() - t_gen
+        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
+        eng.load_ycsb_partition(rows)
+        deps = [dvcc.DeviceEpoch(e) for e in epochs]
+        d_commit = torch.zeros(n_txn_total, dtype=torch.uint8, device="cuda")
+
+        def step(i):
+            return eng.run_epoch_device(deps[i % n_epochs], d_commit)
+    else:
+        weak = not a.no_weak
+        pb = PartitionedBench(a, cc_name, rows, world, rank, local_rank,
+                              n_txn_total if weak else n_txn_rank, R)
+        eng = pb.eng
+        deps = pb.epochs(n_txn_rank, mpr, theta, n_epochs)
+        t_gen = time.perf_counter() - t_gen
+        step = pb.stepper(deps, n_txn_rank)
+
+    stats, el = timed(step, 0, a.warmup, a.steps, world)
+    kstats, sstats = measure_legs(a, eng, step, a.warmup + a.steps, stats)
+    committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     out = {
         "metric": METRIC,
-        "value": value,
+        "value": committed / el,
         "unit": "committed txns/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": el / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic: Deneva YCSB zipf generator (myrand LCG, seeded SEED+97*part+epoch)",
         "config": {
             "workload": desc, "cc_alg": cc_name, "rows_per_partition": rows,
-            "txns_per_epoch_per_gpu": n_txn, "req_per_query": R, "zipf_theta": theta,
-            "txn_write_perc": 1.0, "tup_write_perc": 0.5, "mpr": mpr if world > 1 else 0.0,
-            "part_per_txn": min(2, world), "parallelism": f"partitioned x{world} (PART_CNT={world})",
+            "txns_per_epoch": n_txn_total, "txns_per_epoch_per_gpu": n_txn_rank, "req_per_query": R,
+            "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
+            "mpr": mpr if world > 1 else 0.0, "part_per_txn": min(2, world),
+            "parallelism": f"partitioned x{world} (PART_CNT={world}, RCCL)" if world > 1 else "1 GPU",
             "distinct_epochs": n_epochs,
         },
-        "roofline": {
-            "kernel": "k_round_pass",
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBPS,
-            "traffic": traffic,
-            "bytes_per_launch": bytes_per_launch,
-            "avg_launch_ms": avg_ms,
-            "launches": launches,
-            "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d scan read "
-                                 "8 B + flag 1 B) x live accesses the launch reads",
-            "traffic_source": os.path.relpath(PMC_SUMMARY, ROOT) if traffic is not None else None,
-            "timed_by": ("dispatch timestamps of every pass launch in the timed region"
-                         if a.timing != "off" else
-                         f"dispatch timestamps of every pass launch over {a.steps} epochs run "
-                         "right after the timed region (same epochs, same stream)"),
-        },
-        "sort": {"kernel": "k_radix_scatter", "avg_launch_ms": sc_avg, "achieved_GBps": scatter_gbps,
-                 "keys_per_s": n_acc_step / (sc_avg * 1e-3) if sc_avg > 0 else 0.0},
-        "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1, "achieved_GBps": epoch_gbps,
-                           "frac": epoch_gbps / HBM_PEAK_GBPS},
-        "abort_rate": 1.0 - committed / max(1, txns),
-        "decided_txns_per_s": txns / el,
-        "rounds_mean": float(np.mean([s.rounds for s in stats])),
-        "async_tries": {"launches": int(sum(s.async_launches for s in stats)),
-                        "declined": int(sum(s.async_declined for s in stats)), "epochs": len(stats)},
-        "stage_ms_mean": {k: float(np.mean([getattr(s, k) for s in sstats]))
-                          for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")},
+        "roofline": roofline(kstats, a, cc_name, world),
         "timing_in_timed_region": a.timing,
         "gen_seconds": t_gen,
+        "src_hash": dvcc._lib.source_hash(),
     }
+    out.update(stage_summary(stats, sstats, kstats, el, R))
     if world == 1:
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
-        out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn, min(a.steps, 10), d_commit)
+        out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, min(a.steps, 10), d_commit)
+    else:
+        nxt = 10_000
+        if not a.no_weak:
+            # weak scaling: 1,048,576 txns per GPU per epoch
+            wdeps = pb.epochs(n_txn_total, mpr, theta, 2)
+            wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, 1, min(a.steps, 5), world)
+            wc = sum(s.committed for s in wst)
+            out["weak_scaling"] = {"txns_per_epoch_per_gpu": n_txn_total, "txns_per_epoch": n_txn_total * world,
+                                   "committed_per_s": wc / wel, "decided_txns_per_s": len(wst) * n_txn_total * world / wel,
+                                   "ms_per_epoch": wel / len(wst) * 1e3,
+                                   "abort_rate": 1 - wc / (len(wst) * n_txn_total * world), "epochs": len(wst),
+                                   "mpr": mpr}
+            del wdeps
+            nxt += 100
+        sweep = []
+        for m in [float(x) for x in a.mpr_sweep.split(",") if x.strip()]:
+            mdeps = pb.epochs(n_txn_rank, m, theta, 2)
+            mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            mc = sum(s.committed for s in mst)
+            sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_epoch": mel / len(mst) * 1e3,
+                          "abort_rate": 1 - mc / (len(mst) * n_txn_total),
+                          "rounds_mean": float(np.mean([s.rounds for s in mst]))})
+            nxt += 100
+        if sweep:
+            out["mpr_sweep"] = sweep
     if world == 1 and rank == 0 and not a.no_cpu_baseline:
         # the single-thread E-schedule port (decision-identical) and, for
         # NO_WAIT, the multi-threaded engine, which is then the baseline
@@ -434,6 +545,7 @@ def main():
         out["tpcc"] = tpcc_leg(a)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

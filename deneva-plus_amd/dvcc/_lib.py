@@ -170,6 +170,22 @@ def lib():
     return _lib
 
 
+def source_hash():
+    """12 hex digits over the engine's sources (csrc/, include/dvcc.h): ties a
+    committed profile (e.g. the PMC traffic of a kernel) to the code it
+    measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    root = os.path.dirname(PKG_DIR)
+    files = sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*"))) + [os.path.join(root, "include", "dvcc.h")]
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode())
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
 def check(rc, what=""):
     if rc != DV_OK:
         raise DvccError(rc, what)
