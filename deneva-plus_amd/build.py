@@ -22,7 +22,7 @@ ARCH = os.environ.get("DVCC_OFFLOAD_ARCH", "gfx950")
 
 HEADERS = [os.path.join(INCLUDE, "dvcc.h"), os.path.join(CSRC, "dvcc_internal.h"),
            os.path.join(CSRC, "dvcc_common.h"), os.path.join(CSRC, "dvcc_tpcc.h")]
-HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_carry.hip", "dvcc_comm.hip", "dvcc_tpcc.hip",
+HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_prefix.hip", "dvcc_carry.hip", "dvcc_comm.hip", "dvcc_tpcc.hip",
             "dvcc_runtime.hip"]
 CPP_SRCS = ["ycsb_gen.cpp", "tpcc_gen.cpp"]
 

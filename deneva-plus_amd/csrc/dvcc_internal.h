@@ -74,6 +74,10 @@ struct Counters {
     uint32_t async_declined;  // asynchronous tries that found the live set too large
     uint32_t async_yields;    // asynchronous launches whose workgroups yielded (no more tries this epoch)
     uint32_t calvin_dups;     // CALVIN: some txn touches a row twice (k_calvin_dup_fix)
+    uint32_t async_block;     // the rounds of this (sub-)epoch take no further asynchronous tries
+    uint32_t a_acc;           // prefix-kill: accesses of the prefix txns
+    uint32_t b_txn, b_acc;    // prefix-kill: surviving txns after the prefix, their accesses
+    unsigned long long pass_live;  // live accesses every k_round_pass of the epoch read, summed
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
@@ -129,17 +133,20 @@ __device__ __forceinline__ uint32_t input_err(const Counters *ctr) {
 constexpr uint32_t kProbeHistTiles = 1024;
 // pairs: sort keys; tb_start/tb_end: each txn's access range; tlen (optional):
 // its access count; acc_row (optional): row | wr << 31 per access.  An access
-// at position >= 1 << slog in its txn is an error (ERRB_BIG).
+// at position >= 1 << slog in its txn is an error (ERRB_BIG).  pair_limit <
+// n_txn: sort keys only for txns < pair_limit (the epoch's first accesses),
+// their count added to ctr->a_acc (prefix-kill epochs).
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts);
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
 // digit_tot: kRadix.  scatter_ev (optional): 2 events per pass for timing.
+// n_dev (optional): the real count on the device, n an upper bound.
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done);
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev);
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
                         const uint32_t *tb_start, uint64_t *el, Counters *ctr);
@@ -161,6 +168,7 @@ struct RoundBufs {
     uint8_t *status;         // per txn
     const uint8_t *tlen;     // per txn
     uint32_t *ulist[2];      // undecided txns, ping-pong (single-GPU settle)
+    const uint32_t *n_txn_dev;  // (optional) the real txn count, n_txn an upper bound (sub-epochs)
     uint64_t *desc;
     uint32_t *tile_ctr;
     Counters *ctr;
@@ -172,16 +180,24 @@ struct RoundBufs {
 struct RoundPub {
     unsigned long long ru;  // rounds settled << 32 | undecided txns
     unsigned long long le;  // live accesses << 32 | error bits
-    unsigned long long tl;  // tail launched at round r0 but the live set did not
-                            // fit: r0 << 32 | 1 (the rounds resume from r0)
+    unsigned long long tl;  // r0 << 32 | code: the tail launched at round r0 but the
+                            // live set did not fit (1; the rounds resume from r0);
+                            // the asynchronous try at r0 declined (2), yielded
+                            // (3) -- both halt execution until the host resumes
+                            // the rounds -- decided the rest (4), or found
+                            // nothing left to decide (5)
     // partitioned rounds: undecided txns after round r, at [r % kPubLog]
     // (written before ru publishes r + 1), so every rank reads the count of
     // the same round however far its stream has run ahead
     static constexpr uint32_t kPubLog = 64;
     unsigned int und_log[kPubLog];
+    unsigned long long ai;  // iterations of the last asynchronous launch that ran (r0 << 32 | iters)
 };
+// the rounds of one (sub-)epoch begin: round 0's counts (n_acc_dev /
+// b.n_txn_dev, when given, hold the real ones), its verdict bytes cleared, the
+// asynchronous-try state reset
 void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
-                       uint32_t n_txn_pad);
+                       uint32_t n_txn_pad, const uint32_t *n_acc_dev);
 // settle = single GPU (the following settle compacts the undecided list; a
 // pass whose round starts with no undecided txn is a no-op)
 // ev0/ev1 (optional): recorded by the pass's own dispatch (hipExtLaunchKernel)
@@ -249,6 +265,21 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
                   const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
                   uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot);
 
+// ---- prefix-kill epochs (dvcc_prefix.hip)
+void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                        const uint32_t *acc_row, uint32_t K, uint8_t *row_state, int nowait, int clear,
+                        const Counters *ctr);
+uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (descriptors per array)
+// k_kill (every access after the prefix's against the row state) and
+// k_kill_compact (the survivors' sub-epoch)
+void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
+                         const uint32_t *acc_txn, uint64_t n_acc, uint32_t K, uint32_t n_txn,
+                         const uint8_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
+                         uint8_t *tlen_b, uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr,
+                         uint32_t tag, Counters *ctr);
+void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
+                             uint8_t *status, const Counters *ctr);
+
 // per-epoch reset: counters (err = *err_seed when given), tile tickets,
 // status (value; padding aborted), access ranges and counts
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
@@ -271,6 +302,6 @@ void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const
 void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
                          uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables, uint32_t *err);
 
-inline uint32_t nblocks_for(uint64_t n) { return (uint32_t)((n + kTile - 1) / kTile); }
+__host__ __device__ inline uint32_t nblocks_for(uint64_t n) { return (uint32_t)((n + kTile - 1) / kTile); }
 
 }  // namespace dvcc

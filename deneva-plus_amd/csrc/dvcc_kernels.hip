@@ -74,7 +74,8 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                                                   uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen,
                                                   uint32_t *__restrict__ acc_row, Counters *ctr,
-                                                  uint32_t *__restrict__ counts, uint32_t ntiles) {
+                                                  uint32_t *__restrict__ counts, uint32_t ntiles,
+                                                  uint32_t pair_limit) {
     // The first radix pass's histogram (digit = row bits [0, 8)) is counted
     // here, per 4096-access sort tile, so the sort skips that k_radix_hist
     // launch and its 8-byte-per-access re-read of the pairs.
@@ -200,12 +201,29 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                     if (i0 + j < n) acc_row[i0 + j] = ar[j];
             }
         }
-        if (i0 + kPV <= n) {
-            *reinterpret_cast<ulonglong2 *>(pairs + i0) = ulonglong2{out[0], out[1]};
-            *reinterpret_cast<ulonglong2 *>(pairs + i0 + 2) = ulonglong2{out[2], out[3]};
+        if (pair_limit >= n_txn) {
+            if (i0 + kPV <= n) {
+                *reinterpret_cast<ulonglong2 *>(pairs + i0) = ulonglong2{out[0], out[1]};
+                *reinterpret_cast<ulonglong2 *>(pairs + i0 + 2) = ulonglong2{out[2], out[3]};
+            } else {
+                for (int j = 0; j < kPV; j++)
+                    if (i0 + j < n) pairs[i0 + j] = out[j];
+            }
         } else {
+            // prefix-kill epochs: sort keys only for the prefix txns (the first
+            // accesses of the epoch), and their count (one atomic per wave)
+            uint32_t np = 0;
+#pragma unroll
             for (int j = 0; j < kPV; j++)
-                if (i0 + j < n) pairs[i0 + j] = out[j];
+                if (i0 + j < n && txn[j] < pair_limit) {
+                    pairs[i0 + j] = out[j];
+                    np++;
+                }
+            if (__ballot(np != 0)) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) np += __shfl_xor(np, off, 64);
+                if (lane == 0) atomicAdd(&ctr->a_acc, np);
+            }
         }
         // digit-0 counts of the emitted pairs (as k_radix_hist: a step whose
         // keys share one digit adds once)
@@ -248,9 +266,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t slog, uint64_t *__restrict__ pairs,
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
-                                                  Counters *ctr) {
+                                                  Counters *ctr, uint32_t pair_limit) {
     probe_body<false>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                      ctr, nullptr, 0);
+                      ctr, nullptr, 0, pair_limit);
 }
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     Tables tabs, const uint64_t *__restrict__ keys, const uint8_t *__restrict__ types,
@@ -259,15 +277,16 @@ __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
     uint32_t ntiles) {
     probe_body<true>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                     ctr, counts, ntiles);
+                     ctr, counts, ntiles, n_txn);
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts) {
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
+    if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     if (counts)
@@ -275,7 +294,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                                                tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
     else
         k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
-                                          tb_end, tlen, acc_row, ctr);
+                                          tb_end, tlen, acc_row, ctr, pair_limit < n_txn ? pair_limit : n_txn);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -283,10 +302,19 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
 // 64 consecutive elements, so (step, lane) order == input order: the ballot
 // ranks below are stable.
 
+// n_dev (optional): the key count lives on the device (a sub-epoch's size, known
+// only to the kernels before it); n and the grid are then upper bounds and the
+// tiles past the real count leave at once.
+__device__ __forceinline__ uint64_t sort_n(uint64_t n, const uint32_t *n_dev) {
+    return n_dev && (uint64_t)*n_dev < n ? (uint64_t)*n_dev : n;
+}
+
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restrict__ in, uint64_t n,
                                                        int shift, uint32_t *__restrict__ counts,
-                                                       uint32_t nblocks) {
+                                                       uint32_t nblocks, const uint32_t *__restrict__ n_dev) {
     __shared__ uint32_t wc[4][kRadix];
+    n = sort_n(n, n_dev);
+    if ((uint64_t)blockIdx.x * kTile >= n) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     for (uint32_t d = tid; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
     __syncthreads();
@@ -321,9 +349,11 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
 
 // exclusive scan of counts[d][0..nblocks) in place, one workgroup per digit
 __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ counts, uint32_t nblocks,
-                                                       uint32_t *__restrict__ digit_tot) {
+                                                       uint32_t *__restrict__ digit_tot,
+                                                       const uint32_t *__restrict__ n_dev) {
     __shared__ uint32_t lds4[4];
-    uint32_t *c = counts + (uint64_t)blockIdx.x * nblocks;
+    uint32_t *c = counts + (uint64_t)blockIdx.x * nblocks;  // (row stride: the upper bound)
+    if (n_dev && nblocks_for(*n_dev) < nblocks) nblocks = nblocks_for(*n_dev);
     const uint32_t per = (nblocks + kBlock - 1) / kBlock;
     const uint32_t lo = threadIdx.x * per;
     uint32_t hi = lo + per;
@@ -342,8 +372,10 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ co
 
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n, int shift, const uint32_t *__restrict__ counts,
-    const uint32_t *__restrict__ digit_tot, uint32_t nblocks) {
+    const uint32_t *__restrict__ digit_tot, uint32_t nblocks, const uint32_t *__restrict__ n_dev) {
     __shared__ __attribute__((aligned(16))) uint64_t skeys[kTile];
+    n = sort_n(n, n_dev);
+    if ((uint64_t)blockIdx.x * kTile >= n) return;
     __shared__ uint32_t wc[4][kRadix];
     __shared__ uint32_t dstart[kRadix];
     __shared__ uint64_t gbase[kRadix];
@@ -413,20 +445,20 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
 }
 
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done) {
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        if (pass > 0 || !hist0_done) k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb);
-        k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot);
+        if (pass > 0 || !hist0_done) k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb, n_dev);
+        k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot, n_dev);
         // timing: events recorded by the dispatch itself (no extra packets)
         hipExtLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kBlock), 0, s,
                               scatter_ev ? scatter_ev[2 * pass] : nullptr,
                               scatter_ev ? scatter_ev[2 * pass + 1] : nullptr, 0,
                               (const uint64_t *)pairs[cur], pairs[cur ^ 1], n, shift,
-                              (const uint32_t *)counts, (const uint32_t *)digit_tot, nb);
+                              (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
         cur ^= 1;
     }
     return cur;

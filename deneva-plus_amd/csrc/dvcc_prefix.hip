@@ -1,0 +1,224 @@
+// dvcc_prefix.hip -- prefix-kill decisions for large single-GPU epochs (gfx950).
+//
+// The E-schedule's decisions are the sequence-ordered greedy:
+// txn i commits iff no earlier COMMITTED txn conflicts with it.  Restricted to
+// a prefix T_0..T_{K-1} of the epoch it is the same greedy, so the prefix can
+// be decided on its own.  After that, a later txn that conflicts with a
+// committed prefix txn aborts, whatever else happens -- and at zipf 0.9 the
+// prefix's commits hold the hot rows: deciding the first 16K txns of a
+// 1M-txn config-D epoch kills ~91 % of the rest.  The survivors' fate
+// depends only on each other (a killed txn blocks nobody), so they form a
+// sub-epoch decided by the same rounds, over ~9 % of the accesses.  The
+// runtime (dvcc_runtime.hip, run_prefix_epoch) therefore runs
+//     probe (sort keys for the prefix only) -> sort + rounds on the prefix ->
+//     k_prefix_mark -> k_kill_compact -> k_prefix_mark (clear) ->
+//     sort + rounds on the survivors -> k_sub_scatter_back -> execution,
+// instead of sorting and scanning every access of the epoch round after round.
+//
+// Row state of the prefix's committed txns (one byte per row of the context):
+//   2  a committed txn writes the row
+//   1  (NO_WAIT / WAIT_DIE) a committed txn reads it
+// A later access conflicts with it exactly as Row_lock::lock_get's
+// conflict_lock would with the committed owners (row_lock.cpp:69, 86-90): a
+// write meets 1 or 2, a read meets 2; OCC's central validation
+// (occ.cpp:185-199) kills any access to a row an earlier committed txn writes.
+// Two committed 2PL txns never hold one row as reader and writer, so the plain
+// byte stores below never race on different values.
+#include "dvcc_common.h"
+
+namespace dvcc {
+
+namespace {
+constexpr int kKillIPT = 8;  // txns per thread
+}  // namespace
+
+// mark (clear = 0) or clear (clear = 1) the rows of the committed prefix txns;
+// lane per txn, its accesses from the probe's txn-major acc_row
+__global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restrict__ status,
+                                                        const uint32_t *__restrict__ tb_start,
+                                                        const uint32_t *__restrict__ tb_end,
+                                                        const uint32_t *__restrict__ acc_row, uint32_t K,
+                                                        uint8_t *__restrict__ row_state, int nowait, int clear,
+                                                        const Counters *__restrict__ ctr) {
+    if (input_err(ctr)) return;
+    for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < K; t += gridDim.x * kBlock) {
+        if (status[t] != ST_COMMIT) continue;
+        for (uint32_t a = tb_start[t], e = tb_end[t]; a < e; a++) {
+            const uint32_t ar = acc_row[a];
+            const uint32_t row = ar & ~AR_WR;
+            if (clear) row_state[row] = 0;
+            else if (ar & AR_WR) row_state[row] = 2;
+            else if (nowait) row_state[row] = 1;
+        }
+    }
+}
+
+// Every access after the prefix's (index >= ctr->a_acc) against the row
+// state: a conflict aborts its txn (a plain byte store; the txn's other
+// killed accesses store the same byte).  Access-parallel and coalesced: the
+// txn-major acc_row and the epoch's acc_txn streamed, one byte gathered per
+// access from the row state (the hot rows' bytes stay in L2).
+__global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ acc_row,
+                                                 const uint32_t *__restrict__ acc_txn, uint64_t n,
+                                                 const uint8_t *__restrict__ row_state, int nowait,
+                                                 uint8_t *__restrict__ status, const Counters *__restrict__ ctr) {
+    if (input_err(ctr)) return;
+    const uint64_t first = ctr->a_acc;
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
+    for (uint64_t i0 = first + ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; i0 < n; i0 += stride) {
+        uint32_t ar[4], tx[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const bool ok = i0 + j < n;
+            ar[j] = ok ? acc_row[i0 + j] : 0u;
+            tx[j] = ok ? acc_txn[i0 + j] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            if (i0 + j >= n) continue;
+            const uint8_t s = row_state[ar[j] & ~AR_WR];
+            if (s == 2 || (nowait && s == 1 && (ar[j] & AR_WR))) status[tx[j]] = ST_ABORT;
+        }
+    }
+}
+
+// Txns [K, n_txn) after k_kill: survivors (still undecided) are renumbered
+// 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
+// and their sort keys written densely in that order, pairs_b = row << 32 |
+// sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
+// their layout).  One launch: tiles of kBlock x kKillIPT txns taken by ticket,
+// two decoupled look-backs (survivors, their accesses) give every tile its
+// output offsets; the last tile publishes S and the access count (b_txn,
+// b_acc) for the kernels that follow.
+__global__ __launch_bounds__(kBlock) void k_kill_compact(
+    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
+    const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint8_t *__restrict__ status,
+    uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
+    uint8_t *__restrict__ tlen_b,
+    uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
+    Counters *ctr) {
+    __shared__ uint32_t s_tile;
+    __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
+    __shared__ Agg s_pre_c, s_pre_a;
+    constexpr uint32_t kKillTile = kBlock * kKillIPT;
+    const uint32_t m = n_txn > K ? n_txn - K : 0u;
+    const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
+    if (blockIdx.x >= ntiles || input_err(ctr)) return;  // (b_txn = b_acc = 0 from the epoch clear)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
+    __syncthreads();
+    const uint32_t tile = s_tile;
+    const uint32_t first = K + tile * kKillTile + tid * kKillIPT;
+    uint32_t surv = 0, cnt = 0, acc = 0;
+    uint32_t a0s[kKillIPT], lens[kKillIPT];
+    // the status bytes of the thread's 8 consecutive txns: two 4-byte loads
+    // when aligned (first is a multiple of 8 past K, K is not)
+    uint8_t st[kKillIPT];
+#pragma unroll
+    for (int j = 0; j < kKillIPT; j++) st[j] = first + j < n_txn ? status[first + j] : (uint8_t)ST_ABORT;
+#pragma unroll
+    for (int j = 0; j < kKillIPT; j++) {
+        const uint32_t t = first + j;
+        a0s[j] = 0;
+        lens[j] = 0;
+        if (st[j] != ST_UNDEC) continue;  // killed (k_kill), or past the end
+        const uint32_t a0 = tb_start[t], a1 = tb_end[t];
+        a0s[j] = a0;
+        lens[j] = a1 - a0;
+        surv |= 1u << j;
+        cnt++;
+        acc += a1 - a0;
+    }
+    const Agg inc_c = wave_incl<OpPlain>(Agg{0u, 0u, cnt}, lane);
+    const Agg inc_a = wave_incl<OpPlain>(Agg{0u, 0u, acc}, lane);
+    if (lane == 63) {
+        wt_c[wave] = inc_c;
+        wt_a[wave] = inc_a;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        Agg bc{0u, 0u, 0u}, ba{0u, 0u, 0u};
+        for (int w = 0; w < kBlock / 64; w++) {
+            bc = OpPlain::comb(bc, wt_c[w]);
+            ba = OpPlain::comb(ba, wt_a[w]);
+        }
+        const Agg pc = look_back<OpPlain>(desc_c, tile, tag, bc, lane, ctr);
+        const Agg pa = look_back<OpPlain>(desc_a, tile, tag, ba, lane, ctr);
+        if (lane == 0) {
+            s_pre_c = pc;
+            s_pre_a = pa;
+            if (tile == ntiles - 1) {
+                ctr->b_txn = pc.c + bc.c;
+                ctr->b_acc = pa.c + ba.c;
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t sub = s_pre_c.c, ab = s_pre_a.c;
+    for (uint32_t w = 0; w < wave; w++) {
+        sub += wt_c[w].c;
+        ab += wt_a[w].c;
+    }
+    sub += wave_excl_from_incl<OpPlain>(inc_c, lane).c;
+    ab += wave_excl_from_incl<OpPlain>(inc_a, lane).c;
+#pragma unroll
+    for (int j = 0; j < kKillIPT; j++) {
+        if (!((surv >> j) & 1u)) continue;
+        map[sub] = first + j;
+        tlen_b[sub] = (uint8_t)lens[j];
+        status_b[sub] = ST_UNDEC;
+        for (uint32_t q = 0; q < lens[j]; q++) {
+            const uint32_t ar = acc_row[a0s[j] + q];
+            pairs_b[ab + q] = pair_pack(ar & ~AR_WR, sub, q, ar >> 31);
+        }
+        ab += lens[j];
+        sub++;
+    }
+}
+
+// the survivors' decisions back to their txns (after the survivors' rounds;
+// a no-op while they are halted, Counters::halt)
+__global__ __launch_bounds__(kBlock) void k_sub_scatter_back(const uint32_t *__restrict__ map,
+                                                             const uint8_t *__restrict__ status_b,
+                                                             uint8_t *__restrict__ status, const Counters *ctr) {
+    if (input_err(ctr) || ctr->halt) return;
+    const uint32_t S = ctr->b_txn;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < S; i += gridDim.x * kBlock) status[map[i]] = status_b[i];
+}
+
+namespace {
+uint32_t grid_of(uint64_t n, uint32_t cap) {
+    const uint64_t g = (n + kBlock - 1) / kBlock;
+    return (uint32_t)(g < 1 ? 1 : (g > cap ? cap : g));
+}
+}  // namespace
+
+void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                        const uint32_t *acc_row, uint32_t K, uint8_t *row_state, int nowait, int clear,
+                        const Counters *ctr) {
+    if (!K) return;
+    k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, nowait, clear,
+                                                     ctr);
+}
+
+uint32_t kill_tiles(uint32_t n_after) { return (n_after + kBlock * kKillIPT - 1) / (kBlock * kKillIPT); }
+
+void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
+                         const uint32_t *acc_txn, uint64_t n_acc, uint32_t K, uint32_t n_txn,
+                         const uint8_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
+                         uint8_t *tlen_b, uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr,
+                         uint32_t tag, Counters *ctr) {
+    const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
+    if (!nt) return;
+    k_kill<<<grid_of(n_acc / 4 + 1, 2048), kBlock, 0, s>>>(acc_row, acc_txn, n_acc, row_state, nowait, status, ctr);
+    k_kill_compact<<<nt, kBlock, 0, s>>>(tb_start, tb_end, acc_row, K, n_txn, status, map, status_b, tlen_b, pairs_b,
+                                         desc_c, desc_a, tile_ctr, tag, ctr);
+}
+
+void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
+                             uint8_t *status, const Counters *ctr) {
+    if (!ub) return;
+    k_sub_scatter_back<<<grid_of(ub, 2048), kBlock, 0, s>>>(map, status_b, status, ctr);
+}
+
+}  // namespace dvcc

@@ -416,9 +416,12 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
     // nothing left to decide, or a rejected epoch: no-op
     const uint32_t n = und && !input_err(ctr) ? n_live : 0u;
     const uint32_t ntiles = (n + Geo<EIn>::kTile - 1) / Geo<EIn>::kTile;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && round < (uint32_t)kRoundLog && (und || round == 0)) {
-        ctr->log_live[round] = n_live;
-        ctr->log_und[round] = und_in ? und : 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (round < (uint32_t)kRoundLog && (und || round == 0)) {
+            ctr->log_live[round] = n_live;
+            ctr->log_und[round] = und_in ? und : 0u;
+        }
+        if (n) ctr->pass_live += n;  // (one pass at a time: the stream orders them)
     }
     // one thread publishes the outcome of the previous round to the host
     const bool publisher = pub && threadIdx.x == 0 && blockIdx.x == (ntiles ? ntiles - 1 : 0);
@@ -523,7 +526,8 @@ __global__ __launch_bounds__(kBlock) void k_round_settle(
     const uint32_t *__restrict__ n_in, uint32_t n_txn, uint32_t *__restrict__ list_out,
     uint32_t *__restrict__ n_out) {
     __shared__ SettleLds sh;
-    const uint32_t n = FIRST ? n_txn : *n_in;
+    // round 0: every txn of the (sub-)epoch (its real count from round0_init)
+    const uint32_t n = n_in ? *n_in : n_txn;
     const uint32_t lo = blockIdx.x * kSettleChunk;
     if (lo >= n) return;
     settle_chunk<FIRST>(sh, lo, n, status, vb8, slog, tlen, list_in, list_out, n_out);
@@ -857,7 +861,7 @@ __device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t
 // do (no txn undecided, or an earlier try ran)
 __device__ __forceinline__ uint32_t async_gate(const Counters *ctr, uint32_t r0, uint32_t G,
                                                uint32_t thresh) {
-    if (ctr->async_r0 != 0 || ctr->async_yields != 0 || ctr->nund[r0 & 1] == 0 || input_err(ctr)) return 0u;
+    if (ctr->async_r0 != 0 || ctr->async_block != 0 || ctr->nund[r0 & 1] == 0 || input_err(ctr)) return 0u;
     const uint32_t n_all = ctr->nlive[r0 & 1];
     return n_all <= thresh && ((uint64_t)n_all + G - 1) / G <= kAsyncCap ? 1u : 2u;
 }
@@ -870,8 +874,10 @@ __global__ __launch_bounds__(kBlock) void k_async_words(const uint8_t *__restric
                                                         uint32_t *__restrict__ tword,
                                                         uint32_t *__restrict__ carry, uint32_t G,
                                                         uint32_t thresh, uint32_t r0,
+                                                        const uint32_t *__restrict__ n_txn_dev,
                                                         const Counters *__restrict__ ctr) {
     if (async_gate(ctr, r0, G, thresh) != 1u) return;
+    if (n_txn_dev && *n_txn_dev < n_txn) n_txn = *n_txn_dev;
     const uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x;
     for (uint32_t g = i0; g < G; g += gridDim.x * blockDim.x) carry[g] = kCarryInit;
     for (uint32_t t = i0; t < n_txn; t += gridDim.x * blockDim.x) {
@@ -1068,37 +1074,52 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
 }
 
 // after the asynchronous rounds: the status bytes from the words and the
-// count of txns left undecided (an error).  A declined launch changes nothing
-// and says so through pub->tl = r0 << 32 | 2.
+// count of txns left undecided (an error).  The outcome goes to pub->tl
+// (r0 << 32 | code, RoundPub).  A declined launch changed nothing; like a
+// yielded one it halts execution (Counters::halt) and blocks further tries, and
+// the host resumes the synchronous rounds at r0.
+__device__ __forceinline__ void publish_try(RoundPub *pub, uint32_t r0, uint32_t code) {
+    if (pub)
+        __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | code, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__ status,
                                                            const uint32_t *__restrict__ tword,
                                                            uint32_t n_txn, uint32_t r0, RoundPub *pub,
+                                                           const uint32_t *__restrict__ n_txn_dev,
                                                            Counters *ctr) {
     const uint32_t go = ctr->async_go;
     if (go != 1u) {
-        if (go == 2u && blockIdx.x == 0 && threadIdx.x == 0) {
-            ctr->async_declined++;
-            if (pub)
-                __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 2u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            if (go == 2u) {
+                ctr->async_declined++;
+                ctr->async_block = 1u;
+                ctr->halt = 1u;
+            }
+            publish_try(pub, r0, go == 2u ? 2u : 5u);
         }
         return;
     }
     const bool yielded = ctr->halt != 0;  // some workgroup left undecided txns behind
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (yielded) {
-            // no further tries this epoch; the round state of r0 stays as it
-            // was (nund, the element array), so the host's synchronous rounds
-            // resume from it with these statuses
+            // no further tries in these rounds; the round state of r0 stays as
+            // it was (nund, the element array), so the host's synchronous
+            // rounds resume from it with these statuses
             ctr->async_yields++;
-            if (pub)
-                __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | 3u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            ctr->async_block = 1u;
+            publish_try(pub, r0, 3u);
         } else {
             ctr->async_r0 = r0;
             ctr->nund[r0 & 1] = 0;  // the passes queued behind the try are no-ops
+            if (pub)
+                __hip_atomic_store(&pub->ai, ((unsigned long long)r0 << 32) | ctr->async_iters,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            publish_try(pub, r0, 4u);
         }
     }
+    if (n_txn_dev && *n_txn_dev < n_txn) n_txn = *n_txn_dev;
     uint32_t und = 0;
     for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x) {
         const uint8_t s = word_status(tword[t]);
@@ -1113,10 +1134,18 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
 // 1 << slog bytes per txn)
 __global__ __launch_bounds__(kBlock) void k_round0_init(uint32_t n, uint32_t n_txn, uint32_t n_pad,
                                                         uint4 *__restrict__ vb8, uint32_t slog,
-                                                        Counters *ctr) {
+                                                        const uint32_t *__restrict__ n_dev,
+                                                        const uint32_t *__restrict__ n_txn_dev, Counters *ctr) {
+    if (n_txn_dev) n_pad = (*n_txn_dev + 3u) & ~3u;  // (n_pad: the upper bound's)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctr->nlive[0] = n;
-        ctr->nund[0] = n_txn;  // partitioned rounds: round 0's list is every txn
+        ctr->nlive[0] = n_dev ? *n_dev : n;
+        ctr->nund[0] = n_txn_dev ? *n_txn_dev : n_txn;  // partitioned rounds: round 0's list is every txn
+        // a (sub-)epoch's rounds start with no asynchronous try behind them
+        ctr->async_go = 0;
+        ctr->async_r0 = 0;
+        ctr->async_iters = 0;
+        ctr->async_block = 0;
+        ctr->halt = 0;
     }
     const uint64_t words = (uint64_t)n_pad << (slog - 4);
     for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
@@ -1138,9 +1167,9 @@ bool round_el32(uint32_t n_txn, uint32_t slog) {
 uint32_t tail_cap(bool el32) { return el32 ? TailGeo<uint32_t>::kCap : TailGeo<uint64_t>::kCap; }
 
 void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
-                       uint32_t n_txn_pad) {
+                       uint32_t n_txn_pad, const uint32_t *n_acc_dev) {
     k_round0_init<<<txn_grid(n_txn_pad << (b.slog - 4)), kBlock, 0, s>>>(
-        n_acc, n_txn, n_txn_pad, reinterpret_cast<uint4 *>(b.vb8), b.slog, b.ctr);
+        n_acc, n_txn, n_txn_pad, reinterpret_cast<uint4 *>(b.vb8), b.slog, n_acc_dev, b.n_txn_dev, b.ctr);
 }
 
 template <class E>
@@ -1190,9 +1219,9 @@ void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uin
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
     k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
-                                                                    b.ctr);
+                                                                    b.n_txn_dev, b.ctr);
     k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
-    k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, r0, pub, b.ctr);
+    k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, r0, pub, b.n_txn_dev, b.ctr);
 }
 
 // Every workgroup of the asynchronous launch must be resident at once (one
@@ -1215,7 +1244,7 @@ void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_
     const uint32_t nb = n ? (n + kSettleChunk - 1) / kSettleChunk : 1;
     uint32_t *n_out = &b.ctr->nund[(round + 1) & 1];
     if (round == 0)
-        k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, nullptr, nullptr,
+        k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, nullptr, &b.ctr->nund[0],
                                                    n_txn, b.ulist[1], n_out);
     else
         k_round_settle<false><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,

@@ -111,6 +111,24 @@ struct dv_ctx {
     uint64_t async_idle_ticks = 0;
     uint64_t wall_khz = 100000;  // hipDeviceAttributeWallClockRate
 
+    // the (sub-)epoch the decision rounds work on: the epoch itself, or one
+    // stage of a prefix-kill epoch (the prefix; the survivors, renumbered)
+    uint8_t *v_status = nullptr, *v_tlen = nullptr;
+    uint32_t v_n_txn = 0;                    // its txns (an upper bound when v_n_txn_dev is set)
+    const uint32_t *v_n_txn_dev = nullptr;   // its real txn count, on the device
+    uint32_t v_thresh = 0;                   // asynchronous-try threshold (0: async_thresh's rule)
+
+    // prefix-kill epochs (run_prefix_epoch, dvcc_prefix.hip)
+    uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 64)
+    bool prefix_mode = false;     // the epoch in flight is one
+    uint32_t rounds_prefix = 0;   // rounds the prefix took
+    uint8_t *row_state = nullptr; // per row: the prefix's committed readers (1) / writers (2)
+    uint64_t row_state_cap = 0;
+    uint8_t *b_status = nullptr, *b_tlen = nullptr;  // the survivors' sub-epoch (txn capacity)
+    uint32_t *b_map = nullptr;                      // survivor -> txn
+    uint64_t *kdesc = nullptr;                      // k_kill_compact look-back descriptors (2 arrays)
+    uint32_t kdesc_n = 0;                           // descriptors per array
+
     // timing
     hipEvent_t ev[32] = {};
     hipEvent_t sev[16] = {};
@@ -167,10 +185,11 @@ RoundBufs round_bufs(dv_ctx *c) {
     b.el32 = c->el32;
     b.vb8 = c->vb8;
     b.slog = c->slog;
-    b.status = c->status;
-    b.tlen = c->tlen;
+    b.status = c->v_status;
+    b.tlen = c->v_tlen;
     b.ulist[0] = c->ulist[0];
     b.ulist[1] = c->ulist[1];
+    b.n_txn_dev = c->v_n_txn_dev;
     b.desc = c->desc;
     b.tile_ctr = c->tile_ctr;
     b.ctr = c->ctr;
@@ -182,9 +201,19 @@ uint32_t next_tag(dv_ctx *c) {
     if (++c->round_tag >= (1u << 25)) {
         (void)hipMemsetAsync(c->desc, 0, (size_t)((c->cfg.max_acc + kRTile - 1) / kRTile) * 8,
                              c->stream);
+        if (c->kdesc) (void)hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream);
         c->round_tag = 1;
     }
     return c->round_tag;
+}
+
+// the decision rounds work on the whole epoch
+void view_epoch(dv_ctx *c) {
+    c->v_status = c->status;
+    c->v_tlen = c->tlen;
+    c->v_n_txn = c->n_txn;
+    c->v_n_txn_dev = nullptr;
+    c->v_thresh = 0;
 }
 
 // a zeroed tile-ticket counter for the next single-pass launch
@@ -297,7 +326,8 @@ void dv_close(dv_ctx *c) {
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
-                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap};
+                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
+                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc};
     for (void *b : bufs) dfree(b);
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
@@ -672,10 +702,10 @@ int dv_tpcc_load(dv_ctx *c, const dv_tpcc_params *p, uint64_t seed) {
 // ---------------------------------------------------------------- epoch
 // Probe + sort + per-row queue construction; for CALVIN also the grant groups
 // (the lock thread's whole job for the epoch, calvin_thread.cpp:40-100).
-int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
-    if (!c || !ep) return DV_ERR_ARG;
-    const uint32_t *err_seed = c->err_seed;  // only for the epoch dv_epoch_run staged just now
-    c->err_seed = nullptr;
+namespace {
+// the common start of an epoch: argument checks, the verdict-byte stride,
+// the per-epoch host state
+int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     if (ep->n_acc && (!ep->keys || !ep->types || !ep->acc_txn)) return DV_ERR_ARG;
     bool any = false;
@@ -712,7 +742,22 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     c->applied = 0;
     c->async_launched = 0;
     c->async_unconfirmed = false;
+    c->prefix_mode = false;
+    c->rounds_prefix = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
+    view_epoch(c);
+    return DV_OK;
+}
+}  // namespace
+
+int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
+    if (!c || !ep) return DV_ERR_ARG;
+    const uint32_t *err_seed = c->err_seed;  // only for the epoch dv_epoch_run staged just now
+    c->err_seed = nullptr;
+    int r = epoch_setup(c, ep);
+    if (r) return r;
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    const uint32_t slog = calvin ? 7u : c->slog;  // CALVIN: positions only name access ids
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
                        c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr);
@@ -720,12 +765,12 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
-                 calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr);
+                 calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
-                                ktiming(c) ? c->sev : nullptr, fuse_hist);
+                                ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
@@ -733,7 +778,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         const uint32_t tag = next_tag(c);
         calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
-        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, ep->n_txn, c->n_txn_pad);
+        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, ep->n_txn, c->n_txn_pad, nullptr);
         __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
         __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
         c->live_ub = (uint32_t)ep->n_acc;
@@ -761,7 +806,7 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
                (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr,
                t ? c->pev[2 * c->passes] : nullptr, t ? c->pev[2 * c->passes + 1] : nullptr);
     c->passes++;
-    if (settle) round_settle(c->stream, b, r, c->n_txn, c->und_ub);
+    if (settle) round_settle(c->stream, b, r, c->v_n_txn, c->und_ub);
     else list_verdict(c->stream, b, r, c->und_ub, d_verdict);
     c->rounds++;
 }
@@ -864,6 +909,8 @@ int run_rounds(dv_ctx *c, bool resume);
 // kernel is a no-op for a rejected epoch, input_err, and while the rounds
 // are halted, Counters::halt)
 void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
+    if (c->prefix_mode)  // the survivors' decisions back to their txns
+        launch_sub_scatter_back(c->stream, c->b_map, c->b_status, c->v_n_txn, c->status, c->ctr);
     if (c->cfg.workload == DV_TPCC) {
         const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
         TpccExec x{};
@@ -926,6 +973,8 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     c->phase = 0;
     c->tp_args = nullptr;  // per epoch (dv_tpcc_epoch_begin)
     c->tp_oid = nullptr;
+    const bool prefix = c->prefix_mode;
+    c->prefix_mode = false;
     if (r) return r;
     r = err_from_bits(c->h_ctr->err | c->h_ctr->peer_err);
     if (r) {
@@ -964,6 +1013,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         st->write_cnt = wcnt;
         st->read_digest = dig;
         st->rounds = calvin ? 0 : (c->rounds_real ? c->rounds_real : c->rounds);
+        if (prefix) st->rounds += c->rounds_prefix;  // the prefix's, then the survivors'
         st->sort_passes = c->sort_passes;
         st->async_launches = (uint16_t)std::min(c->async_launched, 0xFFFFu);
         st->async_declined = (uint16_t)std::min(c->h_ctr->async_declined, 0xFFFFu);
@@ -986,16 +1036,14 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             st->scatter_launches = c->n_acc ? c->sort_passes : 0;
             const uint32_t np = std::min(c->passes, (uint32_t)kRoundLog);
             float sp = 0;
-            uint64_t live = 0;
             for (uint32_t p = 0; p < np; p++) {
                 float m = 0;
                 (void)hipEventElapsedTime(&m, c->pev[2 * p], c->pev[2 * p + 1]);
                 sp += m;
-                live += c->h_ctr->log_live[p];  // 0 for a no-op pass past the fixpoint
             }
             st->pass_launches = np;
             st->ms_pass = sp;
-            st->pass_live = live;
+            st->pass_live = c->passes <= (uint32_t)kRoundLog ? c->h_ctr->pass_live : 0;  // (no-op passes add 0)
         }
     }
     return DV_OK;
@@ -1034,6 +1082,7 @@ constexpr bool kAsyncSpeculate = false;
 constexpr uint64_t kAsyncSmallAcc = 2u << 20;
 
 uint32_t async_thresh(dv_ctx *c) {
+    if (c->v_thresh) return std::min<uint32_t>(c->v_thresh, async_try_limit(c->async_g));
     const uint64_t frac = c->n_acc <= kAsyncSmallAcc ? c->n_acc : (uint64_t)(kAsyncLiveFrac * (double)c->n_acc);
     return (uint32_t)std::min<uint64_t>(frac, async_try_limit(c->async_g));
 }
@@ -1041,15 +1090,16 @@ uint32_t async_thresh(dv_ctx *c) {
 void async_try(dv_ctx *c, uint32_t r0) {
     c->async_launched++;
     round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, async_thresh(c),
-                c->abounds, c->tword, c->n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks);
+                c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks);
 }
 
-// resume: continue after an asynchronous launch that yielded (dv_epoch_finish)
-// from the round it started at, without further asynchronous tries
+// resume: continue after an asynchronous launch that yielded or declined
+// (dv_epoch_finish) from the round it started at, without further
+// asynchronous tries
 int run_rounds(dv_ctx *c, bool resume) {
     if (!resume) __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
-    uint32_t prev = c->n_txn + 1, seen = resume ? pub_round(c, nullptr) : 0;
+    uint32_t prev = c->v_n_txn + 1, seen = resume ? pub_round(c, nullptr) : 0;
     uint32_t tail_r0 = 0;             // round the pending tail launch starts at (0: none)
     const uint32_t cap = tail_cap(c->el32);
     uint32_t tail_limit = kTailTryFactor * cap;  // published live count that triggers a try
@@ -1105,10 +1155,200 @@ int run_rounds(dv_ctx *c, bool resume) {
     }
 }
 
+// ---- prefix-kill epochs (dvcc_prefix.hip) ----------------------------------
+// Epochs from kPrefixMinTxn txns up; the prefix is ~1/64 of the epoch, at
+// least kPrefixMin txns (config D: 16,384 of 1,048,576, whose commits kill
+// ~91 % of the later txns).
+constexpr uint32_t kPrefixMinTxn = 1u << 17;
+constexpr uint32_t kPrefixMin = 4096, kPrefixMax = 1u << 16;
+
+uint32_t prefix_size(const dv_ctx *c, uint32_t n_txn) {
+    if (c->prefix_txns) return c->prefix_txns;
+    return std::min(kPrefixMax, std::max(kPrefixMin, n_txn / 64));
+}
+
+bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {
+    if (c->cfg.cc_alg == DV_CALVIN || c->cfg.workload != DV_YCSB) return false;
+    if (c->prefix_txns == ~0u) return false;  // dv_set_prefix: off
+    if (ep->n_txn < (c->prefix_txns ? 2 : kPrefixMinTxn)) return false;
+    return prefix_size(c, ep->n_txn) < ep->n_txn;
+}
+
+// The rounds of one stage: round 0, then every remaining decision in one
+// asynchronous launch (stages are small: a declined or yielded try halts and
+// the synchronous rounds resume), or the pipelined loop when asynchronous
+// rounds are off.
+int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
+    c->rounds = 0;
+    c->rounds_real = 0;
+    c->async_unconfirmed = false;
+    c->el32 = round_el32(c->v_n_txn, c->slog) && !(c->cfg.flags & DV_FLAG_EL64);
+    c->live_ub = n_acc_ub;
+    c->und_ub = c->v_n_txn;
+    rounds_epoch_init(c->stream, round_bufs(c), n_acc_ub, c->v_n_txn, (c->v_n_txn + 3u) & ~3u, n_acc_dev);
+    __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
+    __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
+    const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
+    if (!async) return run_rounds(c, false);
+    c->v_thresh = async_try_limit(c->async_g);  // whatever fits the workgroups
+    enqueue_round(c, nullptr, true);
+    async_try(c, 1);
+    c->async_unconfirmed = true;
+    return hip_fail(hipGetLastError(), "stage rounds");
+}
+
+// the outcome of the asynchronous try at round r0 (RoundPub::tl codes 2-5)
+int wait_try(dv_ctx *c, uint32_t r0, uint32_t *code) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0;; i++) {
+        const unsigned long long tl = __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(tl >> 32) == r0 && (uint32_t)tl >= 2u) {
+            *code = (uint32_t)tl;
+            return DV_OK;
+        }
+        if ((i & 255) == 255) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {
+                const unsigned long long t2 = __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE);
+                if ((uint32_t)(t2 >> 32) == r0 && (uint32_t)t2 >= 2u) {
+                    *code = (uint32_t)t2;
+                    return DV_OK;
+                }
+                return DV_ERR_STATE;
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "stage stream");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
+        }
+        __builtin_ia32_pause();
+    }
+}
+
+// a stage whose decisions the next kernels need: wait for its try, finish it
+// synchronously if the try declined or yielded; returns its rounds
+int stage_complete(dv_ctx *c, uint32_t *rounds) {
+    *rounds = c->rounds_real ? c->rounds_real : c->rounds;
+    if (!c->async_unconfirmed) return DV_OK;
+    uint32_t code = 0;
+    int r = wait_try(c, 1, &code);
+    if (r) return r;
+    c->async_unconfirmed = false;
+    if (code == 4u) {
+        *rounds = 1 + (uint32_t)__atomic_load_n(&c->h_pub->ai, __ATOMIC_ACQUIRE);
+        return DV_OK;
+    }
+    if (code == 5u) {  // round 0 decided everything (or the epoch is rejected)
+        *rounds = 1;
+        return DV_OK;
+    }
+    HIPCHK(hipMemsetAsync(&c->ctr->halt, 0, sizeof(uint32_t), c->stream));
+    r = run_rounds(c, true);
+    *rounds = c->rounds_real;
+    return r;
+}
+
+// Probe -> prefix: sort + rounds -> kill + compaction -> survivors: sort +
+// rounds; dv_epoch_finish then maps the survivors' decisions back and
+// executes.  Only the prefix and the survivors are ever sorted.
+int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
+    const uint32_t *err_seed = c->err_seed;
+    c->err_seed = nullptr;
+    int r = epoch_setup(c, ep);
+    if (r) return r;
+    const uint32_t K = prefix_size(c, ep->n_txn);
+    const uint32_t T = c->cfg.max_txn;
+    if (!c->row_state || c->row_state_cap < c->total_rows) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        dfree(c->row_state);
+        c->row_state = nullptr;
+        c->row_state_cap = 0;
+        r = dalloc(&c->row_state, c->total_rows);
+        if (!r) r = hip_fail(hipMemsetAsync(c->row_state, 0, c->total_rows, c->stream), "memset");
+        if (r) return r;
+        c->row_state_cap = c->total_rows;
+    }
+    if (!c->b_status) {
+        r = dalloc(&c->b_status, (T + 3u) & ~3u);
+        if (!r) r = dalloc(&c->b_tlen, (T + 3u) & ~3u);
+        if (!r) r = dalloc(&c->b_map, T);
+        if (!r) {
+            c->kdesc_n = kill_tiles(T) + 1;
+            r = dalloc(&c->kdesc, 2ull * c->kdesc_n);
+        }
+        if (!r) r = hip_fail(hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream), "memset");
+        if (r) return r;
+    }
+    const bool nowait = c->cfg.cc_alg != DV_OCC;
+    const int key_bits = bits_for(c->total_rows);
+    c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
+    c->prefix_mode = true;
+    rec(c, 0);
+    launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
+                       c->tile_ctr, err_seed, c->ctr);
+    c->ticket = 0;
+    launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
+                 c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K);
+    rec(c, 1);
+    // the prefix: txns [0, K), the first ctr->a_acc accesses
+    const uint32_t ub_a = (uint32_t)std::min<uint64_t>(ep->n_acc, (uint64_t)K * (ep->max_txn_acc ? ep->max_txn_acc
+                                                                                                    : kMaxPos));
+    c->sorted = radix_sort_rows(c->stream, c->pairs, ub_a, key_bits, c->counts, c->digit_tot,
+                                ktiming(c) ? c->sev : nullptr, false, &c->ctr->a_acc);
+    rec(c, 2);
+    c->v_status = c->status;
+    c->v_tlen = c->tlen;
+    c->v_n_txn = K;
+    c->v_n_txn_dev = nullptr;
+    c->phase = 1;
+    r = stage_rounds(c, &c->ctr->a_acc, ub_a);
+    if (!r) r = stage_complete(c, &c->rounds_prefix);
+    if (r) {
+        (void)hipStreamSynchronize(c->stream);
+        c->phase = 0;
+        c->prefix_mode = false;
+        return r;
+    }
+    // kill the later txns that conflict with the prefix's commits; the
+    // survivors become a sub-epoch (sort keys into pairs[0], A is done with it)
+    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, nowait, 0, c->ctr);
+    const uint32_t tag = next_tag(c);
+    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, ep->acc_txn, ep->n_acc, K, c->n_txn,
+                        c->row_state, nowait, c->status,
+                        c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc, c->kdesc + c->kdesc_n,
+                        next_ticket(c), tag, c->ctr);
+    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, nowait, 1, c->ctr);
+    // the survivors: renumbered 0..S-1, counts on the device
+    c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot, nullptr, false,
+                                &c->ctr->b_acc);
+    c->v_status = c->b_status;
+    c->v_tlen = c->b_tlen;
+    c->v_n_txn = c->n_txn - K;
+    c->v_n_txn_dev = &c->ctr->b_txn;
+    r = stage_rounds(c, &c->ctr->b_acc, (uint32_t)ep->n_acc);
+    if (r) {
+        (void)hipStreamSynchronize(c->stream);
+        c->phase = 0;
+        c->prefix_mode = false;
+    }
+    return r;
+}
+
 }  // namespace
+
+int dv_set_prefix(dv_ctx *c, uint32_t prefix_txns) {
+    if (!c) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    c->prefix_txns = prefix_txns;
+    return DV_OK;
+}
 
 int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, uint32_t *d_grant,
                         dv_stats *st) {
+    if (c && ep && prefix_applies(c, ep)) {
+        HIPCHK(hipSetDevice(c->cfg.device));
+        const int r = run_prefix_epoch(c, ep);
+        if (r) return r;
+        return dv_epoch_finish(c, d_commit, st);
+    }
     int r = dv_epoch_begin(c, ep, d_grant);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {

@@ -132,6 +132,7 @@ SIGNATURES = [
     ("dv_epoch_errors_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_errors_combined", ctypes.c_int, [_vp, _vp]),
     ("dv_set_async_limits", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32]),
+    ("dv_set_prefix", ctypes.c_int, [_vp, ctypes.c_uint32]),
     ("dv_ycsb_gen", ctypes.c_int, [_P(YcsbParams), ctypes.c_uint64, ctypes.c_uint32,
                                    ctypes.c_uint32, _vp, _vp, _vp]),
     ("dv_tpcc_table_rows", ctypes.c_int, [_P(TpccParams), ctypes.c_uint32, ctypes.c_uint32,

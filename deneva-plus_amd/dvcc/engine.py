@@ -187,6 +187,12 @@ class CCEngine:
         or idle_us without a decision (0 = defaults); testing knob."""
         L.check(L.lib().dv_set_async_limits(self._ctx, max_iters, idle_us), "dv_set_async_limits")
 
+    def set_prefix(self, prefix_txns=0):
+        """Prefix-kill decisions (dv_set_prefix): 0 automatic, None off, or
+        the prefix size in txns."""
+        v = 0xFFFFFFFF if prefix_txns is None else int(prefix_txns)
+        L.check(L.lib().dv_set_prefix(self._ctx, v), "dv_set_prefix")
+
     def set_timing(self, timing):
         """Between epochs: True = per-stage events, "kernel" = only the scatter
         and pass launches' dispatch timestamps, False = none."""

@@ -309,6 +309,15 @@ int dv_epoch_errors_combined(dv_ctx *ctx, const uint32_t *d_word);
  * epochs; lower values are a testing knob. */
 int dv_set_async_limits(dv_ctx *ctx, uint32_t max_iters, uint32_t idle_us);
 
+/* NO_WAIT / WAIT_DIE / OCC epochs of YCSB from 131,072 txns up (single
+ * partition) are decided prefix first: the first prefix_txns txns on their
+ * own, then every later txn that conflicts with one of their commits aborts at
+ * once, and only the survivors go through the rounds (same decisions;
+ * dvcc_prefix.hip).  prefix_txns: 0 = automatic (n_txn / 64, clamped to
+ * [4096, 65536]), 0xFFFFFFFF = off (every epoch takes the full path), else
+ * that many txns for any epoch longer than it.  Between epochs. */
+int dv_set_prefix(dv_ctx *ctx, uint32_t prefix_txns);
+
 /* diagnostics: per decision round of the last finished epoch, the live
  * accesses entering the round and the undecided txns before it; returns the
  * number of rounds logged (at most cap, and at most 64) */

@@ -45,12 +45,17 @@ def _gpu_epoch(eng, e, path):
 
 
 def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False,
-           asynchronous=True):
+           asynchronous=True, prefix=0, async_iters=0):
+    """prefix: dv_set_prefix (0 automatic -- epochs from 131,072 txns --, None
+    off, else the prefix size for every longer epoch)."""
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
                    max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64,
                    asynchronous=asynchronous)
+    eng.set_prefix(prefix)
+    if async_iters:
+        eng.set_async_limits(async_iters, 0)
     eng.load_ycsb_partition(rows)
     assert (eng.read_table(0, rows) == f0).all()
     for e in epochs:
@@ -402,6 +407,54 @@ def test_many_rounds(cc, rows, req, theta, tail, el64, asyn):
     epochs = [gen.gen(20_000, 300 + k) for k in range(2)]
     st = _check(cc, rows, epochs, tail=tail, el64=el64, asynchronous=asyn)
     assert st.rounds >= 2
+
+
+# ---- prefix-kill epochs (dvcc_prefix.hip): the prefix decided alone, later
+# txns conflicting with its commits killed, the survivors decided as a
+# renumbered sub-epoch -- bit-exact against the oracle however the epoch is cut
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("prefix", [1, 17, 500, 4096])
+def test_prefix_kill_sizes(cc, prefix):
+    g = YCSBQueryGenerator(1 << 16, zipf_theta=0.9)
+    _check(cc, 1 << 16, [g.gen(20_000, 61), g.gen(20_000, 62)], prefix=prefix)
+
+
+@pytest.mark.parametrize("knobs", [dict(asynchronous=False), dict(tail=False, asynchronous=False),
+                                   dict(el64=True), dict(async_iters=1), dict(async_iters=2)])
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_prefix_kill_knobs(cc, knobs):
+    """the stages' rounds on every decision path: pipelined passes, no tail,
+    64-bit elements, asynchronous launches forced to yield (both stages then
+    resume synchronously)"""
+    g = YCSBQueryGenerator(1 << 18, zipf_theta=0.95, req_per_query=12)
+    _check(cc, 1 << 18, [g.gen(30_000, 71)], prefix=2000, **knobs)
+
+
+@pytest.mark.parametrize("theta", [0.0, 0.5, 0.99])
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_prefix_kill_automatic(cc, theta):
+    """the default cut of a 131,072-txn epoch, uniform to very skewed keys
+    (uniform: the kill removes little, the survivors' sub-epoch is most of
+    the epoch)"""
+    g = YCSBQueryGenerator(1 << 20, zipf_theta=theta)
+    _check(cc, 1 << 20, [g.gen(131_072, 81)])
+
+
+def test_prefix_kill_repeated_rows():
+    rng = np.random.default_rng(5)
+    n_txn = 6000
+    lens = rng.integers(1, 11, size=n_txn)
+    tb = np.zeros(n_txn + 1, np.uint32)
+    tb[1:] = np.cumsum(lens)
+    n = int(tb[-1])
+    keys = np.where(rng.random(n) < 0.8, rng.integers(0, 64, size=n), rng.integers(0, 4096, size=n))
+    for t in range(0, n_txn, 2):
+        a, b = int(tb[t]), int(tb[t + 1])
+        if b - a >= 2:
+            keys[b - 1] = keys[a]
+    e = Epoch(keys.astype(np.uint64), (rng.random(n) < 0.5).astype(np.uint8), tb)
+    for cc in (dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC):
+        _check(cc, 4096, [e], prefix=300)
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
