@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--mpr-sweep", default="0,0.1,0.2,0.3,0.4,0.5",
                     help="N>1: config D's MPR values, each a short extra run ('' = none)")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the 1,048,576-txn-per-GPU run")
+    ap.add_argument("--prefix", type=int, default=0,
+                    help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -453,6 +455,7 @@ def main():
         epochs = gen_epochs(gen, n_txn_total, 0, n_epochs)
         t_gen = time.perf_counter() - t_gen
         eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
+        eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.load_ycsb_partition(rows)
         deps = [dvcc.DeviceEpoch(e) for e in epochs]
         d_commit = torch.zeros(n_txn_total, dtype=torch.uint8, device="cuda")

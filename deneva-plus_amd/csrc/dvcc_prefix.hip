@@ -11,34 +11,42 @@
 // sub-epoch decided by the same rounds, over ~9 % of the accesses.  The
 // runtime (dvcc_runtime.hip, run_prefix_epoch) therefore runs
 //     probe (sort keys for the prefix only) -> sort + rounds on the prefix ->
-//     k_prefix_mark -> k_kill_compact -> k_prefix_mark (clear) ->
+//     k_prefix_mark -> k_kill -> k_kill_compact ->
 //     sort + rounds on the survivors -> k_sub_scatter_back -> execution,
 // instead of sorting and scanning every access of the epoch round after round.
 //
-// Row state of the prefix's committed txns (one byte per row of the context):
-//   2  a committed txn writes the row
-//   1  (NO_WAIT / WAIT_DIE) a committed txn reads it
+// Row state of the prefix's committed txns: a bitmap of 2 bits per row of the
+// context (16 rows per 32-bit word; config D's 16.8M rows take 4 MiB, one
+// XCD's L2), cleared before every prefix epoch:
+//   bit 1  a committed txn writes the row
+//   bit 0  (NO_WAIT / WAIT_DIE) a committed txn reads it
 // A later access conflicts with it exactly as Row_lock::lock_get's
 // conflict_lock would with the committed owners (row_lock.cpp:69, 86-90): a
-// write meets 1 or 2, a read meets 2; OCC's central validation
+// write meets either bit, a read meets bit 1; OCC's central validation
 // (occ.cpp:185-199) kills any access to a row an earlier committed txn writes.
-// Two committed 2PL txns never hold one row as reader and writer, so the plain
-// byte stores below never race on different values.
 #include "dvcc_common.h"
 
 namespace dvcc {
 
 namespace {
-constexpr int kKillIPT = 8;  // txns per thread
+constexpr int kKillIPT = 8;                             // txns per thread in k_kill_compact
+constexpr uint32_t kKillTile = kBlock * kKillIPT;       // txns per tile
+constexpr uint32_t RS_RD = 1u, RS_WR = 2u;
+
+__device__ __forceinline__ uint32_t row_bits(const uint32_t *rs, uint32_t row) {
+    return (rs[row >> 4] >> ((row & 15u) * 2u)) & 3u;
+}
 }  // namespace
 
-// mark (clear = 0) or clear (clear = 1) the rows of the committed prefix txns;
-// lane per txn, its accesses from the probe's txn-major acc_row
+uint64_t row_state_words(uint64_t rows) { return (rows + 15) / 16; }
+
+// the rows of the committed prefix txns into the bitmap; lane per txn, its
+// accesses from the probe's txn-major acc_row
 __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restrict__ status,
                                                         const uint32_t *__restrict__ tb_start,
                                                         const uint32_t *__restrict__ tb_end,
                                                         const uint32_t *__restrict__ acc_row, uint32_t K,
-                                                        uint8_t *__restrict__ row_state, int nowait, int clear,
+                                                        uint32_t *__restrict__ row_state, int nowait,
                                                         const Counters *__restrict__ ctr) {
     if (input_err(ctr)) return;
     for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < K; t += gridDim.x * kBlock) {
@@ -46,9 +54,8 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
         for (uint32_t a = tb_start[t], e = tb_end[t]; a < e; a++) {
             const uint32_t ar = acc_row[a];
             const uint32_t row = ar & ~AR_WR;
-            if (clear) row_state[row] = 0;
-            else if (ar & AR_WR) row_state[row] = 2;
-            else if (nowait) row_state[row] = 1;
+            const uint32_t bit = (ar & AR_WR) ? RS_WR : (nowait ? RS_RD : 0u);
+            if (bit) atomicOr(&row_state[row >> 4], bit << ((row & 15u) * 2u));
         }
     }
 }
@@ -56,11 +63,11 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
 // Every access after the prefix's (index >= ctr->a_acc) against the row
 // state: a conflict aborts its txn (a plain byte store; the txn's other
 // killed accesses store the same byte).  Access-parallel and coalesced: the
-// txn-major acc_row and the epoch's acc_txn streamed, one byte gathered per
-// access from the row state (the hot rows' bytes stay in L2).
+// txn-major acc_row and the epoch's acc_txn streamed, one word gathered per
+// access from the bitmap.
 __global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ acc_row,
                                                  const uint32_t *__restrict__ acc_txn, uint64_t n,
-                                                 const uint8_t *__restrict__ row_state, int nowait,
+                                                 const uint32_t *__restrict__ row_state, int nowait,
                                                  uint8_t *__restrict__ status, const Counters *__restrict__ ctr) {
     if (input_err(ctr)) return;
     const uint64_t first = ctr->a_acc;
@@ -76,8 +83,8 @@ __global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ ac
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             if (i0 + j >= n) continue;
-            const uint8_t s = row_state[ar[j] & ~AR_WR];
-            if (s == 2 || (nowait && s == 1 && (ar[j] & AR_WR))) status[tx[j]] = ST_ABORT;
+            const uint32_t s = row_bits(row_state, ar[j] & ~AR_WR);
+            if ((s & RS_WR) || (nowait && s && (ar[j] & AR_WR))) status[tx[j]] = ST_ABORT;
         }
     }
 }
@@ -86,21 +93,21 @@ __global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ ac
 // 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
 // and their sort keys written densely in that order, pairs_b = row << 32 |
 // sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
-// their layout).  One launch: tiles of kBlock x kKillIPT txns taken by ticket,
-// two decoupled look-backs (survivors, their accesses) give every tile its
-// output offsets; the last tile publishes S and the access count (b_txn,
-// b_acc) for the kernels that follow.
+// their layout).  One launch: tiles of kKillTile txns taken by ticket, two
+// decoupled look-backs (survivors, their accesses) give every tile its output
+// offsets; the tile's survivors are listed in LDS and their accesses written
+// by the whole block, one access per thread (no serial per-txn loops).  The
+// last tile publishes S and the access count (b_txn, b_acc).
 __global__ __launch_bounds__(kBlock) void k_kill_compact(
     const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
     const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint8_t *__restrict__ status,
-    uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
-    uint8_t *__restrict__ tlen_b,
+    uint32_t *__restrict__ map, uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b,
     uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
     Counters *ctr) {
     __shared__ uint32_t s_tile;
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
-    __shared__ Agg s_pre_c, s_pre_a;
-    constexpr uint32_t kKillTile = kBlock * kKillIPT;
+    __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
+    __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
     if (blockIdx.x >= ntiles || input_err(ctr)) return;  // (b_txn = b_acc = 0 from the epoch clear)
@@ -111,17 +118,12 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     const uint32_t first = K + tile * kKillTile + tid * kKillIPT;
     uint32_t surv = 0, cnt = 0, acc = 0;
     uint32_t a0s[kKillIPT], lens[kKillIPT];
-    // the status bytes of the thread's 8 consecutive txns: two 4-byte loads
-    // when aligned (first is a multiple of 8 past K, K is not)
-    uint8_t st[kKillIPT];
-#pragma unroll
-    for (int j = 0; j < kKillIPT; j++) st[j] = first + j < n_txn ? status[first + j] : (uint8_t)ST_ABORT;
 #pragma unroll
     for (int j = 0; j < kKillIPT; j++) {
         const uint32_t t = first + j;
         a0s[j] = 0;
         lens[j] = 0;
-        if (st[j] != ST_UNDEC) continue;  // killed (k_kill), or past the end
+        if (t >= n_txn || status[t] != ST_UNDEC) continue;  // past the end, or killed (k_kill)
         const uint32_t a0 = tb_start[t], a1 = tb_end[t];
         a0s[j] = a0;
         lens[j] = a1 - a0;
@@ -145,34 +147,53 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         const Agg pc = look_back<OpPlain>(desc_c, tile, tag, bc, lane, ctr);
         const Agg pa = look_back<OpPlain>(desc_a, tile, tag, ba, lane, ctr);
         if (lane == 0) {
-            s_pre_c = pc;
-            s_pre_a = pa;
+            s_sub0 = pc.c;
+            s_ab0 = pa.c;
+            s_nsurv = bc.c;
+            s_nacc = ba.c;
             if (tile == ntiles - 1) {
                 ctr->b_txn = pc.c + bc.c;
                 ctr->b_acc = pa.c + ba.c;
             }
         }
     }
-    __syncthreads();
-    uint32_t sub = s_pre_c.c, ab = s_pre_a.c;
+    // this thread's survivors: their slots in the tile's list
+    uint32_t ls = 0, la = 0;
     for (uint32_t w = 0; w < wave; w++) {
-        sub += wt_c[w].c;
-        ab += wt_a[w].c;
+        ls += wt_c[w].c;
+        la += wt_a[w].c;
     }
-    sub += wave_excl_from_incl<OpPlain>(inc_c, lane).c;
-    ab += wave_excl_from_incl<OpPlain>(inc_a, lane).c;
+    ls += wave_excl_from_incl<OpPlain>(inc_c, lane).c;
+    la += wave_excl_from_incl<OpPlain>(inc_a, lane).c;
+    __syncthreads();
+    const uint32_t sub0 = s_sub0;
 #pragma unroll
     for (int j = 0; j < kKillIPT; j++) {
         if (!((surv >> j) & 1u)) continue;
+        const uint32_t sub = sub0 + ls;
         map[sub] = first + j;
         tlen_b[sub] = (uint8_t)lens[j];
         status_b[sub] = ST_UNDEC;
-        for (uint32_t q = 0; q < lens[j]; q++) {
-            const uint32_t ar = acc_row[a0s[j] + q];
-            pairs_b[ab + q] = pair_pack(ar & ~AR_WR, sub, q, ar >> 31);
+        l_a0[ls] = a0s[j];
+        l_pre[ls] = la;
+        la += lens[j];
+        ls++;
+    }
+    if (tid == 0) l_pre[s_nsurv] = s_nacc;
+    __syncthreads();
+    // the survivors' sort keys: one access per thread, its survivor found by
+    // binary search over the access prefix
+    const uint32_t ns = s_nsurv, na = s_nacc, ab0 = s_ab0;
+    for (uint32_t g = tid; g < na; g += kBlock) {
+        uint32_t lo = 0, hi = ns;  // largest k with l_pre[k] <= g
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (l_pre[mid] <= g) lo = mid;
+            else hi = mid;
         }
-        ab += lens[j];
-        sub++;
+        const uint32_t q = g - l_pre[lo];
+        const uint32_t ar = acc_row[l_a0[lo] + q];
+        pairs_b[ab0 + g] = pair_pack(ar & ~AR_WR, sub0 + lo, q, ar >> 31);
     }
 }
 
@@ -194,18 +215,18 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 }  // namespace
 
 void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
-                        const uint32_t *acc_row, uint32_t K, uint8_t *row_state, int nowait, int clear,
+                        const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
                         const Counters *ctr) {
+    (void)hipMemsetAsync(row_state, 0, rs_words * 4, s);
     if (!K) return;
-    k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, nowait, clear,
-                                                     ctr);
+    k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, nowait, ctr);
 }
 
-uint32_t kill_tiles(uint32_t n_after) { return (n_after + kBlock * kKillIPT - 1) / (kBlock * kKillIPT); }
+uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKillTile; }
 
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
                          const uint32_t *acc_txn, uint64_t n_acc, uint32_t K, uint32_t n_txn,
-                         const uint8_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
+                         const uint32_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
                          uint8_t *tlen_b, uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr,
                          uint32_t tag, Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);

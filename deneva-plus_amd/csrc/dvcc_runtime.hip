@@ -122,8 +122,8 @@ struct dv_ctx {
     uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 64)
     bool prefix_mode = false;     // the epoch in flight is one
     uint32_t rounds_prefix = 0;   // rounds the prefix took
-    uint8_t *row_state = nullptr; // per row: the prefix's committed readers (1) / writers (2)
-    uint64_t row_state_cap = 0;
+    uint32_t *row_state = nullptr; // 2 bits per row: the prefix's committed readers / writers
+    uint64_t row_state_cap = 0;    // (words)
     uint8_t *b_status = nullptr, *b_tlen = nullptr;  // the survivors' sub-epoch (txn capacity)
     uint32_t *b_map = nullptr;                      // survivor -> txn
     uint64_t *kdesc = nullptr;                      // k_kill_compact look-back descriptors (2 arrays)
@@ -1256,15 +1256,15 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     if (r) return r;
     const uint32_t K = prefix_size(c, ep->n_txn);
     const uint32_t T = c->cfg.max_txn;
-    if (!c->row_state || c->row_state_cap < c->total_rows) {
+    const uint64_t rs_words = row_state_words(c->total_rows);
+    if (!c->row_state || c->row_state_cap < rs_words) {
         HIPCHK(hipStreamSynchronize(c->stream));
         dfree(c->row_state);
         c->row_state = nullptr;
         c->row_state_cap = 0;
-        r = dalloc(&c->row_state, c->total_rows);
-        if (!r) r = hip_fail(hipMemsetAsync(c->row_state, 0, c->total_rows, c->stream), "memset");
+        r = dalloc(&c->row_state, rs_words);
         if (r) return r;
-        c->row_state_cap = c->total_rows;
+        c->row_state_cap = rs_words;
     }
     if (!c->b_status) {
         r = dalloc(&c->b_status, (T + 3u) & ~3u);
@@ -1309,13 +1309,13 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     }
     // kill the later txns that conflict with the prefix's commits; the
     // survivors become a sub-epoch (sort keys into pairs[0], A is done with it)
-    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, nowait, 0, c->ctr);
+    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
+                       c->ctr);
     const uint32_t tag = next_tag(c);
     launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, ep->acc_txn, ep->n_acc, K, c->n_txn,
                         c->row_state, nowait, c->status,
                         c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc, c->kdesc + c->kdesc_n,
                         next_ticket(c), tag, c->ctr);
-    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, nowait, 1, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot, nullptr, false,
                                 &c->ctr->b_acc);
