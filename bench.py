@@ -71,7 +71,9 @@ def parse():
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
     ap.add_argument("--tpcc-only", action="store_true", help="run and print only the TPC-C leg (profiling)")
     ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
-    ap.add_argument("--tpcc-txns", type=int, default=65536, help="txns per TPC-C epoch")
+    ap.add_argument("--tpcc-txns", default="65536,10000",
+                    help="txns per TPC-C epoch, comma-separated (the first is the leg's line; 10000 is the "
+                         "reference's concurrency window, 8 nodes x 1250 in-flight txns)")
     ap.add_argument("--timing", choices=["full", "kernel", "off"], default="off",
                     help="engine timing inside the timed region: per-stage events, only the "
                          "scatter/pass dispatch timestamps, or none (default: the timed region "
@@ -162,50 +164,58 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
     remote customer 15 %, remote item 1 %), this GPU's share of 256
     warehouses (32), full item / customer counts; a step = one epoch of
     --tpcc-txns txns through last-name lookup -> probe -> sort -> decide ->
-    execute, epochs resident in HBM.  Beside it the oracle (single thread)
-    on one of the same epochs."""
+    execute, epochs resident in HBM.  The first size is the leg's line; each
+    further size (the reference's 10,000-txn window) is reported under
+    "window_<n>".  Beside the first size the oracle (single thread) on one of
+    the same epochs."""
     from dvcc import tpcc as T
     p = T.tpcc_params(a.tpcc_wh)
-    n_txn = a.tpcc_txns
-    eps = [T.gen(p, n_txn, dvcc.epoch_seed(0, e)) for e in range(2)]
-    out = {"workload": f"TPC-C config E share: {a.tpcc_wh} warehouses/GPU, {n_txn}-txn epochs, "
-                       "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
-           "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
-    for cc_name in cc_names:
-        eng = T.TpccEngine(cc_name, p, n_txn, seed=1)
-        dev = [T.device_epoch(e) for e in eps]
-        d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
-        d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
-        k = max(a.steps, 5)
-        for i in range(a.warmup):
-            eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        sts = [eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid) for i in range(k)]
-        torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        committed = sum(s.committed for s in sts)
-        byts = sum(tpcc_bytes_per_txn(eps[i % 2]) for i in range(k))
-        out[cc_name] = {"committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el,
-                        "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_txn),
-                        "epochs": k, "epoch_roofline": {"achieved_GBps": byts / el / 1e9,
-                                                        "frac": byts / el / 1e9 / HBM_PEAK_GBPS}}
-        eng.close()
-    if not a.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import _oracle as O
-        po = O.tpcc_params(a.tpcc_wh)
-        e = eps[0]
+    sizes = [int(x) for x in str(a.tpcc_txns).split(",") if x]
+    out = {}
+    for si, n_txn in enumerate(sizes):
+        eps = [T.gen(p, n_txn, dvcc.epoch_seed(0, e)) for e in range(2)]
+        res = {"workload": f"TPC-C config E share: {a.tpcc_wh} warehouses/GPU, {n_txn}-txn epochs, "
+                           "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
+               "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
         for cc_name in cc_names:
-            db = O.TpccDB(po, 1)
-            cc = {"WAIT_DIE": O.WAIT_DIE, "CALVIN": O.CALVIN, "NO_WAIT": O.NO_WAIT, "OCC": O.OCC}[cc_name]
+            eng = T.TpccEngine(cc_name, p, n_txn, seed=1)
+            dev = [T.device_epoch(e) for e in eps]
+            d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+            d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
+            k = max(a.steps, 5) if si == 0 else max(a.steps, 20)
+            for i in range(a.warmup):
+                eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid)
+            torch.cuda.synchronize()
             t0 = time.perf_counter()
-            commit, _, st = db.epoch(cc, e.keys, e.types, e.tables, e.args, e.txn_begin)
+            sts = [eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid) for i in range(k)]
+            torch.cuda.synchronize()
             el = time.perf_counter() - t0
-            out[cc_name]["cpu_baseline"] = {
-                "value": st.committed / el, "unit": "committed txns/s", "cores": 1, "kind": "port",
-                "sample": f"oracle (tpcc.c, E-schedule {cc_name}) on 1 epoch of {n_txn} txns of this "
-                          f"workload in {el:.2f} s on 1 host core; restatement, not the reference binary"}
+            committed = sum(s.committed for s in sts)
+            byts = sum(tpcc_bytes_per_txn(eps[i % 2]) for i in range(k))
+            res[cc_name] = {"committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el,
+                            "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_txn),
+                            "epochs": k, "epoch_roofline": {"achieved_GBps": byts / el / 1e9,
+                                                            "frac": byts / el / 1e9 / HBM_PEAK_GBPS}}
+            eng.close()
+        if si == 0 and not a.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import _oracle as O
+            po = O.tpcc_params(a.tpcc_wh)
+            e = eps[0]
+            for cc_name in cc_names:
+                db = O.TpccDB(po, 1)
+                cc = {"WAIT_DIE": O.WAIT_DIE, "CALVIN": O.CALVIN, "NO_WAIT": O.NO_WAIT, "OCC": O.OCC}[cc_name]
+                t0 = time.perf_counter()
+                commit, _, st = db.epoch(cc, e.keys, e.types, e.tables, e.args, e.txn_begin)
+                el = time.perf_counter() - t0
+                res[cc_name]["cpu_baseline"] = {
+                    "value": st.committed / el, "unit": "committed txns/s", "cores": 1, "kind": "port",
+                    "sample": f"oracle (tpcc.c, E-schedule {cc_name}) on 1 epoch of {n_txn} txns of this "
+                              f"workload in {el:.2f} s on 1 host core; restatement, not the reference binary"}
+        if si == 0:
+            out.update(res)
+        else:
+            out[f"window_{n_txn}"] = res
     return out
 
 

@@ -35,16 +35,33 @@
 
 namespace dvcc {
 
-// ---- owner split: per-block owner counts, then a stable scatter of records
-__global__ __launch_bounds__(kBlock) void k_owner_count(const uint64_t *__restrict__ keys, uint64_t n,
+// flags word of the argument vote (element-wise MAX across ranks)
+constexpr uint32_t kVoteBadArg = 1u, kVoteOverflow = 2u;
+
+// ---- owner split: per-block owner counts, then a stable scatter of records.
+// The owner of an access is key % PART_CNT (YCSB), or the caller's per-access
+// owner byte (TPC-C: the warehouse's partition, TPCCWorkload::wh_to_part,
+// tpcc_helper.cpp:101-104); an owner byte >= PART_CNT is an argument error,
+// voted like the others (xvote[1]) -- the access counts as rank 0's meanwhile.
+__device__ __forceinline__ uint32_t owner_of(const uint64_t *keys, const uint8_t *own, uint64_t i, uint32_t P,
+                                             uint32_t *bad) {
+    if (!own) return (uint32_t)(keys[i] % P);
+    const uint32_t o = own[i];
+    if (o < P) return o;
+    atomicOr(bad, kVoteBadArg);
+    return 0u;
+}
+
+__global__ __launch_bounds__(kBlock) void k_owner_count(const uint64_t *__restrict__ keys,
+                                                        const uint8_t *__restrict__ own, uint64_t n,
                                                         uint32_t P, uint32_t *__restrict__ counts,
-                                                        uint32_t nb) {
+                                                        uint32_t nb, uint32_t *xvote) {
     __shared__ uint32_t c[kRadix];
     for (uint32_t o = threadIdx.x; o < kRadix; o += kBlock) c[o] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kTile;
     for (uint32_t j = threadIdx.x; j < (uint32_t)kTile; j += kBlock)
-        if (base + j < n) atomicAdd(&c[(uint32_t)(keys[base + j] % P)], 1u);
+        if (base + j < n) atomicAdd(&c[owner_of(keys, own, base + j, P, &xvote[1])], 1u);
     __syncthreads();
     for (uint32_t o = threadIdx.x; o < P; o += kBlock) counts[(uint64_t)o * nb + blockIdx.x] = c[o];
 }
@@ -69,14 +86,20 @@ __global__ __launch_bounds__(kBlock) void k_owner_scan(uint32_t *__restrict__ co
 }
 
 // record i of the batch -> its owner's segment, in batch order (stable: a
-// wave walks 64 consecutive records per step, ranks by ballot)
+// wave walks 64 consecutive records per step, ranks by ballot); TPC-C
+// records carry their table, and their operation words go the same way into
+// args_out
 __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__restrict__ keys,
                                                           const uint8_t *__restrict__ types,
                                                           const uint32_t *__restrict__ acc_txn,
+                                                          const uint8_t *__restrict__ own,
+                                                          const uint8_t *__restrict__ tables,
+                                                          const uint64_t *__restrict__ args,
                                                           uint64_t n, uint32_t P, uint32_t txn_base,
                                                           const uint32_t *__restrict__ counts,
                                                           const uint32_t *__restrict__ tot, uint32_t nb,
-                                                          dv_access *__restrict__ out) {
+                                                          dv_access *__restrict__ out,
+                                                          uint64_t *__restrict__ args_out, uint32_t *xvote) {
     __shared__ uint32_t wc[4][kRadix];
     __shared__ uint32_t obase[kRadix];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -90,14 +113,14 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
     for (uint32_t o = tid; o < kRadix; o += kBlock) wc[0][o] = wc[1][o] = wc[2][o] = wc[3][o] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * kTile + wave * (64 * kIPT);
-    uint32_t own[kIPT], r[kIPT];
+    uint32_t own_[kIPT], r[kIPT];
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t o = valid ? (uint32_t)(keys[idx] % P) : 0u;
+        const uint32_t o = valid ? owner_of(keys, own, idx, P, &xvote[1]) : 0u;
         const uint64_t peers = match_digit(o, __ballot(valid));
         const uint32_t before = wc[wave][o];
-        own[j] = o;
+        own_[j] = o;
         r[j] = before + mask_rank(peers);
         if (valid && lane == (uint32_t)__builtin_ctzll(peers)) wc[wave][o] = before + (uint32_t)__popcll(peers);
     }
@@ -105,7 +128,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         if (idx >= n) continue;
-        const uint32_t o = own[j];
+        const uint32_t o = own_[j];
         uint32_t wpre = 0;
         for (uint32_t w = 0; w < wave; w++) wpre += wc[w][o];
         const uint64_t dst = (uint64_t)obase[o] + counts[(uint64_t)o * nb + blockIdx.x] + wpre + r[j];
@@ -113,14 +136,12 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
         a.key = keys[idx];
         a.txn_seq = txn_base + acc_txn[idx];
         a.type = types[idx];
-        a.table = 0;
+        a.table = tables ? tables[idx] : 0;
         a.flags = 0;
         out[dst] = a;
+        if (args_out) args_out[dst] = args[idx];
     }
 }
-
-// flags word of the argument vote (element-wise MAX across ranks)
-constexpr uint32_t kVoteBadArg = 1u, kVoteOverflow = 2u;
 
 // the received record count exceeds this context's capacity: a vote, so every
 // rank leaves together (xvote[1] |= kVoteOverflow)
@@ -155,6 +176,7 @@ struct DvComm {
     uint64_t acc_cap = 0;  // capacity of the record / SoA buffers
     uint32_t nb_cap = 0, txn_cap = 0;
     dv_access *send = nullptr, *recv = nullptr;
+    uint64_t *send_args = nullptr, *recv_args = nullptr;  // TPC-C operation words, routed like the records
     uint64_t *keys = nullptr;
     uint8_t *types = nullptr, *tables = nullptr, *verdict = nullptr;
     uint32_t *txn = nullptr, *counts = nullptr, *tot = nullptr, *err = nullptr;
@@ -207,6 +229,7 @@ struct dvcc::Xport {
     // in place, element-wise MAX
     virtual int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) = 0;
     virtual int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) = 0;
+    virtual int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) = 0;
 };
 
 namespace {
@@ -229,6 +252,9 @@ struct RcclXport final : Xport {
     }
     int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override {
         return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint8, ncclMax, comm, s), "ncclAllReduce");
+    }
+    int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) override {
+        return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint64, ncclMax, comm, s), "ncclAllReduce");
     }
 };
 
@@ -338,14 +364,16 @@ struct LocalXport final : Xport {
     }
     int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
     int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
 };
 
 void free_bufs(DvComm *m) {
-    void *b[] = {m->send, m->recv, m->keys, m->types, m->tables, m->verdict, m->txn,
+    void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
+    m->send_args = m->recv_args = nullptr;
     m->keys = nullptr;
     m->types = m->tables = m->verdict = nullptr;
     m->txn = m->counts = m->tot = m->err = m->xvote = m->gerr = nullptr;
@@ -355,11 +383,15 @@ void free_bufs(DvComm *m) {
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
 // an allocation that fails inside an epoch would leave one rank outside the
 // collectives the others enter
-int reserve(DvComm *m, uint64_t acc, uint32_t txn) {
+int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     const uint32_t nb = nblocks_for(acc ? acc : 1);
     const uint32_t P = (uint32_t)m->nranks;
     CHK(alloc(&m->send, acc));
     CHK(alloc(&m->recv, acc));
+    if (tpcc) {
+        CHK(alloc(&m->send_args, acc));
+        CHK(alloc(&m->recv_args, acc));
+    }
     CHK(alloc(&m->keys, acc));
     CHK(alloc(&m->types, acc));
     CHK(alloc(&m->tables, acc));
@@ -413,7 +445,7 @@ int dv_comm_init(dv_ctx *c, const void *unique_id, int nranks, int rank) {
     slot->x = x;
     int r = nccl_fail(ncclCommInitRank(&x->comm, nranks, id, rank), "ncclCommInitRank");
     if (r) x->comm = nullptr;
-    if (!r) r = reserve(slot, cfg.max_acc, cfg.max_txn);
+    if (!r) r = reserve(slot, cfg.max_acc, cfg.max_txn, cfg.workload == DV_TPCC);
     if (r) {
         comm_free(slot);
         slot = nullptr;
@@ -448,7 +480,7 @@ int dv_comm_init_local(dv_ctx **ctxs, int nranks) {
         x->r = q;
         g->refs++;
         slot->x = x;
-        r = reserve(slot, ctx_config(c).max_acc, ctx_config(c).max_txn);
+        r = reserve(slot, ctx_config(c).max_acc, ctx_config(c).max_txn, ctx_config(c).workload == DV_TPCC);
     }
     if (g->refs == 0) {  // nothing handed out
         for (auto &sl : g->slot) {
@@ -460,41 +492,56 @@ int dv_comm_init_local(dv_ctx **ctxs, int nranks) {
     return r;
 }
 
-int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
-                      dv_stats *st) {
-    // No rank may leave between collectives on its own: arguments are voted
-    // on with the other ranks before anything depends on them, input errors
-    // found by the probe are combined before the rounds (every rank then
-    // reports the error at the same round), and the round loop's own exits
-    // depend only on combined verdicts, identical on every rank.  Only a
-    // missing context or communicator returns at once (no rank of this
-    // communicator can have entered a collective of it).
+}  // extern "C"
+
+namespace {
+
+// The partitioned epoch of one rank (dv_epoch_run_part, dv_tpcc_epoch_run_part).
+// No rank may leave between collectives on its own: arguments are voted on
+// with the other ranks before anything depends on them, input errors found by
+// the probe are combined before the rounds (every rank then reports the error
+// at the same round), and the round loop's own exits depend only on combined
+// verdicts, identical on every rank.  Only a missing context or communicator
+// returns at once (no rank of this communicator can have entered a collective
+// of it).  TPC-C (tpcc): records route by the owner bytes, carry their table
+// and operation word, the epoch runs through dv_tpcc_epoch_begin, and the
+// o_ids -- computed where the district row lives -- are all-reduced (MAX)
+// into every rank's d_oid: Calvin's RFWD of o_id to the other participants
+// (tpcc_txn.cpp:1040, message.cpp:982-1025), for every protocol.
+int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint64_t *args, bool tpcc,
+             uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
     if (!c) return DV_ERR_ARG;
     DvComm *m = ctx_comm(c);
     if (!m) return DV_ERR_STATE;
     const dv_config &cfg = ctx_config(c);
     const uint32_t P = (uint32_t)m->nranks;
     const uint64_t n_txn64 = (uint64_t)txns_per_rank * P;
-    const bool bad = !home || (home->n_acc && (!home->keys || !home->types || !home->acc_txn)) ||
-                     home->n_txn > txns_per_rank || n_txn64 > cfg.max_txn || n_txn64 > m->txn_cap ||
-                     home->n_acc > m->acc_cap || !ctx_has_tables(c);
+    bool bad = !home || (home->n_acc && (!home->keys || !home->types || !home->acc_txn)) ||
+               home->n_txn > txns_per_rank || n_txn64 > cfg.max_txn || n_txn64 > m->txn_cap ||
+               home->n_acc > m->acc_cap || !ctx_has_tables(c) || tpcc != (cfg.workload == DV_TPCC);
+    if (tpcc && !bad) bad = home->n_acc && (!home->tables || !own || !args || !m->send_args);
     const uint32_t n_txn = bad ? 0u : (uint32_t)n_txn64;
     const uint64_t n_home = bad ? 0 : home->n_acc;
     hipStream_t s = ctx_stream(c);
     const uint32_t nb = n_home ? nblocks_for(n_home) : 1;
 
+    // the argument vote: longest txn (sets the verdict-byte stride on every
+    // rank), flags (bad arguments here; owner bytes and capacity below)
+    const uint32_t vote[2] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u};
+    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
     // 1. split the batch by owner (a bad rank sends nothing)
     if (n_home) {
-        k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, n_home, P, m->counts, nb);
+        k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, own, n_home, P, m->counts, nb, m->xvote);
         k_owner_scan<<<P, kBlock, 0, s>>>(m->counts, nb, m->tot);
-        k_owner_scatter<<<nb, kBlock, 0, s>>>(home->keys, home->types, home->acc_txn, n_home, P,
-                                             (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb,
-                                             m->send);
+        k_owner_scatter<<<nb, kBlock, 0, s>>>(home->keys, home->types, home->acc_txn, own,
+                                             tpcc ? home->tables : nullptr, args, n_home, P,
+                                             (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb, m->send,
+                                             tpcc ? m->send_args : nullptr, m->xvote);
     } else {
         CHK(hip_fail2(hipMemsetAsync(m->tot, 0, P * sizeof(uint32_t), s), "memset"));
     }
     CHK(hip_fail2(hipGetLastError(), "owner split"));
-    // 2. counts, the argument vote (longest txn, flags), then the records
+    // 2. counts, the vote, then the records
     std::vector<uint32_t> tot(P);
     CHK(hip_fail2(hipMemcpyAsync(tot.data(), m->tot, P * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
@@ -502,9 +549,6 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
     for (uint32_t o = 0; o < P; o++) sendc[o] = tot[o];
     CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    // the longest txn anywhere sets the verdict-byte stride on every rank
-    const uint32_t vote[2] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u};
-    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
     k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, m->acc_cap), m->xvote);
     CHK(m->x->max_u32(m->xvote, 2, s));
     uint32_t gvote[2] = {0, 0};
@@ -524,6 +568,17 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
     }
     CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->send), sc.data(), sd.data(),
                           reinterpret_cast<uint8_t *>(m->recv), rc.data(), rd.data(), s));
+    if (tpcc) {  // the operation words: the same segments at 8 bytes per record
+        std::vector<size_t> sc8(P), sd8(P), rc8(P), rd8(P);
+        for (uint32_t o = 0; o < P; o++) {
+            sc8[o] = sc[o] / sizeof(dv_access) * 8;
+            sd8[o] = sd[o] / sizeof(dv_access) * 8;
+            rc8[o] = rc[o] / sizeof(dv_access) * 8;
+            rd8[o] = rd[o] / sizeof(dv_access) * 8;
+        }
+        CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->send_args), sc8.data(), sd8.data(),
+                              reinterpret_cast<uint8_t *>(m->recv_args), rc8.data(), rd8.data(), s));
+    }
     CHK(hip_fail2(hipMemsetAsync(m->err, 0, 4, s), "memset"));
     launch_split_access(s, m->recv, n_recv, nullptr, n_txn, m->keys, m->types, m->txn, m->tables, m->err);
     CHK(hip_fail2(hipGetLastError(), "unpack"));
@@ -534,11 +589,15 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
     ep.keys = m->keys;
     ep.types = m->types;
     ep.acc_txn = m->txn;
-    ep.tables = nullptr;
+    ep.tables = tpcc ? m->tables : nullptr;
     ep.n_acc = n_recv;
     ep.n_txn = n_txn;
     ep.max_txn_acc = std::min<uint32_t>(gvote[0], kMaxPos);
-    CHK(dv_epoch_begin(c, &ep, nullptr));
+    if (tpcc) {
+        CHK(dv_tpcc_epoch_begin(c, &ep, m->recv_args, d_oid));
+    } else {
+        CHK(dv_epoch_begin(c, &ep, nullptr));
+    }
     CHK(dv_epoch_errors_local(c, m->gerr));
     CHK(m->x->max_u32(m->gerr, 1, s));
     CHK(dv_epoch_errors_combined(c, m->gerr));
@@ -561,8 +620,26 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
         }
     }
     // 4. execute and report (CALVIN: a rejected epoch executes nothing, and
-    //    every rank reports the combined error)
-    return dv_epoch_finish(c, d_commit, st);
+    //    every rank reports the combined error); the errors are combined, so
+    //    every rank takes the o_id all-reduce or none does
+    const int r = dv_epoch_finish(c, d_commit, st);
+    if (r || !tpcc || !d_oid || !n_txn) return r;
+    CHK(m->x->max_u64(d_oid, n_txn, s));
+    return hip_fail2(hipStreamSynchronize(s), "sync");
+}
+
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
+                      dv_stats *st) {
+    return run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
+}
+
+int dv_tpcc_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, const uint64_t *d_args, const uint8_t *d_owner,
+                           uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
+    return run_part(c, home, d_owner, d_args, true, txns_per_rank, d_commit, d_oid, st);
 }
 
 }  // extern "C"

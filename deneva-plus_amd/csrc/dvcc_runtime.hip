@@ -223,6 +223,18 @@ uint32_t *next_ticket(dv_ctx *c) {
     return &c->tile_ctr[c->ticket++ % kTileCtrs];
 }
 
+// the stable sort of pairs[0][0, n) by row (n_dev: the count on the device,
+// n its upper bound); returns the buffer holding the result.  hist0_done:
+// the probe counted the first pass's tile histogram.  (A one-sweep variant --
+// digit totals in one launch, one scatter launch per pass with a per-digit
+// decoupled look-back -- measured slower here: every tile of these sorts is
+// resident at once, so the look-back became a chain of cross-XCD hand-offs,
+// 167 us of scatters per config-D epoch against 125 us for the three-launch
+// passes.)
+int sort_rows(dv_ctx *c, uint64_t n, int key_bits, hipEvent_t *ev, bool hist0_done, const uint32_t *n_dev) {
+    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev);
+}
+
 Tables make_tables(dv_ctx *c) {
     Tables t{};
     t.n = 0;
@@ -769,8 +781,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
-    c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot,
-                                ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
+    c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
@@ -1093,6 +1104,21 @@ void async_try(dv_ctx *c, uint32_t r0) {
                 c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks);
 }
 
+// Small epochs (a TPC-C epoch, at most kAsyncSmallAcc accesses): round 0,
+// then the asynchronous launch from round 1 with no host wait in between --
+// its slices are a few elements per thread, so it pays from round 1 on.  A
+// declined or yielded try halts execution and dv_epoch_finish resumes the
+// synchronous rounds; larger epochs take the pipelined loop.
+int decide_epoch(dv_ctx *c) {
+    const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
+    if (!async || c->n_acc > kAsyncSmallAcc) return run_rounds(c, false);
+    c->v_thresh = async_try_limit(c->async_g);
+    enqueue_round(c, nullptr, true);
+    async_try(c, 1);
+    c->async_unconfirmed = true;
+    return hip_fail(hipGetLastError(), "rounds");
+}
+
 // resume: continue after an asynchronous launch that yielded or declined
 // (dv_epoch_finish) from the round it started at, without further
 // asynchronous tries
@@ -1291,8 +1317,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     // the prefix: txns [0, K), the first ctr->a_acc accesses
     const uint32_t ub_a = (uint32_t)std::min<uint64_t>(ep->n_acc, (uint64_t)K * (ep->max_txn_acc ? ep->max_txn_acc
                                                                                                     : kMaxPos));
-    c->sorted = radix_sort_rows(c->stream, c->pairs, ub_a, key_bits, c->counts, c->digit_tot,
-                                ktiming(c) ? c->sev : nullptr, false, &c->ctr->a_acc);
+    c->sorted = sort_rows(c, ub_a, key_bits, ktiming(c) ? c->sev : nullptr, false, &c->ctr->a_acc);
     rec(c, 2);
     c->v_status = c->status;
     c->v_tlen = c->tlen;
@@ -1317,8 +1342,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
                         c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc, c->kdesc + c->kdesc_n,
                         next_ticket(c), tag, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
-    c->sorted = radix_sort_rows(c->stream, c->pairs, ep->n_acc, key_bits, c->counts, c->digit_tot, nullptr, false,
-                                &c->ctr->b_acc);
+    c->sorted = sort_rows(c, ep->n_acc, key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
     c->v_tlen = c->b_tlen;
     c->v_n_txn = c->n_txn - K;
@@ -1352,7 +1376,7 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     int r = dv_epoch_begin(c, ep, d_grant);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
-        r = run_rounds(c, false);
+        r = decide_epoch(c);
         if (r) { c->phase = 0; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
@@ -1401,7 +1425,7 @@ int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *
     int r = dv_tpcc_epoch_begin(c, ep, d_args, d_oid);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
-        r = run_rounds(c, false);
+        r = decide_epoch(c);
         if (r) { c->phase = 0; c->tp_args = nullptr; c->tp_oid = nullptr; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);

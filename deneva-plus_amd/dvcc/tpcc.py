@@ -98,6 +98,19 @@ class TpccEngine(CCEngine):
         return st
 
 
+    def run_tpcc_epoch_part(self, home, d_args, d_owner, txns_per_rank, d_commit, d_oid=None):
+        """Config E from the engine (dv_tpcc_epoch_run_part): this rank's
+        client batch `home` (DeviceEpoch), its operation words and owner
+        bytes; d_commit / d_oid sized for the global epoch (ranks x
+        txns_per_rank), d_oid equal on every rank afterwards."""
+        self._after_torch()
+        st = L.Stats()
+        L.check(L.lib().dv_tpcc_epoch_run_part(self._ctx, ctypes.byref(home.desc()), _ptr(d_args), _ptr(d_owner),
+                                               txns_per_rank, _ptr(d_commit), _ptr(d_oid), ctypes.byref(st)),
+                "dv_tpcc_epoch_run_part")
+        return st
+
+
 def device_epoch(e, device="cuda"):
     """(DeviceEpoch, args tensor) of a TpccEpoch."""
     import torch

@@ -408,6 +408,21 @@ int dv_tpcc_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const u
  * committed txns' operations on this partition's rows.  d_args / d_oid must
  * stay valid until dv_epoch_finish. */
 int dv_tpcc_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args, uint64_t *d_oid);
+/* config E from the engine: dv_epoch_run_part for TPC-C
+ * contexts after dv_comm_init / dv_comm_init_local.  `home` is this rank's
+ * client batch (tables required), d_args its operation words and d_owner
+ * the partition of every access (dv_tpcc_gen's owner: the warehouse's
+ * partition, ITEM reads with their supply warehouse); records travel to
+ * their owner with table and operation word (the RQRY fragments of
+ * tpcc_txn.cpp:183-244), each partition resolves last names, decides and
+ * executes its rows, and d_oid[nranks * txns_per_rank] ends equal on every
+ * rank: the o_id of each committed NewOrder, all-reduced (MAX) from the
+ * partition of its district -- Calvin's RFWD forward of o_id
+ * (tpcc_txn.cpp:1040, message.cpp:982-1025).  An owner byte >= nranks is
+ * DV_ERR_ARG on every rank. */
+int dv_tpcc_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, const uint64_t *d_args,
+                           const uint8_t *d_owner, uint32_t txns_per_rank, uint8_t *d_commit,
+                           uint64_t *d_oid, dv_stats *st);
 
 #ifdef __cplusplus
 }

@@ -115,6 +115,9 @@ typedef struct {
 enum { OR_T_WH = 0, OR_T_DIST = 1, OR_T_CUST = 2, OR_T_ITEM = 3, OR_T_STOCK = 4, OR_T_CLAST = 5 };
 typedef struct or_tpcc_db or_tpcc_db;
 or_tpcc_db *or_tpcc_load(const or_tpcc_params *p, uint64_t seed, uint32_t part_id);
+/* the same with i_customer_last kept per partition of an ix_parts-partition
+ * layout (tpcc.c clast_key): the all-warehouse image of PART_CNT = ix_parts */
+or_tpcc_db *or_tpcc_load_layout(const or_tpcc_params *p, uint64_t seed, uint32_t part_id, uint32_t ix_parts);
 void     or_tpcc_free(or_tpcc_db *db);
 uint64_t or_tpcc_rows(const or_tpcc_db *db, uint32_t table);
 /* keys and the three state columns of a table (NULL = skip) */
@@ -128,6 +131,12 @@ int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint
 int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *txn_begin,
                   const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
                   const uint64_t *args, uint8_t *out_commit, uint64_t *out_oid, or_epoch_stats *st);
+/* owner[a]: the partition an access runs on (a by-name lookup reads that
+ * partition's list); required when the db was loaded with ix_parts > 1 */
+int or_tpcc_epoch_owner(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *txn_begin,
+                        const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
+                        const uint64_t *args, const uint8_t *owner, uint8_t *out_commit, uint64_t *out_oid,
+                        or_epoch_stats *st);
 
 uint64_t or_mix64(uint64_t z);
 uint64_t or_table_digest(const uint64_t *f0, uint64_t n);

@@ -98,6 +98,7 @@ struct or_tpcc_db {
     or_tpcc_params p;
     ttab t[5];
     or_index *clast;   /* i_customer_last: custNPKey -> customer row */
+    uint32_t ix_parts; /* partitions of the index layout (or_tpcc_load_layout) */
     uint64_t base[5];  /* global row id of each table's row 0 */
 };
 
@@ -117,10 +118,23 @@ static uint64_t tab_put(ttab *t, uint64_t key, uint64_t a, uint64_t b, uint64_t 
     return r;
 }
 
-or_tpcc_db *or_tpcc_load(const or_tpcc_params *p, uint64_t seed, uint32_t part_id) {
-    if (p->cust_per_dist < 1000 || part_id >= p->part_cnt) return NULL;
+/* i_customer_last lists are per partition (IndexHash::index_read reads the
+ * buckets of its part_id, index_hash.cpp:137-153; tpcc_wl.cpp:421-422 inserts
+ * with wh_to_part(wid)), and custNPKey's w * DIST_PER_WH + d overflows its 10
+ * bits from warehouse 103 on (tpcc_helper.cpp:35-43), so with many warehouses
+ * the last-name lists -- and the customer a Payment by name picks -- depend on
+ * the partition layout.  ix_parts > 1 keeps one list per (key, partition of
+ * ix_parts) in this all-warehouse image, as PART_CNT = ix_parts nodes would;
+ * or_tpcc_epoch_owner then reads the list of the access's owner partition. */
+static uint64_t clast_key(const or_tpcc_db *db, uint64_t key, uint32_t part) {
+    return db->ix_parts > 1 ? key * db->ix_parts + part : key;
+}
+
+or_tpcc_db *or_tpcc_load_layout(const or_tpcc_params *p, uint64_t seed, uint32_t part_id, uint32_t ix_parts) {
+    if (p->cust_per_dist < 1000 || part_id >= p->part_cnt || ix_parts < 1) return NULL;
     or_tpcc_db *db = (or_tpcc_db *)calloc(1, sizeof(or_tpcc_db));
     db->p = *p;
+    db->ix_parts = ix_parts;
     uint64_t wh = 0;
     for (uint64_t w = 1; w <= p->num_wh; w++) wh += wh_part(p, w) == part_id;
     const uint64_t ncust = wh * p->dist_per_wh * p->cust_per_dist;
@@ -160,13 +174,17 @@ or_tpcc_db *or_tpcc_load(const or_tpcc_params *p, uint64_t seed, uint32_t part_i
                 (void)t_rand(&R, 5000);                                /* C_DISCOUNT */
                 if (!mine) continue;
                 uint64_t r = tab_put(&db->t[OR_T_CUST], k_cust(p, c, d, w), dbl(-10.0), dbl(10.0), 1);
-                or_index_insert(db->clast, k_custnp(p, last, d, w), r);
+                or_index_insert(db->clast, clast_key(db, k_custnp(p, last, d, w), (uint32_t)((w - 1) % ix_parts)), r);
             }
         }
     }
     uint64_t b = 0;
     for (int t = 0; t < 5; t++) { db->base[t] = b; b += db->t[t].n; }
     return db;
+}
+
+or_tpcc_db *or_tpcc_load(const or_tpcc_params *p, uint64_t seed, uint32_t part_id) {
+    return or_tpcc_load_layout(p, seed, part_id, 1);
 }
 
 void or_tpcc_free(or_tpcc_db *db) {
@@ -291,9 +309,10 @@ int or_tpcc_gen(const or_tpcc_params *p, uint64_t seed, uint32_t home_part, uint
 }
 
 /* ------------------------------------------------------------------ epoch */
-int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *tb, const uint64_t *keys,
-                  const uint8_t *types, const uint8_t *tables, const uint64_t *args, uint8_t *out_commit,
-                  uint64_t *out_oid, or_epoch_stats *st) {
+int or_tpcc_epoch_owner(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *tb, const uint64_t *keys,
+                        const uint8_t *types, const uint8_t *tables, const uint64_t *args, const uint8_t *owner,
+                        uint8_t *out_commit, uint64_t *out_oid, or_epoch_stats *st) {
+    if (db->ix_parts > 1 && !owner) return -1;
     uint64_t n_acc = tb[n_txn];
     uint64_t *rows = (uint64_t *)malloc((n_acc + 1) * 8);
     uint8_t *tab = (uint8_t *)malloc(n_acc + 1);
@@ -302,7 +321,7 @@ int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *tb
         int rc;
         uint8_t t = tables[a];
         if (t == OR_T_CLAST) {             /* run_payment_4 by last name */
-            rc = or_index_read_mid(db->clast, keys[a], &r);
+            rc = or_index_read_mid(db->clast, clast_key(db, keys[a], owner ? owner[a] : 0u), &r);
             t = OR_T_CUST;
         } else if (t < 5) {
             rc = or_index_read(db->t[t].ix, keys[a], &r);
@@ -358,4 +377,10 @@ int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *tb
     free(rows);
     free(tab);
     return 0;
+}
+
+int or_tpcc_epoch(or_tpcc_db *db, int cc_alg, uint32_t n_txn, const uint32_t *tb, const uint64_t *keys,
+                  const uint8_t *types, const uint8_t *tables, const uint64_t *args, uint8_t *out_commit,
+                  uint64_t *out_oid, or_epoch_stats *st) {
+    return or_tpcc_epoch_owner(db, cc_alg, n_txn, tb, keys, types, tables, args, NULL, out_commit, out_oid, st);
 }

@@ -102,6 +102,11 @@ def lib():
         L.or_tpcc_epoch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, u32p, u64p, u8p, u8p,
                                     u64p, u8p, u64p, P(EpochStats)]
         L.or_tpcc_epoch.restype = ctypes.c_int
+        L.or_tpcc_load_layout.argtypes = [P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32]
+        L.or_tpcc_load_layout.restype = ctypes.c_void_p
+        L.or_tpcc_epoch_owner.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, u32p, u64p, u8p, u8p,
+                                          u64p, u8p, u8p, u64p, P(EpochStats)]
+        L.or_tpcc_epoch_owner.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -151,9 +156,11 @@ def tpcc_gen(p, n_txn, seed, home_part=0):
 class TpccDB:
     """Oracle TPC-C partition (oracle/tpcc.c)."""
 
-    def __init__(self, p, seed, part_id=0):
+    def __init__(self, p, seed, part_id=0, index_parts=1):
+        """index_parts > 1: last-name lists per partition of that layout
+        (or_tpcc_load_layout), for epochs of a partitioned run."""
         self.p = p
-        self.db = lib().or_tpcc_load(ctypes.byref(p), seed, part_id)
+        self.db = lib().or_tpcc_load_layout(ctypes.byref(p), seed, part_id, index_parts)
         assert self.db
 
     def table(self, t):
@@ -162,15 +169,17 @@ class TpccDB:
         assert lib().or_tpcc_table(self.db, t, *[_p(a, ctypes.c_uint64) for a in out]) == 0
         return out
 
-    def epoch(self, cc, keys, types, tables, args, tb):
+    def epoch(self, cc, keys, types, tables, args, tb, owner=None):
         n_txn = len(tb) - 1
         commit = np.zeros(max(1, n_txn), dtype=np.uint8)
         oid = np.zeros(max(1, n_txn), dtype=np.uint64)
         st = EpochStats()
-        rc = lib().or_tpcc_epoch(self.db, cc, n_txn, _p(tb, ctypes.c_uint32), _p(keys, ctypes.c_uint64),
-                                 _p(types, ctypes.c_uint8), _p(tables, ctypes.c_uint8),
-                                 _p(args, ctypes.c_uint64), _p(commit, ctypes.c_uint8),
-                                 _p(oid, ctypes.c_uint64), ctypes.byref(st))
+        own = None if owner is None else np.ascontiguousarray(owner, dtype=np.uint8)
+        rc = lib().or_tpcc_epoch_owner(self.db, cc, n_txn, _p(tb, ctypes.c_uint32), _p(keys, ctypes.c_uint64),
+                                       _p(types, ctypes.c_uint8), _p(tables, ctypes.c_uint8),
+                                       _p(args, ctypes.c_uint64), _p(own, ctypes.c_uint8) if own is not None
+                                       else None, _p(commit, ctypes.c_uint8),
+                                       _p(oid, ctypes.c_uint64), ctypes.byref(st))
         if rc != 0:
             raise RuntimeError(f"oracle tpcc epoch failed rc={rc}")
         return commit[:n_txn], oid[:n_txn], st

@@ -208,3 +208,43 @@ def test_product_generator_matches_tpcc_golden(dv, name):
         for k, v in (("keys", e.keys), ("types", e.types), ("tables", e.tables), ("args", e.args),
                      ("txn_begin", e.txn_begin)):
             assert np.array_equal(z[k], v), k
+
+
+def test_oracle_index_layout_matches_partition_loads():
+    """or_tpcc_load_layout: the all-warehouse image with last-name lists per
+    partition equals, partition by partition, the oracle loaded as that one
+    partition (or_tpcc_load, PART_CNT 4) -- with 128 warehouses custNPKey's
+    w * 10 + d overflows its 10 bits (tpcc_helper.cpp:35-43), so the lists
+    really differ from the one-partition image's (checked too)."""
+    P, nw = 4, 128
+    kw = dict(cust_per_dist=1000, max_items=2000, perc_payment=1.0, mpr=0.0)
+    p1 = O.tpcc_params(nw, part_cnt=1, **kw)
+    pP = O.tpcc_params(nw, part_cnt=P, **kw)
+    img = O.TpccDB(p1, 3, index_parts=P)
+    flat = O.TpccDB(p1, 3)
+    differs = False
+    for q in range(P):
+        keys, types, tables, args, tb, _, own = O.tpcc_gen(pP, 3000, 50 + q, home_part=q)
+        # the txns that run on partition q only (no remote customer)
+        local = [t for t in range(len(tb) - 1) if (own[tb[t]:tb[t + 1]] == q).all()]
+        sel = np.concatenate([np.arange(tb[t], tb[t + 1]) for t in local])
+        sizes = np.array([tb[t + 1] - tb[t] for t in local], np.int64)
+        tbl = np.zeros(len(local) + 1, np.uint32)
+        tbl[1:] = np.cumsum(sizes)
+        e = (keys[sel], types[sel], tables[sel], args[sel], tbl)
+        part = O.TpccDB(pP, 3, part_id=q)
+        c_part, _, _ = part.epoch(O.CALVIN, *e)
+        c_img, _, _ = img.epoch(O.CALVIN, *e, owner=own[sel])
+        assert (c_part == c_img).all()
+        ck, cref = part.table(2)[0], part.table(2)[1:]
+        ik, icols = img.table(2)[0], img.table(2)[1:]
+        idx = np.searchsorted(ik, ck)
+        assert (ik[idx] == ck).all()
+        for col in range(3):
+            assert (icols[col][idx] == cref[col]).all(), (q, col)
+        flat.epoch(O.CALVIN, *e)
+    fk, fcols = flat.table(2)[0], flat.table(2)[1:]
+    ik, icols = img.table(2)[0], img.table(2)[1:]
+    assert (fk == ik).all()
+    differs = any((fcols[c] != icols[c]).any() for c in range(3))
+    assert differs, "expected the flat index to pick other customers at 128 warehouses"

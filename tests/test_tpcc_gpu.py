@@ -181,6 +181,133 @@ def test_tpcc_partitioned_engines(cc, world):
     assert (oid_sum == o_ref).all()
 
 
+def _tpcc_group(cc, kw, world, n_txn, seed, gen_seed):
+    """`world` TPC-C contexts on this GPU joined by the in-process transport
+    (dv_comm_init_local), one epoch through dv_tpcc_epoch_run_part on one
+    host thread each; returns (engines, params, batches, per-rank results)."""
+    import threading
+    pp = T.tpcc_params(part_cnt=world, **kw)
+    batches = [T.gen(pp, n_txn, gen_seed + r, home_part=r) for r in range(world)]
+    engines = [T.TpccEngine(cc, pp, n_txn * world, part_id=p, seed=seed) for p in range(world)]
+    dvcc.CCEngine.comm_init_local(engines)
+    out = [None] * world
+
+    def body(r):
+        try:
+            b = batches[r]
+            dep, d_args = T.device_epoch(b)
+            own = torch.from_numpy(b.owner).cuda()
+            d_commit = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+            d_oid = torch.zeros(n_txn * world, dtype=torch.int64, device="cuda")
+            st = engines[r].run_tpcc_epoch_part(dep, d_args, own, n_txn, d_commit, d_oid)
+            out[r] = (d_commit.cpu().numpy(), d_oid.cpu().numpy().view(np.uint64), st)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=600)
+        assert not t.is_alive(), "a rank hung in the partitioned TPC-C epoch"
+    return engines, pp, batches, out
+
+
+def _check_tpcc_group(cc, kw, world, n_txn, full_tables):
+    engines, pp, batches, out = _tpcc_group(cc, kw, world, n_txn, 5, 60)
+    try:
+        # the oracle's all-warehouse image with last-name lists per partition
+        # of this layout (custNPKey collides across warehouses from 103 on)
+        db = O.TpccDB(O.tpcc_params(**dict(kw, part_cnt=1)), 5, index_parts=world)
+        c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], *_global(batches), owner=np.concatenate([b.owner for b in batches]))
+        committed = 0
+        for r, x in enumerate(out):
+            assert not isinstance(x, Exception), f"rank {r}: {x}"
+            c, o, st = x
+            assert (c == c_ref).all(), f"rank {r}: {(c != c_ref).sum()} commit mismatches"
+            assert (o == o_ref).all(), f"rank {r}: o_id (RFWD all-reduce) differs"
+            committed = st.committed
+        assert committed == st_ref.committed
+        for tid in range(5):
+            ref = db.table(tid)
+            if full_tables or tid == T.L.T_ITEM:  # (ITEM: replicated on every partition)
+                for p, eng in enumerate(engines):
+                    mine = np.isin(ref[0], T.table(pp, 5, tid, p)[0])
+                    for col in range(3):
+                        assert (eng.read_col(tid, col) == ref[1 + col][mine]).all(), (p, tid, col)
+            else:  # order-free digest of every (key, column) pair over all partitions
+                def dig(keys, cols):
+                    h = keys * np.uint64(0x9E3779B97F4A7C15)
+                    for j, c in enumerate(cols):
+                        h ^= (c + np.uint64(j + 1)) * np.uint64(0xC2B2AE3D27D4EB4F)
+                    return int(h.sum(dtype=np.uint64))
+                want = dig(ref[0], ref[1:])
+                got = sum(dig(T.table(pp, 5, tid, p)[0], [eng.read_col(tid, col) for col in range(3)])
+                          for p, eng in enumerate(engines)) % (1 << 64)
+                assert got == want, f"table {tid}"
+    finally:
+        for eng in engines:
+            eng.close()
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("world", [2, 8])
+def test_tpcc_engine_driver(cc, world):
+    """dv_tpcc_epoch_run_part: owner split by the per-access owner byte,
+    records with table and operation word, per-partition last-name lookup,
+    decisions and execution, o_id all-reduced to every rank -- equal to the
+    single-thread E-schedule over the sequenced global epoch."""
+    kw = dict(num_wh=2 * world, cust_per_dist=1000, max_items=2000, part_per_txn=2, mpr=1.0)
+    _check_tpcc_group(cc, kw, world, 1500, full_tables=True)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cc", [dvcc.WAIT_DIE, dvcc.CALVIN])
+def test_tpcc_config_e_full_layout(cc):
+    """Config E's full layout: 256 warehouses over 8 partitions (32 each),
+    full item / customer counts, MPR 1.0, PERC_PAYMENT 0.5 -- 8 contexts on
+    this GPU driven by the engine's partitioned protocol."""
+    kw = dict(num_wh=256, cust_per_dist=3000, max_items=100000, part_per_txn=2, mpr=1.0)
+    _check_tpcc_group(cc, kw, 8, 1250, full_tables=False)
+
+
+def test_tpcc_engine_driver_bad_owner():
+    """An owner byte >= the partition count: DV_ERR_ARG on every rank, no
+    rank hangs, no table changes."""
+    world = 2
+    kw = dict(num_wh=4, cust_per_dist=1000, max_items=2000, part_per_txn=2, mpr=1.0)
+    pp = T.tpcc_params(part_cnt=world, **kw)
+    batches = [T.gen(pp, 500, 70 + r, home_part=r) for r in range(world)]
+    batches[1].owner[3] = 7
+    engines = [T.TpccEngine(dvcc.WAIT_DIE, pp, 500 * world, part_id=p, seed=5) for p in range(world)]
+    dvcc.CCEngine.comm_init_local(engines)
+    import threading
+    before = [[eng.read_col(t, 0) for t in range(5)] for eng in engines]
+    out = [None] * world
+
+    def body(r):
+        try:
+            dep, d_args = T.device_epoch(batches[r])
+            own = torch.from_numpy(batches[r].owner).cuda()
+            d_commit = torch.zeros(500 * world, dtype=torch.uint8, device="cuda")
+            out[r] = engines[r].run_tpcc_epoch_part(dep, d_args, own, 500, d_commit)
+        except Exception as ex:  # noqa: BLE001
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+        assert not t.is_alive()
+    try:
+        for r, x in enumerate(out):
+            assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
+        for eng, b in zip(engines, before):
+            assert all((eng.read_col(t, 0) == b[t]).all() for t in range(5))
+    finally:
+        for eng in engines:
+            eng.close()
+
+
 @pytest.mark.parametrize("cc", [dvcc.WAIT_DIE, dvcc.CALVIN])
 def test_tpcc_runner_single_rank_rccl(cc):
     """The torch.distributed driver (RCCL) over a TPC-C engine, one rank."""

@@ -1,8 +1,9 @@
 """Summaries of a rocprofv3 kernel-trace CSV.
 
-    python tools/ktrace.py <run_kernel_trace.csv> [--epoch K]
+    python tools/ktrace.py <run_kernel_trace.csv> [--epoch K] [--start KERNEL]
 
-Prints per-kernel totals per epoch (an epoch starts at each k_probe) and the
+Prints per-kernel totals per epoch (an epoch starts at each k_probe, or at
+each KERNEL, e.g. k_tpcc_resolve for TPC-C epochs) and the
 dispatch timeline of epoch K (duration and gap to the previous dispatch).
 """
 import csv
@@ -21,12 +22,13 @@ def short(name):
 def main():
     path = sys.argv[1]
     show = int(sys.argv[sys.argv.index("--epoch") + 1]) if "--epoch" in sys.argv else 3
+    start = sys.argv[sys.argv.index("--start") + 1] if "--start" in sys.argv else "k_probe"
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     epochs, cur = [], None
     for r in rows:
         name = short(r["Kernel_Name"])
-        if name.startswith("k_probe"):
+        if name.startswith(start):
             cur = []
             epochs.append(cur)
         if cur is not None:
