@@ -99,13 +99,64 @@ struct TableDesc {
     // pkey column instead of a 16-byte {key, row} entry (config D: a 134 MB
     // probe target instead of 268 MB).
     const uint64_t *pkey;     // implicit-row direct map: pkey of local rows [0, nbuckets)
+    // ... and its key tags (key_tag below), one byte per row: the probe reads
+    // the tag, and the pkey word only behind the kTagWide sentinel
+    const uint8_t *ktag;
     const IxEntry *ix;        // index entries (direct: [nbuckets]; chained: sorted by bucket)
     const uint32_t *bstart;   // chained: [nbuckets+1] bucket starts; nullptr = direct map
     uint64_t nbuckets;
     uint64_t row_base;        // global row id of local row 0
     uint32_t hash_kind;       // DV_HASH_*
     uint32_t part_cnt;
+    uint64_t m_part, m_nb;    // div_magic of part_cnt / nbuckets (key_split)
 };
+
+// Key tag of an implicit-row direct map.  A bucket's keys differ only in
+// what the bucket function drops: with DV_HASH_YCSB, b = (k / P) % nb, a key
+// is (q, b, lo) with q = k / P / nb and lo = k % P; with DV_HASH_MOD,
+// b = k % nb, it is (q, b).  So q * P + lo (P = 1 for MOD) names the key
+// within its bucket exactly; a loaded row stores it in one byte when it is
+// below kTagWide (YCSB's loader: q = 0, the tag is the partition id), else
+// kTagWide, and a probe compares tags -- equal tags below kTagWide mean equal
+// keys, unequal ones a missing key -- reading the 8-byte pkey only for
+// kTagWide.  Config D's probe target shrinks from 134 MB to 16.8 MB.
+constexpr uint32_t kTagWide = 255;
+__host__ __device__ inline uint8_t key_tag(uint32_t hash_kind, uint64_t nbuckets, uint32_t part_cnt, uint64_t key) {
+    const uint64_t P = hash_kind == DV_HASH_YCSB ? part_cnt : 1u;
+    const uint64_t q = key / P / nbuckets;
+    if (q >= kTagWide) return (uint8_t)kTagWide;
+    const uint64_t code = q * P + key % P;
+    return (uint8_t)(code < kTagWide ? code : kTagWide);
+}
+// n / d and n % d for every 64-bit n without a division: m = div_magic(d) =
+// floor((2^64 - 1) / d) puts mulhi(n, m) within 2 below the quotient
+__host__ __device__ inline uint64_t div_magic(uint64_t d) { return d ? ~0ull / d : 0ull; }
+__device__ __forceinline__ uint64_t divmod_magic(uint64_t n, uint64_t d, uint64_t m, uint64_t &r) {
+    uint64_t q = __umul64hi(n, m);
+    r = n - q * d;
+    if (r >= d) { q++; r -= d; }
+    if (r >= d) { q++; r -= d; }
+    return q;
+}
+// the bucket of `key` and its key tag (key_tag) in one pass
+__device__ __forceinline__ uint64_t key_split(const TableDesc &t, uint64_t key, uint32_t &tag) {
+    uint64_t lo = 0, bk = 0, q;
+    if (t.hash_kind == DV_HASH_YCSB) {
+        const uint64_t q1 = divmod_magic(key, t.part_cnt, t.m_part, lo);
+        q = divmod_magic(q1, t.nbuckets, t.m_nb, bk);
+        const uint64_t code = q * t.part_cnt + lo;
+        tag = q >= kTagWide || code >= kTagWide ? kTagWide : (uint32_t)code;
+    } else {
+        q = divmod_magic(key, t.nbuckets, t.m_nb, bk);
+        tag = q >= kTagWide ? kTagWide : (uint32_t)q;
+    }
+    return bk;
+}
+// implicit-row direct map: does bucket bk hold the key of tag `tag`?
+__device__ inline bool direct_holds(const TableDesc &t, uint64_t bk, uint32_t tag, uint64_t key) {
+    const uint32_t tg = t.ktag[bk];
+    return tg != kTagWide ? tg == tag : t.pkey[bk] == key;
+}
 
 struct Tables {
     TableDesc t[kMaxTables];
@@ -299,7 +350,7 @@ void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
-                      uint64_t *f0, uint64_t *pkey);
+                      uint64_t *f0, uint64_t *pkey, uint8_t *ktag);
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
                         uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr);
 void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,

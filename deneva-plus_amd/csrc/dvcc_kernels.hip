@@ -26,21 +26,24 @@
 namespace dvcc {
 
 // ------------------------------------------------------------------ probe
-__device__ __forceinline__ uint64_t bucket_of(const TableDesc &t, uint64_t key) {
-    return t.hash_kind == DV_HASH_YCSB ? (key / t.part_cnt) % t.nbuckets : key % t.nbuckets;
-}
 
-__device__ __forceinline__ bool probe_row(const Tables &tabs, uint32_t tb, uint64_t key, uint64_t &row,
+// One index probe against table descriptor t.  Callers hand t over from
+// where it is uniform or cheap to index: the kernel arguments when the epoch
+// names no tables (YCSB: every access probes table 0, scalar registers), an
+// LDS copy of the descriptors otherwise -- indexing the kernel-argument array
+// with a per-lane table id compiles to a select chain over every descriptor
+// field, which cost a config-D probe 64 of its 172 us.
+__device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64_t key, uint64_t &row,
                                           Counters *ctr) {
-    if (tb >= tabs.n) {
+    if (!tb_ok) {
         set_err(ctr, ERRB_TABLE);
         return false;
     }
-    const TableDesc &t = tabs.t[tb];
-    const uint64_t bk = bucket_of(t, key);
+    uint32_t tag;
+    const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
     bool found = false;
-    if (t.pkey != nullptr) {                  // direct map, local row = bucket
-        if (t.pkey[bk] == key) { row = bk; found = true; }
+    if (t.pkey != nullptr) {                  // direct map, local row = bucket (key tags)
+        if (direct_holds(t, bk, tag, key)) { row = bk; found = true; }
     } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
         const IxEntry e = t.ix[bk];
         if (e.key == key) { row = e.row; found = true; }
@@ -80,7 +83,12 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
     // here, per 4096-access sort tile, so the sort skips that k_radix_hist
     // launch and its 8-byte-per-access re-read of the pairs.
     __shared__ uint32_t wc[4][kRadix];
+    __shared__ TableDesc s_td[kMaxTables];  // per-lane table ids index this copy
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (tables) {
+        if (threadIdx.x < kMaxTables) s_td[threadIdx.x] = tabs.t[threadIdx.x];
+        __syncthreads();
+    }
     const uint64_t per_block = (uint64_t)kBlock * kPV;
     static_assert(kTile % (kBlock * kPV) == 0, "probe chunks tile the sort tiles");
     // work unit of a block: a whole sort tile when counting, else one chunk
@@ -121,11 +129,10 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         for (int j = 0; j < kPV; j++) {
             row[j] = 0;
             if (i0 + j < n) {
-#ifdef DVCC_EXP_NO_INDEX
-                row[j] = key[j];
-#else
-                probe_row(tabs, tb[j], key[j], row[j], ctr);
-#endif
+                if (tables)
+                    probe_row(s_td[tb[j] < kMaxTables ? tb[j] : 0], tb[j] < tabs.n, key[j], row[j], ctr);
+                else
+                    probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr);
             }
         }
         // run starts and their max-scan
@@ -893,18 +900,19 @@ void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uin
 // YCSB bucket (key/P) % rows == r, so the index is a direct map with local
 // row == bucket: an implicit-row map over the pkey column (TableDesc::pkey).
 __global__ void k_ycsb_load(uint64_t rows, uint32_t part_cnt, uint32_t part_id, uint64_t *f0,
-                            uint64_t *pkey) {
+                            uint64_t *pkey, uint8_t *ktag) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) {
         const uint64_t key = r * part_cnt + part_id;
         f0[r] = 0x00006F6C6C6568ull | (key & 0xFFFF000000000000ull);
         pkey[r] = key;
+        ktag[r] = key_tag(DV_HASH_YCSB, rows, part_cnt, key);
     }
 }
 
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
-                      uint64_t *f0, uint64_t *pkey) {
-    k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey);
+                      uint64_t *f0, uint64_t *pkey, uint8_t *ktag) {
+    k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey, ktag);
 }
 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,
@@ -912,7 +920,7 @@ __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys,
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t row = 0;
-        out[i] = probe_row(tabs, table, keys[i], row, ctr) ? f0[row] : 0ull;
+        out[i] = probe_row(tabs.t[table < kMaxTables ? table : 0], table < tabs.n, keys[i], row, ctr) ? f0[row] : 0ull;
     }
 }
 

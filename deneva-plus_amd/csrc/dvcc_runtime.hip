@@ -43,6 +43,7 @@ struct dv_ctx {
     uint64_t total_rows = 0;
     uint64_t *f0 = nullptr;    // hot column, global row id
     uint64_t *pkey = nullptr;  // primary key per row (row_t::get_primary_key)
+    uint8_t *ktag = nullptr;   // key tag per row (key_tag, dvcc_internal.h)
     uint64_t *col1 = nullptr, *col2 = nullptr;  // DV_TPCC: state columns 1 and 2
 
     // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
@@ -92,6 +93,18 @@ struct dv_ctx {
     uint32_t *d_tb = nullptr;         // txn_begin
     uint32_t *split_err = nullptr;    // the record check's error bits (begin clears the counters)
     uint64_t *d_args = nullptr, *d_oid = nullptr;  // dv_tpcc_epoch_run staging
+    // double-buffered host input (dv_epoch_stage_host / dv_epoch_run_staged):
+    // two record slots filled on a copy stream while the context's stream runs
+    struct HostSlot {
+        dv_access *acc = nullptr;
+        uint32_t *tb = nullptr;
+        hipEvent_t copied = nullptr;  // the slot's H2D is done
+        hipEvent_t drained = nullptr; // the split has read the slot
+        uint64_t n_acc = 0;
+        uint32_t n_txn = 0, max_len = 0;
+        bool csr = false, full = false;
+    } hslot[2];
+    hipStream_t copy_stream = nullptr;
 
     // epoch state
     int phase = 0;  // 0 idle, 1 begun
@@ -244,11 +257,14 @@ Tables make_tables(dv_ctx *c) {
         t.n = i + 1;
         t.t[i].ix = h.ix;
         t.t[i].pkey = h.implicit_rows ? c->pkey + h.row_base : nullptr;
+        t.t[i].ktag = h.implicit_rows ? c->ktag + h.row_base : nullptr;
         t.t[i].bstart = h.bstart;
         t.t[i].nbuckets = h.nbuckets ? h.nbuckets : 1;
         t.t[i].row_base = h.row_base;
         t.t[i].hash_kind = h.hash_kind;
         t.t[i].part_cnt = c->cfg.part_cnt ? c->cfg.part_cnt : 1;
+        t.t[i].m_part = div_magic(t.t[i].part_cnt);
+        t.t[i].m_nb = div_magic(t.t[i].nbuckets);
     }
     return t;
 }
@@ -332,15 +348,24 @@ void dv_close(dv_ctx *c) {
         dfree(t.ix);
         dfree(t.bstart);
     }
-    void *bufs[] = {c->f0, c->pkey, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
+    void *bufs[] = {c->f0, c->pkey, c->ktag, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
                     c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tlen, c->acc_row,
                     c->ulist[0], c->ulist[1], c->tb_start, c->tb_end, c->desc, c->tile_ctr,
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
                     c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
-                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc};
+                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc,
+                    c->hslot[0].acc, c->hslot[0].tb, c->hslot[1].acc, c->hslot[1].tb};
     for (void *b : bufs) dfree(b);
+    for (auto &h : c->hslot) {
+        if (h.copied) (void)hipEventDestroy(h.copied);
+        if (h.drained) (void)hipEventDestroy(h.drained);
+    }
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+    }
     if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     if (c->h_pub) (void)hipHostFree(c->h_pub);
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -503,14 +528,17 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     const uint64_t new_total = c->total_rows + capacity_rows;
     const bool cols = c->cfg.workload == DV_TPCC;
     uint64_t *nf0 = nullptr, *npk = nullptr, *nc1 = nullptr, *nc2 = nullptr;
+    uint8_t *ntg = nullptr;
     int r = dalloc(&nf0, new_total);
     if (!r) r = dalloc(&npk, new_total);
+    if (!r) r = dalloc(&ntg, new_total);
     if (!r && cols) r = dalloc(&nc1, new_total);
     if (!r && cols) r = dalloc(&nc2, new_total);
-    if (r) { dfree(nf0); dfree(npk); dfree(nc1); return r; }
+    if (r) { dfree(nf0); dfree(npk); dfree(ntg); dfree(nc1); return r; }
     if (c->total_rows) {
         HIPCHK(hipMemcpyAsync(nf0, c->f0, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(npk, c->pkey, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(ntg, c->ktag, c->total_rows, hipMemcpyDeviceToDevice, c->stream));
         if (cols) {
             HIPCHK(hipMemcpyAsync(nc1, c->col1, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
             HIPCHK(hipMemcpyAsync(nc2, c->col2, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -518,6 +546,7 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     }
     HIPCHK(hipMemsetAsync(nf0 + c->total_rows, 0, capacity_rows * 8, c->stream));
     HIPCHK(hipMemsetAsync(npk + c->total_rows, 0xFF, capacity_rows * 8, c->stream));
+    HIPCHK(hipMemsetAsync(ntg + c->total_rows, kTagWide, capacity_rows, c->stream));  // (no key: pkey decides)
     if (cols) {
         HIPCHK(hipMemsetAsync(nc1 + c->total_rows, 0, capacity_rows * 8, c->stream));
         HIPCHK(hipMemsetAsync(nc2 + c->total_rows, 0, capacity_rows * 8, c->stream));
@@ -525,10 +554,12 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     HIPCHK(hipStreamSynchronize(c->stream));
     dfree(c->f0);
     dfree(c->pkey);
+    dfree(c->ktag);
     dfree(c->col1);
     dfree(c->col2);
     c->f0 = nf0;
     c->pkey = npk;
+    c->ktag = ntg;
     c->col1 = nc1;
     c->col2 = nc2;
     t.created = true;
@@ -600,6 +631,11 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
     if (n) {
         if (f0) HIPCHK(hipMemcpy(c->f0 + t.row_base, f0, n * 8, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->pkey + t.row_base, keys, n * 8, hipMemcpyHostToDevice));
+        if (implicit) {  // row i holds keys[i]
+            std::vector<uint8_t> tg(n);
+            for (uint64_t i = 0; i < n; i++) tg[i] = key_tag(t.hash_kind, nb, P, keys[i]);
+            HIPCHK(hipMemcpy(c->ktag + t.row_base, tg.data(), n, hipMemcpyHostToDevice));
+        }
     }
     t.n_rows = n;
     t.loaded = true;
@@ -622,7 +658,7 @@ int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
     t.bstart = nullptr;
     t.implicit_rows = true;  // row r holds key r * P + part, in bucket r
     launch_ycsb_load(c->stream, rows_per_part, c->cfg.part_cnt, c->cfg.part_id, c->f0 + t.row_base,
-                     c->pkey + t.row_base);
+                     c->pkey + t.row_base, c->ktag + t.row_base);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     t.n_rows = rows_per_part;
@@ -1471,43 +1507,50 @@ int dv_round_log(dv_ctx *c, uint32_t *live, uint32_t *undecided, uint32_t cap) {
 namespace {
 // host buffers -> the context's device epoch (H2D of the 16-B records, then
 // split into SoA on the device, checked against txn_begin there)
-int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
-                     uint32_t n_txn, dv_epoch_dev *ep) {
+// the host side of an epoch from host records: capacity and the CSR form
+// (txn_begin: monotone, ends at n_acc; its longest txn bounds the verdict
+// bytes).  One branch-free pass, so it vectorises (a 1M-txn epoch: ~0.3 ms).
+int check_host_epoch(const dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                     uint32_t n_txn, uint32_t *max_len) {
     if (!c || (n_acc && !acc)) return DV_ERR_ARG;
     if (n_acc > c->cfg.max_acc || n_txn > c->cfg.max_txn) return DV_ERR_ARG;
-    uint32_t max_len = 0;
-    if (txn_begin) {  // CSR form: checked here per txn, against acc[].txn_seq on the device
-        if (txn_begin[0] != 0 || txn_begin[n_txn] != n_acc) return DV_ERR_ARG;
-        for (uint32_t t = 0; t < n_txn; t++) {
-            if (txn_begin[t + 1] < txn_begin[t]) return DV_ERR_ARG;
-            max_len = std::max(max_len, txn_begin[t + 1] - txn_begin[t]);
-        }
-        if (max_len > kMaxPos) return DV_ERR_ARG;
+    *max_len = 0;
+    if (!txn_begin) return DV_OK;  // records only: their txn_seq order is checked by the probe
+    if (txn_begin[0] != 0 || txn_begin[n_txn] != n_acc) return DV_ERR_ARG;
+    uint32_t mx = 0, bad = 0;
+    for (uint32_t t = 0; t < n_txn; t++) {
+        const uint32_t d = txn_begin[t + 1] - txn_begin[t];
+        bad |= (uint32_t)(txn_begin[t + 1] < txn_begin[t]);
+        mx = d > mx ? d : mx;
     }
-    HIPCHK(hipSetDevice(c->cfg.device));
-    int r = DV_OK;
-    if (!c->d_acc) {
-        const uint64_t A = c->cfg.max_acc;
-        r = dalloc(&c->d_acc, A);
-        if (!r) r = dalloc(&c->d_keys, A);
-        if (!r) r = dalloc(&c->d_types, A);
-        if (!r) r = dalloc(&c->d_tables, A);
-        if (!r) r = dalloc(&c->d_txn, A);
-        if (!r) r = dalloc(&c->d_commit, c->cfg.max_txn);
-        if (!r && c->cfg.cc_alg == DV_CALVIN) r = dalloc(&c->d_grant, A);
-        if (!r) r = dalloc(&c->d_tb, (uint64_t)c->cfg.max_txn + 1);
-        if (!r) r = dalloc(&c->split_err, 1);
-        if (r) return r;
-    }
+    if (bad || mx > kMaxPos) return DV_ERR_ARG;
+    *max_len = mx;
+    return DV_OK;
+}
+
+int alloc_host_staging(dv_ctx *c) {
+    if (c->d_acc) return DV_OK;
+    const uint64_t A = c->cfg.max_acc;
+    int r = dalloc(&c->d_acc, A);
+    if (!r) r = dalloc(&c->d_keys, A);
+    if (!r) r = dalloc(&c->d_types, A);
+    if (!r) r = dalloc(&c->d_tables, A);
+    if (!r) r = dalloc(&c->d_txn, A);
+    if (!r) r = dalloc(&c->d_commit, c->cfg.max_txn);
+    if (!r && c->cfg.cc_alg == DV_CALVIN) r = dalloc(&c->d_grant, A);
+    if (!r) r = dalloc(&c->d_tb, (uint64_t)c->cfg.max_txn + 1);
+    if (!r) r = dalloc(&c->split_err, 1);
+    return r;
+}
+
+// device records (d_acc, and d_tb for the CSR form) -> the epoch's arrays,
+// on the context's stream
+void split_records(dv_ctx *c, const dv_access *d_acc, uint64_t n_acc, const uint32_t *d_tb, uint32_t n_txn,
+                   uint32_t max_len, dv_epoch_dev *ep) {
     if (n_acc) {
-        HIPCHK(hipMemcpyAsync(c->d_acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice,
-                              c->stream));
-        if (txn_begin)
-            HIPCHK(hipMemcpyAsync(c->d_tb, txn_begin, ((size_t)n_txn + 1) * sizeof(uint32_t),
-                                  hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemsetAsync(c->split_err, 0, sizeof(uint32_t), c->stream));
-        launch_split_access(c->stream, c->d_acc, n_acc, txn_begin ? c->d_tb : nullptr, n_txn, c->d_keys,
-                            c->d_types, c->d_txn, c->d_tables, c->split_err);
+        (void)hipMemsetAsync(c->split_err, 0, sizeof(uint32_t), c->stream);
+        launch_split_access(c->stream, d_acc, n_acc, d_tb, n_txn, c->d_keys, c->d_types, c->d_txn, c->d_tables,
+                            c->split_err);
         c->err_seed = c->split_err;  // the epoch starts with the record check's verdict (input_err)
     }
     *ep = dv_epoch_dev{};
@@ -1518,6 +1561,23 @@ int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint
     ep->n_acc = n_acc;
     ep->n_txn = n_txn;
     ep->max_txn_acc = max_len;
+}
+
+int stage_host_epoch(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                     uint32_t n_txn, dv_epoch_dev *ep) {
+    uint32_t max_len = 0;
+    int r = check_host_epoch(c, acc, n_acc, txn_begin, n_txn, &max_len);
+    if (r) return r;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    r = alloc_host_staging(c);
+    if (r) return r;
+    if (n_acc) {
+        HIPCHK(hipMemcpyAsync(c->d_acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice, c->stream));
+        if (txn_begin)
+            HIPCHK(hipMemcpyAsync(c->d_tb, txn_begin, ((size_t)n_txn + 1) * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, c->stream));
+    }
+    split_records(c, c->d_acc, n_acc, txn_begin ? c->d_tb : nullptr, n_txn, max_len, ep);
     return DV_OK;
 }
 
@@ -1549,6 +1609,69 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
         HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, n_txn, hipMemcpyDeviceToHost, c->stream));
     if (calvin && out_grant && n_acc)
         HIPCHK(hipMemcpyAsync(out_grant, c->d_grant, n_acc * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+// Double-buffered host input: the H2D copy of the next
+// epoch's records runs on a copy stream while the current epoch decides.
+int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                        uint32_t n_txn) {
+    if (!c || slot < 0 || slot > 1) return DV_ERR_ARG;
+    uint32_t max_len = 0;
+    int r = check_host_epoch(c, acc, n_acc, txn_begin, n_txn, &max_len);
+    if (r) return r;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    r = alloc_host_staging(c);
+    if (r) return r;
+    auto &h = c->hslot[slot];
+    if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!h.acc) {
+        r = dalloc(&h.acc, c->cfg.max_acc);
+        if (!r) r = dalloc(&h.tb, (uint64_t)c->cfg.max_txn + 1);
+        if (!r) r = hip_fail(hipEventCreateWithFlags(&h.copied, hipEventDisableTiming), "event");
+        if (!r) r = hip_fail(hipEventCreateWithFlags(&h.drained, hipEventDisableTiming), "event");
+        if (r) return r;
+        HIPCHK(hipEventRecord(h.drained, c->stream));
+    }
+    // the slot's previous epoch has been split out of it
+    HIPCHK(hipStreamWaitEvent(c->copy_stream, h.drained, 0));
+    if (n_acc) {
+        HIPCHK(hipMemcpyAsync(h.acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice, c->copy_stream));
+        if (txn_begin)
+            HIPCHK(hipMemcpyAsync(h.tb, txn_begin, ((size_t)n_txn + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                  c->copy_stream));
+    }
+    HIPCHK(hipEventRecord(h.copied, c->copy_stream));
+    h.n_acc = n_acc;
+    h.n_txn = n_txn;
+    h.max_len = max_len;
+    h.csr = txn_begin != nullptr;
+    h.full = true;
+    return DV_OK;
+}
+
+int dv_epoch_run_staged(dv_ctx *c, int slot, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
+                        dv_stats *st) {
+    if (!c || slot < 0 || slot > 1 || !out_commit) return DV_ERR_ARG;
+    auto &h = c->hslot[slot];
+    if (!h.full) return DV_ERR_STATE;
+    if (ts && c->cfg.cc_alg == DV_WAIT_DIE)  // as dv_epoch_run
+        for (uint32_t t = 1; t < h.n_txn; t++)
+            if (ts[t] <= ts[t - 1]) return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    h.full = false;
+    HIPCHK(hipStreamWaitEvent(c->stream, h.copied, 0));
+    dv_epoch_dev ep;
+    split_records(c, h.acc, h.n_acc, h.csr ? h.tb : nullptr, h.n_txn, h.max_len, &ep);
+    HIPCHK(hipEventRecord(h.drained, c->stream));
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    int r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);
+    if (r) return r;
+    if (h.n_txn)
+        HIPCHK(hipMemcpyAsync(out_commit, c->d_commit, h.n_txn, hipMemcpyDeviceToHost, c->stream));
+    if (calvin && out_grant && h.n_acc)
+        HIPCHK(hipMemcpyAsync(out_grant, c->d_grant, h.n_acc * 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return DV_OK;
 }

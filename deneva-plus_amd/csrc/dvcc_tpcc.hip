@@ -43,9 +43,6 @@ namespace {
 
 constexpr uint64_t kOpMask = (1ull << 56) - 1;
 
-__device__ __forceinline__ uint64_t bucket_of_t(const TableDesc &t, uint64_t key) {
-    return t.hash_kind == DV_HASH_YCSB ? (key / t.part_cnt) % t.nbuckets : key % t.nbuckets;
-}
 
 __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint64_t *__restrict__ keys,
                                                          const uint8_t *__restrict__ tables, uint64_t n,
@@ -58,10 +55,11 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
         if (tb == DV_TPCC_CUST_LAST) {
             if (tb < tabs.n) {  // else the probe reports the missing table
                 const TableDesc &t = tabs.t[tb];
-                const uint64_t bk = bucket_of_t(t, key);
+                uint32_t tag;
+                const uint64_t bk = key_split(t, key, tag);
                 uint64_t row = ~0ull;
                 if (t.pkey != nullptr) {
-                    if (t.pkey[bk] == key) row = bk;
+                    if (direct_holds(t, bk, tag, key)) row = bk;
                 } else if (t.bstart == nullptr) {
                     if (t.ix[bk].key == key) row = t.ix[bk].row;
                 } else {

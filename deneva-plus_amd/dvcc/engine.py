@@ -246,6 +246,19 @@ class CCEngine:
                                      None, ctypes.byref(st)), "dv_epoch_run")
         return st
 
+    def stage_host(self, slot, acc, tb, n_acc, n_txn):
+        """dv_epoch_stage_host: queue the H2D copy of host records (pinned
+        for an asynchronous copy) into staging slot 0 / 1."""
+        L.check(L.lib().dv_epoch_stage_host(self._ctx, slot, _ptr(acc), n_acc, _ptr(tb), n_txn),
+                "dv_epoch_stage_host")
+
+    def run_staged(self, slot, commit):
+        """dv_epoch_run_staged: run the epoch in `slot`; commit bytes to host."""
+        st = L.Stats()
+        L.check(L.lib().dv_epoch_run_staged(self._ctx, slot, None, _ptr(commit), None, ctypes.byref(st)),
+                "dv_epoch_run_staged")
+        return st
+
     # ---- one epoch already resident in HBM
     def run_epoch_device(self, dep, d_commit=None, d_grant=None):
         st = L.Stats()

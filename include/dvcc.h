@@ -107,13 +107,13 @@ extern "C" {
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
 #define DV_FLAG_NO_ASYNC 8u /* never finish the decision rounds in the
-                               asynchronous multi-workgroup kernel.  That
-                               kernel needs every workgroup of its launch
-                               resident at once, so it assumes the GPU to
-                               itself: contexts that run epochs concurrently
-                               on one GPU (threads or processes) set this
-                               flag, or two such launches can each hold half
-                               the CUs until their bounded wait runs out */
+                               asynchronous multi-workgroup kernel (that
+                               kernel wants every workgroup of its launch
+                               resident at once; when co-running work holds
+                               CUs its workgroups yield after an idle time,
+                               dv_set_async_limits, and the synchronous
+                               rounds finish the epoch -- correct either way,
+                               this flag only skips the attempt) */
 
 typedef struct dv_ctx dv_ctx;
 
@@ -232,6 +232,20 @@ int dv_read_table(dv_ctx *ctx, uint32_t table, uint64_t first_row, uint64_t n, u
 int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                  uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit,
                  uint32_t *out_grant_group, dv_stats *st);
+/* double-buffered host input: dv_epoch_stage_host
+ * checks an epoch's host records as dv_epoch_run does and queues their H2D
+ * copy into staging slot 0 or 1 on the context's copy stream, returning at
+ * once; dv_epoch_run_staged(slot) then runs that epoch on the context's
+ * stream (after its copy) and writes the commit bytes to host memory.
+ * Staging epoch k+1 before running epoch k overlaps the copy with the
+ * decisions.  acc / txn_begin must stay unchanged until the slot's run
+ * returns; pinned host memory makes the copy asynchronous (pageable memory
+ * is copied before dv_epoch_stage_host returns).  A slot holds one epoch:
+ * running an empty slot is DV_ERR_STATE. */
+int dv_epoch_stage_host(dv_ctx *ctx, int slot, const dv_access *acc, uint64_t n_acc,
+                        const uint32_t *txn_begin, uint32_t n_txn);
+int dv_epoch_run_staged(dv_ctx *ctx, int slot, const uint64_t *ts, uint8_t *out_commit,
+                        uint32_t *out_grant_group, dv_stats *st);
 /* whole epoch on a device-resident epoch; outputs are device pointers
  * (d_grant_group only for DV_CALVIN, may be NULL) */
 int dv_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, uint8_t *d_commit,

@@ -98,6 +98,45 @@ def test_ragged_sizes(cc, n_txn, rows, theta):
 
 
 @pytest.mark.parametrize("cc", CCS)
+def test_double_buffered_host_input(cc):
+    """dv_epoch_stage_host / dv_epoch_run_staged: epoch k+1's records copied
+    on the copy stream while epoch k runs, alternating slots -- the same
+    decisions and table state as the oracle epoch after epoch; an empty slot
+    is DV_ERR_STATE, a malformed txn_begin DV_ERR_ARG."""
+    rows = 1 << 14
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    epochs = [g.gen(3000, s) for s in (11, 12, 13, 14, 15)]
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, 3000, max(e.n_acc for e in epochs))
+    try:
+        eng.load_ycsb_partition(rows)
+        bufs = [(torch.from_numpy(e.to_access_array().view(np.uint8)).pin_memory(),
+                 torch.from_numpy(np.ascontiguousarray(e.txn_begin, dtype=np.uint32)).pin_memory(),
+                 e.n_acc, e.n_txn) for e in epochs]
+        commit = torch.zeros(3000, dtype=torch.uint8).pin_memory()
+        with pytest.raises(dvcc.DvccError) as ex:
+            eng.run_staged(1, commit)
+        assert ex.value.code == dvcc._lib.DV_ERR_STATE
+        bad_tb = bufs[0][1].clone()
+        bad_tb[5] = bad_tb[7]  # not monotone
+        with pytest.raises(dvcc.DvccError) as ex:
+            eng.stage_host(0, bufs[0][0], bad_tb, bufs[0][2], bufs[0][3])
+        assert ex.value.code == dvcc._lib.DV_ERR_ARG
+        eng.stage_host(0, *bufs[0])
+        for i, e in enumerate(epochs):
+            if i + 1 < len(epochs):
+                eng.stage_host((i + 1) % 2, *bufs[i + 1])
+            st = eng.run_staged(i % 2, commit)
+            c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+            assert (commit.numpy()[:e.n_txn] == c_ref).all(), i
+            assert st.committed == st_ref.committed and st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == f0).all()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("cc", CCS)
 def test_epochs_carry_table_state(cc):
     g = YCSBQueryGenerator(1 << 14, zipf_theta=0.8)
     _check(cc, 1 << 14, [g.gen(3000, s) for s in (1, 2, 3)])
@@ -126,6 +165,47 @@ def test_missing_key_reports_error():
     e2 = Epoch(np.array([3], np.uint64), np.array([1], np.uint8), np.array([0, 1], np.uint32))
     c, _, st = eng.run_epoch(e2)
     assert c.tolist() == [1] and st.committed == 1
+
+
+@pytest.mark.parametrize("hash_kind,part_cnt", [(dvcc._lib.HASH_MOD, 1), (dvcc._lib.HASH_YCSB, 1),
+                                                (dvcc._lib.HASH_YCSB, 4)])
+def test_direct_map_key_tags(hash_kind, part_cnt):
+    """Implicit-row direct maps probe a one-byte key tag (key_tag,
+    dvcc_internal.h) and the pkey word only behind the wide-tag sentinel:
+    every loaded key is found, whether its tag is narrow, at the edge
+    (codes 253-255) or wide; keys sharing a bucket with a loaded row but not
+    loaded -- other quotient, other residue -- are DV_ERR_KEY_NOT_FOUND."""
+    nb = 64
+    P = part_cnt if hash_kind == dvcc._lib.HASH_YCSB else 1
+    rng = np.random.default_rng(3)
+    # key of bucket b: (q * nb + b) * P + lo, quotients from narrow to wide
+    qs = rng.choice([0, 1, 2, 60, 63, 254 // max(P, 1), 255, 256, 10 ** 6, 2 ** 40], size=nb)
+    lo = rng.integers(0, P, size=nb) if P > 1 else np.zeros(nb, np.int64)
+    keys = ((qs.astype(np.uint64) * np.uint64(nb) + np.arange(nb, dtype=np.uint64)) * np.uint64(P)
+            + lo.astype(np.uint64))
+    eng = CCEngine(dvcc.NO_WAIT, 8, 64, part_cnt=part_cnt if hash_kind == dvcc._lib.HASH_YCSB else 1)
+    try:
+        eng.create_table(0, nb, nb, hash_kind)
+        f0 = np.arange(nb, dtype=np.uint64) * np.uint64(7) + np.uint64(11)
+        eng.load_table(0, keys, f0)
+        assert (eng.read_rows(keys) == f0).all()
+        for b in range(nb):
+            others = [((int(qs[b]) + d) * nb + b) * P + int(lo[b]) for d in (1, -1) if int(qs[b]) + d >= 0]
+            if P > 1:
+                others.append((int(qs[b]) * nb + b) * P + (int(lo[b]) + 1) % P)
+            for k in others:
+                with pytest.raises(dvcc.DvccError) as ex:
+                    eng.read_rows(np.array([k], np.uint64))
+                assert ex.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (b, k)
+        # and through an epoch's probe
+        e = _epoch_of([[(int(keys[3]), 1), (int(keys[9]), 0)], [(int(keys[3]) + nb * P, 1)]])
+        with pytest.raises(dvcc.DvccError) as ex:
+            eng.run_epoch(e)
+        assert ex.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+        c, _, st = eng.run_epoch(_epoch_of([[(int(keys[3]), 1), (int(keys[9]), 0)], [(int(keys[60]), 1)]]))
+        assert st.committed == 2
+    finally:
+        eng.close()
 
 
 def _epoch_of(txns):
