@@ -41,7 +41,8 @@ HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_ACCESS = 67        # algorithmic bytes per access
 SCAN_BYTES = 9               # SURVEY.md 8d per access: scan read 8 B + conflict flag write 1 B
 TIMING = {"full": True, "kernel": "kernel", "off": False}
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_round_pass.json")  # tools/pmc_summary.py
+PROBE_ACC, PROBE_TXN = 18, 9  # k_probe algorithmic bytes per access / per txn (roofline)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_config_d.json")  # tools/pmc_summary.py
 
 CONFIGS = {
     # name: rows per partition, txns per epoch (in total, over all GPUs), zipf theta, description
@@ -280,8 +281,10 @@ def e2e_host_leg(eng, epochs, k):
            "bytes_h2d_per_epoch": int(bufs[0][0].numel()),
            "note": "dv_epoch_run: H2D of the access records, then the same device path"}
     # double-buffered
-    eng.stage_host(0, *bufs[0])
-    eng.run_staged(0, commit)  # slots allocated outside the timing
+    eng.stage_host(0, *bufs[0])  # both slots allocated outside the timing
+    eng.stage_host(1, *bufs[1 % len(bufs)])
+    eng.run_staged(0, commit)
+    eng.run_staged(1, commit)
     t0 = time.perf_counter()
     committed = 0
     eng.stage_host(0, *bufs[0])
@@ -339,9 +342,10 @@ def timed(step, first, warmup, steps, world):
     return stats, el
 
 
-def pmc_traffic(a, cc_name, world):
-    """HBM bytes per k_round_pass launch from the committed PMC summary, only
-    if it was measured on these sources, this config and GPU count."""
+def pmc_traffic(a, cc_name, world, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary
+    (tools/pmc_summary.py), only if it was measured on these sources, this
+    config and GPU count."""
     if not os.path.exists(PMC_SUMMARY):
         return None, "no PMC summary"
     pmc = json.load(open(PMC_SUMMARY))
@@ -349,31 +353,48 @@ def pmc_traffic(a, cc_name, world):
     stale = {k: (pmc.get(k), v) for k, v in want.items() if pmc.get(k) != v}
     if stale:
         return None, f"PMC summary does not match this run: {stale}"
-    return pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
+    k = pmc.get("kernels", {}).get(kernel)
+    if not k:
+        return None, f"no {kernel} in the PMC summary"
+    if "hbm_bytes_per_launch_calibrated" in k:  # tools/pmc_probe_cal.py
+        return k["hbm_bytes_per_launch_calibrated"], os.path.relpath(PMC_SUMMARY, ROOT) + " (calibrated)"
+    return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
 def roofline(kstats, a, cc_name, world):
-    """The dominant kernel, k_round_pass: algorithmic bytes per launch (9 B per
-    live access) / its average duration from the launches' own
-    dispatch timestamps on the engine's stream."""
-    launches = sum(s.pass_launches for s in kstats)
-    pass_ms = sum(s.ms_pass for s in kstats)
-    pass_live = sum(s.pass_live for s in kstats)
-    avg_ms = pass_ms / max(1, launches)
-    bytes_per_launch = SCAN_BYTES * pass_live / max(1, launches)
+    """The largest single launch of the epoch, the index probe (k_probe):
+    algorithmic bytes per launch -- SURVEY.md 8(d)'s probe traffic, PROBE_ACC
+    B per access (key 8 + type 1 + txn id 4 read, key tag 1 gathered, row
+    word 4 written) plus PROBE_TXN B per txn (access range 8 + length 1
+    written); the prefix's sort keys (8 B for ~1.6 % of the accesses) are not
+    counted -- over its average duration from the launch's own dispatch
+    timestamps on the engine's stream.  The decision stage's two asynchronous
+    launches take longer in sum but are bound by hand-off latency, not bytes
+    (DESIGN.md); k_round_pass is reported beside it."""
+    launches = sum(1 for s in kstats if s.ms_probe_kernel > 0)
+    avg_ms = sum(s.ms_probe_kernel for s in kstats) / max(1, launches)
+    bytes_per_launch = float(np.mean([PROBE_ACC * s.n_acc + PROBE_TXN * s.n_txn for s in kstats]))
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, src = pmc_traffic(a, cc_name, world)
+    traffic, src = pmc_traffic(a, cc_name, world, "k_probe")
+    p_launches = sum(s.pass_launches for s in kstats)
+    p_avg = sum(s.ms_pass for s in kstats) / max(1, p_launches)
+    p_bytes = SCAN_BYTES * sum(s.pass_live for s in kstats) / max(1, p_launches)
+    p_ach = p_bytes / (p_avg * 1e-3) / 1e9 if p_avg > 0 else 0.0
+    p_traffic, _ = pmc_traffic(a, cc_name, world, "k_round_pass")
     return {
-        "kernel": "k_round_pass", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+        "kernel": "k_probe", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": avg_ms, "launches": launches,
-        "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d scan read "
-                             "8 B + flag 1 B) x live accesses the launch reads",
+        "algorithmic_bytes": f"{PROBE_ACC} B per access + {PROBE_TXN} B per txn (SURVEY.md 8d probe: key, type, "
+                             "txn id read, key tag gathered, row word written; access ranges per txn)",
         "traffic_source": src,
-        "timed_by": ("dispatch timestamps of every pass launch in the timed region"
+        "timed_by": ("dispatch timestamps of every probe launch in the timed region"
                      if a.timing != "off" else
-                     f"dispatch timestamps of every pass launch over {len(kstats)} epochs run "
+                     f"dispatch timestamps of the probe launch over {len(kstats)} epochs run "
                      "right after the timed region (same epochs, same stream)"),
+        "k_round_pass": {"achieved": p_ach, "frac": p_ach / HBM_PEAK_GBPS, "avg_launch_ms": p_avg,
+                         "launches": p_launches, "bytes_per_launch": p_bytes, "traffic": p_traffic,
+                         "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d)"},
     }
 
 

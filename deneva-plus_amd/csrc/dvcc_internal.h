@@ -190,7 +190,8 @@ constexpr uint32_t kProbeHistTiles = 1024;
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit);
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
+                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),

@@ -43,7 +43,12 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
     const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
     bool found = false;
     if (t.pkey != nullptr) {                  // direct map, local row = bucket (key tags)
+#ifdef DVCC_CAL_NO_GATHER  // PMC calibration build only (tools/gpu_prof.sh): the streams without the gather
+        row = bk;
+        found = tag != kTagWide + 1;
+#else
         if (direct_holds(t, bk, tag, key)) { row = bk; found = true; }
+#endif
     } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
         const IxEntry e = t.ix[bk];
         if (e.key == key) { row = e.row; found = true; }
@@ -290,18 +295,22 @@ __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
-                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit) {
+                  uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
+                  hipEvent_t ev0, hipEvent_t ev1) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
     if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
+    // (ev0 / ev1: the launch's own dispatch timestamps, no extra packets)
     if (counts)
-        k_probe_hist<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs,
-                                               tb_start, tb_end, tlen, acc_row, ctr, counts, ntiles);
+        hipExtLaunchKernelGGL(k_probe_hist, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, types,
+                              acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
+                              counts, ntiles);
     else
-        k_probe<<<blocks, kBlock, 0, s>>>(tabs, keys, types, acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start,
-                                          tb_end, tlen, acc_row, ctr, pair_limit < n_txn ? pair_limit : n_txn);
+        hipExtLaunchKernelGGL(k_probe, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, types, acc_txn,
+                              tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
+                              pair_limit < n_txn ? pair_limit : n_txn);
 }
 
 // ------------------------------------------------------------- radix sort

@@ -209,6 +209,9 @@ RoundBufs round_bufs(dv_ctx *c) {
     return b;
 }
 
+// c->ev slots of the probe launch's dispatch timestamps (0-5: stage markers)
+constexpr int kEvProbe0 = 8, kEvProbe1 = 9;
+
 // descriptor tag of the next single-pass launch (tags are kTagBits wide)
 uint32_t next_tag(dv_ctx *c) {
     if (++c->round_tag >= (1u << 25)) {
@@ -813,7 +816,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
-                 calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn);
+                 calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
     rec(c, 1);
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
@@ -1091,6 +1095,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             st->pass_launches = np;
             st->ms_pass = sp;
             st->pass_live = c->passes <= (uint32_t)kRoundLog ? c->h_ctr->pass_live : 0;  // (no-op passes add 0)
+            if (c->n_acc) (void)hipEventElapsedTime(&st->ms_probe_kernel, c->ev[kEvProbe0], c->ev[kEvProbe1]);
         }
     }
     return DV_OK;
@@ -1348,7 +1353,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
                        c->tile_ctr, err_seed, c->ctr);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
-                 c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K);
+                 c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
     rec(c, 1);
     // the prefix: txns [0, K), the first ctr->a_acc accesses
     const uint32_t ub_a = (uint32_t)std::min<uint64_t>(ep->n_acc, (uint64_t)K * (ep->max_txn_acc ? ep->max_txn_acc

@@ -71,10 +71,10 @@ class Stats(ctypes.Structure):
                 ("ms_pass", ctypes.c_float), ("async_launches", ctypes.c_uint16),
                 ("async_declined", ctypes.c_uint16),
                 ("pass_live", ctypes.c_uint64), ("async_yields", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("ms_probe_kernel", ctypes.c_float)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class YcsbParams(ctypes.Structure):

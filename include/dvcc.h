@@ -177,7 +177,8 @@ typedef struct dv_stats {
     uint64_t pass_live;      /* live accesses those launches read, summed      */
     uint32_t async_yields;   /* asynchronous launches that yielded: the rounds
                                 were finished synchronously (dv_set_async_limits) */
-    uint32_t reserved;
+    float ms_probe_kernel;   /* the index-probe launch alone, from its own
+                                dispatch timestamps (DV_FLAG_KERNEL_TIMING)    */
 } dv_stats;
 
 /* parameters of YCSBQueryGenerator (g_* globals, system/global.cpp:65-195) */

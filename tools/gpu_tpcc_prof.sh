@@ -22,7 +22,8 @@ for C in FETCH_SIZE WRITE_SIZE; do
       > $OUT/pmc_$C.json 2> $OUT/pmc_$C.err
 done
 python3 tools/pmc_summary.py $OUT/pmc_FETCH_SIZE/run_counter_collection.csv \
-    $OUT/pmc_WRITE_SIZE/run_counter_collection.csv k_tpcc_apply $OUT/pmc_tpcc_apply.json \
+    $OUT/pmc_WRITE_SIZE/run_counter_collection.csv $OUT/pmc_tpcc.json \
+    k_tpcc_apply,k_tpcc_oid,k_tpcc_resolve,k_probe,k_round_pass,k_round_async \
     config=E n_txn=10000 n_gpus=1 src_hash=$SRC
 timeout -k 10 300 python -u bench.py --tpcc-only --steps 10 > $OUT/bench_tpcc.json 2> $OUT/bench_tpcc.err
 cat $OUT/bench_tpcc.json
