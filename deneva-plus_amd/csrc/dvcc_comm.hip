@@ -40,8 +40,8 @@ constexpr uint32_t kVoteBadArg = 1u, kVoteOverflow = 2u;
 
 // ---- owner split: per-block owner counts, then a stable scatter of records.
 // The owner of an access is key % PART_CNT (YCSB), or the caller's per-access
-// owner byte (TPC-C: the warehouse's partition, TPCCWorkload::wh_to_part,
-// tpcc_helper.cpp:101-104); an owner byte >= PART_CNT is an argument error,
+// owner byte (TPC-C: the warehouse's partition, wh_to_part,
+// tpcc_helper.cpp:161-164); an owner byte >= PART_CNT is an argument error,
 // voted like the others (xvote[1]) -- the access counts as rank 0's meanwhile.
 __device__ __forceinline__ uint32_t owner_of(const uint64_t *keys, const uint8_t *own, uint64_t i, uint32_t P,
                                              uint32_t *bad) {
@@ -507,7 +507,7 @@ namespace {
 // and operation word, the epoch runs through dv_tpcc_epoch_begin, and the
 // o_ids -- computed where the district row lives -- are all-reduced (MAX)
 // into every rank's d_oid: Calvin's RFWD of o_id to the other participants
-// (tpcc_txn.cpp:1040, message.cpp:982-1025), for every protocol.
+// (tpcc_txn.cpp:1040, txn.cpp:960-972, transport/message.cpp:982-1025), for every protocol.
 int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint64_t *args, bool tpcc,
              uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
     if (!c) return DV_ERR_ARG;

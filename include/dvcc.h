@@ -433,7 +433,7 @@ int dv_tpcc_epoch_begin(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_a
  * executes its rows, and d_oid[nranks * txns_per_rank] ends equal on every
  * rank: the o_id of each committed NewOrder, all-reduced (MAX) from the
  * partition of its district -- Calvin's RFWD forward of o_id
- * (tpcc_txn.cpp:1040, message.cpp:982-1025).  An owner byte >= nranks is
+ * (tpcc_txn.cpp:1040, txn.cpp:960-972, transport/message.cpp:982-1025).  An owner byte >= nranks is
  * DV_ERR_ARG on every rank. */
 int dv_tpcc_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, const uint64_t *d_args,
                            const uint8_t *d_owner, uint32_t txns_per_rank, uint8_t *d_commit,
