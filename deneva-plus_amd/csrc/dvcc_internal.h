@@ -325,13 +325,15 @@ void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
                         const Counters *ctr);
 uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (descriptors per array)
-// k_kill (every access after the prefix's against the row state) and
-// k_kill_compact (the survivors' sub-epoch)
+// k_kill (every access after the prefix's against the row state, one bit
+// per access into kill_bits[kill_words(n_acc)]) and k_kill_compact (killed
+// txns aborted, the survivors' sub-epoch)
+uint64_t kill_words(uint64_t n_acc);
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         const uint32_t *acc_txn, uint64_t n_acc, uint32_t K, uint32_t n_txn,
-                         const uint32_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
-                         uint8_t *tlen_b, uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr,
-                         uint32_t tag, Counters *ctr);
+                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, int nowait,
+                         uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
+                         uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
+                         Counters *ctr);
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
                              uint8_t *status, const Counters *ctr);
 

@@ -61,35 +61,57 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
 }
 
 // Every access after the prefix's (index >= ctr->a_acc) against the row
-// state: a conflict aborts its txn (a plain byte store; the txn's other
-// killed accesses store the same byte).  Access-parallel and coalesced: the
-// txn-major acc_row and the epoch's acc_txn streamed, one word gathered per
-// access from the bitmap.
-__global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ acc_row,
-                                                 const uint32_t *__restrict__ acc_txn, uint64_t n,
+// state, one bit per access: 64 consecutive accesses per wave step, the
+// txn-major acc_row streamed (4 B per access), one bitmap word gathered per
+// access, and the wave's verdicts stored as one ballot word -- k_kill_compact
+// then ORs each txn's range of bits.  (The conflict rule is the one in the
+// header comment; the txn id of an access is never needed here.)
+constexpr int kKillWords = 4;  // ballot words per wave per step (loads in flight)
+__global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
                                                  const uint32_t *__restrict__ row_state, int nowait,
-                                                 uint8_t *__restrict__ status, const Counters *__restrict__ ctr) {
-    if (input_err(ctr)) return;
+                                                 uint64_t *__restrict__ kill_bits, const Counters *__restrict__ ctr) {
+    if (input_err(ctr) || ctr->halt) return;
     const uint64_t first = ctr->a_acc;
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
-    for (uint64_t i0 = first + ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; i0 < n; i0 += stride) {
-        uint32_t ar[4], tx[4];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t w0 = first >> 6, nw = (n + 63) >> 6;
+    const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
+    for (uint64_t w = w0 + ((uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kKillWords; w < nw;
+         w += waves * kKillWords) {
+        uint32_t ar[kKillWords];
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const bool ok = i0 + j < n;
-            ar[j] = ok ? acc_row[i0 + j] : 0u;
-            tx[j] = ok ? acc_txn[i0 + j] : 0u;
+        for (int q = 0; q < kKillWords; q++) {
+            const uint64_t i = ((w + q) << 6) + lane;
+            ar[q] = i >= first && i < n ? acc_row[i] : ~0u;
         }
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            if (i0 + j >= n) continue;
-            const uint32_t s = row_bits(row_state, ar[j] & ~AR_WR);
-            if ((s & RS_WR) || (nowait && s && (ar[j] & AR_WR))) status[tx[j]] = ST_ABORT;
+        for (int q = 0; q < kKillWords; q++) {
+            bool kill = false;
+            if (ar[q] != ~0u) {
+                const uint32_t st = row_bits(row_state, ar[q] & ~AR_WR);
+                kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
+            }
+            const uint64_t m = __ballot(kill);
+            if (lane == 0 && w + q < nw) kill_bits[w + q] = m;
         }
     }
 }
 
-// Txns [K, n_txn) after k_kill: survivors (still undecided) are renumbered
+// any kill bit in accesses [a0, a1)
+__device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_bits, uint32_t a0, uint32_t a1) {
+    if (a0 >= a1) return false;
+    const uint32_t wlo = a0 >> 6, whi = (a1 - 1) >> 6;
+    bool k = false;
+    for (uint32_t w = wlo; w <= whi; w++) {
+        uint64_t m = kill_bits[w];
+        if (w == wlo) m &= ~0ull << (a0 & 63);
+        if (w == whi) m &= ~0ull >> (63 - ((a1 - 1) & 63));
+        k |= m != 0;
+    }
+    return k;
+}
+
+// Txns [K, n_txn) after k_kill: a txn with a kill bit in its access range
+// aborts (status byte), the others -- survivors -- are renumbered
 // 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
 // and their sort keys written densely in that order, pairs_b = row << 32 |
 // sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
@@ -100,8 +122,9 @@ __global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ ac
 // last tile publishes S and the access count (b_txn, b_acc).
 __global__ __launch_bounds__(kBlock) void k_kill_compact(
     const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
-    const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint8_t *__restrict__ status,
-    uint32_t *__restrict__ map, uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b,
+    const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint64_t *__restrict__ kill_bits,
+    uint8_t *__restrict__ status, uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
+    uint8_t *__restrict__ tlen_b,
     uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
     Counters *ctr) {
     __shared__ uint32_t s_tile;
@@ -110,7 +133,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
-    if (blockIdx.x >= ntiles || input_err(ctr)) return;  // (b_txn = b_acc = 0 from the epoch clear)
+    if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;  // (b_txn = b_acc = 0 from the epoch clear)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
     __syncthreads();
@@ -123,8 +146,12 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         const uint32_t t = first + j;
         a0s[j] = 0;
         lens[j] = 0;
-        if (t >= n_txn || status[t] != ST_UNDEC) continue;  // past the end, or killed (k_kill)
+        if (t >= n_txn) continue;
         const uint32_t a0 = tb_start[t], a1 = tb_end[t];
+        if (range_killed(kill_bits, a0, a1)) {  // a committed prefix txn holds one of its rows
+            status[t] = ST_ABORT;
+            continue;
+        }
         a0s[j] = a0;
         lens[j] = a1 - a0;
         surv |= 1u << j;
@@ -224,16 +251,20 @@ void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb
 
 uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKillTile; }
 
+uint64_t kill_words(uint64_t n_acc) { return (n_acc + 63) / 64 + 1; }
+
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         const uint32_t *acc_txn, uint64_t n_acc, uint32_t K, uint32_t n_txn,
-                         const uint32_t *row_state, int nowait, uint8_t *status, uint32_t *map, uint8_t *status_b,
-                         uint8_t *tlen_b, uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr,
-                         uint32_t tag, Counters *ctr) {
+                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, int nowait,
+                         uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
+                         uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
+                         Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
-    k_kill<<<grid_of(n_acc / 4 + 1, 2048), kBlock, 0, s>>>(acc_row, acc_txn, n_acc, row_state, nowait, status, ctr);
-    k_kill_compact<<<nt, kBlock, 0, s>>>(tb_start, tb_end, acc_row, K, n_txn, status, map, status_b, tlen_b, pairs_b,
-                                         desc_c, desc_a, tile_ctr, tag, ctr);
+    const uint64_t nw = (n_acc + 63) / 64;
+    k_kill<<<grid_of(nw * 64 / kKillWords + 1, 2048), kBlock, 0, s>>>(acc_row, n_acc, row_state, nowait, kill_bits,
+                                                                      ctr);
+    k_kill_compact<<<nt, kBlock, 0, s>>>(tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
+                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -830,6 +830,9 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
 // execution (Counters::halt), and the host resumes the synchronous rounds from
 // the element array the launch started from (dv_epoch_finish).  Facts are
 // monotone, so that array plus the newer statuses is a valid round state.
+#ifndef DVCC_ASYNC_SLEEP
+#define DVCC_ASYNC_SLEEP 8  // back-off (x 64 cycles) of a workgroup whose iteration decided nothing
+#endif
 constexpr int kAsyncThreads = 512;
 constexpr int kAsyncWaves = kAsyncThreads / 64;
 // 28 elements per thread (128 VGPRs, two workgroups per CU): 7.3M live
@@ -1065,7 +1068,7 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         }
         __syncthreads();
         if (s_quit) break;
-        if (!s_moved[p]) __builtin_amdgcn_s_sleep(8);
+        if (DVCC_ASYNC_SLEEP && !s_moved[p]) __builtin_amdgcn_s_sleep(DVCC_ASYNC_SLEEP);
     }
     if (tid == 0) {
         if (yielded) ctr->halt = 1u;  // the finalize hands the rest to the synchronous rounds

@@ -140,6 +140,7 @@ struct dv_ctx {
     uint8_t *b_status = nullptr, *b_tlen = nullptr;  // the survivors' sub-epoch (txn capacity)
     uint32_t *b_map = nullptr;                      // survivor -> txn
     uint64_t *kdesc = nullptr;                      // k_kill_compact look-back descriptors (2 arrays)
+    uint64_t *kill_bits = nullptr;                  // one bit per access: killed by the prefix's commits
     uint32_t kdesc_n = 0;                           // descriptors per array
 
     // timing
@@ -358,7 +359,7 @@ void dv_close(dv_ctx *c) {
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
                     c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
-                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc,
+                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc, c->kill_bits,
                     c->hslot[0].acc, c->hslot[0].tb, c->hslot[1].acc, c->hslot[1].tb};
     for (void *b : bufs) dfree(b);
     for (auto &h : c->hslot) {
@@ -1337,6 +1338,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         r = dalloc(&c->b_status, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_tlen, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_map, T);
+        if (!r) r = dalloc(&c->kill_bits, kill_words(c->cfg.max_acc));
         if (!r) {
             c->kdesc_n = kill_tiles(T) + 1;
             r = dalloc(&c->kdesc, 2ull * c->kdesc_n);
@@ -1379,10 +1381,9 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr);
     const uint32_t tag = next_tag(c);
-    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, ep->acc_txn, ep->n_acc, K, c->n_txn,
-                        c->row_state, nowait, c->status,
-                        c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc, c->kdesc + c->kdesc_n,
-                        next_ticket(c), tag, c->ctr);
+    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, ep->n_acc, K, c->n_txn, c->row_state, nowait,
+                        c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
+                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, ep->n_acc, key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
