@@ -77,6 +77,8 @@ struct Counters {
     uint32_t async_block;     // the rounds of this (sub-)epoch take no further asynchronous tries
     uint32_t a_acc;           // prefix-kill: accesses of the prefix txns
     uint32_t b_txn, b_acc;    // prefix-kill: surviving txns after the prefix, their accesses
+    uint32_t a_halt;          // prefix-kill: the prefix's rounds halted (yield / decline), nothing after ran
+    uint32_t a_rounds;        // prefix-kill: rounds the prefix's decisions took (k_prefix_mark)
     unsigned long long pass_live;  // live accesses every k_round_pass of the epoch read, summed
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
     uint32_t nlive[2];    // live accesses of the current / next decision round
@@ -323,7 +325,7 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
 uint64_t row_state_words(uint64_t rows);
 void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
-                        const Counters *ctr);
+                        Counters *ctr);
 uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (descriptors per array)
 // k_kill (every access after the prefix's against the row state, one bit
 // per access into kill_bits[kill_words(n_acc)]) and k_kill_compact (killed

@@ -47,8 +47,18 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
                                                         const uint32_t *__restrict__ tb_end,
                                                         const uint32_t *__restrict__ acc_row, uint32_t K,
                                                         uint32_t *__restrict__ row_state, int nowait,
-                                                        const Counters *__restrict__ ctr) {
+                                                        Counters *__restrict__ ctr) {
     if (input_err(ctr)) return;
+    // queued behind the prefix's rounds with no host wait: when they halted
+    // (a yielded or declined asynchronous try) nothing after this runs -- the
+    // kill, the compaction, the survivors' stage and the execution all read
+    // halt -- and dv_epoch_finish decides the prefix again synchronously
+    if (ctr->halt) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctr->a_halt = 1u;
+        return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)  // (round 0, then the asynchronous iterations)
+        ctr->a_rounds = ctr->async_r0 ? ctr->async_r0 + ctr->async_iters : 1u;
     for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < K; t += gridDim.x * kBlock) {
         if (status[t] != ST_COMMIT) continue;
         for (uint32_t a = tb_start[t], e = tb_end[t]; a < e; a++) {
@@ -243,7 +253,7 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 
 void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
-                        const Counters *ctr) {
+                        Counters *ctr) {
     (void)hipMemsetAsync(row_state, 0, rs_words * 4, s);
     if (!K) return;
     k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, nowait, ctr);

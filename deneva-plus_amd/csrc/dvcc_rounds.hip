@@ -1144,11 +1144,12 @@ __global__ __launch_bounds__(kBlock) void k_round0_init(uint32_t n, uint32_t n_t
         ctr->nlive[0] = n_dev ? *n_dev : n;
         ctr->nund[0] = n_txn_dev ? *n_txn_dev : n_txn;  // partitioned rounds: round 0's list is every txn
         // a (sub-)epoch's rounds start with no asynchronous try behind them
+        // (halt stays: the epoch clear zeroes it, and a prefix-kill epoch's
+        // survivor stage must keep the prefix's halt, k_prefix_mark)
         ctr->async_go = 0;
         ctr->async_r0 = 0;
         ctr->async_iters = 0;
         ctr->async_block = 0;
-        ctr->halt = 0;
     }
     const uint64_t words = (uint64_t)n_pad << (slog - 4);
     for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)

@@ -134,7 +134,11 @@ struct dv_ctx {
     // prefix-kill epochs (run_prefix_epoch, dvcc_prefix.hip)
     uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 64)
     bool prefix_mode = false;     // the epoch in flight is one
-    uint32_t rounds_prefix = 0;   // rounds the prefix took
+    uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
+    // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
+    uint32_t pf_K = 0, pf_ub_a = 0;
+    int pf_sorted_a = 0, pf_key_bits = 0;
+    uint64_t pf_n_acc = 0;
     uint32_t *row_state = nullptr; // 2 bits per row: the prefix's committed readers / writers
     uint64_t row_state_cap = 0;    // (words)
     uint8_t *b_status = nullptr, *b_tlen = nullptr;  // the survivors' sub-epoch (txn capacity)
@@ -956,6 +960,7 @@ int dv_epoch_round_wait(dv_ctx *c, uint32_t round, uint32_t *undecided) {
 
 namespace {
 int run_rounds(dv_ctx *c, bool resume);
+int redo_prefix(dv_ctx *c);
 
 // the execution of the committed txns and the commit bytes (every execution
 // kernel is a no-op for a rejected epoch, input_err, and while the rounds
@@ -1007,6 +1012,18 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     rec(c, 5);
     int r = hip_fail(hipGetLastError(), "execution launch");
     if (!r) r = sync_counters(c);
+    if (!r && c->prefix_mode && c->h_ctr->a_halt) {
+        // the prefix's rounds halted and nothing behind them ran
+        c->async_unconfirmed = false;
+        r = redo_prefix(c);
+        if (!r) {
+            rec(c, 4);
+            enqueue_exec(c, d_commit);
+            rec(c, 5);
+            r = hip_fail(hipGetLastError(), "execution launch");
+        }
+        if (!r) r = sync_counters(c);
+    }
     if (!r && !calvin && c->h_ctr->halt) {
         // the asynchronous rounds yielded (a workgroup waited too long for
         // facts, e.g. while another kernel held CUs): the execution above was
@@ -1065,7 +1082,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         st->write_cnt = wcnt;
         st->read_digest = dig;
         st->rounds = calvin ? 0 : (c->rounds_real ? c->rounds_real : c->rounds);
-        if (prefix) st->rounds += c->rounds_prefix;  // the prefix's, then the survivors'
+        if (prefix) st->rounds += c->rounds_prefix ? c->rounds_prefix : c->h_ctr->a_rounds;  // + the survivors'
         st->sort_passes = c->sort_passes;
         st->async_launches = (uint16_t)std::min(c->async_launched, 0xFFFFu);
         st->async_declined = (uint16_t)std::min(c->h_ctr->async_declined, 0xFFFFu);
@@ -1265,53 +1282,51 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
     return hip_fail(hipGetLastError(), "stage rounds");
 }
 
-// the outcome of the asynchronous try at round r0 (RoundPub::tl codes 2-5)
-int wait_try(dv_ctx *c, uint32_t r0, uint32_t *code) {
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t i = 0;; i++) {
-        const unsigned long long tl = __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE);
-        if ((uint32_t)(tl >> 32) == r0 && (uint32_t)tl >= 2u) {
-            *code = (uint32_t)tl;
-            return DV_OK;
-        }
-        if ((i & 255) == 255) {
-            const hipError_t q = hipStreamQuery(c->stream);
-            if (q == hipSuccess) {
-                const unsigned long long t2 = __atomic_load_n(&c->h_pub->tl, __ATOMIC_ACQUIRE);
-                if ((uint32_t)(t2 >> 32) == r0 && (uint32_t)t2 >= 2u) {
-                    *code = (uint32_t)t2;
-                    return DV_OK;
-                }
-                return DV_ERR_STATE;
-            }
-            if (q != hipErrorNotReady) return hip_fail(q, "stage stream");
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return DV_ERR_STATE;
-        }
-        __builtin_ia32_pause();
-    }
+// Behind the prefix's rounds, with no host wait: the kill of the later txns
+// that conflict with the prefix's commits, the survivors' sub-epoch (sort
+// keys into pairs[0], the prefix is done with it), its sort and rounds.  Every
+// kernel here is a no-op while the prefix's rounds are halted (k_prefix_mark
+// then sets Counters::a_halt and dv_epoch_finish redoes the prefix).
+int enqueue_survivors(dv_ctx *c) {
+    const bool nowait = c->cfg.cc_alg != DV_OCC;
+    const uint64_t rs_words = row_state_words(c->total_rows);
+    const uint32_t K = c->pf_K;
+    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
+                       c->ctr);
+    const uint32_t tag = next_tag(c);
+    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, K, c->n_txn, c->row_state, nowait,
+                        c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
+                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
+    // the survivors: renumbered 0..S-1, counts on the device
+    c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
+    c->v_status = c->b_status;
+    c->v_tlen = c->b_tlen;
+    c->v_n_txn = c->n_txn - K;
+    c->v_n_txn_dev = &c->ctr->b_txn;
+    return stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc);
 }
 
-// a stage whose decisions the next kernels need: wait for its try, finish it
-// synchronously if the try declined or yielded; returns its rounds
-int stage_complete(dv_ctx *c, uint32_t *rounds) {
-    *rounds = c->rounds_real ? c->rounds_real : c->rounds;
-    if (!c->async_unconfirmed) return DV_OK;
-    uint32_t code = 0;
-    int r = wait_try(c, 1, &code);
-    if (r) return r;
-    c->async_unconfirmed = false;
-    if (code == 4u) {
-        *rounds = 1 + (uint32_t)__atomic_load_n(&c->h_pub->ai, __ATOMIC_ACQUIRE);
-        return DV_OK;
-    }
-    if (code == 5u) {  // round 0 decided everything (or the epoch is rejected)
-        *rounds = 1;
-        return DV_OK;
-    }
+// The prefix's rounds halted (an asynchronous try yielded or declined) and
+// nothing behind them ran: decide the prefix again from scratch with the
+// synchronous rounds (its partial decisions are discarded; the greedy's
+// fixpoint is the same), then queue the survivors' stage again.
+int redo_prefix(dv_ctx *c) {
     HIPCHK(hipMemsetAsync(&c->ctr->halt, 0, sizeof(uint32_t), c->stream));
-    r = run_rounds(c, true);
-    *rounds = c->rounds_real;
-    return r;
+    HIPCHK(hipMemsetAsync(&c->ctr->a_halt, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(hipMemsetAsync(c->status, ST_UNDEC, c->pf_K, c->stream));
+    c->sorted = c->pf_sorted_a;
+    c->v_status = c->status;
+    c->v_tlen = c->tlen;
+    c->v_n_txn = c->pf_K;
+    c->v_n_txn_dev = nullptr;
+    c->v_thresh = 0;
+    const uint32_t flags = c->cfg.flags;
+    c->cfg.flags |= DV_FLAG_NO_ASYNC;
+    int r = stage_rounds(c, &c->ctr->a_acc, c->pf_ub_a);
+    c->cfg.flags = flags;
+    if (r) return r;
+    c->rounds_prefix = c->rounds_real ? c->rounds_real : c->rounds;
+    return enqueue_survivors(c);
 }
 
 // Probe -> prefix: sort + rounds -> kill + compaction -> survivors: sort +
@@ -1346,7 +1361,6 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         if (!r) r = hip_fail(hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream), "memset");
         if (r) return r;
     }
-    const bool nowait = c->cfg.cc_alg != DV_OCC;
     const int key_bits = bits_for(c->total_rows);
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->prefix_mode = true;
@@ -1368,29 +1382,16 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->v_n_txn = K;
     c->v_n_txn_dev = nullptr;
     c->phase = 1;
+    c->pf_K = K;
+    c->pf_ub_a = ub_a;
+    c->pf_sorted_a = c->sorted;
+    c->pf_key_bits = key_bits;
+    c->pf_n_acc = ep->n_acc;
     r = stage_rounds(c, &c->ctr->a_acc, ub_a);
-    if (!r) r = stage_complete(c, &c->rounds_prefix);
-    if (r) {
-        (void)hipStreamSynchronize(c->stream);
-        c->phase = 0;
-        c->prefix_mode = false;
-        return r;
-    }
-    // kill the later txns that conflict with the prefix's commits; the
-    // survivors become a sub-epoch (sort keys into pairs[0], A is done with it)
-    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
-                       c->ctr);
-    const uint32_t tag = next_tag(c);
-    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, ep->n_acc, K, c->n_txn, c->row_state, nowait,
-                        c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
-                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
-    // the survivors: renumbered 0..S-1, counts on the device
-    c->sorted = sort_rows(c, ep->n_acc, key_bits, nullptr, false, &c->ctr->b_acc);
-    c->v_status = c->b_status;
-    c->v_tlen = c->b_tlen;
-    c->v_n_txn = c->n_txn - K;
-    c->v_n_txn_dev = &c->ctr->b_txn;
-    r = stage_rounds(c, &c->ctr->b_acc, (uint32_t)ep->n_acc);
+    // the prefix's rounds ran synchronously (no asynchronous try): their count
+    // is known here; else k_prefix_mark records it (Counters::a_rounds)
+    c->rounds_prefix = c->async_unconfirmed ? 0u : (c->rounds_real ? c->rounds_real : c->rounds);
+    if (!r) r = enqueue_survivors(c);
     if (r) {
         (void)hipStreamSynchronize(c->stream);
         c->phase = 0;
