@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--mpr-sweep", default="0,0.1,0.2,0.3,0.4,0.5",
                     help="N>1: config D's MPR values, each a short extra run ('' = none)")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the 1,048,576-txn-per-GPU run")
+    ap.add_argument("--part-mode", type=int, default=0,
+                    help="N>1: dv_comm_set_mode -- 0 replicated when the epoch fits, else the list protocol; "
+                         "1 list protocol; 2 replicated")
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
@@ -459,13 +462,16 @@ class PartitionedBench:
         self.a, self.world, self.rank, self.R = a, world, rank, R
         # received accesses: this rank's share of every origin's batch (keys
         # spread evenly by key % PART_CNT; multi-partition txns add ~MPR / 2)
-        cap = int(max_txn_rank * R * 1.4) + 65536
+        # ... or the whole epoch, which the replicated protocol decides on every
+        # rank (dv_comm_set_mode 0 picks it when the epoch fits)
+        cap = max(int(max_txn_rank * R * 1.4), CONFIGS[a.config][1] * R) + 65536
         self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
                                  part_id=rank, timing=TIMING[a.timing])
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         self.eng.comm_init(uid[0], world, rank)
+        self.eng.comm_set_mode(a.part_mode)
         self.rows = rows
         self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
 
@@ -549,6 +555,10 @@ def main():
             "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
             "mpr": mpr if world > 1 else 0.0, "part_per_txn": min(2, world),
             "parallelism": f"partitioned x{world} (PART_CNT={world}, RCCL)" if world > 1 else "1 GPU",
+            "protocol": ({0: "replicated (the epoch's accesses all-gathered, decided on every rank, own rows "
+                             "executed) when the epoch fits a context, else the list protocol",
+                          1: "list protocol (owner split, per-round verdict all-reduce)",
+                          2: "replicated"}[a.part_mode] if world > 1 else "single GPU"),
             "distinct_epochs": n_epochs,
         },
         "roofline": roofline(kstats, a, cc_name, world),

@@ -153,6 +153,58 @@ __global__ void k_recv_check(const uint64_t *__restrict__ recvc, uint32_t P, uin
     if (n > cap) xvote[1] |= kVoteOverflow;
 }
 
+// ---- replicated epochs (run_part): every rank receives the whole epoch's
+// access list in the global order -- the batches of ranks 0..P-1, which is
+// Calvin's sequence (work_queue.cpp:105-151) -- decides it alone, and
+// executes its own rows.  Keys travel as 32-bit row ids (a key is the row of
+// the global row space; a key >= 2^31 blocks the mode) with their local txn
+// ids and types: 9 bytes per access, one all-gather.
+constexpr uint32_t kRepBlockWideKey = 1u, kRepBlockOff = 2u;
+
+__global__ __launch_bounds__(kBlock) void k_key_wide(const uint64_t *__restrict__ keys, uint64_t n,
+                                                     uint32_t *__restrict__ block) {
+    bool wide = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
+        wide |= (keys[i] >> 31) != 0;
+    if (__ballot(wide) && (threadIdx.x & 63) == 0) atomicOr(block, kRepBlockWideKey);
+}
+
+// this rank's batch into its gather segment: [row ids | txn ids | types], hmax each
+__global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
+                                                     const uint8_t *__restrict__ types,
+                                                     const uint32_t *__restrict__ txn, uint64_t n, uint64_t hmax,
+                                                     uint8_t *__restrict__ seg) {
+    uint32_t *k32 = reinterpret_cast<uint32_t *>(seg);
+    uint32_t *t32 = reinterpret_cast<uint32_t *>(seg + 4 * hmax);
+    uint8_t *ty = seg + 8 * hmax;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        k32[i] = (uint32_t)keys[i];
+        t32[i] = txn[i];
+        ty[i] = types[i];
+    }
+}
+
+// the gathered segments -> one epoch in rank order, txn ids made global
+__global__ __launch_bounds__(kBlock) void k_rep_unpack(const uint8_t *__restrict__ gath, uint64_t hmax,
+                                                       const uint64_t *__restrict__ cnt, uint32_t P,
+                                                       uint32_t txns_per_rank, uint64_t *__restrict__ keys,
+                                                       uint8_t *__restrict__ types, uint32_t *__restrict__ txn) {
+    for (uint32_t r = blockIdx.y; r < P; r += gridDim.y) {
+        uint64_t off = 0;
+        for (uint32_t q = 0; q < r; q++) off += cnt[q];
+        const uint8_t *seg = gath + (uint64_t)r * 9 * hmax;
+        const uint32_t *k32 = reinterpret_cast<const uint32_t *>(seg);
+        const uint32_t *t32 = reinterpret_cast<const uint32_t *>(seg + 4 * hmax);
+        const uint8_t *ty = seg + 8 * hmax;
+        const uint64_t n = cnt[r] < hmax ? cnt[r] : hmax;
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+            keys[off + i] = k32[i];
+            txn[off + i] = t32[i] + r * txns_per_rank;
+            types[off + i] = ty[i];
+        }
+    }
+}
+
 // ---- in-process group: element-wise MAX of the P ranks' buffers
 constexpr int kMaxLocalRanks = 16;
 template <class T>
@@ -181,7 +233,8 @@ struct DvComm {
     uint8_t *types = nullptr, *tables = nullptr, *verdict = nullptr;
     uint32_t *txn = nullptr, *counts = nullptr, *tot = nullptr, *err = nullptr;
     uint64_t *xcnt = nullptr;  // [2 * nranks]: send counts, received counts
-    uint32_t *xvote = nullptr; // [2]: longest txn, argument flags -- all-reduced (MAX)
+    uint32_t *xvote = nullptr; // [4]: longest txn, argument flags, longest batch, replication blockers (MAX)
+    int mode = 0;              // dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible
     uint32_t *gerr = nullptr;  // input-error bits, all-reduced (MAX)
 };
 
@@ -230,6 +283,8 @@ struct dvcc::Xport {
     virtual int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) = 0;
     virtual int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) = 0;
     virtual int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) = 0;
+    // `bytes` from every rank, rank q's at recv + q * bytes
+    virtual int all_gather(const uint8_t *send, size_t bytes, uint8_t *recv, hipStream_t s) = 0;
 };
 
 namespace {
@@ -255,6 +310,9 @@ struct RcclXport final : Xport {
     }
     int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) override {
         return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint64, ncclMax, comm, s), "ncclAllReduce");
+    }
+    int all_gather(const uint8_t *send, size_t bytes, uint8_t *recv, hipStream_t s) override {
+        return nccl_fail(ncclAllGather(send, recv, bytes, ncclUint8, comm, s), "ncclAllGather");
     }
 };
 
@@ -365,6 +423,14 @@ struct LocalXport final : Xport {
     int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
     int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
     int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int all_gather(const uint8_t *send, size_t bytes, uint8_t *recv, hipStream_t s) override {
+        CHK(publish(send, nullptr, s));
+        for (int q = 0; q < g->P; q++)
+            if (bytes)
+                CHK(hip_fail2(hipMemcpyAsync(recv + (size_t)q * bytes, g->slot[q].send, bytes,
+                                             hipMemcpyDeviceToDevice, s), "copy"));
+        return retire(s);
+    }
 };
 
 void free_bufs(DvComm *m) {
@@ -401,7 +467,7 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->tot, P));
     CHK(alloc(&m->err, 1));
     CHK(alloc(&m->xcnt, 2ull * P));
-    CHK(alloc(&m->xvote, 2));
+    CHK(alloc(&m->xvote, 4));
     CHK(alloc(&m->gerr, 1));
     m->acc_cap = acc;
     m->nb_cap = nb;
@@ -410,6 +476,19 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
 }
 
 }  // namespace
+
+// replicated epochs: the probe's input-error bits combined over the ranks
+// (MAX) into peer_err, on the stream -- a key missing on its owner rejects the
+// epoch on every rank before anything executes
+int comm_combine_errors(dv_ctx *c) {
+    DvComm *m = ctx_comm(c);
+    if (!m) return DV_ERR_STATE;
+    hipStream_t s = ctx_stream(c);
+    uint32_t *w = ctx_err_words(c);  // err, peer_err
+    CHK(hip_fail2(hipMemcpyAsync(m->gerr, w, sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "copy"));
+    CHK(m->x->max_u32(m->gerr, 1, s));
+    return hip_fail2(hipMemcpyAsync(w + 1, m->gerr, sizeof(uint32_t), hipMemcpyDeviceToDevice, s), "copy");
+}
 
 void comm_free(DvComm *m) {
     if (!m) return;
@@ -525,11 +604,56 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     hipStream_t s = ctx_stream(c);
     const uint32_t nb = n_home ? nblocks_for(n_home) : 1;
 
-    // the argument vote: longest txn (sets the verdict-byte stride on every
-    // rank), flags (bad arguments here; owner bytes and capacity below)
-    const uint32_t vote[2] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u};
+    // 1. the first vote -- longest txn (the verdict-byte stride on every
+    //    rank), bad arguments, longest batch, what blocks a replicated epoch
+    //    -- and every rank's batch size
+    const bool rep_here = !tpcc && m->mode != 1 && ctx_rep_capable(c, P);
+    const uint32_t vote[4] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u,
+                              (uint32_t)std::min<uint64_t>(n_home, 0xFFFFFFFFull), rep_here ? 0u : kRepBlockOff};
     CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
-    // 1. split the batch by owner (a bad rank sends nothing)
+    if (n_home && rep_here)
+        k_key_wide<<<std::min<uint32_t>(nb * 16, 1024), kBlock, 0, s>>>(home->keys, n_home, &m->xvote[3]);
+    std::vector<uint64_t> sendc(P, n_home), recvc(P);
+    CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
+    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
+    CHK(m->x->max_u32(m->xvote, 4, s));
+    uint32_t gvote[4] = {0, 0, 0, 0};
+    CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments were bad
+    const uint32_t max_len = std::min<uint32_t>(gvote[0], kMaxPos);
+    const uint64_t hmax = gvote[2];
+    // 2. replicated when every rank allows it and the whole epoch fits this
+    //    context (the same decision on every rank: voted values only)
+    const uint64_t cap = std::min<uint64_t>(cfg.max_acc, m->acc_cap);
+    if (!gvote[3] && (P > 1 || m->mode == 2) && hmax * P <= cap && 9 * hmax * P <= 16 * m->acc_cap) {
+        uint64_t total = 0;
+        for (uint32_t q = 0; q < P; q++) total += recvc[q];
+        if (n_home)
+            k_rep_pack<<<std::min<uint32_t>(nb * 16, 2048), kBlock, 0, s>>>(home->keys, home->types, home->acc_txn,
+                                                                             n_home, hmax,
+                                                                             reinterpret_cast<uint8_t *>(m->send));
+        CHK(hip_fail2(hipGetLastError(), "pack"));
+        CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->send), 9 * hmax,
+                             reinterpret_cast<uint8_t *>(m->recv), s));
+        if (hmax) {
+            const dim3 grid((uint32_t)std::min<uint64_t>((hmax + kBlock - 1) / kBlock, 1024), std::min<uint32_t>(P, 64));
+            k_rep_unpack<<<grid, kBlock, 0, s>>>(reinterpret_cast<const uint8_t *>(m->recv), hmax, m->xcnt + P, P,
+                                                 txns_per_rank, m->keys, m->types, m->txn);
+            CHK(hip_fail2(hipGetLastError(), "unpack"));
+        }
+        dv_epoch_dev ep{};
+        ep.keys = m->keys;
+        ep.types = m->types;
+        ep.acc_txn = m->txn;
+        ep.tables = nullptr;
+        ep.n_acc = total;
+        ep.n_txn = n_txn;
+        ep.max_txn_acc = max_len;
+        return epoch_run_replicated(c, &ep, P, d_commit, st);
+    }
+    // 3. the list protocol: split the batch by owner (a bad rank sends nothing)
     if (n_home) {
         k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, own, n_home, P, m->counts, nb, m->xvote);
         k_owner_scan<<<P, kBlock, 0, s>>>(m->counts, nb, m->tot);
@@ -541,21 +665,19 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         CHK(hip_fail2(hipMemsetAsync(m->tot, 0, P * sizeof(uint32_t), s), "memset"));
     }
     CHK(hip_fail2(hipGetLastError(), "owner split"));
-    // 2. counts, the vote, then the records
+    // per-owner counts, the second vote (owner bytes, capacity), the records
     std::vector<uint32_t> tot(P);
     CHK(hip_fail2(hipMemcpyAsync(tot.data(), m->tot, P * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
-    std::vector<uint64_t> sendc(P), recvc(P);
     for (uint32_t o = 0; o < P; o++) sendc[o] = tot[o];
     CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, m->acc_cap), m->xvote);
+    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, cap, m->xvote);
     CHK(m->x->max_u32(m->xvote, 2, s));
-    uint32_t gvote[2] = {0, 0};
     CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
-    if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments or capacity were bad
+    if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's owner bytes or capacity were bad
     std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
     uint64_t n_recv = 0, so = 0;
     for (uint32_t o = 0; o < P; o++) {
@@ -592,7 +714,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     ep.tables = tpcc ? m->tables : nullptr;
     ep.n_acc = n_recv;
     ep.n_txn = n_txn;
-    ep.max_txn_acc = std::min<uint32_t>(gvote[0], kMaxPos);
+    ep.max_txn_acc = max_len;
     if (tpcc) {
         CHK(dv_tpcc_epoch_begin(c, &ep, m->recv_args, d_oid));
     } else {
@@ -635,6 +757,14 @@ extern "C" {
 int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st) {
     return run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
+}
+
+int dv_comm_set_mode(dv_ctx *c, int mode) {
+    if (!c || mode < 0 || mode > 2) return DV_ERR_ARG;
+    DvComm *m = ctx_comm(c);
+    if (!m) return DV_ERR_STATE;
+    m->mode = mode;
+    return DV_OK;
 }
 
 int dv_tpcc_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, const uint64_t *d_args, const uint8_t *d_owner,

@@ -111,7 +111,26 @@ struct TableDesc {
     uint32_t hash_kind;       // DV_HASH_*
     uint32_t part_cnt;
     uint64_t m_part, m_nb;    // div_magic of part_cnt / nbuckets (key_split)
+    // replicated epochs (dv_epoch_run_part, "replicated sequencing"): every
+    // partition's keys probe here -- rep_part is this context's partition, its
+    // own keys are checked against the local direct map, the others are
+    // range-checked only (their owner checks them), and every key's row is the
+    // key itself (the global row space); kNoRep otherwise
+    uint32_t rep_part;
 };
+constexpr uint32_t kNoRep = 0xFFFFFFFFu;
+
+// replicated epochs: a global row (= key) -> this partition's local row, or
+// false for another partition's row (execution touches own rows only)
+struct RowMap {
+    uint32_t P = 0, part = 0;  // P == 0: rows are local already
+};
+__device__ __forceinline__ bool own_row(const RowMap &m, uint64_t &row) {
+    if (m.P == 0) return true;
+    if (row % m.P != m.part) return false;
+    row /= m.P;
+    return true;
+}
 
 // Key tag of an implicit-row direct map.  A bucket's keys differ only in
 // what the bucket function drops: with DV_HASH_YCSB, b = (k / P) % nb, a key
@@ -306,6 +325,13 @@ dvcc::DvComm *&ctx_comm(dv_ctx *c);
 hipStream_t ctx_stream(dv_ctx *c);
 const dv_config &ctx_config(dv_ctx *c);
 bool ctx_has_tables(dv_ctx *c);  // some table is loaded (dv_epoch_begin's precondition)
+// replicated epochs (dvcc_comm.hip run_part): table 0 is a loaded YCSB
+// implicit-row map whose global row space (nranks x buckets) fits 31 bits
+bool ctx_rep_capable(dv_ctx *c, uint32_t nranks);
+uint32_t *ctx_err_words(dv_ctx *c);  // &Counters::err (peer_err follows)
+// the whole epoch on this rank, its own rows executed (dvcc_runtime.hip)
+int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, uint32_t nranks, uint8_t *d_commit, dv_stats *st);
+int comm_combine_errors(dv_ctx *c);  // dvcc_comm.hip
 void comm_free(dvcc::DvComm *m);
 namespace dvcc {
 
@@ -347,11 +373,11 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
-                 Counters *ctr);
+                 Counters *ctr, RowMap rm = RowMap{});
 // NO_WAIT / WAIT_DIE / OCC: in txn order over the committed txns
 void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
-                     const uint64_t *pkey, bool fused, Counters *ctr);
+                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm = RowMap{});
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,

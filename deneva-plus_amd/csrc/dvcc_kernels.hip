@@ -39,6 +39,15 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
         set_err(ctr, ERRB_TABLE);
         return false;
     }
+    if (t.rep_part != kNoRep) {  // replicated epoch: the key is the row; own keys checked here
+        uint64_t lo = 0;
+        const uint64_t q = divmod_magic(key, t.part_cnt, t.m_part, lo);
+        bool found = q < t.nbuckets;
+        if (found && lo == t.rep_part) found = direct_holds(t, q, (uint32_t)lo, key);
+        if (!found) set_err(ctr, ERRB_KEY);
+        row = key;
+        return found;
+    }
     uint32_t tag;
     const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
     bool found = false;
@@ -707,7 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pa
                                                  const uint8_t *__restrict__ ew, uint64_t n,
                                                  const uint8_t *__restrict__ status,
                                                  uint64_t *__restrict__ f0,
-                                                 const uint64_t *__restrict__ pkey, Counters *ctr) {
+                                                 const uint64_t *__restrict__ pkey, Counters *ctr, RowMap rm) {
     __shared__ unsigned long long part[4];
     if (input_err(ctr)) return;  // a rejected epoch changes no row
     const uint64_t per_block = (uint64_t)kBlock * kPV;
@@ -733,7 +742,8 @@ __global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pa
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             if (st[j] != ST_COMMIT) continue;
-            const uint64_t row = pair_row(pairs[i0 + j]);
+            uint64_t row = pair_row(pairs[i0 + j]);
+            if (!own_row(rm, row)) continue;  // (replicated epochs: another partition's row)
             if (WRITES) {
                 f0[row] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
                 acc++;
@@ -755,12 +765,12 @@ __global__ __launch_bounds__(kBlock) void k_exec(const uint64_t *__restrict__ pa
 
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
-                 Counters *ctr) {
+                 Counters *ctr, RowMap rm) {
     if (n == 0) return;
     uint64_t blocks = (n + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     if (blocks > 2048) blocks = 2048;
-    k_exec<false><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
-    k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr);
+    k_exec<false><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr, rm);
+    k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr, rm);
 }
 
 // NO_WAIT / WAIT_DIE / OCC: run_ycsb_1 for the committed txns only (acc_row
@@ -780,7 +790,7 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      const uint8_t *__restrict__ status,
                                                      uint64_t *__restrict__ f0,
                                                      const uint64_t *__restrict__ pkey,
-                                                     Counters *ctr) {
+                                                     Counters *ctr, RowMap rm) {
     __shared__ unsigned long long part[2][4];
     if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -815,10 +825,12 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
             if (g >= total) continue;
             const uint32_t tt = base + src;
             const uint32_t ar = acc_row[sa0 + (g - spre)];
+            uint64_t row = ar & ~AR_WR;
+            if (!own_row(rm, row)) continue;  // (replicated epochs: another partition's row)
             if ((MODE & EX_READS) && !(ar & AR_WR))
-                dig += mix64(f0[ar] ^ mix64(((uint64_t)tt << 32) ^ pkey[ar]));
+                dig += mix64(f0[row] ^ mix64(((uint64_t)tt << 32) ^ pkey[row]));
             if ((MODE & EX_WRITES) && (ar & AR_WR)) {
-                f0[ar & ~AR_WR] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+                f0[row] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
                 wcnt++;
             }
         }
@@ -843,18 +855,18 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
 
 void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
-                     const uint64_t *pkey, bool fused, Counters *ctr) {
+                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm) {
     if (n_txn == 0) return;
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
         k_exec_txn<EX_READS | EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn,
-                                                                  status, f0, pkey, ctr);
+                                                                  status, f0, pkey, ctr, rm);
     } else {
         k_exec_txn<EX_READS><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                       pkey, ctr);
+                                                       pkey, ctr, rm);
         k_exec_txn<EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                        pkey, ctr);
+                                                        pkey, ctr, rm);
     }
 }
 

@@ -135,6 +135,7 @@ struct dv_ctx {
     uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 64)
     bool prefix_mode = false;     // the epoch in flight is one
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
+    uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
     int pf_sorted_a = 0, pf_key_bits = 0;
@@ -273,8 +274,15 @@ Tables make_tables(dv_ctx *c) {
         t.t[i].part_cnt = c->cfg.part_cnt ? c->cfg.part_cnt : 1;
         t.t[i].m_part = div_magic(t.t[i].part_cnt);
         t.t[i].m_nb = div_magic(t.t[i].nbuckets);
+        t.t[i].rep_part = (c->rep_P && i == 0) ? c->cfg.part_id : kNoRep;
     }
     return t;
+}
+
+// the row ids this epoch's sort keys and row-state bitmap span: the context's
+// rows, or in a replicated epoch the global row space (a row id is the key)
+uint64_t row_space(const dv_ctx *c) {
+    return c->rep_P ? (uint64_t)c->rep_P * c->tab[0].nbuckets : c->total_rows;
 }
 
 int err_from_bits(uint32_t b) {
@@ -321,6 +329,12 @@ bool ctx_has_tables(dv_ctx *c) {
         if (t.loaded) return true;
     return false;
 }
+bool ctx_rep_capable(dv_ctx *c, uint32_t nranks) {
+    const HostTable &t = c->tab[0];
+    return c->cfg.workload == DV_YCSB && t.loaded && t.implicit_rows && t.hash_kind == DV_HASH_YCSB &&
+           (uint64_t)nranks * t.nbuckets <= 0x7FFFFFFFull;
+}
+uint32_t *ctx_err_words(dv_ctx *c) { return &c->ctr->err; }
 
 extern "C" {
 
@@ -823,8 +837,12 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+    if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
+        const int re = comm_combine_errors(c);
+        if (re) return re;
+    }
     rec(c, 1);
-    const int key_bits = bits_for(c->total_rows);
+    const int key_bits = bits_for(row_space(c));
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
@@ -989,12 +1007,18 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.ctr = c->ctr;
         if (c->tp_oid) (void)hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream);
         launch_tpcc_exec(c->stream, x);
-    } else if (c->cfg.cc_alg == DV_CALVIN) {
-        launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey,
-                    c->ctr);
     } else {
-        launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0,
-                        c->pkey, c->cfg.cc_alg != DV_OCC, c->ctr);
+        RowMap rm{};  // replicated epoch: global rows -> this partition's
+        if (c->rep_P) {
+            rm.P = c->rep_P;
+            rm.part = c->cfg.part_id;
+        }
+        if (c->cfg.cc_alg == DV_CALVIN)
+            launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey, c->ctr,
+                        rm);
+        else
+            launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
+                            c->cfg.cc_alg != DV_OCC, c->ctr, rm);
     }
     launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
 }
@@ -1289,7 +1313,7 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
 // then sets Counters::a_halt and dv_epoch_finish redoes the prefix).
 int enqueue_survivors(dv_ctx *c) {
     const bool nowait = c->cfg.cc_alg != DV_OCC;
-    const uint64_t rs_words = row_state_words(c->total_rows);
+    const uint64_t rs_words = row_state_words(row_space(c));
     const uint32_t K = c->pf_K;
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr);
@@ -1339,7 +1363,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     if (r) return r;
     const uint32_t K = prefix_size(c, ep->n_txn);
     const uint32_t T = c->cfg.max_txn;
-    const uint64_t rs_words = row_state_words(c->total_rows);
+    const uint64_t rs_words = row_state_words(row_space(c));
     if (!c->row_state || c->row_state_cap < rs_words) {
         HIPCHK(hipStreamSynchronize(c->stream));
         dfree(c->row_state);
@@ -1361,7 +1385,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         if (!r) r = hip_fail(hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream), "memset");
         if (r) return r;
     }
-    const int key_bits = bits_for(c->total_rows);
+    const int key_bits = bits_for(row_space(c));
     c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
     c->prefix_mode = true;
     rec(c, 0);
@@ -1371,6 +1395,10 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+    if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
+        r = comm_combine_errors(c);
+        if (r) return r;
+    }
     rec(c, 1);
     // the prefix: txns [0, K), the first ctr->a_acc accesses
     const uint32_t ub_a = (uint32_t)std::min<uint64_t>(ep->n_acc, (uint64_t)K * (ep->max_txn_acc ? ep->max_txn_acc
@@ -1425,6 +1453,23 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
     }
     return dv_epoch_finish(c, d_commit, st);
 }
+
+}  // extern "C"
+
+// A replicated epoch (dv_epoch_run_part): the whole epoch's accesses, the
+// global txn order, on this rank; every key's row id is the key, keys of this
+// partition are checked against its index and the error bits combined over
+// the ranks after the probe, all txns are decided here, and only this
+// partition's rows execute.  Every rank computes the same decisions.
+int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, uint32_t nranks, uint8_t *d_commit, dv_stats *st) {
+    if (!c || !ep || nranks == 0) return DV_ERR_ARG;
+    c->rep_P = nranks;
+    const int r = dv_epoch_run_device(c, ep, d_commit, nullptr, st);
+    c->rep_P = 0;
+    return r;
+}
+
+extern "C" {
 
 // TPC-C epochs: the last-name lookups resolve into a scratch copy of the
 // epoch, which then runs the generic path; dv_epoch_finish executes the

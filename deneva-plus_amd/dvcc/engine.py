@@ -282,6 +282,10 @@ class CCEngine:
         arr = (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
         L.check(L.lib().dv_comm_init_local(arr, len(engines)), "dv_comm_init_local")
 
+    def comm_set_mode(self, mode):
+        """dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible."""
+        L.check(L.lib().dv_comm_set_mode(self._ctx, mode), "dv_comm_set_mode")
+
     def run_epoch_part(self, home, txns_per_rank, d_commit=None):
         """One partitioned epoch from this rank's client batch (DeviceEpoch,
         txn ids local); d_commit: nranks * txns_per_rank device bytes."""

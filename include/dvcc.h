@@ -287,6 +287,18 @@ int dv_comm_init(dv_ctx *ctx, const void *unique_id, int nranks, int rank);
 int dv_comm_init_local(dv_ctx **ctxs, int nranks);
 int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st);
+/* how dv_epoch_run_part runs a YCSB epoch.  The list protocol above moves
+ * each access to its owner and closes every decision round with an
+ * all-reduce; the replicated protocol all-gathers the epoch's accesses (9 B
+ * each: 32-bit row id = key, txn id, type) so every rank holds the whole epoch
+ * in the global order -- what Calvin's sequencer hands every node -- decides
+ * it alone with the single-GPU path (one all-reduce of the owners' key checks
+ * after the probe) and executes only its own rows.  mode 0 (default):
+ * replicated when every rank's table 0 is a YCSB implicit-row map with a
+ * 31-bit global row space and the whole epoch fits the context (max_acc), else
+ * the list protocol; 1: always the list protocol; 2: replicated whenever
+ * possible, also on a one-rank communicator.  Same decisions either way. */
+int dv_comm_set_mode(dv_ctx *ctx, int mode);
 
 /* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
  * same txn statuses after each round, hence the same list of undecided txns

@@ -373,21 +373,25 @@ def _run_group(engines, homes, n_txn):
     return out
 
 
-def _engine_group(cc, world, rows_pp, n_txn, R=10):
+def _engine_group(cc, world, rows_pp, n_txn, R=10, mode=1):
+    """mode: dv_comm_set_mode -- 1 the list protocol (capacity for this
+    rank's share), 2 replicated (capacity for the whole epoch)."""
     engines = []
     for p in range(world):
-        eng = dvcc.CCEngine(cc, n_txn * world, max(64, int(n_txn * world * R * 1.2 / world) + 4096),
-                            part_cnt=world, part_id=p)
+        cap = n_txn * world * R + 4096 if mode == 2 else max(64, int(n_txn * world * R * 1.2 / world) + 4096)
+        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p, asynchronous=(mode != 2))
         eng.load_ycsb_partition(rows_pp)
         engines.append(eng)
     dvcc.CCEngine.comm_init_local(engines)
+    for eng in engines:
+        eng.comm_set_mode(mode)
     return engines
 
 
-def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9):
+def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9, mode=1):
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
-    engines = _engine_group(cc, world, rows_pp, n_txn)
+    engines = _engine_group(cc, world, rows_pp, n_txn, mode=mode)
     tab = O.YcsbTable(rows_pp * world)  # one-partition view: row == key
     f0 = tab.f0.copy()
     for k in range(epochs):
@@ -423,6 +427,26 @@ def test_engine_driver_8_partitions(cc, mpr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+@pytest.mark.parametrize("world,mpr", [(2, 0.3), (8, 0.1), (8, 0.5)])
+def test_engine_driver_replicated(cc, world, mpr):
+    """The replicated protocol (dv_comm_set_mode 2): the epoch's accesses
+    all-gathered, every rank decides the whole epoch with the single-GPU path
+    and executes its own rows -- the same decisions, digests and rows as the
+    oracle (and so as the list protocol).  (The contexts share one GPU, so
+    their asynchronous rounds are off here.)"""
+    _check_group(cc, world, 1 << 14, 4000, mpr, mode=2)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_engine_driver_replicated_prefix_kill():
+    """Config-D-shaped epoch large enough for the prefix-kill path inside the
+    replicated protocol: 4 partitions x 40,000 txns (160,000 in total)."""
+    _check_group(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, epochs=1, mode=2)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_engine_driver_other_widths(world):
     _check_group(dvcc.NO_WAIT, world, 1 << 13, 3000, 0.3, theta=0.99)
@@ -438,15 +462,15 @@ def test_config_d_8_partitions_full(cc, mpr):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.CALVIN])
-def test_engine_driver_error_is_collective(cc):
+@pytest.mark.parametrize("cc,mode", [(dvcc.NO_WAIT, 1), (dvcc.CALVIN, 1), (dvcc.NO_WAIT, 2), (dvcc.CALVIN, 2)])
+def test_engine_driver_error_is_collective(cc, mode):
     """A missing key on one rank: every rank returns DV_ERR_KEY_NOT_FOUND
     (none hangs in a collective), no table changes, and the group runs the
-    next epoch normally."""
+    next epoch normally -- list and replicated protocols."""
     world, rows_pp, n_txn = 4, 1 << 12, 1000
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
                                   strict_ppt=1, mpr=0.3)
-    engines = _engine_group(cc, world, rows_pp, n_txn)
+    engines = _engine_group(cc, world, rows_pp, n_txn, mode=mode)
     before = [eng.read_table(0, rows_pp) for eng in engines]
     batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 5), r) for r in range(world)]
     bad = [dvcc.Epoch(b.keys.copy(), b.types, b.txn_begin) for b in batches]
