@@ -156,52 +156,42 @@ __global__ void k_recv_check(const uint64_t *__restrict__ recvc, uint32_t P, uin
 // ---- replicated epochs (run_part): every rank receives the whole epoch's
 // access list in the global order -- the batches of ranks 0..P-1, which is
 // Calvin's sequence (work_queue.cpp:105-151) -- decides it alone, and
-// executes its own rows.  Keys travel as 32-bit row ids (a key is the row of
-// the global row space; a key >= 2^31 blocks the mode) with their local txn
-// ids and types: 9 bytes per access, one all-gather.
-constexpr uint32_t kRepBlockWideKey = 1u, kRepBlockOff = 2u;
+// executes its own rows.  Per access 9 bytes travel: the key as a 32-bit row
+// id (a key is the row of the global row space, which fits 31 bits; a wider
+// key saturates and fails the probe like any key no partition holds), the
+// txn id made global by its sender, and the type -- three all-gathers into
+// contiguous arrays that are the epoch's own inputs (no unpacking).
+constexpr uint32_t kRepBlockOff = 2u;
 
-__global__ __launch_bounds__(kBlock) void k_key_wide(const uint64_t *__restrict__ keys, uint64_t n,
-                                                     uint32_t *__restrict__ block) {
-    bool wide = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-        wide |= (keys[i] >> 31) != 0;
-    if (__ballot(wide) && (threadIdx.x & 63) == 0) atomicOr(block, kRepBlockWideKey);
-}
-
-// this rank's batch into its gather segment: [row ids | txn ids | types], hmax each
-__global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
-                                                     const uint8_t *__restrict__ types,
-                                                     const uint32_t *__restrict__ txn, uint64_t n, uint64_t hmax,
-                                                     uint8_t *__restrict__ seg) {
-    uint32_t *k32 = reinterpret_cast<uint32_t *>(seg);
-    uint32_t *t32 = reinterpret_cast<uint32_t *>(seg + 4 * hmax);
-    uint8_t *ty = seg + 8 * hmax;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        k32[i] = (uint32_t)keys[i];
-        t32[i] = txn[i];
-        ty[i] = types[i];
-    }
-}
-
-// the gathered segments -> one epoch in rank order, txn ids made global
-__global__ __launch_bounds__(kBlock) void k_rep_unpack(const uint8_t *__restrict__ gath, uint64_t hmax,
-                                                       const uint64_t *__restrict__ cnt, uint32_t P,
-                                                       uint32_t txns_per_rank, uint64_t *__restrict__ keys,
-                                                       uint8_t *__restrict__ types, uint32_t *__restrict__ txn) {
+// unequal batches: the gathered parts (rank q's at q * hmax) packed together
+__global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restrict__ gk,
+                                                        const uint32_t *__restrict__ gt,
+                                                        const uint8_t *__restrict__ gy, uint64_t hmax,
+                                                        const uint64_t *__restrict__ cnt, uint32_t P,
+                                                        uint32_t *__restrict__ k32, uint32_t *__restrict__ t32,
+                                                        uint8_t *__restrict__ ty) {
     for (uint32_t r = blockIdx.y; r < P; r += gridDim.y) {
         uint64_t off = 0;
         for (uint32_t q = 0; q < r; q++) off += cnt[q];
-        const uint8_t *seg = gath + (uint64_t)r * 9 * hmax;
-        const uint32_t *k32 = reinterpret_cast<const uint32_t *>(seg);
-        const uint32_t *t32 = reinterpret_cast<const uint32_t *>(seg + 4 * hmax);
-        const uint8_t *ty = seg + 8 * hmax;
-        const uint64_t n = cnt[r] < hmax ? cnt[r] : hmax;
+        const uint64_t n = cnt[r] < hmax ? cnt[r] : hmax, src = (uint64_t)r * hmax;
         for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-            keys[off + i] = k32[i];
-            txn[off + i] = t32[i] + r * txns_per_rank;
-            types[off + i] = ty[i];
+            k32[off + i] = gk[src + i];
+            t32[off + i] = gt[src + i];
+            ty[off + i] = gy[src + i];
         }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
+                                                     const uint8_t *__restrict__ types,
+                                                     const uint32_t *__restrict__ txn, uint64_t n,
+                                                     uint32_t txn_base, uint32_t *__restrict__ k32,
+                                                     uint32_t *__restrict__ t32, uint8_t *__restrict__ ty) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = keys[i];
+        k32[i] = (k >> 32) ? 0xFFFFFFFFu : (uint32_t)k;
+        t32[i] = txn[i] + txn_base;
+        ty[i] = types[i];
     }
 }
 
@@ -611,8 +601,6 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     const uint32_t vote[4] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u,
                               (uint32_t)std::min<uint64_t>(n_home, 0xFFFFFFFFull), rep_here ? 0u : kRepBlockOff};
     CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
-    if (n_home && rep_here)
-        k_key_wide<<<std::min<uint32_t>(nb * 16, 1024), kBlock, 0, s>>>(home->keys, n_home, &m->xvote[3]);
     std::vector<uint64_t> sendc(P, n_home), recvc(P);
     CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
@@ -623,35 +611,52 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
     if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments were bad
     const uint32_t max_len = std::min<uint32_t>(gvote[0], kMaxPos);
-    const uint64_t hmax = gvote[2];
     // 2. replicated when every rank allows it and the whole epoch fits this
-    //    context (the same decision on every rank: voted values only)
+    //    context (the same decision on every rank: voted and gathered values)
     const uint64_t cap = std::min<uint64_t>(cfg.max_acc, m->acc_cap);
-    if (!gvote[3] && (P > 1 || m->mode == 2) && hmax * P <= cap && 9 * hmax * P <= 16 * m->acc_cap) {
-        uint64_t total = 0;
-        for (uint32_t q = 0; q < P; q++) total += recvc[q];
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < P; q++) total += recvc[q];
+    if (!gvote[3] && (P > 1 || m->mode == 2) && total <= cap && (uint64_t)gvote[2] * P <= m->acc_cap) {
+        // send and receive areas: [row ids 4 B | txn ids 4 B | types 1 B] per access
+        uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
+        uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *st_ = reinterpret_cast<uint32_t *>(sb + 4 * m->acc_cap);
+        uint8_t *sy = sb + 8 * m->acc_cap;
+        uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * m->acc_cap);
+        uint8_t *ry = rb + 8 * m->acc_cap;
         if (n_home)
             k_rep_pack<<<std::min<uint32_t>(nb * 16, 2048), kBlock, 0, s>>>(home->keys, home->types, home->acc_txn,
-                                                                             n_home, hmax,
-                                                                             reinterpret_cast<uint8_t *>(m->send));
+                                                                             n_home, (uint32_t)m->rank * txns_per_rank,
+                                                                             sk, st_, sy);
         CHK(hip_fail2(hipGetLastError(), "pack"));
-        CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->send), 9 * hmax,
-                             reinterpret_cast<uint8_t *>(m->recv), s));
-        if (hmax) {
+        // one all-gather per array, parts padded to the longest batch; equal
+        // batches (the usual case) land contiguous, others are packed after
+        uint64_t hmax = 0;
+        bool equal = true;
+        for (uint32_t q = 0; q < P; q++) {
+            hmax = std::max<uint64_t>(hmax, recvc[q]);
+            equal &= recvc[q] == recvc[0];
+        }
+        CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(sk), 4 * hmax, reinterpret_cast<uint8_t *>(rk), s));
+        CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(st_), 4 * hmax, reinterpret_cast<uint8_t *>(rt), s));
+        CHK(m->x->all_gather(sy, hmax, ry, s));
+        if (!equal) {
+            uint32_t *ck = reinterpret_cast<uint32_t *>(m->keys), *ct = m->txn;
             const dim3 grid((uint32_t)std::min<uint64_t>((hmax + kBlock - 1) / kBlock, 1024), std::min<uint32_t>(P, 64));
-            k_rep_unpack<<<grid, kBlock, 0, s>>>(reinterpret_cast<const uint8_t *>(m->recv), hmax, m->xcnt + P, P,
-                                                 txns_per_rank, m->keys, m->types, m->txn);
-            CHK(hip_fail2(hipGetLastError(), "unpack"));
+            k_rep_compact<<<grid, kBlock, 0, s>>>(rk, rt, ry, hmax, m->xcnt + P, P, ck, ct, m->types);
+            CHK(hip_fail2(hipGetLastError(), "compact"));
+            rk = ck;
+            rt = ct;
+            ry = m->types;
         }
         dv_epoch_dev ep{};
-        ep.keys = m->keys;
-        ep.types = m->types;
-        ep.acc_txn = m->txn;
+        ep.keys = reinterpret_cast<const uint64_t *>(rk);  // (read as 32-bit row ids)
+        ep.types = ry;
+        ep.acc_txn = rt;
         ep.tables = nullptr;
         ep.n_acc = total;
         ep.n_txn = n_txn;
         ep.max_txn_acc = max_len;
-        return epoch_run_replicated(c, &ep, P, d_commit, st);
+        return epoch_run_replicated(c, &ep, rk, P, d_commit, st);
     }
     // 3. the list protocol: split the batch by owner (a bad rank sends nothing)
     if (n_home) {

@@ -212,7 +212,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -330,7 +330,9 @@ bool ctx_has_tables(dv_ctx *c);  // some table is loaded (dv_epoch_begin's preco
 bool ctx_rep_capable(dv_ctx *c, uint32_t nranks);
 uint32_t *ctx_err_words(dv_ctx *c);  // &Counters::err (peer_err follows)
 // the whole epoch on this rank, its own rows executed (dvcc_runtime.hip)
-int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, uint32_t nranks, uint8_t *d_commit, dv_stats *st);
+// keys32: the epoch's keys as 32-bit row ids (ep->keys is then ignored)
+int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
+                         uint8_t *d_commit, dv_stats *st);
 int comm_combine_errors(dv_ctx *c);  // dvcc_comm.hip
 void comm_free(dvcc::DvComm *m);
 namespace dvcc {

@@ -82,6 +82,7 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
 constexpr int kPV = 4;
 template <bool HIST>
 __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *__restrict__ keys,
+                                           const uint32_t *__restrict__ keys32,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n,
@@ -119,9 +120,14 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         if (i0 + kPV <= n) {
             const uint4 t4 = *reinterpret_cast<const uint4 *>(acc_txn + i0);
             txn[0] = t4.x; txn[1] = t4.y; txn[2] = t4.z; txn[3] = t4.w;
-            const ulonglong2 k0 = *reinterpret_cast<const ulonglong2 *>(keys + i0);
-            const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + 2);
-            key[0] = k0.x; key[1] = k0.y; key[2] = k1.x; key[3] = k1.y;
+            if (keys32) {  // replicated epochs: 32-bit row ids (dvcc_comm.hip)
+                const uint4 k4 = *reinterpret_cast<const uint4 *>(keys32 + i0);
+                key[0] = k4.x; key[1] = k4.y; key[2] = k4.z; key[3] = k4.w;
+            } else {
+                const ulonglong2 k0 = *reinterpret_cast<const ulonglong2 *>(keys + i0);
+                const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + 2);
+                key[0] = k0.x; key[1] = k0.y; key[2] = k1.x; key[3] = k1.y;
+            }
             const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0);
             const uint32_t tt = tables ? *reinterpret_cast<const uint32_t *>(tables + i0) : 0u;
 #pragma unroll
@@ -134,7 +140,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             for (int j = 0; j < kPV; j++) {
                 const bool ok = i0 + j < n;
                 txn[j] = ok ? acc_txn[i0 + j] : 0xFFFFFFFFu;
-                key[j] = ok ? keys[i0 + j] : 0ull;
+                key[j] = ok ? (keys32 ? (uint64_t)keys32[i0 + j] : keys[i0 + j]) : 0ull;
                 wr[j] = ok && types[i0 + j] == DV_WR ? 1u : 0u;
                 tb[j] = ok && tables ? tables[i0 + j] : 0u;
             }
@@ -281,6 +287,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
 
 // the fused-histogram variant needs more registers: capped at 6 waves per SIMD
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
+                                                  const uint32_t *__restrict__ keys32,
                                                   const uint8_t *__restrict__ types,
                                                   const uint32_t *__restrict__ acc_txn,
                                                   const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
@@ -288,16 +295,17 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
                                                   Counters *ctr, uint32_t pair_limit) {
-    probe_body<false>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
+    probe_body<false>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
                       ctr, nullptr, 0, pair_limit);
 }
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
-    Tables tabs, const uint64_t *__restrict__ keys, const uint8_t *__restrict__ types,
+    Tables tabs, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ keys32,
+    const uint8_t *__restrict__ types,
     const uint32_t *__restrict__ acc_txn, const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
     uint32_t slog, uint64_t *__restrict__ pairs, uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
     uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
     uint32_t ntiles) {
-    probe_body<true>(tabs, keys, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
+    probe_body<true>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
                      ctr, counts, ntiles, n_txn);
 }
 
@@ -305,7 +313,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0, hipEvent_t ev1) {
+                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
     if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
@@ -313,11 +321,11 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     // (ev0 / ev1: the launch's own dispatch timestamps, no extra packets)
     if (counts)
-        hipExtLaunchKernelGGL(k_probe_hist, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, types,
+        hipExtLaunchKernelGGL(k_probe_hist, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, keys32, types,
                               acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
                               counts, ntiles);
     else
-        hipExtLaunchKernelGGL(k_probe, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, types, acc_txn,
+        hipExtLaunchKernelGGL(k_probe, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, keys32, types, acc_txn,
                               tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
                               pair_limit < n_txn ? pair_limit : n_txn);
 }

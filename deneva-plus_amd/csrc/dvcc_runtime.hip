@@ -136,6 +136,7 @@ struct dv_ctx {
     bool prefix_mode = false;     // the epoch in flight is one
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
+    const uint32_t *keys32 = nullptr;  // ... its keys as 32-bit row ids
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
     int pf_sorted_a = 0, pf_key_bits = 0;
@@ -836,7 +837,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
-                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
     if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
         const int re = comm_combine_errors(c);
         if (re) return re;
@@ -1394,7 +1395,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
-                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
     if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
         r = comm_combine_errors(c);
         if (r) return r;
@@ -1461,11 +1462,14 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
 // partition are checked against its index and the error bits combined over
 // the ranks after the probe, all txns are decided here, and only this
 // partition's rows execute.  Every rank computes the same decisions.
-int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, uint32_t nranks, uint8_t *d_commit, dv_stats *st) {
+int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
+                         uint8_t *d_commit, dv_stats *st) {
     if (!c || !ep || nranks == 0) return DV_ERR_ARG;
     c->rep_P = nranks;
+    c->keys32 = keys32;
     const int r = dv_epoch_run_device(c, ep, d_commit, nullptr, st);
     c->rep_P = 0;
+    c->keys32 = nullptr;
     return r;
 }
 

@@ -439,6 +439,38 @@ def test_engine_driver_replicated(cc, world, mpr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2])
+def test_engine_driver_unequal_batches(mode):
+    """Ranks with fewer txns than txns_per_rank (the rest of their sequence
+    slots are empty txns): unequal parts through the list protocol and the
+    replicated one (padded all-gather, then packed)."""
+    world, rows_pp, tpr = 3, 1 << 13, 1000
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=0.3)
+    batches = [gen.gen(n, dvcc.epoch_seed(r, 9), r) for r, n in enumerate((1000, 700, 851))]
+    padded = []
+    for b in batches:  # the oracle's epoch: each batch's unused slots as empty txns
+        tb = np.concatenate([b.txn_begin, np.full(tpr - b.n_txn, b.txn_begin[-1], np.uint32)])
+        padded.append(dvcc.Epoch(b.keys, b.types, tb))
+    e = dvcc.sequence(padded)
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    c_ref, _, st_ref = O.epoch_run(O.NO_WAIT, tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, tpr, mode=mode)
+    res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], tpr)
+    digest = 0
+    for r, x in enumerate(res):
+        assert not isinstance(x, Exception), f"rank {r}: {x}"
+        c, st = x
+        assert (c == c_ref).all(), f"rank {r}: {(c != c_ref).sum()} mismatches"
+        digest = (digest + st.read_digest) % (1 << 64)
+    assert digest == st_ref.read_digest
+    for p, eng in enumerate(engines):
+        assert (eng.read_table(0, rows_pp) == f0[p::world]).all()
+        eng.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 def test_engine_driver_replicated_prefix_kill():
     """Config-D-shaped epoch large enough for the prefix-kill path inside the
