@@ -841,7 +841,10 @@ constexpr int kAsyncWaves = kAsyncThreads / 64;
 // more than the synchronous rounds it replaces -- every iteration re-reads
 // the facts of every live access, and while the queues are long a slice
 // iterates many times per round's worth of progress.
-constexpr int kAsyncIPT = 28;
+#ifndef DVCC_ASYNC_IPT
+#define DVCC_ASYNC_IPT 28
+#endif
+constexpr int kAsyncIPT = DVCC_ASYNC_IPT;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
 constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
 constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
@@ -910,26 +913,19 @@ __device__ __forceinline__ uint32_t async_value(uint32_t e, bool undec, bool abo
     return undec ? ((nowait ? B_UA : 0u) | (wr ? B_UW : 0u)) : ((nowait ? B_CA : 0u) | (wr ? B_CW : 0u));
 }
 
-__global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
-                                                               uint32_t r0, uint32_t thresh,
-                                                               uint32_t *tword, uint32_t *carry,
-                                                               int nowait, uint32_t max_iters,
-                                                               uint64_t idle) {
-    constexpr int IPT = kAsyncIPT;
+// The iteration loop of one workgroup, for slices of at most kAsyncThreads *
+// IPT elements: the kernel instantiates it for small slices too (IPT 4: a
+// prefix-kill stage's live set, a few elements per thread), where the wide
+// instantiation's fully unrolled 28-element loops cost a config-D epoch 38 us.
+template <int IPT>
+__device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t *src, uint32_t r0,
+                                             uint32_t *tword, uint32_t *carry, int nowait, uint32_t max_iters,
+                                             uint64_t idle, uint32_t *sel, RAgg *rw, Agg *wt, uint32_t *s_needy,
+                                             uint32_t *s_moved, uint32_t &s_cin, uint32_t &s_quit) {
     using M = uint32_t;  // per-thread element bit masks
-    __shared__ uint32_t sel[kAsyncCap];
-    __shared__ RAgg rw[kAsyncWaves];
-    __shared__ Agg wt[kAsyncWaves];
-    // per-iteration counters, double-buffered by iteration parity: slot p is
-    // reset during the iteration before it is used, after every thread has
-    // read it for the iteration before that
-    __shared__ uint32_t s_needy[2], s_moved[2], s_cin, s_quit;
     Counters *ctr = b.ctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
-    const uint32_t go = async_gate(ctr, r0, G, thresh);
-    if (g == 0 && tid == 0) ctr->async_go = go;  // for the finalize (the gate's inputs change there)
-    if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint32_t n_all = ctr->nlive[r0 & 1];
     const uint32_t lo = (uint32_t)((uint64_t)g * n_all / G), hi = (uint32_t)((uint64_t)(g + 1) * n_all / G);
     uint32_t n = hi - lo;
@@ -1074,6 +1070,34 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         if (yielded) ctr->halt = 1u;  // the finalize hands the rest to the synchronous rounds
         atomicMax(&ctr->async_iters, it);
     }
+}
+
+constexpr int kAsyncIPTSmall = 4;
+
+__global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
+                                                               uint32_t r0, uint32_t thresh,
+                                                               uint32_t *tword, uint32_t *carry,
+                                                               int nowait, uint32_t max_iters,
+                                                               uint64_t idle) {
+    __shared__ uint32_t sel[kAsyncCap];
+    __shared__ RAgg rw[kAsyncWaves];
+    __shared__ Agg wt[kAsyncWaves];
+    // per-iteration counters, double-buffered by iteration parity: slot p is
+    // reset during the iteration before it is used, after every thread has
+    // read it for the iteration before that
+    __shared__ uint32_t s_needy[2], s_moved[2], s_cin, s_quit;
+    Counters *ctr = b.ctr;
+    const uint32_t G = gridDim.x;
+    const uint32_t go = async_gate(ctr, r0, G, thresh);
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->async_go = go;  // for the finalize (its inputs change there)
+    if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
+    const uint32_t n_all = ctr->nlive[r0 & 1];
+    if (((uint64_t)n_all + G - 1) / G <= (uint64_t)kAsyncThreads * kAsyncIPTSmall)  // (uniform)
+        async_slices<kAsyncIPTSmall>(b, src, r0, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
+                                     s_moved, s_cin, s_quit);
+    else
+        async_slices<kAsyncIPT>(b, src, r0, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy, s_moved,
+                                s_cin, s_quit);
 }
 
 // after the asynchronous rounds: the status bytes from the words and the
