@@ -1072,7 +1072,9 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
     }
 }
 
-constexpr int kAsyncIPTSmall = 4;
+// narrower instantiations for small live sets (measured at config D: 1 / 4 /
+// 28 elements per thread 0.565 ms per epoch, 4 / 28 0.574-0.585, 28 alone 0.615)
+constexpr int kAsyncIPTTiny = 1, kAsyncIPTSmall = 4;
 
 __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
                                                                uint32_t r0, uint32_t thresh,
@@ -1092,7 +1094,11 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     if (blockIdx.x == 0 && threadIdx.x == 0) ctr->async_go = go;  // for the finalize (its inputs change there)
     if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint32_t n_all = ctr->nlive[r0 & 1];
-    if (((uint64_t)n_all + G - 1) / G <= (uint64_t)kAsyncThreads * kAsyncIPTSmall)  // (uniform)
+    const uint64_t per = ((uint64_t)n_all + G - 1) / G;  // the largest slice (uniform)
+    if (per <= (uint64_t)kAsyncThreads * kAsyncIPTTiny)
+        async_slices<kAsyncIPTTiny>(b, src, r0, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy, s_moved,
+                                    s_cin, s_quit);
+    else if (per <= (uint64_t)kAsyncThreads * kAsyncIPTSmall)
         async_slices<kAsyncIPTSmall>(b, src, r0, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
                                      s_moved, s_cin, s_quit);
     else
