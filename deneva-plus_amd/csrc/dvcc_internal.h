@@ -360,7 +360,8 @@ uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (de
 // txns aborted, the survivors' sub-epoch)
 uint64_t kill_words(uint64_t n_acc);
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, int nowait,
+                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, uint64_t rs_words,
+                         int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
                          uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
                          Counters *ctr);

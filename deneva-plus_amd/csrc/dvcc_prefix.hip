@@ -29,7 +29,7 @@
 namespace dvcc {
 
 namespace {
-constexpr int kKillIPT = 8;                             // txns per thread in k_kill_compact
+constexpr int kKillIPT = 16;                            // txns per thread in k_kill_compact
 constexpr uint32_t kKillTile = kBlock * kKillIPT;       // txns per tile
 constexpr uint32_t RS_RD = 1u, RS_WR = 2u;
 
@@ -38,7 +38,19 @@ __device__ __forceinline__ uint32_t row_bits(const uint32_t *rs, uint32_t row) {
 }
 }  // namespace
 
-uint64_t row_state_words(uint64_t rows) { return (rows + 15) / 16; }
+// k_kill's LDS copies, so that a later access gathers a bitmap word from L2
+// only when it must -- 10.3M gathers at config D were bound by the L2's
+// request rate (26 of k_kill's 39 us):
+//   the bitmap words of rows [0, kHotRows): zipf's hot rows are the small
+//     keys, so ~58 % of the accesses (top 256K of 16.8M rows) read LDS;
+//   a one-hash Bloom filter (kBloomBits) of the marked rows from kHotRows on,
+//     kept right after the bitmap and cleared with it: a cold access to a row
+//     no committed prefix txn touched reads LDS only.
+constexpr uint32_t kHotRows = 1u << 18, kHotWords = kHotRows / 16;
+constexpr uint32_t kBloomBits = 1u << 19, kBloomWords = kBloomBits / 32;
+__device__ __forceinline__ uint32_t bloom_bit(uint32_t row) { return (row * 0x9E3779B1u) >> (32 - 19); }
+
+uint64_t row_state_words(uint64_t rows) { return (rows + 15) / 16 + kBloomWords; }
 
 // the rows of the committed prefix txns into the bitmap; lane per txn, its
 // accesses from the probe's txn-major acc_row
@@ -46,8 +58,8 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
                                                         const uint32_t *__restrict__ tb_start,
                                                         const uint32_t *__restrict__ tb_end,
                                                         const uint32_t *__restrict__ acc_row, uint32_t K,
-                                                        uint32_t *__restrict__ row_state, int nowait,
-                                                        Counters *__restrict__ ctr) {
+                                                        uint32_t *__restrict__ row_state, uint32_t *__restrict__ bloom,
+                                                        int nowait, Counters *__restrict__ ctr) {
     if (input_err(ctr)) return;
     // queued behind the prefix's rounds with no host wait: when they halted
     // (a yielded or declined asynchronous try) nothing after this runs -- the
@@ -65,7 +77,13 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
             const uint32_t ar = acc_row[a];
             const uint32_t row = ar & ~AR_WR;
             const uint32_t bit = (ar & AR_WR) ? RS_WR : (nowait ? RS_RD : 0u);
-            if (bit) atomicOr(&row_state[row >> 4], bit << ((row & 15u) * 2u));
+            if (bit) {
+                atomicOr(&row_state[row >> 4], bit << ((row & 15u) * 2u));
+                if (row >= kHotRows) {
+                    const uint32_t h = bloom_bit(row);
+                    atomicOr(&bloom[h >> 5], 1u << (h & 31u));
+                }
+            }
         }
     }
 }
@@ -76,16 +94,22 @@ __global__ __launch_bounds__(kBlock) void k_prefix_mark(const uint8_t *__restric
 // access, and the wave's verdicts stored as one ballot word -- k_kill_compact
 // then ORs each txn's range of bits.  (The conflict rule is the one in the
 // header comment; the txn id of an access is never needed here.)
-constexpr int kKillWords = 4;  // ballot words per wave per step (loads in flight)
-__global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
-                                                 const uint32_t *__restrict__ row_state, int nowait,
+constexpr int kKillWords = 8;  // ballot words per wave per step (loads in flight)
+constexpr int kKillBlock = 1024;  // one block per CU (128 KiB of LDS): 16 waves to stream with
+__global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
+                                                 const uint32_t *__restrict__ row_state, uint64_t state_words,
+                                                 const uint32_t *__restrict__ bloom, int nowait,
                                                  uint64_t *__restrict__ kill_bits, const Counters *__restrict__ ctr) {
+    __shared__ uint32_t s_hot[kHotWords], s_bloom[kBloomWords];
     if (input_err(ctr) || ctr->halt) return;
+    for (uint32_t i = threadIdx.x; i < kHotWords; i += kKillBlock) s_hot[i] = i < state_words ? row_state[i] : 0u;
+    for (uint32_t i = threadIdx.x; i < kBloomWords; i += kKillBlock) s_bloom[i] = bloom[i];
+    __syncthreads();
     const uint64_t first = ctr->a_acc;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w0 = first >> 6, nw = (n + 63) >> 6;
-    const uint64_t waves = (uint64_t)gridDim.x * (kBlock / 64);
-    for (uint64_t w = w0 + ((uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6)) * kKillWords; w < nw;
+    const uint64_t waves = (uint64_t)gridDim.x * (kKillBlock / 64);
+    for (uint64_t w = w0 + ((uint64_t)blockIdx.x * (kKillBlock / 64) + (threadIdx.x >> 6)) * kKillWords; w < nw;
          w += waves * kKillWords) {
         uint32_t ar[kKillWords];
 #pragma unroll
@@ -97,7 +121,14 @@ __global__ __launch_bounds__(kBlock) void k_kill(const uint32_t *__restrict__ ac
         for (int q = 0; q < kKillWords; q++) {
             bool kill = false;
             if (ar[q] != ~0u) {
-                const uint32_t st = row_bits(row_state, ar[q] & ~AR_WR);
+                const uint32_t row = ar[q] & ~AR_WR;
+                uint32_t st = 0;
+                if (row < kHotRows) {
+                    st = (s_hot[row >> 4] >> ((row & 15u) * 2u)) & 3u;
+                } else {
+                    const uint32_t h = bloom_bit(row);
+                    if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) st = row_bits(row_state, row);  // maybe marked
+                }
                 kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
             }
             const uint64_t m = __ballot(kill);
@@ -254,9 +285,10 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
                         Counters *ctr) {
-    (void)hipMemsetAsync(row_state, 0, rs_words * 4, s);
+    (void)hipMemsetAsync(row_state, 0, rs_words * 4, s);  // (the bitmap and the Bloom filter after it)
     if (!K) return;
-    k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, nowait, ctr);
+    k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state,
+                                                      row_state + (rs_words - kBloomWords), nowait, ctr);
 }
 
 uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKillTile; }
@@ -264,15 +296,18 @@ uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKill
 uint64_t kill_words(uint64_t n_acc) { return (n_acc + 63) / 64 + 1; }
 
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, int nowait,
+                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, uint64_t rs_words,
+                         int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
                          uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
                          Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
-    k_kill<<<grid_of(nw * 64 / kKillWords + 1, 2048), kBlock, 0, s>>>(acc_row, n_acc, row_state, nowait, kill_bits,
-                                                                      ctr);
+    // (128 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
+    k_kill<<<grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s>>>(acc_row, n_acc, row_state, rs_words - kBloomWords,
+                                                                     row_state + (rs_words - kBloomWords), nowait,
+                                                                     kill_bits, ctr);
     k_kill_compact<<<nt, kBlock, 0, s>>>(tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
                                          tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
 }

@@ -1319,7 +1319,8 @@ int enqueue_survivors(dv_ctx *c) {
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr);
     const uint32_t tag = next_tag(c);
-    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, K, c->n_txn, c->row_state, nowait,
+    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, K, c->n_txn, c->row_state,
+                        rs_words, nowait,
                         c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
                         c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
