@@ -104,6 +104,12 @@ struct TableDesc {
     // ... and its key tags (key_tag below), one byte per row: the probe reads
     // the tag, and the pkey word only behind the kTagWide sentinel
     const uint8_t *ktag;
+    // ... and one bit per row of "the tag is htag", the tag almost every row
+    // of a partition's table carries (YCSB: q = 0, the partition id): a probe
+    // whose key has that tag reads the bit (config D: a 2 MB target that stays
+    // in L2) instead of the byte; nullptr = no such bitmap
+    const uint32_t *hbits;
+    uint32_t htag;
     const IxEntry *ix;        // index entries (direct: [nbuckets]; chained: sorted by bucket)
     const uint32_t *bstart;   // chained: [nbuckets+1] bucket starts; nullptr = direct map
     uint64_t nbuckets;
@@ -175,6 +181,9 @@ __device__ __forceinline__ uint64_t key_split(const TableDesc &t, uint64_t key, 
 }
 // implicit-row direct map: does bucket bk hold the key of tag `tag`?
 __device__ inline bool direct_holds(const TableDesc &t, uint64_t bk, uint32_t tag, uint64_t key) {
+#ifndef DVCC_NO_HOME_BITS
+    if (t.hbits != nullptr && tag == t.htag) return (t.hbits[bk >> 5] >> (bk & 31)) & 1u;
+#endif
     const uint32_t tg = t.ktag[bk];
     return tg != kTagWide ? tg == tag : t.pkey[bk] == key;
 }
@@ -279,7 +288,10 @@ void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, u
                 hipEvent_t ev1);
 // single GPU: settle statuses from the verdicts, walking the undecided-txn
 // list (ub = upper bound of its length)
-void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub);
+// tword / carry / G: round 0 with an asynchronous launch at round 1 behind it
+// (round_async with words_done): the settle writes its fact and carry words
+void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub,
+                  uint32_t *tword = nullptr, uint32_t *carry = nullptr, uint32_t G = 0);
 // partitioned: this partition's verdict byte (bit1 abort, bit0 wait) for every
 // entry of round `round`'s undecided list, in list order (ub: bound of the
 // list length); then apply the MAX-combined bytes, compact the list for the
@@ -311,7 +323,7 @@ constexpr uint32_t kAsyncGroups = 512;
 // pub->tl = r0 << 32 | 3 instead of closing the rounds (the host resumes them).
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
                  uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
-                 uint64_t idle_ticks);
+                 uint64_t idle_ticks, bool words_done = false);
 uint32_t async_groups(int device);  // co-resident workgroups (<= kAsyncGroups; 0: unusable)
 uint32_t async_try_limit(uint32_t G);
 // round elements ((txn << slog | pos) << 3 | flags) fit 32 bits
@@ -372,7 +384,8 @@ void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *
 // status (value; padding aborted), access ranges and counts
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        const uint32_t *err_seed, Counters *ctr);
+                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
+                        uint64_t zero_words = 0);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
@@ -385,6 +398,8 @@ void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uin
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag);
+// bits[w] bit j = (ktag[32 w + j] == htag), rows [0, n)
+void launch_home_bits(hipStream_t s, const uint8_t *ktag, uint64_t n, uint32_t htag, uint32_t *bits);
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
                         uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr);
 void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,

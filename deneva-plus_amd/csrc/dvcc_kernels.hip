@@ -79,7 +79,11 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
 // of equal txns is a max-scan of run-start indices over the wave; a run that
 // began in an earlier wave is walked back in memory (at most one per wave).
 // Repeated rows inside a txn are detected later, in row order (seg_prepare).
-constexpr int kPV = 4;
+#ifndef DVCC_PROBE_PV
+#define DVCC_PROBE_PV 4
+#endif
+constexpr int kPV = DVCC_PROBE_PV;
+static_assert(kPV % 4 == 0, "vector loads of 4 accesses");
 template <bool HIST>
 __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *__restrict__ keys,
                                            const uint32_t *__restrict__ keys32,
@@ -118,22 +122,25 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         uint32_t txn[kPV], wr[kPV], tb[kPV];
         uint64_t key[kPV], row[kPV];
         if (i0 + kPV <= n) {
-            const uint4 t4 = *reinterpret_cast<const uint4 *>(acc_txn + i0);
-            txn[0] = t4.x; txn[1] = t4.y; txn[2] = t4.z; txn[3] = t4.w;
-            if (keys32) {  // replicated epochs: 32-bit row ids (dvcc_comm.hip)
-                const uint4 k4 = *reinterpret_cast<const uint4 *>(keys32 + i0);
-                key[0] = k4.x; key[1] = k4.y; key[2] = k4.z; key[3] = k4.w;
-            } else {
-                const ulonglong2 k0 = *reinterpret_cast<const ulonglong2 *>(keys + i0);
-                const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + 2);
-                key[0] = k0.x; key[1] = k0.y; key[2] = k1.x; key[3] = k1.y;
-            }
-            const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0);
-            const uint32_t tt = tables ? *reinterpret_cast<const uint32_t *>(tables + i0) : 0u;
 #pragma unroll
-            for (int j = 0; j < kPV; j++) {
-                wr[j] = ((ty >> (8 * j)) & 0xFFu) == DV_WR ? 1u : 0u;
-                tb[j] = (tt >> (8 * j)) & 0xFFu;
+            for (int q = 0; q < kPV; q += 4) {
+                const uint4 t4 = *reinterpret_cast<const uint4 *>(acc_txn + i0 + q);
+                txn[q] = t4.x; txn[q + 1] = t4.y; txn[q + 2] = t4.z; txn[q + 3] = t4.w;
+                if (keys32) {  // replicated epochs: 32-bit row ids (dvcc_comm.hip)
+                    const uint4 k4 = *reinterpret_cast<const uint4 *>(keys32 + i0 + q);
+                    key[q] = k4.x; key[q + 1] = k4.y; key[q + 2] = k4.z; key[q + 3] = k4.w;
+                } else {
+                    const ulonglong2 k0 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + q);
+                    const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + q + 2);
+                    key[q] = k0.x; key[q + 1] = k0.y; key[q + 2] = k1.x; key[q + 3] = k1.y;
+                }
+                const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0 + q);
+                const uint32_t tt = tables ? *reinterpret_cast<const uint32_t *>(tables + i0 + q) : 0u;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    wr[q + j] = ((ty >> (8 * j)) & 0xFFu) == DV_WR ? 1u : 0u;
+                    tb[q + j] = (tt >> (8 * j)) & 0xFFu;
+                }
             }
         } else {
 #pragma unroll
@@ -178,14 +185,21 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         }
         uint64_t ex = __shfl_up(inc, 1, 64);
         if (lane == 0) ex = 0;
-        // the wave's first run may have begun before the wave
+        // the wave's first run may have begun before the wave: its start, found
+        // 64 earlier accesses per step by the whole wave (one load, a ballot)
         uint64_t carry = 0;
-        if (lane == 0 && wave0 > 0 && wave0 < n && acc_txn[wave0 - 1] == txn[0]) {
-            uint64_t j = wave0 - 1;
-            while (j > 0 && acc_txn[j - 1] == txn[0]) j--;
-            carry = j + 1;
+        if (wave0 > 0 && wave0 < n) {  // (wave-uniform)
+            const uint32_t t0 = __shfl(txn[0], 0, 64);
+            for (uint64_t base = wave0;; base -= 64) {
+                const bool same = base > lane && acc_txn[base - 1 - lane] == t0;
+                const uint64_t m = __ballot(!same);
+                if (m) {
+                    const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;  // accesses [base - f, base) continue the run
+                    carry = base - f == wave0 ? 0 : base - f + 1;
+                    break;
+                }
+            }
         }
-        carry = __shfl(carry, 0, 64);
         if (ex == 0) ex = carry;
         const uint32_t nxt_lane = __shfl_down(txn[0], 1, 64);
         const uint64_t in_last = i0 + kPV;
@@ -685,7 +699,8 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         uint32_t *__restrict__ tb_end,
                                                         uint8_t *__restrict__ tlen,
                                                         uint32_t *__restrict__ tile_ctr,
-                                                        const uint32_t *__restrict__ err_seed, Counters *ctr) {
+                                                        const uint32_t *__restrict__ err_seed, Counters *ctr,
+                                                        uint4 *__restrict__ zero, uint64_t zero_n) {
     if (blockIdx.x == 0) {
         uint32_t *w = reinterpret_cast<uint32_t *>(ctr);
         for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) w[i] = 0;
@@ -701,15 +716,17 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
         tb_end[i] = 0;
         if (tlen) tlen[i] = 0;
     }
+    for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < zero_n; i += stride) zero[i] = uint4{0, 0, 0, 0};
 }
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        const uint32_t *err_seed, Counters *ctr) {
+                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
-                                       err_seed, ctr);
+                                       err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0);
 }
 
 // ---------------------------------------------------------------- execute
@@ -942,6 +959,18 @@ __global__ void k_ycsb_load(uint64_t rows, uint32_t part_cnt, uint32_t part_id, 
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag) {
     k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey, ktag);
+}
+
+__global__ void k_home_bits(const uint8_t *__restrict__ ktag, uint64_t n, uint32_t htag, uint32_t *__restrict__ bits) {
+    const uint64_t nw = (n + 31) / 32;
+    for (uint64_t w = blockIdx.x * (uint64_t)kBlock + threadIdx.x; w < nw; w += (uint64_t)gridDim.x * kBlock) {
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 32 && w * 32 + j < n; j++) v |= (ktag[w * 32 + j] == htag ? 1u : 0u) << j;
+        bits[w] = v;
+    }
+}
+void launch_home_bits(hipStream_t s, const uint8_t *ktag, uint64_t n, uint32_t htag, uint32_t *bits) {
+    if (n) k_home_bits<<<2048, kBlock, 0, s>>>(ktag, n, htag, bits);
 }
 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,

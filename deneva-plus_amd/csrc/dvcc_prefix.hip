@@ -29,7 +29,10 @@
 namespace dvcc {
 
 namespace {
-constexpr int kKillIPT = 16;                            // txns per thread in k_kill_compact
+#ifndef DVCC_KILL_IPT
+#define DVCC_KILL_IPT 16
+#endif
+constexpr int kKillIPT = DVCC_KILL_IPT;                 // txns per thread in k_kill_compact
 constexpr uint32_t kKillTile = kBlock * kKillIPT;       // txns per tile
 constexpr uint32_t RS_RD = 1u, RS_WR = 2u;
 
@@ -50,7 +53,8 @@ constexpr uint32_t kHotRows = 1u << 18, kHotWords = kHotRows / 16;
 constexpr uint32_t kBloomBits = 1u << 19, kBloomWords = kBloomBits / 32;
 __device__ __forceinline__ uint32_t bloom_bit(uint32_t row) { return (row * 0x9E3779B1u) >> (32 - 19); }
 
-uint64_t row_state_words(uint64_t rows) { return (rows + 15) / 16 + kBloomWords; }
+// (a multiple of 4 words: k_epoch_clear zeroes it in 16-byte stores)
+uint64_t row_state_words(uint64_t rows) { return (((rows + 15) / 16 + 3) & ~3ull) + kBloomWords; }
 
 // the rows of the committed prefix txns into the bitmap; lane per txn, its
 // accesses from the probe's txn-major acc_row
@@ -206,23 +210,15 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         wt_a[wave] = inc_a;
     }
     __syncthreads();
-    if (wave == 0) {
-        Agg bc{0u, 0u, 0u}, ba{0u, 0u, 0u};
-        for (int w = 0; w < kBlock / 64; w++) {
-            bc = OpPlain::comb(bc, wt_c[w]);
-            ba = OpPlain::comb(ba, wt_a[w]);
-        }
-        const Agg pc = look_back<OpPlain>(desc_c, tile, tag, bc, lane, ctr);
-        const Agg pa = look_back<OpPlain>(desc_a, tile, tag, ba, lane, ctr);
+    if (wave < 2) {  // the two look-backs side by side: wave 0 survivors, wave 1 their accesses
+        const Agg *wt = wave == 0 ? wt_c : wt_a;
+        Agg bt{0u, 0u, 0u};
+        for (int w = 0; w < kBlock / 64; w++) bt = OpPlain::comb(bt, wt[w]);
+        const Agg pt = look_back<OpPlain>(wave == 0 ? desc_c : desc_a, tile, tag, bt, lane, ctr);
         if (lane == 0) {
-            s_sub0 = pc.c;
-            s_ab0 = pa.c;
-            s_nsurv = bc.c;
-            s_nacc = ba.c;
-            if (tile == ntiles - 1) {
-                ctr->b_txn = pc.c + bc.c;
-                ctr->b_acc = pa.c + ba.c;
-            }
+            (wave == 0 ? s_sub0 : s_ab0) = pt.c;
+            (wave == 0 ? s_nsurv : s_nacc) = bt.c;
+            if (tile == ntiles - 1) (wave == 0 ? ctr->b_txn : ctr->b_acc) = pt.c + bt.c;
         }
     }
     // this thread's survivors: their slots in the tile's list
@@ -251,17 +247,29 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     __syncthreads();
     // the survivors' sort keys: one access per thread, its survivor found by
     // binary search over the access prefix
+    // (kCompactU accesses per thread per step: their row gathers in flight together)
+    constexpr uint32_t kCompactU = 4;
     const uint32_t ns = s_nsurv, na = s_nacc, ab0 = s_ab0;
-    for (uint32_t g = tid; g < na; g += kBlock) {
-        uint32_t lo = 0, hi = ns;  // largest k with l_pre[k] <= g
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (l_pre[mid] <= g) lo = mid;
-            else hi = mid;
+    for (uint32_t g0 = 0; g0 < na; g0 += kBlock * kCompactU) {
+        uint32_t sv[kCompactU], qv[kCompactU], ar[kCompactU];
+#pragma unroll
+        for (uint32_t u = 0; u < kCompactU; u++) {
+            const uint32_t g = g0 + u * kBlock + tid;
+            uint32_t lo = 0, hi = ns;  // largest k with l_pre[k] <= g
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (l_pre[mid] <= g) lo = mid;
+                else hi = mid;
+            }
+            sv[u] = lo;
+            qv[u] = g - l_pre[lo];
+            ar[u] = g < na ? acc_row[l_a0[lo] + qv[u]] : 0u;
         }
-        const uint32_t q = g - l_pre[lo];
-        const uint32_t ar = acc_row[l_a0[lo] + q];
-        pairs_b[ab0 + g] = pair_pack(ar & ~AR_WR, sub0 + lo, q, ar >> 31);
+#pragma unroll
+        for (uint32_t u = 0; u < kCompactU; u++) {
+            const uint32_t g = g0 + u * kBlock + tid;
+            if (g < na) pairs_b[ab0 + g] = pair_pack(ar[u] & ~AR_WR, sub0 + sv[u], qv[u], ar[u] >> 31);
+        }
     }
 }
 
@@ -285,7 +293,7 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
                         Counters *ctr) {
-    (void)hipMemsetAsync(row_state, 0, rs_words * 4, s);  // (the bitmap and the Bloom filter after it)
+    // (the bitmap and the Bloom filter after it were zeroed by k_epoch_clear)
     if (!K) return;
     k_prefix_mark<<<grid_of(K, 1024), kBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state,
                                                       row_state + (rs_words - kBloomWords), nowait, ctr);

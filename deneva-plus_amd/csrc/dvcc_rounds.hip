@@ -39,6 +39,8 @@ namespace {
 // scan value bits (OR): 1 committed / 2 undecided (any access), 4 committed /
 // 8 undecided (WR accesses), 16 = the access is kept for the next round
 constexpr uint32_t B_CA = 1u, B_UA = 2u, B_CW = 4u, B_UW = 8u, B_KEEP = 16u;
+constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
+constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
 constexpr uint8_t VB_OK = 1, VB_ABORT = 2;
 constexpr uint32_t F_WR = 1u, F_HEAD = 2u, F_DONE = 4u;
 
@@ -448,8 +450,8 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
 // ---- per-txn settle (single GPU): new status from its accesses' verdicts
 // The verdict bytes of txn t are vb8[t << slog, (t << slog) + len): one
 // 16-byte load per 16 accesses (slog >= 4).
-__device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, uint32_t len) {
-    uint32_t any_abort = 0, all_ok = 1;
+__device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, uint32_t len, uint32_t *n_ok = nullptr) {
+    uint32_t any_abort = 0, all_ok = 1, ok = 0;
     for (uint32_t w = 0; w < len; w += 16) {
         const uint4 x4 = *reinterpret_cast<const uint4 *>(v + w);
         const uint32_t x[4] = {x4.x, x4.y, x4.z, x4.w};
@@ -459,8 +461,10 @@ __device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, ui
             const uint32_t m = nb >= 4 ? 0xFFFFFFFFu : (nb <= 0 ? 0u : (1u << (8 * nb)) - 1u);
             any_abort |= x[q] & 0x02020202u & m;
             all_ok &= (x[q] & m) == (0x01010101u & m);
+            if (n_ok) ok += __popc(x[q] & 0x01010101u & m);
         }
     }
+    if (n_ok) *n_ok = ok;
     return any_abort ? V_ABORT : (all_ok ? 0 : V_WAIT);
 }
 
@@ -469,14 +473,24 @@ __device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, ui
 // compacts its survivors in LDS and reserves space with ONE atomic.
 constexpr uint32_t kSettleIPT = 4, kSettleChunk = kBlock * kSettleIPT;
 
+// tword (round 0 with an asynchronous launch behind it): also the txn's fact
+// word for k_round_async, as k_async_words would write it from the settled
+// state -- status | OK verdicts << 8 | accesses << 16
 __device__ __forceinline__ bool settle_txn(uint8_t *__restrict__ status, const uint8_t *__restrict__ vb8,
                                            uint32_t slog, const uint8_t *__restrict__ tlen,
-                                           uint32_t t) {
-    if (status[t] != ST_UNDEC) return false;  // aborted by the pass
-    const uint8_t v = txn_verdict(vb8 + ((size_t)t << slog), tlen[t]);
-    if (v & V_ABORT) status[t] = ST_ABORT;
-    else if (!(v & V_WAIT)) status[t] = ST_COMMIT;
-    return (v & (V_ABORT | V_WAIT)) == V_WAIT;
+                                           uint32_t t, uint32_t *__restrict__ tword = nullptr) {
+    const uint8_t s0 = status[t];
+    if (s0 != ST_UNDEC) {  // aborted by the pass
+        if (tword) tword[t] = s0 | ((uint32_t)tlen[t] << 16);
+        return false;
+    }
+    const uint32_t len = tlen[t];
+    uint32_t ok = 0;
+    const uint8_t v = txn_verdict(vb8 + ((size_t)t << slog), len, tword ? &ok : nullptr);
+    const uint8_t s = (v & V_ABORT) ? ST_ABORT : (!(v & V_WAIT) ? ST_COMMIT : ST_UNDEC);
+    if (s != ST_UNDEC) status[t] = s;
+    if (tword) tword[t] = s | ((s == ST_UNDEC ? ok : 0u) << 8) | (len << 16);
+    return s == ST_UNDEC;
 }
 
 struct SettleLds {
@@ -492,7 +506,8 @@ __device__ __forceinline__ void settle_chunk(SettleLds &sh, uint32_t lo, uint32_
                                              const uint8_t *__restrict__ tlen,
                                              const uint32_t *__restrict__ list_in,
                                              uint32_t *__restrict__ list_out,
-                                             uint32_t *__restrict__ n_out) {
+                                             uint32_t *__restrict__ n_out,
+                                             uint32_t *__restrict__ tword = nullptr) {
     if (threadIdx.x == 0) sh.cnt = 0;
     __syncthreads();
     const uint32_t lane = threadIdx.x & 63;
@@ -503,7 +518,7 @@ __device__ __forceinline__ void settle_chunk(SettleLds &sh, uint32_t lo, uint32_
         bool keep = false;
         if (i < n) {
             t = FIRST ? i : list_in[i];
-            keep = settle_txn(status, vb8, slog, tlen, t);
+            keep = settle_txn(status, vb8, slog, tlen, t, tword);
         }
         const uint64_t m = __ballot(keep);
         uint32_t wb = 0;
@@ -524,13 +539,16 @@ __global__ __launch_bounds__(kBlock) void k_round_settle(
     uint8_t *__restrict__ status, const uint8_t *__restrict__ vb8, uint32_t slog,
     const uint8_t *__restrict__ tlen, const uint32_t *__restrict__ list_in,
     const uint32_t *__restrict__ n_in, uint32_t n_txn, uint32_t *__restrict__ list_out,
-    uint32_t *__restrict__ n_out) {
+    uint32_t *__restrict__ n_out, uint32_t *__restrict__ tword, uint32_t *__restrict__ carry, uint32_t G) {
     __shared__ SettleLds sh;
     // round 0: every txn of the (sub-)epoch (its real count from round0_init)
     const uint32_t n = n_in ? *n_in : n_txn;
     const uint32_t lo = blockIdx.x * kSettleChunk;
     if (lo >= n) return;
-    settle_chunk<FIRST>(sh, lo, n, status, vb8, slog, tlen, list_in, list_out, n_out);
+    // (the asynchronous launch's carry words start pessimistic, k_async_words)
+    if (carry && blockIdx.x == 0)
+        for (uint32_t g = threadIdx.x; g < G; g += kBlock) carry[g] = kCarryInit;
+    settle_chunk<FIRST>(sh, lo, n, status, vb8, slog, tlen, list_in, list_out, n_out, tword);
 }
 
 // ---- partitioned rounds over the undecided-txn list -----------------------
@@ -846,8 +864,6 @@ constexpr int kAsyncWaves = kAsyncThreads / 64;
 #endif
 constexpr int kAsyncIPT = DVCC_ASYNC_IPT;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
-constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
-constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
 
 constexpr uint32_t TW_OK = 1u << 8;  // one more access OK
 
@@ -1249,9 +1265,10 @@ void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, Roun
 
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
                  uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
-                 uint64_t idle_ticks) {
+                 uint64_t idle_ticks, bool words_done) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
-    k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
+    if (!words_done)  // (else round 0's settle wrote them: round_settle with tword)
+        k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
                                                                     b.n_txn_dev, b.ctr);
     k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
@@ -1273,17 +1290,18 @@ uint32_t async_groups(int device) {
 
 uint32_t async_try_limit(uint32_t G) { return G * kAsyncCap; }
 
-void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub) {
+void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub, uint32_t *tword,
+                  uint32_t *carry, uint32_t G) {
     const uint32_t n = round == 0 ? n_txn : (ub < n_txn ? ub : n_txn);
     const uint32_t nb = n ? (n + kSettleChunk - 1) / kSettleChunk : 1;
     uint32_t *n_out = &b.ctr->nund[(round + 1) & 1];
     if (round == 0)
         k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, nullptr, &b.ctr->nund[0],
-                                                   n_txn, b.ulist[1], n_out);
+                                                   n_txn, b.ulist[1], n_out, tword, carry, G);
     else
         k_round_settle<false><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
                                                     b.ulist[round & 1], &b.ctr->nund[round & 1],
-                                                    n_txn, b.ulist[(round + 1) & 1], n_out);
+                                                    n_txn, b.ulist[(round + 1) & 1], n_out, nullptr, nullptr, 0u);
 }
 
 void list_verdict(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, uint8_t *verdict) {

@@ -30,6 +30,8 @@ struct HostTable {
     uint32_t hash_kind = DV_HASH_YCSB;
     IxEntry *ix = nullptr;      // device
     uint32_t *bstart = nullptr; // device (chained only)
+    uint32_t *hbits = nullptr;  // device: home-tag bitmap of an implicit-row map (TableDesc::hbits)
+    uint32_t htag = kTagWide;
     uint64_t ix_cap = 0;
 };
 
@@ -268,6 +270,8 @@ Tables make_tables(dv_ctx *c) {
         t.t[i].ix = h.ix;
         t.t[i].pkey = h.implicit_rows ? c->pkey + h.row_base : nullptr;
         t.t[i].ktag = h.implicit_rows ? c->ktag + h.row_base : nullptr;
+        t.t[i].hbits = h.implicit_rows ? h.hbits : nullptr;
+        t.t[i].htag = h.htag;
         t.t[i].bstart = h.bstart;
         t.t[i].nbuckets = h.nbuckets ? h.nbuckets : 1;
         t.t[i].row_base = h.row_base;
@@ -370,6 +374,7 @@ void dv_close(dv_ctx *c) {
     for (auto &t : c->tab) {
         dfree(t.ix);
         dfree(t.bstart);
+        dfree(t.hbits);
     }
     void *bufs[] = {c->f0, c->pkey, c->ktag, c->pairs[0], c->pairs[1], c->el, c->ew, c->counts,
                     c->digit_tot, c->rel[0], c->rel[1], c->vb8, c->tlen, c->acc_row,
@@ -594,6 +599,22 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     return DV_OK;
 }
 
+// The home-tag bitmap of an implicit-row table: one bit per row, set where
+// the row's key tag is htag (TableDesc::hbits; htag = kTagWide: none).
+int build_home_bits(dv_ctx *c, HostTable &t, uint32_t htag) {
+    dfree(t.hbits);
+    t.hbits = nullptr;
+    t.htag = kTagWide;
+    if (htag >= kTagWide || !t.implicit_rows || t.nbuckets == 0) return DV_OK;
+    int r = dalloc(&t.hbits, (t.nbuckets + 31) / 32);
+    if (r) return r;
+    launch_home_bits(c->stream, c->ktag + t.row_base, t.nbuckets, htag, t.hbits);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    t.htag = htag;
+    return DV_OK;
+}
+
 // table_t::get_new_row + IndexHash::index_insert for n rows (row i = keys[i]).
 // Chains keep BucketHeader::insert_item order (index_hash.cpp:172-201): distinct
 // keys in first-insertion order, repeated keys newest first.
@@ -633,8 +654,11 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
     }
     dfree(t.ix);
     dfree(t.bstart);
+    dfree(t.hbits);
     t.ix = nullptr;
     t.bstart = nullptr;
+    t.hbits = nullptr;
+    t.htag = kTagWide;
     // keys in bucket order: row b is in bucket b, the pkey column is the index
     bool implicit = direct;
     for (uint64_t b = 0; b < nb && implicit; b++) implicit = ent[cnt[b]].row == b;
@@ -656,8 +680,14 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
         HIPCHK(hipMemcpy(c->pkey + t.row_base, keys, n * 8, hipMemcpyHostToDevice));
         if (implicit) {  // row i holds keys[i]
             std::vector<uint8_t> tg(n);
-            for (uint64_t i = 0; i < n; i++) tg[i] = key_tag(t.hash_kind, nb, P, keys[i]);
+            uint64_t hist[256] = {};
+            for (uint64_t i = 0; i < n; i++) hist[tg[i] = key_tag(t.hash_kind, nb, P, keys[i])]++;
             HIPCHK(hipMemcpy(c->ktag + t.row_base, tg.data(), n, hipMemcpyHostToDevice));
+            uint32_t home = 0;  // the most common tag
+            for (uint32_t v = 1; v < kTagWide; v++)
+                if (hist[v] > hist[home]) home = v;
+            r = build_home_bits(c, t, hist[home] ? home : kTagWide);
+            if (r) return r;
         }
     }
     t.n_rows = n;
@@ -684,6 +714,10 @@ int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
                      c->pkey + t.row_base, c->ktag + t.row_base);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
+    // row r holds key r * P + part: every tag is the partition's
+    const int r = build_home_bits(c, t, key_tag(DV_HASH_YCSB, rows_per_part, c->cfg.part_cnt ? c->cfg.part_cnt : 1,
+                                                c->cfg.part_id));
+    if (r) return r;
     t.n_rows = rows_per_part;
     t.loaded = true;
     return DV_OK;
@@ -869,7 +903,7 @@ namespace {
 
 // enqueue one decision round (scan + push + compaction); partitioned epochs
 // then write verdict bytes, single-GPU epochs settle statuses directly
-void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
+void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle, bool async_words = false) {
     const uint32_t r = c->rounds;
     const uint32_t tag = next_tag(c);
     uint32_t *tc = next_ticket(c);
@@ -881,7 +915,9 @@ void enqueue_round(dv_ctx *c, uint8_t *d_verdict, bool settle) {
                (uint32_t)(tc - c->tile_ctr), settle, settle ? c->d_pub : nullptr,
                t ? c->pev[2 * c->passes] : nullptr, t ? c->pev[2 * c->passes + 1] : nullptr);
     c->passes++;
-    if (settle) round_settle(c->stream, b, r, c->v_n_txn, c->und_ub);
+    if (settle && async_words && r == 0)  // round 0 with the asynchronous launch behind it (round0_then_async)
+        round_settle(c->stream, b, r, c->v_n_txn, c->und_ub, c->tword, c->abounds, c->async_g);
+    else if (settle) round_settle(c->stream, b, r, c->v_n_txn, c->und_ub);
     else list_verdict(c->stream, b, r, c->und_ub, d_verdict);
     c->rounds++;
 }
@@ -1182,10 +1218,20 @@ uint32_t async_thresh(dv_ctx *c) {
     return (uint32_t)std::min<uint64_t>(frac, async_try_limit(c->async_g));
 }
 
-void async_try(dv_ctx *c, uint32_t r0) {
+void async_try(dv_ctx *c, uint32_t r0, bool words_done = false) {
     c->async_launched++;
     round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, async_thresh(c),
-                c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks);
+                c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks, words_done);
+}
+
+// round 0, then every remaining decision in one asynchronous launch at round
+// 1, queued with no host wait; round 0's settle writes the launch's fact and
+// carry words (no k_async_words)
+void round0_then_async(dv_ctx *c) {
+    c->v_thresh = async_try_limit(c->async_g);
+    enqueue_round(c, nullptr, true, true);
+    async_try(c, 1, true);
+    c->async_unconfirmed = true;
 }
 
 // Small epochs (a TPC-C epoch, at most kAsyncSmallAcc accesses): round 0,
@@ -1196,10 +1242,7 @@ void async_try(dv_ctx *c, uint32_t r0) {
 int decide_epoch(dv_ctx *c) {
     const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     if (!async || c->n_acc > kAsyncSmallAcc) return run_rounds(c, false);
-    c->v_thresh = async_try_limit(c->async_g);
-    enqueue_round(c, nullptr, true);
-    async_try(c, 1);
-    c->async_unconfirmed = true;
+    round0_then_async(c);
     return hip_fail(hipGetLastError(), "rounds");
 }
 
@@ -1300,10 +1343,7 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
     const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     if (!async) return run_rounds(c, false);
-    c->v_thresh = async_try_limit(c->async_g);  // whatever fits the workgroups
-    enqueue_round(c, nullptr, true);
-    async_try(c, 1);
-    c->async_unconfirmed = true;
+    round0_then_async(c);  // (v_thresh: whatever fits the workgroups)
     return hip_fail(hipGetLastError(), "stage rounds");
 }
 
@@ -1392,7 +1432,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->prefix_mode = true;
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
-                       c->tile_ctr, err_seed, c->ctr);
+                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
