@@ -251,6 +251,10 @@ struct RoundBufs {
     const uint8_t *tlen;     // per txn
     uint32_t *ulist[2];      // undecided txns, ping-pong (single-GPU settle)
     const uint32_t *n_txn_dev;  // (optional) the real txn count, n_txn an upper bound (sub-epochs)
+    // round 0's sizes (set per (sub-)epoch by the runtime): live accesses (n0_dev on the device,
+    // else n0) and txns (n_txn_dev, else n_txn0)
+    const uint32_t *n0_dev;
+    uint32_t n0, n_txn0;
     uint64_t *desc;
     uint32_t *tile_ctr;
     Counters *ctr;
@@ -278,8 +282,8 @@ struct RoundPub {
 // the rounds of one (sub-)epoch begin: round 0's counts (n_acc_dev /
 // b.n_txn_dev, when given, hold the real ones), its verdict bytes cleared, the
 // asynchronous-try state reset
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
-                       uint32_t n_txn_pad, const uint32_t *n_acc_dev);
+// round 0 needs no launch of its own: its pass reads the sizes (RoundBufs n0*)
+// and resets the round counters, and writes every access's verdict byte
 // settle = single GPU (the following settle compacts the undecided list; a
 // pass whose round starts with no undecided txn is a no-op)
 // ev0/ev1 (optional): recorded by the pass's own dispatch (hipExtLaunchKernel)

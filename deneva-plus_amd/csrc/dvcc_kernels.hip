@@ -33,8 +33,11 @@ namespace dvcc {
 // LDS copy of the descriptors otherwise -- indexing the kernel-argument array
 // with a per-lane table id compiles to a select chain over every descriptor
 // field, which cost a config-D probe 64 of its 172 us.
+// miss (optional): a missing key ORs true there instead of setting the error
+// bit here, so the caller can record it later (the probe keeps the tag
+// gather's latency off its path until the access's row is needed)
 __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64_t key, uint64_t &row,
-                                          Counters *ctr) {
+                                          Counters *ctr, bool *miss = nullptr) {
     if (!tb_ok) {
         set_err(ctr, ERRB_TABLE);
         return false;
@@ -67,7 +70,10 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
             if (e.key == key) { row = e.row; found = true; break; }
         }
     }
-    if (!found) set_err(ctr, ERRB_KEY);
+    if (!found) {
+        if (miss) *miss = true;
+        else set_err(ctr, ERRB_KEY);
+    }
     row += t.row_base;
     return found;
 }
@@ -79,11 +85,7 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
 // of equal txns is a max-scan of run-start indices over the wave; a run that
 // began in an earlier wave is walked back in memory (at most one per wave).
 // Repeated rows inside a txn are detected later, in row order (seg_prepare).
-#ifndef DVCC_PROBE_PV
-#define DVCC_PROBE_PV 4
-#endif
-constexpr int kPV = DVCC_PROBE_PV;
-static_assert(kPV % 4 == 0, "vector loads of 4 accesses");
+constexpr int kPV = 4;  // (8 measured slower: fewer waves per SIMD)
 template <bool HIST>
 __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *__restrict__ keys,
                                            const uint32_t *__restrict__ keys32,
@@ -152,14 +154,15 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 tb[j] = ok && tables ? tables[i0 + j] : 0u;
             }
         }
+        bool miss = false;
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             row[j] = 0;
             if (i0 + j < n) {
                 if (tables)
-                    probe_row(s_td[tb[j] < kMaxTables ? tb[j] : 0], tb[j] < tabs.n, key[j], row[j], ctr);
+                    probe_row(s_td[tb[j] < kMaxTables ? tb[j] : 0], tb[j] < tabs.n, key[j], row[j], ctr, &miss);
                 else
-                    probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr);
+                    probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr, &miss);
             }
         }
         // run starts and their max-scan
@@ -206,6 +209,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         uint32_t nxt_last = lane == 63 ? (in_last < n ? acc_txn[in_last] : 0xFFFFFFFFu) : nxt_lane;
         if (i0 + kPV > n) nxt_last = 0xFFFFFFFFu;
         if (bad) set_err(ctr, ERRB_TXN);
+        if (miss) set_err(ctr, ERRB_KEY);
         uint64_t out[kPV];
 #pragma unroll
         for (int j = 0; j < kPV; j++) {

@@ -64,7 +64,9 @@ __device__ __forceinline__ uint32_t elem_value(E e, uint8_t s, int nowait) {
 // txn, so it goes straight to the txn's status byte (readers of that byte in
 // this same pass may or may not see it yet -- either view is a true fact, and
 // the greedy outcome is unique); an OK is recorded per access for the settle.
-template <class E>
+// ALL (round 0): every access's verdict byte is written, 0 where not OK, so
+// the bytes need no clearing before the epoch
+template <bool ALL = false, class E>
 __device__ __forceinline__ E decide_elem(E e, uint32_t excl, int nowait, uint8_t *__restrict__ vb8,
                                          uint32_t slog, uint8_t *status) {
     if (e & F_DONE) return e;
@@ -73,9 +75,12 @@ __device__ __forceinline__ E decide_elem(E e, uint32_t excl, int nowait, uint8_t
     const uint32_t sel = (nowait && (e & F_WR)) ? (excl & (B_CA | B_UA)) : ((excl >> 2) & (B_CA | B_UA));
     if (sel & B_CA) {
         status[r_txn(e, slog)] = ST_ABORT;  // Abort (row_lock.cpp:86-90 / occ.cpp:219-234)
+        if (ALL) vb8[e >> 3] = 0;
     } else if (!(sel & B_UA)) {
         vb8[e >> 3] = VB_OK;  // granted / validated: permanently OK
         e |= F_DONE;
+    } else if (ALL) {
+        vb8[e >> 3] = 0;
     }
     return e;
 }
@@ -390,7 +395,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
         const bool head = (ej & F_HEAD) != 0;
         const uint32_t excl = head ? 0u : run;
 #ifndef DVCC_EXP_NO_DECIDE
-        if ((umask >> j) & 1u) ej = decide_elem(ej, excl, nowait, vb8, slog, status);
+        if ((umask >> j) & 1u) ej = decide_elem<FIRST>(ej, excl, nowait, vb8, slog, status);
 #endif
         if (vj & B_KEEP) s_out[lpos++] = (E)((ej & ~(E)F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD));
         run = head ? vj : (run | vj);
@@ -410,11 +415,24 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
     const EIn *__restrict__ el_in, const uint32_t *__restrict__ n_in, E *__restrict__ el_out,
     uint32_t *__restrict__ n_out, uint8_t *status, uint8_t *__restrict__ vb8, uint32_t slog,
     int nowait, uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, uint32_t *und_reset,
-    const uint32_t *und_in, uint32_t round, RoundPub *pub, Counters *ctr) {
+    const uint32_t *und_in, uint32_t round, RoundPub *pub, Counters *ctr, const uint32_t *n0_dev, uint32_t n0,
+    const uint32_t *n_txn_dev, uint32_t n_txn0) {
     __shared__ TileLds<EIn> sh;
     __shared__ uint32_t s_tile;
-    const uint32_t n_live = *n_in;
-    const uint32_t und = und_in ? *und_in : 1u;
+    // round 0 reads its sizes from the arguments and starts the rounds' counts
+    const uint32_t n_live = FIRST ? (n0_dev ? *n0_dev : n0) : *n_in;
+    const uint32_t und = FIRST || !und_in ? 1u : *und_in;
+    if (FIRST && blockIdx.x == 0 && threadIdx.x == 0) {
+        ctr->nlive[0] = n_live;
+        ctr->nund[0] = n_txn_dev ? *n_txn_dev : n_txn0;  // partitioned rounds: round 0's list is every txn
+        // a (sub-)epoch's rounds start with no asynchronous try behind them
+        // (halt stays: the epoch clear zeroes it, and a prefix-kill epoch's
+        // survivor stage must keep the prefix's halt, k_prefix_mark)
+        ctr->async_go = 0;
+        ctr->async_r0 = 0;
+        ctr->async_iters = 0;
+        ctr->async_block = 0;
+    }
     // nothing left to decide, or a rejected epoch: no-op
     const uint32_t n = und && !input_err(ctr) ? n_live : 0u;
     const uint32_t ntiles = (n + Geo<EIn>::kTile - 1) / Geo<EIn>::kTile;
@@ -541,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void k_round_settle(
     const uint32_t *__restrict__ n_in, uint32_t n_txn, uint32_t *__restrict__ list_out,
     uint32_t *__restrict__ n_out, uint32_t *__restrict__ tword, uint32_t *__restrict__ carry, uint32_t G) {
     __shared__ SettleLds sh;
-    // round 0: every txn of the (sub-)epoch (its real count from round0_init)
+    // round 0: every txn of the (sub-)epoch (its real count from the round-0 pass)
     const uint32_t n = n_in ? *n_in : n_txn;
     const uint32_t lo = blockIdx.x * kSettleChunk;
     if (lo >= n) return;
@@ -1179,29 +1197,6 @@ __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__
 }
 
 
-// round 0's counts, and every txn's verdict bytes cleared (16-byte stores,
-// 1 << slog bytes per txn)
-__global__ __launch_bounds__(kBlock) void k_round0_init(uint32_t n, uint32_t n_txn, uint32_t n_pad,
-                                                        uint4 *__restrict__ vb8, uint32_t slog,
-                                                        const uint32_t *__restrict__ n_dev,
-                                                        const uint32_t *__restrict__ n_txn_dev, Counters *ctr) {
-    if (n_txn_dev) n_pad = (*n_txn_dev + 3u) & ~3u;  // (n_pad: the upper bound's)
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctr->nlive[0] = n_dev ? *n_dev : n;
-        ctr->nund[0] = n_txn_dev ? *n_txn_dev : n_txn;  // partitioned rounds: round 0's list is every txn
-        // a (sub-)epoch's rounds start with no asynchronous try behind them
-        // (halt stays: the epoch clear zeroes it, and a prefix-kill epoch's
-        // survivor stage must keep the prefix's halt, k_prefix_mark)
-        ctr->async_go = 0;
-        ctr->async_r0 = 0;
-        ctr->async_iters = 0;
-        ctr->async_block = 0;
-    }
-    const uint64_t words = (uint64_t)n_pad << (slog - 4);
-    for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < words; i += (uint64_t)gridDim.x * kBlock)
-        vb8[i] = uint4{0u, 0u, 0u, 0u};
-}
-
 // ------------------------------------------------------------- launchers
 static uint32_t txn_grid(uint32_t n_txn) {
     uint32_t g = (n_txn + kBlock - 1) / kBlock;
@@ -1215,12 +1210,6 @@ bool round_el32(uint32_t n_txn, uint32_t slog) {
 }
 
 uint32_t tail_cap(bool el32) { return el32 ? TailGeo<uint32_t>::kCap : TailGeo<uint64_t>::kCap; }
-
-void rounds_epoch_init(hipStream_t s, const RoundBufs &b, uint32_t n_acc, uint32_t n_txn,
-                       uint32_t n_txn_pad, const uint32_t *n_acc_dev) {
-    k_round0_init<<<txn_grid(n_txn_pad << (b.slog - 4)), kBlock, 0, s>>>(
-        n_acc, n_txn, n_txn_pad, reinterpret_cast<uint4 *>(b.vb8), b.slog, n_acc_dev, b.n_txn_dev, b.ctr);
-}
 
 template <class E>
 static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, uint32_t ub_in,
@@ -1240,14 +1229,14 @@ static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int 
         hipExtLaunchKernelGGL(k_round_pass<true, uint64_t, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0,
                               ev1, 0, b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait,
                               b.desc, tc, tag, und, (const uint32_t *)nullptr, round,
-                              (RoundPub *)nullptr, b.ctr);
+                              (RoundPub *)nullptr, b.ctr, b.n0_dev, b.n0, b.n_txn_dev, b.n_txn0);
     } else {
         using G = Geo<E>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
         hipExtLaunchKernelGGL(k_round_pass<false, E, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0, ev1, 0,
                               reinterpret_cast<const E *>(b.rel[(round - 1) & 1]), n_in, out, n_out,
                               b.status, b.vb8, b.slog, nowait, b.desc, tc, tag, und, und_in, round,
-                              pub, b.ctr);
+                              pub, b.ctr, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u);
     }
 }
 

@@ -85,6 +85,8 @@ struct dv_ctx {
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
     Counters *h_ctr = nullptr;  // pinned host mirror
+    uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
+    const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
 
     // staging for dv_epoch_run (host-buffer entry point)
@@ -212,6 +214,9 @@ RoundBufs round_bufs(dv_ctx *c) {
     b.ulist[0] = c->ulist[0];
     b.ulist[1] = c->ulist[1];
     b.n_txn_dev = c->v_n_txn_dev;
+    b.n0_dev = c->r0_n_dev;
+    b.n0 = c->r0_n;
+    b.n_txn0 = c->v_n_txn;
     b.desc = c->desc;
     b.tile_ctr = c->tile_ctr;
     b.ctr = c->ctr;
@@ -887,7 +892,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         const uint32_t tag = next_tag(c);
         calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
-        rounds_epoch_init(c->stream, round_bufs(c), (uint32_t)ep->n_acc, ep->n_txn, c->n_txn_pad, nullptr);
+        c->r0_n = (uint32_t)ep->n_acc;  // (round 0's sizes, RoundBufs)
+        c->r0_n_dev = nullptr;
         __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
         __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
         c->live_ub = (uint32_t)ep->n_acc;
@@ -1338,7 +1344,8 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
     c->el32 = round_el32(c->v_n_txn, c->slog) && !(c->cfg.flags & DV_FLAG_EL64);
     c->live_ub = n_acc_ub;
     c->und_ub = c->v_n_txn;
-    rounds_epoch_init(c->stream, round_bufs(c), n_acc_ub, c->v_n_txn, (c->v_n_txn + 3u) & ~3u, n_acc_dev);
+    c->r0_n = n_acc_ub;  // (round 0's sizes, RoundBufs)
+    c->r0_n_dev = n_acc_dev;
     __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
     const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
