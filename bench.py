@@ -11,13 +11,17 @@ GPU), 10 requests/txn, zipf 0.9, 50 % of the accesses writes (TXN_WRITE_PERC
 1.0, TUP_WRITE_PERC 0.5), NO_WAIT.
 
 --gpus N > 1 starts its own N rank processes (torch.distributed.run) when no
-launcher did; one process per GPU, rank r owns partition r, and every epoch
-runs through the engine's own RCCL driver (dv_comm_init + dv_epoch_run_part:
-one all-to-allv of 16-byte access records, then decision rounds closed by
-all-reduce(MAX) of the undecided txns' verdict bytes, all on the engine's
-stream).  Multi-partition txns follow the MPR gate (2 partitions).  Beside
-the headline (strong scaling: the epoch is fixed) the line carries the
-weak-scaling run (1,048,576 txns per GPU) and the MPR sweep of config D.
+launcher did; one process per GPU, rank r owns partition r (16,777,216 rows),
+all collectives from the engine over RCCL (dv_comm_init).  The headline runs
+config D's epochs -- 1,048,576 txns each IN TOTAL, every rank's client batch
+1,048,576 / N of them, multi-partition txns per the MPR gate (2 partitions) --
+as epoch groups (dv_epoch_group_run): a step is one group of N consecutive
+epochs, rank e receives every batch of epoch e (all-to-allv), decides it with
+the single-GPU path and forwards the committed accesses to their owners, who
+execute the N epochs in order.  Per-GPU work is one epoch decided per step,
+so the line says "scaling": "weak".  Beside it: one epoch per step over
+dv_epoch_run_part (strong scaling; replicated sequencing), the
+1,048,576-txn-per-GPU epochs of the list protocol, and the MPR sweep.
 Rank 0 prints one JSON line.
 """
 import argparse
@@ -64,6 +68,11 @@ def parse():
     ap.add_argument("--mpr-sweep", default="0,0.1,0.2,0.3,0.4,0.5",
                     help="N>1: config D's MPR values, each a short extra run ('' = none)")
     ap.add_argument("--no-weak", action="store_true", help="N>1: skip the 1,048,576-txn-per-GPU run")
+    ap.add_argument("--protocol", choices=["group", "part"], default="group",
+                    help="N>1 headline: epoch groups (dv_epoch_group_run) or one epoch per step "
+                         "(dv_epoch_run_part, --part-mode)")
+    ap.add_argument("--part1", action="store_true",
+                    help="N=1 through the partitioned drivers on a one-rank RCCL communicator (their overhead)")
     ap.add_argument("--part-mode", type=int, default=0,
                     help="N>1: dv_comm_set_mode -- 0 replicated when the epoch fits, else the list protocol; "
                          "1 list protocol; 2 replicated")
@@ -364,7 +373,7 @@ def pmc_traffic(a, cc_name, world, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
-def roofline(kstats, a, cc_name, world):
+def roofline(kstats, a, cc_name, world, txn_div=1):
     """The largest single launch of the epoch, the index probe (k_probe):
     algorithmic bytes per launch -- SURVEY.md 8(d)'s probe traffic, PROBE_ACC
     B per access (key 8 + type 1 + txn id 4 read, key tag 1 gathered, row
@@ -376,7 +385,8 @@ def roofline(kstats, a, cc_name, world):
     (DESIGN.md); k_round_pass is reported beside it."""
     launches = sum(1 for s in kstats if s.ms_probe_kernel > 0)
     avg_ms = sum(s.ms_probe_kernel for s in kstats) / max(1, launches)
-    bytes_per_launch = float(np.mean([PROBE_ACC * s.n_acc + PROBE_TXN * s.n_txn for s in kstats]))
+    # (epoch groups: n_txn counts the group, n_acc the epoch this rank decided)
+    bytes_per_launch = float(np.mean([PROBE_ACC * s.n_acc + PROBE_TXN * s.n_txn // txn_div for s in kstats]))
     achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
     traffic, src = pmc_traffic(a, cc_name, world, "k_probe")
     p_launches = sum(s.pass_launches for s in kstats)
@@ -469,7 +479,8 @@ class PartitionedBench:
                                  part_id=rank, timing=TIMING[a.timing])
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
         self.eng.comm_init(uid[0], world, rank)
         self.eng.comm_set_mode(a.part_mode)
         self.rows = rows
@@ -485,6 +496,22 @@ class PartitionedBench:
     def stepper(self, deps, n_txn_rank):
         def step(i):
             return self.eng.run_epoch_part(deps[i % len(deps)], n_txn_rank, self.d_commit)
+        return step
+
+    def groups(self, n_txn_rank, mpr, theta, count):
+        """count epoch groups: group g holds this rank's batches of epochs
+        g * N .. g * N + N - 1 (seeded SEED + 97 * part + epoch)."""
+        gen = dvcc.YCSBQueryGenerator(self.rows * self.world, part_cnt=self.world, req_per_query=self.R,
+                                      zipf_theta=theta, txn_write_perc=1.0, tup_write_perc=0.5,
+                                      part_per_txn=2, strict_ppt=1, mpr=mpr)
+        with ThreadPoolExecutor(max_workers=8) as ex:
+            futs = [[ex.submit(gen.gen, n_txn_rank, dvcc.epoch_seed(self.rank, g * self.world + e), self.rank)
+                     for e in range(self.world)] for g in range(count)]
+            return [[dvcc.DeviceEpoch(f.result()) for f in grp] for grp in futs]
+
+    def group_stepper(self, groups, n_txn_rank):
+        def step(i):
+            return self.eng.run_epoch_group(groups[i % len(groups)], n_txn_rank, self.d_commit)
         return step
 
 
@@ -506,11 +533,12 @@ def main():
     rows, n_txn_total, theta, desc = CONFIGS[a.config]
     R = 10
     n_txn_rank = n_txn_total // world
-    mpr = a.mpr if world > 1 else -1.0  # N=1: the reference zipf generator, unmodified
+    part = world > 1 or a.part1
+    mpr = a.mpr if part else -1.0  # N=1: the reference zipf generator, unmodified
     n_epochs = max(1, min(a.epochs, a.steps + a.warmup))
     t_gen = time.perf_counter()
     extra = {}
-    if world == 1:
+    if not part:
         gen = dvcc.YCSBQueryGenerator(rows, part_cnt=1, req_per_query=R, zipf_theta=theta,
                                       txn_write_perc=1.0, tup_write_perc=0.5, part_per_txn=1, strict_ppt=1,
                                       mpr=mpr)
@@ -529,13 +557,18 @@ def main():
         pb = PartitionedBench(a, cc_name, rows, world, rank, local_rank,
                               n_txn_total if weak else n_txn_rank, R)
         eng = pb.eng
-        deps = pb.epochs(n_txn_rank, mpr, theta, n_epochs)
+        if a.protocol == "group":
+            groups = pb.groups(n_txn_rank, mpr, theta, n_epochs)
+            step = pb.group_stepper(groups, n_txn_rank)
+        else:
+            deps = pb.epochs(n_txn_rank, mpr, theta, n_epochs)
+            step = pb.stepper(deps, n_txn_rank)
         t_gen = time.perf_counter() - t_gen
-        step = pb.stepper(deps, n_txn_rank)
 
     stats, el = timed(step, 0, a.warmup, a.steps, world)
     kstats, sstats = measure_legs(a, eng, step, a.warmup + a.steps, stats)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
+    group = part and a.protocol == "group"
     out = {
         "metric": METRIC,
         "value": committed / el,
@@ -545,7 +578,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": el / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak" if group else "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic: Deneva YCSB zipf generator (myrand LCG, seeded SEED+97*part+epoch)",
@@ -553,29 +586,43 @@ def main():
             "workload": desc, "cc_alg": cc_name, "rows_per_partition": rows,
             "txns_per_epoch": n_txn_total, "txns_per_epoch_per_gpu": n_txn_rank, "req_per_query": R,
             "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
-            "mpr": mpr if world > 1 else 0.0, "part_per_txn": min(2, world),
+            "mpr": mpr if part else 0.0, "part_per_txn": min(2, world),
             "parallelism": f"partitioned x{world} (PART_CNT={world}, RCCL)" if world > 1 else "1 GPU",
-            "protocol": ({0: "replicated (the epoch's accesses all-gathered, decided on every rank, own rows "
+            "epochs_per_step": world if group else 1,
+            "protocol": ("epoch groups (rank e decides epoch e of each group of N; batches all-to-allv'd to "
+                         "the decider, committed accesses forwarded to their owners, epochs executed in order)"
+                         if group else
+                         {0: "replicated (the epoch's accesses all-gathered, decided on every rank, own rows "
                              "executed) when the epoch fits a context, else the list protocol",
                           1: "list protocol (owner split, per-round verdict all-reduce)",
-                          2: "replicated"}[a.part_mode] if world > 1 else "single GPU"),
+                          2: "replicated"}[a.part_mode] if part else "single GPU"),
             "distinct_epochs": n_epochs,
         },
-        "roofline": roofline(kstats, a, cc_name, world),
+        "roofline": roofline(kstats, a, cc_name, world, world if group else 1),
         "timing_in_timed_region": a.timing,
         "gen_seconds": t_gen,
         "src_hash": dvcc._lib.source_hash(),
     }
     out.update(stage_summary(stats, sstats, kstats, el, R))
-    if world == 1:
+    if not part:
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
         out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, min(a.steps, 10), d_commit)
     else:
         nxt = 10_000
+        if group:
+            # strong scaling: one 1,048,576-txn epoch per step (dv_epoch_run_part)
+            sdeps = pb.epochs(n_txn_rank, mpr, theta, 2)
+            sst, sel = timed(pb.stepper(sdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            scm = sum(s.committed for s in sst)
+            out["strong_scaling"] = {"txns_per_epoch": n_txn_total, "committed_per_s": scm / sel,
+                                     "ms_per_epoch": sel / len(sst) * 1e3, "epochs": len(sst),
+                                     "protocol": "dv_epoch_run_part, mode %d" % a.part_mode}
+            del sdeps
+            nxt += 100
         if not a.no_weak:
-            # weak scaling: 1,048,576 txns per GPU per epoch
+            # weak scaling: 1,048,576 txns per GPU per epoch (list protocol)
             wdeps = pb.epochs(n_txn_total, mpr, theta, 2)
             wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, 1, min(a.steps, 5), world)
             wc = sum(s.committed for s in wst)
@@ -588,16 +635,22 @@ def main():
             nxt += 100
         sweep = []
         for m in [float(x) for x in a.mpr_sweep.split(",") if x.strip()]:
-            mdeps = pb.epochs(n_txn_rank, m, theta, 2)
-            mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            if group:
+                mg = pb.groups(n_txn_rank, m, theta, 1)
+                mst, mel = timed(pb.group_stepper(mg, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+                mtx = len(mst) * n_txn_total * world
+            else:
+                mdeps = pb.epochs(n_txn_rank, m, theta, 2)
+                mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+                mtx = len(mst) * n_txn_total
             mc = sum(s.committed for s in mst)
-            sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_epoch": mel / len(mst) * 1e3,
-                          "abort_rate": 1 - mc / (len(mst) * n_txn_total),
+            sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_step": mel / len(mst) * 1e3,
+                          "abort_rate": 1 - mc / mtx,
                           "rounds_mean": float(np.mean([s.rounds for s in mst]))})
             nxt += 100
         if sweep:
             out["mpr_sweep"] = sweep
-    if world == 1 and rank == 0 and not a.no_cpu_baseline:
+    if not part and rank == 0 and not a.no_cpu_baseline:
         # the single-thread E-schedule port (decision-identical) and, for
         # NO_WAIT, the multi-threaded engine, which is then the baseline
         single = cpu_baseline(epochs, rows, cc_name, a.cpu_seconds)
@@ -610,7 +663,7 @@ def main():
         from dvcc.stats import summary_line
         out["deneva_summary"] = summary_line(el, stats)
         print(out["deneva_summary"], file=sys.stderr, flush=True)
-    if world == 1 and not a.no_tpcc:
+    if not part and not a.no_tpcc:
         out["tpcc"] = tpcc_leg(a)
     if rank == 0:
         print(json.dumps(out), flush=True)

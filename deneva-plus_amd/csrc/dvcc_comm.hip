@@ -195,6 +195,237 @@ __global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict_
     }
 }
 
+
+// ---- epoch groups (run_group): a group is P consecutive epochs; rank e
+// decides epoch e of the group alone (the replicated single-GPU path over the
+// epoch's batches, which every rank sends it), then routes the epoch's
+// committed accesses to their owners, and every rank executes the records of
+// epochs 0..P-1 on its rows, in epoch order.  Decisions depend only on an
+// epoch's accesses, so deciding P epochs side by side gives
+// the decisions of deciding them one after the other; execution keeps the
+// epoch order on every row.
+
+// lanes holding the same owner (restricted to `valid`); owners < 2^obits
+__device__ __forceinline__ uint64_t match_owner(uint32_t o, uint64_t valid, uint32_t obits) {
+    uint64_t peers = valid;
+    for (uint32_t b = 0; b < obits; b++) {
+        const uint32_t bit = (o >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+    }
+    return peers;
+}
+
+// the committed txns' accesses, as k_exec_txn walks them (a wave takes 64
+// txns and spreads their accesses over its lanes); emit(valid, global row,
+// flags, txn) is called by every lane, wave-uniformly
+template <class Emit>
+__device__ __forceinline__ void walk_committed_txns(const uint32_t *__restrict__ tb_start,
+                                                    const uint32_t *__restrict__ tb_end,
+                                                    const uint32_t *__restrict__ acc_row, uint32_t n_txn,
+                                                    const uint8_t *__restrict__ status, Emit &emit) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t step = gridDim.x * (kBlock / 64) * 64;
+    for (uint32_t base = (blockIdx.x * (kBlock / 64) + wave) * 64; base < n_txn; base += step) {
+        const uint32_t t = base + lane;
+        const bool com = t < n_txn && status[t] == ST_COMMIT;
+        if (__ballot(com) == 0) continue;
+        const uint32_t a0 = com ? tb_start[t] : 0u;
+        const uint32_t len = com ? tb_end[t] - a0 : 0u;
+        uint32_t incl = len;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 64);
+            if (lane >= (uint32_t)off) incl += o;
+        }
+        const uint32_t pre = incl - len, total = __shfl(incl, 63, 64);
+        for (uint32_t g0 = 0; g0 < total; g0 += 64) {
+            const uint32_t g = g0 + lane;
+            uint32_t src = 0;
+#pragma unroll
+            for (uint32_t w = 32; w > 0; w >>= 1) {
+                const uint32_t cand = src + w;
+                const uint32_t pv = __shfl(pre, (int)(cand & 63u), 64);
+                if (cand < 64 && pv <= g) src = cand;
+            }
+            const uint32_t sa0 = __shfl(a0, (int)src, 64), spre = __shfl(pre, (int)src, 64);
+            const bool v = g < total;
+            const uint32_t ar = v ? acc_row[sa0 + (g - spre)] : 0u;
+            emit(v, ar & ~AR_WR, (ar & AR_WR) ? RT_WR : 0u, base + src);
+        }
+    }
+}
+
+// CALVIN: every committed access in row order (k_exec's view: a read after
+// an earlier write of its queue sees that write)
+template <class Emit>
+__device__ __forceinline__ void walk_row_queues(const uint64_t *__restrict__ pairs, const uint64_t *__restrict__ el,
+                                                const uint8_t *__restrict__ ew, uint64_t n,
+                                                const uint8_t *__restrict__ status, Emit &emit) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t base = ((uint64_t)blockIdx.x * (kBlock / 64) + wave) * 64; base < n; base += step) {
+        const uint64_t i = base + lane;
+        const uint64_t e = i < n ? el[i] : 0ull;
+        const bool v = i < n && status[el_txn(e)] == ST_COMMIT;
+        const uint32_t wr = (e & EL_WR) ? RT_WR : 0u;
+        const uint32_t seen = (v && !wr && ew && ew[i]) ? RT_SEESW : 0u;
+        emit(v, v ? pair_row(pairs[i]) : 0u, wr | seen, el_txn(e));
+    }
+}
+
+template <int SRC>
+struct RouteSrc {
+    const uint32_t *tb_start, *tb_end, *acc_row;
+    uint32_t n_txn;
+    const uint64_t *pairs, *el;
+    const uint8_t *ew;
+    uint64_t n;
+    const uint8_t *status;
+    template <class Emit>
+    __device__ void walk(Emit &emit) const {
+        if (SRC == 0) walk_committed_txns(tb_start, tb_end, acc_row, n_txn, status, emit);
+        else walk_row_queues(pairs, el, ew, n, status, emit);
+    }
+};
+
+__host__ __device__ inline uint32_t owner_bits(uint32_t P) {
+    uint32_t b = 0;
+    while ((1u << b) < P) b++;
+    return b;
+}
+
+// pass 1: records per owner per block (a halted or rejected epoch routes
+// nothing: zero counts)
+template <int SRC>
+__global__ __launch_bounds__(kBlock) void k_route_count(RouteSrc<SRC> src, RouteOut ro, const Counters *ctr) {
+    __shared__ uint32_t c[kRadix];
+    for (uint32_t o = threadIdx.x; o < ro.P; o += kBlock) c[o] = 0;
+    __syncthreads();
+    if (!(input_err(ctr) || ctr->halt)) {
+        const uint32_t lane = threadIdx.x & 63, P = ro.P, ob = owner_bits(P);
+        auto emit = [&](bool v, uint32_t row, uint32_t, uint32_t) {
+            const uint32_t o = v ? row % P : 0u;
+            const uint64_t peers = match_owner(o, __ballot(v), ob);
+            if (v && lane == (uint32_t)__builtin_ctzll(peers)) atomicAdd(&c[o], (uint32_t)__popcll(peers));
+        };
+        src.walk(emit);
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < ro.P; o += kBlock) ro.blk[o * kRouteBlocks + blockIdx.x] = c[o];
+}
+
+// pass 2: the same walk (same grid, same items per block), each block
+// writing at its owner-major offsets
+template <int SRC>
+__global__ __launch_bounds__(kBlock) void k_route_scatter(RouteSrc<SRC> src, RouteOut ro, const Counters *ctr) {
+    __shared__ uint32_t tots[kRadix], cur[kRadix];
+    const uint32_t P = ro.P;
+    uint32_t pre = 0;
+    for (uint32_t o = threadIdx.x; o < P; o += kBlock) {
+        uint32_t t = 0;
+        for (uint32_t b = 0; b < kRouteBlocks; b++) {
+            const uint32_t v = ro.blk[o * kRouteBlocks + b];
+            if (b < blockIdx.x) pre += v;
+            t += v;
+        }
+        tots[o] = t;
+        cur[o] = pre;
+    }
+    __syncthreads();
+    for (uint32_t o = threadIdx.x; o < P; o += kBlock) {
+        uint32_t off = 0;
+        for (uint32_t q = 0; q < o; q++) off += tots[q];
+        cur[o] += off;
+        if (blockIdx.x == 0) ro.tot[o] = tots[o];
+    }
+    __syncthreads();
+    if (input_err(ctr) || ctr->halt) return;
+    const uint32_t lane = threadIdx.x & 63, ob = owner_bits(P);
+    auto emit = [&](bool v, uint32_t row, uint32_t flags, uint32_t txn) {
+        const uint32_t o = v ? row % P : 0u;
+        const uint64_t peers = match_owner(o, __ballot(v), ob);
+        const uint32_t leader = v ? (uint32_t)__builtin_ctzll(peers) : lane;
+        uint32_t b = 0;
+        if (v && lane == leader) b = atomicAdd(&cur[o], (uint32_t)__popcll(peers));
+        b = __shfl(b, (int)leader, 64);
+        if (v) ro.rec[b + mask_rank(peers)] = make_uint2((row / P) | flags, txn);
+    };
+    src.walk(emit);
+}
+
+// run_ycsb_1 (ycsb_txn.cpp:227-254) of one epoch's routed records on this
+// partition's rows: a read adds mix64(v ^ mix64(txn << 32 ^ pkey)) to the
+// digest (v = 0 when it sees an earlier write of its epoch), a write stores 0
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_route_exec(const uint2 *__restrict__ rec, uint64_t n,
+                                                       uint64_t *__restrict__ f0, const uint64_t *__restrict__ pkey,
+                                                       unsigned long long *acc) {
+    __shared__ unsigned long long part[2][4];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long dig = 0, wcnt = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint2 r = rec[i];
+        const uint32_t row = r.x & ~(RT_WR | RT_SEESW);
+        if (r.x & RT_WR) {
+            if (MODE & 2) {
+                f0[row] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
+                wcnt++;
+            }
+        } else if (MODE & 1) {
+            const uint64_t val = (r.x & RT_SEESW) ? 0ull : f0[row];
+            dig += mix64(val ^ mix64(((uint64_t)r.y << 32) ^ pkey[row]));
+        }
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        dig += __shfl_down(dig, off, 64);
+        wcnt += __shfl_down(wcnt, off, 64);
+    }
+    if (lane == 0) {
+        part[0][wave] = dig;
+        part[1][wave] = wcnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long d = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+        const unsigned long long w = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+        if (d) atomicAdd(&acc[0], d);
+        if (w) atomicAdd(&acc[1], w);
+    }
+}
+
+// the send words of the outcome exchange: committed txns of this epoch << 32
+// | records for owner q
+// the routed records this rank receives exceed its receive area: the group
+// fails on every rank (outcome vote word 0 = -DV_ERR_ARG at least)
+__global__ void k_route_recv_check(const uint64_t *__restrict__ words, uint32_t P, uint64_t cap,
+                                   uint32_t *__restrict__ vote) {
+    if (threadIdx.x != 0) return;
+    uint64_t n = 0;
+    for (uint32_t q = 0; q < P; q++) n += words[q] & 0xFFFFFFFFull;
+    if (n > cap && vote[0] < (uint32_t)(-DV_ERR_ARG)) vote[0] = (uint32_t)(-DV_ERR_ARG);
+}
+
+__global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, int ok,
+                              uint64_t *__restrict__ words) {
+    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) words[q] = (committed << 32) | (ok ? tot[q] : 0u);
+}
+
+void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
+                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr) {
+    const RouteSrc<0> src{tb_start, tb_end, acc_row, n_txn, nullptr, nullptr, nullptr, 0, status};
+    k_route_count<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    k_route_scatter<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+}
+
+void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs, const uint64_t *el,
+                       const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr) {
+    const RouteSrc<1> src{nullptr, nullptr, nullptr, 0, pairs, el, ew, n, status};
+    k_route_count<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    k_route_scatter<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+}
+
 // ---- in-process group: element-wise MAX of the P ranks' buffers
 constexpr int kMaxLocalRanks = 16;
 template <class T>
@@ -223,9 +454,13 @@ struct DvComm {
     uint8_t *types = nullptr, *tables = nullptr, *verdict = nullptr;
     uint32_t *txn = nullptr, *counts = nullptr, *tot = nullptr, *err = nullptr;
     uint64_t *xcnt = nullptr;  // [2 * nranks]: send counts, received counts
-    uint32_t *xvote = nullptr; // [4]: longest txn, argument flags, longest batch, replication blockers (MAX)
+    uint32_t *xvote = nullptr; // [8]: longest txn, argument flags, longest batch, replication blockers (MAX); groups: table widths
     int mode = 0;              // dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible
     uint32_t *gerr = nullptr;  // input-error bits, all-reduced (MAX)
+    // epoch groups (run_group)
+    uint32_t *rblk = nullptr, *rtot = nullptr;  // route counts: [P][kRouteBlocks], [P]
+    uint8_t *gcommit = nullptr;                 // the commit bytes when the caller passes none
+    unsigned long long *xacc = nullptr;         // execution: read digest, writes
 };
 
 }  // namespace dvcc
@@ -266,6 +501,12 @@ struct dvcc::Xport {
     virtual ~Xport() = default;
     // one u64 to every peer, one from every peer
     virtual int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) = 0;
+    // collectives issued between group(true) and group(false) may progress
+    // together (RCCL: ncclGroupStart / ncclGroupEnd)
+    virtual int group(bool begin) {
+        (void)begin;
+        return DV_OK;
+    }
     // bytes: send segment [sd[q], sd[q] + sc[q]) to peer q, receive rc[q] at rd[q]
     virtual int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv,
                             const size_t *rc, const size_t *rd, hipStream_t s) = 0;
@@ -284,6 +525,9 @@ struct RcclXport final : Xport {
     int P = 0;
     ~RcclXport() override {
         if (comm) (void)ncclCommDestroy(comm);
+    }
+    int group(bool begin) override {
+        return nccl_fail(begin ? ncclGroupStart() : ncclGroupEnd(), begin ? "ncclGroupStart" : "ncclGroupEnd");
     }
     int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) override {
         return nccl_fail(ncclAllToAll(send, recv, 1, ncclUint64, comm, s), "ncclAllToAll");
@@ -425,7 +669,7 @@ struct LocalXport final : Xport {
 
 void free_bufs(DvComm *m) {
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
-                 m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr};
+                 m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -434,6 +678,9 @@ void free_bufs(DvComm *m) {
     m->types = m->tables = m->verdict = nullptr;
     m->txn = m->counts = m->tot = m->err = m->xvote = m->gerr = nullptr;
     m->xcnt = nullptr;
+    m->rblk = m->rtot = nullptr;
+    m->gcommit = nullptr;
+    m->xacc = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -457,8 +704,12 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->tot, P));
     CHK(alloc(&m->err, 1));
     CHK(alloc(&m->xcnt, 2ull * P));
-    CHK(alloc(&m->xvote, 4));
+    CHK(alloc(&m->xvote, 8));
     CHK(alloc(&m->gerr, 1));
+    CHK(alloc(&m->rblk, (uint64_t)P * kRouteBlocks));
+    CHK(alloc(&m->rtot, P));
+    CHK(alloc(&m->gcommit, txn));
+    CHK(alloc(&m->xacc, 2));
     m->acc_cap = acc;
     m->nb_cap = nb;
     m->txn_cap = txn;
@@ -755,6 +1006,196 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     return hip_fail2(hipStreamSynchronize(s), "sync");
 }
 
+
+// One epoch group (dv_epoch_group_run): homes[e] is this rank's client batch
+// of epoch e of the group.  Collectives, in the same order on every rank:
+//   1. all-to-all of the batch sizes (rank e learns the parts of epoch e) and
+//      the argument vote (all-reduce MAX);
+//   2. three all-to-allv (grouped) move every batch to its epoch's decider as
+//      9 B per access -- row id, global txn id, type -- landing contiguous in
+//      origin order, Calvin's sequence (work_queue.cpp:105-151);
+//   3. rank e decides epoch e with the replicated single-GPU path (prefix
+//      kill, asynchronous rounds; its one all-reduce of the input-error bits
+//      after the probe fails the group on every rank), routing the committed
+//      accesses by owner instead of executing them;
+//   4. all-to-all of {committed txns, records per owner} and the outcome vote;
+//   5. two all-to-allv (grouped): the records to their owners (RFWD-like
+//      forwarding of what each owner must write, message.cpp:982-1025), and
+//      every origin's commit bytes back to it (the client responses);
+//   6. each rank executes the records of epochs 0..P-1 on its rows, in order.
+int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank, uint8_t *d_commit,
+              dv_stats *st) {
+    if (!c) return DV_ERR_ARG;
+    DvComm *m = ctx_comm(c);
+    if (!m) return DV_ERR_STATE;
+    const dv_config &cfg = ctx_config(c);
+    const uint32_t P = (uint32_t)m->nranks;
+    const uint64_t n_txn64 = (uint64_t)txns_per_rank * P;
+    bool bad = !homes || n_homes != P || n_txn64 > cfg.max_txn || n_txn64 > m->txn_cap || !ctx_has_tables(c) ||
+               cfg.workload != DV_YCSB;
+    uint64_t n_send = 0;
+    uint32_t max_len = 0;
+    for (uint32_t e = 0; e < P && !bad; e++) {
+        const dv_epoch_dev &h = homes[e];
+        bad = h.n_txn > txns_per_rank || (h.n_acc && (!h.keys || !h.types || !h.acc_txn));
+        n_send += h.n_acc;
+        if (h.n_acc) max_len = std::max<uint32_t>(max_len, h.max_txn_acc ? h.max_txn_acc : kMaxPos);
+    }
+    bad = bad || n_send > m->acc_cap;
+    hipStream_t s = ctx_stream(c);
+    const uint64_t acap = m->acc_cap;
+
+    // 1. sizes and the argument vote: longest txn, bad arguments / capacity,
+    //    -, a rank whose table is not a dense YCSB map (then nobody runs), and
+    //    the widest and (complemented) narrowest table: a key's range check on
+    //    its decider is its owner's only if every partition has the same rows
+    const bool capable = ctx_group_capable(c, P);
+    uint64_t *f0 = nullptr;
+    const uint64_t *pkey = nullptr;
+    const uint32_t nb = capable ? (uint32_t)ctx_table0_rows(c) : 0u;
+    const uint32_t vote[6] = {max_len, bad ? kVoteBadArg : 0u, 0u, capable ? 0u : kRepBlockOff, nb, ~nb};
+    std::vector<uint64_t> sendc(P, 0), recvc(P);
+    for (uint32_t e = 0; e < P && !bad; e++) sendc[e] = homes[e].n_acc;
+    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
+    CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
+    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
+    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, acap), m->xvote);
+    CHK(hip_fail2(hipGetLastError(), "k_recv_check"));
+    CHK(m->x->max_u32(m->xvote, 6, s));
+    uint32_t gvote[6] = {0, 0, 0, 0, 0, 0};
+    CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    if (gvote[1] || gvote[3] || gvote[4] != ~gvote[5]) return DV_ERR_ARG;  // every rank
+    const uint32_t glen = std::min<uint32_t>(gvote[0] ? gvote[0] : 1u, kMaxPos);
+
+    // 2. every batch to its decider: [row ids 4 B | txn ids 4 B | types 1 B]
+    uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
+    uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *stx = reinterpret_cast<uint32_t *>(sb + 4 * acap);
+    uint8_t *sy = sb + 8 * acap;
+    uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * acap);
+    uint8_t *ry = rb + 8 * acap;
+    std::vector<size_t> sc(P), sd(P), rc(P), rd(P), sc4(P), sd4(P), rc4(P), rd4(P);
+    uint64_t so = 0, ro = 0;
+    for (uint32_t e = 0; e < P; e++) {
+        const uint64_t n = sendc[e];
+        if (n) {
+            const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
+            k_rep_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                 (uint32_t)m->rank * txns_per_rank, sk + so, stx + so, sy + so);
+        }
+        sc[e] = n;
+        sd[e] = so;
+        sc4[e] = 4 * n;
+        sd4[e] = 4 * so;
+        so += n;
+        rc[e] = recvc[e];
+        rd[e] = ro;
+        rc4[e] = 4 * recvc[e];
+        rd4[e] = 4 * ro;
+        ro += recvc[e];
+    }
+    CHK(hip_fail2(hipGetLastError(), "pack"));
+    CHK(m->x->group(true));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc4.data(), sd4.data(),
+                          reinterpret_cast<uint8_t *>(rk), rc4.data(), rd4.data(), s));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc4.data(), sd4.data(),
+                          reinterpret_cast<uint8_t *>(rt), rc4.data(), rd4.data(), s));
+    CHK(m->x->all_to_allv(sy, sc.data(), sd.data(), ry, rc.data(), rd.data(), s));
+    CHK(m->x->group(false));
+
+    // 3. decide this rank's epoch; its committed accesses are routed into the
+    //    send area (free again once the batches have left)
+    dv_epoch_dev ep{};
+    ep.keys = reinterpret_cast<const uint64_t *>(rk);  // (read as 32-bit row ids)
+    ep.types = ry;
+    ep.acc_txn = rt;
+    ep.tables = nullptr;
+    ep.n_acc = ro;
+    ep.n_txn = (uint32_t)n_txn64;
+    ep.max_txn_acc = glen;
+    const RouteOut rout{reinterpret_cast<uint2 *>(m->send), m->rblk, m->rtot, P};
+    dv_stats est{};
+    const int rd_ = epoch_run_replicated(c, &ep, rk, P, m->verdict, &est, &rout);
+
+    // 4. the outcome vote (a failure on any rank fails the group on every
+    //    rank) and {committed, records per owner}
+    const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
+    CHK(hip_fail2(hipMemcpyAsync(m->xvote, &fail, sizeof(fail), hipMemcpyHostToDevice, s), "H2D"));
+    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, rd_ == 0, m->xcnt);
+    CHK(hip_fail2(hipGetLastError(), "k_route_words"));
+    std::vector<uint64_t> words(2 * P);
+    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
+    k_route_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, 2 * acap, m->xvote);
+    CHK(hip_fail2(hipGetLastError(), "k_route_recv_check"));
+    CHK(m->x->max_u32(m->xvote, 1, s));
+    CHK(hip_fail2(hipMemcpyAsync(words.data(), m->xcnt, 2 * P * 8, hipMemcpyDeviceToHost, s), "D2H"));
+    uint32_t gfail = 0;
+    CHK(hip_fail2(hipMemcpyAsync(&gfail, m->xvote, sizeof(gfail), hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    if (gfail) return -(int)gfail;
+
+    // 5. records to their owners, commit bytes back to their origins
+    uint64_t committed = 0;
+    std::vector<uint64_t> rcnt(P);
+    so = ro = 0;
+    std::vector<size_t> tc(P), td(P), uc(P), ud(P);
+    for (uint32_t q = 0; q < P; q++) {
+        const uint64_t out = words[q] & 0xFFFFFFFFull, in = words[P + q] & 0xFFFFFFFFull;
+        committed += words[P + q] >> 32;
+        rcnt[q] = in;
+        sc[q] = 8 * out;
+        sd[q] = 8 * so;
+        rc[q] = 8 * in;
+        rd[q] = 8 * ro;
+        so += out;
+        ro += in;
+        tc[q] = uc[q] = txns_per_rank;
+        td[q] = (size_t)q * txns_per_rank;
+        ud[q] = (size_t)q * txns_per_rank;
+    }
+    uint8_t *commit_out = d_commit ? d_commit : m->gcommit;
+    CHK(m->x->group(true));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->send), sc.data(), sd.data(),
+                          reinterpret_cast<uint8_t *>(m->recv), rc.data(), rd.data(), s));
+    CHK(m->x->all_to_allv(m->verdict, tc.data(), td.data(), commit_out, uc.data(), ud.data(), s));
+    CHK(m->x->group(false));
+
+    // 6. epochs 0..P-1 on this partition's rows, in order (2PL: a written row
+    //    has one committed txn, reads and writes in one launch; OCC / CALVIN:
+    //    reads first)
+    ctx_table0_cols(c, &f0, &pkey);
+    CHK(hip_fail2(hipMemsetAsync(m->xacc, 0, 2 * sizeof(unsigned long long), s), "memset"));
+    const bool fused = cfg.cc_alg == DV_NO_WAIT || cfg.cc_alg == DV_WAIT_DIE;
+    const uint2 *recs = reinterpret_cast<const uint2 *>(m->recv);
+    uint64_t off = 0;
+    for (uint32_t e = 0; e < P; e++) {
+        const uint64_t n = rcnt[e];
+        if (n) {
+            const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 1024);
+            if (fused) {
+                k_route_exec<3><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
+            } else {
+                k_route_exec<1><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
+                k_route_exec<2><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
+            }
+        }
+        off += n;
+    }
+    CHK(hip_fail2(hipGetLastError(), "k_route_exec"));
+    unsigned long long acc[2] = {0, 0};
+    CHK(hip_fail2(hipMemcpyAsync(acc, m->xacc, sizeof(acc), hipMemcpyDeviceToHost, s), "D2H"));
+    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    if (st) {
+        *st = est;  // this rank's decision: rounds, sort passes, timings
+        st->n_txn = n_txn64 * P;
+        st->committed = committed;
+        st->aborted = n_txn64 * P - committed;
+        st->read_digest = acc[0];
+        st->write_cnt = acc[1];
+    }
+    return DV_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -762,6 +1203,11 @@ extern "C" {
 int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st) {
     return run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
+}
+
+int dv_epoch_group_run(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
+                       uint8_t *d_commit, dv_stats *st) {
+    return run_group(c, homes, n_homes, txns_per_rank, d_commit, st);
 }
 
 int dv_comm_set_mode(dv_ctx *c, int mode) {

@@ -333,7 +333,31 @@ uint32_t async_try_limit(uint32_t G);
 // round elements ((txn << slog | pos) << 3 | flags) fit 32 bits
 bool round_el32(uint32_t n_txn, uint32_t slog);
 
-// ---- execution and outputs (dvcc_kernels.hip)
+// ---- epoch groups (dvcc_comm.hip run_group): the deciding rank routes its
+// epoch's committed accesses to their owners instead of executing them.  A
+// record is {local row | wr << 31 | "sees an earlier write" << 30, global
+// txn}; owner = global row % P, local row = global row / P (YCSB, key % P).
+// Records of one owner are contiguous (owner-major, offsets from per-block
+// counts); their order inside an owner's segment is free, since one epoch's
+// execution on a row does not depend on it (2PL: a written row has one
+// committed txn; OCC and Calvin: reads run before writes and carry what they
+// see).
+constexpr uint32_t kRouteBlocks = 256;
+constexpr uint32_t RT_WR = 0x80000000u, RT_SEESW = 0x40000000u;
+struct RouteOut {
+    uint2 *rec;     // records, owner-major
+    uint32_t *blk;  // [P][kRouteBlocks] records per owner per block
+    uint32_t *tot;  // [P] records per owner
+    uint32_t P;
+};
+// NO_WAIT / WAIT_DIE / OCC: the committed txns' accesses (txn-major acc_row)
+void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
+                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr);
+// CALVIN: every access, in row order (sorted pairs, queue elements, "an
+// earlier write precedes" flags)
+void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs, const uint64_t *el,
+                       const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr);
+
 // ---- runtime accessors for the RCCL driver (dvcc_comm.hip)
 struct DvComm;  // defined in dvcc_comm.hip
 }  // namespace dvcc
@@ -344,11 +368,19 @@ bool ctx_has_tables(dv_ctx *c);  // some table is loaded (dv_epoch_begin's preco
 // replicated epochs (dvcc_comm.hip run_part): table 0 is a loaded YCSB
 // implicit-row map whose global row space (nranks x buckets) fits 31 bits
 bool ctx_rep_capable(dv_ctx *c, uint32_t nranks);
+// epoch groups: ... and the map is dense (dv_load_ycsb_partition: every key
+// b * nranks + rank below the row space exists), so a range check is the
+// owner's key check
+bool ctx_group_capable(dv_ctx *c, uint32_t nranks);
+void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey);  // table 0's local rows
+uint64_t ctx_table0_rows(dv_ctx *c);  // ... their count (buckets of its direct map)
 uint32_t *ctx_err_words(dv_ctx *c);  // &Counters::err (peer_err follows)
 // the whole epoch on this rank, its own rows executed (dvcc_runtime.hip)
 // keys32: the epoch's keys as 32-bit row ids (ep->keys is then ignored)
+// route (epoch groups): committed accesses routed to their owners, nothing
+// executes here
 int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
-                         uint8_t *d_commit, dv_stats *st);
+                         uint8_t *d_commit, dv_stats *st, const dvcc::RouteOut *route = nullptr);
 int comm_combine_errors(dv_ctx *c);  // dvcc_comm.hip
 void comm_free(dvcc::DvComm *m);
 namespace dvcc {

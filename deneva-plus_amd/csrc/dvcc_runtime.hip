@@ -26,6 +26,7 @@ namespace {
 struct HostTable {
     bool created = false, loaded = false;
     bool implicit_rows = false;  // direct map with local row == bucket: probes read pkey
+    bool dense = false;          // dv_load_ycsb_partition: bucket b holds key b * P + part, every b
     uint64_t cap_rows = 0, n_rows = 0, nbuckets = 0, row_base = 0;
     uint32_t hash_kind = DV_HASH_YCSB;
     IxEntry *ix = nullptr;      // device
@@ -141,6 +142,7 @@ struct dv_ctx {
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
     const uint32_t *keys32 = nullptr;  // ... its keys as 32-bit row ids
+    const RouteOut *route = nullptr;   // epoch groups: committed accesses go to their owners (run_group)
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
     int pf_sorted_a = 0, pf_key_bits = 0;
@@ -343,6 +345,14 @@ bool ctx_rep_capable(dv_ctx *c, uint32_t nranks) {
     const HostTable &t = c->tab[0];
     return c->cfg.workload == DV_YCSB && t.loaded && t.implicit_rows && t.hash_kind == DV_HASH_YCSB &&
            (uint64_t)nranks * t.nbuckets <= 0x7FFFFFFFull;
+}
+bool ctx_group_capable(dv_ctx *c, uint32_t nranks) {
+    return ctx_rep_capable(c, nranks) && c->tab[0].dense && c->tab[0].nbuckets < (1ull << 30);
+}
+uint64_t ctx_table0_rows(dv_ctx *c) { return c->tab[0].nbuckets; }
+void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey) {
+    *f0 = c->f0 + c->tab[0].row_base;
+    *pkey = c->pkey + c->tab[0].row_base;
 }
 uint32_t *ctx_err_words(dv_ctx *c) { return &c->ctr->err; }
 
@@ -668,6 +678,7 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
     bool implicit = direct;
     for (uint64_t b = 0; b < nb && implicit; b++) implicit = ent[cnt[b]].row == b;
     t.implicit_rows = implicit;
+    t.dense = false;
     int r = implicit ? DV_OK : dalloc(&t.ix, direct ? nb : (n ? n : 1));
     if (r) return r;
     if (direct && !implicit) {
@@ -715,6 +726,7 @@ int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
     t.ix = nullptr;
     t.bstart = nullptr;
     t.implicit_rows = true;  // row r holds key r * P + part, in bucket r
+    t.dense = true;
     launch_ycsb_load(c->stream, rows_per_part, c->cfg.part_cnt, c->cfg.part_id, c->f0 + t.row_base,
                      c->pkey + t.row_base, c->ktag + t.row_base);
     HIPCHK(hipGetLastError());
@@ -1050,6 +1062,11 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.ctr = c->ctr;
         if (c->tp_oid) (void)hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream);
         launch_tpcc_exec(c->stream, x);
+    } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
+        if (c->cfg.cc_alg == DV_CALVIN)
+            launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);
+        else
+            launch_route_txn(c->stream, *c->route, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->ctr);
     } else {
         RowMap rm{};  // replicated epoch: global rows -> this partition's
         if (c->rep_P) {
@@ -1511,13 +1528,15 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
 // the ranks after the probe, all txns are decided here, and only this
 // partition's rows execute.  Every rank computes the same decisions.
 int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
-                         uint8_t *d_commit, dv_stats *st) {
+                         uint8_t *d_commit, dv_stats *st, const RouteOut *route) {
     if (!c || !ep || nranks == 0) return DV_ERR_ARG;
     c->rep_P = nranks;
     c->keys32 = keys32;
+    c->route = route;
     const int r = dv_epoch_run_device(c, ep, d_commit, nullptr, st);
     c->rep_P = 0;
     c->keys32 = nullptr;
+    c->route = nullptr;
     return r;
 }
 

@@ -295,6 +295,18 @@ class CCEngine:
                                           _ptr(d_commit), ctypes.byref(st)), "dv_epoch_run_part")
         return st
 
+    def run_epoch_group(self, homes, txns_per_rank, d_commit=None):
+        """One epoch group (dv_epoch_group_run): homes[e] is this rank's
+        client batch (DeviceEpoch) of epoch e of the group, one per rank;
+        d_commit: nranks * txns_per_rank device bytes, this rank's txns'
+        commit bytes of epoch e at e * txns_per_rank."""
+        self._after_torch()
+        st = L.Stats()
+        arr = (L.EpochDev * len(homes))(*[h.desc() for h in homes])
+        L.check(L.lib().dv_epoch_group_run(self._ctx, arr, len(homes), txns_per_rank, _ptr(d_commit),
+                                           ctypes.byref(st)), "dv_epoch_group_run")
+        return st
+
     def carry(self, dep, max_txn=None):
         """Abort carry-over: a DeviceEpoch of the last epoch's (`dep`'s)
         aborted txns, in sequence order, at most max_txn of them."""

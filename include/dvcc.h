@@ -300,6 +300,28 @@ int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_r
  * possible, also on a one-rank communicator.  Same decisions either way. */
 int dv_comm_set_mode(dv_ctx *ctx, int mode);
 
+/* Epoch groups -- epoch-parallel scheduling for YCSB: a
+ * group is P = nranks consecutive epochs of the sequencer, and homes[e]
+ * (n_homes == P) is this rank's client batch of epoch e (txn ids local,
+ * global sequence number in epoch e: rank * txns_per_rank + id).  Rank e
+ * receives every rank's batch of epoch e (all-to-allv, 9 B per access, in
+ * origin order = Calvin's sequence), decides epoch e alone with the
+ * single-GPU path, and forwards the committed accesses to the partitions
+ * owning their rows; every rank then executes epochs 0..P-1 on its own rows,
+ * in epoch order.  An epoch's decisions depend only on its own accesses, so
+ * the results equal running the P epochs one after the other (dv_epoch_run_part
+ * or one GPU): same commit bytes, same final rows.  d_commit (device, P *
+ * txns_per_rank bytes, may be NULL): the commit bytes of this rank's txns,
+ * epoch e at e * txns_per_rank.  st: committed / aborted / n_txn over the whole
+ * group, read_digest / write_cnt of this partition's rows, rounds and
+ * timings and n_acc of the epoch this rank decided.
+ * Requires every rank's table 0 loaded by dv_load_ycsb_partition (a dense
+ * map, so a key's range check is its owner's key check); DV_ERR_ARG on every
+ * rank otherwise.  Errors (a key out of range in any epoch, ...) are voted:
+ * every rank returns the same code and no row changes. */
+int dv_epoch_group_run(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
+                       uint8_t *d_commit, dv_stats *st);
+
 /* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
  * same txn statuses after each round, hence the same list of undecided txns
  * (ascending).  dv_epoch_round_local writes this partition's verdict byte for

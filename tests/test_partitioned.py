@@ -518,6 +518,166 @@ def test_engine_driver_error_is_collective(cc, mode):
         eng.close()
 
 
+# ---- epoch groups (dv_epoch_group_run): P epochs per group, epoch e decided
+# by rank e, committed accesses routed to their owners, executed in epoch
+# order on every partition
+def _run_group_epochs(engines, homes, n_txn):
+    """run_epoch_group on every engine concurrently (homes[r] = rank r's
+    batches of the group's epochs); (commit bytes, stats) or the exception."""
+    import threading
+    world = len(engines)
+    out = [None] * world
+
+    def body(r):
+        try:
+            d = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+            st = engines[r].run_epoch_group(homes[r], n_txn, d)
+            out[r] = (d.cpu().numpy(), st)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a rank hung in the epoch group"
+    return out
+
+
+def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None):
+    """Every epoch of every group against the one-partition oracle run over
+    the sequenced epochs one after the other: commit bytes (each rank holds its
+    own txns' bytes of every epoch), committed count, digest and writes summed
+    over the partitions, and every partition's rows after each group.
+    sizes: per-rank batch sizes (unequal batches; the rest of a rank's
+    sequence slots are empty txns)."""
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
+    engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    sizes = sizes or [n_txn] * world
+    for g in range(groups):
+        homes = [[None] * world for _ in range(world)]  # [rank][epoch]
+        refs = []
+        for e in range(world):
+            batches = [gen.gen(sizes[r], dvcc.epoch_seed(r, 40 + g * world + e), r) for r in range(world)]
+            padded = []
+            for b in batches:
+                tb = np.concatenate([b.txn_begin, np.full(n_txn - b.n_txn, b.txn_begin[-1], np.uint32)])
+                padded.append(dvcc.Epoch(b.keys, b.types, tb))
+            q = dvcc.sequence(padded)
+            c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin, q.keys,
+                                           q.types)
+            refs.append((c_ref, st_ref))
+            for r in range(world):
+                homes[r][e] = dvcc.DeviceEpoch(batches[r])
+        res = _run_group_epochs(engines, homes, n_txn)
+        committed = sum(st.committed for _, st in refs)
+        digest = writes = 0
+        for r, x in enumerate(res):
+            assert not isinstance(x, Exception), f"rank {r}: {x}"
+            c, st = x
+            for e in range(world):
+                mine = refs[e][0][r * n_txn:(r + 1) * n_txn]
+                assert (c[e * n_txn:(e + 1) * n_txn] == mine).all(), f"group {g} epoch {e} rank {r}"
+            assert st.committed == committed and st.n_txn == n_txn * world * world
+            digest = (digest + st.read_digest) % (1 << 64)
+            writes += st.write_cnt
+        assert digest == sum(st.read_digest for _, st in refs) % (1 << 64)
+        assert writes == sum(st.write_cnt for _, st in refs)
+        for p, eng in enumerate(engines):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"group {g} partition {p} table"
+    for eng in engines:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+@pytest.mark.parametrize("world,mpr", [(2, 0.3), (8, 0.1), (8, 0.5)])
+def test_epoch_groups(cc, world, mpr):
+    """Epoch-parallel scheduling: P epochs per group decided side by side (one
+    per rank) and executed in epoch order on every partition -- the same
+    commit bytes, digests and rows as the oracle running the epochs in
+    sequence.  (The contexts share one GPU: asynchronous rounds off.)"""
+    _check_epoch_groups(cc, world, 1 << 14, 3000, mpr)
+
+
+@pytest.mark.gpu
+def test_epoch_groups_unequal_batches():
+    _check_epoch_groups(dvcc.NO_WAIT, 3, 1 << 13, 1000, 0.3, sizes=[1000, 640, 913])
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_epoch_groups_prefix_kill():
+    """Epochs large enough for the prefix-kill path in the decider: 4
+    partitions x 40,000 txns per batch (160,000-txn epochs)."""
+    _check_epoch_groups(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, groups=1)
+
+
+@pytest.mark.gpu
+def test_epoch_groups_errors_are_collective():
+    """A key out of range in one batch of one epoch fails the group on every
+    rank with DV_ERR_KEY_NOT_FOUND and changes no row; a rank whose table is
+    not a dense YCSB map makes every rank return DV_ERR_ARG; the group then
+    runs normally."""
+    world, rows_pp, n_txn = 4, 1 << 12, 1000
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    homes = [[dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(r, 60 + e), r)) for e in range(world)]
+             for r in range(world)]
+    bad = gen.gen(n_txn, dvcc.epoch_seed(1, 62), 1)
+    bad.keys[7] = np.uint64(rows_pp * world + 5)
+    bad_homes = [list(h) for h in homes]
+    bad_homes[1][2] = dvcc.DeviceEpoch(bad)
+    res = _run_group_epochs(engines, bad_homes, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, x)
+    for eng, b in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b).all()
+    res = _run_group_epochs(engines, homes, n_txn)
+    assert all(not isinstance(x, Exception) for x in res), res
+    # partition 3 reloaded through dv_load_table (keys in bucket order, so an
+    # implicit-row map, but not known dense): the group is refused everywhere
+    keys = np.arange(rows_pp, dtype=np.uint64) * world + 3
+    engines[3].load_table(0, keys, engines[3].read_table(0, rows_pp))
+    res = _run_group_epochs(engines, homes, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
+    for eng in engines:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC, dvcc.CALVIN])
+def test_rccl_epoch_group_single_rank(cc):
+    """dv_epoch_group_run over RCCL on a one-rank communicator: the batch
+    all-to-allv, route all-to-allv and commit-byte return run for real and
+    must equal the single-GPU path."""
+    rows, n_txn = 1 << 14, 6000
+    gen = dvcc.YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    e = gen.gen(n_txn, dvcc.epoch_seed(0, 3))
+    ref = dvcc.CCEngine(cc, n_txn, e.n_acc)
+    ref.load_ycsb_partition(rows)
+    c_ref = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    eng = dvcc.CCEngine(cc, n_txn, e.n_acc, part_cnt=1, part_id=0)
+    eng.load_ycsb_partition(rows)
+    eng.comm_init(dvcc.comm_unique_id(), 1, 0)
+    c = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    for _ in range(2):  # epochs in sequence: the second sees the first's writes
+        st_ref = ref.run_epoch_device(dvcc.DeviceEpoch(e), c_ref)
+        st = eng.run_epoch_group([dvcc.DeviceEpoch(e)], n_txn, c)
+        assert torch.equal(c, c_ref)
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt)
+        assert (eng.read_table(0, rows) == ref.read_table(0, rows)).all()
+    eng.close()
+    ref.close()
+
+
 class NumpyTpccPartition(NumpyPartition):
     """Test double for TPC-C fragments: the last-name lookup (mid of the
     newest-first list, tpcc_txn.cpp:600-626) on the host, then rows keyed by
