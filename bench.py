@@ -318,6 +318,22 @@ def e2e_host_leg(eng, epochs, k):
     return out
 
 
+class stdout_to_stderr:
+    """RCCL prints its version banner on stdout when a communicator is made;
+    the bench's stdout carries exactly one JSON line, so the C-level stdout
+    points at stderr meanwhile."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def launch_ranks(a):
     """--gpus N > 1 without a launcher: run this script as N rank processes
     under torch.distributed.run (one per GPU) as a child, and return its exit
@@ -481,7 +497,8 @@ class PartitionedBench:
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
         if world > 1:
             dist.broadcast_object_list(uid, src=0)
-        self.eng.comm_init(uid[0], world, rank)
+        with stdout_to_stderr():
+            self.eng.comm_init(uid[0], world, rank)
         self.eng.comm_set_mode(a.part_mode)
         self.rows = rows
         self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
@@ -525,7 +542,9 @@ def main():
     a.gpus = world
     torch.cuda.set_device(local_rank)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.barrier()
     if a.tpcc_only:
         print(json.dumps({"tpcc": tpcc_leg(a)}), flush=True)
         return

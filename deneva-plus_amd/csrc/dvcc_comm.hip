@@ -25,6 +25,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <mutex>
@@ -315,32 +316,41 @@ __global__ __launch_bounds__(kBlock) void k_route_count(RouteSrc<SRC> src, Route
     for (uint32_t o = threadIdx.x; o < ro.P; o += kBlock) ro.blk[o * kRouteBlocks + blockIdx.x] = c[o];
 }
 
+// per owner (one block each): the blocks' counts -> exclusive prefix in
+// place, tot[o] = the owner's records
+__global__ __launch_bounds__(kBlock) void k_route_scan(RouteOut ro) {
+    __shared__ uint32_t lds4[4];
+    uint32_t *c = ro.blk + (uint64_t)blockIdx.x * kRouteBlocks;
+    constexpr uint32_t per = kRouteBlocks / kBlock;
+    uint32_t v[per], sum = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) {
+        v[j] = c[threadIdx.x * per + j];
+        sum += v[j];
+    }
+    uint32_t t = 0;
+    uint32_t pre = block_excl_scan256(sum, lds4, &t);
+#pragma unroll
+    for (uint32_t j = 0; j < per; j++) {
+        c[threadIdx.x * per + j] = pre;
+        pre += v[j];
+    }
+    if (threadIdx.x == 0) ro.tot[blockIdx.x] = t;
+}
+
 // pass 2: the same walk (same grid, same items per block), each block
 // writing at its owner-major offsets
 template <int SRC>
 __global__ __launch_bounds__(kBlock) void k_route_scatter(RouteSrc<SRC> src, RouteOut ro, const Counters *ctr) {
-    __shared__ uint32_t tots[kRadix], cur[kRadix];
+    __shared__ uint32_t cur[kRadix];
     const uint32_t P = ro.P;
-    uint32_t pre = 0;
-    for (uint32_t o = threadIdx.x; o < P; o += kBlock) {
-        uint32_t t = 0;
-        for (uint32_t b = 0; b < kRouteBlocks; b++) {
-            const uint32_t v = ro.blk[o * kRouteBlocks + b];
-            if (b < blockIdx.x) pre += v;
-            t += v;
-        }
-        tots[o] = t;
-        cur[o] = pre;
-    }
-    __syncthreads();
+    if (input_err(ctr) || ctr->halt) return;
     for (uint32_t o = threadIdx.x; o < P; o += kBlock) {
         uint32_t off = 0;
-        for (uint32_t q = 0; q < o; q++) off += tots[q];
-        cur[o] += off;
-        if (blockIdx.x == 0) ro.tot[o] = tots[o];
+        for (uint32_t q = 0; q < o; q++) off += ro.tot[q];
+        cur[o] = off + ro.blk[o * kRouteBlocks + blockIdx.x];
     }
     __syncthreads();
-    if (input_err(ctr) || ctr->halt) return;
     const uint32_t lane = threadIdx.x & 63, ob = owner_bits(P);
     auto emit = [&](bool v, uint32_t row, uint32_t flags, uint32_t txn) {
         const uint32_t o = v ? row % P : 0u;
@@ -397,6 +407,36 @@ __global__ __launch_bounds__(kBlock) void k_route_exec(const uint2 *__restrict__
 
 // the send words of the outcome exchange: committed txns of this epoch << 32
 // | records for owner q
+// ---- host round trips without blits or stream synchronisation: small
+// host values reach the device as kernel arguments (k_put_words), device
+// values reach the host through a host-mapped mailbox written by one kernel
+// with system-scope stores and a sequence word the host spins on
+struct PutArgs {
+    uint64_t v64[kRadix];
+    uint32_t v32[8];
+    uint32_t n64, n32;
+    uint64_t *d64;
+    uint32_t *d32;
+};
+__global__ void k_put_words(PutArgs a) {
+    for (uint32_t i = threadIdx.x; i < a.n64; i += blockDim.x) a.d64[i] = a.v64[i];
+    for (uint32_t i = threadIdx.x; i < a.n32; i += blockDim.x) a.d32[i] = a.v32[i];
+}
+
+struct CommMail {
+    unsigned long long seq;
+    unsigned long long pad[7];
+    unsigned long long w[4 * kRadix];
+};
+__global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const uint32_t *__restrict__ b, uint32_t nb,
+                           CommMail *m, unsigned long long seq) {
+    for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) m->w[i] = a[i];
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m->w[na + i] = b[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // the routed records this rank receives exceed its receive area: the group
 // fails on every rank (outcome vote word 0 = -DV_ERR_ARG at least)
 __global__ void k_route_recv_check(const uint64_t *__restrict__ words, uint32_t P, uint64_t cap,
@@ -407,15 +447,17 @@ __global__ void k_route_recv_check(const uint64_t *__restrict__ words, uint32_t 
     if (n > cap && vote[0] < (uint32_t)(-DV_ERR_ARG)) vote[0] = (uint32_t)(-DV_ERR_ARG);
 }
 
-__global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, int ok,
-                              uint64_t *__restrict__ words) {
-    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) words[q] = (committed << 32) | (ok ? tot[q] : 0u);
+__global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
+                              uint64_t *__restrict__ words, uint32_t *__restrict__ vote) {
+    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) words[q] = (committed << 32) | (fail ? 0u : tot[q]);
+    if (threadIdx.x == 0) vote[0] = fail;
 }
 
 void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
                       const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr) {
     const RouteSrc<0> src{tb_start, tb_end, acc_row, n_txn, nullptr, nullptr, nullptr, 0, status};
     k_route_count<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    k_route_scan<<<ro.P, kBlock, 0, s>>>(ro);
     k_route_scatter<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
 }
 
@@ -423,6 +465,7 @@ void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs,
                        const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr) {
     const RouteSrc<1> src{nullptr, nullptr, nullptr, 0, pairs, el, ew, n, status};
     k_route_count<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    k_route_scan<<<ro.P, kBlock, 0, s>>>(ro);
     k_route_scatter<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
 }
 
@@ -457,6 +500,8 @@ struct DvComm {
     uint32_t *xvote = nullptr; // [8]: longest txn, argument flags, longest batch, replication blockers (MAX); groups: table widths
     int mode = 0;              // dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible
     uint32_t *gerr = nullptr;  // input-error bits, all-reduced (MAX)
+    CommMail *h_mail = nullptr, *d_mail = nullptr;  // host-mapped mailbox (mail_wait)
+    unsigned long long mseq = 0;
     // epoch groups (run_group)
     uint32_t *rblk = nullptr, *rtot = nullptr;  // route counts: [P][kRouteBlocks], [P]
     uint8_t *gcommit = nullptr;                 // the commit bytes when the caller passes none
@@ -668,6 +713,8 @@ struct LocalXport final : Xport {
 };
 
 void free_bufs(DvComm *m) {
+    if (m->h_mail) (void)hipHostFree(m->h_mail);
+    m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc};
     for (void *p : b)
@@ -710,6 +757,11 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->rtot, P));
     CHK(alloc(&m->gcommit, txn));
     CHK(alloc(&m->xacc, 2));
+    CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), sizeof(CommMail),
+                                hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
+    CHK(hip_fail2(hipHostGetDevicePointer(reinterpret_cast<void **>(&m->d_mail), m->h_mail, 0),
+                  "hipHostGetDevicePointer"));
+    std::memset(m->h_mail, 0, sizeof(CommMail));
     m->acc_cap = acc;
     m->nb_cap = nb;
     m->txn_cap = txn;
@@ -816,6 +868,44 @@ int dv_comm_init_local(dv_ctx **ctxs, int nranks) {
 
 namespace {
 
+// device words -> the host: queue the mailbox kernel and spin on its
+// sequence word (a drained stream without it is an error)
+int mail_get(DvComm *m, hipStream_t s, const uint64_t *a, uint32_t na, const uint32_t *b, uint32_t nb,
+             uint64_t *out64, uint32_t *out32) {
+    const unsigned long long want = ++m->mseq;
+    k_mail_out<<<1, kBlock, 0, s>>>(a, na, b, nb, m->d_mail, want);
+    CHK(hip_fail2(hipGetLastError(), "k_mail_out"));
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0;; i++) {
+        if (__atomic_load_n(&m->h_mail->seq, __ATOMIC_ACQUIRE) >= want) break;
+        if ((i & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess && __atomic_load_n(&m->h_mail->seq, __ATOMIC_ACQUIRE) >= want) break;
+            if (q == hipSuccess) return hip_fail2(hipErrorUnknown, "mailbox");
+            if (q != hipErrorNotReady) return hip_fail2(q, "stream");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) return DV_ERR_STATE;
+        }
+        __builtin_ia32_pause();
+    }
+    for (uint32_t i = 0; i < na; i++) out64[i] = m->h_mail->w[i];
+    for (uint32_t i = 0; i < nb; i++) out32[i] = (uint32_t)m->h_mail->w[na + i];
+    return DV_OK;
+}
+
+// host words -> device buffers, as kernel arguments
+int put_words(hipStream_t s, const uint64_t *v64, uint32_t n64, uint64_t *d64, const uint32_t *v32, uint32_t n32,
+              uint32_t *d32) {
+    PutArgs a{};
+    a.n64 = n64;
+    a.n32 = n32;
+    a.d64 = d64;
+    a.d32 = d32;
+    for (uint32_t i = 0; i < n64 && i < (uint32_t)kRadix; i++) a.v64[i] = v64[i];
+    for (uint32_t i = 0; i < n32 && i < 8u; i++) a.v32[i] = v32[i];
+    k_put_words<<<1, kBlock, 0, s>>>(a);
+    return hip_fail2(hipGetLastError(), "k_put_words");
+}
+
 // The partitioned epoch of one rank (dv_epoch_run_part, dv_tpcc_epoch_run_part).
 // No rank may leave between collectives on its own: arguments are voted on
 // with the other ranks before anything depends on them, input errors found by
@@ -851,15 +941,12 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     const bool rep_here = !tpcc && m->mode != 1 && ctx_rep_capable(c, P);
     const uint32_t vote[4] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u,
                               (uint32_t)std::min<uint64_t>(n_home, 0xFFFFFFFFull), rep_here ? 0u : kRepBlockOff};
-    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
     std::vector<uint64_t> sendc(P, n_home), recvc(P);
-    CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
+    CHK(put_words(s, sendc.data(), P, m->xcnt, vote, 4, m->xvote));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
     CHK(m->x->max_u32(m->xvote, 4, s));
     uint32_t gvote[4] = {0, 0, 0, 0};
-    CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 4, recvc.data(), gvote));
     if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments were bad
     const uint32_t max_len = std::min<uint32_t>(gvote[0], kMaxPos);
     // 2. replicated when every rank allows it and the whole epoch fits this
@@ -923,16 +1010,13 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     CHK(hip_fail2(hipGetLastError(), "owner split"));
     // per-owner counts, the second vote (owner bytes, capacity), the records
     std::vector<uint32_t> tot(P);
-    CHK(hip_fail2(hipMemcpyAsync(tot.data(), m->tot, P * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    CHK(mail_get(m, s, nullptr, 0, m->tot, P, nullptr, tot.data()));
     for (uint32_t o = 0; o < P; o++) sendc[o] = tot[o];
-    CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
+    CHK(put_words(s, sendc.data(), P, m->xcnt, nullptr, 0, nullptr));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
     k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, cap, m->xvote);
     CHK(m->x->max_u32(m->xvote, 2, s));
-    CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 2, recvc.data(), gvote));
     if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's owner bytes or capacity were bad
     std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
     uint64_t n_recv = 0, so = 0;
@@ -1056,16 +1140,13 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     const uint32_t vote[6] = {max_len, bad ? kVoteBadArg : 0u, 0u, capable ? 0u : kRepBlockOff, nb, ~nb};
     std::vector<uint64_t> sendc(P, 0), recvc(P);
     for (uint32_t e = 0; e < P && !bad; e++) sendc[e] = homes[e].n_acc;
-    CHK(hip_fail2(hipMemcpyAsync(m->xvote, vote, sizeof(vote), hipMemcpyHostToDevice, s), "H2D"));
-    CHK(hip_fail2(hipMemcpyAsync(m->xcnt, sendc.data(), P * 8, hipMemcpyHostToDevice, s), "H2D"));
+    CHK(put_words(s, sendc.data(), P, m->xcnt, vote, 6, m->xvote));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
     k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, acap), m->xvote);
     CHK(hip_fail2(hipGetLastError(), "k_recv_check"));
     CHK(m->x->max_u32(m->xvote, 6, s));
     uint32_t gvote[6] = {0, 0, 0, 0, 0, 0};
-    CHK(hip_fail2(hipMemcpyAsync(recvc.data(), m->xcnt + P, P * 8, hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipMemcpyAsync(gvote, m->xvote, sizeof(gvote), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 6, recvc.data(), gvote));
     if (gvote[1] || gvote[3] || gvote[4] != ~gvote[5]) return DV_ERR_ARG;  // every rank
     const uint32_t glen = std::min<uint32_t>(gvote[0] ? gvote[0] : 1u, kMaxPos);
 
@@ -1121,18 +1202,15 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     // 4. the outcome vote (a failure on any rank fails the group on every
     //    rank) and {committed, records per owner}
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    CHK(hip_fail2(hipMemcpyAsync(m->xvote, &fail, sizeof(fail), hipMemcpyHostToDevice, s), "H2D"));
-    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, rd_ == 0, m->xcnt);
+    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, m->xcnt, m->xvote);
     CHK(hip_fail2(hipGetLastError(), "k_route_words"));
     std::vector<uint64_t> words(2 * P);
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
     k_route_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, 2 * acap, m->xvote);
     CHK(hip_fail2(hipGetLastError(), "k_route_recv_check"));
     CHK(m->x->max_u32(m->xvote, 1, s));
-    CHK(hip_fail2(hipMemcpyAsync(words.data(), m->xcnt, 2 * P * 8, hipMemcpyDeviceToHost, s), "D2H"));
     uint32_t gfail = 0;
-    CHK(hip_fail2(hipMemcpyAsync(&gfail, m->xvote, sizeof(gfail), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    CHK(mail_get(m, s, m->xcnt, 2 * P, m->xvote, 1, words.data(), &gfail));
     if (gfail) return -(int)gfail;
 
     // 5. records to their owners, commit bytes back to their origins
@@ -1183,9 +1261,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         off += n;
     }
     CHK(hip_fail2(hipGetLastError(), "k_route_exec"));
-    unsigned long long acc[2] = {0, 0};
-    CHK(hip_fail2(hipMemcpyAsync(acc, m->xacc, sizeof(acc), hipMemcpyDeviceToHost, s), "D2H"));
-    CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+    uint64_t acc[2] = {0, 0};
+    CHK(mail_get(m, s, reinterpret_cast<const uint64_t *>(m->xacc), 2, nullptr, 0, acc, nullptr));
     if (st) {
         *st = est;  // this rank's decision: rounds, sort passes, timings
         st->n_txn = n_txn64 * P;

@@ -342,11 +342,11 @@ bool round_el32(uint32_t n_txn, uint32_t slog);
 // execution on a row does not depend on it (2PL: a written row has one
 // committed txn; OCC and Calvin: reads run before writes and carry what they
 // see).
-constexpr uint32_t kRouteBlocks = 256;
+constexpr uint32_t kRouteBlocks = 1024;  // (a multiple of kBlock: k_route_scan)
 constexpr uint32_t RT_WR = 0x80000000u, RT_SEESW = 0x40000000u;
 struct RouteOut {
     uint2 *rec;     // records, owner-major
-    uint32_t *blk;  // [P][kRouteBlocks] records per owner per block
+    uint32_t *blk;  // [P][kRouteBlocks] records per owner per block (then their exclusive prefix)
     uint32_t *tot;  // [P] records per owner
     uint32_t P;
 };
@@ -422,6 +422,10 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
                         uint64_t zero_words = 0);
+// the counters into their host-mapped mirror hctr, then *hseq = seq (device
+// pointers of host-mapped memory)
+void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
+                    unsigned long long seq);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,

@@ -723,6 +723,24 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
     for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < zero_n; i += stride) zero[i] = uint4{0, 0, 0, 0};
 }
 
+// the counters into their host-mapped mirror, then the sequence word the
+// host spins on (sync_counters): no blit and no stream synchronisation
+// between an epoch's last kernel and the host reading its outcome
+__global__ __launch_bounds__(kBlock) void k_ctr_out(const Counters *__restrict__ ctr, Counters *hctr,
+                                                    unsigned long long *hseq, unsigned long long seq) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(ctr);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(hctr);
+    for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
+                    unsigned long long seq) {
+    k_ctr_out<<<1, kBlock, 0, s>>>(ctr, hctr, hseq, seq);
+}
+
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words) {

@@ -85,7 +85,10 @@ struct dv_ctx {
     uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
-    Counters *h_ctr = nullptr;  // pinned host mirror
+    Counters *h_ctr = nullptr;  // host-mapped mirror (written by k_ctr_out) ...
+    Counters *d_hctr = nullptr;                 // ... its device address
+    unsigned long long *h_cseq = nullptr, *d_cseq = nullptr;  // its sequence word (after the mirror)
+    unsigned long long cseq = 0;                // the last sequence number asked for
     uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
     const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
@@ -325,10 +328,27 @@ float elapsed(dv_ctx *c, int a, int b) {
     return ms;
 }
 
+// the counters on the host once everything queued so far has run: the last
+// kernel writes them into host-mapped memory and bumps a sequence word the
+// host spins on (a blit plus a stream synchronisation cost ~25 us per epoch)
 int sync_counters(dv_ctx *c) {
-    HIPCHK(hipMemcpyAsync(c->h_ctr, c->ctr, sizeof(Counters), hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return DV_OK;
+    const unsigned long long want = ++c->cseq;
+    launch_ctr_out(c->stream, c->ctr, c->d_hctr, c->d_cseq, want);
+    HIPCHK(hipGetLastError());
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t i = 0;; i++) {
+        if (__atomic_load_n(c->h_cseq, __ATOMIC_ACQUIRE) >= want) return DV_OK;
+        if ((i & 1023) == 1023) {
+            const hipError_t q = hipStreamQuery(c->stream);
+            if (q == hipSuccess) {  // drained: the word must be there now
+                if (__atomic_load_n(c->h_cseq, __ATOMIC_ACQUIRE) >= want) return DV_OK;
+                return hip_fail(hipErrorUnknown, "counter mirror");
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, "stream");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) return DV_ERR_STATE;
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 }  // namespace
@@ -474,8 +494,18 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     }
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->el, A);
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->ew, A);
-    if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters)),
+    if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters) + 128,
+                                       hipHostMallocMapped | hipHostMallocCoherent),
                          "hipHostMalloc");
+    if (!r) r = hip_fail(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_hctr), c->h_ctr, 0),
+                         "hipHostGetDevicePointer");
+    if (!r) {
+        std::memset(c->h_ctr, 0, sizeof(Counters) + 128);
+        c->h_cseq = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->h_ctr) +
+                                                           ((sizeof(Counters) + 63) & ~size_t(63)));
+        c->d_cseq = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->d_hctr) +
+                                                           ((sizeof(Counters) + 63) & ~size_t(63)));
+    }
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_pub), sizeof(RoundPub),
                                    hipHostMallocMapped | hipHostMallocCoherent),
