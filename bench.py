@@ -493,6 +493,7 @@ class PartitionedBench:
         cap = max(int(max_txn_rank * R * 1.4), CONFIGS[a.config][1] * R) + 65536
         self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
                                  part_id=rank, timing=TIMING[a.timing])
+        self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
         if world > 1:
@@ -541,6 +542,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     a.gpus = world
     torch.cuda.set_device(local_rank)
+    # one stream for torch and the engine: the engine then needs no event
+    # wait on torch's stream before each epoch (CCEngine._after_torch)
+    if not os.environ.get("DVCC_BENCH_OWN_STREAM"):
+        torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         with stdout_to_stderr():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -565,6 +570,7 @@ def main():
         t_gen = time.perf_counter() - t_gen
         eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)
         deps = [dvcc.DeviceEpoch(e) for e in epochs]
         d_commit = torch.zeros(n_txn_total, dtype=torch.uint8, device="cuda")

@@ -183,6 +183,20 @@ __global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restri
     }
 }
 
+// epoch groups: row id | wr << 31 and the global txn id, 8 B per access
+__global__ __launch_bounds__(kBlock) void k_group_pack(const uint64_t *__restrict__ keys,
+                                                       const uint8_t *__restrict__ types,
+                                                       const uint32_t *__restrict__ txn, uint64_t n,
+                                                       uint32_t txn_base, uint32_t *__restrict__ k32,
+                                                       uint32_t *__restrict__ t32) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = keys[i];
+        // a key past 31 bits saturates and fails the decider's range check
+        k32[i] = ((k >> 31) ? 0x7FFFFFFFu : (uint32_t)k) | (types[i] == DV_WR ? 0x80000000u : 0u);
+        t32[i] = txn[i] + txn_base;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
                                                      const uint8_t *__restrict__ types,
                                                      const uint32_t *__restrict__ txn, uint64_t n,
@@ -400,19 +414,18 @@ __global__ __launch_bounds__(kBlock) void k_route_exec(const uint2 *__restrict__
     if (threadIdx.x == 0) {
         const unsigned long long d = part[0][0] + part[0][1] + part[0][2] + part[0][3];
         const unsigned long long w = part[1][0] + part[1][1] + part[1][2] + part[1][3];
-        if (d) atomicAdd(&acc[0], d);
-        if (w) atomicAdd(&acc[1], w);
+        // line-separated slots: one word takes ~88 device-scope adds per us
+        if (d) atomicAdd(&acc[2 * (blockIdx.x & (kSlots - 1))], d);
+        if (w) atomicAdd(&acc[2 * (blockIdx.x & (kSlots - 1)) + 1], w);
     }
 }
 
-// the send words of the outcome exchange: committed txns of this epoch << 32
-// | records for owner q
 // ---- host round trips without blits or stream synchronisation: small
 // host values reach the device as kernel arguments (k_put_words), device
 // values reach the host through a host-mapped mailbox written by one kernel
 // with system-scope stores and a sequence word the host spins on
 struct PutArgs {
-    uint64_t v64[kRadix];
+    uint64_t v64[kRadix + 8];
     uint32_t v32[8];
     uint32_t n64, n32;
     uint64_t *d64;
@@ -426,8 +439,9 @@ __global__ void k_put_words(PutArgs a) {
 struct CommMail {
     unsigned long long seq;
     unsigned long long pad[7];
-    unsigned long long w[4 * kRadix];
+    unsigned long long w[1];  // (allocated for mail_words(P) words)
 };
+__host__ __device__ inline uint64_t mail_words(uint32_t P) { return 4ull * kRadix + (uint64_t)P * (8 + P); }
 __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const uint32_t *__restrict__ b, uint32_t nb,
                            CommMail *m, unsigned long long seq) {
     for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) m->w[i] = a[i];
@@ -437,20 +451,18 @@ __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const ui
     if (threadIdx.x == 0) __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// the routed records this rank receives exceed its receive area: the group
-// fails on every rank (outcome vote word 0 = -DV_ERR_ARG at least)
-__global__ void k_route_recv_check(const uint64_t *__restrict__ words, uint32_t P, uint64_t cap,
-                                   uint32_t *__restrict__ vote) {
-    if (threadIdx.x != 0) return;
-    uint64_t n = 0;
-    for (uint32_t q = 0; q < P; q++) n += words[q] & 0xFFFFFFFFull;
-    if (n > cap && vote[0] < (uint32_t)(-DV_ERR_ARG)) vote[0] = (uint32_t)(-DV_ERR_ARG);
-}
-
+// this rank's outcome record, all-gathered (epoch groups, step 4): failure
+// code, committed txns, receive capacity, then records per owner
+constexpr uint32_t kGroupRecHead = 8;
 __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
-                              uint64_t *__restrict__ words, uint32_t *__restrict__ vote) {
-    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) words[q] = (committed << 32) | (fail ? 0u : tot[q]);
-    if (threadIdx.x == 0) vote[0] = fail;
+                              uint64_t cap, uint64_t *__restrict__ rec) {
+    for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) rec[kGroupRecHead + q] = fail ? 0u : tot[q];
+    if (threadIdx.x == 0) {
+        rec[0] = fail;
+        rec[1] = committed;
+        rec[2] = cap;
+        for (uint32_t k = 3; k < kGroupRecHead; k++) rec[k] = 0;
+    }
 }
 
 void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
@@ -505,7 +517,8 @@ struct DvComm {
     // epoch groups (run_group)
     uint32_t *rblk = nullptr, *rtot = nullptr;  // route counts: [P][kRouteBlocks], [P]
     uint8_t *gcommit = nullptr;                 // the commit bytes when the caller passes none
-    unsigned long long *xacc = nullptr;         // execution: read digest, writes
+    unsigned long long *xacc = nullptr;         // execution: read digest, writes ([2][kSlots])
+    uint64_t *gs = nullptr, *gr = nullptr;      // all-gathered vote / outcome records: [8 + P], [P][8 + P]
 };
 
 }  // namespace dvcc
@@ -716,7 +729,8 @@ void free_bufs(DvComm *m) {
     if (m->h_mail) (void)hipHostFree(m->h_mail);
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
-                 m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc};
+                 m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
+                 m->gs, m->gr};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -728,6 +742,7 @@ void free_bufs(DvComm *m) {
     m->rblk = m->rtot = nullptr;
     m->gcommit = nullptr;
     m->xacc = nullptr;
+    m->gs = m->gr = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -756,12 +771,15 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->rblk, (uint64_t)P * kRouteBlocks));
     CHK(alloc(&m->rtot, P));
     CHK(alloc(&m->gcommit, txn));
-    CHK(alloc(&m->xacc, 2));
-    CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), sizeof(CommMail),
+    CHK(alloc(&m->xacc, 2 * kSlots));
+    CHK(alloc(&m->gs, kGroupRecHead + P));
+    CHK(alloc(&m->gr, (uint64_t)P * (kGroupRecHead + P)));
+    const size_t mail_bytes = sizeof(CommMail) + 8 * mail_words(P);
+    CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), mail_bytes,
                                 hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
     CHK(hip_fail2(hipHostGetDevicePointer(reinterpret_cast<void **>(&m->d_mail), m->h_mail, 0),
                   "hipHostGetDevicePointer"));
-    std::memset(m->h_mail, 0, sizeof(CommMail));
+    std::memset(m->h_mail, 0, mail_bytes);
     m->acc_cap = acc;
     m->nb_cap = nb;
     m->txn_cap = txn;
@@ -900,7 +918,7 @@ int put_words(hipStream_t s, const uint64_t *v64, uint32_t n64, uint64_t *d64, c
     a.n32 = n32;
     a.d64 = d64;
     a.d32 = d32;
-    for (uint32_t i = 0; i < n64 && i < (uint32_t)kRadix; i++) a.v64[i] = v64[i];
+    for (uint32_t i = 0; i < n64 && i < (uint32_t)kRadix + 8; i++) a.v64[i] = v64[i];
     for (uint32_t i = 0; i < n32 && i < 8u; i++) a.v32[i] = v32[i];
     k_put_words<<<1, kBlock, 0, s>>>(a);
     return hip_fail2(hipGetLastError(), "k_put_words");
@@ -1095,9 +1113,9 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
 // of epoch e of the group.  Collectives, in the same order on every rank:
 //   1. all-to-all of the batch sizes (rank e learns the parts of epoch e) and
 //      the argument vote (all-reduce MAX);
-//   2. three all-to-allv (grouped) move every batch to its epoch's decider as
-//      9 B per access -- row id, global txn id, type -- landing contiguous in
-//      origin order, Calvin's sequence (work_queue.cpp:105-151);
+//   2. two all-to-allv (grouped) move every batch to its epoch's decider as
+//      8 B per access -- row id with the write bit, global txn id -- landing
+//      contiguous in origin order, Calvin's sequence (work_queue.cpp:105-151);
 //   3. rank e decides epoch e with the replicated single-GPU path (prefix
 //      kill, asynchronous rounds; its one all-reduce of the input-error bits
 //      after the probe fails the group on every rank), routing the committed
@@ -1129,67 +1147,72 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     hipStream_t s = ctx_stream(c);
     const uint64_t acap = m->acc_cap;
 
-    // 1. sizes and the argument vote: longest txn, bad arguments / capacity,
-    //    -, a rank whose table is not a dense YCSB map (then nobody runs), and
-    //    the widest and (complemented) narrowest table: a key's range check on
-    //    its decider is its owner's only if every partition has the same rows
+    // 1. one all-gather of every rank's vote record -- longest txn, bad
+    //    arguments, "not a dense YCSB map" (then nobody runs), table rows
+    //    (all equal, so a key's range check on its decider is its owner's
+    //    check), receive capacity, then its batch size per epoch -- from which
+    //    every rank derives the same decision and its receive sizes
     const bool capable = ctx_group_capable(c, P);
     uint64_t *f0 = nullptr;
     const uint64_t *pkey = nullptr;
-    const uint32_t nb = capable ? (uint32_t)ctx_table0_rows(c) : 0u;
-    const uint32_t vote[6] = {max_len, bad ? kVoteBadArg : 0u, 0u, capable ? 0u : kRepBlockOff, nb, ~nb};
-    std::vector<uint64_t> sendc(P, 0), recvc(P);
-    for (uint32_t e = 0; e < P && !bad; e++) sendc[e] = homes[e].n_acc;
-    CHK(put_words(s, sendc.data(), P, m->xcnt, vote, 6, m->xvote));
-    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, std::min<uint64_t>(cfg.max_acc, acap), m->xvote);
-    CHK(hip_fail2(hipGetLastError(), "k_recv_check"));
-    CHK(m->x->max_u32(m->xvote, 6, s));
-    uint32_t gvote[6] = {0, 0, 0, 0, 0, 0};
-    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 6, recvc.data(), gvote));
-    if (gvote[1] || gvote[3] || gvote[4] != ~gvote[5]) return DV_ERR_ARG;  // every rank
-    const uint32_t glen = std::min<uint32_t>(gvote[0] ? gvote[0] : 1u, kMaxPos);
+    const uint32_t W = kGroupRecHead + P;
+    std::vector<uint64_t> rec(W, 0), all((size_t)P * W), sendc(P, 0), recvc(P);
+    rec[0] = max_len;
+    rec[1] = bad ? 1u : 0u;
+    rec[2] = capable ? 0u : 1u;
+    rec[3] = capable ? ctx_table0_rows(c) : 0u;
+    rec[4] = std::min<uint64_t>(cfg.max_acc, acap);
+    for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
+    CHK(put_words(s, rec.data(), W, m->gs, nullptr, 0, nullptr));
+    CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
+    CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
+    uint64_t gmax = 0;
+    bool refuse = false;
+    for (uint32_t q = 0; q < P; q++) {
+        const uint64_t *r = &all[(size_t)q * W];
+        gmax = std::max<uint64_t>(gmax, r[0]);
+        refuse |= r[1] || r[2] || r[3] != all[3];
+        uint64_t in = 0;  // what rank q receives: its epoch's batches
+        for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
+        refuse |= in > r[4];
+        recvc[q] = r[kGroupRecHead + m->rank];
+    }
+    if (refuse) return DV_ERR_ARG;  // every rank
+    const uint32_t glen = (uint32_t)std::min<uint64_t>(gmax ? gmax : 1u, kMaxPos);
 
-    // 2. every batch to its decider: [row ids 4 B | txn ids 4 B | types 1 B]
+    // 2. every batch to its decider: [row id | wr << 31, 4 B | txn id, 4 B]
     uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
     uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *stx = reinterpret_cast<uint32_t *>(sb + 4 * acap);
-    uint8_t *sy = sb + 8 * acap;
     uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * acap);
-    uint8_t *ry = rb + 8 * acap;
-    std::vector<size_t> sc(P), sd(P), rc(P), rd(P), sc4(P), sd4(P), rc4(P), rd4(P);
+    std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
     uint64_t so = 0, ro = 0;
     for (uint32_t e = 0; e < P; e++) {
         const uint64_t n = sendc[e];
         if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
-            k_rep_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                 (uint32_t)m->rank * txns_per_rank, sk + so, stx + so, sy + so);
+            k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                   (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
         }
-        sc[e] = n;
-        sd[e] = so;
-        sc4[e] = 4 * n;
-        sd4[e] = 4 * so;
+        sc[e] = 4 * n;
+        sd[e] = 4 * so;
         so += n;
-        rc[e] = recvc[e];
-        rd[e] = ro;
-        rc4[e] = 4 * recvc[e];
-        rd4[e] = 4 * ro;
+        rc[e] = 4 * recvc[e];
+        rd[e] = 4 * ro;
         ro += recvc[e];
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
-    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc4.data(), sd4.data(),
-                          reinterpret_cast<uint8_t *>(rk), rc4.data(), rd4.data(), s));
-    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc4.data(), sd4.data(),
-                          reinterpret_cast<uint8_t *>(rt), rc4.data(), rd4.data(), s));
-    CHK(m->x->all_to_allv(sy, sc.data(), sd.data(), ry, rc.data(), rd.data(), s));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
+                          reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
+    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
+                          reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
     CHK(m->x->group(false));
 
     // 3. decide this rank's epoch; its committed accesses are routed into the
     //    send area (free again once the batches have left)
     dv_epoch_dev ep{};
-    ep.keys = reinterpret_cast<const uint64_t *>(rk);  // (read as 32-bit row ids)
-    ep.types = ry;
+    ep.keys = reinterpret_cast<const uint64_t *>(rk);  // (read as 32-bit row ids with the write bit)
+    ep.types = nullptr;
     ep.acc_txn = rt;
     ep.tables = nullptr;
     ep.n_acc = ro;
@@ -1199,28 +1222,32 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     dv_stats est{};
     const int rd_ = epoch_run_replicated(c, &ep, rk, P, m->verdict, &est, &rout);
 
-    // 4. the outcome vote (a failure on any rank fails the group on every
-    //    rank) and {committed, records per owner}
+    // 4. one all-gather of every rank's outcome record: a failure on any rank
+    //    (or an owner whose receive area is too small) fails the group on
+    //    every rank; committed txns; records per owner
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, m->xcnt, m->xvote);
+    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs);
     CHK(hip_fail2(hipGetLastError(), "k_route_words"));
-    std::vector<uint64_t> words(2 * P);
-    CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    k_route_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, 2 * acap, m->xvote);
-    CHK(hip_fail2(hipGetLastError(), "k_route_recv_check"));
-    CHK(m->x->max_u32(m->xvote, 1, s));
-    uint32_t gfail = 0;
-    CHK(mail_get(m, s, m->xcnt, 2 * P, m->xvote, 1, words.data(), &gfail));
+    CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
+    CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
+    uint64_t gfail = 0, committed = 0;
+    for (uint32_t q = 0; q < P; q++) {
+        const uint64_t *r = &all[(size_t)q * W];
+        gfail = std::max<uint64_t>(gfail, r[0]);
+        committed += r[1];
+        uint64_t in = 0;
+        for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
+        if (in > r[2]) gfail = std::max<uint64_t>(gfail, (uint64_t)(-DV_ERR_ARG));
+    }
     if (gfail) return -(int)gfail;
 
     // 5. records to their owners, commit bytes back to their origins
-    uint64_t committed = 0;
     std::vector<uint64_t> rcnt(P);
     so = ro = 0;
     std::vector<size_t> tc(P), td(P), uc(P), ud(P);
     for (uint32_t q = 0; q < P; q++) {
-        const uint64_t out = words[q] & 0xFFFFFFFFull, in = words[P + q] & 0xFFFFFFFFull;
-        committed += words[P + q] >> 32;
+        const uint64_t out = all[(size_t)m->rank * W + kGroupRecHead + q];
+        const uint64_t in = all[(size_t)q * W + kGroupRecHead + m->rank];
         rcnt[q] = in;
         sc[q] = 8 * out;
         sd[q] = 8 * so;
@@ -1243,7 +1270,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    has one committed txn, reads and writes in one launch; OCC / CALVIN:
     //    reads first)
     ctx_table0_cols(c, &f0, &pkey);
-    CHK(hip_fail2(hipMemsetAsync(m->xacc, 0, 2 * sizeof(unsigned long long), s), "memset"));
+    CHK(hip_fail2(hipMemsetAsync(m->xacc, 0, 2 * kSlots * sizeof(unsigned long long), s), "memset"));
     const bool fused = cfg.cc_alg == DV_NO_WAIT || cfg.cc_alg == DV_WAIT_DIE;
     const uint2 *recs = reinterpret_cast<const uint2 *>(m->recv);
     uint64_t off = 0;
@@ -1261,8 +1288,12 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         off += n;
     }
     CHK(hip_fail2(hipGetLastError(), "k_route_exec"));
-    uint64_t acc[2] = {0, 0};
-    CHK(mail_get(m, s, reinterpret_cast<const uint64_t *>(m->xacc), 2, nullptr, 0, acc, nullptr));
+    uint64_t slots[2 * kSlots], acc[2] = {0, 0};
+    CHK(mail_get(m, s, reinterpret_cast<const uint64_t *>(m->xacc), 2 * kSlots, nullptr, 0, slots, nullptr));
+    for (int k = 0; k < kSlots; k++) {
+        acc[0] += slots[2 * k];
+        acc[1] += slots[2 * k + 1];
+    }
     if (st) {
         *st = est;  // this rank's decision: rounds, sort passes, timings
         st->n_txn = n_txn64 * P;

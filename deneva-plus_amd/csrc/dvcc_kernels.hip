@@ -136,13 +136,20 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                     const ulonglong2 k1 = *reinterpret_cast<const ulonglong2 *>(keys + i0 + q + 2);
                     key[q] = k0.x; key[q + 1] = k0.y; key[q + 2] = k1.x; key[q + 3] = k1.y;
                 }
-                const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0 + q);
                 const uint32_t tt = tables ? *reinterpret_cast<const uint32_t *>(tables + i0 + q) : 0u;
+                if (types) {
+                    const uint32_t ty = *reinterpret_cast<const uint32_t *>(types + i0 + q);
 #pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    wr[q + j] = ((ty >> (8 * j)) & 0xFFu) == DV_WR ? 1u : 0u;
-                    tb[q + j] = (tt >> (8 * j)) & 0xFFu;
+                    for (int j = 0; j < 4; j++) wr[q + j] = ((ty >> (8 * j)) & 0xFFu) == DV_WR ? 1u : 0u;
+                } else {  // epoch groups: row id | wr << 31 (keys32 only)
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        wr[q + j] = (uint32_t)(key[q + j] >> 31);
+                        key[q + j] &= 0x7FFFFFFFull;
+                    }
                 }
+#pragma unroll
+                for (int j = 0; j < 4; j++) tb[q + j] = (tt >> (8 * j)) & 0xFFu;
             }
         } else {
 #pragma unroll
@@ -150,7 +157,8 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 const bool ok = i0 + j < n;
                 txn[j] = ok ? acc_txn[i0 + j] : 0xFFFFFFFFu;
                 key[j] = ok ? (keys32 ? (uint64_t)keys32[i0 + j] : keys[i0 + j]) : 0ull;
-                wr[j] = ok && types[i0 + j] == DV_WR ? 1u : 0u;
+                wr[j] = ok && (types ? types[i0 + j] == DV_WR : (key[j] >> 31) != 0) ? 1u : 0u;
+                if (!types) key[j] &= 0x7FFFFFFFull;
                 tb[j] = ok && tables ? tables[i0 + j] : 0u;
             }
         }

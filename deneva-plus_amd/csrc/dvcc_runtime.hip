@@ -859,7 +859,8 @@ namespace {
 // the per-epoch host state
 int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
-    if (ep->n_acc && (!ep->keys || !ep->types || !ep->acc_txn)) return DV_ERR_ARG;
+    // (epoch groups: no types -- the write bit rides in the 32-bit row ids)
+    if (ep->n_acc && (!ep->keys || (!ep->types && !c->keys32) || !ep->acc_txn)) return DV_ERR_ARG;
     bool any = false;
     for (auto &t : c->tab) any |= t.loaded;
     if (!any) return DV_ERR_NO_TABLE;
@@ -919,7 +920,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
-    if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
+    if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
+        // them (epoch groups vote on every decider's outcome before anything executes)
         const int re = comm_combine_errors(c);
         if (re) return re;
     }
@@ -1491,7 +1493,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
-    if (c->rep_P) {  // replicated epoch: owners' key checks combined before anything depends on them
+    if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
+        // them (epoch groups vote on every decider's outcome before anything executes)
         r = comm_combine_errors(c);
         if (r) return r;
     }
