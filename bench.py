@@ -533,6 +533,51 @@ class PartitionedBench:
         return step
 
 
+def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
+    """N>1 extras beside the headline: strong scaling (one epoch per step),
+    weak scaling (1,048,576 txns per GPU, list protocol) and the MPR sweep."""
+    nxt = 10_000
+    if group:
+        # strong scaling: one 1,048,576-txn epoch per step (dv_epoch_run_part)
+        sdeps = pb.epochs(n_txn_rank, mpr, theta, 2)
+        sst, sel = timed(pb.stepper(sdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+        scm = sum(s.committed for s in sst)
+        out["strong_scaling"] = {"txns_per_epoch": n_txn_total, "committed_per_s": scm / sel,
+                                 "ms_per_epoch": sel / len(sst) * 1e3, "epochs": len(sst),
+                                 "protocol": "dv_epoch_run_part, mode %d" % a.part_mode}
+        del sdeps
+        nxt += 100
+    if not a.no_weak:
+        # weak scaling: 1,048,576 txns per GPU per epoch (list protocol)
+        wdeps = pb.epochs(n_txn_total, mpr, theta, 2)
+        wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, 1, min(a.steps, 5), world)
+        wc = sum(s.committed for s in wst)
+        out["weak_scaling"] = {"txns_per_epoch_per_gpu": n_txn_total, "txns_per_epoch": n_txn_total * world,
+                               "committed_per_s": wc / wel, "decided_txns_per_s": len(wst) * n_txn_total * world / wel,
+                               "ms_per_epoch": wel / len(wst) * 1e3,
+                               "abort_rate": 1 - wc / (len(wst) * n_txn_total * world), "epochs": len(wst),
+                               "mpr": mpr}
+        del wdeps
+        nxt += 100
+    sweep = []
+    for m in [float(x) for x in a.mpr_sweep.split(",") if x.strip()]:
+        if group:
+            mg = pb.groups(n_txn_rank, m, theta, 1)
+            mst, mel = timed(pb.group_stepper(mg, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            mtx = len(mst) * n_txn_total * world
+        else:
+            mdeps = pb.epochs(n_txn_rank, m, theta, 2)
+            mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            mtx = len(mst) * n_txn_total
+        mc = sum(s.committed for s in mst)
+        sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_step": mel / len(mst) * 1e3,
+                      "abort_rate": 1 - mc / mtx,
+                      "rounds_mean": float(np.mean([s.rounds for s in mst]))})
+        nxt += 100
+    if sweep:
+        out["mpr_sweep"] = sweep
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -635,46 +680,10 @@ def main():
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
         out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, min(a.steps, 10), d_commit)
     else:
-        nxt = 10_000
-        if group:
-            # strong scaling: one 1,048,576-txn epoch per step (dv_epoch_run_part)
-            sdeps = pb.epochs(n_txn_rank, mpr, theta, 2)
-            sst, sel = timed(pb.stepper(sdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
-            scm = sum(s.committed for s in sst)
-            out["strong_scaling"] = {"txns_per_epoch": n_txn_total, "committed_per_s": scm / sel,
-                                     "ms_per_epoch": sel / len(sst) * 1e3, "epochs": len(sst),
-                                     "protocol": "dv_epoch_run_part, mode %d" % a.part_mode}
-            del sdeps
-            nxt += 100
-        if not a.no_weak:
-            # weak scaling: 1,048,576 txns per GPU per epoch (list protocol)
-            wdeps = pb.epochs(n_txn_total, mpr, theta, 2)
-            wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, 1, min(a.steps, 5), world)
-            wc = sum(s.committed for s in wst)
-            out["weak_scaling"] = {"txns_per_epoch_per_gpu": n_txn_total, "txns_per_epoch": n_txn_total * world,
-                                   "committed_per_s": wc / wel, "decided_txns_per_s": len(wst) * n_txn_total * world / wel,
-                                   "ms_per_epoch": wel / len(wst) * 1e3,
-                                   "abort_rate": 1 - wc / (len(wst) * n_txn_total * world), "epochs": len(wst),
-                                   "mpr": mpr}
-            del wdeps
-            nxt += 100
-        sweep = []
-        for m in [float(x) for x in a.mpr_sweep.split(",") if x.strip()]:
-            if group:
-                mg = pb.groups(n_txn_rank, m, theta, 1)
-                mst, mel = timed(pb.group_stepper(mg, n_txn_rank), nxt, 1, min(a.steps, 5), world)
-                mtx = len(mst) * n_txn_total * world
-            else:
-                mdeps = pb.epochs(n_txn_rank, m, theta, 2)
-                mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
-                mtx = len(mst) * n_txn_total
-            mc = sum(s.committed for s in mst)
-            sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_step": mel / len(mst) * 1e3,
-                          "abort_rate": 1 - mc / mtx,
-                          "rounds_mean": float(np.mean([s.rounds for s in mst]))})
-            nxt += 100
-        if sweep:
-            out["mpr_sweep"] = sweep
+        try:
+            extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group)
+        except Exception as ex:  # noqa: BLE001 -- the headline above is already measured
+            out["extra_legs_error"] = repr(ex)
     if not part and rank == 0 and not a.no_cpu_baseline:
         # the single-thread E-schedule port (decision-identical) and, for
         # NO_WAIT, the multi-threaded engine, which is then the baseline

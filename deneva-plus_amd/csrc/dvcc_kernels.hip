@@ -173,11 +173,11 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                     probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr, &miss);
             }
         }
-        // run starts and their max-scan
+        // run starts and their max-scan (32-bit: an epoch holds < kMaxAcc accesses)
         uint32_t prev = __shfl_up(txn[kPV - 1], 1, 64);
         if (lane == 0) prev = wave0 > 0 && wave0 - 1 < n ? acc_txn[wave0 - 1] : 0xFFFFFFFEu;
-        uint64_t st[kPV];
-        uint64_t mx = 0;
+        uint32_t st[kPV];
+        uint32_t mx = 0;
         bool bad = false;
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
@@ -185,20 +185,21 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             const bool valid = i0 + j < n;
             const bool start = valid && (i0 + j == 0 || pt != txn[j]);
             if (valid && (txn[j] >= n_txn || (i0 + j > 0 && pt > txn[j] && pt != 0xFFFFFFFEu))) bad = true;
-            mx = start ? i0 + j + 1 : mx;  // +1: 0 means "no start yet"
+            mx = start ? (uint32_t)(i0 + j + 1) : mx;  // +1: 0 means "no start yet"
             st[j] = mx;
         }
-        uint64_t inc = mx;
+        uint32_t inc = mx;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            const uint64_t o = __shfl_up(inc, off, 64);
+            const uint32_t o = __shfl_up(inc, off, 64);
             if (lane >= (uint32_t)off && o > inc) inc = o;
         }
-        uint64_t ex = __shfl_up(inc, 1, 64);
+        uint32_t ex = __shfl_up(inc, 1, 64);
         if (lane == 0) ex = 0;
         // the wave's first run may have begun before the wave: its start, found
         // 64 earlier accesses per step by the whole wave (one load, a ballot)
-        uint64_t carry = 0;
+        uint32_t carry = 0;
+#ifndef DVCC_EXP_NO_LOOKBACK
         if (wave0 > 0 && wave0 < n) {  // (wave-uniform)
             const uint32_t t0 = __shfl(txn[0], 0, 64);
             for (uint64_t base = wave0;; base -= 64) {
@@ -206,11 +207,12 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 const uint64_t m = __ballot(!same);
                 if (m) {
                     const uint32_t f = (uint32_t)__ffsll((unsigned long long)m) - 1;  // accesses [base - f, base) continue the run
-                    carry = base - f == wave0 ? 0 : base - f + 1;
+                    carry = base - f == wave0 ? 0u : (uint32_t)(base - f + 1);
                     break;
                 }
             }
         }
+#endif
         if (ex == 0) ex = carry;
         const uint32_t nxt_lane = __shfl_down(txn[0], 1, 64);
         const uint64_t in_last = i0 + kPV;
@@ -224,8 +226,8 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             const uint64_t i = i0 + j;
             out[j] = 0;
             if (i >= n) continue;
-            const uint64_t start = (st[j] ? st[j] : ex) - 1;
-            const uint32_t pos = (uint32_t)(i - start);
+            const uint32_t start = (st[j] ? st[j] : ex) - 1u;
+            const uint32_t pos = (uint32_t)i - start;
             // a txn longer than the epoch's declared bound (1 << slog verdict
             // bytes per txn): an input error; positions and lengths are clamped
             // so every later index stays inside its txn's slot (the epoch is
@@ -234,6 +236,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             if (big) set_err(ctr, ERRB_BIG);
             const uint32_t t = txn[j] < n_txn ? txn[j] : 0u;
             out[j] = pair_pack(row[j], t, big ? 0u : pos, wr[j]);
+#ifndef DVCC_EXP_NO_TB  // (measurement builds only: tools/exp_variant.sh)
             if (txn[j] < n_txn) {
                 if (pos == 0) tb_start[t] = (uint32_t)i;
                 const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
@@ -242,6 +245,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                     if (tlen) tlen[t] = (uint8_t)(big ? (1u << slog) : pos + 1);
                 }
             }
+#endif
         }
         if (acc_row) {
             uint32_t ar[kPV];
