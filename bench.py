@@ -71,6 +71,8 @@ def parse():
     ap.add_argument("--protocol", choices=["group", "part"], default="group",
                     help="N>1 headline: epoch groups (dv_epoch_group_run) or one epoch per step "
                          "(dv_epoch_run_part, --part-mode)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N=1: one dv_epoch_run_device call per step instead of the pipelined batch call")
     ap.add_argument("--part1", action="store_true",
                     help="N=1 through the partitioned drivers on a one-rank RCCL communicator (their overhead)")
     ap.add_argument("--part-mode", type=int, default=0,
@@ -349,16 +351,22 @@ def launch_ranks(a):
     return subprocess.call(cmd)
 
 
-def timed(step, first, warmup, steps, world):
+def timed(step, first, warmup, steps, world, batch=None):
     """W untimed steps, then exactly K steps between barrier + synchronize
-    on both sides; the slowest rank's time."""
-    for i in range(warmup):
+    on both sides; the slowest rank's time.  batch(first, count): the steps
+    as one pipelined call (dv_epoch_run_device_batch), one epoch per step."""
+    if batch is not None and warmup:
+        batch(first, warmup)
+    for i in range(warmup if batch is None else 0):
         step(first + i)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    stats = [step(first + warmup + i) for i in range(steps)]
+    if batch is not None:
+        stats = batch(first + warmup, steps)
+    else:
+        stats = [step(first + warmup + i) for i in range(steps)]
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -622,6 +630,9 @@ def main():
 
         def step(i):
             return eng.run_epoch_device(deps[i % n_epochs], d_commit)
+
+        def batch(first, count):  # the product's pipelined entry point: epoch k+1 queued before k is read
+            return eng.run_epochs_device([deps[(first + i) % n_epochs] for i in range(count)], d_commit)
     else:
         weak = not a.no_weak
         pb = PartitionedBench(a, cc_name, rows, world, rank, local_rank,
@@ -635,7 +646,7 @@ def main():
             step = pb.stepper(deps, n_txn_rank)
         t_gen = time.perf_counter() - t_gen
 
-    stats, el = timed(step, 0, a.warmup, a.steps, world)
+    stats, el = timed(step, 0, a.warmup, a.steps, world, None if (part or a.no_pipeline) else batch)
     kstats, sstats = measure_legs(a, eng, step, a.warmup + a.steps, stats)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"

@@ -716,14 +716,21 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         uint8_t *__restrict__ tlen,
                                                         uint32_t *__restrict__ tile_ctr,
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
-                                                        uint4 *__restrict__ zero, uint64_t zero_n) {
+                                                        uint4 *__restrict__ zero, uint64_t zero_n, int gate) {
     if (blockIdx.x == 0) {
+        // gate (pipelined epochs, dv_epoch_run_device_batch): the previous
+        // epoch is still unread by the host; if it halted or failed, this one
+        // starts halted, so nothing of it reaches the tables or the commit bytes
+        __shared__ uint32_t s_gate;
+        if (threadIdx.x == 0) s_gate = gate && (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
+        __syncthreads();
         uint32_t *w = reinterpret_cast<uint32_t *>(ctr);
         for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) w[i] = 0;
         for (uint32_t i = threadIdx.x; i < kTileCtrs; i += kBlock) tile_ctr[i] = 0;
         __syncthreads();
         // errors found before the epoch began (the host-record check)
         if (threadIdx.x == 0 && err_seed) ctr->err = *err_seed;
+        if (threadIdx.x == 0 && s_gate) ctr->halt = 1u;
     }
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
@@ -755,12 +762,13 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words) {
+                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
-                                       err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0);
+                                       err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
+                                       gate ? 1 : 0);
 }
 
 // ---------------------------------------------------------------- execute

@@ -85,10 +85,14 @@ struct dv_ctx {
     uint32_t ticket = 0;                             // next tile_ctr slot
     uint8_t *status = nullptr, *verdict = nullptr;
     Counters *ctr = nullptr;    // device
-    Counters *h_ctr = nullptr;  // host-mapped mirror (written by k_ctr_out) ...
+    Counters *h_ctr = nullptr;  // host-mapped mirror (written by k_ctr_out) = h_mir[0] ...
     Counters *d_hctr = nullptr;                 // ... its device address
     unsigned long long *h_cseq = nullptr, *d_cseq = nullptr;  // its sequence word (after the mirror)
     unsigned long long cseq = 0;                // the last sequence number asked for
+    // two mirror slots: pipelined epochs (dv_epoch_run_device_batch) alternate
+    Counters *h_mir[2] = {nullptr, nullptr}, *d_mir[2] = {nullptr, nullptr};
+    unsigned long long *h_mseq[2] = {nullptr, nullptr}, *d_mseq[2] = {nullptr, nullptr};
+    bool clear_gate = false;                    // the next epoch clear is gated on the previous epoch
     uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
     const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
@@ -331,17 +335,22 @@ float elapsed(dv_ctx *c, int a, int b) {
 // the counters on the host once everything queued so far has run: the last
 // kernel writes them into host-mapped memory and bumps a sequence word the
 // host spins on (a blit plus a stream synchronisation cost ~25 us per epoch)
-int sync_counters(dv_ctx *c) {
+// the counters into mirror slot k behind everything queued so far; returns
+// the sequence number mirror_wait waits for
+unsigned long long mirror_out(dv_ctx *c, int k) {
     const unsigned long long want = ++c->cseq;
-    launch_ctr_out(c->stream, c->ctr, c->d_hctr, c->d_cseq, want);
-    HIPCHK(hipGetLastError());
+    launch_ctr_out(c->stream, c->ctr, c->d_mir[k], c->d_mseq[k], want);
+    return want;
+}
+
+int mirror_wait(dv_ctx *c, int k, unsigned long long want) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 0;; i++) {
-        if (__atomic_load_n(c->h_cseq, __ATOMIC_ACQUIRE) >= want) return DV_OK;
+        if (__atomic_load_n(c->h_mseq[k], __ATOMIC_ACQUIRE) >= want) return DV_OK;
         if ((i & 1023) == 1023) {
             const hipError_t q = hipStreamQuery(c->stream);
             if (q == hipSuccess) {  // drained: the word must be there now
-                if (__atomic_load_n(c->h_cseq, __ATOMIC_ACQUIRE) >= want) return DV_OK;
+                if (__atomic_load_n(c->h_mseq[k], __ATOMIC_ACQUIRE) >= want) return DV_OK;
                 return hip_fail(hipErrorUnknown, "counter mirror");
             }
             if (q != hipErrorNotReady) return hip_fail(q, "stream");
@@ -349,6 +358,12 @@ int sync_counters(dv_ctx *c) {
         }
         __builtin_ia32_pause();
     }
+}
+
+int sync_counters(dv_ctx *c) {
+    const unsigned long long want = mirror_out(c, 0);
+    HIPCHK(hipGetLastError());
+    return mirror_wait(c, 0, want);
 }
 
 }  // namespace
@@ -494,17 +509,25 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     }
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->el, A);
     if (!r && cfg->cc_alg == DV_CALVIN) r = dalloc(&c->ew, A);
-    if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), sizeof(Counters) + 128,
+    constexpr size_t kMirBytes = ((sizeof(Counters) + 63) & ~size_t(63)) + 128;  // a mirror slot + its word
+    if (!r) r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_ctr), 2 * kMirBytes,
                                        hipHostMallocMapped | hipHostMallocCoherent),
                          "hipHostMalloc");
     if (!r) r = hip_fail(hipHostGetDevicePointer(reinterpret_cast<void **>(&c->d_hctr), c->h_ctr, 0),
                          "hipHostGetDevicePointer");
     if (!r) {
-        std::memset(c->h_ctr, 0, sizeof(Counters) + 128);
-        c->h_cseq = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->h_ctr) +
-                                                           ((sizeof(Counters) + 63) & ~size_t(63)));
-        c->d_cseq = reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(c->d_hctr) +
-                                                           ((sizeof(Counters) + 63) & ~size_t(63)));
+        std::memset(c->h_ctr, 0, 2 * kMirBytes);
+        const size_t off = (sizeof(Counters) + 63) & ~size_t(63);
+        for (int k = 0; k < 2; k++) {
+            char *h = reinterpret_cast<char *>(c->h_ctr) + k * kMirBytes;
+            char *d = reinterpret_cast<char *>(c->d_hctr) + k * kMirBytes;
+            c->h_mir[k] = reinterpret_cast<Counters *>(h);
+            c->d_mir[k] = reinterpret_cast<Counters *>(d);
+            c->h_mseq[k] = reinterpret_cast<unsigned long long *>(h + off);
+            c->d_mseq[k] = reinterpret_cast<unsigned long long *>(d + off);
+        }
+        c->h_cseq = c->h_mseq[0];
+        c->d_cseq = c->d_mseq[0];
     }
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = hip_fail(hipHostMalloc(reinterpret_cast<void **>(&c->h_pub), sizeof(RoundPub),
@@ -1488,7 +1511,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->prefix_mode = true;
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
-                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words);
+                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
@@ -1551,6 +1574,174 @@ int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, ui
         if (r) { c->phase = 0; return r; }
     }
     return dv_epoch_finish(c, d_commit, st);
+}
+
+
+}  // extern "C"
+
+namespace {
+
+// What a pipelined epoch's statistics need of the host state it was queued
+// with (the next epoch's queueing overwrites the context's copy).
+struct EpochSnap {
+    uint64_t n_acc = 0;
+    uint32_t n_txn = 0, rounds = 0, rounds_real = 0, rounds_prefix = 0, async_launched = 0, sort_passes = 0;
+    bool async_unconfirmed = false;
+    unsigned long long seq = 0;
+    int slot = 0;
+};
+
+// a prefix-kill epoch queued through its execution, commit bytes and counter
+// mirror (slot), with no host wait; gate: the epoch before it is still unread
+int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate, int slot, EpochSnap &sn) {
+    c->clear_gate = gate;
+    int r = run_prefix_epoch(c, ep);
+    c->clear_gate = false;
+    if (r) return r;
+    enqueue_exec(c, d_commit);
+    r = hip_fail(hipGetLastError(), "execution launch");
+    sn.n_acc = c->n_acc;
+    sn.n_txn = c->n_txn;
+    sn.rounds = c->rounds;
+    sn.rounds_real = c->rounds_real;
+    sn.rounds_prefix = c->rounds_prefix;
+    sn.async_launched = c->async_launched;
+    sn.sort_passes = c->sort_passes;
+    sn.async_unconfirmed = c->async_unconfirmed;
+    sn.slot = slot;
+    sn.seq = mirror_out(c, slot);
+    c->phase = 0;
+    c->prefix_mode = false;
+    if (!r) r = hip_fail(hipGetLastError(), "counter mirror");
+    return r;
+}
+
+// wait for a pipelined epoch's counters; *halted: its rounds halted (or the
+// epoch before it did), nothing of it executed -- the caller runs it again
+int pipe_complete(dv_ctx *c, const EpochSnap &sn, dv_stats *st, bool *halted) {
+    *halted = false;
+    int r = mirror_wait(c, sn.slot, sn.seq);
+    if (r) return r;
+    const Counters *hc = c->h_mir[sn.slot];
+    r = err_from_bits(hc->err | hc->peer_err);
+    if (r) return r;
+    if (hc->halt || hc->a_halt) {
+        *halted = true;
+        return DV_OK;
+    }
+    uint32_t rounds_real = sn.rounds_real;
+    if (hc->async_r0) {
+        uint32_t left = 0;
+        for (const CtrSlot &sl : hc->slot) left += sl.undecided;
+        if (left) return DV_ERR_STATE;
+        rounds_real = hc->async_r0 + hc->async_iters;
+    } else if (sn.async_unconfirmed) {
+        if (hc->async_go == 2u) return DV_ERR_STATE;
+        uint32_t r_end = 0;
+        for (uint32_t k = 0; k < std::min(sn.rounds, (uint32_t)kRoundLog); k++)
+            if (hc->log_und[k]) r_end = k + 1;
+        rounds_real = std::max(r_end, 1u);
+    }
+    c->async_hint = hc->async_r0;
+    if (st) {
+        std::memset(st, 0, sizeof(*st));
+        st->n_txn = sn.n_txn;
+        st->n_acc = sn.n_acc;
+        uint64_t committed = 0, wcnt = 0, dig = 0;
+        for (const CtrSlot &sl : hc->slot) {
+            committed += sl.committed;
+            wcnt += sl.write_cnt;
+            dig += sl.read_digest;
+        }
+        st->committed = committed;
+        st->aborted = sn.n_txn - committed;
+        st->write_cnt = wcnt;
+        st->read_digest = dig;
+        st->rounds = (rounds_real ? rounds_real : sn.rounds) + (sn.rounds_prefix ? sn.rounds_prefix : hc->a_rounds);
+        st->sort_passes = sn.sort_passes;
+        st->async_launches = (uint16_t)std::min(sn.async_launched, 0xFFFFu);
+        st->async_declined = (uint16_t)std::min(hc->async_declined, 0xFFFFu);
+        st->async_yields = hc->async_yields;
+    }
+    return DV_OK;
+}
+
+// after a halted pipelined epoch: the stream drained, halts cleared, then the
+// epochs run again one at a time (decisions depend only on an epoch's own
+// accesses, and neither touched the tables)
+int pipe_redo(dv_ctx *c) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemsetAsync(&c->ctr->halt, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(hipMemsetAsync(&c->ctr->a_halt, 0, sizeof(uint32_t), c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return DV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
+                              dv_stats *sts) {
+    if (!c || (n && !eps)) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    EpochSnap snap[2];
+    int64_t pend = -1;  // the epoch queued but not yet read back
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
+    // the pending epoch: read back; if it halted, it runs again, and so does
+    // `next` (queued behind it, gated) when given
+    auto settle = [&](int64_t next) -> int {
+        bool halted = false;
+        int r = pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
+        if (r) {
+            (void)hipStreamSynchronize(c->stream);
+            return r;
+        }
+        if (!halted) return DV_OK;
+        r = pipe_redo(c);
+        if (!r) r = dv_epoch_run_device(c, &eps[pend], commit_of((uint32_t)pend), nullptr, stats_of((uint32_t)pend));
+        if (!r && next >= 0) r = dv_epoch_run_device(c, &eps[next], commit_of((uint32_t)next), nullptr,
+                                                     stats_of((uint32_t)next));
+        return r ? r : 1;  // 1: `next` ran already
+    };
+    for (uint32_t k = 0; k < n; k++) {
+        const bool pipe = prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P;
+        if (!pipe) {
+            if (pend >= 0) {
+                const int r = settle(-1);
+                if (r < 0) return r;
+                pend = -1;
+            }
+            const int r = dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, stats_of(k));
+            if (r) return r;
+            continue;
+        }
+        int r = pipe_enqueue(c, &eps[k], commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1]);
+        if (r) {
+            (void)hipStreamSynchronize(c->stream);
+            if (pend >= 0) {  // (its read-back, for the statistics; the error is returned either way)
+                bool halted = false;
+                (void)pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
+            }
+            return r;
+        }
+        if (pend >= 0) {
+            r = settle((int64_t)k);
+            if (r < 0) return r;
+            if (r == 1) {
+                pend = -1;
+                continue;
+            }
+        }
+        pend = k;
+    }
+    if (pend >= 0) {
+        const int r = settle(-1);
+        if (r < 0) return r;
+    }
+    return DV_OK;
 }
 
 }  // extern "C"

@@ -268,6 +268,21 @@ class CCEngine:
                                             _ptr(d_grant), ctypes.byref(st)), "dv_epoch_run_device")
         return st
 
+    def run_epochs_device(self, deps, d_commits=None):
+        """Several epochs back to back (dv_epoch_run_device_batch): epoch
+        k+1 is queued before epoch k's outcome is read.  d_commits: one device
+        tensor (or None) per epoch, or one tensor for all.  Returns the list of
+        stats."""
+        self._after_torch()
+        n = len(deps)
+        arr = (L.EpochDev * n)(*[d.desc() for d in deps])
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n
+        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        sts = (L.Stats * n)()
+        L.check(L.lib().dv_epoch_run_device_batch(self._ctx, arr, n, cps, sts), "dv_epoch_run_device_batch")
+        return list(sts)
+
     # ---- partitioned epochs over RCCL from the engine (dv_comm_init)
     def comm_init(self, unique_id, nranks, rank):
         """unique_id: the 128 bytes comm_unique_id() returned on rank 0."""

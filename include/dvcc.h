@@ -300,6 +300,18 @@ int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_r
  * possible, also on a one-rank communicator.  Same decisions either way. */
 int dv_comm_set_mode(dv_ctx *ctx, int mode);
 
+/* Several epochs back to back (the same results as one dv_epoch_run_device
+ * per epoch, in order): epoch k+1 is queued on the device before the host
+ * reads epoch k's outcome, so the host's turnaround between epochs hides
+ * behind the device work (prefix-kill epochs; others run one at a time).  If
+ * epoch k's decision rounds halted (an asynchronous launch yielded), epoch
+ * k+1 starts halted too -- nothing of it executes -- and both run again
+ * synchronously.  d_commits: n device pointers (or NULL; entries may be NULL);
+ * sts: n stats (or NULL).  On an error the epochs before the failing one are
+ * complete and nothing of the failing one or later ones has executed. */
+int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
+                              dv_stats *sts);
+
 /* Epoch groups -- epoch-parallel scheduling for YCSB: a
  * group is P = nranks consecutive epochs of the sequencer, and homes[e]
  * (n_homes == P) is this rank's client batch of epoch e (txn ids local,

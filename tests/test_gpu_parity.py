@@ -573,3 +573,74 @@ def test_randomized_sweep(case):
     knobs = dict(tail=bool(rng.integers(0, 2)), el64=bool(rng.integers(0, 2)),
                  asynchronous=bool(rng.integers(0, 2)))
     _check(cc, rows, [g.gen(n_txn, 77 + case), g.gen(n_txn, 78 + case)], **knobs)
+
+
+def _check_batch(cc, rows, epochs, prefix=None, max_iters=None):
+    """dv_epoch_run_device_batch against the oracle run over the same epochs
+    one after the other: every epoch's commit bytes, digest and write count,
+    and the table after the batch."""
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    refs = [_oracle_epoch(cc, tab, f0, e) for e in epochs]
+    eng = CCEngine(cc, max(e.n_txn for e in epochs), max(e.n_acc for e in epochs))
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(prefix)
+    if max_iters:
+        eng.set_async_limits(max_iters, 0)
+    deps = [DeviceEpoch(e) for e in epochs]
+    commits = [torch.zeros(max(1, e.n_txn), dtype=torch.uint8, device="cuda") for e in epochs]
+    sts = eng.run_epochs_device(deps, commits)
+    for k, (e, (c_ref, _, st_ref), st) in enumerate(zip(epochs, refs, sts)):
+        c = commits[k].cpu().numpy()[:e.n_txn]
+        assert (c == c_ref).all(), f"epoch {k}: {(c != c_ref).sum()} mismatches"
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt), f"epoch {k}"
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+    return sts
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+def test_batch_pipelined_prefix_epochs(cc):
+    """Pipelined epochs (each queued before the previous one is read back)
+    give the results of running them one at a time."""
+    rows = 1 << 18
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    _check_batch(cc, rows, [g.gen(20_000, 300 + k) for k in range(5)], prefix=512)
+
+
+@pytest.mark.gpu
+def test_batch_mixed_and_halted_epochs():
+    """A batch mixing prefix-kill epochs with small ones (run one at a time),
+    and asynchronous rounds forced to yield: a halted epoch and the one queued
+    behind it run again synchronously, results unchanged."""
+    rows = 1 << 18
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    sizes = [20_000, 20_000, 1, 20_000, 20_000, 20_000]
+    epochs = [g.gen(n, 400 + k) for k, n in enumerate(sizes)]
+    _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512)
+    sts = _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, max_iters=1)
+    assert sum(st.async_yields for st in sts) > 0, "no asynchronous launch yielded"
+
+
+@pytest.mark.gpu
+def test_batch_error_stops_before_execution():
+    """A missing key in the third epoch: the batch returns the error, the first
+    two epochs are applied, nothing of the third or later ones is."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    epochs = [g.gen(8_000, 500 + k) for k in range(5)]
+    epochs[2].keys[17] = np.uint64(rows + 3)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    for e in epochs[:2]:
+        _oracle_epoch(dvcc.NO_WAIT, tab, f0, e)
+    eng = CCEngine(dvcc.NO_WAIT, 8_000, max(e.n_acc for e in epochs))
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(256)
+    with pytest.raises(dvcc.DvccError) as ei:
+        eng.run_epochs_device([DeviceEpoch(e) for e in epochs])
+    assert ei.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
