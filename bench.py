@@ -659,7 +659,8 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": el / a.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak" if group else "strong",
+        # per GPU and step: one 1,048,576-txn epoch decided (N = 1 too), N epochs per step at N > 1
+        "scaling": "weak" if (group or (world == 1 and a.protocol == "group")) else "strong",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic: Deneva YCSB zipf generator (myrand LCG, seeded SEED+97*part+epoch)",
