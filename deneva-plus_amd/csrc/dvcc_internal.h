@@ -227,6 +227,20 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
 // digit_tot: kRadix.  scatter_ev (optional): 2 events per pass for timing.
 // n_dev (optional): the real count on the device, n an upper bound.
+// digit width of radix_sort_rows: 8 bits, or 9-10 when that saves a pass
+// (never when the probe counted the first 8-bit histogram)
+constexpr int kRadixMaxBits = 10;
+constexpr int kRadixMax = 1 << kRadixMaxBits;  // counts: kRadixMax x sort tiles, digit_tot: kRadixMax
+inline int radix_digit_bits(int key_bits, bool hist0_done) {
+    const int p8 = (key_bits + kRadixBits - 1) / kRadixBits;
+    if (hist0_done || p8 < 2) return kRadixBits;
+    const int w = (key_bits + p8 - 2) / (p8 - 1);  // one pass fewer
+    return w <= kRadixMaxBits ? w : kRadixBits;
+}
+inline int radix_passes(int key_bits, bool hist0_done) {
+    const int w = radix_digit_bits(key_bits, hist0_done);
+    return (key_bits + w - 1) / w;
+}
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
                     uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev);
 

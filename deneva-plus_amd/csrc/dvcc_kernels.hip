@@ -507,11 +507,173 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     }
 }
 
+// ---- 9- and 10-bit digits: one pass fewer where that is all it takes
+// (27-bit global rows of an 8-partition epoch group: 3 passes of 9 instead of
+// 4 of 8; 17-20-bit rows: 2 of 9-10 instead of 3).  Wider digits were
+// measured slower per pass than they save (rejected).  Same
+// structure: per-tile histograms, one scan block per digit (k_radix_scan), a
+// stable scatter ranking keys by wave ballots (W per step).
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_radix_hist_w(const uint64_t *__restrict__ in, uint64_t n, int shift,
+                                                         uint32_t *__restrict__ counts, uint32_t nblocks,
+                                                         const uint32_t *__restrict__ n_dev) {
+    constexpr uint32_t R = 1u << W;
+    __shared__ uint32_t wc[4][R];
+    n = sort_n(n, n_dev);
+    if ((uint64_t)blockIdx.x * kTile >= n) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t d = tid; d < 4 * R; d += kBlock) (&wc[0][0])[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + wave * (64 * kIPT);
+    uint64_t k[kIPT];
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        k[j] = idx < n ? in[idx] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        const uint64_t vmask = __ballot(valid);
+        if (__ballot(valid && d == d0) == vmask) {
+            if (lane == 0) wc[wave][d0] += (uint32_t)__popcll(vmask);
+        } else if (valid) {
+            atomicAdd(&wc[wave][d], 1u);
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = tid; d < R; d += kBlock)
+        counts[(uint64_t)d * nblocks + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
+}
+
+template <int W>
+__global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                            uint64_t n, int shift, const uint32_t *__restrict__ counts,
+                                                            const uint32_t *__restrict__ digit_tot, uint32_t nblocks,
+                                                            const uint32_t *__restrict__ n_dev) {
+    constexpr uint32_t R = 1u << W, PER = R / kBlock;  // digits per thread in the digit scans
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[kTile];
+    __shared__ uint32_t wc[4][R];
+    __shared__ uint32_t dstart[R];
+    __shared__ uint32_t gbase[R];  // (an epoch holds < 2^32 accesses)
+    __shared__ uint32_t lds4[4];
+    n = sort_n(n, n_dev);
+    if ((uint64_t)blockIdx.x * kTile >= n) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t tile0 = (uint64_t)blockIdx.x * kTile;
+    {
+        // global base of each digit for this tile: the smaller digits' totals
+        // + this tile's exclusive prefix within the digit
+        uint32_t t[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            t[q] = digit_tot[tid * PER + q];
+            sum += t[q];
+        }
+        uint32_t pre = block_excl_scan256(sum, lds4, nullptr);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t d = tid * PER + q;
+            gbase[d] = pre + counts[(uint64_t)d * nblocks + blockIdx.x];
+            pre += t[q];
+            wc[0][d] = wc[1][d] = wc[2][d] = wc[3][d] = 0;
+        }
+    }
+    __syncthreads();
+    const uint64_t base = tile0 + wave * (64 * kIPT);
+    uint64_t k[kIPT];
+    uint32_t r[kIPT];
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        k[j] = idx < n ? in[idx] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < W; b++) {
+            const uint32_t bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t before = wc[wave][d];
+        r[j] = before + mask_rank(peers);
+        if (valid && lane == (uint32_t)__builtin_ctzll(peers)) wc[wave][d] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    {
+        uint32_t tot[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t d = tid * PER + q;
+            const uint32_t c0 = wc[0][d], c1 = wc[1][d], c2 = wc[2][d], c3 = wc[3][d];
+            wc[0][d] = 0;
+            wc[1][d] = c0;
+            wc[2][d] = c0 + c1;
+            wc[3][d] = c0 + c1 + c2;
+            tot[q] = c0 + c1 + c2 + c3;
+            sum += tot[q];
+        }
+        uint32_t ds = block_excl_scan256(sum, lds4, nullptr);
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t d = tid * PER + q;
+            dstart[d] = ds;
+            gbase[d] -= ds;
+            ds += tot[q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        if (idx < n) {
+            const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+            skeys[dstart[d] + wc[wave][d] + r[j]] = k[j];
+        }
+    }
+    __syncthreads();
+    const uint32_t tile_n = (uint32_t)((n - tile0) < (uint64_t)kTile ? (n - tile0) : kTile);
+    for (uint32_t p = tid; p < tile_n; p += kBlock) {
+        const uint64_t key = skeys[p];
+        const uint32_t d = (uint32_t)(key >> shift) & (R - 1);
+        out[(uint64_t)gbase[d] + p] = key;
+    }
+}
+
+template <int W>
+void wide_pass(hipStream_t s, const uint64_t *in, uint64_t *out, uint64_t n, int shift, uint32_t *counts,
+               uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1) {
+    k_radix_hist_w<W><<<nb, kBlock, 0, s>>>(in, n, shift, counts, nb, n_dev);
+    k_radix_scan<<<1u << W, kBlock, 0, s>>>(counts, nb, digit_tot, n_dev);
+    hipExtLaunchKernelGGL(k_radix_scatter_w<W>, dim3(nb), dim3(kBlock), 0, s, e0, e1, 0, in, out, n, shift,
+                          (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
+}
+
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
                     uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
+    const int wbits = radix_digit_bits(key_bits, hist0_done);
+    if (wbits > kRadixBits) {
+        for (int bit = 0; bit < key_bits; bit += wbits, pass++) {
+            hipEvent_t e0 = scatter_ev ? scatter_ev[2 * pass] : nullptr, e1 = scatter_ev ? scatter_ev[2 * pass + 1] : nullptr;
+            if (wbits == 9)
+                wide_pass<9>(s, pairs[cur], pairs[cur ^ 1], n, 32 + bit, counts, digit_tot, nb, n_dev, e0, e1);
+            else
+                wide_pass<10>(s, pairs[cur], pairs[cur ^ 1], n, 32 + bit, counts, digit_tot, nb, n_dev, e0, e1);
+            cur ^= 1;
+        }
+        return cur;
+    }
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
         if (pass > 0 || !hist0_done) k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb, n_dev);

@@ -478,8 +478,8 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     const uint32_t nb = nblocks_for(A);
     if (!r) r = dalloc(&c->pairs[0], A);
     if (!r) r = dalloc(&c->pairs[1], A);
-    if (!r) r = dalloc(&c->counts, (uint64_t)kRadix * nb);
-    if (!r) r = dalloc(&c->digit_tot, kRadix);
+    if (!r) r = dalloc(&c->counts, (uint64_t)kRadixMax * nb);
+    if (!r) r = dalloc(&c->digit_tot, kRadixMax);
     if (!r) r = dalloc(&c->status, c->n_txn_cap_pad);
     if (!r) r = dalloc(&c->verdict, c->n_txn_cap_pad);
     if (!r) r = dalloc(&c->ctr, 1);
@@ -950,7 +950,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     }
     rec(c, 1);
     const int key_bits = bits_for(row_space(c));
-    c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
+    c->sort_passes = radix_passes(key_bits, fuse_hist);
     c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
@@ -1507,7 +1507,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         if (r) return r;
     }
     const int key_bits = bits_for(row_space(c));
-    c->sort_passes = (key_bits + kRadixBits - 1) / kRadixBits;
+    c->sort_passes = radix_passes(key_bits, false);
     c->prefix_mode = true;
     rec(c, 0);
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
