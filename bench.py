@@ -45,7 +45,7 @@ HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 BYTES_PER_ACCESS = 67        # algorithmic bytes per access
 SCAN_BYTES = 9               # SURVEY.md 8d per access: scan read 8 B + conflict flag write 1 B
 TIMING = {"full": True, "kernel": "kernel", "off": False}
-PROBE_ACC, PROBE_TXN = 18, 9  # k_probe algorithmic bytes per access / per txn (roofline)
+PROBE_ACC, PROBE_TXN = 17, 9  # k_probe algorithmic bytes per access / per txn (roofline)
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_config_d.json")  # tools/pmc_summary.py
 
 CONFIGS = {
@@ -400,8 +400,9 @@ def pmc_traffic(a, cc_name, world, kernel):
 def roofline(kstats, a, cc_name, world, txn_div=1):
     """The largest single launch of the epoch, the index probe (k_probe):
     algorithmic bytes per launch -- SURVEY.md 8(d)'s probe traffic, PROBE_ACC
-    B per access (key 8 + type 1 + txn id 4 read, key tag 1 gathered, row
-    word 4 written) plus PROBE_TXN B per txn (access range 8 + length 1
+    B per access (key 8 + type 1 + txn id 4 read, row word 4 written; the
+    YCSB table is dense, every key below rows x P exists, so the key check is
+    a range check) plus PROBE_TXN B per txn (access range 8 + length 1
     written); the prefix's sort keys (8 B for ~1.6 % of the accesses) are not
     counted -- over its average duration from the launch's own dispatch
     timestamps on the engine's stream.  The decision stage's two asynchronous
@@ -422,8 +423,9 @@ def roofline(kstats, a, cc_name, world, txn_div=1):
         "kernel": "k_probe", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
         "avg_launch_ms": avg_ms, "launches": launches,
-        "algorithmic_bytes": f"{PROBE_ACC} B per access + {PROBE_TXN} B per txn (SURVEY.md 8d probe: key, type, "
-                             "txn id read, key tag gathered, row word written; access ranges per txn)",
+        "algorithmic_bytes": f"{PROBE_ACC} B per access + {PROBE_TXN} B per txn (SURVEY.md 8d probe: key 8, type 1, "
+                             "txn id 4 read, row word 4 written -- a dense YCSB table's key check is arithmetic, "
+                             "no index bytes; access ranges per txn)",
         "traffic_source": src,
         "timed_by": ("dispatch timestamps of every probe launch in the timed region"
                      if a.timing != "off" else

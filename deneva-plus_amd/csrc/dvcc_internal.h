@@ -110,6 +110,10 @@ struct TableDesc {
     // in L2) instead of the byte; nullptr = no such bitmap
     const uint32_t *hbits;
     uint32_t htag;
+    // ... and for a dense map (dv_load_ycsb_partition: bucket b holds the key
+    // of tag htag, for every b) the key set is known: a key is there iff its
+    // tag is htag -- no gather at all (ycsb_wl.cpp:173-186 loads every key)
+    uint32_t dense;
     const IxEntry *ix;        // index entries (direct: [nbuckets]; chained: sorted by bucket)
     const uint32_t *bstart;   // chained: [nbuckets+1] bucket starts; nullptr = direct map
     uint64_t nbuckets;
@@ -181,6 +185,7 @@ __device__ __forceinline__ uint64_t key_split(const TableDesc &t, uint64_t key, 
 }
 // implicit-row direct map: does bucket bk hold the key of tag `tag`?
 __device__ inline bool direct_holds(const TableDesc &t, uint64_t bk, uint32_t tag, uint64_t key) {
+    if (t.dense) return tag == t.htag;
 #ifndef DVCC_NO_HOME_BITS
     if (t.hbits != nullptr && tag == t.htag) return (t.hbits[bk >> 5] >> (bk & 31)) & 1u;
 #endif

@@ -286,6 +286,7 @@ Tables make_tables(dv_ctx *c) {
         t.t[i].ktag = h.implicit_rows ? c->ktag + h.row_base : nullptr;
         t.t[i].hbits = h.implicit_rows ? h.hbits : nullptr;
         t.t[i].htag = h.htag;
+        t.t[i].dense = h.implicit_rows && h.dense && h.htag < kTagWide ? 1u : 0u;
         t.t[i].bstart = h.bstart;
         t.t[i].nbuckets = h.nbuckets ? h.nbuckets : 1;
         t.t[i].row_base = h.row_base;
