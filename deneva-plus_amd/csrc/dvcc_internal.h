@@ -221,7 +221,7 @@ constexpr uint32_t kProbeHistTiles = 1024;
 // its access count; acc_row (optional): row | wr << 31 per access.  An access
 // at position >= 1 << slog in its txn is an error (ERRB_BIG).  pair_limit <
 // n_txn: sort keys only for txns < pair_limit (the epoch's first accesses),
-// their count added to ctr->a_acc (prefix-kill epochs).
+// their count stored in ctr->a_acc (prefix-kill epochs).
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,

@@ -268,18 +268,22 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             }
         } else {
             // prefix-kill epochs: sort keys only for the prefix txns (the first
-            // accesses of the epoch), and their count (one atomic per wave)
-            uint32_t np = 0;
+            // accesses of the epoch); their count is the index after the last
+            // one, stored by the one thread that holds it (txns ascend) -- a
+            // counter atomic per wave serialised ~1,300 waves on one word
+            if (i0 + kPV <= n && txn[kPV - 1] < pair_limit) {
+                *reinterpret_cast<ulonglong2 *>(pairs + i0) = ulonglong2{out[0], out[1]};
+                *reinterpret_cast<ulonglong2 *>(pairs + i0 + 2) = ulonglong2{out[2], out[3]};
+            } else {
 #pragma unroll
-            for (int j = 0; j < kPV; j++)
-                if (i0 + j < n && txn[j] < pair_limit) {
-                    pairs[i0 + j] = out[j];
-                    np++;
-                }
-            if (__ballot(np != 0)) {
+                for (int j = 0; j < kPV; j++)
+                    if (i0 + j < n && txn[j] < pair_limit) pairs[i0 + j] = out[j];
+            }
 #pragma unroll
-                for (int off = 32; off > 0; off >>= 1) np += __shfl_xor(np, off, 64);
-                if (lane == 0) atomicAdd(&ctr->a_acc, np);
+            for (int j = 0; j < kPV; j++) {
+                const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
+                if (i0 + j < n && txn[j] < pair_limit && (nt >= pair_limit || i0 + j + 1 == n))
+                    ctr->a_acc = (uint32_t)(i0 + j + 1);
             }
         }
         // digit-0 counts of the emitted pairs (as k_radix_hist: a step whose

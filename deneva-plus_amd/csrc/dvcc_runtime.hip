@@ -144,7 +144,7 @@ struct dv_ctx {
     uint32_t v_thresh = 0;                   // asynchronous-try threshold (0: async_thresh's rule)
 
     // prefix-kill epochs (run_prefix_epoch, dvcc_prefix.hip)
-    uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 64)
+    uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 32)
     bool prefix_mode = false;     // the epoch in flight is one
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
@@ -1388,15 +1388,15 @@ int run_rounds(dv_ctx *c, bool resume) {
 }
 
 // ---- prefix-kill epochs (dvcc_prefix.hip) ----------------------------------
-// Epochs from kPrefixMinTxn txns up; the prefix is ~1/64 of the epoch, at
-// least kPrefixMin txns (config D: 16,384 of 1,048,576, whose commits kill
+// Epochs from kPrefixMinTxn txns up; the prefix is ~1/32 of the epoch, at
+// least kPrefixMin txns (config D: 32,768 of 1,048,576, whose commits kill
 // ~91 % of the later txns).
 constexpr uint32_t kPrefixMinTxn = 1u << 17;
 constexpr uint32_t kPrefixMin = 4096, kPrefixMax = 1u << 16;
 
 uint32_t prefix_size(const dv_ctx *c, uint32_t n_txn) {
     if (c->prefix_txns) return c->prefix_txns;
-    return std::min(kPrefixMax, std::max(kPrefixMin, n_txn / 64));
+    return std::min(kPrefixMax, std::max(kPrefixMin, n_txn / 32));
 }
 
 bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {

@@ -374,7 +374,7 @@ int dv_set_async_limits(dv_ctx *ctx, uint32_t max_iters, uint32_t idle_us);
  * partition) are decided prefix first: the first prefix_txns txns on their
  * own, then every later txn that conflicts with one of their commits aborts at
  * once, and only the survivors go through the rounds (same decisions;
- * dvcc_prefix.hip).  prefix_txns: 0 = automatic (n_txn / 64, clamped to
+ * dvcc_prefix.hip).  prefix_txns: 0 = automatic (n_txn / 32, clamped to
  * [4096, 65536]), 0xFFFFFFFF = off (every epoch takes the full path), else
  * that many txns for any epoch longer than it.  Between epochs. */
 int dv_set_prefix(dv_ctx *ctx, uint32_t prefix_txns);
