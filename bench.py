@@ -72,7 +72,8 @@ def parse():
                     help="N>1 headline: epoch groups (dv_epoch_group_run) or one epoch per step "
                          "(dv_epoch_run_part, --part-mode)")
     ap.add_argument("--no-pipeline", action="store_true",
-                    help="N=1: one dv_epoch_run_device call per step instead of the pipelined batch call")
+                    help="one dv_epoch_run_device (N=1) / dv_epoch_group_run (epoch groups) call per step "
+                         "instead of the batch call")
     ap.add_argument("--part1", action="store_true",
                     help="N=1 through the partitioned drivers on a one-rank RCCL communicator (their overhead)")
     ap.add_argument("--part-mode", type=int, default=0,
@@ -542,6 +543,14 @@ class PartitionedBench:
             return self.eng.run_epoch_group(groups[i % len(groups)], n_txn_rank, self.d_commit)
         return step
 
+    def group_batcher(self, groups, n_txn_rank):
+        """count consecutive groups in one dv_epoch_group_run_batch call (one
+        host wait between two groups)."""
+        def batch(first, count):
+            return self.eng.run_epoch_groups([groups[(first + i) % len(groups)] for i in range(count)],
+                                             n_txn_rank, self.d_commit)
+        return batch
+
 
 def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
     """N>1 extras beside the headline: strong scaling (one epoch per step),
@@ -643,12 +652,16 @@ def main():
         if a.protocol == "group":
             groups = pb.groups(n_txn_rank, mpr, theta, n_epochs)
             step = pb.group_stepper(groups, n_txn_rank)
+            batch = pb.group_batcher(groups, n_txn_rank)
         else:
             deps = pb.epochs(n_txn_rank, mpr, theta, n_epochs)
             step = pb.stepper(deps, n_txn_rank)
         t_gen = time.perf_counter() - t_gen
 
-    stats, el = timed(step, 0, a.warmup, a.steps, world, None if (part or a.no_pipeline) else batch)
+    # the pipelined entry points: dv_epoch_run_device_batch (one GPU),
+    # dv_epoch_group_run_batch (epoch groups); the other protocols step
+    pipelined = not a.no_pipeline and (not part or a.protocol == "group")
+    stats, el = timed(step, 0, a.warmup, a.steps, world, batch if pipelined else None)
     kstats, sstats = measure_legs(a, eng, step, a.warmup + a.steps, stats)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"

@@ -443,9 +443,10 @@ struct CommMail {
 };
 __host__ __device__ inline uint64_t mail_words(uint32_t P) { return 4ull * kRadix + (uint64_t)P * (8 + P); }
 __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const uint32_t *__restrict__ b, uint32_t nb,
-                           CommMail *m, unsigned long long seq) {
+                           const uint64_t *__restrict__ c, uint32_t nc, CommMail *m, unsigned long long seq) {
     for (uint32_t i = threadIdx.x; i < na; i += blockDim.x) m->w[i] = a[i];
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) m->w[na + i] = b[i];
+    for (uint32_t i = threadIdx.x; i < nc; i += blockDim.x) m->w[na + nb + i] = c[i];
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -889,9 +890,10 @@ namespace {
 // device words -> the host: queue the mailbox kernel and spin on its
 // sequence word (a drained stream without it is an error)
 int mail_get(DvComm *m, hipStream_t s, const uint64_t *a, uint32_t na, const uint32_t *b, uint32_t nb,
-             uint64_t *out64, uint32_t *out32) {
+             uint64_t *out64, uint32_t *out32, const uint64_t *c = nullptr, uint32_t nc = 0,
+             uint64_t *outc = nullptr) {
     const unsigned long long want = ++m->mseq;
-    k_mail_out<<<1, kBlock, 0, s>>>(a, na, b, nb, m->d_mail, want);
+    k_mail_out<<<1, kBlock, 0, s>>>(a, na, b, nb, c, nc, m->d_mail, want);
     CHK(hip_fail2(hipGetLastError(), "k_mail_out"));
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 0;; i++) {
@@ -907,6 +909,7 @@ int mail_get(DvComm *m, hipStream_t s, const uint64_t *a, uint32_t na, const uin
     }
     for (uint32_t i = 0; i < na; i++) out64[i] = m->h_mail->w[i];
     for (uint32_t i = 0; i < nb; i++) out32[i] = (uint32_t)m->h_mail->w[na + i];
+    for (uint32_t i = 0; i < nc; i++) outc[i] = m->h_mail->w[na + nb + i];
     return DV_OK;
 }
 
@@ -1125,8 +1128,23 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
 //      forwarding of what each owner must write, message.cpp:982-1025), and
 //      every origin's commit bytes back to it (the client responses);
 //   6. each rank executes the records of epochs 0..P-1 on its rows, in order.
+// Groups run back to back (dv_epoch_group_run_batch) leave their execution
+// digest on the device (defer) and the next group's vote reads it in the same
+// mailbox trip: the host then waits once between two groups, not twice.
+struct GroupDefer {
+    dv_stats *st = nullptr;  // the group whose read digest / write count are still on the device
+};
+void group_digest(dv_stats *st, const uint64_t *slots) {
+    uint64_t acc[2] = {0, 0};
+    for (int k = 0; k < kSlots; k++) {
+        acc[0] += slots[2 * k];
+        acc[1] += slots[2 * k + 1];
+    }
+    st->read_digest = acc[0];
+    st->write_cnt = acc[1];
+}
 int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank, uint8_t *d_commit,
-              dv_stats *st) {
+              dv_stats *st, GroupDefer *dfr = nullptr, bool defer = false) {
     if (!c) return DV_ERR_ARG;
     DvComm *m = ctx_comm(c);
     if (!m) return DV_ERR_STATE;
@@ -1165,7 +1183,17 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
     CHK(put_words(s, rec.data(), W, m->gs, nullptr, 0, nullptr));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
-    CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
+    {
+        // (with the previous group's execution digest, when it was deferred)
+        dv_stats *prev = dfr ? dfr->st : nullptr;
+        uint64_t pslots[2 * kSlots];
+        CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr,
+                     prev ? reinterpret_cast<const uint64_t *>(m->xacc) : nullptr, prev ? 2 * kSlots : 0, pslots));
+        if (prev) {
+            group_digest(prev, pslots);
+            dfr->st = nullptr;
+        }
+    }
     uint64_t gmax = 0;
     bool refuse = false;
     for (uint32_t q = 0; q < P; q++) {
@@ -1288,20 +1316,19 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         off += n;
     }
     CHK(hip_fail2(hipGetLastError(), "k_route_exec"));
-    uint64_t slots[2 * kSlots], acc[2] = {0, 0};
-    CHK(mail_get(m, s, reinterpret_cast<const uint64_t *>(m->xacc), 2 * kSlots, nullptr, 0, slots, nullptr));
-    for (int k = 0; k < kSlots; k++) {
-        acc[0] += slots[2 * k];
-        acc[1] += slots[2 * k + 1];
-    }
     if (st) {
         *st = est;  // this rank's decision: rounds, sort passes, timings
         st->n_txn = n_txn64 * P;
         st->committed = committed;
         st->aborted = n_txn64 * P - committed;
-        st->read_digest = acc[0];
-        st->write_cnt = acc[1];
     }
+    if (defer && dfr) {  // the next group's vote reads the digest
+        dfr->st = st;
+        return DV_OK;
+    }
+    uint64_t slots[2 * kSlots];
+    CHK(mail_get(m, s, reinterpret_cast<const uint64_t *>(m->xacc), 2 * kSlots, nullptr, 0, slots, nullptr));
+    if (st) group_digest(st, slots);
     return DV_OK;
 }
 }  // namespace
@@ -1316,6 +1343,17 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
 int dv_epoch_group_run(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st) {
     return run_group(c, homes, n_homes, txns_per_rank, d_commit, st);
+}
+
+int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_groups, uint32_t n_homes,
+                             uint32_t txns_per_rank, uint8_t *const *d_commits, dv_stats *st) {
+    GroupDefer dfr;
+    for (uint32_t g = 0; g < n_groups; g++) {
+        const int r = run_group(c, homes ? homes + (size_t)g * n_homes : nullptr, n_homes, txns_per_rank,
+                                d_commits ? d_commits[g] : nullptr, st ? st + g : nullptr, &dfr, g + 1 < n_groups);
+        if (r) return r;  // (every rank of the communicator, at the same group)
+    }
+    return DV_OK;
 }
 
 int dv_comm_set_mode(dv_ctx *c, int mode) {

@@ -152,6 +152,8 @@ SIGNATURES = [
     ("dv_comm_set_mode", ctypes.c_int, [_vp, ctypes.c_int]),
     ("dv_epoch_run_device_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(_vp), _P(Stats)]),
     ("dv_epoch_group_run", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32, _vp, _P(Stats)]),
+    ("dv_epoch_group_run_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint32, _P(_vp), _P(Stats)]),
     ("dv_epoch_stage_host", ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32]),
     ("dv_epoch_run_staged", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _P(Stats)]),
     ("dv_tpcc_epoch_run_part", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _vp, _vp,

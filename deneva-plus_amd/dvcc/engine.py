@@ -322,6 +322,26 @@ class CCEngine:
                                            ctypes.byref(st)), "dv_epoch_group_run")
         return st
 
+    def run_epoch_groups(self, groups, txns_per_rank, d_commits=None):
+        """Several epoch groups back to back (dv_epoch_group_run_batch), as
+        many run_epoch_group calls with one host wait between two groups.
+        groups: a list of group batch lists (one DeviceEpoch per rank each);
+        d_commits: one device tensor (or None) per group, or one for all.
+        Returns the list of stats."""
+        self._after_torch()
+        n = len(groups)
+        P = len(groups[0]) if n else 0
+        if any(len(g) != P for g in groups):
+            raise ValueError("every group holds one batch per rank")
+        arr = (L.EpochDev * (n * P))(*[h.desc() for g in groups for h in g])
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n
+        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        sts = (L.Stats * n)()
+        L.check(L.lib().dv_epoch_group_run_batch(self._ctx, arr, n, P, txns_per_rank, cps, sts),
+                "dv_epoch_group_run_batch")
+        return list(sts)
+
     def carry(self, dep, max_txn=None):
         """Abort carry-over: a DeviceEpoch of the last epoch's (`dep`'s)
         aborted txns, in sequence order, at most max_txn of them."""

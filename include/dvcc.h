@@ -333,6 +333,15 @@ int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, 
  * every rank returns the same code and no row changes. */
 int dv_epoch_group_run(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st);
+/* n_groups consecutive groups, exactly as n_groups dv_epoch_group_run calls
+ * (homes: n_groups * n_homes batches, group g's at g * n_homes; d_commits:
+ * NULL or one device pointer, each may be NULL, per group; st: NULL or
+ * n_groups stats), with one host wait between two groups instead of two:
+ * a group's execution digest is read together with the next group's vote.
+ * The first failing group's code is returned on every rank and no later
+ * group runs; the stats of the groups before it are then unspecified. */
+int dv_epoch_group_run_batch(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_groups, uint32_t n_homes,
+                             uint32_t txns_per_rank, uint8_t *const *d_commits, dv_stats *st);
 
 /* staged form for partitioned (multi-GPU) epochs.  Every partition holds the
  * same txn statuses after each round, hence the same list of undecided txns

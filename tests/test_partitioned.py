@@ -544,19 +544,82 @@ def _run_group_epochs(engines, homes, n_txn):
     return out
 
 
-def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None):
+def _run_group_batches(engines, homes, n_txn, groups):
+    """run_epoch_groups (one dv_epoch_group_run_batch call of `groups`
+    groups) on every engine concurrently; homes[r][g] = rank r's batches of
+    group g.  Per rank: ([commit bytes per group], [stats per group]) or the
+    exception."""
+    import threading
+    world = len(engines)
+    out = [None] * world
+
+    def body(r):
+        try:
+            ds = [torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda") for _ in range(groups)]
+            sts = engines[r].run_epoch_groups(homes[r], n_txn, ds)
+            out[r] = ([d.cpu().numpy() for d in ds], sts)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a rank hung in the epoch groups"
+    return out
+
+
+def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False):
     """Every epoch of every group against the one-partition oracle run over
     the sequenced epochs one after the other: commit bytes (each rank holds its
     own txns' bytes of every epoch), committed count, digest and writes summed
     over the partitions, and every partition's rows after each group.
     sizes: per-rank batch sizes (unequal batches; the rest of a rank's
-    sequence slots are empty txns)."""
+    sequence slots are empty txns).  batch: all groups in one
+    dv_epoch_group_run_batch call (rows checked after the last group)."""
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
     engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
     tab = O.YcsbTable(rows_pp * world)
     f0 = tab.f0.copy()
     sizes = sizes or [n_txn] * world
+    if batch:
+        all_homes = [[] for _ in range(world)]  # [rank][group][epoch]
+        all_refs = []
+        for g in range(groups):
+            homes = [[None] * world for _ in range(world)]
+            refs = []
+            for e in range(world):
+                batches = [gen.gen(sizes[r], dvcc.epoch_seed(r, 40 + g * world + e), r) for r in range(world)]
+                q = dvcc.sequence(batches)
+                c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin,
+                                               q.keys, q.types)
+                refs.append((c_ref, st_ref))
+                for r in range(world):
+                    homes[r][e] = dvcc.DeviceEpoch(batches[r])
+            for r in range(world):
+                all_homes[r].append(homes[r])
+            all_refs.append(refs)
+        res = _run_group_batches(engines, all_homes, n_txn, groups)
+        for r, x in enumerate(res):
+            assert not isinstance(x, Exception), f"rank {r}: {x}"
+        for g, refs in enumerate(all_refs):
+            committed = sum(st.committed for _, st in refs)
+            digest = writes = 0
+            for r, (cs, sts) in enumerate(res):
+                for e in range(world):
+                    assert (cs[g][e * n_txn:(e + 1) * n_txn] == refs[e][0][r * n_txn:(r + 1) * n_txn]).all(), \
+                        f"group {g} epoch {e} rank {r}"
+                assert sts[g].committed == committed and sts[g].n_txn == n_txn * world * world
+                digest = (digest + sts[g].read_digest) % (1 << 64)
+                writes += sts[g].write_cnt
+            assert digest == sum(st.read_digest for _, st in refs) % (1 << 64), f"group {g} digest"
+            assert writes == sum(st.write_cnt for _, st in refs), f"group {g} writes"
+        for p, eng in enumerate(engines):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+        for eng in engines:
+            eng.close()
+        return
     for g in range(groups):
         homes = [[None] * world for _ in range(world)]  # [rank][epoch]
         refs = []
@@ -601,6 +664,15 @@ def test_epoch_groups(cc, world, mpr):
     commit bytes, digests and rows as the oracle running the epochs in
     sequence.  (The contexts share one GPU: asynchronous rounds off.)"""
     _check_epoch_groups(cc, world, 1 << 14, 3000, mpr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,world", [(dvcc.NO_WAIT, 4), (dvcc.OCC, 2), (dvcc.CALVIN, 8)])
+def test_epoch_group_batch(cc, world):
+    """dv_epoch_group_run_batch: three groups in one call (each group's
+    digest read with the next group's vote) equal the oracle's epochs in
+    sequence, group by group."""
+    _check_epoch_groups(cc, world, 1 << 13, 2000, 0.3, groups=3, batch=True)
 
 
 @pytest.mark.gpu
@@ -674,6 +746,15 @@ def test_rccl_epoch_group_single_rank(cc):
         assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
                                                                st_ref.write_cnt)
         assert (eng.read_table(0, rows) == ref.read_table(0, rows)).all()
+    # three groups in one batch call
+    cs = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in range(3)]
+    sts = eng.run_epoch_groups([[dvcc.DeviceEpoch(e)]] * 3, n_txn, cs)
+    for c, st in zip(cs, sts):
+        st_ref = ref.run_epoch_device(dvcc.DeviceEpoch(e), c_ref)
+        assert torch.equal(c, c_ref)
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt)
+    assert (eng.read_table(0, rows) == ref.read_table(0, rows)).all()
     eng.close()
     ref.close()
 
