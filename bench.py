@@ -78,7 +78,7 @@ def parse():
                     help="N=1 through the partitioned drivers on a one-rank RCCL communicator (their overhead)")
     ap.add_argument("--part-mode", type=int, default=0,
                     help="N>1: dv_comm_set_mode -- 0 replicated when the epoch fits, else the list protocol; "
-                         "1 list protocol; 2 replicated")
+                         "1 list protocol; 2 replicated; + 4: 8-byte epoch-group batches (DV_COMM_WIDE_BATCHES)")
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")

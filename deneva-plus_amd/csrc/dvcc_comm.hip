@@ -197,6 +197,104 @@ __global__ __launch_bounds__(kBlock) void k_group_pack(const uint64_t *__restric
     }
 }
 
+// Compact batches (epoch groups whose global row space P x rows is below
+// 2^30, P <= kXMaxP): 4 B per access -- row id | start << 30 | wr << 31,
+// start = the first access of its txn -- in place of the 8 B above (half the
+// all-to-allv bytes over xGMI); the decider numbers the txns again from the
+// starts (k_group_txn_count, k_group_txn_ids).  That needs dense txn ids (0
+// first, then +0 or +1 per access, below n_txn): anything else sets *bad, and
+// the outcome vote fails the group on every rank before anything executes.
+constexpr uint32_t GP_START = 1u << 30;
+constexpr uint32_t kXMaxP = 64;
+__global__ __launch_bounds__(kBlock) void k_group_pack_c(const uint64_t *__restrict__ keys,
+                                                         const uint8_t *__restrict__ types,
+                                                         const uint32_t *__restrict__ txn, uint64_t n,
+                                                         uint32_t n_txn, uint32_t *__restrict__ k32,
+                                                         uint32_t *__restrict__ bad) {
+    bool b = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = keys[i];
+        const uint32_t t = txn[i];
+        const uint32_t pt = i ? txn[i - 1] : 0u;
+        const bool start = i == 0 || t != pt;
+        if (t >= n_txn || (i == 0 ? t != 0u : (t != pt && t != pt + 1u))) b = true;
+        // (a key past 30 bits saturates and fails the decider's range check)
+        k32[i] = ((k >> 30) ? 0x3FFFFFFFu : (uint32_t)k) | (start ? GP_START : 0u) |
+                 (types[i] == DV_WR ? 0x80000000u : 0u);
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+// the received compact batches: origin q's accesses at [eoff[q], eoff[q+1]),
+// cut into tiles of kXTile that never span two origins (origin q's tiles
+// from toff[q])
+constexpr int kXIPT = 16;
+constexpr uint32_t kXTile = kBlock * kXIPT;
+struct XSegs {
+    uint32_t P, tpr;
+    uint64_t eoff[kXMaxP + 1];
+    uint32_t toff[kXMaxP + 1];
+};
+__device__ __forceinline__ uint32_t xseg_of(const XSegs &s, uint32_t tile) {
+    uint32_t q = 0;
+    while (q + 1 < s.P && s.toff[q + 1] <= tile) q++;  // (origins without accesses hold no tile)
+    return q;
+}
+
+__device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *red) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    v = wave_incl_sum(v, lane);
+    if (lane == 63) red[wave] = v;
+    __syncthreads();
+    const uint32_t t = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+    return t;
+}
+
+// txn starts per tile
+__global__ __launch_bounds__(kBlock) void k_group_txn_count(const uint32_t *__restrict__ rk, XSegs s,
+                                                            uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t red[kBlock / 64];
+    const uint32_t tile = blockIdx.x, q = xseg_of(s, tile);
+    const uint64_t b0 = s.eoff[q] + (uint64_t)(tile - s.toff[q]) * kXTile;
+    const uint64_t e = b0 + kXTile < s.eoff[q + 1] ? b0 + kXTile : s.eoff[q + 1];
+    uint32_t c = 0;
+    for (uint64_t i = b0 + threadIdx.x; i < e; i += kBlock) c += (rk[i] & GP_START) ? 1u : 0u;
+    c = block_sum(c, red);
+    if (threadIdx.x == 0) cnt[tile] = c;
+}
+
+// global txn id of every access (origin q's txn j is q * tpr + j, the id
+// dv_epoch_group_run gives it) into rt, the start bits cleared from rk
+__global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__ rk, XSegs s,
+                                                          const uint32_t *__restrict__ cnt, uint32_t *__restrict__ rt) {
+    __shared__ uint32_t red[kBlock / 64], wt[2][kBlock / 64];
+    const uint32_t tile = blockIdx.x, q = xseg_of(s, tile);
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t b0 = s.eoff[q] + (uint64_t)(tile - s.toff[q]) * kXTile;
+    const uint64_t e = b0 + kXTile < s.eoff[q + 1] ? b0 + kXTile : s.eoff[q + 1];
+    uint32_t pre = 0;  // the starts of this origin's earlier tiles
+    for (uint32_t k = s.toff[q] + threadIdx.x; k < tile; k += kBlock) pre += cnt[k];
+    uint32_t run = block_sum(pre, red) + q * s.tpr;
+    for (uint32_t u = 0; u < (uint32_t)kXIPT; u++) {  // 256 consecutive accesses per step
+        const uint64_t i = b0 + (uint64_t)u * kBlock + threadIdx.x;
+        const uint32_t w = i < e ? rk[i] : 0u;
+        const bool f = (w & GP_START) != 0;
+        const uint64_t m = __ballot(f);
+        const uint32_t p = u & 1u;
+        if (lane == 0) wt[p][wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t base = run;
+        for (uint32_t v = 0; v < wave; v++) base += wt[p][v];
+        const uint32_t incl = base + (uint32_t)__popcll(m & ((2ull << lane) - 1ull));
+        if (i < e) {
+            rt[i] = incl - 1u;
+            rk[i] = w & ~GP_START;
+        }
+        run += wt[p][0] + wt[p][1] + wt[p][2] + wt[p][3];
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
                                                      const uint8_t *__restrict__ types,
                                                      const uint32_t *__restrict__ txn, uint64_t n,
@@ -456,7 +554,12 @@ __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const ui
 // code, committed txns, receive capacity, then records per owner
 constexpr uint32_t kGroupRecHead = 8;
 __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
-                              uint64_t cap, uint64_t *__restrict__ rec) {
+                              uint64_t cap, uint64_t *__restrict__ rec, uint32_t *__restrict__ pack_bad) {
+    // a compact batch with txn ids that are not dense (k_group_pack_c) fails
+    // the group as an argument error; the flag is reset for the next group
+    if (!fail && *pack_bad) fail = (uint32_t)(-DV_ERR_ARG);
+    __syncthreads();
+    if (threadIdx.x == 0) *pack_bad = 0;
     for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) rec[kGroupRecHead + q] = fail ? 0u : tot[q];
     if (threadIdx.x == 0) {
         rec[0] = fail;
@@ -512,6 +615,7 @@ struct DvComm {
     uint64_t *xcnt = nullptr;  // [2 * nranks]: send counts, received counts
     uint32_t *xvote = nullptr; // [8]: longest txn, argument flags, longest batch, replication blockers (MAX); groups: table widths
     int mode = 0;              // dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible
+    bool wide = false;         // epoch groups: 8-byte batches even where the compact ones fit (DV_COMM_WIDE_BATCHES)
     uint32_t *gerr = nullptr;  // input-error bits, all-reduced (MAX)
     CommMail *h_mail = nullptr, *d_mail = nullptr;  // host-mapped mailbox (mail_wait)
     unsigned long long mseq = 0;
@@ -520,6 +624,8 @@ struct DvComm {
     uint8_t *gcommit = nullptr;                 // the commit bytes when the caller passes none
     unsigned long long *xacc = nullptr;         // execution: read digest, writes ([2][kSlots])
     uint64_t *gs = nullptr, *gr = nullptr;      // all-gathered vote / outcome records: [8 + P], [P][8 + P]
+    uint32_t *gtc = nullptr;                    // compact batches: txn starts per received tile
+    uint32_t *gbad = nullptr;                   // compact batches: a sender's txn ids were not dense
 };
 
 }  // namespace dvcc
@@ -731,7 +837,7 @@ void free_bufs(DvComm *m) {
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
-                 m->gs, m->gr};
+                 m->gs, m->gr, m->gtc, m->gbad};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -744,6 +850,7 @@ void free_bufs(DvComm *m) {
     m->gcommit = nullptr;
     m->xacc = nullptr;
     m->gs = m->gr = nullptr;
+    m->gtc = m->gbad = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -775,6 +882,9 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->xacc, 2 * kSlots));
     CHK(alloc(&m->gs, kGroupRecHead + P));
     CHK(alloc(&m->gr, (uint64_t)P * (kGroupRecHead + P)));
+    CHK(alloc(&m->gtc, acc / kXTile + kXMaxP + 2));
+    CHK(alloc(&m->gbad, 1));
+    CHK(hip_fail2(hipMemset(m->gbad, 0, sizeof(uint32_t)), "memset"));
     const size_t mail_bytes = sizeof(CommMail) + 8 * mail_words(P);
     CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), mail_bytes,
                                 hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
@@ -1180,6 +1290,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     rec[2] = capable ? 0u : 1u;
     rec[3] = capable ? ctx_table0_rows(c) : 0u;
     rec[4] = std::min<uint64_t>(cfg.max_acc, acap);
+    // compact batches (k_group_pack_c) need the global row ids below 2^30
+    rec[5] = capable && !m->wide && P <= kXMaxP && ctx_table0_rows(c) * P < (1ull << 30) ? 0u : 1u;
     for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
     CHK(put_words(s, rec.data(), W, m->gs, nullptr, 0, nullptr));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
@@ -1195,10 +1307,11 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         }
     }
     uint64_t gmax = 0;
-    bool refuse = false;
+    bool refuse = false, compact = true;
     for (uint32_t q = 0; q < P; q++) {
         const uint64_t *r = &all[(size_t)q * W];
         gmax = std::max<uint64_t>(gmax, r[0]);
+        compact &= r[5] == 0;
         refuse |= r[1] || r[2] || r[3] != all[3];
         uint64_t in = 0;  // what rank q receives: its epoch's batches
         for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
@@ -1208,33 +1321,56 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     if (refuse) return DV_ERR_ARG;  // every rank
     const uint32_t glen = (uint32_t)std::min<uint64_t>(gmax ? gmax : 1u, kMaxPos);
 
-    // 2. every batch to its decider: [row id | wr << 31, 4 B | txn id, 4 B]
+    // 2. every batch to its decider: [row id | wr << 31, 4 B | txn id, 4 B],
+    //    or compact: [row id | start << 30 | wr << 31, 4 B] and the txn ids
+    //    numbered again on the decider
     uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
     uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *stx = reinterpret_cast<uint32_t *>(sb + 4 * acap);
     uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * acap);
     std::vector<size_t> sc(P), sd(P), rc(P), rd(P);
     uint64_t so = 0, ro = 0;
+    XSegs xs{};
+    xs.P = P;
+    xs.tpr = txns_per_rank;
+    uint32_t xtiles = 0;
     for (uint32_t e = 0; e < P; e++) {
         const uint64_t n = sendc[e];
         if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
-            k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                   (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
+            if (compact)
+                k_group_pack_c<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                         homes[e].n_txn, sk + so, m->gbad);
+            else
+                k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                       (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
         }
         sc[e] = 4 * n;
         sd[e] = 4 * so;
         so += n;
         rc[e] = 4 * recvc[e];
         rd[e] = 4 * ro;
+        if (compact) {
+            xs.eoff[e] = ro;
+            xs.toff[e] = xtiles;
+            xtiles += (uint32_t)((recvc[e] + kXTile - 1) / kXTile);
+        }
         ro += recvc[e];
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
     CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
                           reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
-    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
-                          reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
+    if (!compact)
+        CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
+                              reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
     CHK(m->x->group(false));
+    if (compact && xtiles) {
+        xs.eoff[P] = ro;
+        xs.toff[P] = xtiles;
+        k_group_txn_count<<<xtiles, kBlock, 0, s>>>(rk, xs, m->gtc);
+        k_group_txn_ids<<<xtiles, kBlock, 0, s>>>(rk, xs, m->gtc, rt);
+        CHK(hip_fail2(hipGetLastError(), "k_group_txn_ids"));
+    }
 
     // 3. decide this rank's epoch; its committed accesses are routed into the
     //    send area (free again once the batches have left)
@@ -1254,7 +1390,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    (or an owner whose receive area is too small) fails the group on
     //    every rank; committed txns; records per owner
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs);
+    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad);
     CHK(hip_fail2(hipGetLastError(), "k_route_words"));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
@@ -1357,10 +1493,11 @@ int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_gr
 }
 
 int dv_comm_set_mode(dv_ctx *c, int mode) {
-    if (!c || mode < 0 || mode > 2) return DV_ERR_ARG;
+    if (!c || (mode & ~DV_COMM_WIDE_BATCHES) < 0 || (mode & ~DV_COMM_WIDE_BATCHES) > 2) return DV_ERR_ARG;
     DvComm *m = ctx_comm(c);
     if (!m) return DV_ERR_STATE;
-    m->mode = mode;
+    m->mode = mode & ~DV_COMM_WIDE_BATCHES;
+    m->wide = (mode & DV_COMM_WIDE_BATCHES) != 0;
     return DV_OK;
 }
 

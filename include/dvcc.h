@@ -297,7 +297,11 @@ int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_r
  * replicated when every rank's table 0 is a YCSB implicit-row map with a
  * 31-bit global row space and the whole epoch fits the context (max_acc), else
  * the list protocol; 1: always the list protocol; 2: replicated whenever
- * possible, also on a one-rank communicator.  Same decisions either way. */
+ * possible, also on a one-rank communicator.  Same decisions either way.
+ * OR DV_COMM_WIDE_BATCHES into mode: epoch groups move every batch as 8 bytes
+ * per access even where the compact 4-byte form (global rows below 2^30,
+ * dense txn ids) applies -- results are identical. */
+#define DV_COMM_WIDE_BATCHES 4
 int dv_comm_set_mode(dv_ctx *ctx, int mode);
 
 /* Several epochs back to back (the same results as one dv_epoch_run_device
@@ -330,7 +334,12 @@ int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, 
  * Requires every rank's table 0 loaded by dv_load_ycsb_partition (a dense
  * map, so a key's range check is its owner's key check); DV_ERR_ARG on every
  * rank otherwise.  Errors (a key out of range in any epoch, ...) are voted:
- * every rank returns the same code and no row changes. */
+ * every rank returns the same code and no row changes.  Batches move as 4 B
+ * per access (row id, txn-start and write bits; the decider numbers the txns
+ * again) when P x rows < 2^30, else as 8 B (row id, txn id); the compact form
+ * needs every txn id below a batch's n_txn to have an access -- a batch with
+ * an empty txn fails the group with DV_ERR_ARG on every rank
+ * (DV_COMM_WIDE_BATCHES lifts that). */
 int dv_epoch_group_run(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st);
 /* n_groups consecutive groups, exactly as n_groups dv_epoch_group_run calls

@@ -569,17 +569,22 @@ def _run_group_batches(engines, homes, n_txn, groups):
     return out
 
 
-def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False):
+def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False,
+                        wide=False):
     """Every epoch of every group against the one-partition oracle run over
     the sequenced epochs one after the other: commit bytes (each rank holds its
     own txns' bytes of every epoch), committed count, digest and writes summed
     over the partitions, and every partition's rows after each group.
     sizes: per-rank batch sizes (unequal batches; the rest of a rank's
     sequence slots are empty txns).  batch: all groups in one
-    dv_epoch_group_run_batch call (rows checked after the last group)."""
+    dv_epoch_group_run_batch call (rows checked after the last group).
+    wide: 8-byte batches (DV_COMM_WIDE_BATCHES) instead of the compact ones."""
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
     engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
+    if wide:
+        for eng in engines:
+            eng.comm_set_mode(2 | dvcc._lib.DV_COMM_WIDE_BATCHES)
     tab = O.YcsbTable(rows_pp * world)
     f0 = tab.f0.copy()
     sizes = sizes or [n_txn] * world
@@ -667,6 +672,14 @@ def test_epoch_groups(cc, world, mpr):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+def test_epoch_groups_wide_batches(cc):
+    """The 8-byte batch form (row id, txn id per access), which groups whose
+    global row space reaches 2^30 take: the same results."""
+    _check_epoch_groups(cc, 4, 1 << 13, 2000, 0.3, wide=True)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cc,world", [(dvcc.NO_WAIT, 4), (dvcc.OCC, 2), (dvcc.CALVIN, 8)])
 def test_epoch_group_batch(cc, world):
     """dv_epoch_group_run_batch: three groups in one call (each group's
@@ -709,6 +722,21 @@ def test_epoch_groups_errors_are_collective():
     for r, x in enumerate(res):
         assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, x)
     for eng, b in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b).all()
+    res = _run_group_epochs(engines, homes, n_txn)
+    assert all(not isinstance(x, Exception) for x in res), res
+    # an empty txn inside a batch (txn ids not dense): the compact batch
+    # format cannot number it, so the group fails with DV_ERR_ARG everywhere
+    after = [eng.read_table(0, rows_pp) for eng in engines]
+    gap = gen.gen(n_txn, dvcc.epoch_seed(2, 63), 2)
+    tb = gap.txn_begin.copy()
+    tb[5] = tb[4]
+    gap_homes = [list(h) for h in homes]
+    gap_homes[2][0] = dvcc.DeviceEpoch(dvcc.Epoch(gap.keys, gap.types, tb))
+    res = _run_group_epochs(engines, gap_homes, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
+    for eng, b in zip(engines, after):
         assert (eng.read_table(0, rows_pp) == b).all()
     res = _run_group_epochs(engines, homes, n_txn)
     assert all(not isinstance(x, Exception) for x in res), res
