@@ -206,11 +206,23 @@ __global__ __launch_bounds__(kBlock) void k_group_pack(const uint64_t *__restric
 // the outcome vote fails the group on every rank before anything executes.
 constexpr uint32_t GP_START = 1u << 30;
 constexpr uint32_t kXMaxP = 64;
-__global__ __launch_bounds__(kBlock) void k_group_pack_c(const uint64_t *__restrict__ keys,
-                                                         const uint8_t *__restrict__ types,
-                                                         const uint32_t *__restrict__ txn, uint64_t n,
-                                                         uint32_t n_txn, uint32_t *__restrict__ k32,
+// (every batch of the group in one launch: blockIdx.y = epoch)
+struct PackSrc {
+    const uint64_t *keys[kXMaxP];
+    const uint8_t *types[kXMaxP];
+    const uint32_t *txn[kXMaxP];
+    uint64_t n[kXMaxP], off[kXMaxP];
+    uint32_t n_txn[kXMaxP];
+};
+__global__ __launch_bounds__(kBlock) void k_group_pack_c(PackSrc src, uint32_t *__restrict__ k32_all,
                                                          uint32_t *__restrict__ bad) {
+    const uint32_t e = blockIdx.y;
+    const uint64_t *__restrict__ keys = src.keys[e];
+    const uint8_t *__restrict__ types = src.types[e];
+    const uint32_t *__restrict__ txn = src.txn[e];
+    const uint64_t n = src.n[e];
+    const uint32_t n_txn = src.n_txn[e];
+    uint32_t *__restrict__ k32 = k32_all + src.off[e];
     bool b = false;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = keys[i];
@@ -1333,16 +1345,22 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     xs.P = P;
     xs.tpr = txns_per_rank;
     uint32_t xtiles = 0;
+    PackSrc ps{};
+    uint64_t nmax = 0;
     for (uint32_t e = 0; e < P; e++) {
         const uint64_t n = sendc[e];
-        if (n) {
+        if (compact) {
+            ps.keys[e] = homes[e].keys;
+            ps.types[e] = homes[e].types;
+            ps.txn[e] = homes[e].acc_txn;
+            ps.n[e] = n;
+            ps.off[e] = so;
+            ps.n_txn[e] = homes[e].n_txn;
+            nmax = std::max(nmax, n);
+        } else if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
-            if (compact)
-                k_group_pack_c<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                         homes[e].n_txn, sk + so, m->gbad);
-            else
-                k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                       (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
+            k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                   (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
         }
         sc[e] = 4 * n;
         sd[e] = 4 * so;
@@ -1355,6 +1373,10 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
             xtiles += (uint32_t)((recvc[e] + kXTile - 1) / kXTile);
         }
         ro += recvc[e];
+    }
+    if (compact && nmax) {
+        const uint32_t bx = (uint32_t)std::min<uint64_t>((nmax + kBlock - 1) / kBlock, std::max(1u, 2048u / P));
+        k_group_pack_c<<<dim3(bx, P), kBlock, 0, s>>>(ps, sk, m->gbad);
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
