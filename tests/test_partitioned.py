@@ -702,6 +702,42 @@ def test_epoch_groups_prefix_kill():
 
 
 @pytest.mark.gpu
+def test_epoch_group_batch_stops_at_failing_group():
+    """dv_epoch_group_run_batch with a bad key in its second group: every
+    rank returns DV_ERR_KEY_NOT_FOUND, the first group's rows stay applied,
+    the rest of the batch never runs, and the engines run groups again."""
+    world, rows_pp, n_txn = 2, 1 << 12, 800
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    ref = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    groups = [[[dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(r, 80 + g * world + e), r)) for e in range(world)]
+               for g in range(3)] for r in range(world)]  # [rank][group][epoch]
+    bad = gen.gen(n_txn, dvcc.epoch_seed(0, 99), 0)
+    bad.keys[3] = np.uint64(rows_pp * world + 1)
+    bad_groups = [[list(g) for g in gr] for gr in groups]
+    bad_groups[0][1][1] = dvcc.DeviceEpoch(bad)
+    res = _run_group_batches(engines, bad_groups, n_txn, 3)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, x)
+    res = _run_group_epochs(ref, [groups[r][0] for r in range(world)], n_txn)  # the first group alone
+    assert all(not isinstance(x, Exception) for x in res), res
+    for eng, e_ref in zip(engines, ref):
+        assert (eng.read_table(0, rows_pp) == e_ref.read_table(0, rows_pp)).all()
+    res = _run_group_batches(engines, [groups[r][1:] for r in range(world)], n_txn, 2)
+    ref_res = _run_group_batches(ref, [groups[r][1:] for r in range(world)], n_txn, 2)
+    for x, y in zip(res, ref_res):
+        assert not isinstance(x, Exception) and not isinstance(y, Exception), (x, y)
+        for g in range(2):
+            assert (x[0][g] == y[0][g]).all()
+            assert (x[1][g].committed, x[1][g].read_digest) == (y[1][g].committed, y[1][g].read_digest)
+    for eng, e_ref in zip(engines, ref):
+        assert (eng.read_table(0, rows_pp) == e_ref.read_table(0, rows_pp)).all()
+    for eng in engines + ref:
+        eng.close()
+
+
+@pytest.mark.gpu
 def test_epoch_groups_errors_are_collective():
     """A key out of range in one batch of one epoch fails the group on every
     rank with DV_ERR_KEY_NOT_FOUND and changes no row; a rank whose table is
