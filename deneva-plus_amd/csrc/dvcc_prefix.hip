@@ -47,13 +47,23 @@ __device__ __forceinline__ uint32_t row_bits(const uint32_t *rs, uint32_t row) {
 // only when it must -- 10.3M gathers at config D were bound by the L2's
 // request rate (26 of k_kill's 39 us):
 //   the bitmap words of rows [0, kHotRows): zipf's hot rows are the small
-//     keys, so ~58 % of the accesses (top 256K of 16.8M rows) read LDS;
+//     keys, so over half of the accesses (top 64K of 16.8M rows) read LDS;
 //   a one-hash Bloom filter (kBloomBits) of the marked rows from kHotRows on,
 //     kept right after the bitmap and cleared with it: a cold access to a row
 //     no committed prefix txn touched reads LDS only.
-constexpr uint32_t kHotRows = 1u << 18, kHotWords = kHotRows / 16;
-constexpr uint32_t kBloomBits = 1u << 19, kBloomWords = kBloomBits / 32;
-__device__ __forceinline__ uint32_t bloom_bit(uint32_t row) { return (row * 0x9E3779B1u) >> (32 - 19); }
+// 16 KiB of hot words + 128 KiB of filter: a filter twice as large took
+// k_kill from 28.0 to 25.3 us at config D (fewer false positives, each an L2
+// gather; 2^16 or 2^17 hot rows beside it, the same), and a filter half as
+// large cost 1.8 us more (tools/kstat_ab.sh).
+#ifndef DVCC_HOT_LOG
+#define DVCC_HOT_LOG 16
+#endif
+#ifndef DVCC_BLOOM_LOG
+#define DVCC_BLOOM_LOG 20
+#endif
+constexpr uint32_t kHotRows = 1u << DVCC_HOT_LOG, kHotWords = kHotRows / 16;
+constexpr uint32_t kBloomBits = 1u << DVCC_BLOOM_LOG, kBloomWords = kBloomBits / 32;
+__device__ __forceinline__ uint32_t bloom_bit(uint32_t row) { return (row * 0x9E3779B1u) >> (32 - DVCC_BLOOM_LOG); }
 
 // (a multiple of 4 words: k_epoch_clear zeroes it in 16-byte stores)
 uint64_t row_state_words(uint64_t rows) { return (((rows + 15) / 16 + 3) & ~3ull) + kBloomWords; }
@@ -64,7 +74,7 @@ uint64_t row_state_words(uint64_t rows) { return (((rows + 15) / 16 + 3) & ~3ull
 // their bitmap words first, then each nonzero word into the bitmap with one
 // atomic per block (one device-scope atomic per access on a shared word ran
 // at ~88 per us); other rows go straight to the bitmap and the Bloom filter.
-constexpr int kMarkBlock = 1024;  // (64 KiB of LDS per block)
+constexpr int kMarkBlock = 1024;  // (16 KiB of LDS per block)
 __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(const uint8_t *__restrict__ status,
                                                             const uint32_t *__restrict__ tb_start,
                                                             const uint32_t *__restrict__ tb_end,
@@ -116,7 +126,7 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(const uint8_t *__res
 // then ORs each txn's range of bits.  (The conflict rule is the one in the
 // header comment; the txn id of an access is never needed here.)
 constexpr int kKillWords = 8;  // ballot words per wave per step (loads in flight)
-constexpr int kKillBlock = 1024;  // one block per CU (128 KiB of LDS): 16 waves to stream with
+constexpr int kKillBlock = 1024;  // one block per CU (144 KiB of LDS): 16 waves to stream with
 __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
                                                  const uint32_t *__restrict__ row_state, uint64_t state_words,
                                                  const uint32_t *__restrict__ bloom, int nowait,
@@ -330,7 +340,7 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
-    // (128 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
+    // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
     k_kill<<<grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s>>>(acc_row, n_acc, row_state, rs_words - kBloomWords,
                                                                      row_state + (rs_words - kBloomWords), nowait,
                                                                      kill_bits, ctr);
