@@ -436,11 +436,14 @@ void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *
                              uint8_t *status, const Counters *ctr);
 
 // per-epoch reset: counters (err = *err_seed when given), tile tickets,
-// status (value; padding aborted), access ranges and counts
+// status (value; padding aborted), access ranges and counts; with hctr, the
+// counters as they stand first go to that host mirror and *hseq = seq (the
+// previous pipelined epoch's read-back, launch_ctr_out folded in)
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
-                        uint64_t zero_words = 0, bool gate = false);
+                        uint64_t zero_words = 0, bool gate = false, Counters *hctr = nullptr,
+                        unsigned long long *hseq = nullptr, unsigned long long seq = 0);
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,

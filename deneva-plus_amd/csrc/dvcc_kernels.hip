@@ -882,8 +882,20 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         uint8_t *__restrict__ tlen,
                                                         uint32_t *__restrict__ tile_ctr,
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
-                                                        uint4 *__restrict__ zero, uint64_t zero_n, int gate) {
+                                                        uint4 *__restrict__ zero, uint64_t zero_n, int gate,
+                                                        Counters *hctr, unsigned long long *hseq,
+                                                        unsigned long long seq) {
     if (blockIdx.x == 0) {
+        // pipelined epochs: the previous epoch's counters into their host
+        // mirror first (what k_ctr_out would have done as one more launch)
+        if (hctr) {
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(ctr);
+            uint32_t *dst = reinterpret_cast<uint32_t *>(hctr);
+            for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) dst[i] = src[i];
+            __threadfence_system();
+            __syncthreads();
+            if (threadIdx.x == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
         // gate (pipelined epochs, dv_epoch_run_device_batch): the previous
         // epoch is still unread by the host; if it halted or failed, this one
         // starts halted, so nothing of it reaches the tables or the commit bytes
@@ -928,13 +940,14 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
-                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate) {
+                        const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
+                        Counters *hctr, unsigned long long *hseq, unsigned long long seq) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
-                                       gate ? 1 : 0);
+                                       gate ? 1 : 0, hctr, hseq, seq);
 }
 
 // ---------------------------------------------------------------- execute

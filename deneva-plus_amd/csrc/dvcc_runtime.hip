@@ -93,6 +93,11 @@ struct dv_ctx {
     Counters *h_mir[2] = {nullptr, nullptr}, *d_mir[2] = {nullptr, nullptr};
     unsigned long long *h_mseq[2] = {nullptr, nullptr}, *d_mseq[2] = {nullptr, nullptr};
     bool clear_gate = false;                    // the next epoch clear is gated on the previous epoch
+    // a pipelined epoch whose counter mirror the next epoch's clear writes
+    // (pipe_enqueue with defer); mirror_flush writes it if that clear never came
+    bool mir_pending = false;
+    int mir_slot = 0;
+    unsigned long long mir_seq = 0;
     uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
     const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
@@ -359,6 +364,13 @@ int mirror_wait(dv_ctx *c, int k, unsigned long long want) {
         }
         __builtin_ia32_pause();
     }
+}
+
+// a deferred counter mirror that no epoch clear has written yet: now
+void mirror_flush(dv_ctx *c) {
+    if (!c->mir_pending) return;
+    c->mir_pending = false;
+    launch_ctr_out(c->stream, c->ctr, c->d_mir[c->mir_slot], c->d_mseq[c->mir_slot], c->mir_seq);
 }
 
 int sync_counters(dv_ctx *c) {
@@ -1511,8 +1523,12 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->sort_passes = radix_passes(key_bits, false);
     c->prefix_mode = true;
     rec(c, 0);
+    const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
+    c->mir_pending = false;
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
-                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate);
+                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate,
+                       mir ? c->d_mir[c->mir_slot] : nullptr, mir ? c->d_mseq[c->mir_slot] : nullptr,
+                       mir ? c->mir_seq : 0ull);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
@@ -1593,12 +1609,18 @@ struct EpochSnap {
 };
 
 // a prefix-kill epoch queued through its execution, commit bytes and counter
-// mirror (slot), with no host wait; gate: the epoch before it is still unread
-int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate, int slot, EpochSnap &sn) {
+// mirror (slot), with no host wait; gate: the epoch before it is still unread;
+// defer: another pipelined epoch is queued right behind it, whose clear
+// writes this one's mirror (one launch fewer per epoch)
+int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate, int slot, EpochSnap &sn,
+                 bool defer) {
     c->clear_gate = gate;
     int r = run_prefix_epoch(c, ep);
     c->clear_gate = false;
-    if (r) return r;
+    if (r) {
+        mirror_flush(c);  // (the previous epoch's read-back, when this one never reached its clear)
+        return r;
+    }
     enqueue_exec(c, d_commit);
     r = hip_fail(hipGetLastError(), "execution launch");
     sn.n_acc = c->n_acc;
@@ -1610,7 +1632,14 @@ int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate
     sn.sort_passes = c->sort_passes;
     sn.async_unconfirmed = c->async_unconfirmed;
     sn.slot = slot;
-    sn.seq = mirror_out(c, slot);
+    if (defer && !r) {
+        sn.seq = ++c->cseq;
+        c->mir_pending = true;
+        c->mir_slot = slot;
+        c->mir_seq = sn.seq;
+    } else {
+        sn.seq = mirror_out(c, slot);
+    }
     c->phase = 0;
     c->prefix_mode = false;
     if (!r) r = hip_fail(hipGetLastError(), "counter mirror");
@@ -1701,36 +1730,45 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
             return r;
         }
         if (!halted) return DV_OK;
+        c->mir_pending = false;  // (`next`'s read-back: it runs again below)
         r = pipe_redo(c);
         if (!r) r = dv_epoch_run_device(c, &eps[pend], commit_of((uint32_t)pend), nullptr, stats_of((uint32_t)pend));
         if (!r && next >= 0) r = dv_epoch_run_device(c, &eps[next], commit_of((uint32_t)next), nullptr,
                                                      stats_of((uint32_t)next));
         return r ? r : 1;  // 1: `next` ran already
     };
+    auto pipelined = [&](uint32_t k) {
+        return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P;
+    };
+    auto fail = [&](int r) {  // (no read-back is waited for after an error)
+        c->mir_pending = false;
+        return r;
+    };
     for (uint32_t k = 0; k < n; k++) {
-        const bool pipe = prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P;
-        if (!pipe) {
+        if (!pipelined(k)) {
             if (pend >= 0) {
                 const int r = settle(-1);
-                if (r < 0) return r;
+                if (r < 0) return fail(r);
                 pend = -1;
             }
             const int r = dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, stats_of(k));
-            if (r) return r;
+            if (r) return fail(r);
             continue;
         }
-        int r = pipe_enqueue(c, &eps[k], commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1]);
+        // the next epoch's clear writes this one's read-back when it is queued right behind
+        const bool defer = k + 1 < n && pipelined(k + 1);
+        int r = pipe_enqueue(c, &eps[k], commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1], defer);
         if (r) {
             (void)hipStreamSynchronize(c->stream);
             if (pend >= 0) {  // (its read-back, for the statistics; the error is returned either way)
                 bool halted = false;
                 (void)pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
             }
-            return r;
+            return fail(r);
         }
         if (pend >= 0) {
             r = settle((int64_t)k);
-            if (r < 0) return r;
+            if (r < 0) return fail(r);
             if (r == 1) {
                 pend = -1;
                 continue;
@@ -1740,7 +1778,7 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
     }
     if (pend >= 0) {
         const int r = settle(-1);
-        if (r < 0) return r;
+        if (r < 0) return fail(r);
     }
     return DV_OK;
 }
