@@ -1027,7 +1027,10 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
 // its committed ones over its lanes (a prefix sum of their lengths): at a
 // ~2 % commit rate a thread per txn left most lanes idle behind a few serial
 // access loops, and at high commit rates this keeps every lane busy.
-enum : int { EX_READS = 1, EX_WRITES = 2 };
+// COMMIT (the launch that reads, the first): also the commit bytes and the
+// committed count, what k_commit_out does -- for a rejected epoch too, whose
+// rows stay untouched.
+enum : int { EX_READS = 1, EX_WRITES = 2, EX_COMMIT = 4 };
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict__ tb_start,
                                                      const uint32_t *__restrict__ tb_end,
@@ -1036,16 +1039,23 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      const uint8_t *__restrict__ status,
                                                      uint64_t *__restrict__ f0,
                                                      const uint64_t *__restrict__ pkey,
-                                                     Counters *ctr, RowMap rm) {
-    __shared__ unsigned long long part[2][4];
-    if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
+                                                     Counters *ctr, RowMap rm, uint8_t *__restrict__ commit_out) {
+    __shared__ unsigned long long part[3][4];
+    if (ctr->halt) return;  // rounds not finished (dv_epoch_finish resumes them)
+    const bool rows = !input_err(ctr);  // a rejected epoch changes no row
+    if (!(MODE & EX_COMMIT) && !rows) return;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long dig = 0, wcnt = 0;
+    unsigned long long dig = 0, wcnt = 0, ncom = 0;
     const uint32_t step = gridDim.x * (kBlock / 64) * 64;
     for (uint32_t base = (blockIdx.x * (kBlock / 64) + wave) * 64; base < n_txn; base += step) {
         const uint32_t t = base + lane;
         const bool com = t < n_txn && status[t] == ST_COMMIT;
-        if (__ballot(com) == 0) continue;
+        const uint64_t cm = __ballot(com);
+        if (MODE & EX_COMMIT) {
+            if (commit_out && t < n_txn) commit_out[t] = com ? 1u : 0u;
+            if (lane == 0) ncom += (unsigned long long)__popcll(cm);
+        }
+        if (cm == 0 || !rows) continue;
         const uint32_t a0 = com ? tb_start[t] : 0u;
         const uint32_t len = com ? tb_end[t] - a0 : 0u;
         uint32_t incl = len;  // inclusive prefix of the lengths over the wave
@@ -1089,30 +1099,33 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
     if (lane == 0) {
         part[0][wave] = dig;
         part[1][wave] = wcnt;
+        part[2][wave] = ncom;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long d = part[0][0] + part[0][1] + part[0][2] + part[0][3];
         const unsigned long long w = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+        const unsigned long long n = part[2][0] + part[2][1] + part[2][2] + part[2][3];
         if (d) atomicAdd(&my_slot(ctr).read_digest, d);
         if (w) atomicAdd(&my_slot(ctr).write_cnt, w);
+        if ((MODE & EX_COMMIT) && n) atomicAdd(&my_slot(ctr).committed, (uint32_t)n);
     }
 }
 
 void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
-                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm) {
+                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit) {
     if (n_txn == 0) return;
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
-        k_exec_txn<EX_READS | EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn,
-                                                                  status, f0, pkey, ctr, rm);
+        k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn,
+                                                                              status, f0, pkey, ctr, rm, d_commit);
     } else {
-        k_exec_txn<EX_READS><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                       pkey, ctr, rm);
+        k_exec_txn<EX_READS | EX_COMMIT><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
+                                                                   pkey, ctr, rm, d_commit);
         k_exec_txn<EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                        pkey, ctr, rm);
+                                                        pkey, ctr, rm, nullptr);
     }
 }
 

@@ -1144,9 +1144,11 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         if (c->cfg.cc_alg == DV_CALVIN)
             launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey, c->ctr,
                         rm);
-        else
+        else {  // (the commit bytes and count too)
             launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
-                            c->cfg.cc_alg != DV_OCC, c->ctr, rm);
+                            c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit);
+            return;
+        }
     }
     launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
 }
