@@ -132,33 +132,51 @@ def cpu_baseline(epochs, rows, cc_name, seconds):
 def cpu_baseline_mt(epochs, rows, seconds):
     """a Deneva-style multi-threaded NO_WAIT engine
     (oracle/mt_engine.c: per-row lock words, index probe, run_ycsb_1, no
-    retry) on every host core the box gives this job -- its CPU share for
-    one GPU, CPU_SHARE threads; nproc reports the whole machine -- same
-    epochs.  Its aborts depend on the interleaving (THREAD_CNT txns in
+    retry) on the same epochs.  The headline figure uses the box's CPU share
+    for one GPU, CPU_SHARE threads: the GPU box gives one GPU's job 16 host
+    cores and asks that worker pools stay within them, while nproc reports
+    the whole machine (256).  Beside it the same engine at 1 and 4 threads
+    (its scaling), and the CPU_SHARE rate scaled to every core nproc counts,
+    labelled as an extrapolation (linear in threads: an upper bound, not a
+    measurement).  Its aborts depend on the interleaving (THREAD_CNT txns in
     flight), not the E-schedule's 1M; a throughput reference only."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = max(1, min(CPU_SHARE, avail))
     tab = O.YcsbTable(rows)
-    f0 = tab.f0.copy()
-    lock = np.zeros(rows, np.uint32)
-    committed = txns = 0
-    t0 = time.perf_counter()
-    i = 0
-    while True:
-        e = epochs[i % len(epochs)]
-        c, _ = O.mt_epoch_run(tab.ix, f0, lock, e.n_txn, e.txn_begin, e.keys, e.types, threads)
-        committed += c
-        txns += e.n_txn
-        i += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": committed / el, "unit": "committed txns/s", "cores": threads, "kind": "port",
-            "nproc": os.cpu_count(), "affinity": avail,
+
+    def run(threads, secs):
+        f0 = tab.f0.copy()
+        lock = np.zeros(rows, np.uint32)
+        committed = txns = 0
+        t0 = time.perf_counter()
+        i = 0
+        while True:
+            e = epochs[i % len(epochs)]
+            c, _ = O.mt_epoch_run(tab.ix, f0, lock, e.n_txn, e.txn_begin, e.keys, e.types, threads)
+            committed += c
+            txns += e.n_txn
+            i += 1
+            el = time.perf_counter() - t0
+            if el >= secs:
+                return committed / el, txns, i, el, committed
+
+    threads = max(1, min(CPU_SHARE, avail))
+    v, txns, i, el, committed = run(threads, seconds)
+    scaling = {}
+    for t in (1, 4):
+        if t < threads:
+            scaling[str(t)] = run(t, min(3.0, seconds))[0]
+    scaling[str(threads)] = v
+    nproc = os.cpu_count() or threads
+    return {"value": v, "unit": "committed txns/s", "cores": threads, "kind": "port",
+            "nproc": nproc, "affinity": avail, "threads_scaling": scaling,
+            "all_cores_extrapolated": {"value": v * nproc / threads, "cores": nproc,
+                                       "note": f"{threads}-thread rate x {nproc}/{threads}, linear: an upper bound, "
+                                               "not measured (the box asks one GPU's job to keep its worker "
+                                               f"pools within its {CPU_SHARE}-core share)"},
             "sample": f"Deneva-style multi-threaded NO_WAIT engine (per-row lock words, {threads} "
-                      f"threads = the box's CPU share for one GPU; nproc {os.cpu_count()}, affinity {avail}) "
+                      f"threads = the box's CPU share for one GPU; nproc {nproc}, affinity {avail}) "
                       f"over {i} epoch(s) of {epochs[0].n_txn} txns of the bench workload, "
                       f"{txns} txns in {el:.1f} s, abort rate {1 - committed / max(1, txns):.3f}; "
                       "restatement of the reference CC, not the reference binary"}
@@ -398,74 +416,140 @@ def pmc_traffic(a, cc_name, world, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
-def roofline(kstats, a, cc_name, world, txn_div=1):
-    """The largest single launch of the epoch, the index probe (k_probe):
-    algorithmic bytes per launch -- SURVEY.md 8(d)'s probe traffic, PROBE_ACC
-    B per access (key 8 + type 1 + txn id 4 read, row word 4 written; the
-    YCSB table is dense, every key below rows x P exists, so the key check is
-    a range check) plus PROBE_TXN B per txn (access range 8 + length 1
-    written); the prefix's sort keys (8 B for ~1.6 % of the accesses) are not
-    counted -- over its average duration from the launch's own dispatch
-    timestamps on the engine's stream.  The decision stage's two asynchronous
-    launches take longer in sum but are bound by hand-off latency, not bytes
-    (DESIGN.md); k_round_pass is reported beside it."""
-    launches = sum(1 for s in kstats if s.ms_probe_kernel > 0)
-    avg_ms = sum(s.ms_probe_kernel for s in kstats) / max(1, launches)
-    # (epoch groups: n_txn counts the group, n_acc the epoch this rank decided)
-    bytes_per_launch = float(np.mean([PROBE_ACC * s.n_acc + PROBE_TXN * s.n_txn // txn_div for s in kstats]))
-    achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-    traffic, src = pmc_traffic(a, cc_name, world, "k_probe")
-    p_launches = sum(s.pass_launches for s in kstats)
-    p_avg = sum(s.ms_pass for s in kstats) / max(1, p_launches)
-    p_bytes = SCAN_BYTES * sum(s.pass_live for s in kstats) / max(1, p_launches)
-    p_ach = p_bytes / (p_avg * 1e-3) / 1e9 if p_avg > 0 else 0.0
-    p_traffic, _ = pmc_traffic(a, cc_name, world, "k_round_pass")
-    return {
-        "kernel": "k_probe", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-        "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic, "bytes_per_launch": bytes_per_launch,
-        "avg_launch_ms": avg_ms, "launches": launches,
-        "algorithmic_bytes": f"{PROBE_ACC} B per access + {PROBE_TXN} B per txn (SURVEY.md 8d probe: key 8, type 1, "
-                             "txn id 4 read, row word 4 written -- a dense YCSB table's key check is arithmetic, "
-                             "no index bytes; access ranges per txn)",
-        "traffic_source": src,
-        "timed_by": ("dispatch timestamps of every probe launch in the timed region"
-                     if a.timing != "off" else
-                     f"dispatch timestamps of the probe launch over {len(kstats)} epochs run "
-                     "right after the timed region (same epochs, same stream)"),
-        "k_round_pass": {"achieved": p_ach, "frac": p_ach / HBM_PEAK_GBPS, "avg_launch_ms": p_avg,
-                         "launches": p_launches, "bytes_per_launch": p_bytes, "traffic": p_traffic,
-                         "algorithmic_bytes": f"{SCAN_BYTES} B per live access per launch (SURVEY.md 8d)"},
+def epoch_bytes(st, rows, R):
+    """SURVEY.md 8(d) algorithmic bytes of each kernel for ONE epoch with the
+    stats `st` (mean over the profiled epochs), counted on what the launches of
+    that kernel actually processed: {kernel: (bytes per epoch, what is counted)}.
+    A stage's bytes are counted once per launch that reads them (a sort pass
+    reads and writes its keys; the decision launches read each live access
+    once, rounds being overhead).  Kernels not listed move only counters."""
+    n_acc, n_txn = st["n_acc"], st["n_txn"]
+    ka, kb = st["prefix_acc"], st["surv_acc"]          # keys the prefix's / survivors' sorts order
+    ta, tb = st["prefix_txn"], st["surv_txn"]
+    keys = (ka + kb) if (ka or kb) else n_acc           # (no prefix: the whole epoch is sorted)
+    stage_txn = (ta + tb) if (ka or kb) else n_txn
+    passes = max(1, st["sort_passes"])
+    tiles = sum((k + 4095) // 4096 for k in ((ka, kb) if (ka or kb) else (n_acc,)))
+    later = max(0, n_acc - ka)
+    per_txn = n_acc / max(1, n_txn)
+    out = {
+        "k_epoch_clear": (10 * n_txn + (rows // 4 + (1 << 17) if ka else 0),
+                          "per txn: status 1 + access range 8 + length 1 written; prefix epochs: the 2-bit "
+                          "row-state bitmap + Bloom filter zeroed"),
+        "k_probe": (PROBE_ACC * n_acc + PROBE_TXN * n_txn + 8 * ka,
+                    f"{PROBE_ACC} B per access (key 8, type 1, txn id 4 read; row word 4 written; a dense YCSB "
+                    f"table's key check is arithmetic) + {PROBE_TXN} B per txn (access range, length) + 8 B per "
+                    "prefix sort key written"),
+        "k_radix_hist": (8 * passes * keys, "8 B per key read, per pass"),
+        "k_radix_scan": (8 * 256 * passes * tiles, "per pass: 256 digit counts per 4096-key tile, read + written"),
+        "k_radix_scatter": (16 * passes * keys, "per pass: 8 B per key read + 8 B written"),
+        "k_round_pass": (SCAN_BYTES * st["pass_live"], f"{SCAN_BYTES} B per live access read (scan 8 + verdict 1)"),
+        "k_round_settle": (17 * stage_txn, "per txn of the stage: length 1, status 1 + 1, verdict bytes 10, "
+                                           "fact word 4"),
+        "k_round_async": (SCAN_BYTES * st["async_live"],
+                          f"{SCAN_BYTES} B per live access entering the launch (scan 8 + verdict 1), once: "
+                          "its iterations are rounds, overhead (SURVEY.md 8d)"),
+        "k_round_finalize": (5 * stage_txn, "per txn of the stage: fact word 4 read, status 1 written"),
+        "k_prefix_mark": (9 * ta + 4 * ka * 0, "per prefix txn: status 1 + access range 8 (lower bound: the "
+                                              "committed txns' rows are not counted)"),
+        "k_kill": (4 * later + later // 8, "per access after the prefix: row word 4 read + kill bit written"),
+        "k_kill_compact": (9 * max(0, n_txn - ta) + later // 8 + 12 * kb + 6 * tb,
+                           "per later txn: access range 8 + status 1; kill bits; per survivor access: row word 4 "
+                           "read + sort key 8 written; per survivor: map 4 + length 1 + status 1"),
+        "k_sub_scatter_back": (6 * tb, "per survivor: map 4 + status 1 read, status 1 written"),
+        "k_exec_txn": (10 * n_txn + int(12 * st["committed"] * per_txn),
+                       "per txn: status 1 + access range 8 + commit byte 1; per committed access: row word 4 + "
+                       "the 8-byte F0 field"),
     }
+    return out
 
 
-def measure_legs(a, eng, step, nxt, stats):
-    """Event-timed legs after the timed region, on the same epochs and stream:
-    event timing adds launch latency (dispatch timestamps ~6 us per timed
-    launch, stage markers more), so the timed region runs without it unless
-    --timing asks.  Returns (kernel-timed stats, stage-timed stats)."""
-    if a.timing == "off":
-        eng.set_timing("kernel")
-        kstats = [step(nxt + i) for i in range(a.steps)]
-        nxt += a.steps
+def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1):
+    """Per-kernel table of the profiled epochs: launches per epoch, average
+    launch time (its own dispatch timestamps), share of the epoch's kernel
+    time, algorithmic bytes per launch (epoch_bytes), achieved GB/s and
+    fraction of the HBM peak, and PMC traffic per launch where profiles/ holds
+    it for these sources."""
+    ep = max(1, len(sts))
+    mean = {k: float(np.mean([getattr(s, k) for s in sts])) for k in
+            ("n_acc", "n_txn", "prefix_acc", "surv_acc", "prefix_txn", "surv_txn", "pass_live", "async_live",
+             "committed", "sort_passes")}
+    mean["n_txn"] /= txn_div  # (epoch groups: the stats count the group's txns, n_acc the decided epoch's)
+    mean["committed"] /= txn_div
+    eb = epoch_bytes(mean, rows, R)
+    total_ms = sum(ms for _, ms in ktimes.values())
+    rows_out = []
+    for name, (launches, ms) in sorted(ktimes.items(), key=lambda kv: -kv[1][1]):
+        lpe = launches / ep
+        avg = ms / max(1, launches)
+        r = {"kernel": name, "launches_per_epoch": lpe, "avg_us": avg * 1e3,
+             "us_per_epoch": ms / ep * 1e3, "share": ms / total_ms if total_ms else 0.0}
+        if name in eb and lpe > 0:
+            b = eb[name][0] / lpe
+            ach = b / (avg * 1e-3) / 1e9 if avg > 0 else 0.0
+            r.update({"bytes_per_launch": b, "achieved_GBps": ach, "frac": ach / HBM_PEAK_GBPS,
+                      "bytes": eb[name][1]})
+            tr, src = pmc_traffic(a, cc_name, world, name)
+            r["traffic"] = tr
+            if tr is None:
+                r["traffic_note"] = src
+        rows_out.append(r)
+    return rows_out, total_ms / ep * 1e3
+
+
+def roofline(table, epochs, a):
+    """`roofline` of the line: the kernel with the largest share of the
+    epoch's kernel time (its algorithmic bytes per launch over its average
+    launch time), with the index probe beside it."""
+    def entry(r):
+        return {"kernel": r["kernel"], "bound": "hbm", "achieved": r.get("achieved_GBps", 0.0),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": r.get("frac", 0.0), "traffic": r.get("traffic"),
+                "bytes_per_launch": r.get("bytes_per_launch"), "avg_launch_ms": r["avg_us"] * 1e-3,
+                "launches_per_epoch": r["launches_per_epoch"], "share_of_epoch": r["share"],
+                "algorithmic_bytes": r.get("bytes")}
+    timed = [r for r in table if "bytes_per_launch" in r]
+    if not timed:
+        return {"kernel": None, "bound": "hbm", "achieved": 0.0, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": 0.0, "traffic": None}
+    top = max(timed, key=lambda r: r["share"])
+    out = entry(top)
+    out["timed_by"] = (f"each launch's own dispatch timestamps (hipExtLaunchKernelGGL events, "
+                       f"dv_kernel_times) over {epochs} epochs run right after the timed region, same epochs "
+                       "and stream, as the timed region runs them")
+    probe = next((r for r in table if r["kernel"] in ("k_probe", "k_probe_hist")), None)
+    if probe is not None and probe is not top:
+        out["k_probe"] = entry(probe)
+    return out
+
+
+def measure_legs(a, eng, step, nxt, stats, batch=None):
+    """Legs after the timed region, on the same epochs and stream: per-launch
+    kernel timing (every launch dispatched with its own timestamps; it adds
+    launch latency, so the timed region runs without it), then per-stage
+    events.  Returns (profiled stats, stage-timed stats, kernel times)."""
+    eng.set_timing(False, profile=True)
+    eng.kernel_times(reset=True)
+    if batch is not None:
+        pstats = batch(nxt, a.steps)
     else:
-        kstats = stats
+        pstats = [step(nxt + i) for i in range(a.steps)]
+    ktimes = eng.kernel_times(reset=True)
+    eng.set_timing(False)
+    nxt += a.steps
     if a.timing != "full":
         eng.set_timing(True)
         sstats = [step(nxt + i) for i in range(min(a.steps, 5))]
     else:
         sstats = stats
     eng.set_timing(False)
-    return kstats, sstats
+    return pstats, sstats, ktimes
 
 
-def stage_summary(stats, sstats, kstats, el, R):
+def stage_summary(stats, sstats, table, el, R):
     committed = sum(s.committed for s in stats)
     txns = sum(s.n_txn for s in stats)
     acc_local = sum(s.n_acc for s in stats)
-    sc_ms = [s.ms_scatter / max(1, s.scatter_launches) for s in kstats if s.scatter_launches]
-    sc_avg = float(np.mean(sc_ms)) if sc_ms else 0.0
     n_acc_step = acc_local / max(1, len(stats))
-    scatter_gbps = n_acc_step * 16 / (sc_avg * 1e-3) / 1e9 if sc_avg > 0 else 0.0
     epoch_gbps = (txns / el) * (BYTES_PER_ACCESS * R + 1) / 1e9
     stage = {k: float(np.mean([getattr(s, k) for s in sstats]))
              for k in ("ms_probe", "ms_sort", "ms_decide", "ms_exec", "ms_total")}
@@ -473,9 +557,7 @@ def stage_summary(stats, sstats, kstats, el, R):
     # over the whole decide stage (rounds are overhead, not algorithmic)
     dec = stage["ms_decide"]
     scan_stage_gbps = n_acc_step * SCAN_BYTES / (dec * 1e-3) / 1e9 if dec > 0 else 0.0
-    return {
-        "sort": {"kernel": "k_radix_scatter", "avg_launch_ms": sc_avg, "achieved_GBps": scatter_gbps,
-                 "keys_per_s": n_acc_step / (sc_avg * 1e-3) if sc_avg > 0 else 0.0},
+    out = {
         "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1, "achieved_GBps": epoch_gbps,
                            "frac": epoch_gbps / HBM_PEAK_GBPS},
         "decide_stage_roofline": {"bytes": f"{SCAN_BYTES} B per access of this partition, counted once "
@@ -489,6 +571,14 @@ def stage_summary(stats, sstats, kstats, el, R):
                         "yields": int(sum(s.async_yields for s in stats)), "epochs": len(stats)},
         "stage_ms_mean": stage,
     }
+    sc = next((r for r in table if r["kernel"] == "k_radix_scatter" and "bytes_per_launch" in r), None)
+    if sc is not None:  # keys each scatter launch actually ordered (the prefix's and the survivors' sorts)
+        keys = sc["bytes_per_launch"] / 16
+        out["sort"] = {"kernel": "k_radix_scatter", "avg_launch_ms": sc["avg_us"] * 1e-3,
+                       "keys_per_launch": keys, "keys_per_s": keys / (sc["avg_us"] * 1e-6),
+                       "achieved_GBps": sc["achieved_GBps"], "frac": sc["frac"],
+                       "bytes": "16 B per key per pass (read 8 + write 8)"}
+    return out
 
 
 class PartitionedBench:
@@ -662,7 +752,8 @@ def main():
     # dv_epoch_group_run_batch (epoch groups); the other protocols step
     pipelined = not a.no_pipeline and (not part or a.protocol == "group")
     stats, el = timed(step, 0, a.warmup, a.steps, world, batch if pipelined else None)
-    kstats, sstats = measure_legs(a, eng, step, a.warmup + a.steps, stats)
+    pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats, batch if pipelined else None)
+    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"
     out = {
@@ -695,12 +786,14 @@ def main():
                           2: "replicated"}[a.part_mode] if part else "single GPU"),
             "distinct_epochs": n_epochs,
         },
-        "roofline": roofline(kstats, a, cc_name, world, world if group else 1),
+        "roofline": roofline(table, len(pstats), a),
         "timing_in_timed_region": a.timing,
         "gen_seconds": t_gen,
         "src_hash": dvcc._lib.source_hash(),
     }
-    out.update(stage_summary(stats, sstats, kstats, el, R))
+    out.update(stage_summary(stats, sstats, table, el, R))
+    out["kernels"] = table
+    out["kernel_us_per_epoch"] = kus
     if not part:
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}

@@ -145,10 +145,10 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
         (void)hipMemsetAsync(tot, 0, 3 * sizeof(uint32_t), s);
         return;
     }
-    k_carry_count<<<nb, kBlock, 0, s>>>(status, tb_start, tb_end, n_txn, bt, ba);
-    k_carry_scan<<<1, kBlock, 0, s>>>(bt, ba, nb);
-    k_carry_total<<<1, 64, 0, s>>>(status, n_txn, bt, nb, tot);
-    k_carry_copy<<<nb, kBlock, 0, s>>>(status, tb_start, tb_end, n_txn, bt, ba, max_txn, keys, types, tables,
+    DV_LAUNCH(k_carry_count, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba);
+    DV_LAUNCH(k_carry_scan, 1, kBlock, 0, s, bt, ba, nb);
+    DV_LAUNCH(k_carry_total, 1, 64, 0, s, status, n_txn, bt, nb, tot);
+    DV_LAUNCH(k_carry_copy, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba, max_txn, keys, types, tables,
                                        okeys, otypes, otxn, otables, tot);
 }
 

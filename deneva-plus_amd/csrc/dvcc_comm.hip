@@ -183,17 +183,26 @@ __global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restri
     }
 }
 
+// A batch's txn id at or past txns_per_rank would become another origin's
+// global id (rank * tpr + id) and merge two txns: it is sent as an id past
+// every epoch (kBadTxn), which the decider's probe rejects (ERRB_TXN, an
+// input error voted out on every rank before anything executes).
+constexpr uint32_t kBadTxn = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t global_txn(uint32_t t, uint32_t tpr, uint32_t base) {
+    return t < tpr ? t + base : kBadTxn;
+}
+
 // epoch groups: row id | wr << 31 and the global txn id, 8 B per access
 __global__ __launch_bounds__(kBlock) void k_group_pack(const uint64_t *__restrict__ keys,
                                                        const uint8_t *__restrict__ types,
                                                        const uint32_t *__restrict__ txn, uint64_t n,
-                                                       uint32_t txn_base, uint32_t *__restrict__ k32,
+                                                       uint32_t tpr, uint32_t txn_base, uint32_t *__restrict__ k32,
                                                        uint32_t *__restrict__ t32) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = keys[i];
         // a key past 31 bits saturates and fails the decider's range check
         k32[i] = ((k >> 31) ? 0x7FFFFFFFu : (uint32_t)k) | (types[i] == DV_WR ? 0x80000000u : 0u);
-        t32[i] = txn[i] + txn_base;
+        t32[i] = global_txn(txn[i], tpr, txn_base);
     }
 }
 
@@ -310,12 +319,12 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
 __global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
                                                      const uint8_t *__restrict__ types,
                                                      const uint32_t *__restrict__ txn, uint64_t n,
-                                                     uint32_t txn_base, uint32_t *__restrict__ k32,
+                                                     uint32_t tpr, uint32_t txn_base, uint32_t *__restrict__ k32,
                                                      uint32_t *__restrict__ t32, uint8_t *__restrict__ ty) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = keys[i];
         k32[i] = (k >> 32) ? 0xFFFFFFFFu : (uint32_t)k;
-        t32[i] = txn[i] + txn_base;
+        t32[i] = global_txn(txn[i], tpr, txn_base);
         ty[i] = types[i];
     }
 }
@@ -584,17 +593,17 @@ __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint
 void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
                       const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr) {
     const RouteSrc<0> src{tb_start, tb_end, acc_row, n_txn, nullptr, nullptr, nullptr, 0, status};
-    k_route_count<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
-    k_route_scan<<<ro.P, kBlock, 0, s>>>(ro);
-    k_route_scatter<0><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    DV_LAUNCH((k_route_count<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
+    DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
+    DV_LAUNCH((k_route_scatter<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
 
 void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs, const uint64_t *el,
                        const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr) {
     const RouteSrc<1> src{nullptr, nullptr, nullptr, 0, pairs, el, ew, n, status};
-    k_route_count<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
-    k_route_scan<<<ro.P, kBlock, 0, s>>>(ro);
-    k_route_scatter<1><<<kRouteBlocks, kBlock, 0, s>>>(src, ro, ctr);
+    DV_LAUNCH((k_route_count<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
+    DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
+    DV_LAUNCH((k_route_scatter<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
 
 // ---- in-process group: element-wise MAX of the P ranks' buffers
@@ -824,7 +833,7 @@ struct LocalXport final : Xport {
         for (int q = 0; q < g->P; q++) in.p[q] = reinterpret_cast<const T *>(g->slot[q].send);
         if (n) {
             const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
-            k_max_reduce<T><<<(uint32_t)blocks, kBlock, 0, s>>>(in, g->P, reinterpret_cast<T *>(scratch), n);
+            DV_LAUNCH((k_max_reduce<T>), (uint32_t)blocks, kBlock, 0, s, in, g->P, reinterpret_cast<T *>(scratch), n);
             CHK(hip_fail2(hipGetLastError(), "k_max_reduce"));
         }
         CHK(retire(s));
@@ -1015,7 +1024,7 @@ int mail_get(DvComm *m, hipStream_t s, const uint64_t *a, uint32_t na, const uin
              uint64_t *out64, uint32_t *out32, const uint64_t *c = nullptr, uint32_t nc = 0,
              uint64_t *outc = nullptr) {
     const unsigned long long want = ++m->mseq;
-    k_mail_out<<<1, kBlock, 0, s>>>(a, na, b, nb, c, nc, m->d_mail, want);
+    DV_LAUNCH(k_mail_out, 1, kBlock, 0, s, a, na, b, nb, c, nc, m->d_mail, want);
     CHK(hip_fail2(hipGetLastError(), "k_mail_out"));
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t i = 0;; i++) {
@@ -1045,7 +1054,7 @@ int put_words(hipStream_t s, const uint64_t *v64, uint32_t n64, uint64_t *d64, c
     a.d32 = d32;
     for (uint32_t i = 0; i < n64 && i < (uint32_t)kRadix + 8; i++) a.v64[i] = v64[i];
     for (uint32_t i = 0; i < n32 && i < 8u; i++) a.v32[i] = v32[i];
-    k_put_words<<<1, kBlock, 0, s>>>(a);
+    DV_LAUNCH(k_put_words, 1, kBlock, 0, s, a);
     return hip_fail2(hipGetLastError(), "k_put_words");
 }
 
@@ -1073,6 +1082,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
                home->n_txn > txns_per_rank || n_txn64 > cfg.max_txn || n_txn64 > m->txn_cap ||
                home->n_acc > m->acc_cap || !ctx_has_tables(c) || tpcc != (cfg.workload == DV_TPCC);
     if (tpcc && !bad) bad = home->n_acc && (!home->tables || !own || !args || !m->send_args);
+    if (!bad && home->ts && cfg.cc_alg == DV_WAIT_DIE) bad = true;  // (dvcc.h: partitioned epochs take no ts)
     const uint32_t n_txn = bad ? 0u : (uint32_t)n_txn64;
     const uint64_t n_home = bad ? 0 : home->n_acc;
     hipStream_t s = ctx_stream(c);
@@ -1105,8 +1115,8 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * m->acc_cap);
         uint8_t *ry = rb + 8 * m->acc_cap;
         if (n_home)
-            k_rep_pack<<<std::min<uint32_t>(nb * 16, 2048), kBlock, 0, s>>>(home->keys, home->types, home->acc_txn,
-                                                                             n_home, (uint32_t)m->rank * txns_per_rank,
+            DV_LAUNCH(k_rep_pack, std::min<uint32_t>(nb * 16, 2048), kBlock, 0, s, home->keys, home->types, home->acc_txn,
+                                                                             n_home, txns_per_rank, (uint32_t)m->rank * txns_per_rank,
                                                                              sk, st_, sy);
         CHK(hip_fail2(hipGetLastError(), "pack"));
         // one all-gather per array, parts padded to the longest batch; equal
@@ -1123,7 +1133,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         if (!equal) {
             uint32_t *ck = reinterpret_cast<uint32_t *>(m->keys), *ct = m->txn;
             const dim3 grid((uint32_t)std::min<uint64_t>((hmax + kBlock - 1) / kBlock, 1024), std::min<uint32_t>(P, 64));
-            k_rep_compact<<<grid, kBlock, 0, s>>>(rk, rt, ry, hmax, m->xcnt + P, P, ck, ct, m->types);
+            DV_LAUNCH(k_rep_compact, grid, kBlock, 0, s, rk, rt, ry, hmax, m->xcnt + P, P, ck, ct, m->types);
             CHK(hip_fail2(hipGetLastError(), "compact"));
             rk = ck;
             rt = ct;
@@ -1141,9 +1151,9 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     }
     // 3. the list protocol: split the batch by owner (a bad rank sends nothing)
     if (n_home) {
-        k_owner_count<<<nb, kBlock, 0, s>>>(home->keys, own, n_home, P, m->counts, nb, m->xvote);
-        k_owner_scan<<<P, kBlock, 0, s>>>(m->counts, nb, m->tot);
-        k_owner_scatter<<<nb, kBlock, 0, s>>>(home->keys, home->types, home->acc_txn, own,
+        DV_LAUNCH(k_owner_count, nb, kBlock, 0, s, home->keys, own, n_home, P, m->counts, nb, m->xvote);
+        DV_LAUNCH(k_owner_scan, P, kBlock, 0, s, m->counts, nb, m->tot);
+        DV_LAUNCH(k_owner_scatter, nb, kBlock, 0, s, home->keys, home->types, home->acc_txn, own,
                                              tpcc ? home->tables : nullptr, args, n_home, P,
                                              (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb, m->send,
                                              tpcc ? m->send_args : nullptr, m->xvote);
@@ -1157,7 +1167,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     for (uint32_t o = 0; o < P; o++) sendc[o] = tot[o];
     CHK(put_words(s, sendc.data(), P, m->xcnt, nullptr, 0, nullptr));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    k_recv_check<<<1, 64, 0, s>>>(m->xcnt + P, P, cap, m->xvote);
+    DV_LAUNCH(k_recv_check, 1, 64, 0, s, m->xcnt + P, P, cap, m->xvote);
     CHK(m->x->max_u32(m->xvote, 2, s));
     CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 2, recvc.data(), gvote));
     if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's owner bytes or capacity were bad
@@ -1279,7 +1289,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     uint32_t max_len = 0;
     for (uint32_t e = 0; e < P && !bad; e++) {
         const dv_epoch_dev &h = homes[e];
-        bad = h.n_txn > txns_per_rank || (h.n_acc && (!h.keys || !h.types || !h.acc_txn));
+        bad = h.n_txn > txns_per_rank || (h.n_acc && (!h.keys || !h.types || !h.acc_txn)) ||
+              (h.ts && cfg.cc_alg == DV_WAIT_DIE);
         n_send += h.n_acc;
         if (h.n_acc) max_len = std::max<uint32_t>(max_len, h.max_txn_acc ? h.max_txn_acc : kMaxPos);
     }
@@ -1305,7 +1316,10 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     // compact batches (k_group_pack_c) need the global row ids below 2^30
     rec[5] = capable && !m->wide && P <= kXMaxP && ctx_table0_rows(c) * P < (1ull << 30) ? 0u : 1u;
     for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
-    CHK(put_words(s, rec.data(), W, m->gs, nullptr, 0, nullptr));
+    // (and the compact pack's bad flag cleared for this group: a group that
+    // failed after setting it must not leave it to the next one)
+    const uint32_t zero = 0;
+    CHK(put_words(s, rec.data(), W, m->gs, &zero, 1, m->gbad));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     {
         // (with the previous group's execution digest, when it was deferred)
@@ -1359,8 +1373,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
             nmax = std::max(nmax, n);
         } else if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
-            k_group_pack<<<blocks, kBlock, 0, s>>>(homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                   (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
+            DV_LAUNCH(k_group_pack, blocks, kBlock, 0, s, homes[e].keys, homes[e].types, homes[e].acc_txn, n,
+                                                   txns_per_rank, (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
         }
         sc[e] = 4 * n;
         sd[e] = 4 * so;
@@ -1376,7 +1390,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     }
     if (compact && nmax) {
         const uint32_t bx = (uint32_t)std::min<uint64_t>((nmax + kBlock - 1) / kBlock, std::max(1u, 2048u / P));
-        k_group_pack_c<<<dim3(bx, P), kBlock, 0, s>>>(ps, sk, m->gbad);
+        DV_LAUNCH(k_group_pack_c, dim3(bx, P), kBlock, 0, s, ps, sk, m->gbad);
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
@@ -1389,8 +1403,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     if (compact && xtiles) {
         xs.eoff[P] = ro;
         xs.toff[P] = xtiles;
-        k_group_txn_count<<<xtiles, kBlock, 0, s>>>(rk, xs, m->gtc);
-        k_group_txn_ids<<<xtiles, kBlock, 0, s>>>(rk, xs, m->gtc, rt);
+        DV_LAUNCH(k_group_txn_count, xtiles, kBlock, 0, s, rk, xs, m->gtc);
+        DV_LAUNCH(k_group_txn_ids, xtiles, kBlock, 0, s, rk, xs, m->gtc, rt);
         CHK(hip_fail2(hipGetLastError(), "k_group_txn_ids"));
     }
 
@@ -1412,7 +1426,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    (or an owner whose receive area is too small) fails the group on
     //    every rank; committed txns; records per owner
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    k_route_words<<<1, 64, 0, s>>>(m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad);
+    DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad);
     CHK(hip_fail2(hipGetLastError(), "k_route_words"));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
@@ -1465,10 +1479,10 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 1024);
             if (fused) {
-                k_route_exec<3><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
+                DV_LAUNCH((k_route_exec<3>), blocks, kBlock, 0, s, recs + off, n, f0, pkey, m->xacc);
             } else {
-                k_route_exec<1><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
-                k_route_exec<2><<<blocks, kBlock, 0, s>>>(recs + off, n, f0, pkey, m->xacc);
+                DV_LAUNCH((k_route_exec<1>), blocks, kBlock, 0, s, recs + off, n, f0, pkey, m->xacc);
+                DV_LAUNCH((k_route_exec<2>), blocks, kBlock, 0, s, recs + off, n, f0, pkey, m->xacc);
             }
         }
         off += n;
@@ -1495,16 +1509,19 @@ extern "C" {
 
 int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st) {
+    KProfScope kps_(c);
     return run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
 }
 
 int dv_epoch_group_run(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st) {
+    KProfScope kps_(c);
     return run_group(c, homes, n_homes, txns_per_rank, d_commit, st);
 }
 
 int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_groups, uint32_t n_homes,
                              uint32_t txns_per_rank, uint8_t *const *d_commits, dv_stats *st) {
+    KProfScope kps_(c);
     GroupDefer dfr;
     for (uint32_t g = 0; g < n_groups; g++) {
         const int r = run_group(c, homes ? homes + (size_t)g * n_homes : nullptr, n_homes, txns_per_rank,
@@ -1525,6 +1542,7 @@ int dv_comm_set_mode(dv_ctx *c, int mode) {
 
 int dv_tpcc_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, const uint64_t *d_args, const uint8_t *d_owner,
                            uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
+    KProfScope kps_(c);
     return run_part(c, home, d_owner, d_args, true, txns_per_rank, d_commit, d_oid, st);
 }
 

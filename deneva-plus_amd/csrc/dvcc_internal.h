@@ -1,12 +1,56 @@
 // dvcc_internal.h -- shared declarations between the epoch runtime and the
 // gfx950 kernels.  Not part of the public ABI (see include/dvcc.h).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "dvcc.h"
 
 namespace dvcc {
+
+// ---- per-launch kernel timing (dv_kernel_times, DV_FLAG_KERNEL_PROFILE).
+// Every launch of the engine goes through DV_LAUNCH.  While the profile of
+// the context a C-ABI entry works for is on, that entry points tl_kprof at it
+// (this host thread only), and each launch is dispatched with its own start
+// and stop timestamps (hipExtLaunchKernelGGL events: no marker packets in the
+// stream); the entry reads them once its work has completed.
+struct KProf;
+extern thread_local KProf *tl_kprof;
+// a fresh event pair for one launch of `kernel` (both null when the pool is spent)
+void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1);
+// events the caller owns and records itself (the probe / scatter / pass
+// timing of dv_stats): the profile reads them too
+void kprof_add(const char *kernel, hipEvent_t e0, hipEvent_t e1);
+// every C-ABI entry that queues work opens one: points tl_kprof at the
+// context's profile while DV_FLAG_KERNEL_PROFILE is set, and when the
+// outermost scope closes reads the timestamps of the launches that completed
+class KProfScope {
+  public:
+    explicit KProfScope(dv_ctx *c);
+    ~KProfScope();
+    KProfScope(const KProfScope &) = delete;
+    KProfScope &operator=(const KProfScope &) = delete;
+
+  private:
+    KProf *prev_, *mine_;
+};
+#define DV_LAUNCH(kernel, grid, block, shm, stream, ...)                                                     \
+    do {                                                                                                     \
+        hipEvent_t dv_e0_ = nullptr, dv_e1_ = nullptr;                                                       \
+        if (::dvcc::tl_kprof) ::dvcc::kprof_events(#kernel, &dv_e0_, &dv_e1_);                              \
+        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), shm, stream, dv_e0_, dv_e1_, 0, __VA_ARGS__); \
+    } while (0)
+// the same with the caller's own events (may be null)
+#define DV_LAUNCH_EV(kernel, grid, block, shm, stream, ev0, ev1, ...)                                        \
+    do {                                                                                                     \
+        hipEvent_t dv_e0_ = (ev0), dv_e1_ = (ev1);                                                           \
+        if (::dvcc::tl_kprof) {                                                                              \
+            if (dv_e0_ && dv_e1_) ::dvcc::kprof_add(#kernel, dv_e0_, dv_e1_);                                \
+            else ::dvcc::kprof_events(#kernel, &dv_e0_, &dv_e1_);                                            \
+        }                                                                                                    \
+        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), shm, stream, dv_e0_, dv_e1_, 0, __VA_ARGS__); \
+    } while (0)
 
 constexpr int kBlock = 256;           // 4 waves of 64
 constexpr int kIPT = 16;              // items per thread in the radix kernels
@@ -80,6 +124,7 @@ struct Counters {
     uint32_t a_halt;          // prefix-kill: the prefix's rounds halted (yield / decline), nothing after ran
     uint32_t a_rounds;        // prefix-kill: rounds the prefix's decisions took (k_prefix_mark)
     unsigned long long pass_live;  // live accesses every k_round_pass of the epoch read, summed
+    unsigned long long async_live; // live accesses entering every asynchronous launch that ran, summed
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
@@ -186,9 +231,7 @@ __device__ __forceinline__ uint64_t key_split(const TableDesc &t, uint64_t key, 
 // implicit-row direct map: does bucket bk hold the key of tag `tag`?
 __device__ inline bool direct_holds(const TableDesc &t, uint64_t bk, uint32_t tag, uint64_t key) {
     if (t.dense) return tag == t.htag;
-#ifndef DVCC_NO_HOME_BITS
     if (t.hbits != nullptr && tag == t.htag) return (t.hbits[bk >> 5] >> (bk & 31)) & 1u;
-#endif
     const uint32_t tg = t.ktag[bk];
     return tg != kTagWide ? tg == tag : t.pkey[bk] == key;
 }
@@ -200,14 +243,15 @@ struct Tables {
 
 // error bits recorded by kernels
 enum : uint32_t {
-    ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16, ERRB_BIG = 32
+    ERRB_KEY = 1, ERRB_DUP = 2, ERRB_TXN = 4, ERRB_TABLE = 8, ERRB_SPIN = 16, ERRB_BIG = 32,
+    ERRB_TS = 64  // WAIT_DIE timestamps that do not rise strictly in sequence order
 };
 // errors in the epoch's input, all found by the probe (or the host-record
 // check before it): once one is set -- on this partition or, for partitioned
 // epochs, on any (Counters::peer_err) -- the decision rounds are no-ops and
 // no execution kernel touches the tables, so a rejected epoch leaves them as
 // they were
-constexpr uint32_t ERRB_INPUT = ERRB_KEY | ERRB_DUP | ERRB_TXN | ERRB_TABLE | ERRB_BIG;
+constexpr uint32_t ERRB_INPUT = ERRB_KEY | ERRB_DUP | ERRB_TXN | ERRB_TABLE | ERRB_BIG | ERRB_TS;
 __device__ __forceinline__ uint32_t input_err(const Counters *ctr) {
     return (ctr->err | ctr->peer_err) & ERRB_INPUT;
 }
@@ -226,7 +270,8 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr);
+                  hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr,
+                  const uint64_t *ts = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),

@@ -55,12 +55,7 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
     const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
     bool found = false;
     if (t.pkey != nullptr) {                  // direct map, local row = bucket (key tags)
-#ifdef DVCC_CAL_NO_GATHER  // PMC calibration build only (tools/gpu_prof.sh): the streams without the gather
-        row = bk;
-        found = tag != kTagWide + 1;
-#else
         if (direct_holds(t, bk, tag, key)) { row = bk; found = true; }
-#endif
     } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
         const IxEntry e = t.ix[bk];
         if (e.key == key) { row = e.row; found = true; }
@@ -99,7 +94,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                                                   uint8_t *__restrict__ tlen,
                                                   uint32_t *__restrict__ acc_row, Counters *ctr,
                                                   uint32_t *__restrict__ counts, uint32_t ntiles,
-                                                  uint32_t pair_limit) {
+                                                  uint32_t pair_limit, const uint64_t *__restrict__ ts) {
     // The first radix pass's histogram (digit = row bits [0, 8)) is counted
     // here, per 4096-access sort tile, so the sort skips that k_radix_hist
     // launch and its 8-byte-per-access re-read of the pairs.
@@ -162,7 +157,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 tb[j] = ok && tables ? tables[i0 + j] : 0u;
             }
         }
-        bool miss = false;
+        bool miss = false, ts_bad = false;
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             row[j] = 0;
@@ -199,7 +194,6 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         // the wave's first run may have begun before the wave: its start, found
         // 64 earlier accesses per step by the whole wave (one load, a ballot)
         uint32_t carry = 0;
-#ifndef DVCC_EXP_NO_LOOKBACK
         if (wave0 > 0 && wave0 < n) {  // (wave-uniform)
             const uint32_t t0 = __shfl(txn[0], 0, 64);
             for (uint64_t base = wave0;; base -= 64) {
@@ -212,7 +206,6 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 }
             }
         }
-#endif
         if (ex == 0) ex = carry;
         const uint32_t nxt_lane = __shfl_down(txn[0], 1, 64);
         const uint64_t in_last = i0 + kPV;
@@ -236,17 +229,20 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             if (big) set_err(ctr, ERRB_BIG);
             const uint32_t t = txn[j] < n_txn ? txn[j] : 0u;
             out[j] = pair_pack(row[j], t, big ? 0u : pos, wr[j]);
-#ifndef DVCC_EXP_NO_TB  // (measurement builds only: tools/exp_variant.sh)
             if (txn[j] < n_txn) {
-                if (pos == 0) tb_start[t] = (uint32_t)i;
+                if (pos == 0) {
+                    tb_start[t] = (uint32_t)i;
+                    // WAIT_DIE: owners must be older than every later txn
+                    if (ts && t > 0 && ts[t] <= ts[t - 1]) ts_bad = true;
+                }
                 const uint32_t nt = j + 1 < kPV ? txn[j + 1] : nxt_last;
                 if (i + 1 == n || nt != txn[j]) {
                     tb_end[t] = (uint32_t)(i + 1);
                     if (tlen) tlen[t] = (uint8_t)(big ? (1u << slog) : pos + 1);
                 }
             }
-#endif
         }
+        if (ts_bad) set_err(ctr, ERRB_TS);
         if (acc_row) {
             uint32_t ar[kPV];
 #pragma unroll
@@ -328,9 +324,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t slog, uint64_t *__restrict__ pairs,
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
-                                                  Counters *ctr, uint32_t pair_limit) {
+                                                  Counters *ctr, uint32_t pair_limit, const uint64_t *__restrict__ ts) {
     probe_body<false>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                      ctr, nullptr, 0, pair_limit);
+                      ctr, nullptr, 0, pair_limit, ts);
 }
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     Tables tabs, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ keys32,
@@ -338,16 +334,16 @@ __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     const uint32_t *__restrict__ acc_txn, const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
     uint32_t slog, uint64_t *__restrict__ pairs, uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
     uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
-    uint32_t ntiles) {
+    uint32_t ntiles, const uint64_t *__restrict__ ts) {
     probe_body<true>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                     ctr, counts, ntiles, n_txn);
+                     ctr, counts, ntiles, n_txn, ts);
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32) {
+                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
     if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
@@ -355,13 +351,13 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     // (ev0 / ev1: the launch's own dispatch timestamps, no extra packets)
     if (counts)
-        hipExtLaunchKernelGGL(k_probe_hist, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, keys32, types,
+        DV_LAUNCH_EV(k_probe_hist, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types,
                               acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              counts, ntiles);
+                              counts, ntiles, ts);
     else
-        hipExtLaunchKernelGGL(k_probe, dim3(blocks), dim3(kBlock), 0, s, ev0, ev1, 0, tabs, keys, keys32, types, acc_txn,
+        DV_LAUNCH_EV(k_probe, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
                               tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              pair_limit < n_txn ? pair_limit : n_txn);
+                              pair_limit < n_txn ? pair_limit : n_txn, ts);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -655,9 +651,9 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__re
 template <int W>
 void wide_pass(hipStream_t s, const uint64_t *in, uint64_t *out, uint64_t n, int shift, uint32_t *counts,
                uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1) {
-    k_radix_hist_w<W><<<nb, kBlock, 0, s>>>(in, n, shift, counts, nb, n_dev);
-    k_radix_scan<<<1u << W, kBlock, 0, s>>>(counts, nb, digit_tot, n_dev);
-    hipExtLaunchKernelGGL(k_radix_scatter_w<W>, dim3(nb), dim3(kBlock), 0, s, e0, e1, 0, in, out, n, shift,
+    DV_LAUNCH((k_radix_hist_w<W>), nb, kBlock, 0, s, in, n, shift, counts, nb, n_dev);
+    DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev);
+    DV_LAUNCH_EV((k_radix_scatter_w<W>), nb, kBlock, 0, s, e0, e1, in, out, n, shift,
                           (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
 }
 
@@ -680,12 +676,10 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
     }
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        if (pass > 0 || !hist0_done) k_radix_hist<<<nb, kBlock, 0, s>>>(pairs[cur], n, shift, counts, nb, n_dev);
-        k_radix_scan<<<kRadix, kBlock, 0, s>>>(counts, nb, digit_tot, n_dev);
+        if (pass > 0 || !hist0_done) DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
+        DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev);
         // timing: events recorded by the dispatch itself (no extra packets)
-        hipExtLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(kBlock), 0, s,
-                              scatter_ev ? scatter_ev[2 * pass] : nullptr,
-                              scatter_ev ? scatter_ev[2 * pass + 1] : nullptr, 0,
+        DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, scatter_ev ? scatter_ev[2 * pass] : nullptr, scatter_ev ? scatter_ev[2 * pass + 1] : nullptr,
                               (const uint64_t *)pairs[cur], pairs[cur ^ 1], n, shift,
                               (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
         cur ^= 1;
@@ -775,7 +769,7 @@ void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int ca
     if (n == 0) return;
     uint64_t blocks = (n + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     if (blocks > 4096) blocks = 4096;
-    k_seg_prepare<<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, n, calvin, tb_start, el, ctr);
+    DV_LAUNCH(k_seg_prepare, (uint32_t)blocks, kBlock, 0, s, pairs, n, calvin, tb_start, el, ctr);
 }
 
 // ------------------------------------------------------- Calvin grants
@@ -865,9 +859,9 @@ void calvin_grant(hipStream_t s, const uint64_t *el, uint64_t n, uint32_t *grant
                   uint64_t *desc, uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
     if (n == 0) return;
     const uint32_t nb = (uint32_t)((n + kRTile - 1) / kRTile);
-    k_calvin_pass<<<nb, kBlock, 0, s>>>(el, (uint32_t)n, grant_out, ew, desc, tile_ctr, tag, ctr);
+    DV_LAUNCH(k_calvin_pass, nb, kBlock, 0, s, el, (uint32_t)n, grant_out, ew, desc, tile_ctr, tag, ctr);
     const uint64_t fb = (n + kBlock - 1) / kBlock;
-    k_calvin_dup_fix<<<(uint32_t)(fb > 1024 ? 1024 : fb), kBlock, 0, s>>>(el, n, ew, ctr);
+    DV_LAUNCH(k_calvin_dup_fix, (uint32_t)(fb > 1024 ? 1024 : fb), kBlock, 0, s, el, n, ew, ctr);
 }
 
 // ---------------------------------------------------------------- status
@@ -935,7 +929,7 @@ __global__ __launch_bounds__(kBlock) void k_ctr_out(const Counters *__restrict__
 
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
                     unsigned long long seq) {
-    k_ctr_out<<<1, kBlock, 0, s>>>(ctr, hctr, hseq, seq);
+    DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq);
 }
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
@@ -945,7 +939,7 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
-    k_epoch_clear<<<g, kBlock, 0, s>>>(status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
+    DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
                                        gate ? 1 : 0, hctr, hseq, seq);
 }
@@ -1015,8 +1009,8 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
     if (n == 0) return;
     uint64_t blocks = (n + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     if (blocks > 2048) blocks = 2048;
-    k_exec<false><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr, rm);
-    k_exec<true><<<(uint32_t)blocks, kBlock, 0, s>>>(pairs, el, ew, n, status, f0, pkey, ctr, rm);
+    DV_LAUNCH((k_exec<false>), (uint32_t)blocks, kBlock, 0, s, pairs, el, ew, n, status, f0, pkey, ctr, rm);
+    DV_LAUNCH((k_exec<true>), (uint32_t)blocks, kBlock, 0, s, pairs, el, ew, n, status, f0, pkey, ctr, rm);
 }
 
 // NO_WAIT / WAIT_DIE / OCC: run_ycsb_1 for the committed txns only (acc_row
@@ -1119,12 +1113,12 @@ void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
-        k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn,
+        DV_LAUNCH((k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn,
                                                                               status, f0, pkey, ctr, rm, d_commit);
     } else {
-        k_exec_txn<EX_READS | EX_COMMIT><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
+        DV_LAUNCH((k_exec_txn<EX_READS | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
                                                                    pkey, ctr, rm, d_commit);
-        k_exec_txn<EX_WRITES><<<blocks, kBlock, 0, s>>>(tb_start, tb_end, acc_row, n_txn, status, f0,
+        DV_LAUNCH((k_exec_txn<EX_WRITES>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
                                                         pkey, ctr, rm, nullptr);
     }
 }
@@ -1171,7 +1165,7 @@ void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uin
     if (!n_txn) return;
     uint32_t blocks = (n_txn + kBlock * 16 - 1) / (kBlock * 16);
     if (blocks > 1024) blocks = 1024;
-    k_commit_out<<<blocks, kBlock, 0, s>>>(status, n_txn, d_commit, ctr);
+    DV_LAUNCH(k_commit_out, blocks, kBlock, 0, s, status, n_txn, d_commit, ctr);
 }
 
 // ------------------------------------------------------------- loaders
@@ -1192,7 +1186,7 @@ __global__ void k_ycsb_load(uint64_t rows, uint32_t part_cnt, uint32_t part_id, 
 
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag) {
-    k_ycsb_load<<<2048, kBlock, 0, s>>>(rows, part_cnt, part_id, f0, pkey, ktag);
+    DV_LAUNCH(k_ycsb_load, 2048, kBlock, 0, s, rows, part_cnt, part_id, f0, pkey, ktag);
 }
 
 __global__ void k_home_bits(const uint8_t *__restrict__ ktag, uint64_t n, uint32_t htag, uint32_t *__restrict__ bits) {
@@ -1204,7 +1198,7 @@ __global__ void k_home_bits(const uint8_t *__restrict__ ktag, uint64_t n, uint32
     }
 }
 void launch_home_bits(hipStream_t s, const uint8_t *ktag, uint64_t n, uint32_t htag, uint32_t *bits) {
-    if (n) k_home_bits<<<2048, kBlock, 0, s>>>(ktag, n, htag, bits);
+    if (n) DV_LAUNCH(k_home_bits, 2048, kBlock, 0, s, ktag, n, htag, bits);
 }
 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,
@@ -1219,7 +1213,7 @@ __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys,
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
                         uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr) {
     if (!n) return;
-    k_gather_rows<<<1024, kBlock, 0, s>>>(tabs, table, keys, n, f0, out, ctr);
+    DV_LAUNCH(k_gather_rows, 1024, kBlock, 0, s, tabs, table, keys, n, f0, out, ctr);
 }
 
 // host records -> the epoch's arrays; with txn_begin (CSR), every record's
@@ -1243,7 +1237,7 @@ __global__ void k_split_access(const dv_access *acc, uint64_t n, const uint32_t 
 void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
                          uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables, uint32_t *err) {
     if (!n) return;
-    k_split_access<<<2048, kBlock, 0, s>>>(acc, n, tb, n_txn, keys, types, acc_txn, tables, err);
+    DV_LAUNCH(k_split_access, 2048, kBlock, 0, s, acc, n, tb, n_txn, keys, types, acc_txn, tables, err);
 }
 
 }  // namespace dvcc

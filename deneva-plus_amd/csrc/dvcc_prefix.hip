@@ -63,6 +63,10 @@ __device__ __forceinline__ uint32_t row_bits(const uint32_t *rs, uint32_t row) {
 #endif
 constexpr uint32_t kHotRows = 1u << DVCC_HOT_LOG, kHotWords = kHotRows / 16;
 constexpr uint32_t kBloomBits = 1u << DVCC_BLOOM_LOG, kBloomWords = kBloomBits / 32;
+// k_kill stages both in LDS: gfx950 gives a workgroup 160 KiB (a target with
+// less, e.g. gfx942's 64 KiB, needs smaller DVCC_HOT_LOG / DVCC_BLOOM_LOG)
+static_assert((kHotWords + kBloomWords) * sizeof(uint32_t) <= 160u * 1024u,
+              "k_kill's hot row words + Bloom filter exceed gfx950's 160 KiB of LDS per workgroup");
 __device__ __forceinline__ uint32_t bloom_bit(uint32_t row) { return (row * 0x9E3779B1u) >> (32 - DVCC_BLOOM_LOG); }
 
 // (a multiple of 4 words: k_epoch_clear zeroes it in 16-byte stores)
@@ -323,7 +327,7 @@ void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb
     // (the bitmap and the Bloom filter after it were zeroed by k_epoch_clear)
     if (!K) return;
     const uint32_t g = std::min<uint32_t>((K + kMarkBlock - 1) / kMarkBlock, 64);
-    k_prefix_mark<<<g, kMarkBlock, 0, s>>>(status, tb_start, tb_end, acc_row, K, row_state, rs_words - kBloomWords,
+    DV_LAUNCH(k_prefix_mark, g, kMarkBlock, 0, s, status, tb_start, tb_end, acc_row, K, row_state, rs_words - kBloomWords,
                                            row_state + (rs_words - kBloomWords), nowait, ctr);
 }
 
@@ -341,17 +345,17 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
     // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
-    k_kill<<<grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s>>>(acc_row, n_acc, row_state, rs_words - kBloomWords,
+    DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, row_state, rs_words - kBloomWords,
                                                                      row_state + (rs_words - kBloomWords), nowait,
                                                                      kill_bits, ctr);
-    k_kill_compact<<<nt, kBlock, 0, s>>>(tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
+    DV_LAUNCH(k_kill_compact, nt, kBlock, 0, s, tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
                                          tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
                              uint8_t *status, const Counters *ctr) {
     if (!ub) return;
-    k_sub_scatter_back<<<grid_of(ub, 2048), kBlock, 0, s>>>(map, status_b, status, ctr);
+    DV_LAUNCH(k_sub_scatter_back, grid_of(ub, 2048), kBlock, 0, s, map, status_b, status, ctr);
 }
 
 }  // namespace dvcc

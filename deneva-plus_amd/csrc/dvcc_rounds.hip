@@ -155,25 +155,12 @@ __device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw,
 // aggregates at about the same time and each walks back to the nearest
 // inclusive prefix, 64 descriptors per step (config D: 16K/8K-element tiles
 // took 2.5 % less epoch time than 8K/4K, 4K/4K took 3 % more).
-// DVCC_EXP_* override the geometry for experiments (tools/gpu_exp.sh).
-#ifndef DVCC_EXP_T32
-#define DVCC_EXP_T32 1024
-#endif
-#ifndef DVCC_EXP_IPT
-#define DVCC_EXP_IPT 16
-#endif
-#ifndef DVCC_EXP_MW32
-#define DVCC_EXP_MW32 4
-#endif
-#ifndef DVCC_EXP_T64
-#define DVCC_EXP_T64 512
-#endif
 template <class EIn>
 struct Geo {
-    static constexpr int kThreads = sizeof(EIn) == 4 ? DVCC_EXP_T32 : DVCC_EXP_T64;
-    static constexpr int kMinWaves = sizeof(EIn) == 4 ? DVCC_EXP_MW32 : 3;  // per SIMD: <= 128 / 168 VGPRs
+    static constexpr int kThreads = sizeof(EIn) == 4 ? 1024 : 512;
+    static constexpr int kMinWaves = sizeof(EIn) == 4 ? 4 : 3;  // per SIMD: <= 128 / 168 VGPRs
     static constexpr int kWaves = kThreads / 64;
-    static constexpr int kIPT = sizeof(EIn) == 4 ? DVCC_EXP_IPT : 16;
+    static constexpr int kIPT = 16;
     static constexpr uint32_t kTile = kThreads * kIPT;
 };
 __device__ __forceinline__ uint32_t pad16(uint32_t j) { return j + (j >> 4); }
@@ -325,12 +312,8 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
 #pragma unroll
     for (int j = 0; j < IPT; j++) {
         const bool valid = j < cnt;
-#ifdef DVCC_EXP_NO_GATHER
-        const uint8_t s = valid ? (uint8_t)ST_UNDEC : (uint8_t)ST_ABORT;
-#else
         const uint8_t s0 = FIRST ? (uint8_t)ST_UNDEC : status[r_txn(e[j], slog)];
         const uint8_t s = valid ? s0 : (uint8_t)ST_ABORT;
-#endif
         umask |= (s == ST_UNDEC ? 1u : 0u) << j;
         needy |= (s == ST_UNDEC && !(e[j] & F_DONE) ? 1u : 0u) << j;
         const bool single = (e[j] & F_HEAD) && ((nhm >> j) & 1u);
@@ -361,11 +344,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     if (wave == 0) {
         bagg = sh.wt[0];
         for (int w = 1; w < G::kWaves; w++) bagg = OpPlain::comb(bagg, sh.wt[w]);
-#ifdef DVCC_EXP_NO_LOOKBACK
-        const Agg pre{0u, 0u, tile * G::kTile};
-#else
         const Agg pre = look_back<OpPlain, true>(desc, tile, tag, bagg, lane, ctr);
-#endif
         if (lane == 0) {
             sh.pre = Agg{pre.f, pre.v, 0u};
             sh.tot = bagg.c;
@@ -374,11 +353,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     }
     __syncthreads();
     if (wave == 0) {
-#ifdef DVCC_EXP_NO_LOOKBACK
-        const uint32_t gpos = tile * G::kTile;
-#else
         const uint32_t gpos = look_back<OpPlain>(desc, tile, tag, bagg, lane, ctr).c;
-#endif
         if (lane == 0) sh.gpos = gpos;
     }
     Agg wpre{0u, 0u, 0u};  // this wave's prefix within the tile
@@ -394,9 +369,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
         const uint32_t vj = v[j];
         const bool head = (ej & F_HEAD) != 0;
         const uint32_t excl = head ? 0u : run;
-#ifndef DVCC_EXP_NO_DECIDE
         if ((umask >> j) & 1u) ej = decide_elem<FIRST>(ej, excl, nowait, vb8, slog, status);
-#endif
         if (vj & B_KEEP) s_out[lpos++] = (E)((ej & ~(E)F_HEAD) | ((excl & B_KEEP) ? 0u : F_HEAD));
         run = head ? vj : (run | vj);
     }
@@ -448,11 +421,7 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
     if (blockIdx.x >= ntiles) {  // spare blocks of a stale upper bound: no ticket
         if (ntiles == 0 && blockIdx.x == 0 && threadIdx.x == 0) { *n_out = 0; reset_und(und_reset, ctr); }
     } else {
-#ifdef DVCC_EXP_TICKET_BLOCKIDX
-        if (threadIdx.x == 0) s_tile = blockIdx.x;
-#else
         if (threadIdx.x == 0) s_tile = atomicAdd(tile_ctr, 1u);
-#endif
         __syncthreads();
         round_tile<FIRST, EIn, E>(sh, s_tile, n, ntiles, el_in, el_out, n_out, status, vb8, slog,
                                   nowait, desc, tag, und_reset, ctr);
@@ -1125,9 +1094,12 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     Counters *ctr = b.ctr;
     const uint32_t G = gridDim.x;
     const uint32_t go = async_gate(ctr, r0, G, thresh);
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->async_go = go;  // for the finalize (its inputs change there)
-    if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint32_t n_all = ctr->nlive[r0 & 1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctr->async_go = go;  // for the finalize (its inputs change there)
+        if (go == 1u) ctr->async_live += n_all;
+    }
+    if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint64_t per = ((uint64_t)n_all + G - 1) / G;  // the largest slice (uniform)
     if (per <= (uint64_t)kAsyncThreads * kAsyncIPTTiny)
         async_slices<kAsyncIPTTiny>(b, src, r0, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy, s_moved,
@@ -1226,14 +1198,13 @@ static void round_pass_t(hipStream_t s, const RoundBufs &b, uint32_t round, int 
     if (round == 0) {
         using G = Geo<uint64_t>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
-        hipExtLaunchKernelGGL(k_round_pass<true, uint64_t, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0,
-                              ev1, 0, b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait,
+        DV_LAUNCH_EV((k_round_pass<true, uint64_t, E>), nb, G::kThreads, 0, s, ev0, ev1, b.pairs0, n_in, out, n_out, b.status, b.vb8, b.slog, nowait,
                               b.desc, tc, tag, und, (const uint32_t *)nullptr, round,
                               (RoundPub *)nullptr, b.ctr, b.n0_dev, b.n0, b.n_txn_dev, b.n_txn0);
     } else {
         using G = Geo<E>;
         const uint32_t nb = ub_in ? (ub_in + G::kTile - 1) / G::kTile : 1;
-        hipExtLaunchKernelGGL(k_round_pass<false, E, E>, dim3(nb), dim3(G::kThreads), 0, s, ev0, ev1, 0,
+        DV_LAUNCH_EV((k_round_pass<false, E, E>), nb, G::kThreads, 0, s, ev0, ev1,
                               reinterpret_cast<const E *>(b.rel[(round - 1) & 1]), n_in, out, n_out,
                               b.status, b.vb8, b.slog, nowait, b.desc, tc, tag, und, und_in, round,
                               pub, b.ctr, (const uint32_t *)nullptr, 0u, (const uint32_t *)nullptr, 0u);
@@ -1248,8 +1219,8 @@ void round_pass(hipStream_t s, const RoundBufs &b, uint32_t round, int nowait, u
 }
 
 void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, RoundPub *pub) {
-    if (b.el32) k_round_tail<uint32_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
-    else k_round_tail<uint64_t><<<1, kTailThreads, 0, s>>>(b, r0, nowait, pub);
+    if (b.el32) DV_LAUNCH((k_round_tail<uint32_t>), 1, kTailThreads, 0, s, b, r0, nowait, pub);
+    else DV_LAUNCH((k_round_tail<uint64_t>), 1, kTailThreads, 0, s, b, r0, nowait, pub);
 }
 
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
@@ -1257,11 +1228,11 @@ void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uin
                  uint64_t idle_ticks, bool words_done) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
     if (!words_done)  // (else round 0's settle wrote them: round_settle with tword)
-        k_async_words<<<txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
+        DV_LAUNCH(k_async_words, txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s, b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
                                                                     b.n_txn_dev, b.ctr);
-    k_round_async<<<G, kAsyncThreads, 0, s>>>(b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
-    k_round_finalize<<<txn_grid(n_txn), kBlock, 0, s>>>(b.status, tword, n_txn, r0, pub, b.n_txn_dev, b.ctr);
+    DV_LAUNCH(k_round_async, G, kAsyncThreads, 0, s, b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
+    DV_LAUNCH(k_round_finalize, txn_grid(n_txn), kBlock, 0, s, b.status, tword, n_txn, r0, pub, b.n_txn_dev, b.ctr);
 }
 
 // Every workgroup of the asynchronous launch must be resident at once (one
@@ -1285,17 +1256,17 @@ void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_
     const uint32_t nb = n ? (n + kSettleChunk - 1) / kSettleChunk : 1;
     uint32_t *n_out = &b.ctr->nund[(round + 1) & 1];
     if (round == 0)
-        k_round_settle<true><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen, nullptr, &b.ctr->nund[0],
+        DV_LAUNCH((k_round_settle<true>), nb, kBlock, 0, s, b.status, b.vb8, b.slog, b.tlen, nullptr, &b.ctr->nund[0],
                                                    n_txn, b.ulist[1], n_out, tword, carry, G);
     else
-        k_round_settle<false><<<nb, kBlock, 0, s>>>(b.status, b.vb8, b.slog, b.tlen,
+        DV_LAUNCH((k_round_settle<false>), nb, kBlock, 0, s, b.status, b.vb8, b.slog, b.tlen,
                                                     b.ulist[round & 1], &b.ctr->nund[round & 1],
                                                     n_txn, b.ulist[(round + 1) & 1], n_out, nullptr, nullptr, 0u);
 }
 
 void list_verdict(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, uint8_t *verdict) {
     const uint32_t *list = round == 0 ? nullptr : b.ulist[round & 1];
-    k_list_verdict<<<txn_grid(ub), kBlock, 0, s>>>(list, &b.ctr->nund[round & 1], b.status, b.vb8,
+    DV_LAUNCH(k_list_verdict, txn_grid(ub), kBlock, 0, s, list, &b.ctr->nund[round & 1], b.status, b.vb8,
                                                   b.slog, b.tlen, verdict);
 }
 
@@ -1303,7 +1274,7 @@ void list_apply(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t ub, 
                 uint32_t tag, uint32_t *tile_ctr, RoundPub *pub) {
     const uint32_t *list = round == 0 ? nullptr : b.ulist[round & 1];
     const uint32_t nb = ub ? (ub + kRTile - 1) / kRTile : 1;
-    k_list_apply<<<nb, kBlock, 0, s>>>(list, &b.ctr->nund[round & 1], verdict, b.status,
+    DV_LAUNCH(k_list_apply, nb, kBlock, 0, s, list, &b.ctr->nund[round & 1], verdict, b.status,
                                        b.ulist[(round + 1) & 1], &b.ctr->nund[(round + 1) & 1],
                                        &b.ctr->nlive[(round + 1) & 1], b.desc, tile_ctr, tag, round, pub,
                                        b.ctr);

@@ -13,7 +13,9 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
 #include <new>
+#include <string>
 #include <vector>
 
 #include "dvcc_common.h"
@@ -37,6 +39,27 @@ struct HostTable {
 };
 
 }  // namespace
+
+// per-launch kernel timing of one context (DV_FLAG_KERNEL_PROFILE,
+// dv_kernel_times; DV_LAUNCH in dvcc_internal.h)
+struct dvcc::KProf {
+    struct Pending {
+        const char *name;
+        hipEvent_t e0, e1;
+        bool owned;  // from the pool (else the runtime's own timing events)
+    };
+    struct Sum {
+        uint64_t launches = 0;
+        double ms = 0;
+    };
+    static constexpr size_t kPool = 8192;  // event pairs (a 1M-txn epoch takes ~40)
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    size_t used = 0;                       // pool pairs handed out and not yet read
+    std::vector<Pending> pending;
+    std::map<std::string, Sum> sums;
+    uint64_t dropped = 0;                  // launches not timed: the pool was spent
+    int depth = 0;                         // nested C-ABI entries (KProfScope)
+};
 
 struct dv_ctx {
     dv_config cfg{};
@@ -177,7 +200,88 @@ struct dv_ctx {
     bool async_unconfirmed = false;      // the rounds ended in a try nobody waited for
     uint32_t async_hint = 0;             // round the last epoch's asynchronous launch ran at
     float ms_probe = 0, ms_sort = 0, ms_decide = 0, ms_exec = 0;
+    KProf kprof;                         // DV_FLAG_KERNEL_PROFILE
 };
+
+// ---- per-launch kernel timing (dvcc_internal.h, DV_LAUNCH)
+namespace dvcc {
+thread_local KProf *tl_kprof = nullptr;
+
+void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1) {
+    KProf *p = tl_kprof;
+    *e0 = *e1 = nullptr;
+    if (!p) return;
+    if (p->used >= KProf::kPool) {
+        p->dropped++;
+        return;
+    }
+    if (p->used == p->pool.size()) {
+        hipEvent_t a = nullptr, b = nullptr;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) {
+            if (a) (void)hipEventDestroy(a);
+            p->dropped++;
+            return;
+        }
+        p->pool.push_back({a, b});
+    }
+    *e0 = p->pool[p->used].first;
+    *e1 = p->pool[p->used].second;
+    p->used++;
+    p->pending.push_back({kernel, *e0, *e1, true});
+}
+
+void kprof_add(const char *kernel, hipEvent_t e0, hipEvent_t e1) {
+    if (tl_kprof) tl_kprof->pending.push_back({kernel, e0, e1, false});
+}
+
+namespace {
+// "(k_round_pass<true, uint64_t, E>)" -> "k_round_pass"
+std::string kernel_base(const char *s) {
+    std::string out;
+    for (; *s; s++) {
+        if (*s == '(' || *s == ' ') continue;
+        if (*s == '<' || *s == ')') break;
+        out += *s;
+    }
+    return out;
+}
+
+// read every pending pair whose stop event has completed (wait: all of them);
+// the pool is reused once nothing is pending
+void kprof_harvest(KProf *p, bool wait) {
+    size_t keep = 0;
+    for (size_t i = 0; i < p->pending.size(); i++) {
+        KProf::Pending &q = p->pending[i];
+        if (wait) (void)hipEventSynchronize(q.e1);
+        else if (hipEventQuery(q.e1) != hipSuccess) {
+            p->pending[keep++] = q;
+            continue;
+        }
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, q.e0, q.e1) == hipSuccess) {
+            KProf::Sum &s = p->sums[kernel_base(q.name)];
+            s.launches++;
+            s.ms += ms;
+        }
+    }
+    p->pending.resize(keep);
+    if (keep == 0) p->used = 0;
+}
+}  // namespace
+
+KProfScope::KProfScope(dv_ctx *c) : prev_(tl_kprof), mine_(nullptr) {
+    if (c && (c->cfg.flags & DV_FLAG_KERNEL_PROFILE)) {
+        mine_ = &c->kprof;
+        mine_->depth++;
+        tl_kprof = mine_;
+    }
+}
+
+KProfScope::~KProfScope() {
+    if (mine_ && --mine_->depth == 0) kprof_harvest(mine_, false);
+    tl_kprof = prev_;
+}
+}  // namespace dvcc
 
 namespace {
 
@@ -314,7 +418,7 @@ int err_from_bits(uint32_t b) {
     if (b & ERRB_TABLE) return DV_ERR_NO_TABLE;
     if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
     if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
-    if (b & ERRB_BIG) return DV_ERR_ARG;  // a txn longer than the epoch's max_txn_acc
+    if (b & (ERRB_BIG | ERRB_TS)) return DV_ERR_ARG;  // a txn longer than max_txn_acc; WAIT_DIE ts not rising
     if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
     if (b & ERRB_SPIN) return DV_ERR_HIP;
     return DV_OK;
@@ -462,6 +566,10 @@ void dv_close(dv_ctx *c) {
     for (auto &e : c->ev) if (e) (void)hipEventDestroy(e);
     for (auto &e : c->sev) if (e) (void)hipEventDestroy(e);
     for (auto &e : c->pev) if (e) (void)hipEventDestroy(e);
+    for (auto &pr : c->kprof.pool) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     delete c;
 }
@@ -577,6 +685,7 @@ int dv_set_stream(dv_ctx *c, void *stream) {
 }
 
 int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch_dev *out) {
+    KProfScope kps_(c);
     if (!c || !ep || !out) return DV_ERR_ARG;
     if (c->phase != 0 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
     if (ep->n_txn != c->n_txn || ep->n_acc != c->n_acc) return DV_ERR_STATE;  // not the last epoch
@@ -612,7 +721,11 @@ int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch
 int dv_set_timing(dv_ctx *c, uint32_t flags) {
     if (!c) return DV_ERR_ARG;
     if (c->phase != 0) return DV_ERR_STATE;
-    constexpr uint32_t kBits = DV_FLAG_TIMING | DV_FLAG_KERNEL_TIMING;
+    constexpr uint32_t kBits = DV_FLAG_TIMING | DV_FLAG_KERNEL_TIMING | DV_FLAG_KERNEL_PROFILE;
+    if ((c->cfg.flags & DV_FLAG_KERNEL_PROFILE) && !(flags & DV_FLAG_KERNEL_PROFILE)) {
+        HIPCHK(hipStreamSynchronize(c->stream));  // the launches still pending are read now
+        kprof_harvest(&c->kprof, true);
+    }
     c->cfg.flags = (c->cfg.flags & ~kBits) | (flags & kBits);
     if (ktiming(c) && !c->ev[0]) {
         HIPCHK(hipSetDevice(c->cfg.device));
@@ -621,6 +734,30 @@ int dv_set_timing(dv_ctx *c, uint32_t flags) {
         for (auto &e : c->pev) HIPCHK(hipEventCreate(&e));
     }
     return DV_OK;
+}
+
+int dv_kernel_times(dv_ctx *c, dv_kernel_time *out, uint32_t cap, int reset) {
+    if (!c || (cap && !out)) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    kprof_harvest(&c->kprof, true);
+    uint32_t n = 0;
+    for (const auto &kv : c->kprof.sums) {
+        if (n < cap) {
+            dv_kernel_time &k = out[n];
+            std::memset(&k, 0, sizeof(k));
+            std::snprintf(k.name, sizeof(k.name), "%s", kv.first.c_str());
+            k.launches = kv.second.launches;
+            k.ms_total = kv.second.ms;
+        }
+        n++;
+    }
+    if (reset) {
+        c->kprof.sums.clear();
+        c->kprof.dropped = 0;
+    }
+    return (int)n;
 }
 
 // Workload::init_schema (system/wl.cpp:31-149) + IndexHash::init (index_hash.cpp:22-42)
@@ -940,6 +1077,7 @@ int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
 }  // namespace
 
 int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
+    KProfScope kps_(c);
     if (!c || !ep) return DV_ERR_ARG;
     const uint32_t *err_seed = c->err_seed;  // only for the epoch dv_epoch_run staged just now
     c->err_seed = nullptr;
@@ -955,7 +1093,8 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
-                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         const int re = comm_combine_errors(c);
@@ -1052,6 +1191,7 @@ int wait_published(dv_ctx *c, uint32_t target, uint32_t tail_r0) {
 // one decision round on this partition's accesses; writes this partition's
 // verdict byte per txn (bit1 abort, bit0 wait) into d_verdict (NULL = internal)
 int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
+    KProfScope kps_(c);
     if (!c || c->phase != 1) return DV_ERR_STATE;
     if (c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
     enqueue_round(c, d_verdict ? d_verdict : c->verdict, false);
@@ -1061,6 +1201,7 @@ int dv_epoch_round_local(dv_ctx *c, uint8_t *d_verdict) {
 
 // apply verdicts combined over all partitions (MAX); returns undecided txns
 int dv_epoch_round_apply(dv_ctx *c, const uint8_t *d_verdict, uint32_t *undecided) {
+    KProfScope kps_(c);
     if (!c || c->phase != 1 || c->cfg.cc_alg == DV_CALVIN) return DV_ERR_STATE;
     if (c->rounds == 0 || c->applied >= c->rounds) return DV_ERR_STATE;
     const uint32_t tag = next_tag(c);
@@ -1155,6 +1296,7 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
 }  // namespace
 
 int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
+    KProfScope kps_(c);
     if (!c || c->phase != 1) return DV_ERR_STATE;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     if (c->cfg.workload == DV_TPCC && !c->tp_args) {  // only through dv_tpcc_epoch_begin
@@ -1268,6 +1410,13 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             st->ms_pass = sp;
             st->pass_live = c->passes <= (uint32_t)kRoundLog ? c->h_ctr->pass_live : 0;  // (no-op passes add 0)
             if (c->n_acc) (void)hipEventElapsedTime(&st->ms_probe_kernel, c->ev[kEvProbe0], c->ev[kEvProbe1]);
+        }
+        st->async_live = c->h_ctr->async_live;
+        if (prefix) {
+            st->prefix_txn = c->pf_K;
+            st->prefix_acc = c->h_ctr->a_acc;
+            st->surv_txn = c->h_ctr->b_txn;
+            st->surv_acc = c->h_ctr->b_acc;
         }
     }
     return DV_OK;
@@ -1534,7 +1683,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
-                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32);
+                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         r = comm_combine_errors(c);
@@ -1580,6 +1730,7 @@ int dv_set_prefix(dv_ctx *c, uint32_t prefix_txns) {
 
 int dv_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, uint32_t *d_grant,
                         dv_stats *st) {
+    KProfScope kps_(c);
     if (c && ep && prefix_applies(c, ep)) {
         HIPCHK(hipSetDevice(c->cfg.device));
         const int r = run_prefix_epoch(c, ep);
@@ -1605,6 +1756,7 @@ namespace {
 struct EpochSnap {
     uint64_t n_acc = 0;
     uint32_t n_txn = 0, rounds = 0, rounds_real = 0, rounds_prefix = 0, async_launched = 0, sort_passes = 0;
+    uint32_t prefix_txn = 0;
     bool async_unconfirmed = false;
     unsigned long long seq = 0;
     int slot = 0;
@@ -1632,6 +1784,7 @@ int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate
     sn.rounds_prefix = c->rounds_prefix;
     sn.async_launched = c->async_launched;
     sn.sort_passes = c->sort_passes;
+    sn.prefix_txn = c->pf_K;
     sn.async_unconfirmed = c->async_unconfirmed;
     sn.slot = slot;
     if (defer && !r) {
@@ -1694,6 +1847,11 @@ int pipe_complete(dv_ctx *c, const EpochSnap &sn, dv_stats *st, bool *halted) {
         st->async_launches = (uint16_t)std::min(sn.async_launched, 0xFFFFu);
         st->async_declined = (uint16_t)std::min(hc->async_declined, 0xFFFFu);
         st->async_yields = hc->async_yields;
+        st->async_live = hc->async_live;
+        st->prefix_txn = sn.prefix_txn;
+        st->prefix_acc = hc->a_acc;
+        st->surv_txn = hc->b_txn;
+        st->surv_acc = hc->b_acc;
     }
     return DV_OK;
 }
@@ -1715,6 +1873,7 @@ extern "C" {
 
 int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
                               dv_stats *sts) {
+    KProfScope kps_(c);
     if (!c || (n && !eps)) return DV_ERR_ARG;
     if (c->phase != 0) return DV_ERR_STATE;
     HIPCHK(hipSetDevice(c->cfg.device));
@@ -1811,6 +1970,7 @@ extern "C" {
 // epoch, which then runs the generic path; dv_epoch_finish executes the
 // committed txns' TPC-C operations (dvcc_tpcc.hip).
 int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint64_t *d_oid) {
+    KProfScope kps_(c);
     if (!c || !ep || (ep->n_acc && (!d_args || !ep->tables)) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
@@ -1847,6 +2007,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
 
 int dv_tpcc_epoch_run_device(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_args, uint8_t *d_commit,
                              uint64_t *d_oid, dv_stats *st) {
+    KProfScope kps_(c);
     int r = dv_tpcc_epoch_begin(c, ep, d_args, d_oid);
     if (r) return r;
     if (c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
@@ -1867,6 +2028,7 @@ int dv_set_async_limits(dv_ctx *c, uint32_t max_iters, uint32_t idle_us) {
 // partitioned epochs: every partition must learn of an input error found on
 // any of them before the rounds, so that all leave at the same collective
 int dv_epoch_errors_local(dv_ctx *c, uint32_t *d_word) {
+    KProfScope kps_(c);
     if (!c || !d_word) return DV_ERR_ARG;
     if (c->phase != 1) return DV_ERR_STATE;
     HIPCHK(hipMemcpyAsync(d_word, &c->ctr->err, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
@@ -1874,6 +2036,7 @@ int dv_epoch_errors_local(dv_ctx *c, uint32_t *d_word) {
 }
 
 int dv_epoch_errors_combined(dv_ctx *c, const uint32_t *d_word) {
+    KProfScope kps_(c);
     if (!c || !d_word) return DV_ERR_ARG;
     if (c->phase != 1) return DV_ERR_STATE;
     HIPCHK(hipMemcpyAsync(&c->ctr->peer_err, d_word, sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
@@ -1977,6 +2140,7 @@ extern "C" {
 int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                  uint32_t n_txn, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
                  dv_stats *st) {
+    KProfScope kps_(c);
     if (!c || !out_commit) return DV_ERR_ARG;
     // WAIT_DIE: decisions follow sequence order, which equals timestamp order
     // when ts rises with it (TS_CAS, manager.cpp:52-57, taken in sequence
@@ -2006,6 +2170,7 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
 // epoch's records runs on a copy stream while the current epoch decides.
 int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                         uint32_t n_txn) {
+    KProfScope kps_(c);
     if (!c || slot < 0 || slot > 1) return DV_ERR_ARG;
     uint32_t max_len = 0;
     int r = check_host_epoch(c, acc, n_acc, txn_begin, n_txn, &max_len);
@@ -2042,6 +2207,7 @@ int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_ac
 
 int dv_epoch_run_staged(dv_ctx *c, int slot, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
                         dv_stats *st) {
+    KProfScope kps_(c);
     if (!c || slot < 0 || slot > 1 || !out_commit) return DV_ERR_ARG;
     auto &h = c->hslot[slot];
     if (!h.full) return DV_ERR_STATE;
@@ -2068,6 +2234,7 @@ int dv_epoch_run_staged(dv_ctx *c, int slot, const uint64_t *ts, uint8_t *out_co
 int dv_tpcc_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
                       uint32_t n_txn, const uint64_t *args, uint8_t *out_commit, uint64_t *out_oid,
                       dv_stats *st) {
+    KProfScope kps_(c);
     if (!out_commit || (n_acc && !args)) return DV_ERR_ARG;
     dv_epoch_dev ep;
     int r = stage_host_epoch(c, acc, n_acc, txn_begin, n_txn, &ep);

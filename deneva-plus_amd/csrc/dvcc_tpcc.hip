@@ -265,15 +265,15 @@ void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys
                          uint64_t n, const uint64_t *col0, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
     if (n == 0) return;
     (void)ctr;
-    k_tpcc_resolve<<<grid_for(n), kBlock, 0, s>>>(tabs, keys, tables, n, col0, okeys, otables);
+    DV_LAUNCH(k_tpcc_resolve, grid_for(n), kBlock, 0, s, tabs, keys, tables, n, col0, okeys, otables);
 }
 
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
     if (x.n == 0) return;
-    k_tpcc_apply<<<grid_for(x.n), kBlock, 0, s>>>(x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2,
+    DV_LAUNCH(k_tpcc_apply, grid_for(x.n), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2,
                                                   x.dsnap, x.dist_base, x.dist_rows, x.ctr);
     const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
-    k_tpcc_oid<<<ntiles, kBlock, 0, s>>>(x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
+    DV_LAUNCH(k_tpcc_oid, ntiles, kBlock, 0, s, x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
                                          x.dist_base, x.dist_rows, x.c1, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
 }
 

@@ -33,6 +33,7 @@ FLAG_NO_TAIL = 2
 FLAG_EL64 = 4
 FLAG_NO_ASYNC = 8
 FLAG_KERNEL_TIMING = 16
+FLAG_KERNEL_PROFILE = 32
 
 
 class DvccError(RuntimeError):
@@ -57,7 +58,7 @@ class Access(ctypes.Structure):
 class EpochDev(ctypes.Structure):
     _fields_ = [("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("acc_txn", ctypes.c_void_p),
                 ("tables", ctypes.c_void_p), ("n_acc", ctypes.c_uint64), ("n_txn", ctypes.c_uint32),
-                ("max_txn_acc", ctypes.c_uint32)]
+                ("max_txn_acc", ctypes.c_uint32), ("ts", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -72,10 +73,17 @@ class Stats(ctypes.Structure):
                 ("ms_pass", ctypes.c_float), ("async_launches", ctypes.c_uint16),
                 ("async_declined", ctypes.c_uint16),
                 ("pass_live", ctypes.c_uint64), ("async_yields", ctypes.c_uint32),
-                ("ms_probe_kernel", ctypes.c_float)]
+                ("ms_probe_kernel", ctypes.c_float),
+                ("prefix_txn", ctypes.c_uint32), ("surv_txn", ctypes.c_uint32),
+                ("prefix_acc", ctypes.c_uint64), ("surv_acc", ctypes.c_uint64),
+                ("async_live", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class KernelTime(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char * 48), ("launches", ctypes.c_uint64), ("ms_total", ctypes.c_double)]
 
 
 class YcsbParams(ctypes.Structure):
@@ -110,6 +118,7 @@ SIGNATURES = [
     ("dv_own_stream", _vp, [_vp]),
     ("dv_set_stream", ctypes.c_int, [_vp, _vp]),
     ("dv_set_timing", ctypes.c_int, [_vp, ctypes.c_uint32]),
+    ("dv_kernel_times", ctypes.c_int, [_vp, _P(KernelTime), ctypes.c_uint32, ctypes.c_int]),
     ("dv_create_table", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
                                        ctypes.c_uint32]),
     ("dv_load_table", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, _vp, ctypes.c_uint64]),

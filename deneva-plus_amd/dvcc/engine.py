@@ -80,6 +80,11 @@ class DeviceEpoch:
         self.acc_txn = torch.from_numpy(epoch.acc_txn().view(np.int32)).to(device)
         self.tables = (torch.from_numpy(epoch.tables).to(device)
                        if epoch.tables is not None else None)
+        # every txn id below the last one used has an access (what the compact
+        # epoch-group batches need, dv_epoch_group_run); None = unknown
+        n = np.diff(epoch.txn_begin.astype(np.int64))
+        used = np.flatnonzero(n)
+        self.dense = bool(used.size == 0 or (n[:used[-1] + 1] > 0).all())
 
     @classmethod
     def from_tensors(cls, keys, types, acc_txn, n_txn, tables=None, max_txn_acc=0):
@@ -90,6 +95,7 @@ class DeviceEpoch:
         self.n_acc = int(keys.numel())
         self.n_txn = int(n_txn)
         self.max_txn_acc = int(max_txn_acc)
+        self.dense = None
         return self
 
     @classmethod
@@ -108,9 +114,10 @@ class DeviceEpoch:
                                 max_txn_acc=max(first.max_txn_acc, second.max_txn_acc))
 
     def desc(self):
+        ts = getattr(self, "ts", None)
         return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
                           self.tables.data_ptr() if self.tables is not None else None,
-                          self.n_acc, self.n_txn, self.max_txn_acc)
+                          self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None)
 
 
 class CCEngine:
@@ -193,11 +200,23 @@ class CCEngine:
         v = 0xFFFFFFFF if prefix_txns is None else int(prefix_txns)
         L.check(L.lib().dv_set_prefix(self._ctx, v), "dv_set_prefix")
 
-    def set_timing(self, timing):
+    def set_timing(self, timing, profile=False):
         """Between epochs: True = per-stage events, "kernel" = only the scatter
-        and pass launches' dispatch timestamps, False = none."""
+        and pass launches' dispatch timestamps, False = none; profile=True
+        also times every launch on its own (kernel_times)."""
         flag = L.FLAG_KERNEL_TIMING if timing == "kernel" else (L.FLAG_TIMING if timing else 0)
-        L.check(L.lib().dv_set_timing(self._ctx, flag), "dv_set_timing")
+        L.check(L.lib().dv_set_timing(self._ctx, flag | (L.FLAG_KERNEL_PROFILE if profile else 0)),
+                "dv_set_timing")
+
+    def kernel_times(self, reset=True):
+        """{kernel name: (launches, total ms)} of the launches timed while
+        set_timing(..., profile=True) was on (dv_kernel_times)."""
+        cap = 128
+        arr = (L.KernelTime * cap)()
+        n = L.lib().dv_kernel_times(self._ctx, arr, cap, 1 if reset else 0)
+        if n < 0:
+            L.check(n, "dv_kernel_times")
+        return {arr[i].name.decode(): (int(arr[i].launches), float(arr[i].ms_total)) for i in range(min(n, cap))}
 
     # ---- storage (Workload::init_schema / init_table; IndexHash::index_insert)
     def load_ycsb_partition(self, rows_per_part):
@@ -300,6 +319,19 @@ class CCEngine:
     def comm_set_mode(self, mode):
         """dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible."""
         L.check(L.lib().dv_comm_set_mode(self._ctx, mode), "dv_comm_set_mode")
+        self._comm_mode = mode
+
+    def _wide_for(self, batches):
+        """Epoch groups move compact 4-byte batches only when every rank's txn
+        ids are dense; a batch with an empty txn in the middle would fail the
+        group (DV_ERR_ARG).  Such a batch switches this rank to the 8-byte
+        form for the call -- the group's vote then takes it on every rank, so
+        the results are the same -- and the previous mode is returned."""
+        mode = getattr(self, "_comm_mode", 0)
+        if mode & L.DV_COMM_WIDE_BATCHES or all(getattr(b, "dense", None) is not False for b in batches):
+            return None
+        L.check(L.lib().dv_comm_set_mode(self._ctx, mode | L.DV_COMM_WIDE_BATCHES), "dv_comm_set_mode")
+        return mode
 
     def run_epoch_part(self, home, txns_per_rank, d_commit=None):
         """One partitioned epoch from this rank's client batch (DeviceEpoch,
@@ -318,8 +350,13 @@ class CCEngine:
         self._after_torch()
         st = L.Stats()
         arr = (L.EpochDev * len(homes))(*[h.desc() for h in homes])
-        L.check(L.lib().dv_epoch_group_run(self._ctx, arr, len(homes), txns_per_rank, _ptr(d_commit),
-                                           ctypes.byref(st)), "dv_epoch_group_run")
+        prev = self._wide_for(homes)
+        try:
+            L.check(L.lib().dv_epoch_group_run(self._ctx, arr, len(homes), txns_per_rank, _ptr(d_commit),
+                                               ctypes.byref(st)), "dv_epoch_group_run")
+        finally:
+            if prev is not None:
+                L.lib().dv_comm_set_mode(self._ctx, prev)
         return st
 
     def run_epoch_groups(self, groups, txns_per_rank, d_commits=None):
@@ -338,8 +375,13 @@ class CCEngine:
             d_commits = [d_commits] * n
         cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
         sts = (L.Stats * n)()
-        L.check(L.lib().dv_epoch_group_run_batch(self._ctx, arr, n, P, txns_per_rank, cps, sts),
-                "dv_epoch_group_run_batch")
+        prev = self._wide_for([h for g in groups for h in g])
+        try:
+            L.check(L.lib().dv_epoch_group_run_batch(self._ctx, arr, n, P, txns_per_rank, cps, sts),
+                    "dv_epoch_group_run_batch")
+        finally:
+            if prev is not None:
+                L.lib().dv_comm_set_mode(self._ctx, prev)
         return list(sts)
 
     def carry(self, dep, max_txn=None):

@@ -103,6 +103,10 @@ extern "C" {
 #define DV_FLAG_KERNEL_TIMING 16u /* only the sort-scatter and round-pass
                               launches' own dispatch timestamps (ms_scatter,
                               ms_pass): no marker packets between kernels   */
+#define DV_FLAG_KERNEL_PROFILE 32u /* every launch dispatched with its own
+                              start / stop timestamps, summed per kernel for
+                              dv_kernel_times (measurement legs only: each
+                              timed launch costs a few us of latency)       */
 #define DV_FLAG_NO_TAIL 2u /* never finish the decision rounds in the single-
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
@@ -151,6 +155,16 @@ typedef struct dv_epoch_dev {
     uint32_t max_txn_acc;    /* upper bound on one txn's accesses in this
                                 epoch (e.g. REQ_PER_QUERY); 0 = unknown
                                 (<= 128 is always required)                 */
+    const uint64_t *ts;      /* [n_txn] WAIT_DIE timestamps (device), or NULL:
+                                TS_CAS in sequence order (manager.cpp:52-57), a
+                                retried txn keeping its ts and sequenced first.
+                                Given, they must rise strictly in sequence order
+                                -- else the reference would make txns wait
+                                (row_lock.cpp:119-147) -- checked by the probe:
+                                DV_ERR_ARG, nothing executes.  Other algorithms
+                                never read it.  The partitioned drivers
+                                (dv_epoch_run_part, dv_epoch_group_run) take
+                                NULL only (DV_ERR_ARG voted on every rank). */
 } dv_epoch_dev;
 
 typedef struct dv_stats {
@@ -179,7 +193,21 @@ typedef struct dv_stats {
                                 were finished synchronously (dv_set_async_limits) */
     float ms_probe_kernel;   /* the index-probe launch alone, from its own
                                 dispatch timestamps (DV_FLAG_KERNEL_TIMING)    */
+    /* prefix-kill epochs (dv_set_prefix): the stages' sizes, 0 otherwise */
+    uint32_t prefix_txn;     /* txns decided as the prefix                     */
+    uint32_t surv_txn;       /* later txns that survived the prefix's kill     */
+    uint64_t prefix_acc;     /* the prefix's accesses (its sort keys)          */
+    uint64_t surv_acc;       /* the survivors' accesses (their sort keys)      */
+    uint64_t async_live;     /* live accesses entering the asynchronous
+                                decision launches that ran, summed            */
 } dv_stats;
+
+/* per-kernel launch timing (DV_FLAG_KERNEL_PROFILE via dv_set_timing) */
+typedef struct dv_kernel_time {
+    char name[48];           /* kernel function name, template arguments dropped */
+    uint64_t launches;
+    double ms_total;         /* sum of the launches' own dispatch-to-end times   */
+} dv_kernel_time;
 
 /* parameters of YCSBQueryGenerator (g_* globals, system/global.cpp:65-195) */
 typedef struct dv_ycsb_params {
@@ -211,6 +239,10 @@ int dv_set_stream(dv_ctx *ctx, void *stream);
  * launch latency (a marker packet per stage, dispatch timestamps per launch:
  * ~70 us per 1M-txn epoch), so a caller measures with it on and runs without. */
 int dv_set_timing(dv_ctx *ctx, uint32_t flags);
+/* the per-kernel sums of the launches timed so far under DV_FLAG_KERNEL_PROFILE
+ * (waits for the context's stream); fills at most cap entries and returns the
+ * number of kernels (>= 0) or an error; reset != 0 starts the sums again */
+int dv_kernel_times(dv_ctx *ctx, dv_kernel_time *out, uint32_t cap, int reset);
 
 /* tables: hot column = the 8-byte F0 prefix every YCSB txn reads/writes
  * (ycsb_txn.cpp:227-254); bytes beyond it are never touched by the path (H3). */
@@ -340,6 +372,12 @@ int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, 
  * needs every txn id below a batch's n_txn to have an access -- a batch with
  * an empty txn fails the group with DV_ERR_ARG on every rank
  * (DV_COMM_WIDE_BATCHES lifts that). */
+/* Precondition (open loop): the P epochs of a group are decided side by
+ * side, so no epoch of a group may depend on the outcome of an earlier epoch
+ * of the same group -- in particular a txn aborted in epoch e of group g can
+ * be retried at the earliest in group g + 1 (a penalty of up to 2P - 1
+ * epochs instead of one; dv_epoch_group_carry builds that retry batch).
+ * A caller retrying aborts epoch by epoch needs dv_epoch_run_part. */
 int dv_epoch_group_run(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st);
 /* n_groups consecutive groups, exactly as n_groups dv_epoch_group_run calls

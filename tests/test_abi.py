@@ -41,7 +41,8 @@ def test_struct_layouts_match_header(tmp_path):
     import subprocess
     from dvcc import _lib
     structs = {"dv_access": _lib.Access, "dv_config": _lib.Config, "dv_epoch_dev": _lib.EpochDev,
-               "dv_ycsb_params": _lib.YcsbParams, "dv_stats": _lib.Stats, "dv_tpcc_params": _lib.TpccParams}
+               "dv_ycsb_params": _lib.YcsbParams, "dv_stats": _lib.Stats, "dv_tpcc_params": _lib.TpccParams,
+               "dv_kernel_time": _lib.KernelTime}
     src = tmp_path / "sz.c"
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dvcc.h"', "int main(void) {"]
     for name, cls in structs.items():

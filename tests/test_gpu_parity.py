@@ -320,6 +320,45 @@ def test_wait_die_timestamps_must_rise_in_sequence_order():
     eng.close()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_txn,prefix", [(3000, None), (40_000, 512)])
+def test_wait_die_device_timestamps(n_txn, prefix):
+    """dv_epoch_dev.ts on the device entry points (the plain path and a
+    prefix-kill epoch): rising timestamps give the sequence-order decisions;
+    a pair that does not rise is DV_ERR_ARG from the probe, and no row
+    changes; NO_WAIT never reads them."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    e = g.gen(n_txn, 31)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    c_ref, _, st_ref = _oracle_epoch(dvcc.WAIT_DIE, tab, f0, e)
+    eng = CCEngine(dvcc.WAIT_DIE, n_txn, e.n_acc)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(prefix)
+    before = eng.read_table(0, rows)
+    dep = DeviceEpoch(e)
+    ts = torch.arange(n_txn, dtype=torch.int64, device="cuda") * 3 + 7
+    ts[n_txn // 2] = ts[n_txn // 2 - 1]  # not rising
+    dep.ts = ts
+    d = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    with pytest.raises(dvcc.DvccError) as ei:
+        eng.run_epoch_device(dep, d)
+    assert ei.value.code == dvcc._lib.DV_ERR_ARG
+    assert (eng.read_table(0, rows) == before).all()
+    ts[n_txn // 2] += 1
+    st = eng.run_epoch_device(dep, d)
+    assert (d.cpu().numpy() == c_ref).all()
+    assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+    nw = CCEngine(dvcc.NO_WAIT, n_txn, e.n_acc)
+    nw.load_ycsb_partition(rows)
+    ts[3] = 0
+    nw.run_epoch_device(dep, d)  # (ignored)
+    nw.close()
+
+
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
 @pytest.mark.parametrize("max_iters", [1, 3])
 def test_async_rounds_yield_and_resume(cc, max_iters):
@@ -642,5 +681,49 @@ def test_batch_error_stops_before_execution():
     with pytest.raises(dvcc.DvccError) as ei:
         eng.run_epochs_device([DeviceEpoch(e) for e in epochs])
     assert ei.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("what", ["n_txn", "n_acc"])
+def test_batch_setup_error_after_pipelined_epochs(what):
+    """Pipelined epochs followed by one the context cannot hold (n_txn past
+    max_txn / n_acc past max_acc): the epoch fails in its setup, before any
+    epoch clear would write the previous epoch's deferred counter read-back.
+    The call returns DV_ERR_ARG at once (the read-back is flushed, no 120-s
+    wait), the earlier epochs are applied and their stats filled, and the
+    context runs epochs again."""
+    import ctypes
+    import time
+    from dvcc import _lib as L
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    epochs = [g.gen(8_000, 600 + k) for k in range(3)]
+    big = g.gen(8_001 if what == "n_txn" else 8_000, 700)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    refs = [_oracle_epoch(dvcc.NO_WAIT, tab, f0, e) for e in epochs]
+    cap_acc = max(e.n_acc for e in epochs)
+    if what == "n_acc":
+        big = dvcc.Epoch(np.concatenate([big.keys, big.keys[:64]]), np.concatenate([big.types, big.types[:64]]),
+                         np.concatenate([big.txn_begin[:-1], [big.txn_begin[-1] + 64]]).astype(np.uint32))
+        assert big.n_acc > cap_acc
+    eng = CCEngine(dvcc.NO_WAIT, 8_000, cap_acc)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(256)
+    deps = [DeviceEpoch(e) for e in epochs + [big]]
+    arr = (L.EpochDev * 4)(*[d.desc() for d in deps])
+    sts = (L.Stats * 4)()
+    t0 = time.perf_counter()
+    rc = L.lib().dv_epoch_run_device_batch(eng._ctx, arr, 4, None, sts)
+    assert rc == L.DV_ERR_ARG and time.perf_counter() - t0 < 30
+    for k, (_, _, st_ref) in enumerate(refs):
+        assert (sts[k].committed, sts[k].read_digest) == (st_ref.committed, st_ref.read_digest), k
+    assert (eng.read_table(0, rows) == f0).all()
+    e2 = g.gen(8_000, 800)
+    _, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e2)
+    st = eng.run_epoch_device(DeviceEpoch(e2))
+    assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
     assert (eng.read_table(0, rows) == f0).all()
     eng.close()

@@ -761,14 +761,17 @@ def test_epoch_groups_errors_are_collective():
         assert (eng.read_table(0, rows_pp) == b).all()
     res = _run_group_epochs(engines, homes, n_txn)
     assert all(not isinstance(x, Exception) for x in res), res
-    # an empty txn inside a batch (txn ids not dense): the compact batch
-    # format cannot number it, so the group fails with DV_ERR_ARG everywhere
+    # an empty txn inside a batch (txn ids not dense) handed over as raw
+    # device arrays (density unknown to the wrapper): the compact batch format
+    # cannot number it, so the group fails with DV_ERR_ARG everywhere
     after = [eng.read_table(0, rows_pp) for eng in engines]
     gap = gen.gen(n_txn, dvcc.epoch_seed(2, 63), 2)
     tb = gap.txn_begin.copy()
     tb[5] = tb[4]
+    gd = dvcc.DeviceEpoch(dvcc.Epoch(gap.keys, gap.types, tb))
     gap_homes = [list(h) for h in homes]
-    gap_homes[2][0] = dvcc.DeviceEpoch(dvcc.Epoch(gap.keys, gap.types, tb))
+    gap_homes[2][0] = dvcc.DeviceEpoch.from_tensors(gd.keys, gd.types, gd.acc_txn, gd.n_txn,
+                                                    max_txn_acc=gd.max_txn_acc)
     res = _run_group_epochs(engines, gap_homes, n_txn)
     for r, x in enumerate(res):
         assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
@@ -784,6 +787,81 @@ def test_epoch_groups_errors_are_collective():
     for r, x in enumerate(res):
         assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
     for eng in engines:
+        eng.close()
+
+
+@pytest.mark.gpu
+def test_epoch_groups_nondense_batch_goes_wide():
+    """A host-built batch with an empty txn in the middle: the wrapper moves
+    that rank to the 8-byte batch form for the call, the group's vote takes
+    it on every rank, and the results equal the oracle over the sequenced
+    epochs (the empty txn commits with no accesses, as on one GPU)."""
+    world, rows_pp, n_txn = 2, 1 << 12, 700
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    homes = [[None] * world for _ in range(world)]
+    refs = []
+    for e in range(world):
+        batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 70 + e), r) for r in range(world)]
+        if e == 1:  # rank 0's batch of epoch 1: txn 9 loses its accesses
+            b = batches[0]
+            tb = b.txn_begin.astype(np.int64)
+            keep = np.ones(b.n_acc, bool)
+            keep[tb[9]:tb[10]] = False
+            nt = np.diff(tb)
+            nt[9] = 0
+            batches[0] = dvcc.Epoch(b.keys[keep], b.types[keep],
+                                    np.concatenate([[0], np.cumsum(nt)]).astype(np.uint32))
+        q = dvcc.sequence(batches)
+        c_ref, _, st_ref = O.epoch_run(O.NO_WAIT, tab.ix, f0, q.n_txn, q.txn_begin, q.keys, q.types)
+        refs.append((c_ref, st_ref))
+        for r in range(world):
+            homes[r][e] = dvcc.DeviceEpoch(batches[r])
+    assert homes[0][1].dense is False and homes[1][1].dense
+    res = _run_group_epochs(engines, homes, n_txn)
+    for r, x in enumerate(res):
+        assert not isinstance(x, Exception), f"rank {r}: {x}"
+        c, _ = x
+        for e in range(world):
+            assert (c[e * n_txn:(e + 1) * n_txn] == refs[e][0][r * n_txn:(r + 1) * n_txn]).all(), (r, e)
+    for p, eng in enumerate(engines):
+        assert (eng.read_table(0, rows_pp) == f0[p::world]).all()
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["group_wide", "replicated"])
+def test_txn_id_past_txns_per_rank_is_rejected(kind):
+    """A batch whose device txn ids reach txns_per_rank (its n_txn within the
+    bound): the id would alias the next origin's txn 0 in the global order, so
+    the pack sends it as an invalid id and every rank returns
+    DV_ERR_TXN_RANGE with no row changed (the 8-byte epoch-group batches and
+    the replicated protocol; the compact batches reject it as non-dense)."""
+    world, rows_pp, n_txn = 2, 1 << 12, 500
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    if kind == "group_wide":
+        for eng in engines:
+            eng.comm_set_mode(2 | dvcc._lib.DV_COMM_WIDE_BATCHES)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    batches = [[dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(r, 90 + e), r)) for e in range(world)]
+               for r in range(world)]
+    d = batches[0][0]
+    t = d.acc_txn.clone()
+    t[-3:] = n_txn  # the last txn's accesses name txn n_txn
+    batches[0][0] = dvcc.DeviceEpoch.from_tensors(d.keys, d.types, t, n_txn, max_txn_acc=d.max_txn_acc)
+    if kind == "group_wide":
+        res = _run_group_epochs(engines, batches, n_txn)
+    else:
+        res = _run_group(engines, [batches[r][0] for r in range(world)], n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_TXN_RANGE, (r, x)
+    for eng, b in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b).all()
         eng.close()
 
 

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Profiles for one tag: rocprofv3 kernel-trace summary of the config-D bench
 # command, separate FETCH_SIZE / WRITE_SIZE passes reduced to per-launch
-# traffic of the epoch's main kernels (k_probe is the line's roofline kernel),
+# traffic of the epoch's kernels (2 x FETCH_SIZE + WRITE_SIZE, the guide's
+# gfx950 correction),
 # the kernel trace of the TPC-C leg, and the default bench line.
 #   tools/gpu_prof.sh <tag>
 set -e
@@ -20,13 +21,8 @@ done
 SRC=$(python3 -c "import sys; sys.path.insert(0, 'deneva-plus_amd'); from dvcc import _lib; print(_lib.source_hash())")
 python3 tools/pmc_summary.py $OUT/pmc_FETCH_SIZE/run_counter_collection.csv \
     $OUT/pmc_WRITE_SIZE/run_counter_collection.csv $OUT/pmc_config_d.json \
-    k_probe,k_round_pass,k_round_async,k_radix_scatter,k_kill,k_kill_compact,k_exec_txn \
+    k_probe,k_round_pass,k_round_settle,k_round_async,k_round_finalize,k_radix_hist,k_radix_scan,k_radix_scatter,k_prefix_mark,k_kill,k_kill_compact,k_sub_scatter_back,k_exec_txn,k_epoch_clear \
     config=D cc=NO_WAIT n_gpus=1 src_hash=$SRC
-# k_probe calibration: the same bench with the no-gather build (exp_build/cal, tools/exp_variant.sh)
-DVCC_LIB=$PWD/exp_build/cal/libdvcc.so timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -f csv -T -d $OUT/pmc_cal -o run \
-    -- python3 $B > $OUT/pmc_cal.json 2> $OUT/pmc_cal.err
-NACC=$(python3 -c "import json; c = json.load(open('$OUT/kt_bench.json'))['config']; print(c['txns_per_epoch'] * c['req_per_query'])")
-python3 tools/pmc_probe_cal.py $OUT/pmc_config_d.json $OUT/pmc_cal/run_counter_collection.csv $NACC
 T="bench.py --tpcc-only --steps 5 --warmup 2 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -T -d $OUT/kt_tpcc -o run -- python3 $T \
     > $OUT/kt_tpcc.json 2> $OUT/kt_tpcc.err
