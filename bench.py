@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
+    ap.add_argument("--no-async0", action="store_true",
+                    help="prefix-kill stages: a round-0 pass and settle before the asynchronous launch (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
@@ -593,7 +595,7 @@ class PartitionedBench:
         # rank (dv_comm_set_mode 0 picks it when the epoch fits)
         cap = max(int(max_txn_rank * R * 1.4), CONFIGS[a.config][1] * R) + 65536
         self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
-                                 part_id=rank, timing=TIMING[a.timing])
+                                 part_id=rank, timing=TIMING[a.timing], async0=not a.no_async0)
         self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
@@ -722,7 +724,8 @@ def main():
                                       mpr=mpr)
         epochs = gen_epochs(gen, n_txn_total, 0, n_epochs)
         t_gen = time.perf_counter() - t_gen
-        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
+        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing],
+                            async0=not a.no_async0)
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)

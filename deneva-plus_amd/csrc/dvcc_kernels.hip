@@ -94,7 +94,8 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                                                   uint8_t *__restrict__ tlen,
                                                   uint32_t *__restrict__ acc_row, Counters *ctr,
                                                   uint32_t *__restrict__ counts, uint32_t ntiles,
-                                                  uint32_t pair_limit, const uint64_t *__restrict__ ts) {
+                                                  uint32_t pair_limit, const uint64_t *__restrict__ ts,
+                                                  uint32_t *__restrict__ tword) {
     // The first radix pass's histogram (digit = row bits [0, 8)) is counted
     // here, per 4096-access sort tile, so the sort skips that k_radix_hist
     // launch and its 8-byte-per-access re-read of the pairs.
@@ -239,6 +240,9 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 if (i + 1 == n || nt != txn[j]) {
                     tb_end[t] = (uint32_t)(i + 1);
                     if (tlen) tlen[t] = (uint8_t)(big ? (1u << slog) : pos + 1);
+                    // the prefix's fact words for its one asynchronous launch
+                    // (round_async0): no access OK yet
+                    if (tword && t < pair_limit) tword[t] = (big ? (1u << slog) : pos + 1) << 16;
                 }
             }
         }
@@ -324,9 +328,10 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t slog, uint64_t *__restrict__ pairs,
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
-                                                  Counters *ctr, uint32_t pair_limit, const uint64_t *__restrict__ ts) {
+                                                  Counters *ctr, uint32_t pair_limit, const uint64_t *__restrict__ ts,
+                                                  uint32_t *__restrict__ tword) {
     probe_body<false>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                      ctr, nullptr, 0, pair_limit, ts);
+                      ctr, nullptr, 0, pair_limit, ts, tword);
 }
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     Tables tabs, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ keys32,
@@ -336,14 +341,14 @@ __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
     uint32_t ntiles, const uint64_t *__restrict__ ts) {
     probe_body<true>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                     ctr, counts, ntiles, n_txn, ts);
+                     ctr, counts, ntiles, n_txn, ts, nullptr);
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts) {
+                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts, uint32_t *tword) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
     if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
@@ -357,7 +362,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     else
         DV_LAUNCH_EV(k_probe, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
                               tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              pair_limit < n_txn ? pair_limit : n_txn, ts);
+                              pair_limit < n_txn ? pair_limit : n_txn, ts, pair_limit < n_txn ? tword : nullptr);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -878,8 +883,11 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
                                                         uint4 *__restrict__ zero, uint64_t zero_n, int gate,
                                                         Counters *hctr, unsigned long long *hseq,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq, uint32_t *__restrict__ carry,
+                                                        uint32_t G) {
     if (blockIdx.x == 0) {
+        // a prefix-kill epoch's asynchronous slices start pessimistic (round_async0)
+        for (uint32_t g = threadIdx.x; g < G; g += kBlock) carry[g] = kAsyncCarryInit;
         // pipelined epochs: the previous epoch's counters into their host
         // mirror first (what k_ctr_out would have done as one more launch)
         if (hctr) {
@@ -935,13 +943,14 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
-                        Counters *hctr, unsigned long long *hseq, unsigned long long seq) {
+                        Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint32_t *carry,
+                        uint32_t G) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
-                                       gate ? 1 : 0, hctr, hseq, seq);
+                                       gate ? 1 : 0, hctr, hseq, seq, carry, carry ? G : 0u);
 }
 
 // ---------------------------------------------------------------- execute

@@ -79,13 +79,15 @@ uint64_t row_state_words(uint64_t rows) { return (((rows + 15) / 16 + 3) & ~3ull
 // atomic per block (one device-scope atomic per access on a shared word ran
 // at ~88 per us); other rows go straight to the bitmap and the Bloom filter.
 constexpr int kMarkBlock = 1024;  // (16 KiB of LDS per block)
-__global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(const uint8_t *__restrict__ status,
+__global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict__ status,
                                                             const uint32_t *__restrict__ tb_start,
                                                             const uint32_t *__restrict__ tb_end,
                                                             const uint32_t *__restrict__ acc_row, uint32_t K,
                                                             uint32_t *__restrict__ row_state, uint64_t state_words,
                                                             uint32_t *__restrict__ bloom, int nowait,
-                                                            Counters *__restrict__ ctr) {
+                                                            Counters *__restrict__ ctr,
+                                                            const uint32_t *__restrict__ words,
+                                                            uint32_t *__restrict__ carry, uint32_t G) {
     __shared__ uint32_t s_hot[kHotWords];
     if (input_err(ctr)) return;
     // queued behind the prefix's rounds with no host wait: when they halted
@@ -96,12 +98,25 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(const uint8_t *__res
         if (blockIdx.x == 0 && threadIdx.x == 0) ctr->a_halt = 1u;
         return;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0)  // (round 0, then the asynchronous iterations)
-        ctr->a_rounds = ctr->async_r0 ? ctr->async_r0 + ctr->async_iters : 1u;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (round 0, then the asynchronous iterations)
+        ctr->a_rounds = ctr->async0 ? ctr->async_iters : (ctr->async_r0 ? ctr->async_r0 + ctr->async_iters : 1u);
+        // the survivors' stage starts with no asynchronous try behind it
+        ctr->async0 = ctr->async_go = ctr->async_r0 = ctr->async_iters = ctr->async_block = 0;
+    }
+    if (blockIdx.x == 0)
+        for (uint32_t g = threadIdx.x; g < G; g += kMarkBlock) carry[g] = kAsyncCarryInit;
     for (uint32_t i = threadIdx.x; i < kHotWords; i += kMarkBlock) s_hot[i] = 0;
     __syncthreads();
+    uint32_t und = 0;
     for (uint32_t t = blockIdx.x * kMarkBlock + threadIdx.x; t < K; t += gridDim.x * kMarkBlock) {
-        if (status[t] != ST_COMMIT) continue;
+        if (words) {  // decided by round_async0: the status bytes from the fact words
+            const uint8_t st = word_status(words[t]);
+            status[t] = st;
+            und += st == ST_UNDEC ? 1u : 0u;
+            if (st != ST_COMMIT) continue;
+        } else if (status[t] != ST_COMMIT) {
+            continue;
+        }
         for (uint32_t a = tb_start[t], e = tb_end[t]; a < e; a++) {
             const uint32_t ar = acc_row[a];
             const uint32_t row = ar & ~AR_WR;
@@ -115,6 +130,10 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(const uint8_t *__res
                 atomicOr(&bloom[h >> 5], 1u << (h & 31u));
             }
         }
+    }
+    if (und) {  // cannot happen: the launch decided every txn or yielded (halt)
+        set_err(ctr, ERRB_SPIN);
+        atomicMax(&ctr->spin_site, 2u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < kHotWords && i < state_words; i += kMarkBlock) {
@@ -202,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     uint8_t *__restrict__ status, uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
     uint8_t *__restrict__ tlen_b,
     uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-    Counters *ctr) {
+    Counters *ctr, uint32_t *__restrict__ tword_b) {
     __shared__ uint32_t s_tile;
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
@@ -269,6 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         map[sub] = first + j;
         tlen_b[sub] = (uint8_t)lens[j];
         status_b[sub] = ST_UNDEC;
+        if (tword_b) tword_b[sub] = lens[j] << 16;  // (round_async0: no access OK yet)
         l_a0[ls] = a0s[j];
         l_pre[ls] = la;
         la += lens[j];
@@ -308,10 +328,20 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
 // a no-op while they are halted, Counters::halt)
 __global__ __launch_bounds__(kBlock) void k_sub_scatter_back(const uint32_t *__restrict__ map,
                                                              const uint8_t *__restrict__ status_b,
-                                                             uint8_t *__restrict__ status, const Counters *ctr) {
+                                                             uint8_t *__restrict__ status, Counters *ctr,
+                                                             const uint32_t *__restrict__ words) {
     if (input_err(ctr) || ctr->halt) return;
     const uint32_t S = ctr->b_txn;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < S; i += gridDim.x * kBlock) status[map[i]] = status_b[i];
+    uint32_t und = 0;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < S; i += gridDim.x * kBlock) {
+        const uint8_t st = words ? word_status(words[i]) : status_b[i];
+        status[map[i]] = st;
+        und += st == ST_UNDEC ? 1u : 0u;
+    }
+    if (und) {  // cannot happen: the launch decided every txn or yielded (halt)
+        set_err(ctr, ERRB_SPIN);
+        atomicMax(&ctr->spin_site, 2u);
+    }
 }
 
 namespace {
@@ -321,14 +351,14 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 }
 }  // namespace
 
-void launch_prefix_mark(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+void launch_prefix_mark(hipStream_t s, uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
-                        Counters *ctr) {
+                        Counters *ctr, const uint32_t *words, uint32_t *carry, uint32_t G) {
     // (the bitmap and the Bloom filter after it were zeroed by k_epoch_clear)
-    if (!K) return;
-    const uint32_t g = std::min<uint32_t>((K + kMarkBlock - 1) / kMarkBlock, 64);
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>((K + kMarkBlock - 1) / kMarkBlock, 64));
     DV_LAUNCH(k_prefix_mark, g, kMarkBlock, 0, s, status, tb_start, tb_end, acc_row, K, row_state, rs_words - kBloomWords,
-                                           row_state + (rs_words - kBloomWords), nowait, ctr);
+                                           row_state + (rs_words - kBloomWords), nowait, ctr, words, carry,
+                                           carry ? G : 0u);
 }
 
 uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKillTile; }
@@ -340,7 +370,7 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
                          uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-                         Counters *ctr) {
+                         Counters *ctr, uint32_t *tword_b) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
@@ -349,13 +379,13 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                                                                      row_state + (rs_words - kBloomWords), nowait,
                                                                      kill_bits, ctr);
     DV_LAUNCH(k_kill_compact, nt, kBlock, 0, s, tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
-                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
+                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr, tword_b);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
-                             uint8_t *status, const Counters *ctr) {
+                             uint8_t *status, Counters *ctr, const uint32_t *words) {
     if (!ub) return;
-    DV_LAUNCH(k_sub_scatter_back, grid_of(ub, 2048), kBlock, 0, s, map, status_b, status, ctr);
+    DV_LAUNCH(k_sub_scatter_back, grid_of(ub, 2048), kBlock, 0, s, map, status_b, status, ctr, words);
 }
 
 }  // namespace dvcc

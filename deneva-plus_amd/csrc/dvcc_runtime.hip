@@ -174,6 +174,9 @@ struct dv_ctx {
     // prefix-kill epochs (run_prefix_epoch, dvcc_prefix.hip)
     uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 32)
     bool prefix_mode = false;     // the epoch in flight is one
+    // the stage's decisions are one round_async0 launch (statuses in tword):
+    // the prefix's (k_prefix_mark reads them), the survivors' (k_sub_scatter_back)
+    bool prefix_words = false, surv_words = false;
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
     const uint32_t *keys32 = nullptr;  // ... its keys as 32-bit row ids
@@ -1243,13 +1246,15 @@ int dv_epoch_round_wait(dv_ctx *c, uint32_t round, uint32_t *undecided) {
 namespace {
 int run_rounds(dv_ctx *c, bool resume);
 int redo_prefix(dv_ctx *c);
+int redo_survivors(dv_ctx *c);
 
 // the execution of the committed txns and the commit bytes (every execution
 // kernel is a no-op for a rejected epoch, input_err, and while the rounds
 // are halted, Counters::halt)
 void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
     if (c->prefix_mode)  // the survivors' decisions back to their txns
-        launch_sub_scatter_back(c->stream, c->b_map, c->b_status, c->v_n_txn, c->status, c->ctr);
+        launch_sub_scatter_back(c->stream, c->b_map, c->b_status, c->v_n_txn, c->status, c->ctr,
+                                c->surv_words ? c->tword : nullptr);
     if (c->cfg.workload == DV_TPCC) {
         const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
         TpccExec x{};
@@ -1323,10 +1328,12 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     if (!r && !calvin && c->h_ctr->halt) {
         // the asynchronous rounds yielded (a workgroup waited too long for
         // facts, e.g. while another kernel held CUs): the execution above was
-        // a no-op; finish the rounds synchronously, then execute
+        // a no-op; finish the rounds synchronously, then execute (a stage
+        // decided by one launch from round 0 has no round state to resume
+        // from: its rounds start again)
         r = hip_fail(hipMemsetAsync(&c->ctr->halt, 0, sizeof(uint32_t), c->stream), "memset");
         c->async_unconfirmed = false;
-        if (!r) r = run_rounds(c, true);
+        if (!r) r = c->prefix_mode && c->surv_words ? redo_survivors(c) : run_rounds(c, true);
         if (!r) {
             rec(c, 4);
             enqueue_exec(c, d_commit);
@@ -1348,7 +1355,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
                          c->h_ctr->spin_site);
         return r;
     }
-    if (!calvin && c->h_ctr->async_r0) {  // an asynchronous launch decided the rest
+    if (!calvin && (c->h_ctr->async_r0 || c->h_ctr->async0)) {  // an asynchronous launch decided the rest
         uint32_t left = 0;
         for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
         if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
@@ -1569,11 +1576,25 @@ bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {
     return prefix_size(c, ep->n_txn) < ep->n_txn;
 }
 
-// The rounds of one stage: round 0, then every remaining decision in one
+// A stage of n_txn txns can be decided by ONE launch from round 0
+// (round_async0): its round elements fit 32 bits and asynchronous rounds are
+// on.  The kernel that makes the stage then writes its fact words (the probe,
+// k_kill_compact) and the one before it its carries (k_epoch_clear,
+// k_prefix_mark).
+bool async0_possible(const dv_ctx *c, uint32_t n_txn) {
+    return round_el32(n_txn, c->slog) && c->async_g &&
+           !(c->cfg.flags & (DV_FLAG_EL64 | DV_FLAG_NO_ASYNC | DV_FLAG_NO_ASYNC0));
+}
+
+// The rounds of one stage: one asynchronous launch from round 0 when the
+// stage's words are ready (async0; *words = true: the statuses stay in the
+// fact words), else round 0, then every remaining decision in one
 // asynchronous launch (stages are small: a declined or yielded try halts and
 // the synchronous rounds resume), or the pipelined loop when asynchronous
 // rounds are off.
-int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
+int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub, bool async0 = false,
+                 bool *words = nullptr) {
+    if (words) *words = false;
     c->rounds = 0;
     c->rounds_real = 0;
     c->async_unconfirmed = false;
@@ -1586,6 +1607,14 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub) {
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
     const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     if (!async) return run_rounds(c, false);
+    if (async0 && words) {
+        c->async_launched++;
+        c->async_unconfirmed = true;
+        *words = true;
+        round_async0(c->stream, round_bufs(c), c->cfg.cc_alg != DV_OCC, c->async_g, c->abounds, c->tword,
+                     c->async_max_iters, c->async_idle_ticks);
+        return hip_fail(hipGetLastError(), "stage launch");
+    }
     round0_then_async(c);  // (v_thresh: whatever fits the workgroups)
     return hip_fail(hipGetLastError(), "stage rounds");
 }
@@ -1599,20 +1628,33 @@ int enqueue_survivors(dv_ctx *c) {
     const bool nowait = c->cfg.cc_alg != DV_OCC;
     const uint64_t rs_words = row_state_words(row_space(c));
     const uint32_t K = c->pf_K;
+    const bool a0 = async0_possible(c, c->n_txn - K);
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
-                       c->ctr);
+                       c->ctr, c->prefix_words ? c->tword : nullptr, a0 ? c->abounds : nullptr, c->async_g);
     const uint32_t tag = next_tag(c);
     launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, K, c->n_txn, c->row_state,
                         rs_words, nowait,
                         c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
-                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
+                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr, a0 ? c->tword : nullptr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
     c->v_tlen = c->b_tlen;
     c->v_n_txn = c->n_txn - K;
     c->v_n_txn_dev = &c->ctr->b_txn;
-    return stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc);
+    return stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, a0, &c->surv_words);
+}
+
+// The survivors' one launch (round_async0) yielded or declined: nothing
+// behind it executed, and it leaves no round state to resume from, so their
+// rounds run again from round 0, synchronously (their status bytes are still
+// undecided; the greedy's fixpoint is the same).
+int redo_survivors(dv_ctx *c) {
+    const uint32_t flags = c->cfg.flags;
+    c->cfg.flags |= DV_FLAG_NO_ASYNC;
+    int r = stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, false, &c->surv_words);
+    c->cfg.flags = flags;
+    return r;
 }
 
 // The prefix's rounds halted (an asynchronous try yielded or declined) and
@@ -1631,7 +1673,7 @@ int redo_prefix(dv_ctx *c) {
     c->v_thresh = 0;
     const uint32_t flags = c->cfg.flags;
     c->cfg.flags |= DV_FLAG_NO_ASYNC;
-    int r = stage_rounds(c, &c->ctr->a_acc, c->pf_ub_a);
+    int r = stage_rounds(c, &c->ctr->a_acc, c->pf_ub_a, false, &c->prefix_words);
     c->cfg.flags = flags;
     if (r) return r;
     c->rounds_prefix = c->rounds_real ? c->rounds_real : c->rounds;
@@ -1673,18 +1715,20 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     const int key_bits = bits_for(row_space(c));
     c->sort_passes = radix_passes(key_bits, false);
     c->prefix_mode = true;
+    c->prefix_words = c->surv_words = false;
+    const bool a0 = async0_possible(c, K);  // the prefix in one launch from round 0
     rec(c, 0);
     const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
     c->mir_pending = false;
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
                        c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate,
                        mir ? c->d_mir[c->mir_slot] : nullptr, mir ? c->d_mseq[c->mir_slot] : nullptr,
-                       mir ? c->mir_seq : 0ull);
+                       mir ? c->mir_seq : 0ull, a0 ? c->abounds : nullptr, c->async_g);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
-                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr);
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, a0 ? c->tword : nullptr);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         r = comm_combine_errors(c);
@@ -1706,7 +1750,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->pf_sorted_a = c->sorted;
     c->pf_key_bits = key_bits;
     c->pf_n_acc = ep->n_acc;
-    r = stage_rounds(c, &c->ctr->a_acc, ub_a);
+    r = stage_rounds(c, &c->ctr->a_acc, ub_a, a0, &c->prefix_words);
     // the prefix's rounds ran synchronously (no asynchronous try): their count
     // is known here; else k_prefix_mark records it (Counters::a_rounds)
     c->rounds_prefix = c->async_unconfirmed ? 0u : (c->rounds_real ? c->rounds_real : c->rounds);
@@ -1815,7 +1859,7 @@ int pipe_complete(dv_ctx *c, const EpochSnap &sn, dv_stats *st, bool *halted) {
         return DV_OK;
     }
     uint32_t rounds_real = sn.rounds_real;
-    if (hc->async_r0) {
+    if (hc->async_r0 || hc->async0) {
         uint32_t left = 0;
         for (const CtrSlot &sl : hc->slot) left += sl.undecided;
         if (left) return DV_ERR_STATE;

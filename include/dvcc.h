@@ -119,6 +119,12 @@ extern "C" {
                                rounds finish the epoch -- correct either way,
                                this flag only skips the attempt) */
 
+#define DV_FLAG_NO_ASYNC0 64u /* prefix-kill stages run round 0 as a pass and a
+                              settle before their asynchronous launch instead
+                              of deciding everything in one launch from the
+                              sorted accesses (round_async0; A/B and testing:
+                              same decisions) */
+
 typedef struct dv_ctx dv_ctx;
 
 typedef struct dv_config {

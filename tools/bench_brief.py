@@ -1,0 +1,19 @@
+"""One-screen summary of a bench.py JSON line: headline, roofline, kernel table."""
+import json
+import sys
+
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(f"value {d['value']:.4g} {d['unit']}  ms/step {d['ms_per_step']:.4f}  abort {d.get('abort_rate', 0):.4f}")
+r = d["roofline"]
+print(f"roofline {r['kernel']}: {r['achieved']:.1f} GB/s frac {r['frac']:.4f} share {r.get('share_of_epoch', 0):.3f}")
+if "k_probe" in r:
+    p = r["k_probe"]
+    print(f"  k_probe: {p['achieved']:.1f} GB/s frac {p['frac']:.4f} avg {p['avg_launch_ms'] * 1e3:.1f} us")
+print(f"kernel us/epoch {d.get('kernel_us_per_epoch', 0):.1f}; stages {d.get('stage_ms_mean')}")
+for k in d.get("kernels", []):
+    print(f"  {k['kernel']:<22} x{k['launches_per_epoch']:5.2f} {k['avg_us']:8.1f} us  {k['us_per_epoch']:8.1f} us/ep"
+          f"  {k['share']:.3f}  frac {k.get('frac', float('nan')):.4f}")
+for key in ("cpu_baseline", "closed_loop_retry", "sort"):
+    if key in d:
+        v = d[key]
+        print(key, {a: b for a, b in v.items() if not isinstance(b, (dict, list)) and a != "sample"})
