@@ -292,8 +292,11 @@ inline int radix_passes(int key_bits, bool hist0_done) {
     const int w = radix_digit_bits(key_bits, hist0_done);
     return (key_bits + w - 1) / w;
 }
+// tickets (optional): one zeroed arrival counter per pass -- sorts of at most
+// 256 tiles then fold each pass's digit scan into its histogram launch
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev);
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev,
+                    uint32_t *tickets = nullptr);
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
                         const uint32_t *tb_start, uint64_t *el, Counters *ctr);

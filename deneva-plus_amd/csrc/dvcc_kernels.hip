@@ -415,13 +415,85 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
         counts[(uint64_t)d * nblocks + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
 }
 
+// Small sorts (the prefix's and the survivors' keys: <= kFusedScanTiles
+// tiles): the histogram and the digit scan in ONE launch.  Every tile
+// publishes its counts write-through (sc1 stores), waits for them, and adds
+// one arrival to a ticket; the tile whose add comes last scans every digit's
+// counts with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1) -- one
+// kernel boundary fewer per pass, where these launch-bound sorts spend it.
+constexpr uint32_t kFusedScanTiles = 256;
+__global__ __launch_bounds__(kBlock) void k_radix_hist_scan(const uint64_t *__restrict__ in, uint64_t n, int shift,
+                                                            uint32_t *__restrict__ counts, uint32_t nblocks,
+                                                            const uint32_t *__restrict__ n_dev,
+                                                            uint32_t *__restrict__ digit_tot,
+                                                            uint32_t *__restrict__ ticket) {
+    __shared__ uint32_t wc[4][kRadix];
+    __shared__ uint32_t s_last;
+    n = sort_n(n, n_dev);
+    const uint32_t tiles = nblocks_for(n);
+    if (blockIdx.x >= tiles) return;  // (past a device-side count: no arrival)
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    for (uint32_t d = tid; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * kTile + wave * (64 * kIPT);
+    uint64_t k[kIPT];
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        k[j] = idx < n ? in[idx] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < kIPT; j++) {
+        const uint64_t idx = base + j * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        const uint64_t vmask = __ballot(valid);
+        if (__ballot(valid && d == d0) == vmask) {
+            if (lane == 0) wc[wave][d0] += (uint32_t)__popcll(vmask);
+        } else if (valid) {
+            atomicAdd(&wc[wave][d], 1u);
+        }
+    }
+    __syncthreads();
+    {
+        const uint32_t d = tid;  // kBlock == kRadix
+        __hip_atomic_store(&counts[(uint64_t)d * nblocks + blockIdx.x], wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) s_last = atomicAdd(ticket, 1u) == tiles - 1 ? 1u : 0u;
+    __syncthreads();
+    if (!s_last || tiles > kFusedScanTiles) return;  // (more tiles: k_radix_scan follows and scans them)
+    // the last tile: every digit's exclusive scan over the tiles, in place
+    const uint32_t d = tid;
+    uint32_t *c = counts + (uint64_t)d * nblocks;
+    uint32_t v[kFusedScanTiles / 16];  // 16 tiles per step, loads in flight together
+    uint32_t run = 0;
+    for (uint32_t t0 = 0; t0 < tiles; t0 += kFusedScanTiles / 16) {
+#pragma unroll
+        for (uint32_t q = 0; q < kFusedScanTiles / 16; q++)
+            v[q] = t0 + q < tiles ? __hip_atomic_load(&c[t0 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kFusedScanTiles / 16; q++) {
+            if (t0 + q < tiles) c[t0 + q] = run;
+            run += v[q];
+        }
+    }
+    digit_tot[d] = run;
+}
+
 // exclusive scan of counts[d][0..nblocks) in place, one workgroup per digit
+// fused_upto: behind k_radix_hist_scan, which has scanned a device-side count
+// of at most that many tiles itself (then nothing to do here)
 __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ counts, uint32_t nblocks,
                                                        uint32_t *__restrict__ digit_tot,
-                                                       const uint32_t *__restrict__ n_dev) {
+                                                       const uint32_t *__restrict__ n_dev, uint32_t fused_upto) {
     __shared__ uint32_t lds4[4];
     uint32_t *c = counts + (uint64_t)blockIdx.x * nblocks;  // (row stride: the upper bound)
     if (n_dev && nblocks_for(*n_dev) < nblocks) nblocks = nblocks_for(*n_dev);
+    if (nblocks <= fused_upto) return;
     const uint32_t per = (nblocks + kBlock - 1) / kBlock;
     const uint32_t lo = threadIdx.x * per;
     uint32_t hi = lo + per;
@@ -657,13 +729,14 @@ template <int W>
 void wide_pass(hipStream_t s, const uint64_t *in, uint64_t *out, uint64_t n, int shift, uint32_t *counts,
                uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1) {
     DV_LAUNCH((k_radix_hist_w<W>), nb, kBlock, 0, s, in, n, shift, counts, nb, n_dev);
-    DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev);
+    DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev, 0u);
     DV_LAUNCH_EV((k_radix_scatter_w<W>), nb, kBlock, 0, s, e0, e1, in, out, n, shift,
                           (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
 }
 
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev) {
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev,
+                    uint32_t *tickets) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
@@ -681,8 +754,18 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
     }
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        if (pass > 0 || !hist0_done) DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
-        DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev);
+        // small sorts: the scan folded into the histogram launch; a device-side
+        // count under a larger host bound keeps a scan launch behind it, a
+        // no-op unless the count turned out larger
+        const bool fuse = tickets && (pass > 0 || !hist0_done) && (nb <= kFusedScanTiles || n_dev);
+        if (fuse) {
+            DV_LAUNCH(k_radix_hist_scan, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev, digit_tot,
+                      tickets + pass);
+        } else if (pass > 0 || !hist0_done) {
+            DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
+        }
+        if (!fuse || nb > kFusedScanTiles)
+            DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev, fuse ? kFusedScanTiles : 0u);
         // timing: events recorded by the dispatch itself (no extra packets)
         DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, scatter_ev ? scatter_ev[2 * pass] : nullptr, scatter_ev ? scatter_ev[2 * pass + 1] : nullptr,
                               (const uint64_t *)pairs[cur], pairs[cur ^ 1], n, shift,

@@ -383,7 +383,19 @@ uint32_t *next_ticket(dv_ctx *c) {
 // 167 us of scatters per config-D epoch against 125 us for the three-launch
 // passes.)
 int sort_rows(dv_ctx *c, uint64_t n, int key_bits, hipEvent_t *ev, bool hist0_done, const uint32_t *n_dev) {
-    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev);
+    // (one zeroed arrival ticket per pass for the fused histogram + scan)
+    constexpr uint32_t kSortTickets = 8;
+    uint32_t pos = c->ticket % kTileCtrs;
+    if (pos + kSortTickets > kTileCtrs) {  // (not across the wrap: skip to it)
+        c->ticket += kTileCtrs - pos;
+        pos = 0;
+    }
+    if (c->ticket > 0 && pos == 0)  // the wrap: zeroed again, as next_ticket does
+        (void)hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream);
+    uint32_t *tickets = &c->tile_ctr[pos];
+    c->ticket += kSortTickets;
+    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev,
+                           tickets);
 }
 
 Tables make_tables(dv_ctx *c) {
