@@ -24,12 +24,19 @@
 // over torch.distributed.
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
 #include <mutex>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "dvcc_common.h"
@@ -853,6 +860,133 @@ struct LocalXport final : Xport {
     }
 };
 
+// P processes of one node (e.g. several ranks on one GPU, which RCCL
+// refuses: ncclCommInitRank "invalid usage"), for testing the protocols across
+// real process boundaries.  Each rank exports one device staging buffer
+// through a HIP IPC handle and publishes it, with its all-to-allv offsets,
+// in a POSIX shared-memory segment that also holds a process-shared barrier.
+// A collective: the rank copies its payload into its staging buffer and
+// drains its stream; barrier; it pulls from the peers' staging buffers
+// (device copies, or a MAX kernel over them) and drains again; barrier -- so
+// no peer still reads a staging buffer when it is written next.  Host-
+// synchronous by design: test infrastructure, the product's transport is RCCL.
+constexpr int kMaxIpcRanks = kMaxLocalRanks;
+struct IpcShm {
+    std::atomic<uint32_t> arrived, gen, joined;
+    uint32_t P;
+    struct Slot {
+        hipIpcMemHandle_t h;
+        uint64_t sd[kMaxIpcRanks];  // this rank's all-to-allv send offsets
+        uint64_t staging_bytes;
+        int32_t device;
+    } slot[kMaxIpcRanks];
+};
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics");
+
+struct IpcXport final : Xport {
+    IpcShm *shm = nullptr;
+    int P = 0, r = 0;
+    uint8_t *staging = nullptr;  // this rank's, exported
+    uint64_t staging_cap = 0;
+    uint8_t *peer[kMaxIpcRanks] = {};  // every rank's staging buffer (own included)
+    uint8_t *scratch = nullptr;
+    uint64_t scratch_cap = 0;
+    ~IpcXport() override {
+        for (int q = 0; q < P; q++)
+            if (q != r && peer[q]) (void)hipIpcCloseMemHandle(peer[q]);
+        if (staging) (void)hipFree(staging);
+        if (scratch) (void)hipFree(scratch);
+        if (shm) (void)munmap(shm, sizeof(IpcShm));
+    }
+    // every rank arrives; a rank that does not come within 120 s (it died or
+    // left the protocol) fails the others instead of hanging them
+    int barrier() {
+        const uint32_t g = shm->gen.load(std::memory_order_acquire);
+        if (shm->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == (uint32_t)P) {
+            shm->arrived.store(0, std::memory_order_relaxed);
+            shm->gen.fetch_add(1, std::memory_order_acq_rel);
+            return DV_OK;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        while (shm->gen.load(std::memory_order_acquire) == g) {
+            std::this_thread::yield();
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) return DV_ERR_STATE;
+        }
+        return DV_OK;
+    }
+    int stage(const uint8_t *src, uint64_t bytes, hipStream_t s) {
+        if (bytes > staging_cap) return DV_ERR_ARG;
+        if (bytes) CHK(hip_fail2(hipMemcpyAsync(staging, src, bytes, hipMemcpyDeviceToDevice, s), "stage"));
+        CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+        return barrier();
+    }
+    int drain(hipStream_t s) {
+        CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+        return barrier();
+    }
+    int all_to_all_u64(const uint64_t *send, uint64_t *recv, hipStream_t s) override {
+        CHK(stage(reinterpret_cast<const uint8_t *>(send), 8ull * P, s));
+        for (int q = 0; q < P; q++)
+            CHK(hip_fail2(hipMemcpyAsync(recv + q, peer[q] + 8ull * r, 8, hipMemcpyDeviceToDevice, s), "copy"));
+        return drain(s);
+    }
+    int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv, const size_t *rc,
+                    const size_t *rd, hipStream_t s) override {
+        uint64_t end = 0;
+        for (int q = 0; q < P; q++) {
+            shm->slot[r].sd[q] = sd[q];
+            end = std::max<uint64_t>(end, sd[q] + sc[q]);
+        }
+        CHK(stage(send, end, s));
+        for (int q = 0; q < P; q++)
+            if (rc[q])
+                CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], peer[q] + shm->slot[q].sd[r], rc[q],
+                                             hipMemcpyDeviceToDevice, s), "copy"));
+        return drain(s);
+    }
+    template <class T>
+    int max_t(T *buf, uint64_t n, hipStream_t s) {
+        if (n * sizeof(T) > scratch_cap) {
+            CHK(hip_fail2(hipStreamSynchronize(s), "sync"));
+            if (scratch) (void)hipFree(scratch);
+            scratch = nullptr;
+            scratch_cap = 0;
+            CHK(alloc(&scratch, n * sizeof(T)));
+            scratch_cap = n * sizeof(T);
+        }
+        CHK(stage(reinterpret_cast<const uint8_t *>(buf), n * sizeof(T), s));
+        PeerPtrs<T> in{};
+        for (int q = 0; q < P; q++) in.p[q] = reinterpret_cast<const T *>(peer[q]);
+        if (n) {
+            const uint64_t blocks = std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
+            DV_LAUNCH((k_max_reduce<T>), (uint32_t)blocks, kBlock, 0, s, in, P, reinterpret_cast<T *>(scratch), n);
+            CHK(hip_fail2(hipGetLastError(), "k_max_reduce"));
+        }
+        CHK(drain(s));
+        if (n) CHK(hip_fail2(hipMemcpyAsync(buf, scratch, n * sizeof(T), hipMemcpyDeviceToDevice, s), "copy"));
+        return DV_OK;
+    }
+    int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int max_u64(uint64_t *buf, uint64_t n, hipStream_t s) override { return max_t(buf, n, s); }
+    int all_gather(const uint8_t *send, size_t bytes, uint8_t *recv, hipStream_t s) override {
+        CHK(stage(send, bytes, s));
+        for (int q = 0; q < P; q++)
+            if (bytes)
+                CHK(hip_fail2(hipMemcpyAsync(recv + (size_t)q * bytes, peer[q], bytes, hipMemcpyDeviceToDevice, s),
+                              "copy"));
+        return drain(s);
+    }
+};
+
+// the largest payload one collective of a context's protocols stages
+uint64_t ipc_staging_bytes(const dv_config &cfg, uint32_t P) {
+    const uint64_t acc = cfg.max_acc, txn = cfg.max_txn;
+    uint64_t b = std::max<uint64_t>(acc * sizeof(dv_access), 8 * txn);  // records; o_ids (TPC-C)
+    b = std::max<uint64_t>(b, 8ull * (kGroupRecHead + P) + 64);          // vote records
+    return (b + 255) & ~255ull;
+}
+
 void free_bufs(DvComm *m) {
     if (m->h_mail) (void)hipHostFree(m->h_mail);
     m->h_mail = m->d_mail = nullptr;
@@ -973,6 +1107,60 @@ int dv_comm_init(dv_ctx *c, const void *unique_id, int nranks, int rank) {
         slot = nullptr;
     }
     return r;
+}
+
+int dv_comm_init_ipc(dv_ctx *c, const char *name, int nranks, int rank) {
+    if (!c || !name || name[0] != '/' || nranks < 1 || nranks > kMaxIpcRanks || rank < 0 || rank >= nranks)
+        return DV_ERR_ARG;
+    const dv_config &cfg = ctx_config(c);
+    if ((int)cfg.part_cnt != nranks || (int)cfg.part_id != rank) return DV_ERR_ARG;
+    CHK(hip_fail2(hipSetDevice(cfg.device), "hipSetDevice"));
+    DvComm *&slot = ctx_comm(c);
+    comm_free(slot);
+    slot = nullptr;
+    // the segment: created by whoever comes first, sized once
+    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return DV_ERR_STATE;
+    const int tr = ftruncate(fd, sizeof(IpcShm));
+    void *mp = tr == 0 ? mmap(nullptr, sizeof(IpcShm), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+    close(fd);
+    if (mp == MAP_FAILED) return DV_ERR_STATE;
+    IpcXport *x = new IpcXport();
+    x->shm = static_cast<IpcShm *>(mp);  // (a fresh segment is zero-filled: counters start at 0)
+    x->P = nranks;
+    x->r = rank;
+    DvComm *m = new DvComm();
+    m->nranks = nranks;
+    m->rank = rank;
+    m->x = x;
+    auto fail = [&](int r) {
+        comm_free(m);
+        return r;
+    };
+    x->staging_cap = ipc_staging_bytes(cfg, (uint32_t)nranks);
+    int r = alloc(&x->staging, x->staging_cap);
+    if (!r) r = hip_fail2(hipIpcGetMemHandle(&x->shm->slot[rank].h, x->staging), "hipIpcGetMemHandle");
+    if (r) return fail(r);
+    x->shm->slot[rank].staging_bytes = x->staging_cap;
+    x->shm->slot[rank].device = cfg.device;
+    x->shm->joined.fetch_add(1, std::memory_order_acq_rel);
+    r = x->barrier();  // every handle published
+    for (int q = 0; q < nranks && !r; q++) {
+        if (q == rank) {
+            x->peer[q] = x->staging;
+            continue;
+        }
+        void *p = nullptr;
+        r = hip_fail2(hipIpcOpenMemHandle(&p, x->shm->slot[q].h, hipIpcMemLazyEnablePeerAccess),
+                      "hipIpcOpenMemHandle");
+        x->peer[q] = static_cast<uint8_t *>(p);
+    }
+    if (!r) r = x->barrier();  // every rank opened its peers: the name can go
+    if (!r && rank == 0) (void)shm_unlink(name);
+    if (!r) r = reserve(m, cfg.max_acc, cfg.max_txn, cfg.workload == DV_TPCC);
+    if (r) return fail(r);
+    slot = m;
+    return DV_OK;
 }
 
 int dv_comm_init_local(dv_ctx **ctxs, int nranks) {

@@ -134,6 +134,7 @@ SIGNATURES = [
     ("dv_comm_unique_id", ctypes.c_int, [_vp]),
     ("dv_comm_init", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     ("dv_comm_init_local", ctypes.c_int, [_P(_vp), ctypes.c_int]),
+    ("dv_comm_init_ipc", ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]),
     ("dv_epoch_run_part", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _vp, _P(Stats)]),
     ("dv_epoch_round_local", ctypes.c_int, [_vp, _vp]),
     ("dv_epoch_round_apply", ctypes.c_int, [_vp, _vp, _P(ctypes.c_uint32)]),

@@ -319,6 +319,11 @@ class CCEngine:
         arr = (ctypes.c_void_p * len(engines))(*[e._ctx.value for e in engines])
         L.check(L.lib().dv_comm_init_local(arr, len(engines)), "dv_comm_init_local")
 
+    def comm_init_ipc(self, name, nranks, rank):
+        """Partitioned epochs among PROCESSES of this node (dv_comm_init_ipc):
+        every rank passes the same fresh shared-memory name ("/...")."""
+        L.check(L.lib().dv_comm_init_ipc(self._ctx, name.encode(), nranks, rank), "dv_comm_init_ipc")
+
     def comm_set_mode(self, mode):
         """dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible."""
         L.check(L.lib().dv_comm_set_mode(self._ctx, mode), "dv_comm_set_mode")

@@ -323,6 +323,15 @@ int dv_comm_init(dv_ctx *ctx, const void *unique_id, int nranks, int rank);
  * barrier, so each context must be driven by its own host thread
  * (dv_epoch_run_part called concurrently).  Same protocol, same decisions. */
 int dv_comm_init_local(dv_ctx **ctxs, int nranks);
+/* the same partitioned epochs for nranks (<= 16) PROCESSES of one node, one
+ * context each -- e.g. several ranks sharing one GPU, which RCCL refuses --
+ * for testing the protocols across real process boundaries: each rank exports
+ * a device staging buffer through a HIP IPC handle and meets the others at a
+ * barrier in the POSIX shared-memory segment `name` ("/..." , the same string
+ * on every rank, unused before; rank 0 unlinks it once all have joined).
+ * Collectives are host-synchronous here (test transport; RCCL is the
+ * product's).  Same protocol, same decisions. */
+int dv_comm_init_ipc(dv_ctx *ctx, const char *name, int nranks, int rank);
 int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st);
 /* how dv_epoch_run_part runs a YCSB epoch.  The list protocol above moves

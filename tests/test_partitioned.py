@@ -702,6 +702,17 @@ def test_epoch_groups_prefix_kill():
 
 
 @pytest.mark.gpu
+@pytest.mark.slow
+def test_epoch_groups_config_d_size():
+    """The N>1 headline's exact shape: config D at 8 partitions -- 16,777,216
+    rows per partition, 131,072 txns per batch (1,048,576-txn epochs), zipf
+    0.9, MPR 0.1 -- one group of 8 epochs, NO_WAIT: every epoch's commit
+    bytes, the digests and every partition's rows against the oracle running
+    the 8 sequenced epochs one after the other."""
+    _check_epoch_groups(dvcc.NO_WAIT, 8, 16_777_216, 131_072, 0.1, groups=1)
+
+
+@pytest.mark.gpu
 def test_epoch_group_batch_stops_at_failing_group():
     """dv_epoch_group_run_batch with a bad key in its second group: every
     rank returns DV_ERR_KEY_NOT_FOUND, the first group's rows stay applied,
