@@ -82,8 +82,6 @@ def parse():
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
-    ap.add_argument("--no-async0", action="store_true",
-                    help="prefix-kill stages: a round-0 pass and settle before the asynchronous launch (A/B)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
@@ -255,42 +253,36 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
     return out
 
 
-def closed_loop_leg(eng, gen, n_txn, k, d_commit):
-    """Closed loop with retries: every epoch holds n_txn
-    txns, the previous epoch's aborted ones first (dv_epoch_carry), new ones
-    from a pre-generated pool filling the rest.  Committed txns/s over k
-    epochs, the carry-over and epoch assembly included."""
-    pool_n = 2 * n_txn  # new txns are drawn in order, wrapping around
+def closed_loop_leg(eng, gen, n_txn, k, d_commit, open_ms=None):
+    """Closed loop with retries on the device
+    (dv_epoch_run_closed_loop): every epoch holds n_txn txns, the previous
+    epoch's aborted ones first, new ones from a pre-generated pool (2 x n_txn
+    txns, drawn in order, wrapping) filling the rest -- built on the device
+    behind the previous epoch's execution, nothing read back between epochs,
+    epoch k+1 queued before epoch k's outcome is read.  Committed txns/s over
+    k epochs in one call, the carry-over and epoch assembly included."""
+    pool_n = 2 * n_txn
     pool = gen.gen(pool_n, dvcc.epoch_seed(0, 999))
     dpool = dvcc.DeviceEpoch(pool)
-    tb = pool.txn_begin.astype(np.int64)
-    nxt = 0
-
-    def fresh(m):
-        nonlocal nxt
-        if nxt + m > pool_n:
-            nxt = 0
-        a, b = int(tb[nxt]), int(tb[nxt + m])
-        d = dvcc.DeviceEpoch.from_tensors(dpool.keys[a:b], dpool.types[a:b], dpool.acc_txn[a:b] - nxt, m,
-                                          max_txn_acc=dpool.max_txn_acc)
-        nxt += m
-        return d
-
-    cur = fresh(n_txn)
-    eng.run_epoch_device(cur, d_commit)  # warm: the first epoch has nothing carried
+    pb = torch.from_numpy(pool.txn_begin.astype(np.int32)).cuda()
+    commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    sts, bufs, cursor = eng.closed_loop(dpool, pb, n_txn, 2, d_commits=commits[:2])  # warm
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    committed = carried = 0
-    for _ in range(k):
-        c = eng.carry(cur, n_txn)
-        carried += c.n_txn
-        cur = dvcc.DeviceEpoch.concat(c, fresh(n_txn - c.n_txn)) if c.n_txn < n_txn else c
-        committed += eng.run_epoch_device(cur, d_commit).committed
+    sts, bufs, cursor = eng.closed_loop(dpool, pb, n_txn, k, cursor=cursor, bufs=bufs, d_commits=commits,
+                                        resume=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    return {"committed_per_s": committed / el, "ms_per_epoch": el / k * 1e3, "epochs": k,
-            "carried_per_epoch": carried / k,
-            "note": "aborted txns retried in the next epoch ahead of new ones (one-epoch penalty)"}
+    committed = sum(s.committed for s in sts)
+    carried = sum(s.n_txn - s.committed for s in sts[:-1])
+    out = {"committed_per_s": committed / el, "ms_per_epoch": el / k * 1e3, "epochs": k,
+           "carried_per_epoch": carried / max(1, k - 1),
+           "entry_point": "dv_epoch_run_closed_loop",
+           "note": "aborted txns retried in the next epoch ahead of new ones (one-epoch penalty); "
+                   "the next epoch built on the device (no host readback)"}
+    if open_ms:
+        out["vs_open_loop_ms"] = out["ms_per_epoch"] / open_ms
+    return out
 
 
 def e2e_host_leg(eng, epochs, k):
@@ -595,7 +587,7 @@ class PartitionedBench:
         # rank (dv_comm_set_mode 0 picks it when the epoch fits)
         cap = max(int(max_txn_rank * R * 1.4), CONFIGS[a.config][1] * R) + 65536
         self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
-                                 part_id=rank, timing=TIMING[a.timing], async0=not a.no_async0)
+                                 part_id=rank, timing=TIMING[a.timing])
         self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
@@ -724,8 +716,7 @@ def main():
                                       mpr=mpr)
         epochs = gen_epochs(gen, n_txn_total, 0, n_epochs)
         t_gen = time.perf_counter() - t_gen
-        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing],
-                            async0=not a.no_async0)
+        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)
@@ -801,7 +792,8 @@ def main():
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
-        out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, min(a.steps, 10), d_commit)
+        out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, max(4, min(a.steps, 10)), d_commit,
+                                                   out["ms_per_step"])
     else:
         try:
             extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group)

@@ -71,8 +71,9 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
     const uint32_t *__restrict__ ba, uint32_t max_txn, const uint64_t *__restrict__ keys,
     const uint8_t *__restrict__ types, const uint8_t *__restrict__ tables, uint64_t *__restrict__ okeys,
     uint8_t *__restrict__ otypes, uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
-    uint32_t *__restrict__ tot) {
+    uint32_t *__restrict__ tot, const uint32_t *__restrict__ skip) {
     __shared__ uint32_t lds4[4];
+    if (skip && *skip) return;  // (a refill behind a halted epoch: k_refill_plan)
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t t = blockIdx.x * kCarryTpb + threadIdx.x;
     const bool cr = t < n_txn && carried(status, t);
@@ -134,6 +135,89 @@ __global__ void k_carry_total(const uint8_t *__restrict__ status, uint32_t n_txn
     }
 }
 
+// ---- the closed loop on the device (dv_epoch_refill): the next epoch is the
+// carried txns (as above, capped at n_out), then fresh txns taken in order
+// from a pool, starting at a device-side cursor that wraps around the pool.
+// Nothing is read back: the epoch's access count stays on the device
+// (dv_epoch_dev::n_acc_dev).  An epoch whose rounds halted has no final
+// statuses yet: then every refill kernel is a no-op (the host redoes both).
+// tot: [0] carried txns, [1] their accesses, [2] aborted before the cap,
+// [3] the cursor's value, [4] skip (halted), [5] fresh txns (kRefillTot)
+__device__ __forceinline__ bool refill_skip(const Counters *ctr) {
+    return ctr && (ctr->halt || ctr->a_halt || input_err(ctr));  // (no ctr: the loop's first epoch)
+}
+
+__global__ void k_refill_plan(const uint8_t *__restrict__ status, uint32_t n_txn, const uint32_t *bt, uint32_t nb,
+                              uint32_t *tot, uint32_t n_out, uint32_t *cursor, uint32_t pool_n,
+                              const Counters *ctr) {
+    uint32_t c = 0;
+    for (uint32_t t = (nb ? nb - 1 : 0) * kCarryTpb + threadIdx.x; nb && t < n_txn; t += blockDim.x)
+        c += carried(status, t) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (threadIdx.x != 0) return;
+    const uint32_t skip = refill_skip(ctr) ? 1u : 0u;
+    const uint32_t total = nb ? bt[nb - 1] + c : 0u;
+    const uint32_t C = total < n_out ? total : n_out;
+    const uint32_t cur = *cursor, F = n_out - C;
+    tot[0] = 0;
+    tot[1] = 0;
+    tot[2] = skip ? 0u : total;  // (skip: k_carry_copy copies nothing)
+    tot[3] = cur;
+    tot[4] = skip;
+    tot[5] = F;
+    if (!skip) *cursor = (uint32_t)(((uint64_t)cur + F) % pool_n);
+}
+
+// the fresh txns [cur, cur + F) of the pool (wrapping), renumbered after the
+// C carried ones, their accesses after the carried accesses; the epoch's
+// access count into *n_acc_dev
+__global__ __launch_bounds__(kBlock) void k_refill_fresh(const uint64_t *__restrict__ keys,
+                                                         const uint8_t *__restrict__ types,
+                                                         const uint8_t *__restrict__ tables,
+                                                         const uint32_t *__restrict__ txn,
+                                                         const uint32_t *__restrict__ tb, uint32_t pool_n,
+                                                         const uint32_t *__restrict__ tot, uint32_t n_out,
+                                                         uint64_t *__restrict__ okeys, uint8_t *__restrict__ otypes,
+                                                         uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
+                                                         uint32_t *__restrict__ n_acc_dev) {
+    if (tot[4]) return;
+    const uint32_t C = tot[2] < n_out ? tot[2] : n_out, A = tot[1], cur = tot[3], F = tot[5];
+    const uint32_t e1 = cur + F < pool_n ? cur + F : pool_n;     // [cur, e1) then [0, F - (e1 - cur))
+    const uint32_t n2 = F - (e1 - cur);
+    const uint32_t b1 = tb[cur], fa1 = tb[e1] - b1, fa2 = tb[n2] - tb[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_acc_dev = A + fa1 + fa2;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < fa1 + fa2; i += gridDim.x * kBlock) {
+        const bool first = i < fa1;
+        const uint32_t src = first ? b1 + i : tb[0] + (i - fa1);
+        const uint32_t t = first ? txn[src] - cur : txn[src] + (pool_n - cur);
+        okeys[A + i] = keys[src];
+        otypes[A + i] = types[src];
+        otxn[A + i] = C + t;
+        if (otables) otables[A + i] = tables ? tables[src] : 0;
+    }
+}
+
+void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                   uint32_t n_txn, const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
+                   const uint64_t *pkeys, const uint8_t *ptypes, const uint8_t *ptables, const uint32_t *ptxn,
+                   const uint32_t *ptb, uint32_t pool_n, uint32_t *cursor, uint32_t n_out, uint64_t fresh_bound,
+                   uint64_t *okeys, uint8_t *otypes, uint32_t *otxn, uint8_t *otables, uint32_t *n_acc_dev,
+                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr) {
+    const uint32_t nb = carry_blocks(n_txn);
+    if (nb) {
+        DV_LAUNCH(k_carry_count, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba);
+        DV_LAUNCH(k_carry_scan, 1, kBlock, 0, s, bt, ba, nb);
+    }
+    DV_LAUNCH(k_refill_plan, 1, 64, 0, s, status, n_txn, bt, nb, tot, n_out, cursor, pool_n, ctr);
+    if (nb)
+        DV_LAUNCH(k_carry_copy, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba, n_out, keys, types, tables,
+                  okeys, otypes, otxn, otables, tot, (const uint32_t *)(tot + 4));
+    const uint64_t g = (fresh_bound + kBlock - 1) / kBlock;
+    DV_LAUNCH(k_refill_fresh, (uint32_t)(g < 1 ? 1 : (g > 4096 ? 4096 : g)), kBlock, 0, s, pkeys, ptypes, ptables,
+              ptxn, ptb, pool_n, tot, n_out, okeys, otypes, otxn, otables, n_acc_dev);
+}
+
 uint32_t carry_blocks(uint32_t n_txn) { return n_txn ? (n_txn + kCarryTpb - 1) / kCarryTpb : 0; }
 
 void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
@@ -149,7 +233,7 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
     DV_LAUNCH(k_carry_scan, 1, kBlock, 0, s, bt, ba, nb);
     DV_LAUNCH(k_carry_total, 1, 64, 0, s, status, n_txn, bt, nb, tot);
     DV_LAUNCH(k_carry_copy, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba, max_txn, keys, types, tables,
-                                       okeys, otypes, otxn, otables, tot);
+                                       okeys, otypes, otxn, otables, tot, (const uint32_t *)nullptr);
 }
 
 }  // namespace dvcc

@@ -123,7 +123,10 @@ struct Counters {
     uint32_t b_txn, b_acc;    // prefix-kill: surviving txns after the prefix, their accesses
     uint32_t a_halt;          // prefix-kill: the prefix's rounds halted (yield / decline), nothing after ran
     uint32_t a_rounds;        // prefix-kill: rounds the prefix's decisions took (k_prefix_mark)
-    uint32_t async0;          // the (sub-)epoch's rounds ran as ONE launch from round 0 (round_async0)
+    uint32_t async_wr0;       // an accepted asynchronous launch from this round left its statuses in the
+                              // fact words, no finalize (a prefix-kill stage: k_prefix_mark /
+                              // k_sub_scatter_back read them)
+    uint32_t n_acc;           // the accesses the probe read (the real count of a device-built epoch)
     unsigned long long pass_live;  // live accesses every k_round_pass of the epoch read, summed
     unsigned long long async_live; // live accesses entering every asynchronous launch that ran, summed
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
@@ -272,7 +275,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
                   hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr,
-                  const uint64_t *ts = nullptr, uint32_t *tword = nullptr);
+                  const uint64_t *ts = nullptr, const uint32_t *n_dev = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -292,11 +295,8 @@ inline int radix_passes(int key_bits, bool hist0_done) {
     const int w = radix_digit_bits(key_bits, hist0_done);
     return (key_bits + w - 1) / w;
 }
-// tickets (optional): one zeroed arrival counter per pass -- sorts of at most
-// 256 tiles then fold each pass's digit scan into its histogram launch
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev,
-                    uint32_t *tickets = nullptr);
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev);
 
 void launch_seg_prepare(hipStream_t s, const uint64_t *pairs, uint64_t n, int calvin,
                         const uint32_t *tb_start, uint64_t *el, Counters *ctr);
@@ -393,24 +393,13 @@ constexpr uint32_t kAsyncGroups = 512;
 // yields after max_iters iterations or idle_ticks wall-clock ticks without a
 // decision; if any did, the finalize sets Counters::halt and publishes
 // pub->tl = r0 << 32 | 3 instead of closing the rounds (the host resumes them).
+// words: no finalize -- the statuses stay in tword for the stage's consumer
+// (k_prefix_mark, k_sub_scatter_back), which also checks nothing is left
+// undecided; the launch does the finalize's yield / decline bookkeeping
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
                  uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
-                 uint64_t idle_ticks, bool words_done = false);
+                 uint64_t idle_ticks, bool words_done = false, bool words = false);
 uint32_t async_groups(int device);  // co-resident workgroups (<= kAsyncGroups; 0: unusable)
-// A prefix-kill stage in ONE asynchronous launch straight from its sorted
-// pairs (b.pairs0; b.n0_dev / b.n0 accesses, b.n_txn_dev / b.n_txn0 txns): round
-// 0's classification and every decision, no pass, settle or finalize.  Before
-// it, every txn t of the stage holds tword[t] = len << 16 (probe /
-// k_kill_compact) and carry[0, G) = kAsyncCarryInit (k_epoch_clear /
-// k_prefix_mark); after it the statuses are word_status(tword[t]).  A slice
-// too large for LDS declines and halts (Counters::halt) -- as does a launch
-// whose workgroups yield -- and dv_epoch_finish decides the stage again with
-// the synchronous rounds.
-void round_async0(hipStream_t s, const RoundBufs &b, int nowait, uint32_t G, uint32_t *carry, uint32_t *tword,
-                  uint32_t max_iters, uint64_t idle_ticks);
-// an asynchronous slice's carry word before anything is known: undecided
-// blockers in front, a queue head (walks stop there)
-constexpr uint32_t kAsyncCarryInit = (1u << 31) | 16u | 8u | 2u;
 // a txn's fact word (status | OK accesses << 8 | accesses << 16) -> its status
 __device__ __forceinline__ uint8_t word_status(uint32_t w) {
     const uint32_t s = w & 0xFFu;
@@ -483,29 +472,46 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
                   const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
                   uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot);
 
+// the closed loop (dv_epoch_refill): the aborted txns of the decided epoch
+// (status, access ranges, its keys / types / tables) carried first, capped
+// at n_out, then n_out - C fresh txns of the pool (pkeys ... ptb, pool_n txns)
+// from *cursor on (advanced, wrapping), into o*; *n_acc_dev = the accesses
+// written.  fresh_bound: a bound on the fresh accesses (grid size).  A halted
+// or rejected epoch (Counters; NULL for the loop's first epoch, n_txn 0) makes
+// every kernel a no-op.  tot: kRefillTot words.
+constexpr uint32_t kRefillTot = 6;
+void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
+                   uint32_t n_txn, const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
+                   const uint64_t *pkeys, const uint8_t *ptypes, const uint8_t *ptables, const uint32_t *ptxn,
+                   const uint32_t *ptb, uint32_t pool_n, uint32_t *cursor, uint32_t n_out, uint64_t fresh_bound,
+                   uint64_t *okeys, uint8_t *otypes, uint32_t *otxn, uint8_t *otables, uint32_t *n_acc_dev,
+                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr);
+
 // ---- prefix-kill epochs (dvcc_prefix.hip)
 // the row-state bitmap (2 bits per row): its 32-bit words for `rows` rows;
 // launch_prefix_mark clears it and marks the committed prefix txns' rows
 uint64_t row_state_words(uint64_t rows);
-// words (the prefix decided by round_async0): the prefix's statuses are read
-// from its fact words and written to status; carry / G: the survivors'
-// asynchronous slices start pessimistic
+// words (the prefix's asynchronous launch left its statuses there, no
+// finalize): the prefix's statuses are read from its fact words and written
+// to status
 void launch_prefix_mark(hipStream_t s, uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
-                        Counters *ctr, const uint32_t *words, uint32_t *carry, uint32_t G);
+                        Counters *ctr, const uint32_t *words);
 uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (descriptors per array)
 // k_kill (every access after the prefix's against the row state, one bit
 // per access into kill_bits[kill_words(n_acc)]) and k_kill_compact (killed
 // txns aborted, the survivors' sub-epoch)
 uint64_t kill_words(uint64_t n_acc);
+// (n_acc_dev: the epoch's real access count when n_acc is a bound, else null)
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, uint64_t rs_words,
+                         uint64_t n_acc, const uint32_t *n_acc_dev, uint32_t K, uint32_t n_txn,
+                         const uint32_t *row_state, uint64_t rs_words,
                          int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
                          uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-                         Counters *ctr, uint32_t *tword_b);
-// words (the survivors decided by round_async0): their statuses from the fact
-// words, else from status_b
+                         Counters *ctr);
+// words (the survivors' asynchronous launch left their statuses there): their
+// statuses from the fact words, else from status_b
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,
                              uint8_t *status, Counters *ctr, const uint32_t *words);
 
@@ -517,8 +523,7 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
                         uint64_t zero_words = 0, bool gate = false, Counters *hctr = nullptr,
-                        unsigned long long *hseq = nullptr, unsigned long long seq = 0,
-                        uint32_t *carry = nullptr, uint32_t G = 0);
+                        unsigned long long *hseq = nullptr, unsigned long long seq = 0);
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,

@@ -95,7 +95,9 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                                                   uint32_t *__restrict__ acc_row, Counters *ctr,
                                                   uint32_t *__restrict__ counts, uint32_t ntiles,
                                                   uint32_t pair_limit, const uint64_t *__restrict__ ts,
-                                                  uint32_t *__restrict__ tword) {
+                                                  const uint32_t *__restrict__ n_dev) {
+    if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (the real count of a device-built epoch)
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->n_acc = (uint32_t)n;
     // The first radix pass's histogram (digit = row bits [0, 8)) is counted
     // here, per 4096-access sort tile, so the sort skips that k_radix_hist
     // launch and its 8-byte-per-access re-read of the pairs.
@@ -240,9 +242,6 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                 if (i + 1 == n || nt != txn[j]) {
                     tb_end[t] = (uint32_t)(i + 1);
                     if (tlen) tlen[t] = (uint8_t)(big ? (1u << slog) : pos + 1);
-                    // the prefix's fact words for its one asynchronous launch
-                    // (round_async0): no access OK yet
-                    if (tword && t < pair_limit) tword[t] = (big ? (1u << slog) : pos + 1) << 16;
                 }
             }
         }
@@ -329,9 +328,9 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
                                                   Counters *ctr, uint32_t pair_limit, const uint64_t *__restrict__ ts,
-                                                  uint32_t *__restrict__ tword) {
+                                                  const uint32_t *__restrict__ n_dev) {
     probe_body<false>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                      ctr, nullptr, 0, pair_limit, ts, tword);
+                      ctr, nullptr, 0, pair_limit, ts, n_dev);
 }
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     Tables tabs, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ keys32,
@@ -348,10 +347,11 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   const uint32_t *acc_txn, const uint8_t *tables, uint64_t n_acc, uint32_t n_txn,
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
-                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts, uint32_t *tword) {
+                  hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts,
+                  const uint32_t *n_dev) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
-    if (pair_limit < n_txn) counts = nullptr;  // the prefix's sort keys only: no first histogram
+    if (pair_limit < n_txn || n_dev) counts = nullptr;  // the prefix's keys only / a device count: no first histogram
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     // (ev0 / ev1: the launch's own dispatch timestamps, no extra packets)
@@ -362,7 +362,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
     else
         DV_LAUNCH_EV(k_probe, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
                               tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              pair_limit < n_txn ? pair_limit : n_txn, ts, pair_limit < n_txn ? tword : nullptr);
+                              pair_limit < n_txn ? pair_limit : n_txn, ts, n_dev);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -415,85 +415,17 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
         counts[(uint64_t)d * nblocks + blockIdx.x] = wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d];
 }
 
-// Small sorts (the prefix's and the survivors' keys: <= kFusedScanTiles
-// tiles): the histogram and the digit scan in ONE launch.  Every tile
-// publishes its counts write-through (sc1 stores), waits for them, and adds
-// one arrival to a ticket; the tile whose add comes last scans every digit's
-// counts with sc1 loads (MI355X_MICROARCH.md, hand-off table row 1) -- one
-// kernel boundary fewer per pass, where these launch-bound sorts spend it.
-constexpr uint32_t kFusedScanTiles = 256;
-__global__ __launch_bounds__(kBlock) void k_radix_hist_scan(const uint64_t *__restrict__ in, uint64_t n, int shift,
-                                                            uint32_t *__restrict__ counts, uint32_t nblocks,
-                                                            const uint32_t *__restrict__ n_dev,
-                                                            uint32_t *__restrict__ digit_tot,
-                                                            uint32_t *__restrict__ ticket) {
-    __shared__ uint32_t wc[4][kRadix];
-    __shared__ uint32_t s_last;
-    n = sort_n(n, n_dev);
-    const uint32_t tiles = nblocks_for(n);
-    if (blockIdx.x >= tiles) return;  // (past a device-side count: no arrival)
-    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    for (uint32_t d = tid; d < 4 * kRadix; d += kBlock) (&wc[0][0])[d] = 0;
-    __syncthreads();
-    const uint64_t base = (uint64_t)blockIdx.x * kTile + wave * (64 * kIPT);
-    uint64_t k[kIPT];
-#pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        const uint64_t idx = base + j * 64 + lane;
-        k[j] = idx < n ? in[idx] : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < kIPT; j++) {
-        const uint64_t idx = base + j * 64 + lane;
-        const bool valid = idx < n;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
-        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-        const uint64_t vmask = __ballot(valid);
-        if (__ballot(valid && d == d0) == vmask) {
-            if (lane == 0) wc[wave][d0] += (uint32_t)__popcll(vmask);
-        } else if (valid) {
-            atomicAdd(&wc[wave][d], 1u);
-        }
-    }
-    __syncthreads();
-    {
-        const uint32_t d = tid;  // kBlock == kRadix
-        __hip_atomic_store(&counts[(uint64_t)d * nblocks + blockIdx.x], wc[0][d] + wc[1][d] + wc[2][d] + wc[3][d],
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) s_last = atomicAdd(ticket, 1u) == tiles - 1 ? 1u : 0u;
-    __syncthreads();
-    if (!s_last || tiles > kFusedScanTiles) return;  // (more tiles: k_radix_scan follows and scans them)
-    // the last tile: every digit's exclusive scan over the tiles, in place
-    const uint32_t d = tid;
-    uint32_t *c = counts + (uint64_t)d * nblocks;
-    uint32_t v[kFusedScanTiles / 16];  // 16 tiles per step, loads in flight together
-    uint32_t run = 0;
-    for (uint32_t t0 = 0; t0 < tiles; t0 += kFusedScanTiles / 16) {
-#pragma unroll
-        for (uint32_t q = 0; q < kFusedScanTiles / 16; q++)
-            v[q] = t0 + q < tiles ? __hip_atomic_load(&c[t0 + q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-#pragma unroll
-        for (uint32_t q = 0; q < kFusedScanTiles / 16; q++) {
-            if (t0 + q < tiles) c[t0 + q] = run;
-            run += v[q];
-        }
-    }
-    digit_tot[d] = run;
-}
-
-// exclusive scan of counts[d][0..nblocks) in place, one workgroup per digit
-// fused_upto: behind k_radix_hist_scan, which has scanned a device-side count
-// of at most that many tiles itself (then nothing to do here)
+// exclusive scan of counts[d][0..nblocks) in place, one workgroup per digit.
+// (Folding it into the histogram launch -- the last-arriving tile scanning
+// every digit over write-through counts -- measured 47 us per pass against
+// 5.5 + 4.2: one workgroup's dependent cross-XCD loads cost more than the
+// kernel boundary they save.)
 __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ counts, uint32_t nblocks,
                                                        uint32_t *__restrict__ digit_tot,
-                                                       const uint32_t *__restrict__ n_dev, uint32_t fused_upto) {
+                                                       const uint32_t *__restrict__ n_dev) {
     __shared__ uint32_t lds4[4];
     uint32_t *c = counts + (uint64_t)blockIdx.x * nblocks;  // (row stride: the upper bound)
     if (n_dev && nblocks_for(*n_dev) < nblocks) nblocks = nblocks_for(*n_dev);
-    if (nblocks <= fused_upto) return;
     const uint32_t per = (nblocks + kBlock - 1) / kBlock;
     const uint32_t lo = threadIdx.x * per;
     uint32_t hi = lo + per;
@@ -729,14 +661,13 @@ template <int W>
 void wide_pass(hipStream_t s, const uint64_t *in, uint64_t *out, uint64_t n, int shift, uint32_t *counts,
                uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1) {
     DV_LAUNCH((k_radix_hist_w<W>), nb, kBlock, 0, s, in, n, shift, counts, nb, n_dev);
-    DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev, 0u);
+    DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev);
     DV_LAUNCH_EV((k_radix_scatter_w<W>), nb, kBlock, 0, s, e0, e1, in, out, n, shift,
                           (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
 }
 
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev,
-                    uint32_t *tickets) {
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
@@ -754,22 +685,12 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
     }
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        // small sorts: the scan folded into the histogram launch; a device-side
-        // count under a larger host bound keeps a scan launch behind it, a
-        // no-op unless the count turned out larger
-        const bool fuse = tickets && (pass > 0 || !hist0_done) && (nb <= kFusedScanTiles || n_dev);
-        if (fuse) {
-            DV_LAUNCH(k_radix_hist_scan, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev, digit_tot,
-                      tickets + pass);
-        } else if (pass > 0 || !hist0_done) {
-            DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
-        }
-        if (!fuse || nb > kFusedScanTiles)
-            DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev, fuse ? kFusedScanTiles : 0u);
+        if (pass > 0 || !hist0_done) DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
+        DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev);
         // timing: events recorded by the dispatch itself (no extra packets)
-        DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, scatter_ev ? scatter_ev[2 * pass] : nullptr, scatter_ev ? scatter_ev[2 * pass + 1] : nullptr,
-                              (const uint64_t *)pairs[cur], pairs[cur ^ 1], n, shift,
-                              (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
+        DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, scatter_ev ? scatter_ev[2 * pass] : nullptr,
+                     scatter_ev ? scatter_ev[2 * pass + 1] : nullptr, (const uint64_t *)pairs[cur], pairs[cur ^ 1], n,
+                     shift, (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
         cur ^= 1;
     }
     return cur;
@@ -966,11 +887,8 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
                                                         uint4 *__restrict__ zero, uint64_t zero_n, int gate,
                                                         Counters *hctr, unsigned long long *hseq,
-                                                        unsigned long long seq, uint32_t *__restrict__ carry,
-                                                        uint32_t G) {
+                                                        unsigned long long seq) {
     if (blockIdx.x == 0) {
-        // a prefix-kill epoch's asynchronous slices start pessimistic (round_async0)
-        for (uint32_t g = threadIdx.x; g < G; g += kBlock) carry[g] = kAsyncCarryInit;
         // pipelined epochs: the previous epoch's counters into their host
         // mirror first (what k_ctr_out would have done as one more launch)
         if (hctr) {
@@ -1026,14 +944,13 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
-                        Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint32_t *carry,
-                        uint32_t G) {
+                        Counters *hctr, unsigned long long *hseq, unsigned long long seq) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
-                                       gate ? 1 : 0, hctr, hseq, seq, carry, carry ? G : 0u);
+                                       gate ? 1 : 0, hctr, hseq, seq);
 }
 
 // ---------------------------------------------------------------- execute

@@ -86,8 +86,7 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
                                                             uint32_t *__restrict__ row_state, uint64_t state_words,
                                                             uint32_t *__restrict__ bloom, int nowait,
                                                             Counters *__restrict__ ctr,
-                                                            const uint32_t *__restrict__ words,
-                                                            uint32_t *__restrict__ carry, uint32_t G) {
+                                                            const uint32_t *__restrict__ words) {
     __shared__ uint32_t s_hot[kHotWords];
     if (input_err(ctr)) return;
     // queued behind the prefix's rounds with no host wait: when they halted
@@ -99,17 +98,14 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
         return;
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // (round 0, then the asynchronous iterations)
-        ctr->a_rounds = ctr->async0 ? ctr->async_iters : (ctr->async_r0 ? ctr->async_r0 + ctr->async_iters : 1u);
-        // the survivors' stage starts with no asynchronous try behind it
-        ctr->async0 = ctr->async_go = ctr->async_r0 = ctr->async_iters = ctr->async_block = 0;
+        const uint32_t r0 = ctr->async_wr0 ? ctr->async_wr0 : ctr->async_r0;
+        ctr->a_rounds = r0 ? r0 + ctr->async_iters : 1u;
     }
-    if (blockIdx.x == 0)
-        for (uint32_t g = threadIdx.x; g < G; g += kMarkBlock) carry[g] = kAsyncCarryInit;
     for (uint32_t i = threadIdx.x; i < kHotWords; i += kMarkBlock) s_hot[i] = 0;
     __syncthreads();
     uint32_t und = 0;
     for (uint32_t t = blockIdx.x * kMarkBlock + threadIdx.x; t < K; t += gridDim.x * kMarkBlock) {
-        if (words) {  // decided by round_async0: the status bytes from the fact words
+        if (words) {  // the asynchronous launch's statuses: the status bytes from the fact words
             const uint8_t st = word_status(words[t]);
             status[t] = st;
             und += st == ST_UNDEC ? 1u : 0u;
@@ -131,7 +127,7 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
             }
         }
     }
-    if (und) {  // cannot happen: the launch decided every txn or yielded (halt)
+    if (und) {  // cannot happen: the asynchronous launch decided every txn or yielded (halt)
         set_err(ctr, ERRB_SPIN);
         atomicMax(&ctr->spin_site, 2u);
     }
@@ -151,11 +147,13 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
 constexpr int kKillWords = 8;  // ballot words per wave per step (loads in flight)
 constexpr int kKillBlock = 1024;  // one block per CU (144 KiB of LDS): 16 waves to stream with
 __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
+                                                 const uint32_t *__restrict__ n_dev,
                                                  const uint32_t *__restrict__ row_state, uint64_t state_words,
                                                  const uint32_t *__restrict__ bloom, int nowait,
                                                  uint64_t *__restrict__ kill_bits, const Counters *__restrict__ ctr) {
     __shared__ uint32_t s_hot[kHotWords], s_bloom[kBloomWords];
     if (input_err(ctr) || ctr->halt) return;
+    if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (rows past the real count were never probed)
     for (uint32_t i = threadIdx.x; i < kHotWords; i += kKillBlock) s_hot[i] = i < state_words ? row_state[i] : 0u;
     for (uint32_t i = threadIdx.x; i < kBloomWords; i += kKillBlock) s_bloom[i] = bloom[i];
     __syncthreads();
@@ -221,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     uint8_t *__restrict__ status, uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
     uint8_t *__restrict__ tlen_b,
     uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-    Counters *ctr, uint32_t *__restrict__ tword_b) {
+    Counters *ctr) {
     __shared__ uint32_t s_tile;
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
@@ -288,7 +286,6 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         map[sub] = first + j;
         tlen_b[sub] = (uint8_t)lens[j];
         status_b[sub] = ST_UNDEC;
-        if (tword_b) tword_b[sub] = lens[j] << 16;  // (round_async0: no access OK yet)
         l_a0[ls] = a0s[j];
         l_pre[ls] = la;
         la += lens[j];
@@ -353,12 +350,11 @@ uint32_t grid_of(uint64_t n, uint32_t cap) {
 
 void launch_prefix_mark(hipStream_t s, uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                         const uint32_t *acc_row, uint32_t K, uint32_t *row_state, uint64_t rs_words, int nowait,
-                        Counters *ctr, const uint32_t *words, uint32_t *carry, uint32_t G) {
+                        Counters *ctr, const uint32_t *words) {
     // (the bitmap and the Bloom filter after it were zeroed by k_epoch_clear)
     const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>((K + kMarkBlock - 1) / kMarkBlock, 64));
     DV_LAUNCH(k_prefix_mark, g, kMarkBlock, 0, s, status, tb_start, tb_end, acc_row, K, row_state, rs_words - kBloomWords,
-                                           row_state + (rs_words - kBloomWords), nowait, ctr, words, carry,
-                                           carry ? G : 0u);
+                                           row_state + (rs_words - kBloomWords), nowait, ctr, words);
 }
 
 uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKillTile; }
@@ -366,20 +362,21 @@ uint32_t kill_tiles(uint32_t n_after) { return (n_after + kKillTile - 1) / kKill
 uint64_t kill_words(uint64_t n_acc) { return (n_acc + 63) / 64 + 1; }
 
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
-                         uint64_t n_acc, uint32_t K, uint32_t n_txn, const uint32_t *row_state, uint64_t rs_words,
+                         uint64_t n_acc, const uint32_t *n_acc_dev, uint32_t K, uint32_t n_txn,
+                         const uint32_t *row_state, uint64_t rs_words,
                          int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
                          uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-                         Counters *ctr, uint32_t *tword_b) {
+                         Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
     // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
-    DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, row_state, rs_words - kBloomWords,
+    DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
                                                                      row_state + (rs_words - kBloomWords), nowait,
                                                                      kill_bits, ctr);
     DV_LAUNCH(k_kill_compact, nt, kBlock, 0, s, tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
-                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr, tword_b);
+                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -41,7 +41,6 @@ namespace {
 constexpr uint32_t B_CA = 1u, B_UA = 2u, B_CW = 4u, B_UW = 8u, B_KEEP = 16u;
 constexpr uint32_t kCarryHead = 1u << 31;  // carry word: the slice holds a queue head
 constexpr uint32_t kCarryInit = B_UA | B_UW | B_KEEP | kCarryHead;  // "undecided blockers in front"
-static_assert(kCarryInit == kAsyncCarryInit, "dvcc_internal.h's copy of the pessimistic carry word");
 constexpr uint8_t VB_OK = 1, VB_ABORT = 2;
 constexpr uint32_t F_WR = 1u, F_HEAD = 2u, F_DONE = 4u;
 
@@ -404,6 +403,7 @@ __global__ __launch_bounds__(Geo<EIn>::kThreads, Geo<EIn>::kMinWaves) void k_rou
         // survivor stage must keep the prefix's halt, k_prefix_mark)
         ctr->async_go = 0;
         ctr->async_r0 = 0;
+        ctr->async_wr0 = 0;
         ctr->async_iters = 0;
         ctr->async_block = 0;
     }
@@ -915,61 +915,21 @@ __device__ __forceinline__ uint32_t async_value(uint32_t e, bool undec, bool abo
 // IPT elements: the kernel instantiates it for small slices too (IPT 4: a
 // prefix-kill stage's live set, a few elements per thread), where the wide
 // instantiation's fully unrolled 28-element loops cost a config-D epoch 38 us.
-//
-// FROM_PAIRS (a prefix-kill stage's one launch, round_async0): the slice is
-// cut from the stage's row-sorted pairs (row << 32 | txn << 8 | pos << 1 |
-// wr) and turned into round elements here, doing round 0's classification
-// (k_round_pass<true>): queue heads from the neighbouring pair's row, and a
-// txn's repeated accesses to one row -- transparent, OK at once, the group's
-// first access standing for all of them with the OR of their types; NO_WAIT
-// and WAIT_DIE abort the txn unless every access of the group reads (its own
-// lock conflicts, row_lock.cpp:69, 86-90).  Round 0's
-// decisions are then the first iteration's.  The fact words start as "no
-// access OK" (len << 16, written by the kernel that made the stage: the probe
-// or k_kill_compact) and the carries pessimistic (k_epoch_clear /
-// k_prefix_mark).
-template <int IPT, bool FROM_PAIRS = false>
-__device__ __forceinline__ void async_slices(const RoundBufs &b, const void *src_v, uint32_t n_all,
+template <int IPT>
+__device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t *src, uint32_t n_all,
                                              uint32_t *tword, uint32_t *carry, int nowait, uint32_t max_iters,
                                              uint64_t idle, uint32_t *sel, RAgg *rw, Agg *wt, uint32_t *s_needy,
-                                             uint32_t *s_moved, uint32_t &s_cin, uint32_t &s_quit) {
+                                             uint32_t *s_moved, uint32_t &s_cin, uint32_t &s_quit, bool words) {
     using M = uint32_t;  // per-thread element bit masks
     Counters *ctr = b.ctr;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t slog = b.slog, g = blockIdx.x, G = gridDim.x;
     const uint32_t lo = (uint32_t)((uint64_t)g * n_all / G), hi = (uint32_t)((uint64_t)(g + 1) * n_all / G);
     uint32_t n = hi - lo;
-    bool cont_in, cont_out;  // does a queue run in from the previous slice / out into the next one?
-    if constexpr (FROM_PAIRS) {
-        const uint64_t *pairs = static_cast<const uint64_t *>(src_v);
-        cont_in = lo > 0 && lo < n_all && pair_row(pairs[lo]) == pair_row(pairs[lo - 1]);
-        cont_out = hi > 0 && hi < n_all && pair_row(pairs[hi]) == pair_row(pairs[hi - 1]);
-        for (uint32_t i = tid; i < n; i += kAsyncThreads) {
-            const uint32_t at = lo + i;
-            const uint64_t p = pairs[at], pp = at > 0 ? pairs[at - 1] : ~0ull;
-            const bool head = pair_row(pp) != pair_row(p);
-            const bool rep = !head && pair_txn(pp) == pair_txn(p);
-            const uint32_t t = pair_txn(p);
-            uint32_t wr = (uint32_t)(p & 1u);
-            if (rep) {
-                atomicAdd(tword + t, TW_OK);
-                if (nowait && ((p | pp) & 1u)) atomicOr(tword + t, (uint32_t)ST_ABORT);
-            } else {  // the first of a group: the OR of its types
-                for (uint32_t k = at + 1; k < n_all && !wr; k++) {
-                    const uint64_t x = pairs[k];
-                    if ((x >> 8) != (p >> 8)) break;
-                    wr |= (uint32_t)(x & 1u);
-                }
-            }
-            const uint32_t id = (t << slog) | pair_pos(p);
-            sel[i] = (id << 3) | (head && !(i == 0 && cont_in) ? F_HEAD : 0u) | (rep ? F_DONE : 0u) | wr;
-        }
-    } else {
-        const uint32_t *src = static_cast<const uint32_t *>(src_v);
-        cont_in = lo > 0 && lo < n_all && !(src[lo] & F_HEAD);
-        cont_out = hi < n_all && !(src[hi] & F_HEAD);
-        for (uint32_t i = tid; i < n; i += kAsyncThreads) sel[i] = src[lo + i] & ~(i == 0 && cont_in ? F_HEAD : 0u);
-    }
+    // does a queue run in from the previous slice / out into the next one?
+    const bool cont_in = lo > 0 && lo < n_all && !(src[lo] & F_HEAD);
+    const bool cont_out = hi < n_all && !(src[hi] & F_HEAD);
+    for (uint32_t i = tid; i < n; i += kAsyncThreads) sel[i] = src[lo + i] & ~(i == 0 && cont_in ? F_HEAD : 0u);
     if (tid == 0) s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
     __syncthreads();
     uint32_t it = 0;
@@ -1104,9 +1064,12 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const void *src
         if (DVCC_ASYNC_SLEEP && !s_moved[p]) __builtin_amdgcn_s_sleep(DVCC_ASYNC_SLEEP);
     }
     if (tid == 0) {
-        // the finalize (or, for round_async0, dv_epoch_finish) hands the rest
-        // to the synchronous rounds; one yield counted per launch
-        if (yielded && atomicExch(&ctr->halt, 1u) == 0u && FROM_PAIRS) atomicAdd(&ctr->async_yields, 1u);
+        // the finalize (or, with the statuses left in the words, dv_epoch_finish)
+        // hands the rest to the synchronous rounds; one yield counted per launch
+        if (yielded && atomicExch(&ctr->halt, 1u) == 0u && words) {
+            atomicAdd(&ctr->async_yields, 1u);
+            ctr->async_block = 1u;
+        }
         atomicMax(&ctr->async_iters, it);
     }
 }
@@ -1115,51 +1078,15 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const void *src
 // 28 elements per thread 0.565 ms per epoch, 4 / 28 0.574-0.585, 28 alone 0.615)
 constexpr int kAsyncIPTTiny = 1, kAsyncIPTSmall = 4;
 
-// a prefix-kill stage decided by ONE launch from its sorted pairs (no round-0
-// pass, settle or finalize): go = 1 runs, 2 declines (a slice would exceed
-// the workgroup's LDS: halt, dv_epoch_finish decides the stage again
-// synchronously), 0 nothing to do (an input error or a halted epoch).  The
-// stage's statuses stay in the fact words: k_prefix_mark / k_sub_scatter_back
-// read them (word_status).
-__global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async0(RoundBufs b, uint32_t *tword, uint32_t *carry,
-                                                                int nowait, uint32_t max_iters, uint64_t idle) {
-    __shared__ uint32_t sel[kAsyncCap];
-    __shared__ RAgg rw[kAsyncWaves];
-    __shared__ Agg wt[kAsyncWaves];
-    __shared__ uint32_t s_needy[2], s_moved[2], s_cin, s_quit;
-    Counters *ctr = b.ctr;
-    const uint32_t G = gridDim.x;
-    const uint32_t n_all = b.n0_dev ? *b.n0_dev : b.n0;
-    const uint64_t per = ((uint64_t)n_all + G - 1) / G;  // the largest slice (uniform)
-    const uint32_t go = input_err(ctr) || ctr->halt || n_all == 0 ? 0u : (per <= kAsyncCap ? 1u : 2u);
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctr->async_go = go;
-        if (go == 1u) {
-            ctr->async0 = 1u;
-            ctr->async_live += n_all;
-        } else if (go == 2u) {
-            ctr->async_declined++;
-            ctr->async_block = 1u;
-            ctr->halt = 1u;
-        }
-    }
-    if (go != 1u) return;
-    if (per <= (uint64_t)kAsyncThreads * kAsyncIPTTiny)
-        async_slices<kAsyncIPTTiny, true>(b, b.pairs0, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt,
-                                          s_needy, s_moved, s_cin, s_quit);
-    else if (per <= (uint64_t)kAsyncThreads * kAsyncIPTSmall)
-        async_slices<kAsyncIPTSmall, true>(b, b.pairs0, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt,
-                                           s_needy, s_moved, s_cin, s_quit);
-    else
-        async_slices<kAsyncIPT, true>(b, b.pairs0, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt,
-                                      s_needy, s_moved, s_cin, s_quit);
-}
-
+// words: no finalize follows (a prefix-kill stage: k_prefix_mark /
+// k_sub_scatter_back read the statuses from the words); the launch then does
+// the finalize's bookkeeping itself -- a declined try halts, a yield halts
+// (async_slices), an accepted one records its first round (async_wr0)
 __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, const uint32_t *src,
                                                                uint32_t r0, uint32_t thresh,
                                                                uint32_t *tword, uint32_t *carry,
                                                                int nowait, uint32_t max_iters,
-                                                               uint64_t idle) {
+                                                               uint64_t idle, int words) {
     __shared__ uint32_t sel[kAsyncCap];
     __shared__ RAgg rw[kAsyncWaves];
     __shared__ Agg wt[kAsyncWaves];
@@ -1174,18 +1101,24 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctr->async_go = go;  // for the finalize (its inputs change there)
         if (go == 1u) ctr->async_live += n_all;
+        if (words && go == 1u) ctr->async_wr0 = r0;
+        if (words && go == 2u) {
+            ctr->async_declined++;
+            ctr->async_block = 1u;
+            ctr->halt = 1u;
+        }
     }
     if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint64_t per = ((uint64_t)n_all + G - 1) / G;  // the largest slice (uniform)
     if (per <= (uint64_t)kAsyncThreads * kAsyncIPTTiny)
         async_slices<kAsyncIPTTiny>(b, src, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
-                                    s_moved, s_cin, s_quit);
+                                    s_moved, s_cin, s_quit, words != 0);
     else if (per <= (uint64_t)kAsyncThreads * kAsyncIPTSmall)
         async_slices<kAsyncIPTSmall>(b, src, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
-                                     s_moved, s_cin, s_quit);
+                                     s_moved, s_cin, s_quit, words != 0);
     else
         async_slices<kAsyncIPT>(b, src, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
-                                s_moved, s_cin, s_quit);
+                                s_moved, s_cin, s_quit, words != 0);
 }
 
 // after the asynchronous rounds: the status bytes from the words and the
@@ -1299,21 +1232,19 @@ void round_tail(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, Roun
     else DV_LAUNCH((k_round_tail<uint64_t>), 1, kTailThreads, 0, s, b, r0, nowait, pub);
 }
 
-void round_async0(hipStream_t s, const RoundBufs &b, int nowait, uint32_t G, uint32_t *carry, uint32_t *tword,
-                  uint32_t max_iters, uint64_t idle_ticks) {
-    DV_LAUNCH(k_round_async0, G, kAsyncThreads, 0, s, b, tword, carry, nowait, max_iters, idle_ticks);
-}
-
 void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uint32_t G, uint32_t thresh,
                  uint32_t *carry, uint32_t *tword, uint32_t n_txn, RoundPub *pub, uint32_t max_iters,
-                 uint64_t idle_ticks, bool words_done) {
+                 uint64_t idle_ticks, bool words_done, bool words) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(b.rel[(r0 - 1) & 1]);
     if (!words_done)  // (else round 0's settle wrote them: round_settle with tword)
         DV_LAUNCH(k_async_words, txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s, b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
                                                                     b.n_txn_dev, b.ctr);
-    DV_LAUNCH(k_round_async, G, kAsyncThreads, 0, s, b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks);
-    DV_LAUNCH(k_round_finalize, txn_grid(n_txn), kBlock, 0, s, b.status, tword, n_txn, r0, pub, b.n_txn_dev, b.ctr);
+    DV_LAUNCH(k_round_async, G, kAsyncThreads, 0, s, b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks,
+              words ? 1 : 0);
+    if (!words)
+        DV_LAUNCH(k_round_finalize, txn_grid(n_txn), kBlock, 0, s, b.status, tword, n_txn, r0, pub, b.n_txn_dev,
+                  b.ctr);
 }
 
 // Every workgroup of the asynchronous launch must be resident at once (one

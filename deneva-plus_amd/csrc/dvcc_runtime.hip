@@ -102,7 +102,7 @@ struct dv_ctx {
     uint32_t async_g = 0;                            // its workgroups (all co-resident)
     uint32_t *carry_b = nullptr;                     // abort carry-over: block counts (2 x carry_nb)
     uint32_t carry_nb = 0;
-    uint32_t *carry_tot = nullptr;                   // its totals (3 words)
+    uint32_t *carry_tot = nullptr;                   // its totals (kRefillTot words)
     DvComm *comm = nullptr;                          // RCCL communicator (dv_comm_init)
     uint32_t round_tag = 0;                          // descriptor tag of the last pass
     uint32_t ticket = 0;                             // next tile_ctr slot
@@ -149,6 +149,7 @@ struct dv_ctx {
     // epoch state
     int phase = 0;  // 0 idle, 1 begun
     uint64_t n_acc = 0;
+    bool n_acc_is_bound = false;  // n_acc bounds a device-side count (dv_epoch_dev::n_acc_dev)
     uint32_t n_txn = 0, n_txn_pad = 0;
     int sorted = 0;
     uint32_t rounds = 0, sort_passes = 0;
@@ -174,8 +175,9 @@ struct dv_ctx {
     // prefix-kill epochs (run_prefix_epoch, dvcc_prefix.hip)
     uint32_t prefix_txns = 0;     // dv_set_prefix: prefix size (0: automatic, ~n_txn / 32)
     bool prefix_mode = false;     // the epoch in flight is one
-    // the stage's decisions are one round_async0 launch (statuses in tword):
-    // the prefix's (k_prefix_mark reads them), the survivors' (k_sub_scatter_back)
+    // the stage's asynchronous launch leaves its statuses in tword, no
+    // finalize: the prefix's (k_prefix_mark reads them), the survivors'
+    // (k_sub_scatter_back)
     bool prefix_words = false, surv_words = false;
     uint32_t rounds_prefix = 0;   // rounds the prefix took (0: read from the counters, a_rounds)
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
@@ -183,6 +185,7 @@ struct dv_ctx {
     const RouteOut *route = nullptr;   // epoch groups: committed accesses go to their owners (run_group)
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
+    const uint32_t *pf_n_acc_dev = nullptr;  // the epoch's device-side access count (dv_epoch_dev::n_acc_dev)
     int pf_sorted_a = 0, pf_key_bits = 0;
     uint64_t pf_n_acc = 0;
     uint32_t *row_state = nullptr; // 2 bits per row: the prefix's committed readers / writers
@@ -383,19 +386,7 @@ uint32_t *next_ticket(dv_ctx *c) {
 // 167 us of scatters per config-D epoch against 125 us for the three-launch
 // passes.)
 int sort_rows(dv_ctx *c, uint64_t n, int key_bits, hipEvent_t *ev, bool hist0_done, const uint32_t *n_dev) {
-    // (one zeroed arrival ticket per pass for the fused histogram + scan)
-    constexpr uint32_t kSortTickets = 8;
-    uint32_t pos = c->ticket % kTileCtrs;
-    if (pos + kSortTickets > kTileCtrs) {  // (not across the wrap: skip to it)
-        c->ticket += kTileCtrs - pos;
-        pos = 0;
-    }
-    if (c->ticket > 0 && pos == 0)  // the wrap: zeroed again, as next_ticket does
-        (void)hipMemsetAsync(c->tile_ctr, 0, kTileCtrs * sizeof(uint32_t), c->stream);
-    uint32_t *tickets = &c->tile_ctr[pos];
-    c->ticket += kSortTickets;
-    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev,
-                           tickets);
+    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev);
 }
 
 Tables make_tables(dv_ctx *c) {
@@ -699,6 +690,26 @@ int dv_set_stream(dv_ctx *c, void *stream) {
     return DV_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// the carry-over's block counts for nb blocks and its totals (kRefillTot words)
+int carry_bufs(dv_ctx *c, uint32_t nb) {
+    if (nb <= c->carry_nb && c->carry_tot) return DV_OK;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    dfree(c->carry_b);
+    c->carry_b = nullptr;
+    c->carry_nb = 0;
+    int r = dalloc(&c->carry_b, 2ull * (nb ? nb : 1));
+    if (!r && !c->carry_tot) r = dalloc(&c->carry_tot, kRefillTot);
+    if (r) return r;
+    c->carry_nb = nb ? nb : 1;
+    return DV_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch_dev *out) {
     KProfScope kps_(c);
     if (!c || !ep || !out) return DV_ERR_ARG;
@@ -708,16 +719,8 @@ int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch
         return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     const uint32_t nb = carry_blocks(ep->n_txn);
-    if (nb > c->carry_nb || !c->carry_tot) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        dfree(c->carry_b);
-        c->carry_b = nullptr;
-        c->carry_nb = 0;
-        int r = dalloc(&c->carry_b, 2ull * (nb ? nb : 1));
-        if (!r && !c->carry_tot) r = dalloc(&c->carry_tot, 3);
-        if (r) return r;
-        c->carry_nb = nb ? nb : 1;
-    }
+    int r = carry_bufs(c, nb);
+    if (r) return r;
     launch_carry(c->stream, c->status, c->tb_start, c->tb_end, ep->n_txn, max_txn, ep->keys, ep->types,
                  ep->tables, const_cast<uint64_t *>(out->keys), const_cast<uint8_t *>(out->types),
                  const_cast<uint32_t *>(out->acc_txn),
@@ -1055,6 +1058,8 @@ int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
     HIPCHK(hipSetDevice(c->cfg.device));
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     if (ep->n_txn > kMaxTxn || ep->max_txn_acc > kMaxPos) return DV_ERR_ARG;
+    // a device-side access count: single-GPU YCSB, decision rounds (dvcc.h)
+    if (ep->n_acc_dev && (calvin || c->cfg.workload != DV_YCSB || c->rep_P)) return DV_ERR_ARG;
     // verdict-byte stride: 1 << slog >= the longest txn (16 at least)
     uint32_t slog = 7;
     if (!calvin) {
@@ -1075,6 +1080,7 @@ int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
         c->el32 = round_el32(ep->n_txn, slog) && !(c->cfg.flags & DV_FLAG_EL64);
     }
     c->n_acc = ep->n_acc;
+    c->n_acc_is_bound = ep->n_acc_dev != nullptr;
     c->n_txn = ep->n_txn;
     c->n_txn_pad = (ep->n_txn + 3u) & ~3u;
     c->rounds = 0;
@@ -1104,12 +1110,12 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
                        c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr);
     c->ticket = 0;
-    const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles;
+    const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles && !ep->n_acc_dev;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
-                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr);
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         const int re = comm_combine_errors(c);
@@ -1118,7 +1124,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     rec(c, 1);
     const int key_bits = bits_for(row_space(c));
     c->sort_passes = radix_passes(key_bits, fuse_hist);
-    c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, nullptr);
+    c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, ep->n_acc_dev);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
     rec(c, 2);
@@ -1127,7 +1133,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
         calvin_grant(c->stream, c->el, ep->n_acc, d_grant, c->ew, c->desc, next_ticket(c), tag, c->ctr);
     } else {
         c->r0_n = (uint32_t)ep->n_acc;  // (round 0's sizes, RoundBufs)
-        c->r0_n_dev = nullptr;
+        c->r0_n_dev = ep->n_acc_dev;
         __atomic_store_n(&c->h_pub->ru, 0ull, __ATOMIC_RELEASE);
         __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
         c->live_ub = (uint32_t)ep->n_acc;
@@ -1367,7 +1373,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
                          c->h_ctr->spin_site);
         return r;
     }
-    if (!calvin && (c->h_ctr->async_r0 || c->h_ctr->async0)) {  // an asynchronous launch decided the rest
+    if (!calvin && (c->h_ctr->async_r0 || c->h_ctr->async_wr0)) {  // an asynchronous launch decided the rest
         uint32_t left = 0;
         for (const CtrSlot &sl : c->h_ctr->slot) left += sl.undecided;
         if (left) return DV_ERR_STATE;  // cannot happen: every workgroup left decided
@@ -1431,6 +1437,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
             if (c->n_acc) (void)hipEventElapsedTime(&st->ms_probe_kernel, c->ev[kEvProbe0], c->ev[kEvProbe1]);
         }
         st->async_live = c->h_ctr->async_live;
+        if (c->n_acc_is_bound) st->n_acc = c->h_ctr->n_acc;
         if (prefix) {
             st->prefix_txn = c->pf_K;
             st->prefix_acc = c->h_ctr->a_acc;
@@ -1479,19 +1486,21 @@ uint32_t async_thresh(dv_ctx *c) {
     return (uint32_t)std::min<uint64_t>(frac, async_try_limit(c->async_g));
 }
 
-void async_try(dv_ctx *c, uint32_t r0, bool words_done = false) {
+void async_try(dv_ctx *c, uint32_t r0, bool words_done = false, bool words = false) {
     c->async_launched++;
     round_async(c->stream, round_bufs(c), r0, c->cfg.cc_alg != DV_OCC, c->async_g, async_thresh(c),
-                c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks, words_done);
+                c->abounds, c->tword, c->v_n_txn, c->d_pub, c->async_max_iters, c->async_idle_ticks, words_done,
+                words);
 }
 
 // round 0, then every remaining decision in one asynchronous launch at round
 // 1, queued with no host wait; round 0's settle writes the launch's fact and
-// carry words (no k_async_words)
-void round0_then_async(dv_ctx *c) {
+// carry words (no k_async_words).  words: the statuses stay in the fact
+// words for the stage's consumer (no k_round_finalize)
+void round0_then_async(dv_ctx *c, bool words = false) {
     c->v_thresh = async_try_limit(c->async_g);
     enqueue_round(c, nullptr, true, true);
-    async_try(c, 1, true);
+    async_try(c, 1, true, words);
     c->async_unconfirmed = true;
 }
 
@@ -1588,24 +1597,13 @@ bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {
     return prefix_size(c, ep->n_txn) < ep->n_txn;
 }
 
-// A stage of n_txn txns can be decided by ONE launch from round 0
-// (round_async0): its round elements fit 32 bits and asynchronous rounds are
-// on.  The kernel that makes the stage then writes its fact words (the probe,
-// k_kill_compact) and the one before it its carries (k_epoch_clear,
-// k_prefix_mark).
-bool async0_possible(const dv_ctx *c, uint32_t n_txn) {
-    return round_el32(n_txn, c->slog) && c->async_g &&
-           !(c->cfg.flags & (DV_FLAG_EL64 | DV_FLAG_NO_ASYNC | DV_FLAG_NO_ASYNC0));
-}
-
-// The rounds of one stage: one asynchronous launch from round 0 when the
-// stage's words are ready (async0; *words = true: the statuses stay in the
-// fact words), else round 0, then every remaining decision in one
+// The rounds of one stage: round 0, then every remaining decision in one
 // asynchronous launch (stages are small: a declined or yielded try halts and
-// the synchronous rounds resume), or the pipelined loop when asynchronous
-// rounds are off.
-int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub, bool async0 = false,
-                 bool *words = nullptr) {
+// the stage is decided again synchronously), or the pipelined loop when
+// asynchronous rounds are off.  words (a prefix-kill stage): the launch leaves
+// the statuses in the fact words and *words = true -- its consumer
+// (k_prefix_mark, k_sub_scatter_back) reads them, no k_round_finalize.
+int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub, bool *words = nullptr) {
     if (words) *words = false;
     c->rounds = 0;
     c->rounds_real = 0;
@@ -1619,15 +1617,8 @@ int stage_rounds(dv_ctx *c, const uint32_t *n_acc_dev, uint32_t n_acc_ub, bool a
     __atomic_store_n(&c->h_pub->tl, 0ull, __ATOMIC_RELEASE);
     const bool async = c->el32 && c->async_g && !(c->cfg.flags & DV_FLAG_NO_ASYNC);
     if (!async) return run_rounds(c, false);
-    if (async0 && words) {
-        c->async_launched++;
-        c->async_unconfirmed = true;
-        *words = true;
-        round_async0(c->stream, round_bufs(c), c->cfg.cc_alg != DV_OCC, c->async_g, c->abounds, c->tword,
-                     c->async_max_iters, c->async_idle_ticks);
-        return hip_fail(hipGetLastError(), "stage launch");
-    }
-    round0_then_async(c);  // (v_thresh: whatever fits the workgroups)
+    if (words) *words = true;
+    round0_then_async(c, words != nullptr);  // (v_thresh: whatever fits the workgroups)
     return hip_fail(hipGetLastError(), "stage rounds");
 }
 
@@ -1640,31 +1631,31 @@ int enqueue_survivors(dv_ctx *c) {
     const bool nowait = c->cfg.cc_alg != DV_OCC;
     const uint64_t rs_words = row_state_words(row_space(c));
     const uint32_t K = c->pf_K;
-    const bool a0 = async0_possible(c, c->n_txn - K);
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
-                       c->ctr, c->prefix_words ? c->tword : nullptr, a0 ? c->abounds : nullptr, c->async_g);
+                       c->ctr, c->prefix_words ? c->tword : nullptr);
     const uint32_t tag = next_tag(c);
-    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, K, c->n_txn, c->row_state,
+    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, c->pf_n_acc_dev, K, c->n_txn,
+                        c->row_state,
                         rs_words, nowait,
                         c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
-                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr, a0 ? c->tword : nullptr);
+                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
     c->v_tlen = c->b_tlen;
     c->v_n_txn = c->n_txn - K;
     c->v_n_txn_dev = &c->ctr->b_txn;
-    return stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, a0, &c->surv_words);
+    return stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, &c->surv_words);
 }
 
-// The survivors' one launch (round_async0) yielded or declined: nothing
-// behind it executed, and it leaves no round state to resume from, so their
-// rounds run again from round 0, synchronously (their status bytes are still
-// undecided; the greedy's fixpoint is the same).
+// The survivors' asynchronous launch yielded or declined: nothing behind it
+// executed, and with no finalize their status bytes hold only round 0's
+// decisions, so their rounds run again from round 0, synchronously (the
+// greedy's fixpoint is the same).
 int redo_survivors(dv_ctx *c) {
     const uint32_t flags = c->cfg.flags;
     c->cfg.flags |= DV_FLAG_NO_ASYNC;
-    int r = stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, false, &c->surv_words);
+    int r = stage_rounds(c, &c->ctr->b_acc, (uint32_t)c->pf_n_acc, &c->surv_words);
     c->cfg.flags = flags;
     return r;
 }
@@ -1685,7 +1676,7 @@ int redo_prefix(dv_ctx *c) {
     c->v_thresh = 0;
     const uint32_t flags = c->cfg.flags;
     c->cfg.flags |= DV_FLAG_NO_ASYNC;
-    int r = stage_rounds(c, &c->ctr->a_acc, c->pf_ub_a, false, &c->prefix_words);
+    int r = stage_rounds(c, &c->ctr->a_acc, c->pf_ub_a, &c->prefix_words);
     c->cfg.flags = flags;
     if (r) return r;
     c->rounds_prefix = c->rounds_real ? c->rounds_real : c->rounds;
@@ -1728,19 +1719,18 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->sort_passes = radix_passes(key_bits, false);
     c->prefix_mode = true;
     c->prefix_words = c->surv_words = false;
-    const bool a0 = async0_possible(c, K);  // the prefix in one launch from round 0
     rec(c, 0);
     const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
     c->mir_pending = false;
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
                        c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate,
                        mir ? c->d_mir[c->mir_slot] : nullptr, mir ? c->d_mseq[c->mir_slot] : nullptr,
-                       mir ? c->mir_seq : 0ull, a0 ? c->abounds : nullptr, c->async_g);
+                       mir ? c->mir_seq : 0ull);
     c->ticket = 0;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                  c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
-                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, a0 ? c->tword : nullptr);
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         r = comm_combine_errors(c);
@@ -1762,7 +1752,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->pf_sorted_a = c->sorted;
     c->pf_key_bits = key_bits;
     c->pf_n_acc = ep->n_acc;
-    r = stage_rounds(c, &c->ctr->a_acc, ub_a, a0, &c->prefix_words);
+    c->pf_n_acc_dev = ep->n_acc_dev;
+    r = stage_rounds(c, &c->ctr->a_acc, ub_a, &c->prefix_words);
     // the prefix's rounds ran synchronously (no asynchronous try): their count
     // is known here; else k_prefix_mark records it (Counters::a_rounds)
     c->rounds_prefix = c->async_unconfirmed ? 0u : (c->rounds_real ? c->rounds_real : c->rounds);
@@ -1813,7 +1804,7 @@ struct EpochSnap {
     uint64_t n_acc = 0;
     uint32_t n_txn = 0, rounds = 0, rounds_real = 0, rounds_prefix = 0, async_launched = 0, sort_passes = 0;
     uint32_t prefix_txn = 0;
-    bool async_unconfirmed = false;
+    bool async_unconfirmed = false, n_acc_is_bound = false;
     unsigned long long seq = 0;
     int slot = 0;
 };
@@ -1841,6 +1832,7 @@ int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate
     sn.async_launched = c->async_launched;
     sn.sort_passes = c->sort_passes;
     sn.prefix_txn = c->pf_K;
+    sn.n_acc_is_bound = c->n_acc_is_bound;
     sn.async_unconfirmed = c->async_unconfirmed;
     sn.slot = slot;
     if (defer && !r) {
@@ -1871,7 +1863,7 @@ int pipe_complete(dv_ctx *c, const EpochSnap &sn, dv_stats *st, bool *halted) {
         return DV_OK;
     }
     uint32_t rounds_real = sn.rounds_real;
-    if (hc->async_r0 || hc->async0) {
+    if (hc->async_r0 || hc->async_wr0) {
         uint32_t left = 0;
         for (const CtrSlot &sl : hc->slot) left += sl.undecided;
         if (left) return DV_ERR_STATE;
@@ -1904,6 +1896,7 @@ int pipe_complete(dv_ctx *c, const EpochSnap &sn, dv_stats *st, bool *halted) {
         st->async_declined = (uint16_t)std::min(hc->async_declined, 0xFFFFu);
         st->async_yields = hc->async_yields;
         st->async_live = hc->async_live;
+        if (sn.n_acc_is_bound) st->n_acc = hc->n_acc;
         st->prefix_txn = sn.prefix_txn;
         st->prefix_acc = hc->a_acc;
         st->surv_txn = hc->b_txn;
@@ -1997,6 +1990,133 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
         const int r = settle(-1);
         if (r < 0) return fail(r);
     }
+    return DV_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+// the closed loop's next epoch (launch_refill) into `out`: prev's aborted txns
+// (prev: the epoch the context decided last; NULL: none, all fresh), then fresh
+// ones from the pool
+void enqueue_refill(dv_ctx *c, const dv_epoch_dev *prev, const dv_epoch_dev *pool, const uint32_t *pool_begin,
+                    uint32_t *cursor, uint32_t n_out, const dv_epoch_dev &out) {
+    launch_refill(c->stream, c->status, c->tb_start, c->tb_end, prev ? prev->n_txn : 0u,
+                  prev ? prev->keys : nullptr, prev ? prev->types : nullptr, prev ? prev->tables : nullptr,
+                  pool->keys, pool->types, pool->tables, pool->acc_txn, pool_begin, pool->n_txn, cursor, n_out,
+                  (uint64_t)n_out * pool->max_txn_acc, const_cast<uint64_t *>(out.keys),
+                  const_cast<uint8_t *>(out.types), const_cast<uint32_t *>(out.acc_txn),
+                  const_cast<uint8_t *>(out.tables), const_cast<uint32_t *>(out.n_acc_dev), c->carry_b,
+                  c->carry_b + c->carry_nb, c->carry_tot, prev ? c->ctr : nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t *pool_begin, uint32_t *cursor,
+                             uint32_t n_txn, dv_epoch_dev *bufs, uint64_t buf_cap, uint32_t n_epochs,
+                             int resume, uint8_t *const *d_commits, dv_stats *sts) {
+    KProfScope kps_(c);
+    if (!c || !pool || !pool_begin || !cursor || !bufs || !n_txn) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    if (c->cfg.cc_alg == DV_CALVIN || c->cfg.workload != DV_YCSB || c->comm) return DV_ERR_STATE;
+    const uint64_t bound = (uint64_t)n_txn * pool->max_txn_acc;
+    if (!pool->max_txn_acc || n_txn > pool->n_txn || n_txn > c->cfg.max_txn || bound > buf_cap ||
+        bound > c->cfg.max_acc || !pool->keys || !pool->types || !pool->acc_txn)
+        return DV_ERR_ARG;
+    for (int b = 0; b < 2; b++)
+        if (!bufs[b].keys || !bufs[b].types || !bufs[b].acc_txn || !bufs[b].n_acc_dev ||
+            (pool->tables && !bufs[b].tables))
+            return DV_ERR_ARG;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int r = carry_bufs(c, carry_blocks(n_txn));
+    if (r) return r;
+    // epoch k's descriptor: buffer k & 1, its access count on the device
+    auto desc = [&](uint32_t k) {
+        dv_epoch_dev d = bufs[k & 1];
+        d.tables = pool->tables ? bufs[k & 1].tables : nullptr;
+        d.n_txn = n_txn;
+        d.n_acc = bound;
+        d.max_txn_acc = pool->max_txn_acc;
+        d.ts = nullptr;  // (sequence order: carried txns first keep their priority)
+        return d;
+    };
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
+    auto fail = [&](int e) {
+        c->mir_pending = false;
+        (void)hipStreamSynchronize(c->stream);
+        return e;
+    };
+    if (!resume) enqueue_refill(c, nullptr, pool, pool_begin, cursor, n_txn, bufs[0]);
+    const dv_epoch_dev d0 = desc(0);
+    const bool pipelined = prefix_applies(c, &d0) && !timing(c) && !ktiming(c) && !c->rep_P;
+    EpochSnap snap[2];
+    int64_t pend = -1;
+    // epoch k run synchronously, then its refill
+    auto run_one = [&](uint32_t k) {
+        const dv_epoch_dev d = desc(k);
+        int e = dv_epoch_run_device(c, &d, commit_of(k), nullptr, stats_of(k));
+        if (!e) {
+            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1]);
+            e = hip_fail(hipGetLastError(), "refill");
+        }
+        return e;
+    };
+    for (uint32_t k = 0; k < n_epochs; k++) {
+        if (!pipelined) {
+            r = run_one(k);
+            if (r) return fail(r);
+            continue;
+        }
+        const dv_epoch_dev d = desc(k);
+        r = pipe_enqueue(c, &d, commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1], k + 1 < n_epochs);
+        if (!r) {
+            // behind the execution: epoch k + 1 from epoch k's final statuses (a
+            // no-op when k halted -- the host redoes both below)
+            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1]);
+            r = hip_fail(hipGetLastError(), "refill");
+        }
+        if (r) {
+            (void)hipStreamSynchronize(c->stream);
+            if (pend >= 0) {
+                bool halted = false;
+                (void)pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
+            }
+            return fail(r);
+        }
+        if (pend >= 0) {
+            bool halted = false;
+            r = pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
+            if (r) return fail(r);
+            if (halted) {
+                // epoch pend halted: epoch k started halted and neither refill
+                // ran.  Decide pend again synchronously, refill from it, and
+                // queue epoch k again.
+                c->mir_pending = false;
+                r = pipe_redo(c);
+                if (!r) r = run_one((uint32_t)pend);
+                if (r) return fail(r);
+                pend = -1;
+                k--;  // (k = pend + 1 again)
+                continue;
+            }
+        }
+        pend = k;
+    }
+    if (pend >= 0) {
+        bool halted = false;
+        r = pipe_complete(c, snap[pend & 1], stats_of((uint32_t)pend), &halted);
+        if (r) return fail(r);
+        if (halted) {
+            r = pipe_redo(c);
+            if (!r) r = run_one((uint32_t)pend);
+            if (r) return fail(r);
+        }
+    }
+    HIPCHK(hipStreamSynchronize(c->stream));  // (the next epoch's refill: the caller may read it)
     return DV_OK;
 }
 

@@ -34,7 +34,6 @@ FLAG_EL64 = 4
 FLAG_NO_ASYNC = 8
 FLAG_KERNEL_TIMING = 16
 FLAG_KERNEL_PROFILE = 32
-FLAG_NO_ASYNC0 = 64
 
 
 class DvccError(RuntimeError):
@@ -59,7 +58,7 @@ class Access(ctypes.Structure):
 class EpochDev(ctypes.Structure):
     _fields_ = [("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("acc_txn", ctypes.c_void_p),
                 ("tables", ctypes.c_void_p), ("n_acc", ctypes.c_uint64), ("n_txn", ctypes.c_uint32),
-                ("max_txn_acc", ctypes.c_uint32), ("ts", ctypes.c_void_p)]
+                ("max_txn_acc", ctypes.c_uint32), ("ts", ctypes.c_void_p), ("n_acc_dev", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -163,6 +162,9 @@ SIGNATURES = [
     ("dv_tpcc_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _vp, _P(Stats)]),
     ("dv_comm_set_mode", ctypes.c_int, [_vp, ctypes.c_int]),
     ("dv_epoch_run_device_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(_vp), _P(Stats)]),
+    ("dv_epoch_run_closed_loop", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _P(EpochDev),
+                                                 ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, _P(_vp),
+                                                 _P(Stats)]),
     ("dv_epoch_group_run", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32, _vp, _P(Stats)]),
     ("dv_epoch_group_run_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32, _P(_vp), _P(Stats)]),

@@ -120,18 +120,48 @@ class DeviceEpoch:
                           self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None)
 
 
+class ClosedLoopBufs:
+    """The closed loop's two epoch buffers (dv_epoch_run_closed_loop)."""
+
+    def __init__(self, cap, tables, device):
+        import torch
+        self.cap = int(cap)
+        n = max(1, self.cap)
+        self.keys = [torch.empty(n, dtype=torch.int64, device=device) for _ in range(2)]
+        self.types = [torch.empty(n, dtype=torch.uint8, device=device) for _ in range(2)]
+        self.acc_txn = [torch.empty(n, dtype=torch.int32, device=device) for _ in range(2)]
+        self.tables = [torch.empty(n, dtype=torch.uint8, device=device) for _ in range(2)] if tables else None
+        self.n_acc = [torch.zeros(1, dtype=torch.int32, device=device) for _ in range(2)]
+
+    def desc(self, b):
+        return L.EpochDev(self.keys[b].data_ptr(), self.types[b].data_ptr(), self.acc_txn[b].data_ptr(),
+                          self.tables[b].data_ptr() if self.tables is not None else None, 0, 0, 0, None,
+                          self.n_acc[b].data_ptr())
+
+    def swap(self):
+        """after a call of n_epochs odd: the next epoch moves to buffer 0"""
+        for a in (self.keys, self.types, self.acc_txn, self.tables, self.n_acc):
+            if a is not None:
+                a.reverse()
+
+    def epoch(self, b, n_txn, max_txn_acc):
+        """buffer b's epoch as a DeviceEpoch (reads its access count)"""
+        n = int(self.n_acc[b].item())
+        return DeviceEpoch.from_tensors(self.keys[b][:n], self.types[b][:n], self.acc_txn[b][:n], n_txn,
+                                        tables=self.tables[b][:n] if self.tables is not None else None,
+                                        max_txn_acc=max_txn_acc)
+
+
 class CCEngine:
     """One context = one GPU (one process per GPU)."""
 
     def __init__(self, cc_alg, max_txn, max_acc, device=0, part_cnt=1, part_id=0, timing=False,
-                 workload=L.YCSB, tail=True, el64=False, asynchronous=True, async0=True):
+                 workload=L.YCSB, tail=True, el64=False, asynchronous=True):
         """tail=False keeps every decision round in the multi-workgroup pass
         (no single-workgroup tail kernel); el64=True forces 64-bit round
         elements; asynchronous=False never finishes the rounds in the
-        asynchronous kernel; async0=False decides prefix-kill stages with a
-        round-0 pass and settle before their asynchronous launch instead of
-        one launch from the sorted accesses.  Decisions are the same either
-        way (testing knobs)."""
+        asynchronous kernel.  Decisions are the same either way (testing
+        knobs)."""
         if isinstance(cc_alg, str):
             cc_alg = L.CC_NAMES[cc_alg.upper()]
         self.cc_alg = cc_alg
@@ -141,8 +171,7 @@ class CCEngine:
         # launches' own dispatch timestamps (no marker packets between kernels)
         tflag = L.FLAG_KERNEL_TIMING if timing == "kernel" else (L.FLAG_TIMING if timing else 0)
         flags = (tflag | (0 if tail else L.FLAG_NO_TAIL)
-                 | (L.FLAG_EL64 if el64 else 0) | (0 if asynchronous else L.FLAG_NO_ASYNC)
-                 | (0 if async0 else L.FLAG_NO_ASYNC0))
+                 | (L.FLAG_EL64 if el64 else 0) | (0 if asynchronous else L.FLAG_NO_ASYNC))
         cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc, flags, 0)
         self._ctx = ctypes.c_void_p()
         L.check(L.lib().dv_open(ctypes.byref(self._ctx), ctypes.byref(cfg)), "dv_open")
@@ -391,6 +420,33 @@ class CCEngine:
             if prev is not None:
                 L.lib().dv_comm_set_mode(self._ctx, prev)
         return list(sts)
+
+    def closed_loop(self, pool, pool_begin, n_txn, n_epochs, cursor=None, bufs=None, d_commits=None,
+                    resume=False):
+        """The closed loop on the device (dv_epoch_run_closed_loop): n_epochs
+        epochs of n_txn txns, each the previous one's aborted txns then fresh
+        ones from `pool` (a DeviceEpoch with max_txn_acc > 0; pool_begin: its
+        n_txn + 1 access offsets, int32 device tensor) from the device word
+        `cursor` (int32 tensor, advanced).  bufs: ClosedLoopBufs (allocated when
+        None); d_commits: a device tensor per epoch (or None).  Returns (stats
+        list, bufs, cursor); the next epoch is in bufs.epoch(n_epochs & 1)."""
+        import torch
+        dev = pool.keys.device
+        if cursor is None:
+            cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        if bufs is None:
+            bufs = ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev)
+        arr = (L.EpochDev * 2)(*[bufs.desc(b) for b in range(2)])
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n_epochs
+        cps = (ctypes.c_void_p * max(1, n_epochs))(*[(int(t.data_ptr()) if t is not None else None)
+                                                     for t in d_commits])
+        sts = (L.Stats * max(1, n_epochs))()
+        self._after_torch()
+        L.check(L.lib().dv_epoch_run_closed_loop(self._ctx, ctypes.byref(pool.desc()), _ptr(pool_begin),
+                                                 _ptr(cursor), n_txn, arr, bufs.cap, n_epochs, int(resume),
+                                                 cps, sts), "dv_epoch_run_closed_loop")
+        return list(sts)[:n_epochs], bufs, cursor
 
     def carry(self, dep, max_txn=None):
         """Abort carry-over: a DeviceEpoch of the last epoch's (`dep`'s)

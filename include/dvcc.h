@@ -119,12 +119,6 @@ extern "C" {
                                rounds finish the epoch -- correct either way,
                                this flag only skips the attempt) */
 
-#define DV_FLAG_NO_ASYNC0 64u /* prefix-kill stages run round 0 as a pass and a
-                              settle before their asynchronous launch instead
-                              of deciding everything in one launch from the
-                              sorted accesses (round_async0; A/B and testing:
-                              same decisions) */
-
 typedef struct dv_ctx dv_ctx;
 
 typedef struct dv_config {
@@ -171,6 +165,11 @@ typedef struct dv_epoch_dev {
                                 never read it.  The partitioned drivers
                                 (dv_epoch_run_part, dv_epoch_group_run) take
                                 NULL only (DV_ERR_ARG voted on every rank). */
+    const uint32_t *n_acc_dev; /* (device) the real access count when it is
+                                known only on the device (dv_epoch_refill):
+                                n_acc is then an upper bound.  NULL: n_acc is
+                                exact.  Single-GPU YCSB entry points, NO_WAIT /
+                                WAIT_DIE / OCC (DV_ERR_ARG otherwise). */
 } dv_epoch_dev;
 
 typedef struct dv_stats {
@@ -362,6 +361,36 @@ int dv_comm_set_mode(dv_ctx *ctx, int mode);
  * complete and nothing of the failing one or later ones has executed. */
 int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
                               dv_stats *sts);
+
+/* The closed loop on the device (the reference's retry path,
+ * WorkerThread::abort -> AbortQueue, worker_thread.cpp:160-172,
+ * abort_queue.cpp:26-82, with a one-epoch penalty): n_epochs epochs of n_txn
+ * txns each, single GPU (YCSB, not CALVIN, no communicator).  Epoch k + 1 is
+ * epoch k's aborted txns, in sequence order and renumbered from 0 (they keep
+ * their priority), then fresh txns taken in order from `pool` starting at
+ * *cursor (a device word, advanced and wrapping around pool->n_txn) -- built
+ * on the device behind epoch k's execution, its access count left on the
+ * device (dv_epoch_dev::n_acc_dev), nothing read back between epochs, epoch
+ * k + 1 queued before the host reads epoch k's outcome.
+ *   pool: device arrays (keys, types, acc_txn = pool txn ids, tables may be
+ *     NULL), n_txn >= n_txn of an epoch, max_txn_acc > 0 (required: it bounds
+ *     an epoch's accesses, n_txn * max_txn_acc <= buf_cap and <= the
+ *     context's max_acc); pool_begin: device, pool->n_txn + 1 access offsets.
+ *   bufs[2]: the epochs' device buffers (keys / types / acc_txn, tables when
+ *     the pool has them: buf_cap accesses each; n_acc_dev: a device word);
+ *     epoch k lives in bufs[k & 1].
+ *   resume 0: epoch 0 is all fresh; 1: epoch 0 is already in bufs[0] (the
+ *     epoch a previous call left: on return the next epoch -- the last one's
+ *     aborts, then fresh txns -- is in bufs[n_epochs & 1]; swap the buffers
+ *     to continue).
+ * d_commits / sts: NULL or n_epochs entries (commit bytes of epoch k's txns,
+ * its stats; st->n_acc is the real count).  A halted epoch is decided again
+ * synchronously before its successor is rebuilt, so the epochs are exactly
+ * those of a host loop of dv_epoch_run_device + dv_epoch_carry + the fresh
+ * txns (tests/test_closed_loop.py). */
+int dv_epoch_run_closed_loop(dv_ctx *ctx, const dv_epoch_dev *pool, const uint32_t *pool_begin, uint32_t *cursor,
+                             uint32_t n_txn, dv_epoch_dev *bufs, uint64_t buf_cap, uint32_t n_epochs, int resume,
+                             uint8_t *const *d_commits, dv_stats *sts);
 
 /* Epoch groups -- epoch-parallel scheduling for YCSB: a
  * group is P = nranks consecutive epochs of the sequencer, and homes[e]

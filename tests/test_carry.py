@@ -113,3 +113,123 @@ def test_carry_rejects_calvin_and_stale_epochs():
     with pytest.raises(dvcc.DvccError):  # not the epoch the context decided last
         eng.carry(DeviceEpoch(gen.gen(100, 2)))
     eng.close()
+
+
+def host_take(pool, cur, n):
+    """txns [cur, cur + n) of the pool, wrapping around it (the fresh txns of
+    the device closed loop)"""
+    ids = (cur + np.arange(n)) % pool.n_txn
+    tb = pool.txn_begin.astype(np.int64)
+    lens = tb[ids + 1] - tb[ids]
+    idx = np.concatenate([np.arange(tb[t], tb[t + 1]) for t in ids]) if n else np.zeros(0, np.int64)
+    ntb = np.zeros(n + 1, np.uint32)
+    ntb[1:] = np.cumsum(lens)
+    return Epoch(pool.keys[idx].copy(), pool.types[idx].copy(), ntb)
+
+
+def host_closed_loop(cc, tab, f0, pool, cur, n_txn, n_epochs, first=None):
+    """the oracle's closed loop: each epoch decided by the E-schedule, its
+    aborts carried ahead of fresh pool txns.  Returns the per-epoch commit
+    bytes and stats, the next epoch and the cursor."""
+    host = first if first is not None else host_take(pool, cur, n_txn)
+    if first is None:
+        cur = (cur + n_txn) % pool.n_txn
+    out = []
+    for _ in range(n_epochs):
+        c_ref, _, st_ref = O.epoch_run(ORACLE_CC[cc], tab.ix, f0, host.n_txn, host.txn_begin, host.keys,
+                                       host.types)
+        out.append((c_ref[:host.n_txn].copy(), st_ref, host))
+        hc = host_carry(host, c_ref, n_txn)
+        fresh = n_txn - hc.n_txn
+        host = host_concat(hc, host_take(pool, cur, fresh))
+        cur = (cur + fresh) % pool.n_txn
+    return out, host, cur
+
+
+def _pool(rows, n, seed, R=10):
+    gen = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5, req_per_query=R)
+    return gen.gen(n, seed)
+
+
+def _check_loop(eng, cc, rows, pool, n_txn, n_epochs, calls=1, cur0=0):
+    import torch
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    ref, nxt, cur_ref = host_closed_loop(cc, tab, f0, pool, cur0, n_txn, n_epochs * calls)
+    dpool = DeviceEpoch(pool)
+    pb = torch.from_numpy(pool.txn_begin.astype(np.int32)).cuda()
+    cursor = torch.full((1,), cur0, dtype=torch.int32, device="cuda")
+    commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in range(n_epochs)]
+    bufs = None
+    got = []
+    for call in range(calls):
+        sts, bufs, cursor = eng.closed_loop(dpool, pb, n_txn, n_epochs, cursor=cursor, bufs=bufs,
+                                            d_commits=commits, resume=call > 0)
+        got += [(c.cpu().numpy().copy(), s) for c, s in zip(commits, sts)]
+        if n_epochs & 1:
+            bufs.swap()
+    for k, ((c, st), (c_ref, st_ref, host)) in enumerate(zip(got, ref)):
+        assert np.array_equal(c, c_ref), k
+        assert (st.n_txn, st.n_acc, st.committed) == (host.n_txn, host.n_acc, st_ref.committed), k
+        assert (st.read_digest, st.write_cnt) == (st_ref.read_digest, st_ref.write_cnt), k
+    # the next epoch the loop left, and the cursor
+    assert int(cursor.item()) == cur_ref
+    e = bufs.epoch(0, n_txn, pool.max_txn_acc())
+    assert e.n_acc == nxt.n_acc
+    assert np.array_equal(e.keys.cpu().numpy().view(np.uint64), nxt.keys)
+    assert np.array_equal(e.types.cpu().numpy(), nxt.types)
+    assert np.array_equal(e.acc_txn.cpu().numpy().view(np.uint32), nxt.acc_txn())
+    assert np.array_equal(eng.read_table(0, rows), f0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("prefix", [None, 400])
+def test_device_closed_loop(cc, prefix):
+    """dv_epoch_run_closed_loop against the oracle's host loop: epochs one at
+    a time (prefix off) and pipelined prefix-kill epochs, the pool wrapping"""
+    rows, N = 1 << 13, 2000
+    pool = _pool(rows, 5000, 11)
+    eng = CCEngine(cc, N, N * 10)
+    eng.set_prefix(prefix)
+    eng.load_ycsb_partition(rows)
+    _check_loop(eng, cc, rows, pool, N, 6, cur0=1234)
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
+def test_device_closed_loop_halts_and_resume(cc):
+    """asynchronous launches forced to yield (every epoch halts and is decided
+    again before its successor is rebuilt), and a loop continued over three
+    calls (resume) -- the same epochs as one host loop"""
+    rows, N = 1 << 13, 3000
+    pool = _pool(rows, 4000, 12, R=12)
+    eng = CCEngine(cc, N, N * 12)
+    eng.set_prefix(500)
+    eng.set_async_limits(1, 0)
+    eng.load_ycsb_partition(rows)
+    _check_loop(eng, cc, rows, pool, N, 3, calls=3)
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_device_closed_loop_args():
+    import torch
+    rows = 1 << 10
+    pool = _pool(rows, 300, 13)
+    dpool = DeviceEpoch(pool)
+    pb = torch.from_numpy(pool.txn_begin.astype(np.int32)).cuda()
+    eng = CCEngine(dvcc.CALVIN, 300, 3000)
+    eng.load_ycsb_partition(rows)
+    with pytest.raises(dvcc.DvccError):  # no aborts to carry
+        eng.closed_loop(dpool, pb, 100, 2)
+    eng.close()
+    eng = CCEngine(dvcc.NO_WAIT, 300, 3000)
+    eng.load_ycsb_partition(rows)
+    with pytest.raises(dvcc.DvccError):  # more txns per epoch than the pool holds
+        eng.closed_loop(dpool, pb, 301, 2)
+    with pytest.raises(dvcc.DvccError):  # an epoch's bound past the context's max_acc
+        eng.closed_loop(DeviceEpoch(_pool(rows, 400, 14, R=16)), pb, 300, 1)
+    eng.closed_loop(dpool, pb, 250, 2)
+    eng.close()

@@ -45,16 +45,14 @@ def _gpu_epoch(eng, e, path):
 
 
 def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False,
-           asynchronous=True, prefix=0, async_iters=0, async0=True):
+           asynchronous=True, prefix=0, async_iters=0):
     """prefix: dv_set_prefix (0 automatic -- epochs from 131,072 txns --, None
-    off, else the prefix size for every longer epoch).  async0=False: the
-    prefix-kill stages take a round-0 pass and settle before their
-    asynchronous launch (DV_FLAG_NO_ASYNC0)."""
+    off, else the prefix size for every longer epoch)."""
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
                    max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64,
-                   asynchronous=asynchronous, async0=async0)
+                   asynchronous=asynchronous)
     eng.set_prefix(prefix)
     if async_iters:
         eng.set_async_limits(async_iters, 0)
@@ -535,17 +533,16 @@ def test_many_rounds(cc, rows, req, theta, tail, el64, asyn):
 # renumbered sub-epoch -- bit-exact against the oracle however the epoch is cut
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
 @pytest.mark.parametrize("prefix", [1, 17, 500, 4096])
-@pytest.mark.parametrize("async0", [True, False])
-def test_prefix_kill_sizes(cc, prefix, async0):
-    """stages decided by one asynchronous launch straight from their sorted
-    accesses (round_async0), and by a round-0 pass + settle before it"""
+def test_prefix_kill_sizes(cc, prefix):
+    """each stage: round 0, then one asynchronous launch whose statuses stay
+    in the fact words for the stage's consumer (no finalize)"""
     g = YCSBQueryGenerator(1 << 16, zipf_theta=0.9)
-    _check(cc, 1 << 16, [g.gen(20_000, 61), g.gen(20_000, 62)], prefix=prefix, async0=async0)
+    _check(cc, 1 << 16, [g.gen(20_000, 61), g.gen(20_000, 62)], prefix=prefix)
 
 
 @pytest.mark.parametrize("knobs", [dict(asynchronous=False), dict(tail=False, asynchronous=False),
                                    dict(el64=True), dict(async_iters=1), dict(async_iters=2),
-                                   dict(async_iters=1, async0=False), dict(async_iters=3, async0=False)])
+                                   dict(async_iters=3)])
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC])
 def test_prefix_kill_knobs(cc, knobs):
     """the stages' rounds on every decision path: pipelined passes, no tail,
@@ -579,8 +576,7 @@ def test_prefix_kill_repeated_rows():
             keys[b - 1] = keys[a]
     e = Epoch(keys.astype(np.uint64), (rng.random(n) < 0.5).astype(np.uint8), tb)
     for cc in (dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC):
-        for a0 in (True, False):
-            _check(cc, 4096, [e], prefix=300, async0=a0)
+        _check(cc, 4096, [e], prefix=300)
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
