@@ -1243,6 +1243,52 @@ __global__ void k_split_access(const dv_access *acc, uint64_t n, const uint32_t 
     if (bad) atomicOr(err, ERRB_TXN);
 }
 
+// 4-byte host records (dv_epoch_stage_host_rows): row | write << 31, txn ids
+// from the CSR txn_begin.  A wave owns 64 consecutive txns, whose accesses
+// are one contiguous range: its lanes walk that range together (coalesced)
+// and find each access's txn among the 64 starts by a binary search over the
+// lanes' registers.
+__global__ __launch_bounds__(kBlock) void k_split_rows(const uint32_t *__restrict__ rw, const uint32_t *__restrict__ tb,
+                                                       uint32_t n_txn, uint64_t *__restrict__ keys,
+                                                       uint8_t *__restrict__ types, uint32_t *__restrict__ acc_txn,
+                                                       uint8_t *__restrict__ tables) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t waves = gridDim.x * (kBlock / 64);
+    for (uint32_t t0 = (blockIdx.x * kBlock + threadIdx.x) / 64 * 64; t0 < n_txn; t0 += waves * 64) {
+        const uint32_t t = t0 + lane;
+        const uint32_t start = tb[t < n_txn ? t : n_txn];           // (n_txn: the end)
+        const uint32_t lo = __shfl(start, 0, 64);
+        const uint32_t hi = tb[t0 + 64 < n_txn ? t0 + 64 : n_txn];
+        const uint32_t trips = (hi - lo + 63) / 64;  // (wave-uniform: the shuffles read every lane)
+        for (uint32_t k = 0; k < trips; k++) {
+            const uint32_t a = lo + k * 64 + lane;
+            // the last of the 64 txns starting at or before a (lanes past
+            // n_txn hold the end, never <= a; empty txns share a start with
+            // the next one, which wins)
+            uint32_t src = 0;
+#pragma unroll
+            for (uint32_t w = 32; w > 0; w >>= 1) {
+                const uint32_t cand = src + w;
+                if (__shfl(start, (int)cand, 64) <= a) src = cand;
+            }
+            if (a >= hi) continue;
+            const uint32_t v = rw[a];
+            keys[a] = v & 0x7FFFFFFFu;
+            types[a] = (uint8_t)(v >> 31);  // DV_WR = 1, DV_RD = 0
+            acc_txn[a] = t0 + src;
+            tables[a] = 0;
+        }
+    }
+}
+
+void launch_split_rows(hipStream_t s, const uint32_t *rw, uint64_t n, const uint32_t *tb, uint32_t n_txn,
+                       uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables) {
+    if (!n || !n_txn) return;
+    const uint32_t waves = (n_txn + 63) / 64, per = kBlock / 64;
+    const uint32_t g = (waves + per - 1) / per;
+    DV_LAUNCH(k_split_rows, g < 4096 ? g : 4096, kBlock, 0, s, rw, tb, n_txn, keys, types, acc_txn, tables);
+}
+
 void launch_split_access(hipStream_t s, const dv_access *acc, uint64_t n, const uint32_t *tb, uint32_t n_txn,
                          uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables, uint32_t *err) {
     if (!n) return;

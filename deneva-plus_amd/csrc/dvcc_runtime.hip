@@ -143,6 +143,7 @@ struct dv_ctx {
         uint64_t n_acc = 0;
         uint32_t n_txn = 0, max_len = 0;
         bool csr = false, full = false;
+        bool rows = false;  // 4-byte row records (dv_epoch_stage_host_rows)
     } hslot[2];
     hipStream_t copy_stream = nullptr;
 
@@ -2344,15 +2345,14 @@ int dv_epoch_run(dv_ctx *c, const dv_access *acc, uint64_t n_acc, const uint32_t
 
 // Double-buffered host input: the H2D copy of the next
 // epoch's records runs on a copy stream while the current epoch decides.
-int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
-                        uint32_t n_txn) {
-    KProfScope kps_(c);
-    if (!c || slot < 0 || slot > 1) return DV_ERR_ARG;
-    uint32_t max_len = 0;
-    int r = check_host_epoch(c, acc, n_acc, txn_begin, n_txn, &max_len);
-    if (r) return r;
+}  // extern "C"
+
+namespace {
+// queue the H2D of a slot's records (bytes per record: rec) on the copy stream
+int stage_slot(dv_ctx *c, int slot, const void *recs, size_t rec, uint64_t n_acc, const uint32_t *txn_begin,
+               uint32_t n_txn, uint32_t max_len, bool rows) {
     HIPCHK(hipSetDevice(c->cfg.device));
-    r = alloc_host_staging(c);
+    int r = alloc_host_staging(c);
     if (r) return r;
     auto &h = c->hslot[slot];
     if (!c->copy_stream) HIPCHK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
@@ -2367,7 +2367,7 @@ int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_ac
     // the slot's previous epoch has been split out of it
     HIPCHK(hipStreamWaitEvent(c->copy_stream, h.drained, 0));
     if (n_acc) {
-        HIPCHK(hipMemcpyAsync(h.acc, acc, n_acc * sizeof(dv_access), hipMemcpyHostToDevice, c->copy_stream));
+        HIPCHK(hipMemcpyAsync(h.acc, recs, n_acc * rec, hipMemcpyHostToDevice, c->copy_stream));
         if (txn_begin)
             HIPCHK(hipMemcpyAsync(h.tb, txn_begin, ((size_t)n_txn + 1) * sizeof(uint32_t), hipMemcpyHostToDevice,
                                   c->copy_stream));
@@ -2377,8 +2377,32 @@ int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_ac
     h.n_txn = n_txn;
     h.max_len = max_len;
     h.csr = txn_begin != nullptr;
+    h.rows = rows;
     h.full = true;
     return DV_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_stage_host_rows(dv_ctx *c, int slot, const uint32_t *row_wr, uint64_t n_acc,
+                             const uint32_t *txn_begin, uint32_t n_txn) {
+    KProfScope kps_(c);
+    if (!c || slot < 0 || slot > 1 || !txn_begin) return DV_ERR_ARG;
+    uint32_t max_len = 0;
+    int r = check_host_epoch(c, reinterpret_cast<const dv_access *>(row_wr), n_acc, txn_begin, n_txn, &max_len);
+    if (r) return r;
+    return stage_slot(c, slot, row_wr, sizeof(uint32_t), n_acc, txn_begin, n_txn, max_len, true);
+}
+
+int dv_epoch_stage_host(dv_ctx *c, int slot, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
+                        uint32_t n_txn) {
+    KProfScope kps_(c);
+    if (!c || slot < 0 || slot > 1) return DV_ERR_ARG;
+    uint32_t max_len = 0;
+    int r = check_host_epoch(c, acc, n_acc, txn_begin, n_txn, &max_len);
+    if (r) return r;
+    return stage_slot(c, slot, acc, sizeof(dv_access), n_acc, txn_begin, n_txn, max_len, false);
 }
 
 int dv_epoch_run_staged(dv_ctx *c, int slot, const uint64_t *ts, uint8_t *out_commit, uint32_t *out_grant,
@@ -2394,7 +2418,20 @@ int dv_epoch_run_staged(dv_ctx *c, int slot, const uint64_t *ts, uint8_t *out_co
     h.full = false;
     HIPCHK(hipStreamWaitEvent(c->stream, h.copied, 0));
     dv_epoch_dev ep;
-    split_records(c, h.acc, h.n_acc, h.csr ? h.tb : nullptr, h.n_txn, h.max_len, &ep);
+    if (h.rows) {
+        launch_split_rows(c->stream, reinterpret_cast<const uint32_t *>(h.acc), h.n_acc, h.tb, h.n_txn, c->d_keys,
+                          c->d_types, c->d_txn, c->d_tables);
+        ep = dv_epoch_dev{};
+        ep.keys = c->d_keys;
+        ep.types = c->d_types;
+        ep.acc_txn = c->d_txn;
+        ep.tables = c->d_tables;
+        ep.n_acc = h.n_acc;
+        ep.n_txn = h.n_txn;
+        ep.max_txn_acc = h.max_len;
+    } else {
+        split_records(c, h.acc, h.n_acc, h.csr ? h.tb : nullptr, h.n_txn, h.max_len, &ep);
+    }
     HIPCHK(hipEventRecord(h.drained, c->stream));
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     int r = dv_epoch_run_device(c, &ep, c->d_commit, (calvin && out_grant) ? c->d_grant : nullptr, st);

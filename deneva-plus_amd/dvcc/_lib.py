@@ -169,6 +169,7 @@ SIGNATURES = [
     ("dv_epoch_group_run_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint32, _P(_vp), _P(Stats)]),
     ("dv_epoch_stage_host", ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32]),
+    ("dv_epoch_stage_host_rows", ctypes.c_int, [_vp, ctypes.c_int, _vp, ctypes.c_uint64, _vp, ctypes.c_uint32]),
     ("dv_epoch_run_staged", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _P(Stats)]),
     ("dv_tpcc_epoch_run_part", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                               _P(Stats)]),

@@ -56,6 +56,14 @@ class Epoch:
         counts = np.diff(self.txn_begin.astype(np.int64))
         return np.repeat(np.arange(self.n_txn, dtype=np.uint32), counts)
 
+    def to_row_records(self):
+        """4-byte records for dv_epoch_stage_host_rows: key | write << 31
+        (table 0 reads / writes, keys below 2^31)"""
+        if self.n_acc and (int(self.keys.max()) >> 31 or (self.types > 1).any()
+                           or (self.tables is not None and self.tables.any())):
+            raise ValueError("4-byte records hold table-0 reads / writes of keys below 2^31")
+        return (self.keys.astype(np.uint32) | (self.types.astype(np.uint32) << 31)).astype(np.uint32)
+
     def to_access_array(self):
         a = np.zeros(self.n_acc, dtype=[("key", "<u8"), ("txn_seq", "<u4"), ("type", "u1"),
                                         ("table", "u1"), ("flags", "<u2")])
@@ -302,6 +310,12 @@ class CCEngine:
         for an asynchronous copy) into staging slot 0 / 1."""
         L.check(L.lib().dv_epoch_stage_host(self._ctx, slot, _ptr(acc), n_acc, _ptr(tb), n_txn),
                 "dv_epoch_stage_host")
+
+    def stage_host_rows(self, slot, row_wr, tb, n_acc, n_txn):
+        """dv_epoch_stage_host_rows: the same from 4-byte records (key |
+        write << 31, table 0, keys below 2^31) and txn_begin."""
+        L.check(L.lib().dv_epoch_stage_host_rows(self._ctx, slot, _ptr(row_wr), n_acc, _ptr(tb), n_txn),
+                "dv_epoch_stage_host_rows")
 
     def run_staged(self, slot, commit):
         """dv_epoch_run_staged: run the epoch in `slot`; commit bytes to host."""

@@ -282,6 +282,13 @@ int dv_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32
  * running an empty slot is DV_ERR_STATE. */
 int dv_epoch_stage_host(dv_ctx *ctx, int slot, const dv_access *acc, uint64_t n_acc,
                         const uint32_t *txn_begin, uint32_t n_txn);
+/* the same staging from 4-byte records (a quarter of the PCIe bytes): record
+ * i = key | (type == DV_WR) << 31 for a table-0 read or write of a key below
+ * 2^31 (YCSB keys: rows < 2^31), txn_begin (required, n_txn + 1 offsets)
+ * giving each txn's records in sequence order; dv_epoch_run_staged runs it
+ * like any staged epoch. */
+int dv_epoch_stage_host_rows(dv_ctx *ctx, int slot, const uint32_t *row_wr, uint64_t n_acc,
+                             const uint32_t *txn_begin, uint32_t n_txn);
 int dv_epoch_run_staged(dv_ctx *ctx, int slot, const uint64_t *ts, uint8_t *out_commit,
                         uint32_t *out_grant_group, dv_stats *st);
 /* whole epoch on a device-resident epoch; outputs are device pointers

@@ -137,6 +137,50 @@ def test_double_buffered_host_input(cc):
 
 
 @pytest.mark.parametrize("cc", CCS)
+def test_double_buffered_row_records(cc):
+    """dv_epoch_stage_host_rows: 4-byte records (key | write << 31) with
+    txn_begin, slots alternating with 16-byte records; epochs with empty txns
+    (equal starts) and a txn count that is no multiple of a wave's 64"""
+    rows = 1 << 14
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    epochs = [g.gen(n, s) for n, s in ((3001, 21), (2999, 22), (3000, 23))]
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 9, size=1777)  # empty txns among them
+    lens[:3] = 0
+    tb = np.zeros(len(lens) + 1, np.uint32)
+    tb[1:] = np.cumsum(lens)
+    epochs.append(Epoch(rng.integers(0, rows, size=int(tb[-1])).astype(np.uint64),
+                        (rng.random(int(tb[-1])) < 0.4).astype(np.uint8), tb))
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, 3001, max(e.n_acc for e in epochs))
+    try:
+        eng.load_ycsb_partition(rows)
+
+        def stage(slot, e):
+            tbp = torch.from_numpy(np.ascontiguousarray(e.txn_begin, dtype=np.uint32)).pin_memory()
+            if slot == 0:
+                eng.stage_host_rows(0, torch.from_numpy(e.to_row_records()).pin_memory(), tbp, e.n_acc, e.n_txn)
+            else:
+                eng.stage_host(1, torch.from_numpy(e.to_access_array().view(np.uint8)).pin_memory(), tbp,
+                               e.n_acc, e.n_txn)
+        commit = torch.zeros(3001, dtype=torch.uint8).pin_memory()
+        stage(0, epochs[0])
+        for i, e in enumerate(epochs):
+            if i + 1 < len(epochs):
+                stage((i + 1) % 2, epochs[i + 1])
+            st = eng.run_staged(i % 2, commit)
+            c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+            assert (commit.numpy()[:e.n_txn] == c_ref).all(), i
+            assert st.committed == st_ref.committed and st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == f0).all()
+        with pytest.raises(ValueError):
+            Epoch(np.array([1 << 31], np.uint64), np.zeros(1, np.uint8), np.array([0, 1], np.uint32)).to_row_records()
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("cc", CCS)
 def test_epochs_carry_table_state(cc):
     g = YCSBQueryGenerator(1 << 14, zipf_theta=0.8)
     _check(cc, 1 << 14, [g.gen(3000, s) for s in (1, 2, 3)])

@@ -14,6 +14,8 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 B="bench.py --steps 5 --warmup 2 --epochs 2 --no-cpu-baseline --no-tpcc"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -T -d $OUT/kt -o run -- python3 $B \
     > $OUT/kt_bench.json 2> $OUT/kt.err
+KT=$(find $OUT/kt -name 'run_kernel_trace.csv' | head -1)
+python3 tools/ktrace.py $KT --epoch 5 > $OUT/timeline.txt
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 120 rocprofv3 --pmc $C -f csv -T -d $OUT/pmc_$C -o run -- python3 $B \
       > $OUT/pmc_$C.json 2> $OUT/pmc_$C.err
