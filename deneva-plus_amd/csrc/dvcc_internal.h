@@ -523,7 +523,8 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
                         uint64_t zero_words = 0, bool gate = false, Counters *hctr = nullptr,
-                        unsigned long long *hseq = nullptr, unsigned long long seq = 0);
+                        unsigned long long *hseq = nullptr, unsigned long long seq = 0,
+                        uint64_t *txn_zero8 = nullptr);  // (one 8-byte word per txn zeroed: TPC-C o_ids)
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,

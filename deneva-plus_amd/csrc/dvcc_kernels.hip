@@ -887,7 +887,7 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
                                                         uint4 *__restrict__ zero, uint64_t zero_n, int gate,
                                                         Counters *hctr, unsigned long long *hseq,
-                                                        unsigned long long seq) {
+                                                        unsigned long long seq, uint64_t *__restrict__ zero8) {
     if (blockIdx.x == 0) {
         // pipelined epochs: the previous epoch's counters into their host
         // mirror first (what k_ctr_out would have done as one more launch)
@@ -919,6 +919,7 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
         tb_start[i] = 0;
         tb_end[i] = 0;
         if (tlen) tlen[i] = 0;
+        if (zero8 && i < n_txn) zero8[i] = 0;
     }
     for (uint64_t i = blockIdx.x * kBlock + threadIdx.x; i < zero_n; i += stride) zero[i] = uint4{0, 0, 0, 0};
 }
@@ -944,13 +945,13 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
-                        Counters *hctr, unsigned long long *hseq, unsigned long long seq) {
+                        Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint64_t *txn_zero8) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
-                                       gate ? 1 : 0, hctr, hseq, seq);
+                                       gate ? 1 : 0, hctr, hseq, seq, txn_zero8);
 }
 
 // ---------------------------------------------------------------- execute

@@ -189,17 +189,18 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
     }
 }
 
-// any kill bit in accesses [a0, a1)
+// any kill bit in accesses [a0, a1): the first and last words loaded
+// unconditionally (a txn spans at most 3 words), so the callers' unrolled
+// loops keep every txn's loads in flight together
 __device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_bits, uint32_t a0, uint32_t a1) {
     if (a0 >= a1) return false;
     const uint32_t wlo = a0 >> 6, whi = (a1 - 1) >> 6;
-    bool k = false;
-    for (uint32_t w = wlo; w <= whi; w++) {
-        uint64_t m = kill_bits[w];
-        if (w == wlo) m &= ~0ull << (a0 & 63);
-        if (w == whi) m &= ~0ull >> (63 - ((a1 - 1) & 63));
-        k |= m != 0;
-    }
+    uint64_t lo = kill_bits[wlo], hi = kill_bits[whi];
+    lo &= ~0ull << (a0 & 63);
+    hi &= ~0ull >> (63 - ((a1 - 1) & 63));
+    if (wlo == whi) return (lo & hi) != 0;
+    bool k = (lo | hi) != 0;
+    for (uint32_t w = wlo + 1; w < whi; w++) k |= kill_bits[w] != 0;
     return k;
 }
 
@@ -208,11 +209,14 @@ __device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_b
 // 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
 // and their sort keys written densely in that order, pairs_b = row << 32 |
 // sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
-// their layout).  One launch: tiles of kKillTile txns taken by ticket, two
-// decoupled look-backs (survivors, their accesses) give every tile its output
-// offsets; the tile's survivors are listed in LDS and their accesses written
-// by the whole block, one access per thread (no serial per-txn loops).  The
-// last tile publishes S and the access count (b_txn, b_acc).
+// their layout).  One launch: tiles of kKillTile txns taken by ticket.  The
+// tile's txns are checked block-strided (coalesced access-range loads and
+// status stores, every txn's kill words in flight together) into LDS; each
+// thread then ranks its kKillIPT consecutive txns from there, two decoupled
+// look-backs (survivors, their accesses) give every tile its output offsets,
+// the tile's survivors are listed in LDS and their accesses written by the
+// whole block, one access per thread (no serial per-txn loops).  The last
+// tile publishes S and the access count (b_txn, b_acc).
 __global__ __launch_bounds__(kBlock) void k_kill_compact(
     const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
     const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint64_t *__restrict__ kill_bits,
@@ -224,6 +228,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
     __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
+    __shared__ uint32_t l_st[kKillTile], l_len[kKillTile];      // per tile txn: first access, survivor length
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;  // (b_txn = b_acc = 0 from the epoch clear)
@@ -231,25 +236,38 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
-    const uint32_t first = K + tile * kKillTile + tid * kKillIPT;
+    const uint32_t t_lo = K + tile * kKillTile;
+    {
+        uint32_t a0[kKillIPT], a1[kKillIPT];
+#pragma unroll
+        for (int j = 0; j < kKillIPT; j++) {
+            const uint32_t t = t_lo + j * kBlock + tid;
+            a0[j] = t < n_txn ? tb_start[t] : 0u;
+            a1[j] = t < n_txn ? tb_end[t] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kKillIPT; j++) {
+            const uint32_t t = t_lo + j * kBlock + tid;
+            // a committed prefix txn holds one of its rows
+            const bool killed = range_killed(kill_bits, a0[j], a1[j]);
+            if (killed && t < n_txn) status[t] = ST_ABORT;
+            l_st[j * kBlock + tid] = a0[j];
+            l_len[j * kBlock + tid] = (t < n_txn && !killed) ? (a1[j] - a0[j]) | 0x80000000u : 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t first = t_lo + tid * kKillIPT;
     uint32_t surv = 0, cnt = 0, acc = 0;
     uint32_t a0s[kKillIPT], lens[kKillIPT];
 #pragma unroll
     for (int j = 0; j < kKillIPT; j++) {
-        const uint32_t t = first + j;
-        a0s[j] = 0;
-        lens[j] = 0;
-        if (t >= n_txn) continue;
-        const uint32_t a0 = tb_start[t], a1 = tb_end[t];
-        if (range_killed(kill_bits, a0, a1)) {  // a committed prefix txn holds one of its rows
-            status[t] = ST_ABORT;
-            continue;
-        }
-        a0s[j] = a0;
-        lens[j] = a1 - a0;
+        const uint32_t info = l_len[tid * kKillIPT + j];
+        a0s[j] = l_st[tid * kKillIPT + j];
+        lens[j] = info & 0x7FFFFFFFu;
+        if (!info) continue;
         surv |= 1u << j;
         cnt++;
-        acc += a1 - a0;
+        acc += lens[j];
     }
     const Agg inc_c = wave_incl<OpPlain>(Agg{0u, 0u, cnt}, lane);
     const Agg inc_a = wave_incl<OpPlain>(Agg{0u, 0u, acc}, lane);

@@ -385,7 +385,11 @@ uint32_t *next_ticket(dv_ctx *c) {
 // decoupled look-back -- measured slower here: every tile of these sorts is
 // resident at once, so the look-back became a chain of cross-XCD hand-offs,
 // 167 us of scatters per config-D epoch against 125 us for the three-launch
-// passes.)
+// passes.  Round 3 measured it again with a thread per digit walking 16 tiles
+// per round trip: 17.6 us per pass + 10.4 us of histogram per sort against
+// 19.5 us per three-launch pass, 127 us per epoch against 114; and with every
+// predecessor's count summed in one hop (no inclusive prefixes), 21.8 us per
+// pass: the hand-offs cost more than the two kernel boundaries they save.)
 int sort_rows(dv_ctx *c, uint64_t n, int key_bits, hipEvent_t *ev, bool hist0_done, const uint32_t *n_dev) {
     return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev);
 }
@@ -1108,8 +1112,11 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     const uint32_t slog = calvin ? 7u : c->slog;  // CALVIN: positions only name access ids
     rec(c, 0);
+    // (TPC-C: the o_id outputs zeroed here, k_tpcc_oid writes the committed NewOrders')
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
-                       c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr);
+                       c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr, nullptr,
+                       0, false, nullptr, nullptr, 0,
+                       c->cfg.workload == DV_TPCC ? c->tp_oid : nullptr);
     c->ticket = 0;
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles && !ep->n_acc_dev;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
@@ -1293,7 +1300,6 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.tile_ctr = next_ticket(c);
         x.oid = c->tp_oid;
         x.ctr = c->ctr;
-        if (c->tp_oid) (void)hipMemsetAsync(c->tp_oid, 0, (size_t)c->n_txn * 8, c->stream);
         launch_tpcc_exec(c->stream, x);
     } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
         if (c->cfg.cc_alg == DV_CALVIN)

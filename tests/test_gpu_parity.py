@@ -623,6 +623,18 @@ def test_prefix_kill_repeated_rows():
         _check(cc, 4096, [e], prefix=300)
 
 
+@pytest.mark.parametrize("cc", CCS)
+def test_sorts_past_2_20_rows(cc):
+    """rows past 2^20 (24-bit sort keys, 3 passes of 8 bits): whole epochs,
+    and prefix and survivors stages (their count only on the device)"""
+    rows = 1 << 22
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    eps = [g.gen(30_000, 131), g.gen(7_000, 132), g.gen(1, 133)]
+    _check(cc, rows, eps, prefix=None)
+    if cc != dvcc.CALVIN:
+        _check(cc, rows, eps[:2], prefix=3000)
+
+
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
 def test_medium_epoch_without_tail(cc):
     g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)
