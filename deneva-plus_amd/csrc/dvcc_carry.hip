@@ -218,6 +218,33 @@ void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_star
               ptxn, ptb, pool_n, tot, n_out, okeys, otypes, otxn, otables, n_acc_dev);
 }
 
+// a client batch's per-txn access ranges from its acc_txn (non-decreasing;
+// ids at or past n_txn were rejected by the run that decided it): zeroed
+// first (a txn without accesses keeps an empty range), then each run's ends
+__global__ void k_txn_ranges_zero(uint32_t *__restrict__ tbs, uint32_t *__restrict__ tbe, uint32_t n_txn) {
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n_txn; t += gridDim.x * blockDim.x)
+        tbs[t] = tbe[t] = 0;
+}
+__global__ void k_txn_ranges(const uint32_t *__restrict__ acc_txn, uint64_t n, uint32_t n_txn,
+                             uint32_t *__restrict__ tbs, uint32_t *__restrict__ tbe) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t t = acc_txn[i];
+        if (t >= n_txn) continue;
+        if (i == 0 || acc_txn[i - 1] != t) tbs[t] = (uint32_t)i;
+        if (i + 1 == n || acc_txn[i + 1] != t) tbe[t] = (uint32_t)(i + 1);
+    }
+}
+
+void launch_txn_ranges(hipStream_t s, const uint32_t *acc_txn, uint64_t n, uint32_t n_txn, uint32_t *tbs,
+                       uint32_t *tbe) {
+    if (!n_txn) return;
+    const uint32_t gt = (n_txn + kBlock - 1) / kBlock;
+    DV_LAUNCH(k_txn_ranges_zero, gt < 2048 ? gt : 2048, kBlock, 0, s, tbs, tbe, n_txn);
+    if (!n) return;
+    const uint64_t ga = (n + kBlock - 1) / kBlock;
+    DV_LAUNCH(k_txn_ranges, (uint32_t)(ga < 4096 ? ga : 4096), kBlock, 0, s, acc_txn, n, n_txn, tbs, tbe);
+}
+
 uint32_t carry_blocks(uint32_t n_txn) { return n_txn ? (n_txn + kCarryTpb - 1) / kCarryTpb : 0; }
 
 void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,

@@ -472,6 +472,10 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
                   const uint8_t *tables, uint64_t *okeys, uint8_t *otypes, uint32_t *otxn,
                   uint8_t *otables, uint32_t *bt, uint32_t *ba, uint32_t *tot);
 
+// per-txn access ranges of a batch from its acc_txn (dv_epoch_group_carry)
+void launch_txn_ranges(hipStream_t s, const uint32_t *acc_txn, uint64_t n, uint32_t n_txn, uint32_t *tbs,
+                       uint32_t *tbe);
+
 // the closed loop (dv_epoch_refill): the aborted txns of the decided epoch
 // (status, access ranges, its keys / types / tables) carried first, capped
 // at n_out, then n_out - C fresh txns of the pool (pkeys ... ptb, pool_n txns)
@@ -508,8 +512,8 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          const uint32_t *row_state, uint64_t rs_words,
                          int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
-                         uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-                         Counters *ctr);
+                         uint64_t *pairs_b, uint32_t *info, uint32_t *tsum, Counters *ctr);
+// (info: one word per txn after the prefix; tsum: 2 x kill_tiles words)
 // words (the survivors' asynchronous launch left their statuses there): their
 // statuses from the fact words, else from status_b
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -32,7 +32,7 @@ namespace dvcc {
 
 namespace {
 #ifndef DVCC_KILL_IPT
-#define DVCC_KILL_IPT 16
+#define DVCC_KILL_IPT 4
 #endif
 constexpr int kKillIPT = DVCC_KILL_IPT;                 // txns per thread in k_kill_compact
 constexpr uint32_t kKillTile = kBlock * kKillIPT;       // txns per tile
@@ -209,50 +209,84 @@ __device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_b
 // 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
 // and their sort keys written densely in that order, pairs_b = row << 32 |
 // sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
-// their layout).  One launch: tiles of kKillTile txns taken by ticket.  The
-// tile's txns are checked block-strided (coalesced access-range loads and
-// status stores, every txn's kill words in flight together) into LDS; each
-// thread then ranks its kKillIPT consecutive txns from there, two decoupled
-// look-backs (survivors, their accesses) give every tile its output offsets,
-// the tile's survivors are listed in LDS and their accesses written by the
-// whole block, one access per thread (no serial per-txn loops).  The last
-// tile publishes S and the access count (b_txn, b_acc).
-__global__ __launch_bounds__(kBlock) void k_kill_compact(
-    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end,
-    const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn, const uint64_t *__restrict__ kill_bits,
-    uint8_t *__restrict__ status, uint32_t *__restrict__ map, uint8_t *__restrict__ status_b,
-    uint8_t *__restrict__ tlen_b,
-    uint64_t *__restrict__ pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-    Counters *ctr) {
-    __shared__ uint32_t s_tile;
+// their layout).  Two launches over tiles of kKillTile txns:
+//   k_kill_count: the tile's txns checked block-strided (coalesced access
+//     ranges and status stores, every txn's kill words in flight together),
+//     one info word per txn (survivor: its length | 1 << 31) and the tile's
+//     survivor and access counts;
+//   k_kill_emit: each tile sums the counts of the tiles before it (plain
+//     loads behind the kernel boundary), ranks its survivors, lists them in
+//     LDS and writes their accesses with the whole block, one access per
+//     thread.  The last tile publishes S and the access count (b_txn, b_acc).
+// (One launch with decoupled look-backs for the tile offsets took 33 us at
+// config D: the look-backs' cross-CU hand-offs cost more than the boundary.)
+__global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restrict__ tb_start,
+                                                       const uint32_t *__restrict__ tb_end, uint32_t K,
+                                                       uint32_t n_txn, const uint64_t *__restrict__ kill_bits,
+                                                       uint8_t *__restrict__ status, uint32_t *__restrict__ info,
+                                                       uint32_t *__restrict__ tsum, const Counters *ctr) {
+    __shared__ uint32_t lds4[4];
+    const uint32_t m = n_txn > K ? n_txn - K : 0u;
+    const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
+    if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t_lo = K + blockIdx.x * kKillTile;
+    uint32_t a0[kKillIPT], a1[kKillIPT];
+#pragma unroll
+    for (int j = 0; j < kKillIPT; j++) {
+        const uint32_t t = t_lo + j * kBlock + tid;
+        a0[j] = t < n_txn ? tb_start[t] : 0u;
+        a1[j] = t < n_txn ? tb_end[t] : 0u;
+    }
+    uint32_t cnt = 0, acc = 0;
+#pragma unroll
+    for (int j = 0; j < kKillIPT; j++) {
+        const uint32_t t = t_lo + j * kBlock + tid;
+        if (t >= n_txn) continue;
+        // a committed prefix txn holds one of its rows
+        const bool killed = range_killed(kill_bits, a0[j], a1[j]);
+        if (killed) status[t] = ST_ABORT;
+        info[t - K] = killed ? 0u : (a1[j] - a0[j]) | 0x80000000u;
+        cnt += killed ? 0u : 1u;
+        acc += killed ? 0u : a1[j] - a0[j];
+    }
+    uint32_t tc = 0, ta = 0;
+    (void)block_excl_scan256(cnt, lds4, &tc);
+    (void)block_excl_scan256(acc, lds4, &ta);
+    if (tid == 0) {
+        tsum[2 * blockIdx.x] = tc;
+        tsum[2 * blockIdx.x + 1] = ta;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_kill_emit(
+    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn,
+    const uint32_t *__restrict__ info, const uint32_t *__restrict__ tsum, uint32_t *__restrict__ map,
+    uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b, uint64_t *__restrict__ pairs_b, Counters *ctr) {
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
     __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
-    __shared__ uint32_t l_st[kKillTile], l_len[kKillTile];      // per tile txn: first access, survivor length
+    __shared__ uint32_t l_st[kKillTile], l_len[kKillTile];      // per tile txn: first access, info word
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;  // (b_txn = b_acc = 0 from the epoch clear)
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(tile_ctr, 1u);
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = blockIdx.x;
     const uint32_t t_lo = K + tile * kKillTile;
-    {
-        uint32_t a0[kKillIPT], a1[kKillIPT];
 #pragma unroll
-        for (int j = 0; j < kKillIPT; j++) {
-            const uint32_t t = t_lo + j * kBlock + tid;
-            a0[j] = t < n_txn ? tb_start[t] : 0u;
-            a1[j] = t < n_txn ? tb_end[t] : 0u;
-        }
+    for (int j = 0; j < kKillIPT; j++) {
+        const uint32_t t = t_lo + j * kBlock + tid;
+        l_st[j * kBlock + tid] = t < n_txn ? tb_start[t] : 0u;
+        l_len[j * kBlock + tid] = t < n_txn ? info[t - K] : 0u;
+    }
+    if (wave < 2) {  // the tiles before this one: wave 0 survivors, wave 1 their accesses
+        uint32_t sum = 0;
+        for (uint32_t q = lane; q < tile; q += 64) sum += tsum[2 * q + wave];
 #pragma unroll
-        for (int j = 0; j < kKillIPT; j++) {
-            const uint32_t t = t_lo + j * kBlock + tid;
-            // a committed prefix txn holds one of its rows
-            const bool killed = range_killed(kill_bits, a0[j], a1[j]);
-            if (killed && t < n_txn) status[t] = ST_ABORT;
-            l_st[j * kBlock + tid] = a0[j];
-            l_len[j * kBlock + tid] = (t < n_txn && !killed) ? (a1[j] - a0[j]) | 0x80000000u : 0u;
+        for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+        if (lane == 0) {
+            (wave == 0 ? s_sub0 : s_ab0) = sum;
+            if (tile == ntiles - 1) (wave == 0 ? ctr->b_txn : ctr->b_acc) = sum + tsum[2 * tile + wave];
         }
     }
     __syncthreads();
@@ -261,10 +295,10 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
     uint32_t a0s[kKillIPT], lens[kKillIPT];
 #pragma unroll
     for (int j = 0; j < kKillIPT; j++) {
-        const uint32_t info = l_len[tid * kKillIPT + j];
+        const uint32_t w = l_len[tid * kKillIPT + j];
         a0s[j] = l_st[tid * kKillIPT + j];
-        lens[j] = info & 0x7FFFFFFFu;
-        if (!info) continue;
+        lens[j] = w & 0x7FFFFFFFu;
+        if (!w) continue;
         surv |= 1u << j;
         cnt++;
         acc += lens[j];
@@ -276,16 +310,14 @@ __global__ __launch_bounds__(kBlock) void k_kill_compact(
         wt_a[wave] = inc_a;
     }
     __syncthreads();
-    if (wave < 2) {  // the two look-backs side by side: wave 0 survivors, wave 1 their accesses
-        const Agg *wt = wave == 0 ? wt_c : wt_a;
-        Agg bt{0u, 0u, 0u};
-        for (int w = 0; w < kBlock / 64; w++) bt = OpPlain::comb(bt, wt[w]);
-        const Agg pt = look_back<OpPlain>(wave == 0 ? desc_c : desc_a, tile, tag, bt, lane, ctr);
-        if (lane == 0) {
-            (wave == 0 ? s_sub0 : s_ab0) = pt.c;
-            (wave == 0 ? s_nsurv : s_nacc) = bt.c;
-            if (tile == ntiles - 1) (wave == 0 ? ctr->b_txn : ctr->b_acc) = pt.c + bt.c;
+    if (tid == 0) {
+        uint32_t c = 0, a = 0;
+        for (int w = 0; w < kBlock / 64; w++) {
+            c += wt_c[w].c;
+            a += wt_a[w].c;
         }
+        s_nsurv = c;
+        s_nacc = a;
     }
     // this thread's survivors: their slots in the tile's list
     uint32_t ls = 0, la = 0;
@@ -384,8 +416,7 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          const uint32_t *row_state, uint64_t rs_words,
                          int nowait,
                          uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
-                         uint64_t *pairs_b, uint64_t *desc_c, uint64_t *desc_a, uint32_t *tile_ctr, uint32_t tag,
-                         Counters *ctr) {
+                         uint64_t *pairs_b, uint32_t *info, uint32_t *tsum, Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
@@ -393,8 +424,9 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
     DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
                                                                      row_state + (rs_words - kBloomWords), nowait,
                                                                      kill_bits, ctr);
-    DV_LAUNCH(k_kill_compact, nt, kBlock, 0, s, tb_start, tb_end, acc_row, K, n_txn, kill_bits, status, map, status_b,
-                                         tlen_b, pairs_b, desc_c, desc_a, tile_ctr, tag, ctr);
+    DV_LAUNCH(k_kill_count, nt, kBlock, 0, s, tb_start, tb_end, K, n_txn, kill_bits, status, info, tsum, ctr);
+    DV_LAUNCH(k_kill_emit, nt, kBlock, 0, s, tb_start, acc_row, K, n_txn, info, tsum, map, status_b, tlen_b, pairs_b,
+              ctr);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -156,11 +156,17 @@ __device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw,
 // inclusive prefix, 64 descriptors per step (config D: 16K/8K-element tiles
 // took 2.5 % less epoch time than 8K/4K, 4K/4K took 3 % more).
 template <class EIn>
+#ifndef DVCC_ROUND_IPT
+#define DVCC_ROUND_IPT 16
+#endif
+#ifndef DVCC_ROUND_T64
+#define DVCC_ROUND_T64 512
+#endif
 struct Geo {
-    static constexpr int kThreads = sizeof(EIn) == 4 ? 1024 : 512;
+    static constexpr int kThreads = sizeof(EIn) == 4 ? 1024 : DVCC_ROUND_T64;
     static constexpr int kMinWaves = sizeof(EIn) == 4 ? 4 : 3;  // per SIMD: <= 128 / 168 VGPRs
     static constexpr int kWaves = kThreads / 64;
-    static constexpr int kIPT = 16;
+    static constexpr int kIPT = DVCC_ROUND_IPT;
     static constexpr uint32_t kTile = kThreads * kIPT;
 };
 __device__ __forceinline__ uint32_t pad16(uint32_t j) { return j + (j >> 4); }

@@ -103,6 +103,8 @@ struct dv_ctx {
     uint32_t *carry_b = nullptr;                     // abort carry-over: block counts (2 x carry_nb)
     uint32_t carry_nb = 0;
     uint32_t *carry_tot = nullptr;                   // its totals (kRefillTot words)
+    uint32_t *gc_tb = nullptr;                       // dv_epoch_group_carry: a batch's ranges (2 x max_txn)
+    uint32_t *gc_tot = nullptr;                      // ... 3 totals per batch (kMaxGroupBatches)
     DvComm *comm = nullptr;                          // RCCL communicator (dv_comm_init)
     uint32_t round_tag = 0;                          // descriptor tag of the last pass
     uint32_t ticket = 0;                             // next tile_ctr slot
@@ -193,9 +195,9 @@ struct dv_ctx {
     uint64_t row_state_cap = 0;    // (words)
     uint8_t *b_status = nullptr, *b_tlen = nullptr;  // the survivors' sub-epoch (txn capacity)
     uint32_t *b_map = nullptr;                      // survivor -> txn
-    uint64_t *kdesc = nullptr;                      // k_kill_compact look-back descriptors (2 arrays)
+    uint32_t *kinfo = nullptr;                      // k_kill_count -> k_kill_emit: one word per txn
+    uint32_t *ktsum = nullptr;                      // ... and two counts per tile
     uint64_t *kill_bits = nullptr;                  // one bit per access: killed by the prefix's commits
-    uint32_t kdesc_n = 0;                           // descriptors per array
 
     // timing
     hipEvent_t ev[32] = {};
@@ -356,7 +358,6 @@ uint32_t next_tag(dv_ctx *c) {
     if (++c->round_tag >= (1u << 25)) {
         (void)hipMemsetAsync(c->desc, 0, (size_t)((c->cfg.max_acc + kRTile - 1) / kRTile) * 8,
                              c->stream);
-        if (c->kdesc) (void)hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream);
         c->round_tag = 1;
     }
     return c->round_tag;
@@ -561,7 +562,7 @@ void dv_close(dv_ctx *c) {
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
                     c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
-                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kdesc, c->kill_bits,
+                    c->row_state, c->b_status, c->b_tlen, c->b_map, c->kinfo, c->ktsum, c->kill_bits, c->gc_tb, c->gc_tot,
                     c->hslot[0].acc, c->hslot[0].tb, c->hslot[1].acc, c->hslot[1].tb};
     for (void *b : bufs) dfree(b);
     for (auto &h : c->hslot) {
@@ -738,6 +739,49 @@ int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch
     out->n_txn = tot[0];
     out->n_acc = tot[1];
     out->max_txn_acc = ep->max_txn_acc;
+    return DV_OK;
+}
+
+int dv_epoch_group_carry(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
+                         const uint8_t *d_commit, uint32_t max_txn, dv_epoch_dev *outs) {
+    KProfScope kps_(c);
+    constexpr uint32_t kMaxGroupBatches = 64;
+    if (!c || !homes || !d_commit || !outs || !n_homes || n_homes > kMaxGroupBatches) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    if (txns_per_rank > c->cfg.max_txn) return DV_ERR_ARG;
+    for (uint32_t e = 0; e < n_homes; e++) {
+        const dv_epoch_dev &h = homes[e];
+        const dv_epoch_dev &o = outs[e];
+        if (h.n_txn > txns_per_rank || (h.n_acc && (!h.keys || !h.types || !h.acc_txn))) return DV_ERR_ARG;
+        if (h.n_acc && (!o.keys || !o.types || !o.acc_txn || (h.tables && !o.tables))) return DV_ERR_ARG;
+    }
+    HIPCHK(hipSetDevice(c->cfg.device));
+    int r = carry_bufs(c, carry_blocks(txns_per_rank));
+    if (!r && !c->gc_tb) r = dalloc(&c->gc_tb, 2ull * c->cfg.max_txn + 2);
+    if (!r && !c->gc_tot) r = dalloc(&c->gc_tot, 3ull * kMaxGroupBatches);
+    if (r) return r;
+    uint32_t *tbs = c->gc_tb, *tbe = c->gc_tb + c->cfg.max_txn + 1;
+    for (uint32_t e = 0; e < n_homes; e++) {
+        const dv_epoch_dev &h = homes[e];
+        dv_epoch_dev &o = outs[e];
+        launch_txn_ranges(c->stream, h.acc_txn, h.n_acc, h.n_txn, tbs, tbe);
+        // the commit bytes of this rank's txns of epoch e: 1 committed (== ST_COMMIT), 0 aborted
+        launch_carry(c->stream, d_commit + (size_t)e * txns_per_rank, tbs, tbe, h.n_txn, max_txn, h.keys, h.types,
+                     h.tables, const_cast<uint64_t *>(o.keys), const_cast<uint8_t *>(o.types),
+                     const_cast<uint32_t *>(o.acc_txn), h.tables ? const_cast<uint8_t *>(o.tables) : nullptr,
+                     c->carry_b, c->carry_b + c->carry_nb, c->gc_tot + 3 * e);
+    }
+    HIPCHK(hipGetLastError());
+    uint32_t tot[3 * kMaxGroupBatches];
+    HIPCHK(hipMemcpyAsync(tot, c->gc_tot, 3ull * n_homes * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (uint32_t e = 0; e < n_homes; e++) {
+        outs[e].n_txn = tot[3 * e];
+        outs[e].n_acc = tot[3 * e + 1];
+        outs[e].max_txn_acc = homes[e].max_txn_acc;
+        outs[e].ts = nullptr;
+        outs[e].n_acc_dev = nullptr;
+    }
     return DV_OK;
 }
 
@@ -1640,12 +1684,9 @@ int enqueue_survivors(dv_ctx *c) {
     const uint32_t K = c->pf_K;
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr, c->prefix_words ? c->tword : nullptr);
-    const uint32_t tag = next_tag(c);
     launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, c->pf_n_acc_dev, K, c->n_txn,
-                        c->row_state,
-                        rs_words, nowait,
-                        c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen, c->pairs[0], c->kdesc,
-                        c->kdesc + c->kdesc_n, next_ticket(c), tag, c->ctr);
+                        c->row_state, rs_words, nowait, c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen,
+                        c->pairs[0], c->kinfo, c->ktsum, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
@@ -1715,11 +1756,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         if (!r) r = dalloc(&c->b_tlen, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_map, T);
         if (!r) r = dalloc(&c->kill_bits, kill_words(c->cfg.max_acc));
-        if (!r) {
-            c->kdesc_n = kill_tiles(T) + 1;
-            r = dalloc(&c->kdesc, 2ull * c->kdesc_n);
-        }
-        if (!r) r = hip_fail(hipMemsetAsync(c->kdesc, 0, 2ull * c->kdesc_n * 8, c->stream), "memset");
+        if (!r) r = dalloc(&c->kinfo, T);
+        if (!r) r = dalloc(&c->ktsum, 2ull * kill_tiles(T) + 2);
         if (r) return r;
     }
     const int key_bits = bits_for(row_space(c));

@@ -130,6 +130,8 @@ SIGNATURES = [
     ("dv_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _P(Stats)]),
     ("dv_epoch_begin", ctypes.c_int, [_vp, _P(EpochDev), _vp]),
     ("dv_epoch_carry", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(EpochDev)]),
+    ("dv_epoch_group_carry", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, ctypes.c_uint32, _vp,
+                                            ctypes.c_uint32, _P(EpochDev)]),
     ("dv_comm_unique_id", ctypes.c_int, [_vp]),
     ("dv_comm_init", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     ("dv_comm_init_local", ctypes.c_int, [_P(_vp), ctypes.c_int]),

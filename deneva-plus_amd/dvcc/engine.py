@@ -462,6 +462,37 @@ class CCEngine:
                                                  cps, sts), "dv_epoch_run_closed_loop")
         return list(sts)[:n_epochs], bufs, cursor
 
+    def group_carry(self, homes, d_commit, txns_per_rank, max_txn=None):
+        """Retries across epoch groups (dv_epoch_group_carry): for each of this
+        rank's batches of the group just run (DeviceEpochs), a DeviceEpoch of
+        its aborted txns (commit byte 0 in d_commit at e * txns_per_rank), in
+        sequence order, at most max_txn each -- the head of the same epoch
+        slot's batch in the next group."""
+        import torch
+        outs, keep = [], []
+        for h in homes:
+            dev = h.keys.device
+            n = max(1, h.n_acc)
+            t = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.uint8, device=dev),
+                 torch.empty(n, dtype=torch.int32, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev) if h.tables is not None else None)
+            keep.append(t)
+            outs.append(L.EpochDev(t[0].data_ptr(), t[1].data_ptr(), t[2].data_ptr(),
+                                   t[3].data_ptr() if t[3] is not None else None, 0, 0, 0))
+        arr = (L.EpochDev * len(homes))(*[h.desc() for h in homes])
+        oarr = (L.EpochDev * len(homes))(*outs)
+        cap = txns_per_rank if max_txn is None else max_txn
+        self._after_torch()
+        L.check(L.lib().dv_epoch_group_carry(self._ctx, arr, len(homes), txns_per_rank, _ptr(d_commit), cap, oarr),
+                "dv_epoch_group_carry")
+        res = []
+        for o, t in zip(oarr, keep):
+            n = int(o.n_acc)
+            res.append(DeviceEpoch.from_tensors(t[0][:n], t[1][:n], t[2][:n], int(o.n_txn),
+                                                tables=t[3][:n] if t[3] is not None else None,
+                                                max_txn_acc=int(o.max_txn_acc)))
+        return res
+
     def carry(self, dep, max_txn=None):
         """Abort carry-over: a DeviceEpoch of the last epoch's (`dep`'s)
         aborted txns, in sequence order, at most max_txn of them."""

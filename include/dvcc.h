@@ -431,6 +431,22 @@ int dv_epoch_run_closed_loop(dv_ctx *ctx, const dv_epoch_dev *pool, const uint32
  * A caller retrying aborts epoch by epoch needs dv_epoch_run_part. */
 int dv_epoch_group_run(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st);
+/* Retries across epoch groups (the reference's AbortQueue, abort_queue.cpp:
+ * 26-82, with a penalty of one group = P epochs): after dv_epoch_group_run
+ * (or one group of dv_epoch_group_run_batch) returned d_commit for `homes`,
+ * writes into outs[e] the accesses of this rank's txns of homes[e] whose
+ * commit byte is 0 -- in sequence order, renumbered 0..C-1, C = min(aborted,
+ * max_txn) -- into outs[e].keys / types / acc_txn (/ tables when
+ * homes[e].tables is set: device arrays with room for homes[e].n_acc
+ * accesses), and sets outs[e].n_txn / n_acc / max_txn_acc.  The caller opens
+ * rank r's batch of epoch e of group g + 1 with them, ahead of its new txns:
+ * a txn aborted in epoch e of group g is retried in epoch e of group g + 1
+ * (same epoch slot, so the retries of group g enter group g + 1 in their
+ * order), P epochs later instead of one -- the price of deciding a group's
+ * epochs side by side (the open-loop precondition above).  Purely local: no
+ * collective; one host wait for the counts. */
+int dv_epoch_group_carry(dv_ctx *ctx, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
+                         const uint8_t *d_commit, uint32_t max_txn, dv_epoch_dev *outs);
 /* n_groups consecutive groups, exactly as n_groups dv_epoch_group_run calls
  * (homes: n_groups * n_homes batches, group g's at g * n_homes; d_commits:
  * NULL or one device pointer, each may be NULL, per group; st: NULL or

@@ -994,3 +994,79 @@ def test_tpcc_runner_protocol_gloo_world2(cc):
     assert 0 < c_ref.sum() < len(c_ref)
     for rank, buf in res:
         assert (np.frombuffer(buf, np.uint8) == c_ref).all(), rank
+
+
+def _host_carry(ep, commit, max_txn):
+    """The aborted txns of batch `ep` (commit byte 0), in order, at most
+    max_txn (tests/test_carry.py's rule, restated for batches)."""
+    tb = ep.txn_begin.astype(np.int64)
+    ab = np.flatnonzero(commit[:ep.n_txn] == 0)[:max_txn]
+    idx = np.concatenate([np.arange(tb[t], tb[t + 1]) for t in ab]) if len(ab) else np.zeros(0, np.int64)
+    ntb = np.zeros(len(ab) + 1, np.uint32)
+    ntb[1:] = np.cumsum(tb[ab + 1] - tb[ab])
+    return dvcc.Epoch(ep.keys[idx].copy(), ep.types[idx].copy(), ntb)
+
+
+def _host_concat(a, b):
+    tb = np.concatenate([a.txn_begin, b.txn_begin[1:] + a.txn_begin[-1]]).astype(np.uint32)
+    return dvcc.Epoch(np.concatenate([a.keys, b.keys]), np.concatenate([a.types, b.types]), tb)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,world", [(dvcc.NO_WAIT, 2), (dvcc.WAIT_DIE, 2), (dvcc.OCC, 3)])
+def test_epoch_group_retries(cc, world):
+    """dv_epoch_group_carry: closed-loop epoch groups -- rank r's txns aborted
+    in epoch e of group g open its batch of epoch e of group g + 1, in order,
+    ahead of new txns (a penalty of one group), built on the device from the
+    group's commit bytes.  Every epoch of three groups equals the oracle over
+    the same sequenced epochs, and the carried batches equal the host rule."""
+    rows_pp, n_txn = 1 << 13, 1500
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=0.3)
+    engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    # group 0: all new txns
+    host = [[gen.gen(n_txn, dvcc.epoch_seed(r, 70 + e), r) for e in range(world)] for r in range(world)]
+    dev = [[dvcc.DeviceEpoch(b) for b in host[r]] for r in range(world)]
+    carried_total = 0
+    for g in range(3):
+        refs = []
+        for e in range(world):
+            q = dvcc.sequence([host[r][e] for r in range(world)])
+            c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin, q.keys,
+                                           q.types)
+            refs.append((c_ref, st_ref))
+        res = _run_group_epochs(engines, dev, n_txn)
+        for r, x in enumerate(res):
+            assert not isinstance(x, Exception), f"group {g} rank {r}: {x}"
+            c, st = x
+            for e in range(world):
+                assert (c[e * n_txn:e * n_txn + host[r][e].n_txn] ==
+                        refs[e][0][r * n_txn:r * n_txn + host[r][e].n_txn]).all(), f"group {g} epoch {e} rank {r}"
+            assert st.committed == sum(s.committed for _, s in refs)
+        for p, eng in enumerate(engines):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"group {g} partition {p} table"
+        # the next group's batches: this group's aborts first, then new txns
+        nhost, ndev = [], []
+        for r in range(world):
+            d_commit = torch.from_numpy(res[r][0]).cuda()
+            carried = engines[r].group_carry(dev[r], d_commit, n_txn)
+            hb, db = [], []
+            for e in range(world):
+                hc = _host_carry(host[r][e], res[r][0][e * n_txn:(e + 1) * n_txn], n_txn)
+                dc = carried[e]
+                assert (dc.n_txn, dc.n_acc) == (hc.n_txn, hc.n_acc), f"group {g} rank {r} epoch {e}"
+                assert np.array_equal(dc.keys.cpu().numpy().view(np.uint64), hc.keys)
+                assert np.array_equal(dc.types.cpu().numpy(), hc.types)
+                assert np.array_equal(dc.acc_txn.cpu().numpy().view(np.uint32), hc.acc_txn())
+                carried_total += hc.n_txn
+                new = gen.gen(n_txn - hc.n_txn, dvcc.epoch_seed(r, 80 + g * world + e), r)
+                hb.append(_host_concat(hc, new))
+                db.append(dvcc.DeviceEpoch.concat(dc, dvcc.DeviceEpoch(new)) if hc.n_txn else dvcc.DeviceEpoch(new))
+            nhost.append(hb)
+            ndev.append(db)
+        host, dev = nhost, ndev
+    assert carried_total > 0
+    for eng in engines:
+        eng.close()
