@@ -87,6 +87,9 @@ def parse():
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
     ap.add_argument("--tpcc-only", action="store_true", help="run and print only the TPC-C leg (profiling)")
     ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
+    ap.add_argument("--tpcc-part-wh", type=int, default=256,
+                    help="N>1 (or --part1): warehouses of the partitioned TPC-C leg, split over the ranks")
+    ap.add_argument("--no-tpcc-part", action="store_true", help="N>1: skip the partitioned TPC-C leg")
     ap.add_argument("--tpcc-txns", default="65536,10000",
                     help="txns per TPC-C epoch, comma-separated (the first is the leg's line; 10000 is the "
                          "reference's concurrency window, 8 nodes x 1250 in-flight txns)")
@@ -652,6 +655,51 @@ class PartitionedBench:
         return batch
 
 
+def tpcc_part_leg(a, world, rank, local_rank, first_step):
+    """Config E across the ranks (dv_tpcc_epoch_run_part over RCCL):
+    --tpcc-part-wh warehouses (256) split over the N ranks, each rank's client
+    batch 1/N of a global epoch of each --tpcc-txns size (65,536, and the
+    reference's 10,000-txn window), records sent to the partition owning their
+    warehouse, decided, executed there, o_ids all-reduced; WAIT_DIE and
+    CALVIN.  Max over ranks of the time of K epochs, like the headline."""
+    from dvcc import tpcc as T
+    pp = T.tpcc_params(a.tpcc_part_wh, part_cnt=world)
+    sizes = [int(x) for x in str(a.tpcc_txns).split(",") if x]
+    out = {"warehouses": a.tpcc_part_wh, "warehouses_per_gpu": a.tpcc_part_wh / world,
+           "protocol": "dv_tpcc_epoch_run_part (owner split, per-round verdict all-reduce, o_id all-reduce)"}
+    nxt = first_step
+    for cc_name in ("WAIT_DIE", "CALVIN"):
+        n_max = max(sizes) // world
+        eng = T.TpccEngine(cc_name, pp, n_max * world, device=local_rank, part_id=rank, seed=1)
+        eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        uid = [dvcc.comm_unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        with stdout_to_stderr():
+            eng.comm_init(uid[0], world, rank)
+        for total in sizes:
+            n_rank = total // world
+            batches = [T.gen(pp, n_rank, dvcc.epoch_seed(rank, 500 + e), home_part=rank) for e in range(2)]
+            dev = [(T.device_epoch(b), torch.from_numpy(b.owner).cuda()) for b in batches]
+            d_commit = torch.zeros(n_rank * world, dtype=torch.uint8, device="cuda")
+            d_oid = torch.zeros(n_rank * world, dtype=torch.int64, device="cuda")
+
+            def step(i, dev=dev, n_rank=n_rank, d_commit=d_commit, d_oid=d_oid):
+                (dep, d_args), own = dev[i % 2]
+                return eng.run_tpcc_epoch_part(dep, d_args, own, n_rank, d_commit, d_oid)
+            k = max(a.steps, 5) if total == sizes[0] else max(a.steps, 20)
+            sts, el = timed(step, nxt, a.warmup, k, world)
+            nxt += 100
+            committed = sum(st.committed for st in sts)
+            key = cc_name if total == sizes[0] else f"window_{total}_{cc_name}"
+            out[key] = {"txns_per_epoch": n_rank * world, "txns_per_rank": n_rank,
+                        "committed_per_s": committed / el, "decided_txns_per_s": k * n_rank * world / el,
+                        "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_rank * world),
+                        "epochs": k}
+        eng.close()
+    return out
+
+
 def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
     """N>1 extras beside the headline: strong scaling (one epoch per step),
     weak scaling (1,048,576 txns per GPU, list protocol) and the MPR sweep."""
@@ -695,6 +743,8 @@ def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
         nxt += 100
     if sweep:
         out["mpr_sweep"] = sweep
+    if not a.no_tpcc_part and not a.no_tpcc:
+        out["tpcc_partitioned"] = tpcc_part_leg(a, world, pb.rank, int(os.environ.get("LOCAL_RANK", 0)), nxt)
 
 
 def main():
