@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
+    ap.add_argument("--lsd-sort", action="store_true",
+                    help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
@@ -215,7 +217,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
                            "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
                "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
         for cc_name in cc_names:
-            eng = T.TpccEngine(cc_name, p, n_txn, seed=1)
+            eng = T.TpccEngine(cc_name, p, n_txn, seed=1, lsd_sort=a.lsd_sort)
             dev = [T.device_epoch(e) for e in eps]
             d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
             d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
@@ -429,7 +431,7 @@ def pmc_traffic(a, cc_name, world, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
-def epoch_bytes(st, rows, R):
+def epoch_bytes(st, rows, R, bucket=False):
     """SURVEY.md 8(d) algorithmic bytes of each kernel for ONE epoch with the
     stats `st` (mean over the profiled epochs), counted on what the launches of
     that kernel actually processed: {kernel: (bytes per epoch, what is counted)}.
@@ -441,7 +443,9 @@ def epoch_bytes(st, rows, R):
     ta, tb = st["prefix_txn"], st["surv_txn"]
     keys = (ka + kb) if (ka or kb) else n_acc           # (no prefix: the whole epoch is sorted)
     stage_txn = (ta + tb) if (ka or kb) else n_txn
-    passes = max(1, st["sort_passes"])
+    # bucket sorts (k_bucket_sort, small sorts): one histogram / scan /
+    # scatter pass, then the bucket launch; else sort_passes LSD passes
+    passes = 1 if bucket else max(1, st["sort_passes"])
     tiles = sum((k + 4095) // 4096 for k in ((ka, kb) if (ka or kb) else (n_acc,)))
     later = max(0, n_acc - ka)
     per_txn = n_acc / max(1, n_txn)
@@ -456,6 +460,8 @@ def epoch_bytes(st, rows, R):
         "k_radix_hist": (8 * passes * keys, "8 B per key read, per pass"),
         "k_radix_scan": (8 * 256 * passes * tiles, "per pass: 256 digit counts per 4096-key tile, read + written"),
         "k_radix_scatter": (16 * passes * keys, "per pass: 8 B per key read + 8 B written"),
+        "k_bucket_sort": (16 * keys, "8 B per key read + 8 B written (the bucket's sort by the rest of the row "
+                                     "hash, in LDS)"),
         "k_round_pass": (SCAN_BYTES * st["pass_live"], f"{SCAN_BYTES} B per live access read (scan 8 + verdict 1)"),
         "k_round_settle": (17 * stage_txn, "per txn of the stage: length 1, status 1 + 1, verdict bytes 10, "
                                            "fact word 4"),
@@ -466,9 +472,11 @@ def epoch_bytes(st, rows, R):
         "k_prefix_mark": (9 * ta + 4 * ka * 0, "per prefix txn: status 1 + access range 8 (lower bound: the "
                                               "committed txns' rows are not counted)"),
         "k_kill": (4 * later + later // 8, "per access after the prefix: row word 4 read + kill bit written"),
-        "k_kill_compact": (9 * max(0, n_txn - ta) + later // 8 + 12 * kb + 6 * tb,
-                           "per later txn: access range 8 + status 1; kill bits; per survivor access: row word 4 "
-                           "read + sort key 8 written; per survivor: map 4 + length 1 + status 1"),
+        "k_kill_count": (13 * max(0, n_txn - ta) + later // 4,
+                         "per later txn: access range 8 + status 1 + info word 4 written; kill and skip bits read"),
+        "k_kill_emit": (8 * max(0, n_txn - ta) + 12 * kb + 6 * tb,
+                        "per later txn: first access 4 + info word 4; per survivor access kept: row word 4 read + "
+                        "sort key 8 written; per survivor: map 4 + length 1 + status 1"),
         "k_sub_scatter_back": (6 * tb, "per survivor: map 4 + status 1 read, status 1 written"),
         "k_exec_txn": (10 * n_txn + int(12 * st["committed"] * per_txn),
                        "per txn: status 1 + access range 8 + commit byte 1; per committed access: row word 4 + "
@@ -489,7 +497,7 @@ def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1):
              "committed", "sort_passes")}
     mean["n_txn"] /= txn_div  # (epoch groups: the stats count the group's txns, n_acc the decided epoch's)
     mean["committed"] /= txn_div
-    eb = epoch_bytes(mean, rows, R)
+    eb = epoch_bytes(mean, rows, R, bucket="k_bucket_sort" in ktimes)
     total_ms = sum(ms for _, ms in ktimes.values())
     rows_out = []
     for name, (launches, ms) in sorted(ktimes.items(), key=lambda kv: -kv[1][1]):
@@ -606,7 +614,7 @@ class PartitionedBench:
         # rank (dv_comm_set_mode 0 picks it when the epoch fits)
         cap = max(int(max_txn_rank * R * 1.4), CONFIGS[a.config][1] * R) + 65536
         self.eng = dvcc.CCEngine(cc_name, max_txn_rank * world, cap, device=local_rank, part_cnt=world,
-                                 part_id=rank, timing=TIMING[a.timing])
+                                 part_id=rank, timing=TIMING[a.timing], lsd_sort=a.lsd_sort)
         self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
         uid = [dvcc.comm_unique_id() if rank == 0 else None]
@@ -782,7 +790,8 @@ def main():
                                       mpr=mpr)
         epochs = gen_epochs(gen, n_txn_total, 0, n_epochs)
         t_gen = time.perf_counter() - t_gen
-        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing])
+        eng = dvcc.CCEngine(cc_name, n_txn_total, n_txn_total * R, device=local_rank, timing=TIMING[a.timing],
+                            lsd_sort=a.lsd_sort)
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)
@@ -854,6 +863,8 @@ def main():
     out.update(stage_summary(stats, sstats, table, el, R))
     out["kernels"] = table
     out["kernel_us_per_epoch"] = kus
+    out["stage_sizes_mean"] = {k: float(np.mean([getattr(st, k) for st in pstats]))
+                               for k in ("n_txn", "n_acc", "prefix_txn", "prefix_acc", "surv_txn", "surv_acc")}
     if not part:
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}

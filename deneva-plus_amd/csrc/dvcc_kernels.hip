@@ -377,9 +377,24 @@ __device__ __forceinline__ uint64_t sort_n(uint64_t n, const uint32_t *n_dev) {
     return n_dev && (uint64_t)*n_dev < n ? (uint64_t)*n_dev : n;
 }
 
+// the radix digit of a sort key: bits [shift, shift + W) -- or, for the one
+// pass of a bucket sort (hmul != 0), the top W bits of the row's hash
+// h = row * hmul mod 2^hbits (a bijection on hbits-bit rows: rows sharing a
+// bucket differ in h's low hbits - W bits, which k_bucket_sort sorts by).
+// Low row bits would bucket TPC-C's NURand ids -- whose low bits lean to
+// ones -- a tenth of them into one bucket.
+__device__ __forceinline__ uint32_t row_hash(uint64_t key, uint32_t hmul, int hbits) {
+    return ((uint32_t)(key >> 32) * hmul) & ((1u << hbits) - 1u);
+}
+template <int W>
+__device__ __forceinline__ uint32_t key_digit(uint64_t key, int shift, uint32_t hmul, int hbits) {
+    return hmul ? row_hash(key, hmul, hbits) >> (hbits - W) : (uint32_t)(key >> shift) & ((1u << W) - 1u);
+}
+
 __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restrict__ in, uint64_t n,
                                                        int shift, uint32_t *__restrict__ counts,
-                                                       uint32_t nblocks, const uint32_t *__restrict__ n_dev) {
+                                                       uint32_t nblocks, const uint32_t *__restrict__ n_dev,
+                                                       uint32_t hmul, int hbits) {
     __shared__ uint32_t wc[4][kRadix];
     n = sort_n(n, n_dev);
     if ((uint64_t)blockIdx.x * kTile >= n) return;
@@ -401,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist(const uint64_t *__restric
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+        const uint32_t d = key_digit<kRadixBits>(k[j], shift, hmul, hbits);
         const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
         const uint64_t vmask = __ballot(valid);
         if (__ballot(valid && d == d0) == vmask) {
@@ -444,7 +459,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ co
 
 __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     const uint64_t *__restrict__ in, uint64_t *__restrict__ out, uint64_t n, int shift, const uint32_t *__restrict__ counts,
-    const uint32_t *__restrict__ digit_tot, uint32_t nblocks, const uint32_t *__restrict__ n_dev) {
+    const uint32_t *__restrict__ digit_tot, uint32_t nblocks, const uint32_t *__restrict__ n_dev,
+    uint32_t hmul, int hbits) {
     __shared__ __attribute__((aligned(16))) uint64_t skeys[kTile];
     n = sort_n(n, n_dev);
     if ((uint64_t)blockIdx.x * kTile >= n) return;
@@ -477,7 +493,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+        const uint32_t d = key_digit<kRadixBits>(k[j], shift, hmul, hbits);
         const uint64_t vmask = __ballot(valid);
         const uint64_t peers = match_digit(d, vmask);
         const uint32_t before = wc[wave][d];
@@ -501,7 +517,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         if (idx < n) {
-            const uint32_t d = (uint32_t)(k[j] >> shift) & (kRadix - 1);
+            const uint32_t d = key_digit<kRadixBits>(k[j], shift, hmul, hbits);
             const uint32_t pos = dstart[d] + wc[wave][d] + r[j];
             skeys[pos] = k[j];
         }
@@ -510,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
     const uint32_t tile_n = (uint32_t)((n - tile0) < (uint64_t)kTile ? (n - tile0) : kTile);
     for (uint32_t p = tid; p < tile_n; p += kBlock) {
         const uint64_t key = skeys[p];
-        const uint32_t d = (uint32_t)(key >> shift) & (kRadix - 1);
+        const uint32_t d = key_digit<kRadixBits>(key, shift, hmul, hbits);
         const uint64_t dst = gbase[d] + p;
         out[dst] = key;
     }
@@ -525,7 +541,8 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter(
 template <int W>
 __global__ __launch_bounds__(kBlock) void k_radix_hist_w(const uint64_t *__restrict__ in, uint64_t n, int shift,
                                                          uint32_t *__restrict__ counts, uint32_t nblocks,
-                                                         const uint32_t *__restrict__ n_dev) {
+                                                         const uint32_t *__restrict__ n_dev, uint32_t hmul,
+                                                         int hbits) {
     constexpr uint32_t R = 1u << W;
     __shared__ uint32_t wc[4][R];
     n = sort_n(n, n_dev);
@@ -544,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_hist_w(const uint64_t *__restr
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+        const uint32_t d = key_digit<W>(k[j], shift, hmul, hbits);
         const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
         const uint64_t vmask = __ballot(valid);
         if (__ballot(valid && d == d0) == vmask) {
@@ -562,7 +579,8 @@ template <int W>
 __global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                             uint64_t n, int shift, const uint32_t *__restrict__ counts,
                                                             const uint32_t *__restrict__ digit_tot, uint32_t nblocks,
-                                                            const uint32_t *__restrict__ n_dev) {
+                                                            const uint32_t *__restrict__ n_dev, uint32_t hmul,
+                                                            int hbits) {
     constexpr uint32_t R = 1u << W, PER = R / kBlock;  // digits per thread in the digit scans
     __shared__ __attribute__((aligned(16))) uint64_t skeys[kTile];
     __shared__ uint32_t wc[4][R];
@@ -604,7 +622,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__re
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         const bool valid = idx < n;
-        const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+        const uint32_t d = key_digit<W>(k[j], shift, hmul, hbits);
         uint64_t peers = __ballot(valid);
 #pragma unroll
         for (int b = 0; b < W; b++) {
@@ -644,7 +662,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__re
     for (int j = 0; j < kIPT; j++) {
         const uint64_t idx = base + j * 64 + lane;
         if (idx < n) {
-            const uint32_t d = (uint32_t)(k[j] >> shift) & (R - 1);
+            const uint32_t d = key_digit<W>(k[j], shift, hmul, hbits);
             skeys[dstart[d] + wc[wave][d] + r[j]] = k[j];
         }
     }
@@ -652,25 +670,265 @@ __global__ __launch_bounds__(kBlock) void k_radix_scatter_w(const uint64_t *__re
     const uint32_t tile_n = (uint32_t)((n - tile0) < (uint64_t)kTile ? (n - tile0) : kTile);
     for (uint32_t p = tid; p < tile_n; p += kBlock) {
         const uint64_t key = skeys[p];
-        const uint32_t d = (uint32_t)(key >> shift) & (R - 1);
+        const uint32_t d = key_digit<W>(key, shift, hmul, hbits);
         out[(uint64_t)gbase[d] + p] = key;
     }
 }
 
 template <int W>
 void wide_pass(hipStream_t s, const uint64_t *in, uint64_t *out, uint64_t n, int shift, uint32_t *counts,
-               uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1) {
-    DV_LAUNCH((k_radix_hist_w<W>), nb, kBlock, 0, s, in, n, shift, counts, nb, n_dev);
+               uint32_t *digit_tot, uint32_t nb, const uint32_t *n_dev, hipEvent_t e0, hipEvent_t e1,
+               uint32_t hmul = 0, int hbits = 0) {
+    DV_LAUNCH((k_radix_hist_w<W>), nb, kBlock, 0, s, in, n, shift, counts, nb, n_dev, hmul, hbits);
     DV_LAUNCH(k_radix_scan, 1u << W, kBlock, 0, s, counts, nb, digit_tot, n_dev);
     DV_LAUNCH_EV((k_radix_scatter_w<W>), nb, kBlock, 0, s, e0, e1, in, out, n, shift,
-                          (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
+                          (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev, hmul, hbits);
+}
+
+// ---- bucket sort (small sorts, dvcc_internal.h bucket_sort_applies) --------
+// After one stable pass on the top digit of the row's hash (key_digit) every
+// bucket holds its keys in sequence order; a workgroup per bucket then sorts
+// them stably by the hash's remaining bits, which tell its rows apart.  The keys stay where they are: the workgroup
+// sorts 32-bit tags (remaining row bits << 14 | the key's index in the
+// bucket) in LDS with 8-bit digits, wave-ballot ranks as in k_radix_scatter,
+// and finally gathers the keys (L2-resident: the bucket was just read) into
+// place.  A bucket larger than its LDS (a hot row read by many survivors)
+// is sorted the same way from global memory, in 16K-key chunks, with the
+// bucket's region of the input buffer as the ping-pong scratch.
+constexpr int kBucketThreads = 1024;
+constexpr int kBucketWaves = kBucketThreads / 64;
+constexpr int kBucketIdxBits = 32 - kBucketHiMax;
+constexpr uint32_t kBucketCap = 1u << kBucketIdxBits;       // keys a workgroup sorts in LDS
+constexpr int kBucketSteps = (int)kBucketCap / kBucketThreads;  // 64-key steps per wave, at most
+// two tag arrays + per-wave digit counts: one workgroup per CU on gfx950
+static_assert((2 * kBucketCap + (kBucketWaves + 2) * kRadix + kBucketWaves) * sizeof(uint32_t) <= 160u * 1024u,
+              "k_bucket_sort's LDS exceeds gfx950's 160 KiB per workgroup");
+
+// stable rank of this lane's digit among the wave's keys so far (wcw: the
+// wave's running digit counts, updated)
+__device__ __forceinline__ uint32_t bucket_rank(uint32_t d, bool valid, uint32_t *wcw, uint32_t lane) {
+    const uint64_t peers = match_digit(d, __ballot(valid));
+    const uint32_t before = wcw[d];
+    if (valid && lane == (uint32_t)__builtin_ctzll(peers)) wcw[d] = before + (uint32_t)__popcll(peers);
+    return before + mask_rank(peers);
+}
+
+// wc[w][d] (keys of digit d in wave w's part of the chunk) -> the position of
+// that part's first key: run[d] (the digit's next free slot; advanced by the
+// digit's chunk total) or, with run == nullptr, the chunk's own digit-major
+// offsets.  Called by every thread.
+__device__ __forceinline__ void bucket_bases(uint32_t (*wc)[kRadix], uint32_t *tot, uint32_t *run) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    uint32_t sum = 0;
+    if (tid < (uint32_t)kRadix) {
+#pragma unroll
+        for (int w = 0; w < kBucketWaves; w++) {
+            const uint32_t c = wc[w][tid];
+            wc[w][tid] = sum;
+            sum += c;
+        }
+        if (!run) tot[tid] = sum;
+    }
+    __syncthreads();
+    if (!run && tid < 64) {  // exclusive scan of the 256 digit totals, 4 per lane
+        uint32_t v[4], s4 = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            v[q] = tot[4 * lane + q];
+            s4 += v[q];
+        }
+        uint32_t pre = wave_incl_sum(s4, lane) - s4;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            tot[4 * lane + q] = pre;
+            pre += v[q];
+        }
+    }
+    if (!run) __syncthreads();
+    if (tid < (uint32_t)kRadix) {
+        const uint32_t b = run ? run[tid] : tot[tid];
+        if (run) run[tid] = b + sum;
+#pragma unroll
+        for (int w = 0; w < kBucketWaves; w++) wc[w][tid] += b;
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint64_t *__restrict__ in, uint64_t *__restrict__ out,
+                                                                const uint32_t *__restrict__ digit_tot,
+                                                                uint32_t hmul, int hbits, int hi_bits) {
+    __shared__ uint32_t tg[2][kBucketCap];
+    __shared__ uint32_t wc[kBucketWaves][kRadix];
+    __shared__ uint32_t tot[kRadix], run[kRadix];
+    __shared__ uint32_t s_part[kBucketWaves];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x;
+    {  // the bucket's offset: the sizes of the buckets before it (gridDim.x <= kBucketThreads)
+        uint32_t v = tid < b ? digit_tot[tid] : 0u;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0) s_part[wave] = v;
+    }
+    __syncthreads();
+    uint32_t base = 0;
+#pragma unroll
+    for (int w = 0; w < kBucketWaves; w++) base += s_part[w];
+    const uint32_t m = digit_tot[b];
+    if (m <= 1) {  // nothing to order (one key: copied into place)
+        if (m == 1 && tid == 0) out[base] = in[base];
+        return;
+    }
+    const int passes = (hi_bits + kRadixBits - 1) / kRadixBits;
+    const uint32_t hmask = (1u << hi_bits) - 1u;
+    if (m <= kBucketCap) {
+        {  // every key's load in flight at once (a loop would wait on each)
+            uint64_t kv[kBucketSteps];
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                const uint32_t i = s * kBucketThreads + tid;
+                kv[s] = i < m ? in[base + i] : 0ull;
+            }
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                const uint32_t i = s * kBucketThreads + tid;
+                if (i < m) tg[0][i] = ((row_hash(kv[s], hmul, hbits) & hmask) << kBucketIdxBits) | i;
+            }
+        }
+        __syncthreads();
+        const uint32_t steps = (m + kBucketThreads - 1) / kBucketThreads;
+        int cur = 0;
+        for (int p = 0; p < passes; p++) {
+            const int sh = kBucketIdxBits + kRadixBits * p;
+            for (uint32_t d = lane; d < (uint32_t)kRadix; d += 64) wc[wave][d] = 0;
+            uint32_t t[kBucketSteps], r[kBucketSteps];
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                if ((uint32_t)s < steps) {
+                    const uint32_t e = (wave * steps + s) * 64 + lane;
+                    const bool valid = e < m;
+                    t[s] = valid ? tg[cur][e] : 0u;
+                    r[s] = bucket_rank((t[s] >> sh) & (kRadix - 1), valid, wc[wave], lane);
+                }
+            }
+            __syncthreads();
+            bucket_bases(wc, tot, nullptr);
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                if ((uint32_t)s < steps) {
+                    const uint32_t e = (wave * steps + s) * 64 + lane;
+                    if (e < m) tg[cur ^ 1][wc[wave][(t[s] >> sh) & (kRadix - 1)] + r[s]] = t[s];
+                }
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+        uint64_t kv[kBucketSteps];
+#pragma unroll
+        for (int s = 0; s < kBucketSteps; s++) {
+            const uint32_t i = s * kBucketThreads + tid;
+            kv[s] = i < m ? in[base + (tg[cur][i] & (kBucketCap - 1))] : 0ull;
+        }
+#pragma unroll
+        for (int s = 0; s < kBucketSteps; s++) {
+            const uint32_t i = s * kBucketThreads + tid;
+            if (i < m) out[base + i] = kv[s];
+        }
+        return;
+    }
+    // a bucket larger than the LDS: the same passes over global memory, the
+    // bucket's region of `in` as scratch
+    uint64_t *A = in + base, *B = out + base;
+    for (int p = 0; p < passes; p++) {
+        const uint64_t *src = (p & 1) ? B : A;
+        uint64_t *dst = (p & 1) ? A : B;
+        const int sh = kRadixBits * p;
+        if (tid < (uint32_t)kRadix) tot[tid] = 0;
+        __syncthreads();
+        for (uint32_t i0 = 0; i0 < m; i0 += kBucketThreads) {
+            const uint32_t i = i0 + tid;
+            const bool valid = i < m;
+            const uint32_t d = valid ? ((row_hash(src[i], hmul, hbits) & hmask) >> sh) & (kRadix - 1) : 0u;
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            const uint64_t vm = __ballot(valid);
+            if (__ballot(valid && d == d0) == vm) {  // a hot row: one add for the wave
+                if (lane == 0 && vm) atomicAdd(&tot[d0], (uint32_t)__popcll(vm));
+            } else if (valid) {
+                atomicAdd(&tot[d], 1u);
+            }
+        }
+        __syncthreads();
+        if (tid < 64) {
+            uint32_t v[4], s4 = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                v[q] = tot[4 * lane + q];
+                s4 += v[q];
+            }
+            uint32_t pre = wave_incl_sum(s4, lane) - s4;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                run[4 * lane + q] = pre;
+                pre += v[q];
+            }
+        }
+        __syncthreads();
+        for (uint32_t c0 = 0; c0 < m; c0 += kBucketCap) {
+            const uint32_t mc = m - c0 < kBucketCap ? m - c0 : kBucketCap;
+            const uint32_t steps = (mc + kBucketThreads - 1) / kBucketThreads;
+            for (uint32_t d = lane; d < (uint32_t)kRadix; d += 64) wc[wave][d] = 0;
+            uint64_t k[kBucketSteps];
+            uint32_t r[kBucketSteps];
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                if ((uint32_t)s < steps) {
+                    const uint32_t e = (wave * steps + s) * 64 + lane;
+                    const bool valid = e < mc;
+                    k[s] = valid ? src[c0 + e] : 0ull;
+                    r[s] = bucket_rank(((row_hash(k[s], hmul, hbits) & hmask) >> sh) & (kRadix - 1), valid,
+                                       wc[wave], lane);
+                }
+            }
+            __syncthreads();
+            bucket_bases(wc, tot, run);
+#pragma unroll
+            for (int s = 0; s < kBucketSteps; s++) {
+                if ((uint32_t)s < steps) {
+                    const uint32_t e = (wave * steps + s) * 64 + lane;
+                    if (e < mc) dst[wc[wave][((row_hash(k[s], hmul, hbits) & hmask) >> sh) & (kRadix - 1)] + r[s]] = k[s];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (!(passes & 1)) {  // the result is in the scratch region
+        for (uint32_t i = tid; i < m; i += kBucketThreads) B[i] = A[i];
+    }
 }
 
 int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits, uint32_t *counts,
-                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev) {
+                    uint32_t *digit_tot, hipEvent_t *scatter_ev, bool hist0_done, const uint32_t *n_dev,
+                    bool lsd_only) {
     if (n == 0) return 0;
     const uint32_t nb = nblocks_for(n);
     int cur = 0, pass = 0;
+    if (!lsd_only && bucket_sort_applies(n, key_bits, hist0_done, n_dev != nullptr)) {
+        const int lo = kBucketLoBits(key_bits);
+        const uint32_t hmul = kRowHashMul;
+        hipEvent_t e0 = scatter_ev ? scatter_ev[0] : nullptr, e1 = scatter_ev ? scatter_ev[1] : nullptr;
+        if (lo == 9)
+            wide_pass<9>(s, pairs[0], pairs[1], n, 32, counts, digit_tot, nb, n_dev, e0, e1, hmul, key_bits);
+        else if (lo == 10)
+            wide_pass<10>(s, pairs[0], pairs[1], n, 32, counts, digit_tot, nb, n_dev, e0, e1, hmul, key_bits);
+        else {
+            DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[0], n, 32, counts, nb, n_dev, hmul, key_bits);
+            DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev);
+            DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, e0, e1, (const uint64_t *)pairs[0], pairs[1], n, 32,
+                         (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev, hmul, key_bits);
+        }
+        DV_LAUNCH_EV(k_bucket_sort, 1u << lo, kBucketThreads, 0, s, scatter_ev ? scatter_ev[2] : nullptr,
+                     scatter_ev ? scatter_ev[3] : nullptr, pairs[1], pairs[0], (const uint32_t *)digit_tot,
+                     hmul, key_bits, key_bits - lo);
+        return 0;
+    }
     const int wbits = radix_digit_bits(key_bits, hist0_done);
     if (wbits > kRadixBits) {
         for (int bit = 0; bit < key_bits; bit += wbits, pass++) {
@@ -685,12 +943,13 @@ int radix_sort_rows(hipStream_t s, uint64_t *pairs[2], uint64_t n, int key_bits,
     }
     for (int bit = 0; bit < key_bits; bit += kRadixBits, pass++) {
         const int shift = 32 + bit;
-        if (pass > 0 || !hist0_done) DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev);
+        if (pass > 0 || !hist0_done)
+            DV_LAUNCH(k_radix_hist, nb, kBlock, 0, s, pairs[cur], n, shift, counts, nb, n_dev, 0u, 0);
         DV_LAUNCH(k_radix_scan, kRadix, kBlock, 0, s, counts, nb, digit_tot, n_dev);
         // timing: events recorded by the dispatch itself (no extra packets)
         DV_LAUNCH_EV(k_radix_scatter, nb, kBlock, 0, s, scatter_ev ? scatter_ev[2 * pass] : nullptr,
                      scatter_ev ? scatter_ev[2 * pass + 1] : nullptr, (const uint64_t *)pairs[cur], pairs[cur ^ 1], n,
-                     shift, (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev);
+                     shift, (const uint32_t *)counts, (const uint32_t *)digit_tot, nb, n_dev, 0u, 0);
         cur ^= 1;
     }
     return cur;

@@ -24,6 +24,12 @@
 // conflict_lock would with the committed owners (row_lock.cpp:69, 86-90): a
 // write meets either bit, a read meets bit 1; OCC's central validation
 // (occ.cpp:185-199) kills any access to a row an earlier committed txn writes.
+// NO_WAIT / WAIT_DIE: every surviving access to a row in state 01 (read by a
+// committed prefix txn, written by none) reads it -- a write there is killed
+// -- so it conflicts with no other survivor and blocks none: the survivors'
+// sub-epoch leaves such accesses out (k_kill's skip bits), their txns wait
+// only for the rest.  At config D these are the hot rows' readers, about
+// half of the survivors' accesses.
 #include <algorithm>
 
 #include "dvcc_common.h"
@@ -150,7 +156,8 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
                                                  const uint32_t *__restrict__ n_dev,
                                                  const uint32_t *__restrict__ row_state, uint64_t state_words,
                                                  const uint32_t *__restrict__ bloom, int nowait,
-                                                 uint64_t *__restrict__ kill_bits, const Counters *__restrict__ ctr) {
+                                                 uint64_t *__restrict__ kill_bits, uint64_t *__restrict__ skip_bits,
+                                                 const Counters *__restrict__ ctr) {
     __shared__ uint32_t s_hot[kHotWords], s_bloom[kBloomWords];
     if (input_err(ctr) || ctr->halt) return;
     if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (rows past the real count were never probed)
@@ -171,7 +178,7 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
         }
 #pragma unroll
         for (int q = 0; q < kKillWords; q++) {
-            bool kill = false;
+            bool kill = false, skip = false;
             if (ar[q] != ~0u) {
                 const uint32_t row = ar[q] & ~AR_WR;
                 uint32_t st = 0;
@@ -182,9 +189,13 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
                     if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) st = row_bits(row_state, row);  // maybe marked
                 }
                 kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
+                skip = st == RS_RD && !(ar[q] & AR_WR);  // (nowait only: skip_bits is null for OCC)
             }
-            const uint64_t m = __ballot(kill);
-            if (lane == 0 && w + q < nw) kill_bits[w + q] = m;
+            const uint64_t m = __ballot(kill), sm = __ballot(skip);
+            if (lane == 0 && w + q < nw) {
+                kill_bits[w + q] = m;
+                if (skip_bits) skip_bits[w + q] = sm;
+            }
         }
     }
 }
@@ -204,12 +215,38 @@ __device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_b
     return k;
 }
 
+// set bits of `bits` in [a0, a1)
+__device__ __forceinline__ uint32_t range_count(const uint64_t *__restrict__ bits, uint32_t a0, uint32_t a1) {
+    if (a0 >= a1) return 0u;
+    const uint32_t wlo = a0 >> 6, whi = (a1 - 1) >> 6;
+    uint64_t lo = bits[wlo] & (~0ull << (a0 & 63));
+    const uint64_t hmask = ~0ull >> (63 - ((a1 - 1) & 63));
+    if (wlo == whi) return (uint32_t)__popcll(lo & hmask);
+    uint32_t c = (uint32_t)__popcll(lo) + (uint32_t)__popcll(bits[whi] & hmask);
+    for (uint32_t w = wlo + 1; w < whi; w++) c += (uint32_t)__popcll(bits[w]);
+    return c;
+}
+
+// the index of the r-th access from a0 on whose skip bit is clear (the
+// caller knows there is one)
+__device__ __forceinline__ uint32_t nth_kept(const uint64_t *__restrict__ skip, uint32_t a0, uint32_t r) {
+    uint32_t w = a0 >> 6;
+    uint64_t m = ~skip[w] & (~0ull << (a0 & 63));
+    for (uint32_t c = (uint32_t)__popcll(m); r >= c; c = (uint32_t)__popcll(m)) {
+        r -= c;
+        m = ~skip[++w];
+    }
+    for (; r; r--) m &= m - 1;
+    return (w << 6) + (uint32_t)__builtin_ctzll(m);
+}
+
 // Txns [K, n_txn) after k_kill: a txn with a kill bit in its access range
 // aborts (status byte), the others -- survivors -- are renumbered
-// 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses --
-// and their sort keys written densely in that order, pairs_b = row << 32 |
-// sub << 8 | pos << 1 | wr (same positions, so the verdict-byte slots keep
-// their layout).  Two launches over tiles of kKillTile txns:
+// 0..S-1 in sequence order -- map[sub] = txn, tlen_b[sub] = its accesses
+// without the skipped ones (skip_bits: NO_WAIT / WAIT_DIE, header) -- and
+// their sort keys written densely in that order, pairs_b = row << 32 |
+// sub << 8 | pos << 1 | wr, pos numbering the txn's accesses left in.  Two
+// launches over tiles of kKillTile txns:
 //   k_kill_count: the tile's txns checked block-strided (coalesced access
 //     ranges and status stores, every txn's kill words in flight together),
 //     one info word per txn (survivor: its length | 1 << 31) and the tile's
@@ -223,6 +260,7 @@ __device__ __forceinline__ bool range_killed(const uint64_t *__restrict__ kill_b
 __global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restrict__ tb_start,
                                                        const uint32_t *__restrict__ tb_end, uint32_t K,
                                                        uint32_t n_txn, const uint64_t *__restrict__ kill_bits,
+                                                       const uint64_t *__restrict__ skip_bits,
                                                        uint8_t *__restrict__ status, uint32_t *__restrict__ info,
                                                        uint32_t *__restrict__ tsum, const Counters *ctr) {
     __shared__ uint32_t lds4[4];
@@ -246,9 +284,10 @@ __global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restric
         // a committed prefix txn holds one of its rows
         const bool killed = range_killed(kill_bits, a0[j], a1[j]);
         if (killed) status[t] = ST_ABORT;
-        info[t - K] = killed ? 0u : (a1[j] - a0[j]) | 0x80000000u;
+        const uint32_t len = killed ? 0u : a1[j] - a0[j] - (skip_bits ? range_count(skip_bits, a0[j], a1[j]) : 0u);
+        info[t - K] = killed ? 0u : len | 0x80000000u;
         cnt += killed ? 0u : 1u;
-        acc += killed ? 0u : a1[j] - a0[j];
+        acc += len;
     }
     uint32_t tc = 0, ta = 0;
     (void)block_excl_scan256(cnt, lds4, &tc);
@@ -261,7 +300,8 @@ __global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restric
 
 __global__ __launch_bounds__(kBlock) void k_kill_emit(
     const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn,
-    const uint32_t *__restrict__ info, const uint32_t *__restrict__ tsum, uint32_t *__restrict__ map,
+    const uint64_t *__restrict__ skip_bits, const uint32_t *__restrict__ info, const uint32_t *__restrict__ tsum,
+    uint32_t *__restrict__ map,
     uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b, uint64_t *__restrict__ pairs_b, Counters *ctr) {
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
@@ -361,7 +401,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             }
             sv[u] = lo;
             qv[u] = g - l_pre[lo];
-            ar[u] = g < na ? acc_row[l_a0[lo] + qv[u]] : 0u;
+            ar[u] = g < na ? acc_row[skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u]] : 0u;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kCompactU; u++) {
@@ -415,18 +455,20 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          uint64_t n_acc, const uint32_t *n_acc_dev, uint32_t K, uint32_t n_txn,
                          const uint32_t *row_state, uint64_t rs_words,
                          int nowait,
-                         uint64_t *kill_bits, uint8_t *status, uint32_t *map, uint8_t *status_b, uint8_t *tlen_b,
-                         uint64_t *pairs_b, uint32_t *info, uint32_t *tsum, Counters *ctr) {
+                         uint64_t *kill_bits, uint64_t *skip_bits, uint8_t *status, uint32_t *map,
+                         uint8_t *status_b, uint8_t *tlen_b, uint64_t *pairs_b, uint32_t *info, uint32_t *tsum,
+                         Counters *ctr) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
     // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
     DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
                                                                      row_state + (rs_words - kBloomWords), nowait,
-                                                                     kill_bits, ctr);
-    DV_LAUNCH(k_kill_count, nt, kBlock, 0, s, tb_start, tb_end, K, n_txn, kill_bits, status, info, tsum, ctr);
-    DV_LAUNCH(k_kill_emit, nt, kBlock, 0, s, tb_start, acc_row, K, n_txn, info, tsum, map, status_b, tlen_b, pairs_b,
-              ctr);
+                                                                     kill_bits, skip_bits, ctr);
+    DV_LAUNCH(k_kill_count, nt, kBlock, 0, s, tb_start, tb_end, K, n_txn, (const uint64_t *)kill_bits,
+              (const uint64_t *)skip_bits, status, info, tsum, ctr);
+    DV_LAUNCH(k_kill_emit, nt, kBlock, 0, s, tb_start, acc_row, K, n_txn, (const uint64_t *)skip_bits, info, tsum, map,
+              status_b, tlen_b, pairs_b, ctr);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -391,8 +391,18 @@ uint32_t *next_ticket(dv_ctx *c) {
 // 19.5 us per three-launch pass, 127 us per epoch against 114; and with every
 // predecessor's count summed in one hop (no inclusive prefixes), 21.8 us per
 // pass: the hand-offs cost more than the two kernel boundaries they save.)
+// Small sorts: one LSD pass, then every bucket sorted inside one workgroup
+// (k_bucket_sort, dvcc_internal.h bucket_sort_applies; DV_FLAG_LSD_SORT: off).
+bool lsd_only(const dv_ctx *c) { return (c->cfg.flags & DV_FLAG_LSD_SORT) != 0; }
 int sort_rows(dv_ctx *c, uint64_t n, int key_bits, hipEvent_t *ev, bool hist0_done, const uint32_t *n_dev) {
-    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev);
+    return radix_sort_rows(c->stream, c->pairs, n, key_bits, c->counts, c->digit_tot, ev, hist0_done, n_dev,
+                           lsd_only(c));
+}
+// the sort's timed launches (dv_stats.sort_passes): the scatter of every
+// pass, or the one pass's scatter and the bucket launch
+uint32_t sort_launches(const dv_ctx *c, uint64_t n, int key_bits, bool hist0_done, bool n_on_dev) {
+    if (!lsd_only(c) && bucket_sort_applies(n, key_bits, hist0_done, n_on_dev)) return 2;
+    return (uint32_t)radix_passes(key_bits, hist0_done);
 }
 
 Tables make_tables(dv_ctx *c) {
@@ -1175,7 +1185,7 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     }
     rec(c, 1);
     const int key_bits = bits_for(row_space(c));
-    c->sort_passes = radix_passes(key_bits, fuse_hist);
+    c->sort_passes = sort_launches(c, ep->n_acc, key_bits, fuse_hist, ep->n_acc_dev != nullptr);
     c->sorted = sort_rows(c, ep->n_acc, key_bits, ktiming(c) ? c->sev : nullptr, fuse_hist, ep->n_acc_dev);
     if (calvin)  // NO_WAIT / WAIT_DIE / OCC: classified by round 0 itself
         launch_seg_prepare(c->stream, c->pairs[c->sorted], ep->n_acc, 1, c->tb_start, c->el, c->ctr);
@@ -1685,7 +1695,9 @@ int enqueue_survivors(dv_ctx *c) {
     launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr, c->prefix_words ? c->tword : nullptr);
     launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, c->pf_n_acc_dev, K, c->n_txn,
-                        c->row_state, rs_words, nowait, c->kill_bits, c->status, c->b_map, c->b_status, c->b_tlen,
+                        c->row_state, rs_words, nowait, c->kill_bits,
+                        nowait ? c->kill_bits + kill_words(c->cfg.max_acc) : nullptr, c->status, c->b_map, c->b_status,
+                        c->b_tlen,
                         c->pairs[0], c->kinfo, c->ktsum, c->ctr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
@@ -1755,13 +1767,14 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         r = dalloc(&c->b_status, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_tlen, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_map, T);
-        if (!r) r = dalloc(&c->kill_bits, kill_words(c->cfg.max_acc));
+        if (!r) r = dalloc(&c->kill_bits, 2 * kill_words(c->cfg.max_acc));  // kill bits, then skip bits
         if (!r) r = dalloc(&c->kinfo, T);
         if (!r) r = dalloc(&c->ktsum, 2ull * kill_tiles(T) + 2);
         if (r) return r;
     }
     const int key_bits = bits_for(row_space(c));
-    c->sort_passes = radix_passes(key_bits, false);
+    // (the prefix's sort: its count is on the device)
+    c->sort_passes = sort_launches(c, ep->n_acc, key_bits, false, true);
     c->prefix_mode = true;
     c->prefix_words = c->surv_words = false;
     rec(c, 0);

@@ -34,6 +34,7 @@ FLAG_EL64 = 4
 FLAG_NO_ASYNC = 8
 FLAG_KERNEL_TIMING = 16
 FLAG_KERNEL_PROFILE = 32
+FLAG_LSD_SORT = 64
 
 
 class DvccError(RuntimeError):

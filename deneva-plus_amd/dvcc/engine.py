@@ -164,12 +164,13 @@ class CCEngine:
     """One context = one GPU (one process per GPU)."""
 
     def __init__(self, cc_alg, max_txn, max_acc, device=0, part_cnt=1, part_id=0, timing=False,
-                 workload=L.YCSB, tail=True, el64=False, asynchronous=True):
+                 workload=L.YCSB, tail=True, el64=False, asynchronous=True, lsd_sort=False):
         """tail=False keeps every decision round in the multi-workgroup pass
         (no single-workgroup tail kernel); el64=True forces 64-bit round
         elements; asynchronous=False never finishes the rounds in the
-        asynchronous kernel.  Decisions are the same either way (testing
-        knobs)."""
+        asynchronous kernel; lsd_sort=True sorts with the plain LSD passes
+        (no bucket sort of small sorts).  Decisions are the same either way
+        (testing knobs)."""
         if isinstance(cc_alg, str):
             cc_alg = L.CC_NAMES[cc_alg.upper()]
         self.cc_alg = cc_alg
@@ -179,7 +180,8 @@ class CCEngine:
         # launches' own dispatch timestamps (no marker packets between kernels)
         tflag = L.FLAG_KERNEL_TIMING if timing == "kernel" else (L.FLAG_TIMING if timing else 0)
         flags = (tflag | (0 if tail else L.FLAG_NO_TAIL)
-                 | (L.FLAG_EL64 if el64 else 0) | (0 if asynchronous else L.FLAG_NO_ASYNC))
+                 | (L.FLAG_EL64 if el64 else 0) | (0 if asynchronous else L.FLAG_NO_ASYNC)
+                 | (L.FLAG_LSD_SORT if lsd_sort else 0))
         cfg = L.Config(device, cc_alg, workload, part_cnt, part_id, max_txn, max_acc, flags, 0)
         self._ctx = ctypes.c_void_p()
         L.check(L.lib().dv_open(ctypes.byref(self._ctx), ctypes.byref(cfg)), "dv_open")

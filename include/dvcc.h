@@ -110,6 +110,9 @@ extern "C" {
 #define DV_FLAG_NO_TAIL 2u /* never finish the decision rounds in the single-
                               workgroup tail kernel (testing) */
 #define DV_FLAG_EL64 4u    /* always use 64-bit round elements (testing)     */
+#define DV_FLAG_LSD_SORT 64u /* sort every epoch's row queues with the plain
+                              LSD radix passes, never the one-pass-plus-
+                              bucket form of small sorts (testing, A/B)      */
 #define DV_FLAG_NO_ASYNC 8u /* never finish the decision rounds in the
                                asynchronous multi-workgroup kernel (that
                                kernel wants every workgroup of its launch

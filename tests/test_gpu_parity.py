@@ -45,14 +45,14 @@ def _gpu_epoch(eng, e, path):
 
 
 def _check(cc, rows, epochs, path="device", max_txn=None, max_acc=None, tail=True, el64=False,
-           asynchronous=True, prefix=0, async_iters=0):
+           asynchronous=True, prefix=0, async_iters=0, lsd_sort=False):
     """prefix: dv_set_prefix (0 automatic -- epochs from 131,072 txns --, None
     off, else the prefix size for every longer epoch)."""
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     eng = CCEngine(cc, max_txn or max(1, max(e.n_txn for e in epochs)),
                    max_acc or max(1, max(e.n_acc for e in epochs)), tail=tail, el64=el64,
-                   asynchronous=asynchronous)
+                   asynchronous=asynchronous, lsd_sort=lsd_sort)
     eng.set_prefix(prefix)
     if async_iters:
         eng.set_async_limits(async_iters, 0)
@@ -633,6 +633,44 @@ def test_sorts_past_2_20_rows(cc):
     _check(cc, rows, eps, prefix=None)
     if cc != dvcc.CALVIN:
         _check(cc, rows, eps[:2], prefix=3000)
+
+
+def _hot_read_epoch(rows, n_txn, seed, hot=0, R=4):
+    """every txn reads row `hot` first, then R - 1 random rows (half written):
+    one sort bucket holds every txn's hot access -- more than a workgroup's
+    LDS takes (k_bucket_sort's global-memory passes)"""
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, rows, size=(n_txn, R)).astype(np.uint64)
+    keys[:, 0] = hot
+    types = (rng.random((n_txn, R)) < 0.5).astype(np.uint8)
+    types[:, 0] = 0
+    tb = (np.arange(n_txn + 1) * R).astype(np.uint32)
+    return Epoch(keys.reshape(-1), types.reshape(-1), tb)
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("rows", [1 << 16, 1 << 20, 1 << 24])
+def test_bucket_sort_oversized_bucket(cc, rows):
+    """row bits above the bucket digit: 8 (one pass), 12 and 16 (two passes,
+    the result copied out of the scratch region); a 40,000-key bucket and the
+    rest in LDS; whole epochs and, for the 2PL / OCC algorithms, prefix and
+    survivors stages (counts on the device)"""
+    e = _hot_read_epoch(rows, 40_000, 7)
+    _check(cc, rows, [e], prefix=None)
+    if cc != dvcc.CALVIN:
+        _check(cc, rows, [e], prefix=5000)
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_lsd_sort_knob(cc):
+    """DV_FLAG_LSD_SORT: the plain LSD passes on the sizes that take the
+    bucket sort by default, same decisions"""
+    rows = 1 << 22
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    eps = [g.gen(30_000, 141), _hot_read_epoch(rows, 20_000, 8)]
+    _check(cc, rows, eps, prefix=None, lsd_sort=True)
+    if cc != dvcc.CALVIN:
+        _check(cc, rows, eps, prefix=3000, lsd_sort=True)
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
