@@ -222,11 +222,15 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
             d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
             d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
             k = max(a.steps, 5) if si == 0 else max(a.steps, 20)
-            for i in range(a.warmup):
-                eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid)
+
+            def batch(m):  # the pipelined entry point (epoch k+1 queued before k is read back)
+                return eng.run_tpcc_epochs_device([dev[i % 2][0] for i in range(m)],
+                                                  [dev[i % 2][1] for i in range(m)], d_commit, d_oid)
+            if a.warmup:
+                batch(a.warmup)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            sts = [eng.run_tpcc_epoch_device(*dev[i % 2], d_commit, d_oid) for i in range(k)]
+            sts = batch(k)
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             committed = sum(s.committed for s in sts)

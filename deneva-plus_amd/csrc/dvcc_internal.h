@@ -571,8 +571,9 @@ void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t 
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag);
 // bits[w] bit j = (ktag[32 w + j] == htag), rows [0, n)
 void launch_home_bits(hipStream_t s, const uint8_t *ktag, uint64_t n, uint32_t htag, uint32_t *bits);
+// (f0[row * cstride]: TPC-C contexts keep their three state columns row-major)
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
-                        uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr);
+                        uint64_t n, const uint64_t *f0, uint32_t cstride, uint64_t *out, Counters *ctr);
 // 4-byte row records (row | write << 31) + CSR txn_begin -> the epoch's arrays (table 0)
 void launch_split_rows(hipStream_t s, const uint32_t *rw, uint64_t n, const uint32_t *tb, uint32_t n_txn,
                        uint64_t *keys, uint8_t *types, uint32_t *acc_txn, uint8_t *tables);

@@ -1471,18 +1471,20 @@ void launch_home_bits(hipStream_t s, const uint8_t *ktag, uint64_t n, uint32_t h
 }
 
 __global__ void k_gather_rows(Tables tabs, uint32_t table, const uint64_t *keys, uint64_t n,
-                              const uint64_t *f0, uint64_t *out, Counters *ctr) {
+                              const uint64_t *f0, uint32_t cstride, uint64_t *out, Counters *ctr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint64_t row = 0;
-        out[i] = probe_row(tabs.t[table < kMaxTables ? table : 0], table < tabs.n, keys[i], row, ctr) ? f0[row] : 0ull;
+        out[i] = probe_row(tabs.t[table < kMaxTables ? table : 0], table < tabs.n, keys[i], row, ctr)
+                     ? f0[row * cstride]
+                     : 0ull;
     }
 }
 
 void launch_gather_rows(hipStream_t s, const Tables &tabs, uint32_t table, const uint64_t *keys,
-                        uint64_t n, const uint64_t *f0, uint64_t *out, Counters *ctr) {
+                        uint64_t n, const uint64_t *f0, uint32_t cstride, uint64_t *out, Counters *ctr) {
     if (!n) return;
-    DV_LAUNCH(k_gather_rows, 1024, kBlock, 0, s, tabs, table, keys, n, f0, out, ctr);
+    DV_LAUNCH(k_gather_rows, 1024, kBlock, 0, s, tabs, table, keys, n, f0, cstride, out, ctr);
 }
 
 // host records -> the epoch's arrays; with txn_begin (CSR), every record's

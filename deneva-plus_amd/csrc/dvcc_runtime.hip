@@ -70,7 +70,10 @@ struct dv_ctx {
     uint64_t *f0 = nullptr;    // hot column, global row id
     uint64_t *pkey = nullptr;  // primary key per row (row_t::get_primary_key)
     uint8_t *ktag = nullptr;   // key tag per row (key_tag, dvcc_internal.h)
-    uint64_t *col1 = nullptr, *col2 = nullptr;  // DV_TPCC: state columns 1 and 2
+    // DV_TPCC: the three 8-byte state columns of a row side by side (24 B,
+    // row-major: k_tpcc_apply touches all three of a row), f0 = column 0;
+    // YCSB: f0 alone (cstride 1)
+    uint32_t cstride = 1;
 
     // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
     // execution scratch, and the operation words / o_id output of this epoch
@@ -571,7 +574,7 @@ void dv_close(dv_ctx *c) {
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
-                    c->col1, c->col2, c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
+                    c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
                     c->row_state, c->b_status, c->b_tlen, c->b_map, c->kinfo, c->ktsum, c->kill_bits, c->gc_tb, c->gc_tot,
                     c->hslot[0].acc, c->hslot[0].tb, c->hslot[1].acc, c->hslot[1].tb};
     for (void *b : bufs) dfree(b);
@@ -612,6 +615,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     dv_ctx *c = new (std::nothrow) dv_ctx();
     if (!c) return DV_ERR_NOMEM;
     c->cfg = *cfg;
+    c->cstride = cfg->workload == DV_TPCC ? 3u : 1u;
     int r = hip_fail(hipSetDevice(cfg->device), "hipSetDevice");
     if (!r) r = hip_fail(hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking), "stream");
     c->stream = c->own_stream;
@@ -837,6 +841,19 @@ int dv_kernel_times(dv_ctx *c, dv_kernel_time *out, uint32_t cap, int reset) {
     return (int)n;
 }
 
+namespace {
+// one state column of n rows between the host (dense) and the context's
+// column array (every cstride-th word), synchronously
+hipError_t col_copy(dv_ctx *c, void *dst, const void *src, uint64_t n, hipMemcpyKind kind) {
+    const size_t cs = (size_t)c->cstride * 8;
+    const bool to_dev = kind == hipMemcpyHostToDevice;
+    hipError_t e = c->cstride == 1 ? hipMemcpyAsync(dst, src, n * 8, kind, c->stream)
+                                   : hipMemcpy2DAsync(dst, to_dev ? cs : 8, src, to_dev ? 8 : cs, 8, n, kind,
+                                                      c->stream);
+    return e == hipSuccess ? hipStreamSynchronize(c->stream) : e;
+}
+}  // namespace
+
 // Workload::init_schema (system/wl.cpp:31-149) + IndexHash::init (index_hash.cpp:22-42)
 int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t nbuckets,
                     uint32_t hash_kind) {
@@ -849,42 +866,28 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     HIPCHK(hipSetDevice(c->cfg.device));
     // grow the global hot column / primary-key arrays (load-time only)
     const uint64_t new_total = c->total_rows + capacity_rows;
-    const bool cols = c->cfg.workload == DV_TPCC;
-    uint64_t *nf0 = nullptr, *npk = nullptr, *nc1 = nullptr, *nc2 = nullptr;
+    const uint64_t cs = c->cstride;  // (TPC-C: 3 state columns per row, row-major)
+    uint64_t *nf0 = nullptr, *npk = nullptr;
     uint8_t *ntg = nullptr;
-    int r = dalloc(&nf0, new_total);
+    int r = dalloc(&nf0, new_total * cs);
     if (!r) r = dalloc(&npk, new_total);
     if (!r) r = dalloc(&ntg, new_total);
-    if (!r && cols) r = dalloc(&nc1, new_total);
-    if (!r && cols) r = dalloc(&nc2, new_total);
-    if (r) { dfree(nf0); dfree(npk); dfree(ntg); dfree(nc1); return r; }
+    if (r) { dfree(nf0); dfree(npk); dfree(ntg); return r; }
     if (c->total_rows) {
-        HIPCHK(hipMemcpyAsync(nf0, c->f0, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(nf0, c->f0, c->total_rows * cs * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(npk, c->pkey, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
         HIPCHK(hipMemcpyAsync(ntg, c->ktag, c->total_rows, hipMemcpyDeviceToDevice, c->stream));
-        if (cols) {
-            HIPCHK(hipMemcpyAsync(nc1, c->col1, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
-            HIPCHK(hipMemcpyAsync(nc2, c->col2, c->total_rows * 8, hipMemcpyDeviceToDevice, c->stream));
-        }
     }
-    HIPCHK(hipMemsetAsync(nf0 + c->total_rows, 0, capacity_rows * 8, c->stream));
+    HIPCHK(hipMemsetAsync(nf0 + c->total_rows * cs, 0, capacity_rows * cs * 8, c->stream));
     HIPCHK(hipMemsetAsync(npk + c->total_rows, 0xFF, capacity_rows * 8, c->stream));
     HIPCHK(hipMemsetAsync(ntg + c->total_rows, kTagWide, capacity_rows, c->stream));  // (no key: pkey decides)
-    if (cols) {
-        HIPCHK(hipMemsetAsync(nc1 + c->total_rows, 0, capacity_rows * 8, c->stream));
-        HIPCHK(hipMemsetAsync(nc2 + c->total_rows, 0, capacity_rows * 8, c->stream));
-    }
     HIPCHK(hipStreamSynchronize(c->stream));
     dfree(c->f0);
     dfree(c->pkey);
     dfree(c->ktag);
-    dfree(c->col1);
-    dfree(c->col2);
     c->f0 = nf0;
     c->pkey = npk;
     c->ktag = ntg;
-    c->col1 = nc1;
-    c->col2 = nc2;
     t.created = true;
     t.cap_rows = capacity_rows;
     t.row_base = c->total_rows;
@@ -972,7 +975,7 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
         HIPCHK(hipMemcpy(t.bstart, cnt.data(), (nb + 1) * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     if (n) {
-        if (f0) HIPCHK(hipMemcpy(c->f0 + t.row_base, f0, n * 8, hipMemcpyHostToDevice));
+        if (f0) HIPCHK(col_copy(c, c->f0 + t.row_base * c->cstride, f0, n, hipMemcpyHostToDevice));
         HIPCHK(hipMemcpy(c->pkey + t.row_base, keys, n * 8, hipMemcpyHostToDevice));
         if (implicit) {  // row i holds keys[i]
             std::vector<uint8_t> tg(n);
@@ -1031,7 +1034,7 @@ int dv_read_rows(dv_ctx *c, uint32_t table, const uint64_t *keys, uint64_t n, ui
     if (!r) {
         HIPCHK(hipMemsetAsync(c->ctr, 0, sizeof(Counters), c->stream));
         HIPCHK(hipMemcpyAsync(dk, keys, n * 8, hipMemcpyHostToDevice, c->stream));
-        launch_gather_rows(c->stream, make_tables(c), table, dk, n, c->f0, dout, c->ctr);
+        launch_gather_rows(c->stream, make_tables(c), table, dk, n, c->f0, c->cstride, dout, c->ctr);
         HIPCHK(hipMemcpyAsync(out_f0, dout, n * 8, hipMemcpyDeviceToHost, c->stream));
         r = sync_counters(c);
         if (!r) r = err_from_bits(c->h_ctr->err);
@@ -1048,9 +1051,7 @@ int dv_read_table(dv_ctx *c, uint32_t table, uint64_t first_row, uint64_t n, uin
     if (first_row + n > t.cap_rows) return DV_ERR_ARG;
     if (!n) return DV_OK;
     HIPCHK(hipSetDevice(c->cfg.device));
-    HIPCHK(hipMemcpyAsync(out_f0, c->f0 + t.row_base + first_row, n * 8, hipMemcpyDeviceToHost,
-                          c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(col_copy(c, out_f0, c->f0 + (t.row_base + first_row) * c->cstride, n, hipMemcpyDeviceToHost));
     return DV_OK;
 }
 
@@ -1061,8 +1062,9 @@ int dv_load_table_cols(dv_ctx *c, uint32_t table, const uint64_t *keys, const ui
     int r = dv_load_table(c, table, keys, col0, n);
     if (r || !n) return r;
     const HostTable &t = c->tab[table];
-    if (col1) HIPCHK(hipMemcpy(c->col1 + t.row_base, col1, n * 8, hipMemcpyHostToDevice));
-    if (col2) HIPCHK(hipMemcpy(c->col2 + t.row_base, col2, n * 8, hipMemcpyHostToDevice));
+    uint64_t *g = c->f0 + t.row_base * c->cstride;
+    if (col1) HIPCHK(col_copy(c, g + 1, col1, n, hipMemcpyHostToDevice));
+    if (col2) HIPCHK(col_copy(c, g + 2, col2, n, hipMemcpyHostToDevice));
     return DV_OK;
 }
 
@@ -1076,9 +1078,7 @@ int dv_read_table_col(dv_ctx *c, uint32_t table, uint32_t col, uint64_t first_ro
     if (first_row + n > t.cap_rows) return DV_ERR_ARG;
     if (!n) return DV_OK;
     HIPCHK(hipSetDevice(c->cfg.device));
-    const uint64_t *src = (col == 1 ? c->col1 : c->col2) + t.row_base + first_row;
-    HIPCHK(hipMemcpyAsync(out, src, n * 8, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(col_copy(c, out, c->f0 + (t.row_base + first_row) * c->cstride + col, n, hipMemcpyDeviceToHost));
     return DV_OK;
 }
 
@@ -1166,10 +1166,15 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     const uint32_t slog = calvin ? 7u : c->slog;  // CALVIN: positions only name access ids
     rec(c, 0);
-    // (TPC-C: the o_id outputs zeroed here, k_tpcc_oid writes the committed NewOrders')
+    // (TPC-C: the o_id outputs zeroed here, the execution writes the committed NewOrders'; a
+    // pipelined batch, dv_tpcc_epoch_run_device_batch: gated on the epoch before, whose
+    // read-back this clear writes)
+    const bool mir = c->mir_pending;
+    c->mir_pending = false;
     launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, calvin ? ST_COMMIT : ST_UNDEC,
                        c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr, nullptr,
-                       0, false, nullptr, nullptr, 0,
+                       0, c->clear_gate, mir ? c->d_mir[c->mir_slot] : nullptr,
+                       mir ? c->d_mseq[c->mir_slot] : nullptr, mir ? c->mir_seq : 0ull,
                        c->cfg.workload == DV_TPCC ? c->tp_oid : nullptr);
     c->ticket = 0;
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles && !ep->n_acc_dev;
@@ -1343,9 +1348,8 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.status = c->status;
         x.tb_start = c->tb_start;
         x.args = c->tp_args;
-        x.c0 = c->f0;
-        x.c1 = c->col1;
-        x.c2 = c->col2;
+        x.cols = c->f0;
+        x.oid_direct = c->cfg.cc_alg != DV_CALVIN;
         x.dsnap = c->tp_dsnap;
         x.dist_base = dt.row_base;
         x.dist_rows = dt.created ? dt.cap_rows : 0;
@@ -1871,10 +1875,10 @@ struct EpochSnap {
 // mirror (slot), with no host wait; gate: the epoch before it is still unread;
 // defer: another pipelined epoch is queued right behind it, whose clear
 // writes this one's mirror (one launch fewer per epoch)
-int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate, int slot, EpochSnap &sn,
-                 bool defer) {
+template <class Decide>
+int pipe_enqueue(dv_ctx *c, Decide &&decide, uint8_t *d_commit, bool gate, int slot, EpochSnap &sn, bool defer) {
     c->clear_gate = gate;
-    int r = run_prefix_epoch(c, ep);
+    int r = decide();
     c->clear_gate = false;
     if (r) {
         mirror_flush(c);  // (the previous epoch's read-back, when this one never reached its clear)
@@ -1903,6 +1907,7 @@ int pipe_enqueue(dv_ctx *c, const dv_epoch_dev *ep, uint8_t *d_commit, bool gate
     }
     c->phase = 0;
     c->prefix_mode = false;
+    c->tp_args = c->tp_oid = nullptr;
     if (!r) r = hip_fail(hipGetLastError(), "counter mirror");
     return r;
 }
@@ -1974,19 +1979,16 @@ int pipe_redo(dv_ctx *c) {
     return DV_OK;
 }
 
-}  // namespace
-
-extern "C" {
-
-int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
-                              dv_stats *sts) {
-    KProfScope kps_(c);
-    if (!c || (n && !eps)) return DV_ERR_ARG;
-    if (c->phase != 0) return DV_ERR_STATE;
-    HIPCHK(hipSetDevice(c->cfg.device));
+// Pipelined epochs: epoch k+1 is queued (gated on epoch k) before epoch k
+// is read back.  pipelined(k): epoch k can be queued that way; enqueue(k):
+// queues its decision (the clear honours clear_gate / mir_pending); run(k,
+// st): runs it synchronously (an epoch that cannot be pipelined, or one to
+// redo after a halt).
+template <class Commit, class Pipelined, class Enqueue, class Run>
+int run_batch(dv_ctx *c, uint32_t n, dv_stats *sts, Commit &&commit_of, Pipelined &&pipelined, Enqueue &&enqueue,
+              Run &&run) {
     EpochSnap snap[2];
     int64_t pend = -1;  // the epoch queued but not yet read back
-    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
     auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
     // the pending epoch: read back; if it halted, it runs again, and so does
     // `next` (queued behind it, gated) when given
@@ -2000,13 +2002,9 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
         if (!halted) return DV_OK;
         c->mir_pending = false;  // (`next`'s read-back: it runs again below)
         r = pipe_redo(c);
-        if (!r) r = dv_epoch_run_device(c, &eps[pend], commit_of((uint32_t)pend), nullptr, stats_of((uint32_t)pend));
-        if (!r && next >= 0) r = dv_epoch_run_device(c, &eps[next], commit_of((uint32_t)next), nullptr,
-                                                     stats_of((uint32_t)next));
+        if (!r) r = run((uint32_t)pend, stats_of((uint32_t)pend));
+        if (!r && next >= 0) r = run((uint32_t)next, stats_of((uint32_t)next));
         return r ? r : 1;  // 1: `next` ran already
-    };
-    auto pipelined = [&](uint32_t k) {
-        return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P;
     };
     auto fail = [&](int r) {  // (no read-back is waited for after an error)
         c->mir_pending = false;
@@ -2019,13 +2017,14 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
                 if (r < 0) return fail(r);
                 pend = -1;
             }
-            const int r = dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, stats_of(k));
+            const int r = run(k, stats_of(k));
             if (r) return fail(r);
             continue;
         }
         // the next epoch's clear writes this one's read-back when it is queued right behind
         const bool defer = k + 1 < n && pipelined(k + 1);
-        int r = pipe_enqueue(c, &eps[k], commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1], defer);
+        int r = pipe_enqueue(c, [&] { return enqueue(k); }, commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1],
+                             defer);
         if (r) {
             (void)hipStreamSynchronize(c->stream);
             if (pend >= 0) {  // (its read-back, for the statistics; the error is returned either way)
@@ -2049,6 +2048,50 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
         if (r < 0) return fail(r);
     }
     return DV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
+                              dv_stats *sts) {
+    KProfScope kps_(c);
+    if (!c || (n && !eps)) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    return run_batch(
+        c, n, sts, commit_of,
+        [&](uint32_t k) { return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P; },
+        [&](uint32_t k) { return run_prefix_epoch(c, &eps[k]); },
+        [&](uint32_t k, dv_stats *st) { return dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, st); });
+}
+
+int dv_tpcc_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, const uint64_t *const *d_args, uint32_t n,
+                                   uint8_t *const *d_commits, uint64_t *const *d_oids, dv_stats *sts) {
+    KProfScope kps_(c);
+    if (!c || (n && (!eps || !d_args)) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
+    if (c->phase != 0) return DV_ERR_STATE;
+    HIPCHK(hipSetDevice(c->cfg.device));
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    auto oid_of = [&](uint32_t k) { return d_oids ? d_oids[k] : nullptr; };
+    return run_batch(
+        c, n, sts, commit_of, [&](uint32_t) { return !timing(c) && !ktiming(c); },
+        [&](uint32_t k) {
+            int r = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
+            if (!r && c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
+                r = decide_epoch(c);
+                if (r) {
+                    c->phase = 0;
+                    c->tp_args = c->tp_oid = nullptr;
+                }
+            }
+            return r;
+        },
+        [&](uint32_t k, dv_stats *st) {
+            return dv_tpcc_epoch_run_device(c, &eps[k], d_args[k], commit_of(k), oid_of(k), st);
+        });
 }
 
 }  // extern "C"
@@ -2130,7 +2173,8 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
             continue;
         }
         const dv_epoch_dev d = desc(k);
-        r = pipe_enqueue(c, &d, commit_of(k), pend >= 0, (int)(k & 1), snap[k & 1], k + 1 < n_epochs);
+        r = pipe_enqueue(c, [&] { return run_prefix_epoch(c, &d); }, commit_of(k), pend >= 0, (int)(k & 1),
+                         snap[k & 1], k + 1 < n_epochs);
         if (!r) {
             // behind the execution: epoch k + 1 from epoch k's final statuses (a
             // no-op when k halted -- the host redoes both below)

@@ -26,10 +26,15 @@
 //     in any order.  C_PAYMENT_CNT is loaded as the integer 1 and read as a
 //     double (a denormal): denormal + 1.0 rounds to 1.0 either way.
 //   - D_NEXT_O_ID: o_id of a NewOrder = D_NEXT_O_ID + 1 + (committed NewOrders
-//     before it in the district's queue): the apply pass snapshots D_NEXT_O_ID
-//     at each district queue's head, then one single-pass segmented count
-//     (decoupled look-back, dvcc_common.h) numbers the committed NewOrders of
-//     every queue and the queue's last element stores the grown word.
+//     before it in the district's queue).  NO_WAIT / WAIT_DIE / OCC commit at
+//     most one writer of a district row (NewOrder and Payment both write it),
+//     so the update pass sets o_id = ++D_NEXT_O_ID itself.  CALVIN commits
+//     them all: the apply pass snapshots D_NEXT_O_ID at each district queue's
+//     head, then one single-pass segmented count (decoupled look-back,
+//     dvcc_common.h) numbers the committed NewOrders of every queue and the
+//     queue's last element stores the grown word.
+//   - The three state columns of a row are one 24-byte group (row-major): a
+//     row's updates touch one or two 128-B lines instead of three.
 //   - S_QUANTITY is piecewise (s > q + 10 ? s - q : s - q + 91): the queue
 //     head walks its stock row's queue in order (stock queues are short: the
 //     NURand(8191) item choice spreads over max_items x warehouses rows).
@@ -46,7 +51,7 @@ constexpr uint64_t kOpMask = (1ull << 56) - 1;
 
 __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint64_t *__restrict__ keys,
                                                          const uint8_t *__restrict__ tables, uint64_t n,
-                                                         const uint64_t *__restrict__ col0,
+                                                         const uint64_t *__restrict__ cols,
                                                          uint64_t *__restrict__ okeys,
                                                          uint8_t *__restrict__ otables) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
@@ -75,7 +80,7 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
                     if (cnt) row = t.ix[first + cnt / 2].row;
                 }
                 // no customer of that name: key ~0 misses in the probe (DV_ERR_KEY_NOT_FOUND)
-                key = row == ~0ull ? ~0ull : col0[t.row_base + row];
+                key = row == ~0ull ? ~0ull : cols[(t.row_base + row) * kTpccCols];
                 tb = DV_TPCC_CUSTOMER;
             }
         }
@@ -94,9 +99,10 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint
 __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restrict__ pairs, uint64_t n,
                                                        const uint8_t *__restrict__ status,
                                                        const uint32_t *__restrict__ tb_start,
-                                                       const uint64_t *__restrict__ args, uint64_t *c0,
-                                                       uint64_t *c1, uint64_t *c2, uint64_t *__restrict__ dsnap,
-                                                       uint64_t dist_base, uint64_t dist_rows, Counters *ctr) {
+                                                       const uint64_t *__restrict__ args, uint64_t *cols,
+                                                       int oid_direct, uint64_t *__restrict__ oid,
+                                                       uint64_t *__restrict__ dsnap, uint64_t dist_base,
+                                                       uint64_t dist_rows, Counters *ctr) {
     if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
     const uint32_t lane = threadIdx.x & 63;
     unsigned long long wcnt = 0;
@@ -113,7 +119,17 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
         const uint32_t prow = __shfl_up(row, 1, 64);
         const bool head = valid && (i == 0 || (lane ? prow : pair_row(pairs[i - 1])) != row);
         const bool dist_row = row >= dist_base && row < dist_base + dist_rows;
-        if (head && dist_row) dsnap[row - dist_base] = c1[row];  // D_NEXT_O_ID before the epoch
+        uint64_t *rc = cols + (uint64_t)row * kTpccCols;  // the row's three columns (24 B)
+        if (oid_direct) {
+            // the district's only committed writer: o_id = ++D_NEXT_O_ID (new_order_5)
+            if (com && dist_row && op == DV_TOP_NO_DIST) {
+                const uint64_t o = rc[1] + 1;
+                rc[1] = o;
+                if (oid) oid[txn] = o;
+            }
+        } else if (head && dist_row) {
+            dsnap[row - dist_base] = rc[1];  // D_NEXT_O_ID before the epoch
+        }
         if (com && (p & 1)) wcnt++;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0;
         if (com) {
@@ -139,13 +155,13 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
         }
         const bool run_first = valid && (lane == 0 || prow != row);
         if (run_first) {
-            if (a0 != 0.0) atomicAdd(reinterpret_cast<double *>(c0 + row), a0);
-            if (a1 != 0.0) atomicAdd(reinterpret_cast<double *>(c1 + row), a1);
-            if (a2 != 0.0) atomicAdd(reinterpret_cast<double *>(c2 + row), a2);
+            if (a0 != 0.0) atomicAdd(reinterpret_cast<double *>(rc), a0);
+            if (a1 != 0.0) atomicAdd(reinterpret_cast<double *>(rc + 1), a1);
+            if (a2 != 0.0) atomicAdd(reinterpret_cast<double *>(rc + 2), a2);
         }
         if (head && op == DV_TOP_NO_STOCK) {  // new_order_9 in queue order
-            uint64_t s = c0[row];
-            int64_t ytd = (int64_t)c1[row], ocnt = (int64_t)c2[row];
+            uint64_t s = rc[0];
+            int64_t ytd = (int64_t)rc[1], ocnt = (int64_t)rc[2];
             bool any = false;
             for (uint64_t j = i; j < n; j++) {
                 const uint64_t q = pairs[j];
@@ -159,9 +175,9 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                 any = true;
             }
             if (any) {
-                c0[row] = s;
-                c1[row] = (uint64_t)ytd;
-                c2[row] = (uint64_t)ocnt;
+                rc[0] = s;
+                rc[1] = (uint64_t)ytd;
+                rc[2] = (uint64_t)ocnt;
             }
         }
     }
@@ -182,7 +198,7 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
                                                      const uint32_t *__restrict__ tb_start,
                                                      const uint64_t *__restrict__ args,
                                                      const uint64_t *__restrict__ dsnap, uint64_t dist_base,
-                                                     uint64_t dist_rows, uint64_t *__restrict__ c1,
+                                                     uint64_t dist_rows, uint64_t *__restrict__ cols,
                                                      uint64_t *__restrict__ oid, uint64_t *desc,
                                                      uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
     __shared__ uint64_t s_el[kRTile + kRTile / kRIPT];
@@ -248,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
                 const uint64_t snap = dsnap[row - dist_base];
                 if (f && oid) oid[pair_txn(e[j])] = snap + run.c;
                 const uint64_t q = j + 1 < cnt ? e[j + 1] : (j + 1 < kRIPT ? ~0ull : nxt);
-                if (pair_row(q) != row && run.c) c1[row] = snap + run.c;  // the queue's last element
+                if (pair_row(q) != row && run.c) cols[(uint64_t)row * kTpccCols + 1] = snap + run.c;  // queue's last
             }
         }
     }
@@ -262,19 +278,20 @@ uint32_t grid_for(uint64_t n) {
 }  // namespace
 
 void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *tables,
-                         uint64_t n, const uint64_t *col0, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
+                         uint64_t n, const uint64_t *cols, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
     if (n == 0) return;
     (void)ctr;
-    DV_LAUNCH(k_tpcc_resolve, grid_for(n), kBlock, 0, s, tabs, keys, tables, n, col0, okeys, otables);
+    DV_LAUNCH(k_tpcc_resolve, grid_for(n), kBlock, 0, s, tabs, keys, tables, n, cols, okeys, otables);
 }
 
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
     if (x.n == 0) return;
-    DV_LAUNCH(k_tpcc_apply, grid_for(x.n), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.c0, x.c1, x.c2,
-                                                  x.dsnap, x.dist_base, x.dist_rows, x.ctr);
+    DV_LAUNCH(k_tpcc_apply, grid_for(x.n), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.cols,
+              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr);
+    if (x.oid_direct) return;
     const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
     DV_LAUNCH(k_tpcc_oid, ntiles, kBlock, 0, s, x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
-                                         x.dist_base, x.dist_rows, x.c1, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
+                                         x.dist_base, x.dist_rows, x.cols, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
 }
 
 }  // namespace dvcc

@@ -163,6 +163,8 @@ SIGNATURES = [
     ("dv_read_table_col", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64,
                                          ctypes.c_uint64, _vp]),
     ("dv_tpcc_epoch_run_device", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, _vp, _P(Stats)]),
+    ("dv_tpcc_epoch_run_device_batch", ctypes.c_int, [_vp, _P(EpochDev), _vp, ctypes.c_uint32, _vp, _vp,
+                                                      _P(Stats)]),
     ("dv_comm_set_mode", ctypes.c_int, [_vp, ctypes.c_int]),
     ("dv_epoch_run_device_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(_vp), _P(Stats)]),
     ("dv_epoch_run_closed_loop", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _P(EpochDev),

@@ -98,6 +98,28 @@ class TpccEngine(CCEngine):
         return st
 
 
+    def run_tpcc_epochs_device(self, deps, d_args, d_commits=None, d_oids=None):
+        """Several TPC-C epochs back to back (dv_tpcc_epoch_run_device_batch):
+        epoch k+1 is queued before epoch k is read back.  deps / d_args: one
+        DeviceEpoch and operation-word tensor per epoch; d_commits / d_oids:
+        one device tensor per epoch, one tensor for all, or None.  Returns
+        the list of stats."""
+        self._after_torch()
+        n = len(deps)
+
+        def ptrs(x):
+            if x is None:
+                return None
+            xs = x if isinstance(x, (list, tuple)) else [x] * n
+            return (ctypes.c_void_p * n)(*[_ptr(t) for t in xs])
+        descs = (L.EpochDev * n)(*[d.desc() for d in deps])
+        args = ptrs(list(d_args))
+        sts = (L.Stats * n)()
+        self._keep = (deps, d_args, d_commits, d_oids)
+        L.check(L.lib().dv_tpcc_epoch_run_device_batch(self._ctx, descs, args, n, ptrs(d_commits), ptrs(d_oids),
+                                                       sts), "dv_tpcc_epoch_run_device_batch")
+        return list(sts)
+
     def run_tpcc_epoch_part(self, home, d_args, d_owner, txns_per_rank, d_commit, d_oid=None):
         """Config E from the engine (dv_tpcc_epoch_run_part): this rank's
         client batch `home` (DeviceEpoch), its operation words and owner

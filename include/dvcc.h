@@ -585,6 +585,17 @@ int dv_read_table_col(dv_ctx *ctx, uint32_t table, uint32_t col, uint64_t first_
  * whose district is local (0 otherwise) */
 int dv_tpcc_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t *d_args,
                              uint8_t *d_commit, uint64_t *d_oid, dv_stats *st);
+/* n TPC-C epochs back to back, pipelined like dv_epoch_run_device_batch
+ * (replaces TPCCTxnManager's per-txn loop, tpcc_txn.cpp:117-244, for a
+ * stream of epochs): epoch k+1 is queued before epoch k is read back, its
+ * clear gated on epoch k (a halted epoch and the one behind it run again
+ * synchronously), and its clear writes epoch k's read-back.  d_args[k],
+ * d_commits[k] / d_oids[k] (either array, or an entry, may be NULL) as for
+ * dv_tpcc_epoch_run_device; sts (may be NULL): n stats.  Stops at the first
+ * failing epoch; the ones before it are applied. */
+int dv_tpcc_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, const uint64_t *const *d_args,
+                                   uint32_t n, uint8_t *const *d_commits, uint64_t *const *d_oids,
+                                   dv_stats *sts);
 /* the same from host buffers (H2D + run + D2H; records as dv_epoch_run);
  * out_oid (may be NULL): n_txn words */
 int dv_tpcc_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,
