@@ -82,6 +82,10 @@ def parse():
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
+    ap.add_argument("--ipc-rehearsal", action="store_true",
+                    help="N>1 ranks sharing fewer GPUs (a rehearsal of the N>1 path on a one-GPU box): torch "
+                         "collectives over gloo, the engine's over dv_comm_init_ipc (a test transport); the "
+                         "numbers are no scaling result")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -410,7 +414,7 @@ def timed(step, first, warmup, steps, world, batch=None):
         dist.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el], dtype=torch.float64, device="cpu" if dist.get_backend() == "gloo" else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     return stats, el
@@ -606,6 +610,23 @@ def stage_summary(stats, sstats, table, el, R):
     return out
 
 
+def engine_comm_init(a, eng, world, rank, tag):
+    """The engine's communicator: RCCL (dv_comm_init), or for --ipc-rehearsal
+    the process-boundary test transport (dv_comm_init_ipc), ranks meeting at a
+    shared-memory name rank 0 picks."""
+    if a.ipc_rehearsal:
+        name = [f"/dvcc_bench_{os.getpid()}_{tag}" if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(name, src=0)
+        eng.comm_init_ipc(name[0], world, rank)
+        return
+    uid = [dvcc.comm_unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0)
+    with stdout_to_stderr():
+        eng.comm_init(uid[0], world, rank)
+
+
 class PartitionedBench:
     """One rank of a partitioned run: the engine bound to partition `rank`,
     its RCCL communicator (dv_comm_init) and device-resident home batches."""
@@ -621,11 +642,7 @@ class PartitionedBench:
                                  part_id=rank, timing=TIMING[a.timing], lsd_sort=a.lsd_sort)
         self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
-        uid = [dvcc.comm_unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        with stdout_to_stderr():
-            self.eng.comm_init(uid[0], world, rank)
+        engine_comm_init(a, self.eng, world, rank, "ycsb")
         self.eng.comm_set_mode(a.part_mode)
         self.rows = rows
         self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
@@ -684,11 +701,7 @@ def tpcc_part_leg(a, world, rank, local_rank, first_step):
         n_max = max(sizes) // world
         eng = T.TpccEngine(cc_name, pp, n_max * world, device=local_rank, part_id=rank, seed=1)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
-        uid = [dvcc.comm_unique_id() if rank == 0 else None]
-        if world > 1:
-            dist.broadcast_object_list(uid, src=0)
-        with stdout_to_stderr():
-            eng.comm_init(uid[0], world, rank)
+        engine_comm_init(a, eng, world, rank, "tpcc_" + cc_name)
         for total in sizes:
             n_rank = total // world
             batches = [T.gen(pp, n_rank, dvcc.epoch_seed(rank, 500 + e), home_part=rank) for e in range(2)]
@@ -766,6 +779,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.ipc_rehearsal:  # (ranks share the box's GPUs)
+        local_rank %= max(1, torch.cuda.device_count())
+        os.environ["LOCAL_RANK"] = str(local_rank)
     a.gpus = world
     torch.cuda.set_device(local_rank)
     # one stream for torch and the engine: the engine then needs no event
@@ -774,7 +790,10 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream())
     if world > 1:
         with stdout_to_stderr():
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            if a.ipc_rehearsal:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
             dist.barrier()
     if a.tpcc_only:
         print(json.dumps({"tpcc": tpcc_leg(a)}), flush=True)
@@ -848,7 +867,9 @@ def main():
             "txns_per_epoch": n_txn_total, "txns_per_epoch_per_gpu": n_txn_rank, "req_per_query": R,
             "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
             "mpr": mpr if part else 0.0, "part_per_txn": min(2, world),
-            "parallelism": f"partitioned x{world} (PART_CNT={world}, RCCL)" if world > 1 else "1 GPU",
+            "parallelism": (f"partitioned x{world} (PART_CNT={world}, "
+                            + ("IPC rehearsal: ranks sharing a GPU, not a scaling result)" if a.ipc_rehearsal
+                               else "RCCL)")) if world > 1 else "1 GPU",
             "epochs_per_step": world if group else 1,
             "protocol": ("epoch groups (rank e decides epoch e of each group of N; batches all-to-allv'd to "
                          "the decider, committed accesses forwarded to their owners, epochs executed in order)"
