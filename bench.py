@@ -86,6 +86,9 @@ def parse():
                     help="N>1 ranks sharing fewer GPUs (a rehearsal of the N>1 path on a one-GPU box): torch "
                          "collectives over gloo, the engine's over dv_comm_init_ipc (a test transport); the "
                          "numbers are no scaling result")
+    ap.add_argument("--lanes", type=int, default=2,
+                    help="one GPU: decision lanes (dv_epoch_run_device_lanes) -- epochs decided on this many "
+                         "contexts in turn, executions in epoch order; 1 = dv_epoch_run_device_batch")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -824,7 +827,17 @@ def main():
         def step(i):
             return eng.run_epoch_device(deps[i % n_epochs], d_commit)
 
+        # decision lanes: more contexts over the engine's tables, each on its
+        # own stream, so one epoch's (latency-bound) rounds overlap the next's
+        lanes = [eng.open_lane() for _ in range(max(1, a.lanes) - 1)]
+
         def batch(first, count):  # the product's pipelined entry point: epoch k+1 queued before k is read
+            run = [deps[(first + i) % n_epochs] for i in range(count)]
+            if lanes:
+                return eng.run_epochs_lanes(lanes, run, d_commit)
+            return eng.run_epochs_device(run, d_commit)
+
+        def batch1(first, count):
             return eng.run_epochs_device([deps[(first + i) % n_epochs] for i in range(count)], d_commit)
     else:
         weak = not a.no_weak
@@ -844,7 +857,9 @@ def main():
     # dv_epoch_group_run_batch (epoch groups); the other protocols step
     pipelined = not a.no_pipeline and (not part or a.protocol == "group")
     stats, el = timed(step, 0, a.warmup, a.steps, world, batch if pipelined else None)
-    pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats, batch if pipelined else None)
+    # (the profiling legs time one context's launches: one lane)
+    pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats,
+                                          (batch1 if not part else batch) if pipelined else None)
     table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"
@@ -879,6 +894,7 @@ def main():
                           1: "list protocol (owner split, per-round verdict all-reduce)",
                           2: "replicated"}[a.part_mode] if part else "single GPU"),
             "distinct_epochs": n_epochs,
+            "decision_lanes": (max(1, a.lanes) if not part and not a.no_pipeline else 1),
         },
         "roofline": roofline(table, len(pstats), a),
         "timing_in_timed_region": a.timing,

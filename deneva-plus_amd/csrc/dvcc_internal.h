@@ -554,7 +554,9 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
-                    unsigned long long seq);
+                    unsigned long long seq, uint32_t *gate = nullptr);
+// decision lanes (dv_epoch_run_device_lanes): halt this epoch if *prev_gate
+void launch_lane_gate(hipStream_t s, const uint32_t *prev_gate, Counters *ctr);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,

@@ -1186,19 +1186,34 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
 // the counters into their host-mapped mirror, then the sequence word the
 // host spins on (sync_counters): no blit and no stream synchronisation
 // between an epoch's last kernel and the host reading its outcome
+// gate (decision lanes, optional): one device word for the epoch executed
+// after this one on another lane -- nonzero when this epoch halted or failed
 __global__ __launch_bounds__(kBlock) void k_ctr_out(const Counters *__restrict__ ctr, Counters *hctr,
-                                                    unsigned long long *hseq, unsigned long long seq) {
+                                                    unsigned long long *hseq, unsigned long long seq,
+                                                    uint32_t *gate) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(ctr);
     uint32_t *dst = reinterpret_cast<uint32_t *>(hctr);
     for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) dst[i] = src[i];
+    if (gate && threadIdx.x == 0) *gate = (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
-                    unsigned long long seq) {
-    DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq);
+                    unsigned long long seq, uint32_t *gate) {
+    DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq, gate);
+}
+
+// decision lanes: before an epoch executes, the epoch executed before it (on
+// another lane) must have neither halted nor failed -- else this one halts
+// too (nothing of it executes; the host runs both again, in order)
+__global__ void k_lane_gate(const uint32_t *__restrict__ prev_gate, Counters *ctr) {
+    if (threadIdx.x == 0 && *prev_gate) ctr->halt = 1u;
+}
+
+void launch_lane_gate(hipStream_t s, const uint32_t *prev_gate, Counters *ctr) {
+    DV_LAUNCH(k_lane_gate, 1, 64, 0, s, prev_gate, ctr);
 }
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,

@@ -25,6 +25,11 @@ using namespace dvcc;
 
 namespace {
 
+// dv_epoch_run_device_lanes: two lanes, each on half of the CUs (with three,
+// gpurun_out r03_w, a lane's asynchronous launch did not find its
+// workgroups co-resident on its third and yielded every epoch)
+constexpr uint32_t kMaxLanes = 2;
+
 struct HostTable {
     bool created = false, loaded = false;
     bool implicit_rows = false;  // direct map with local row == bucket: probes read pkey
@@ -74,6 +79,21 @@ struct dv_ctx {
     // row-major: k_tpcc_apply touches all three of a row), f0 = column 0;
     // YCSB: f0 alone (cstride 1)
     uint32_t cstride = 1;
+    // decision lanes (dv_open_lane): a lane shares its owner's tables (the
+    // arrays above and tab[]'s index arrays are the owner's, never freed
+    // here); lanes_open counts the lanes of an owner (its tables are frozen)
+    dv_ctx *table_owner = nullptr;
+    uint32_t lanes_open = 0;
+    uint32_t *d_gate = nullptr;    // 2 words: this context's epochs' gate words (k_ctr_out)
+    hipEvent_t lane_ev = nullptr;  // recorded after this context's last queued execution
+    // dv_epoch_run_device_lanes runs lane l of n on lane_stream, masked to
+    // the CUs i with i % n == l: a lane's asynchronous round launch needs all
+    // of its workgroups resident at once, and on the whole chip the other
+    // lane's kernels keep taking the CUs its last workgroups wait for (its
+    // workgroups yield, the epochs run again -- 0.69 ms per epoch instead of
+    // 0.29, gpurun_out r03_w); lane_g: its workgroups on its share
+    hipStream_t lane_stream = nullptr;
+    uint32_t lane_n = 0, lane_l = 0, lane_g = 0;
 
     // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
     // execution scratch, and the operation words / o_id output of this epoch
@@ -472,9 +492,9 @@ float elapsed(dv_ctx *c, int a, int b) {
 // host spins on (a blit plus a stream synchronisation cost ~25 us per epoch)
 // the counters into mirror slot k behind everything queued so far; returns
 // the sequence number mirror_wait waits for
-unsigned long long mirror_out(dv_ctx *c, int k) {
+unsigned long long mirror_out(dv_ctx *c, int k, bool gate = false) {
     const unsigned long long want = ++c->cseq;
-    launch_ctr_out(c->stream, c->ctr, c->d_mir[k], c->d_mseq[k], want);
+    launch_ctr_out(c->stream, c->ctr, c->d_mir[k], c->d_mseq[k], want, gate ? c->d_gate + k : nullptr);
     return want;
 }
 
@@ -563,6 +583,14 @@ void dv_close(dv_ctx *c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     comm_free(c->comm);
     c->comm = nullptr;
+    if (c->table_owner) {  // a lane: the tables are its owner's
+        if (c->table_owner->lanes_open) c->table_owner->lanes_open--;
+        for (auto &t : c->tab) t.ix = nullptr, t.bstart = nullptr, t.hbits = nullptr;
+        c->f0 = c->pkey = nullptr;
+        c->ktag = nullptr;
+    }
+    dfree(c->d_gate);
+    if (c->lane_ev) (void)hipEventDestroy(c->lane_ev);
     for (auto &t : c->tab) {
         dfree(t.ix);
         dfree(t.bstart);
@@ -596,6 +624,7 @@ void dv_close(dv_ctx *c) {
         (void)hipEventDestroy(pr.second);
     }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    if (c->lane_stream) (void)hipStreamDestroy(c->lane_stream);
     delete c;
 }
 
@@ -635,6 +664,8 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r) r = dalloc(&c->tb_end, c->n_txn_cap_pad);
     if (!r) r = dalloc(&c->desc, rnb);
     if (!r) r = dalloc(&c->tile_ctr, kTileCtrs);
+    if (!r) r = dalloc(&c->d_gate, 2);
+    if (!r) r = hip_fail(hipEventCreateWithFlags(&c->lane_ev, hipEventDisableTiming), "hipEventCreate");
     if (!r) r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)rnb * 8, c->stream), "memset");
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = dalloc(&c->rel[0], A);
@@ -695,6 +726,36 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
         dv_close(c);
         return r;
     }
+    *out = c;
+    return DV_OK;
+}
+
+// a decision lane of `owner`: a context of the same configuration whose
+// epochs run against the owner's tables (dv_epoch_run_device_lanes); the
+// owner's tables are loaded first and stay frozen while lanes are open
+int dv_open_lane(dv_ctx *owner, dv_ctx **out) {
+    if (!owner || !out) return DV_ERR_ARG;
+    *out = nullptr;
+    if (owner->table_owner || owner->comm || owner->cfg.workload != DV_YCSB) return DV_ERR_ARG;
+    if (owner->phase != 0) return DV_ERR_STATE;
+    if (!ctx_has_tables(owner)) return DV_ERR_NO_TABLE;
+    dv_ctx *c = nullptr;
+    int r = dv_open(&c, &owner->cfg);
+    if (r) return r;
+    r = hip_fail(hipStreamSynchronize(owner->stream), "sync");
+    if (r) {
+        dv_close(c);
+        return r;
+    }
+    for (uint32_t i = 0; i < kMaxTables; i++) c->tab[i] = owner->tab[i];
+    c->total_rows = owner->total_rows;
+    c->f0 = owner->f0;
+    c->pkey = owner->pkey;
+    c->ktag = owner->ktag;
+    c->cstride = owner->cstride;
+    c->prefix_txns = owner->prefix_txns;
+    c->table_owner = owner;
+    owner->lanes_open++;
     *out = c;
     return DV_OK;
 }
@@ -861,7 +922,7 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
         (hash_kind != DV_HASH_YCSB && hash_kind != DV_HASH_MOD))
         return DV_ERR_ARG;
     HostTable &t = c->tab[table];
-    if (t.created) return DV_ERR_STATE;
+    if (t.created || c->lanes_open || c->table_owner) return DV_ERR_STATE;  // (lanes share frozen tables)
     if (c->total_rows + capacity_rows > kMaxRows) return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
     // grow the global hot column / primary-key arrays (load-time only)
@@ -921,6 +982,7 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
     HostTable &t = c->tab[table];
     if (!t.created) return DV_ERR_NO_TABLE;
     if (n > t.cap_rows) return DV_ERR_ARG;
+    if (c->lanes_open || c->table_owner) return DV_ERR_STATE;
     HIPCHK(hipSetDevice(c->cfg.device));
     const uint64_t nb = t.nbuckets;
     const uint32_t P = c->cfg.part_cnt;
@@ -996,6 +1058,7 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
 
 int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
     if (!c || rows_per_part == 0) return DV_ERR_ARG;
+    if (c->lanes_open || c->table_owner) return DV_ERR_STATE;
     HostTable &t = c->tab[0];
     if (!t.created) {
         int r = dv_create_table(c, 0, rows_per_part, rows_per_part, DV_HASH_YCSB);
@@ -2092,6 +2155,186 @@ int dv_tpcc_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, const uin
         [&](uint32_t k, dv_stats *st) {
             return dv_tpcc_epoch_run_device(c, &eps[k], d_args[k], commit_of(k), oid_of(k), st);
         });
+}
+
+// Decision lanes: epoch k is decided on lanes[k % n_lanes] (each lane its own
+// stream and workspace), so one lane's rounds overlap another's; executions
+// stay in epoch order -- epoch k's waits for epoch k-1's (an event across the
+// lanes' streams) and starts halted when k-1 halted or failed (its gate word,
+// k_ctr_out / k_lane_gate).  The host reads epochs back oldest first; a halted
+// one is run again with every epoch queued behind it, synchronously and in
+// order, as dv_epoch_run_device_batch does on one stream.
+int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
+                              uint8_t *const *d_commits, dv_stats *sts) {
+    if (!lanes || n_lanes == 0 || n_lanes > kMaxLanes || (n && !eps)) return DV_ERR_ARG;
+    dv_ctx *const c0 = lanes[0];
+    for (uint32_t l = 0; l < n_lanes; l++) {
+        dv_ctx *c = lanes[l];
+        if (!c) return DV_ERR_ARG;
+        if (c->phase != 0) return DV_ERR_STATE;
+        // every lane runs against the same tables: lanes of lanes[0] (or of its owner)
+        const dv_ctx *own = c->table_owner ? c->table_owner : c;
+        const dv_ctx *own0 = c0->table_owner ? c0->table_owner : c0;
+        if (own != own0 || c->cfg.device != c0->cfg.device || c->cfg.cc_alg != c0->cfg.cc_alg) return DV_ERR_ARG;
+        for (uint32_t m = 0; m < l; m++)
+            if (lanes[m] == c) return DV_ERR_ARG;
+    }
+    if (n_lanes == 1) return dv_epoch_run_device_batch(c0, eps, n, d_commits, sts);
+    HIPCHK(hipSetDevice(c0->cfg.device));
+    int cus = 0;
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c0->cfg.device));
+    for (uint32_t l = 0; l < n_lanes; l++) {
+        dv_ctx *c = lanes[l];
+        if (c->lane_stream && c->lane_n == n_lanes && c->lane_l == l) continue;
+        if (c->lane_stream) (void)hipStreamDestroy(c->lane_stream);
+        c->lane_stream = nullptr;
+        std::vector<uint32_t> mask((cus + 31) / 32, 0u);
+        uint32_t mine = 0;
+        for (int i = 0; i < cus; i++)
+            if ((uint32_t)i % n_lanes == l) mask[i / 32] |= 1u << (i % 32), mine++;
+        HIPCHK(hipExtStreamCreateWithCUMask(&c->lane_stream, (uint32_t)mask.size(), mask.data()));
+        c->lane_n = n_lanes;
+        c->lane_l = l;
+        c->lane_g = (uint32_t)((uint64_t)c->async_g * mine / (uint32_t)cus);
+    }
+    // while the call runs each lane works on its masked stream, ordered after
+    // the caller's stream at the start, and the caller's after it at the end
+    struct OnLaneStreams {
+        dv_ctx *const *ls;
+        uint32_t n;
+        hipStream_t saved[kMaxLanes];
+        uint32_t saved_g[kMaxLanes];
+        OnLaneStreams(dv_ctx *const *l, uint32_t m) : ls(l), n(m) {
+            for (uint32_t i = 0; i < n; i++) {
+                saved[i] = ls[i]->stream;
+                saved_g[i] = ls[i]->async_g;
+                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+                (void)hipStreamWaitEvent(ls[i]->lane_stream, ls[i]->lane_ev, 0);
+                ls[i]->stream = ls[i]->lane_stream;
+                ls[i]->async_g = ls[i]->lane_g;
+            }
+        }
+        ~OnLaneStreams() {
+            for (uint32_t i = 0; i < n; i++) {
+                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+                (void)hipStreamWaitEvent(saved[i], ls[i]->lane_ev, 0);
+                ls[i]->stream = saved[i];
+                ls[i]->async_g = saved_g[i];
+            }
+        }
+    } on_lanes_(lanes, n_lanes);
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
+    auto lane_of = [&](uint32_t k) { return lanes[k % n_lanes]; };
+    auto pipelined = [&](uint32_t k) {
+        dv_ctx *c = lane_of(k);
+        return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P && !c->comm;
+    };
+    struct Pend {
+        uint32_t k;
+        EpochSnap sn;
+    };
+    // queued and unread epochs, oldest first; each lane holds at most two
+    // (its two mirror slots and gate words)
+    const uint32_t window = 2 * n_lanes - 1;
+    Pend ring[2 * kMaxLanes];
+    uint32_t head = 0, count = 0;
+    uint32_t lane_slot[kMaxLanes] = {};
+    dv_ctx *prev = nullptr;  // the lane of the last queued epoch (nullptr: nothing queued is unfinished)
+    int prev_slot = 0;
+    auto drain = [&] {
+        for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
+    };
+    auto run_sync = [&](uint32_t k) { return dv_epoch_run_device(lane_of(k), &eps[k], commit_of(k), nullptr, stats_of(k)); };
+    // read back the oldest queued epoch; a halted one and all behind it run again
+    auto settle = [&]() -> int {
+        Pend &p = ring[head];
+        bool halted = false;
+        int r = pipe_complete(lane_of(p.k), p.sn, stats_of(p.k), &halted);
+        if (r) {
+            drain();
+            return r;
+        }
+        head = (head + 1) % (2 * kMaxLanes);
+        count--;
+        if (!halted) return DV_OK;
+        drain();
+        for (uint32_t l = 0; l < n_lanes; l++) {
+            r = pipe_redo(lanes[l]);
+            if (r) return r;
+        }
+        r = run_sync(p.k);
+        for (; !r && count; count--, head = (head + 1) % (2 * kMaxLanes)) r = run_sync(ring[head].k);
+        count = 0;
+        prev = nullptr;
+        return r;
+    };
+    for (uint32_t k = 0; k < n; k++) {
+        dv_ctx *c = lane_of(k);
+        if (!pipelined(k)) {
+            while (count) {
+                const int r = settle();
+                if (r) return r;
+            }
+            const int r = run_sync(k);
+            if (r) return r;
+            prev = nullptr;
+            continue;
+        }
+        while (count >= window) {
+            const int r = settle();
+            if (r) return r;
+        }
+        const uint32_t l = k % n_lanes;
+        const int slot = (int)(lane_slot[l]++ & 1u);
+        Pend &p = ring[(head + count) % (2 * kMaxLanes)];
+        p.k = k;
+        int r = run_prefix_epoch(c, &eps[k]);
+        if (!r && prev) {
+            r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
+            if (!r) launch_lane_gate(c->stream, prev->d_gate + prev_slot, c->ctr);
+        }
+        if (!r) {
+            enqueue_exec(c, commit_of(k));
+            r = hip_fail(hipGetLastError(), "execution launch");
+        }
+        if (!r) {
+            EpochSnap &sn = p.sn;
+            sn.n_acc = c->n_acc;
+            sn.n_txn = c->n_txn;
+            sn.rounds = c->rounds;
+            sn.rounds_real = c->rounds_real;
+            sn.rounds_prefix = c->rounds_prefix;
+            sn.async_launched = c->async_launched;
+            sn.sort_passes = c->sort_passes;
+            sn.prefix_txn = c->pf_K;
+            sn.n_acc_is_bound = c->n_acc_is_bound;
+            sn.async_unconfirmed = c->async_unconfirmed;
+            sn.slot = slot;
+            sn.seq = mirror_out(c, slot, true);
+            r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
+        }
+        c->phase = 0;
+        c->prefix_mode = false;
+        if (r) {
+            drain();
+            while (count) {  // (the read-backs, for the statistics; the error is returned either way)
+                bool halted = false;
+                (void)pipe_complete(lane_of(ring[head].k), ring[head].sn, stats_of(ring[head].k), &halted);
+                head = (head + 1) % (2 * kMaxLanes);
+                count--;
+            }
+            return r;
+        }
+        count++;
+        prev = c;
+        prev_slot = slot;
+    }
+    while (count) {
+        const int r = settle();
+        if (r) return r;
+    }
+    return DV_OK;
 }
 
 }  // extern "C"

@@ -187,9 +187,27 @@ class CCEngine:
         L.check(L.lib().dv_open(ctypes.byref(self._ctx), ctypes.byref(cfg)), "dv_open")
 
     def close(self):
+        for lane in getattr(self, "_lanes", []):  # (a lane closes before its owner)
+            lane.close()
+        self._lanes = []
         if self._ctx:
             L.lib().dv_close(self._ctx)
             self._ctx = ctypes.c_void_p()
+        self._owner = None
+
+    def open_lane(self):
+        """A decision lane (dv_open_lane): a second context of the same
+        configuration over this engine's tables (loaded first; frozen while
+        lanes are open).  Closed with, or before, this engine."""
+        lane = CCEngine.__new__(CCEngine)
+        lane.__dict__.update({k: v for k, v in self.__dict__.items() if k not in ("_ctx", "_lanes", "_ev", "_ext")})
+        lane._ctx = ctypes.c_void_p()
+        L.check(L.lib().dv_open_lane(self._ctx, ctypes.byref(lane._ctx)), "dv_open_lane")
+        lane._owner, lane._lanes = self, []
+        if not hasattr(self, "_lanes"):
+            self._lanes = []
+        self._lanes.append(lane)
+        return lane
 
     def __del__(self):
         try:
@@ -348,6 +366,23 @@ class CCEngine:
         cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
         sts = (L.Stats * n)()
         L.check(L.lib().dv_epoch_run_device_batch(self._ctx, arr, n, cps, sts), "dv_epoch_run_device_batch")
+        return list(sts)
+
+    def run_epochs_lanes(self, lanes, deps, d_commits=None):
+        """dv_epoch_run_device_lanes over [self] + lanes (open_lane):
+        epoch k decided on context k % len, executions in epoch order; same
+        results as run_epochs_device.  Returns the list of stats."""
+        ctxs = [self] + list(lanes)
+        for e in ctxs:
+            e._after_torch()
+        n = len(deps)
+        arr = (L.EpochDev * n)(*[d.desc() for d in deps])
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n
+        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        sts = (L.Stats * n)()
+        lp = (ctypes.c_void_p * len(ctxs))(*[e._ctx.value for e in ctxs])
+        L.check(L.lib().dv_epoch_run_device_lanes(lp, len(ctxs), arr, n, cps, sts), "dv_epoch_run_device_lanes")
         return list(sts)
 
     # ---- partitioned epochs over RCCL from the engine (dv_comm_init)

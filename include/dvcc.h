@@ -372,6 +372,28 @@ int dv_comm_set_mode(dv_ctx *ctx, int mode);
 int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, uint8_t *const *d_commits,
                               dv_stats *sts);
 
+/* Decision lanes.  dv_open_lane: a second context (same dv_config, its own
+ * stream and workspace) that runs epochs against `owner`'s tables -- no
+ * copy; the owner's tables are loaded first and are frozen (dv_create_table /
+ * dv_load_* return DV_ERR_STATE) while it has lanes open; close the lanes
+ * before the owner.  Single-GPU YCSB contexts without a communicator only.
+ * The reference's analogue is its pool of worker threads deciding txns of
+ * the same tables concurrently (worker_thread.cpp:119-180); here the unit is
+ * a whole epoch. */
+int dv_open_lane(dv_ctx *owner, dv_ctx **lane);
+
+/* n epochs over n_lanes (1 or 2) contexts -- an owner and its lane: epoch k
+ * is decided on lanes[k % n_lanes], so one epoch's decision (latency-bound
+ * rounds) overlaps the next epoch's, while executions run strictly in epoch
+ * order (epoch k's waits on epoch k-1's, across the lanes' streams, and is
+ * skipped when k-1 halted or failed).  Each lane runs on a stream of its own
+ * masked to half of the CUs (ordered after the context's stream at the start
+ * of the call, and the context's stream after it at the end).  The same
+ * results, commit bytes, statistics and error behaviour as
+ * dv_epoch_run_device_batch on one context; n_lanes == 1 is exactly that. */
+int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
+                              uint8_t *const *d_commits, dv_stats *sts);
+
 /* The closed loop on the device (the reference's retry path,
  * WorkerThread::abort -> AbortQueue, worker_thread.cpp:160-172,
  * abort_queue.cpp:26-82, with a one-epoch penalty): n_epochs epochs of n_txn

@@ -711,21 +711,27 @@ def test_randomized_sweep(case):
     _check(cc, rows, [g.gen(n_txn, 77 + case), g.gen(n_txn, 78 + case)], **knobs)
 
 
-def _check_batch(cc, rows, epochs, prefix=None, max_iters=None):
-    """dv_epoch_run_device_batch against the oracle run over the same epochs
-    one after the other: every epoch's commit bytes, digest and write count,
-    and the table after the batch."""
+def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1):
+    """dv_epoch_run_device_batch (lanes > 1: dv_epoch_run_device_lanes over
+    the engine and lanes - 1 decision lanes) against the oracle run over the
+    same epochs one after the other: every epoch's commit bytes, digest and
+    write count, and the table after the batch."""
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     refs = [_oracle_epoch(cc, tab, f0, e) for e in epochs]
     eng = CCEngine(cc, max(e.n_txn for e in epochs), max(e.n_acc for e in epochs))
     eng.load_ycsb_partition(rows)
     eng.set_prefix(prefix)
-    if max_iters:
-        eng.set_async_limits(max_iters, 0)
+    extra = [eng.open_lane() for _ in range(lanes - 1)]
+    for e in [eng] + extra:
+        if max_iters:
+            e.set_async_limits(max_iters, 0)
     deps = [DeviceEpoch(e) for e in epochs]
     commits = [torch.zeros(max(1, e.n_txn), dtype=torch.uint8, device="cuda") for e in epochs]
-    sts = eng.run_epochs_device(deps, commits)
+    if lanes > 1:
+        sts = eng.run_epochs_lanes(extra, deps, commits)
+    else:
+        sts = eng.run_epochs_device(deps, commits)
     for k, (e, (c_ref, _, st_ref), st) in enumerate(zip(epochs, refs, sts)):
         c = commits[k].cpu().numpy()[:e.n_txn]
         assert (c == c_ref).all(), f"epoch {k}: {(c != c_ref).sum()} mismatches"
@@ -823,4 +829,92 @@ def test_batch_setup_error_after_pipelined_epochs(what):
     st = eng.run_epoch_device(DeviceEpoch(e2))
     assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
     assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,lanes", [(dvcc.NO_WAIT, 2), (dvcc.WAIT_DIE, 2), (dvcc.OCC, 2)])
+def test_lanes_pipelined_prefix_epochs(cc, lanes):
+    """Decision lanes: epochs decided on alternating contexts, executed in
+    epoch order -- commit bytes, read digests (reads see every earlier
+    epoch's writes) and the final table equal the sequential oracle's."""
+    rows = 1 << 18
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    _check_batch(cc, rows, [g.gen(20_000, 900 + k) for k in range(7)], prefix=512, lanes=lanes)
+
+
+@pytest.mark.gpu
+def test_lanes_mixed_and_halted_epochs():
+    """Lanes with a small epoch (run synchronously) in the middle and
+    asynchronous rounds forced to yield: a halted epoch and every epoch queued
+    behind it (on any lane) run again in order, results unchanged."""
+    rows = 1 << 18
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    sizes = [20_000, 20_000, 20_000, 1, 20_000, 20_000, 20_000, 20_000]
+    epochs = [g.gen(n, 1000 + k) for k, n in enumerate(sizes)]
+    _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, lanes=2)
+    sts = _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, max_iters=1, lanes=2)
+    assert sum(st.async_yields for st in sts) > 0, "no asynchronous launch yielded"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad", [1, 2])
+def test_lanes_error_stops_before_execution(bad):
+    """A missing key in epoch `bad` (either lane): the call returns the error,
+    the epochs before it are applied, nothing of it or the epochs queued
+    behind it on the other lane is."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    epochs = [g.gen(8_000, 1100 + k) for k in range(5)]
+    epochs[bad].keys[17] = np.uint64(rows + 3)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    for e in epochs[:bad]:
+        _oracle_epoch(dvcc.NO_WAIT, tab, f0, e)
+    eng = CCEngine(dvcc.NO_WAIT, 8_000, max(e.n_acc for e in epochs))
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(256)
+    lane = eng.open_lane()
+    with pytest.raises(dvcc.DvccError) as ei:
+        eng.run_epochs_lanes([lane], [DeviceEpoch(e) for e in epochs])
+    assert ei.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    assert (eng.read_table(0, rows) == f0).all()
+    # both contexts run epochs again afterwards
+    e2 = g.gen(8_000, 1200)
+    _, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e2)
+    st = lane.run_epoch_device(DeviceEpoch(e2))
+    assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_lane_tables_frozen_and_shared():
+    """A lane sees the owner's tables (no copy) and the owner's tables cannot
+    be reloaded while it is open; lanes of a different owner are refused."""
+    from dvcc import _lib as L
+    rows = 1 << 12
+    eng = CCEngine(dvcc.NO_WAIT, 1024, 16_384)
+    with pytest.raises(dvcc.DvccError):
+        eng.open_lane()  # (no tables yet)
+    eng.load_ycsb_partition(rows)
+    lane = eng.open_lane()
+    assert (lane.read_table(0, rows) == eng.read_table(0, rows)).all()
+    with pytest.raises(dvcc.DvccError) as ei:
+        eng.load_ycsb_partition(rows)
+    assert ei.value.code == L.DV_ERR_STATE
+    other = CCEngine(dvcc.NO_WAIT, 1024, 16_384)
+    other.load_ycsb_partition(rows)
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    with pytest.raises(dvcc.DvccError) as ei:
+        eng.run_epochs_lanes([other], [DeviceEpoch(g.gen(100, 1))])
+    assert ei.value.code == L.DV_ERR_ARG
+    lane2 = eng.open_lane()
+    with pytest.raises(dvcc.DvccError) as ei:  # (two lanes at most)
+        eng.run_epochs_lanes([lane, lane2], [DeviceEpoch(g.gen(100, 1))])
+    assert ei.value.code == L.DV_ERR_ARG
+    lane2.close()
+    other.close()
+    lane.close()
+    eng.load_ycsb_partition(rows)  # (unfrozen once its lanes are closed)
     eng.close()
