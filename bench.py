@@ -225,6 +225,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
                "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
         for cc_name in cc_names:
             eng = T.TpccEngine(cc_name, p, n_txn, seed=1, lsd_sort=a.lsd_sort)
+            lanes = [eng.open_lane() for _ in range(max(1, a.lanes) - 1)]  # decision lanes, as config D
             dev = [T.device_epoch(e) for e in eps]
             d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
             d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
@@ -232,7 +233,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
 
             def batch(m):  # the pipelined entry point (epoch k+1 queued before k is read back)
                 return eng.run_tpcc_epochs_device([dev[i % 2][0] for i in range(m)],
-                                                  [dev[i % 2][1] for i in range(m)], d_commit, d_oid)
+                                                  [dev[i % 2][1] for i in range(m)], d_commit, d_oid, lanes=lanes)
             if a.warmup:
                 batch(a.warmup)
             torch.cuda.synchronize()
@@ -244,7 +245,8 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
             byts = sum(tpcc_bytes_per_txn(eps[i % 2]) for i in range(k))
             res[cc_name] = {"committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el,
                             "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_txn),
-                            "epochs": k, "epoch_roofline": {"achieved_GBps": byts / el / 1e9,
+                            "epochs": k, "decision_lanes": 1 + len(lanes),
+                            "epoch_roofline": {"achieved_GBps": byts / el / 1e9,
                                                             "frac": byts / el / 1e9 / HBM_PEAK_GBPS}}
             eng.close()
         if si == 0 and not a.no_cpu_baseline:

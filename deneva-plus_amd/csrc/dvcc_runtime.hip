@@ -736,7 +736,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
 int dv_open_lane(dv_ctx *owner, dv_ctx **out) {
     if (!owner || !out) return DV_ERR_ARG;
     *out = nullptr;
-    if (owner->table_owner || owner->comm || owner->cfg.workload != DV_YCSB) return DV_ERR_ARG;
+    if (owner->table_owner || owner->comm) return DV_ERR_ARG;
     if (owner->phase != 0) return DV_ERR_STATE;
     if (!ctx_has_tables(owner)) return DV_ERR_NO_TABLE;
     dv_ctx *c = nullptr;
@@ -2157,32 +2157,35 @@ int dv_tpcc_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, const uin
         });
 }
 
-// Decision lanes: epoch k is decided on lanes[k % n_lanes] (each lane its own
-// stream and workspace), so one lane's rounds overlap another's; executions
-// stay in epoch order -- epoch k's waits for epoch k-1's (an event across the
-// lanes' streams) and starts halted when k-1 halted or failed (its gate word,
-// k_ctr_out / k_lane_gate).  The host reads epochs back oldest first; a halted
-// one is run again with every epoch queued behind it, synchronously and in
-// order, as dv_epoch_run_device_batch does on one stream.
-int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
-                              uint8_t *const *d_commits, dv_stats *sts) {
-    if (!lanes || n_lanes == 0 || n_lanes > kMaxLanes || (n && !eps)) return DV_ERR_ARG;
+}  // extern "C"
+
+namespace {
+
+// the lanes of one call: non-null, distinct, one owner's tables, one device,
+// one CC algorithm and workload
+int check_lanes(dv_ctx *const *lanes, uint32_t n_lanes) {
+    if (!lanes || n_lanes == 0 || n_lanes > kMaxLanes) return DV_ERR_ARG;
     dv_ctx *const c0 = lanes[0];
     for (uint32_t l = 0; l < n_lanes; l++) {
         dv_ctx *c = lanes[l];
         if (!c) return DV_ERR_ARG;
         if (c->phase != 0) return DV_ERR_STATE;
-        // every lane runs against the same tables: lanes of lanes[0] (or of its owner)
         const dv_ctx *own = c->table_owner ? c->table_owner : c;
         const dv_ctx *own0 = c0->table_owner ? c0->table_owner : c0;
-        if (own != own0 || c->cfg.device != c0->cfg.device || c->cfg.cc_alg != c0->cfg.cc_alg) return DV_ERR_ARG;
+        if (own != own0 || c->cfg.device != c0->cfg.device || c->cfg.cc_alg != c0->cfg.cc_alg ||
+            c->cfg.workload != c0->cfg.workload)
+            return DV_ERR_ARG;
         for (uint32_t m = 0; m < l; m++)
             if (lanes[m] == c) return DV_ERR_ARG;
     }
-    if (n_lanes == 1) return dv_epoch_run_device_batch(c0, eps, n, d_commits, sts);
-    HIPCHK(hipSetDevice(c0->cfg.device));
+    return DV_OK;
+}
+
+// each lane's CU-masked stream (lane l of n: the CUs i with i % n == l) and
+// its asynchronous launch's workgroups on that share
+int lane_streams(dv_ctx *const *lanes, uint32_t n_lanes) {
     int cus = 0;
-    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c0->cfg.device));
+    HIPCHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, lanes[0]->cfg.device));
     for (uint32_t l = 0; l < n_lanes; l++) {
         dv_ctx *c = lanes[l];
         if (c->lane_stream && c->lane_n == n_lanes && c->lane_l == l) continue;
@@ -2197,39 +2200,54 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         c->lane_l = l;
         c->lane_g = (uint32_t)((uint64_t)c->async_g * mine / (uint32_t)cus);
     }
-    // while the call runs each lane works on its masked stream, ordered after
-    // the caller's stream at the start, and the caller's after it at the end
-    struct OnLaneStreams {
-        dv_ctx *const *ls;
-        uint32_t n;
-        hipStream_t saved[kMaxLanes];
-        uint32_t saved_g[kMaxLanes];
-        OnLaneStreams(dv_ctx *const *l, uint32_t m) : ls(l), n(m) {
-            for (uint32_t i = 0; i < n; i++) {
-                saved[i] = ls[i]->stream;
-                saved_g[i] = ls[i]->async_g;
-                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
-                (void)hipStreamWaitEvent(ls[i]->lane_stream, ls[i]->lane_ev, 0);
-                ls[i]->stream = ls[i]->lane_stream;
-                ls[i]->async_g = ls[i]->lane_g;
-            }
+    return DV_OK;
+}
+
+// while a lanes call runs each lane works on its masked stream, ordered after
+// the caller's stream at the start, and the caller's after it at the end
+struct OnLaneStreams {
+    dv_ctx *const *ls;
+    uint32_t n;
+    hipStream_t saved[kMaxLanes];
+    uint32_t saved_g[kMaxLanes];
+    OnLaneStreams(dv_ctx *const *l, uint32_t m) : ls(l), n(m) {
+        for (uint32_t i = 0; i < n; i++) {
+            saved[i] = ls[i]->stream;
+            saved_g[i] = ls[i]->async_g;
+            (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+            (void)hipStreamWaitEvent(ls[i]->lane_stream, ls[i]->lane_ev, 0);
+            ls[i]->stream = ls[i]->lane_stream;
+            ls[i]->async_g = ls[i]->lane_g;
         }
-        ~OnLaneStreams() {
-            for (uint32_t i = 0; i < n; i++) {
-                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
-                (void)hipStreamWaitEvent(saved[i], ls[i]->lane_ev, 0);
-                ls[i]->stream = saved[i];
-                ls[i]->async_g = saved_g[i];
-            }
+    }
+    ~OnLaneStreams() {
+        for (uint32_t i = 0; i < n; i++) {
+            (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+            (void)hipStreamWaitEvent(saved[i], ls[i]->lane_ev, 0);
+            ls[i]->stream = saved[i];
+            ls[i]->async_g = saved_g[i];
         }
-    } on_lanes_(lanes, n_lanes);
-    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    }
+};
+
+// Decision lanes: epoch k is decided on lanes[k % n_lanes] (each lane its own
+// stream and workspace), so one lane's rounds overlap another's; executions
+// stay in epoch order -- epoch k's waits for epoch k-1's (an event across the
+// lanes' streams) and starts halted when k-1 halted or failed (its gate word,
+// k_ctr_out / k_lane_gate).  The host reads epochs back oldest first; a halted
+// one is run again with every epoch queued behind it, synchronously and in
+// order, as run_batch does on one stream.  pipelined(k): epoch k can be
+// queued that way; decide(c, k): queues its decision on lane c (up to the
+// execution); run(k, st): runs it synchronously on its lane.
+template <class Commit, class Pipelined, class Decide, class Run>
+int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts, Commit &&commit_of,
+              Pipelined &&pipelined, Decide &&decide, Run &&run) {
+    HIPCHK(hipSetDevice(lanes[0]->cfg.device));
+    int r0 = lane_streams(lanes, n_lanes);
+    if (r0) return r0;
+    OnLaneStreams on_lanes_(lanes, n_lanes);
     auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
     auto lane_of = [&](uint32_t k) { return lanes[k % n_lanes]; };
-    auto pipelined = [&](uint32_t k) {
-        dv_ctx *c = lane_of(k);
-        return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P && !c->comm;
-    };
     struct Pend {
         uint32_t k;
         EpochSnap sn;
@@ -2245,7 +2263,7 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
     auto drain = [&] {
         for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
     };
-    auto run_sync = [&](uint32_t k) { return dv_epoch_run_device(lane_of(k), &eps[k], commit_of(k), nullptr, stats_of(k)); };
+    auto run_sync = [&](uint32_t k) { return run(k, stats_of(k)); };
     // read back the oldest queued epoch; a halted one and all behind it run again
     auto settle = [&]() -> int {
         Pend &p = ring[head];
@@ -2289,7 +2307,7 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         const int slot = (int)(lane_slot[l]++ & 1u);
         Pend &p = ring[(head + count) % (2 * kMaxLanes)];
         p.k = k;
-        int r = run_prefix_epoch(c, &eps[k]);
+        int r = decide(c, k);
         if (!r && prev) {
             r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
             if (!r) launch_lane_gate(c->stream, prev->d_gate + prev_slot, c->ctr);
@@ -2316,6 +2334,7 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         }
         c->phase = 0;
         c->prefix_mode = false;
+        c->tp_args = c->tp_oid = nullptr;
         if (r) {
             drain();
             while (count) {  // (the read-backs, for the statistics; the error is returned either way)
@@ -2335,6 +2354,56 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         if (r) return r;
     }
     return DV_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
+                              uint8_t *const *d_commits, dv_stats *sts) {
+    int r = check_lanes(lanes, n_lanes);
+    if (r) return r;
+    if (n && !eps) return DV_ERR_ARG;
+    if (lanes[0]->cfg.workload != DV_YCSB) return DV_ERR_ARG;
+    if (n_lanes == 1) return dv_epoch_run_device_batch(lanes[0], eps, n, d_commits, sts);
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    return run_lanes(
+        lanes, n_lanes, n, sts, commit_of,
+        [&](uint32_t k) {
+            dv_ctx *c = lanes[k % n_lanes];
+            return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P && !c->comm;
+        },
+        [&](dv_ctx *c, uint32_t k) { return run_prefix_epoch(c, &eps[k]); },
+        [&](uint32_t k, dv_stats *st) {
+            return dv_epoch_run_device(lanes[k % n_lanes], &eps[k], commit_of(k), nullptr, st);
+        });
+}
+
+int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps,
+                                   const uint64_t *const *d_args, uint32_t n, uint8_t *const *d_commits,
+                                   uint64_t *const *d_oids, dv_stats *sts) {
+    int r = check_lanes(lanes, n_lanes);
+    if (r) return r;
+    if (n && (!eps || !d_args)) return DV_ERR_ARG;
+    if (lanes[0]->cfg.workload != DV_TPCC) return DV_ERR_ARG;
+    if (n_lanes == 1) return dv_tpcc_epoch_run_device_batch(lanes[0], eps, d_args, n, d_commits, d_oids, sts);
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    auto oid_of = [&](uint32_t k) { return d_oids ? d_oids[k] : nullptr; };
+    return run_lanes(
+        lanes, n_lanes, n, sts, commit_of,
+        [&](uint32_t k) {
+            dv_ctx *c = lanes[k % n_lanes];
+            return !timing(c) && !ktiming(c) && !c->comm;
+        },
+        [&](dv_ctx *c, uint32_t k) {
+            int rr = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
+            if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
+            return rr;
+        },
+        [&](uint32_t k, dv_stats *st) {
+            return dv_tpcc_epoch_run_device(lanes[k % n_lanes], &eps[k], d_args[k], commit_of(k), oid_of(k), st);
+        });
 }
 
 }  // extern "C"

@@ -199,7 +199,7 @@ class CCEngine:
         """A decision lane (dv_open_lane): a second context of the same
         configuration over this engine's tables (loaded first; frozen while
         lanes are open).  Closed with, or before, this engine."""
-        lane = CCEngine.__new__(CCEngine)
+        lane = type(self).__new__(type(self))
         lane.__dict__.update({k: v for k, v in self.__dict__.items() if k not in ("_ctx", "_lanes", "_ev", "_ext")})
         lane._ctx = ctypes.c_void_p()
         L.check(L.lib().dv_open_lane(self._ctx, ctypes.byref(lane._ctx)), "dv_open_lane")

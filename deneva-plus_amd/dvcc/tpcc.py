@@ -98,13 +98,16 @@ class TpccEngine(CCEngine):
         return st
 
 
-    def run_tpcc_epochs_device(self, deps, d_args, d_commits=None, d_oids=None):
+    def run_tpcc_epochs_device(self, deps, d_args, d_commits=None, d_oids=None, lanes=None):
         """Several TPC-C epochs back to back (dv_tpcc_epoch_run_device_batch):
         epoch k+1 is queued before epoch k is read back.  deps / d_args: one
         DeviceEpoch and operation-word tensor per epoch; d_commits / d_oids:
-        one device tensor per epoch, one tensor for all, or None.  Returns
-        the list of stats."""
-        self._after_torch()
+        one device tensor per epoch, one tensor for all, or None.  lanes:
+        decision lanes (open_lane) -- dv_tpcc_epoch_run_device_lanes over
+        [self] + lanes.  Returns the list of stats."""
+        ctxs = [self] + list(lanes or [])
+        for e in ctxs:
+            e._after_torch()
         n = len(deps)
 
         def ptrs(x):
@@ -116,8 +119,13 @@ class TpccEngine(CCEngine):
         args = ptrs(list(d_args))
         sts = (L.Stats * n)()
         self._keep = (deps, d_args, d_commits, d_oids)
-        L.check(L.lib().dv_tpcc_epoch_run_device_batch(self._ctx, descs, args, n, ptrs(d_commits), ptrs(d_oids),
-                                                       sts), "dv_tpcc_epoch_run_device_batch")
+        if len(ctxs) > 1:
+            lp = (ctypes.c_void_p * len(ctxs))(*[e._ctx.value for e in ctxs])
+            L.check(L.lib().dv_tpcc_epoch_run_device_lanes(lp, len(ctxs), descs, args, n, ptrs(d_commits),
+                                                           ptrs(d_oids), sts), "dv_tpcc_epoch_run_device_lanes")
+        else:
+            L.check(L.lib().dv_tpcc_epoch_run_device_batch(self._ctx, descs, args, n, ptrs(d_commits),
+                                                           ptrs(d_oids), sts), "dv_tpcc_epoch_run_device_batch")
         return list(sts)
 
     def run_tpcc_epoch_part(self, home, d_args, d_owner, txns_per_rank, d_commit, d_oid=None):

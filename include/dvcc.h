@@ -375,8 +375,8 @@ int dv_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, uint32_t n, 
 /* Decision lanes.  dv_open_lane: a second context (same dv_config, its own
  * stream and workspace) that runs epochs against `owner`'s tables -- no
  * copy; the owner's tables are loaded first and are frozen (dv_create_table /
- * dv_load_* return DV_ERR_STATE) while it has lanes open; close the lanes
- * before the owner.  Single-GPU YCSB contexts without a communicator only.
+ * dv_load_* / dv_tpcc_load return DV_ERR_STATE) while it has lanes open; close
+ * the lanes before the owner.  Contexts without a communicator only.
  * The reference's analogue is its pool of worker threads deciding txns of
  * the same tables concurrently (worker_thread.cpp:119-180); here the unit is
  * a whole epoch. */
@@ -618,6 +618,14 @@ int dv_tpcc_epoch_run_device(dv_ctx *ctx, const dv_epoch_dev *ep, const uint64_t
 int dv_tpcc_epoch_run_device_batch(dv_ctx *ctx, const dv_epoch_dev *eps, const uint64_t *const *d_args,
                                    uint32_t n, uint8_t *const *d_commits, uint64_t *const *d_oids,
                                    dv_stats *sts);
+
+/* TPC-C epochs over decision lanes (dv_open_lane on a DV_TPCC context), as
+ * dv_epoch_run_device_lanes: epoch k decided on lanes[k % n_lanes], executions
+ * -- the table updates and each NewOrder's o_id -- in epoch order.  The same
+ * results as dv_tpcc_epoch_run_device_batch; n_lanes == 1 is exactly that. */
+int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps,
+                                   const uint64_t *const *d_args, uint32_t n, uint8_t *const *d_commits,
+                                   uint64_t *const *d_oids, dv_stats *sts);
 /* the same from host buffers (H2D + run + D2H; records as dv_epoch_run);
  * out_oid (may be NULL): n_txn words */
 int dv_tpcc_epoch_run(dv_ctx *ctx, const dv_access *acc, uint64_t n_acc, const uint32_t *txn_begin,

@@ -86,21 +86,24 @@ def test_tpcc_epochs_accumulate(cc):
 
 
 @pytest.mark.parametrize("cc", CCS)
-@pytest.mark.parametrize("kind,n_txn,epochs", [("small", 2048, 5), ("e", 10_000, 3)])
-def test_tpcc_batch_pipelined(cc, kind, n_txn, epochs):
+@pytest.mark.parametrize("kind,n_txn,epochs,lanes", [("small", 2048, 5, 1), ("e", 10_000, 3, 1),
+                                                     ("small", 2048, 7, 2), ("e", 10_000, 5, 2)])
+def test_tpcc_batch_pipelined(cc, kind, n_txn, epochs, lanes):
     """dv_tpcc_epoch_run_device_batch (epoch k+1 queued before k is read
-    back) against the oracle running the epochs one after the other: commit
-    bytes, o_id, stats of every epoch and every table after the batch."""
+    back; lanes 2: dv_tpcc_epoch_run_device_lanes, epochs decided alternately
+    on two contexts) against the oracle running the epochs one after the
+    other: commit bytes, o_id, stats of every epoch and every table after."""
     po, pp = _params(kind, num_wh=2) if kind == "small" else _params(kind)
     db = O.TpccDB(po, 9)
     eng = T.TpccEngine(cc, pp, n_txn, seed=9)
+    extra = [eng.open_lane() for _ in range(lanes - 1)]
     try:
         es = [T.gen(pp, n_txn, 300 + k) for k in range(epochs)]
         refs = [db.epoch(ORACLE_CC[cc], e.keys, e.types, e.tables, e.args, e.txn_begin) for e in es]
         devs = [T.device_epoch(e) for e in es]
         commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in es]
         oids = [torch.zeros(n_txn, dtype=torch.int64, device="cuda") for _ in es]
-        sts = eng.run_tpcc_epochs_device([d for d, _ in devs], [a for _, a in devs], commits, oids)
+        sts = eng.run_tpcc_epochs_device([d for d, _ in devs], [a for _, a in devs], commits, oids, lanes=extra)
         for k, (e, (c_ref, o_ref, st_ref), st) in enumerate(zip(es, refs, sts)):
             c = commits[k].cpu().numpy()
             o = oids[k].cpu().numpy().view(np.uint64)
@@ -112,21 +115,24 @@ def test_tpcc_batch_pipelined(cc, kind, n_txn, epochs):
         eng.close()
 
 
-def test_tpcc_batch_halted_epochs_rerun():
-    """Asynchronous rounds forced to yield in a pipelined TPC-C batch: the
-    halted epoch and the one queued behind it run again synchronously,
-    results unchanged."""
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_tpcc_batch_halted_epochs_rerun(lanes):
+    """Asynchronous rounds forced to yield in a pipelined TPC-C batch (or over
+    two decision lanes): the halted epoch and the ones queued behind it run
+    again synchronously, results unchanged."""
     po, pp = _params("small", num_wh=2)
     db = O.TpccDB(po, 9)
     eng = T.TpccEngine(dvcc.WAIT_DIE, pp, 2048, seed=9)
-    eng.set_async_limits(1, 0)
+    extra = [eng.open_lane() for _ in range(lanes - 1)]
+    for e in [eng] + extra:
+        e.set_async_limits(1, 0)
     try:
         es = [T.gen(pp, 2048, 400 + k) for k in range(4)]
         refs = [db.epoch(O.WAIT_DIE, e.keys, e.types, e.tables, e.args, e.txn_begin) for e in es]
         devs = [T.device_epoch(e) for e in es]
         commits = [torch.zeros(2048, dtype=torch.uint8, device="cuda") for _ in es]
         oids = [torch.zeros(2048, dtype=torch.int64, device="cuda") for _ in es]
-        sts = eng.run_tpcc_epochs_device([d for d, _ in devs], [a for _, a in devs], commits, oids)
+        sts = eng.run_tpcc_epochs_device([d for d, _ in devs], [a for _, a in devs], commits, oids, lanes=extra)
         assert sum(st.async_yields for st in sts) > 0, "no asynchronous launch yielded"
         for k, (c_ref, o_ref, _) in enumerate(refs):
             assert (commits[k].cpu().numpy() == c_ref).all(), k
