@@ -23,7 +23,7 @@ eng.load_ycsb_partition(rows)
 deps = [DeviceEpoch(e) for e in host]
 d = torch.zeros(n, dtype=torch.uint8, device="cuda")
 lanes = [eng.open_lane()]
-for L in (1, 2, 1, 2, 1, 2):
+for L in (1, 2) if len(sys.argv) > 3 else (1, 2, 1, 2, 1, 2):
     run = lambda k: eng.run_epochs_lanes(lanes[:L - 1], [deps[i % 4] for i in range(k)], d)
     run(4)
     torch.cuda.synchronize()
