@@ -86,7 +86,7 @@ def parse():
                     help="N>1 ranks sharing fewer GPUs (a rehearsal of the N>1 path on a one-GPU box): torch "
                          "collectives over gloo, the engine's over dv_comm_init_ipc (a test transport); the "
                          "numbers are no scaling result")
-    ap.add_argument("--lanes", type=int, default=2,
+    ap.add_argument("--lanes", type=int, default=4,
                     help="one GPU: decision lanes (dv_epoch_run_device_lanes) -- epochs decided on this many "
                          "contexts in turn, executions in epoch order; 1 = dv_epoch_run_device_batch")
     ap.add_argument("--lsd-sort", action="store_true",

@@ -833,7 +833,8 @@ def test_batch_setup_error_after_pipelined_epochs(what):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("cc,lanes", [(dvcc.NO_WAIT, 2), (dvcc.WAIT_DIE, 2), (dvcc.OCC, 2)])
+@pytest.mark.parametrize("cc,lanes", [(dvcc.NO_WAIT, 2), (dvcc.WAIT_DIE, 2), (dvcc.OCC, 2), (dvcc.NO_WAIT, 4),
+                                      (dvcc.OCC, 3), (dvcc.WAIT_DIE, 8)])
 def test_lanes_pipelined_prefix_epochs(cc, lanes):
     """Decision lanes: epochs decided on alternating contexts, executed in
     epoch order -- commit bytes, read digests (reads see every earlier
@@ -850,15 +851,15 @@ def test_lanes_mixed_and_halted_epochs():
     behind it (on any lane) run again in order, results unchanged."""
     rows = 1 << 18
     g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
-    sizes = [20_000, 20_000, 20_000, 1, 20_000, 20_000, 20_000, 20_000]
+    sizes = [20_000, 20_000, 20_000, 1, 20_000, 20_000, 20_000, 20_000, 20_000, 20_000]
     epochs = [g.gen(n, 1000 + k) for k, n in enumerate(sizes)]
-    _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, lanes=2)
-    sts = _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, max_iters=1, lanes=2)
+    _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, lanes=4)
+    sts = _check_batch(dvcc.NO_WAIT, rows, epochs, prefix=512, max_iters=1, lanes=4)
     assert sum(st.async_yields for st in sts) > 0, "no asynchronous launch yielded"
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("bad", [1, 2])
+@pytest.mark.parametrize("bad", [1, 2, 3])
 def test_lanes_error_stops_before_execution(bad):
     """A missing key in epoch `bad` (either lane): the call returns the error,
     the epochs before it are applied, nothing of it or the epochs queued
@@ -875,8 +876,9 @@ def test_lanes_error_stops_before_execution(bad):
     eng.load_ycsb_partition(rows)
     eng.set_prefix(256)
     lane = eng.open_lane()
+    more = [eng.open_lane() for _ in range(2)]
     with pytest.raises(dvcc.DvccError) as ei:
-        eng.run_epochs_lanes([lane], [DeviceEpoch(e) for e in epochs])
+        eng.run_epochs_lanes([lane] + more, [DeviceEpoch(e) for e in epochs])
     assert ei.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
     assert (eng.read_table(0, rows) == f0).all()
     # both contexts run epochs again afterwards
@@ -909,11 +911,15 @@ def test_lane_tables_frozen_and_shared():
     with pytest.raises(dvcc.DvccError) as ei:
         eng.run_epochs_lanes([other], [DeviceEpoch(g.gen(100, 1))])
     assert ei.value.code == L.DV_ERR_ARG
-    lane2 = eng.open_lane()
-    with pytest.raises(dvcc.DvccError) as ei:  # (two lanes at most)
-        eng.run_epochs_lanes([lane, lane2], [DeviceEpoch(g.gen(100, 1))])
+    more = [eng.open_lane() for _ in range(8)]
+    with pytest.raises(dvcc.DvccError) as ei:  # (eight lanes at most)
+        eng.run_epochs_lanes([lane] + more, [DeviceEpoch(g.gen(100, 1))])
     assert ei.value.code == L.DV_ERR_ARG
-    lane2.close()
+    with pytest.raises(dvcc.DvccError) as ei:  # (each context once)
+        eng.run_epochs_lanes([lane, lane], [DeviceEpoch(g.gen(100, 1))])
+    assert ei.value.code == L.DV_ERR_ARG
+    for m in more:
+        m.close()
     other.close()
     lane.close()
     eng.load_ycsb_partition(rows)  # (unfrozen once its lanes are closed)

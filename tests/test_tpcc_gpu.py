@@ -87,7 +87,7 @@ def test_tpcc_epochs_accumulate(cc):
 
 @pytest.mark.parametrize("cc", CCS)
 @pytest.mark.parametrize("kind,n_txn,epochs,lanes", [("small", 2048, 5, 1), ("e", 10_000, 3, 1),
-                                                     ("small", 2048, 7, 2), ("e", 10_000, 5, 2)])
+                                                     ("small", 2048, 7, 2), ("e", 10_000, 9, 4)])
 def test_tpcc_batch_pipelined(cc, kind, n_txn, epochs, lanes):
     """dv_tpcc_epoch_run_device_batch (epoch k+1 queued before k is read
     back; lanes 2: dv_tpcc_epoch_run_device_lanes, epochs decided alternately
@@ -115,7 +115,7 @@ def test_tpcc_batch_pipelined(cc, kind, n_txn, epochs, lanes):
         eng.close()
 
 
-@pytest.mark.parametrize("lanes", [1, 2])
+@pytest.mark.parametrize("lanes", [1, 2, 4])
 def test_tpcc_batch_halted_epochs_rerun(lanes):
     """Asynchronous rounds forced to yield in a pipelined TPC-C batch (or over
     two decision lanes): the halted epoch and the ones queued behind it run

@@ -22,8 +22,8 @@ if not own:
 eng.load_ycsb_partition(rows)
 deps = [DeviceEpoch(e) for e in host]
 d = torch.zeros(n, dtype=torch.uint8, device="cuda")
-lanes = [eng.open_lane()]
-for L in (1, 2) if len(sys.argv) > 3 else (1, 2, 1, 2, 1, 2):
+lanes = [eng.open_lane() for _ in range(int(os.environ.get('EXP_NLANES', '2')) - 1)]
+for L in (1, 2) if len(sys.argv) > 3 else tuple(int(x) for x in os.environ.get('EXP_LSEQ', '1,2,1,2,1,2').split(',')):
     run = lambda k: eng.run_epochs_lanes(lanes[:L - 1], [deps[i % 4] for i in range(k)], d)
     run(4)
     torch.cuda.synchronize()
