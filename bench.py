@@ -647,10 +647,28 @@ class PartitionedBench:
                                  part_id=rank, timing=TIMING[a.timing], lsd_sort=a.lsd_sort)
         self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
         self.eng.load_ycsb_partition(rows)
+        # epoch groups over ordered decision lanes (dv_lanes_order): L contexts
+        # over this partition's tables, each with its own communicator, group
+        # g decided on lane g % L, executions in group order
+        nl = max(1, a.lanes) if a.protocol == "group" and not a.no_pipeline else 1
+        self.lanes = [self.eng.open_lane() for _ in range(nl - 1)]
         engine_comm_init(a, self.eng, world, rank, "ycsb")
         self.eng.comm_set_mode(a.part_mode)
+        for ln, lane in enumerate(self.lanes):
+            engine_comm_init(a, lane, world, rank, f"ycsb_lane{ln + 1}")
+            lane.comm_set_mode(a.part_mode)
+        if self.lanes:
+            self.eng.lanes_order(self.lanes)
         self.rows = rows
         self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
+        self.d_commits = [self.d_commit] + [torch.zeros_like(self.d_commit) for _ in self.lanes]
+
+    def unorder(self):
+        """After the timed region: the engine alone on the bench's stream
+        again (the measurement legs and extras run one context)."""
+        if self.lanes:
+            self.eng.lanes_order([])
+            self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
 
     def epochs(self, n_txn_rank, mpr, theta, count):
         gen = dvcc.YCSBQueryGenerator(self.rows * self.world, part_cnt=self.world, req_per_query=self.R,
@@ -680,12 +698,17 @@ class PartitionedBench:
             return self.eng.run_epoch_group(groups[i % len(groups)], n_txn_rank, self.d_commit)
         return step
 
-    def group_batcher(self, groups, n_txn_rank):
+    def group_batcher(self, groups, n_txn_rank, lanes=True):
         """count consecutive groups in one dv_epoch_group_run_batch call (one
-        host wait between two groups)."""
+        host wait between two groups), or over the ordered lanes."""
         def batch(first, count):
-            return self.eng.run_epoch_groups([groups[(first + i) % len(groups)] for i in range(count)],
-                                             n_txn_rank, self.d_commit)
+            run = [groups[(first + i) % len(groups)] for i in range(count)]
+            if lanes and self.lanes:
+                nl = len(self.d_commits)
+                base = self.eng._order_next
+                return self.eng.run_epoch_groups_ordered(run, n_txn_rank,
+                                                         [self.d_commits[(base + i) % nl] for i in range(count)])
+            return self.eng.run_epoch_groups(run, n_txn_rank, self.d_commit)
         return batch
 
 
@@ -850,6 +873,7 @@ def main():
             groups = pb.groups(n_txn_rank, mpr, theta, n_epochs)
             step = pb.group_stepper(groups, n_txn_rank)
             batch = pb.group_batcher(groups, n_txn_rank)
+            batch1 = pb.group_batcher(groups, n_txn_rank, lanes=False)
         else:
             deps = pb.epochs(n_txn_rank, mpr, theta, n_epochs)
             step = pb.stepper(deps, n_txn_rank)
@@ -860,8 +884,10 @@ def main():
     pipelined = not a.no_pipeline and (not part or a.protocol == "group")
     stats, el = timed(step, 0, a.warmup, a.steps, world, batch if pipelined else None)
     # (the profiling legs time one context's launches: one lane)
+    if part:
+        pb.unorder()
     pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats,
-                                          (batch1 if not part else batch) if pipelined else None)
+                                          batch1 if pipelined else None)
     table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"
@@ -896,7 +922,7 @@ def main():
                           1: "list protocol (owner split, per-round verdict all-reduce)",
                           2: "replicated"}[a.part_mode] if part else "single GPU"),
             "distinct_epochs": n_epochs,
-            "decision_lanes": (max(1, a.lanes) if not part and not a.no_pipeline else 1),
+            "decision_lanes": 1 + (len(pb.lanes) if part else len(lanes)),
         },
         "roofline": roofline(table, len(pstats), a),
         "timing_in_timed_region": a.timing,

@@ -1659,6 +1659,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    reads first)
     ctx_table0_cols(c, &f0, &pkey);
     CHK(hip_fail2(hipMemsetAsync(m->xacc, 0, 2 * kSlots * sizeof(unsigned long long), s), "memset"));
+    // (ordered lanes: after the previous group's execution, dv_lanes_order)
+    CHK(lane_exec_begin(c, s));
     const bool fused = cfg.cc_alg == DV_NO_WAIT || cfg.cc_alg == DV_WAIT_DIE;
     const uint2 *recs = reinterpret_cast<const uint2 *>(m->recv);
     uint64_t off = 0;
@@ -1676,6 +1678,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         off += n;
     }
     CHK(hip_fail2(hipGetLastError(), "k_route_exec"));
+    lane_exec_end(c, s);
     if (st) {
         *st = est;  // this rank's decision: rounds, sort passes, timings
         st->n_txn = n_txn64 * P;
@@ -1704,7 +1707,9 @@ int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_ran
 int dv_epoch_group_run(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
                        uint8_t *d_commit, dv_stats *st) {
     KProfScope kps_(c);
-    return run_group(c, homes, n_homes, txns_per_rank, d_commit, st);
+    const int r = run_group(c, homes, n_homes, txns_per_rank, d_commit, st);
+    if (r && c) lane_fail(c);  // (ordered lanes waiting for this group's turn stop)
+    return r;
 }
 
 int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_groups, uint32_t n_homes,
@@ -1714,7 +1719,10 @@ int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_gr
     for (uint32_t g = 0; g < n_groups; g++) {
         const int r = run_group(c, homes ? homes + (size_t)g * n_homes : nullptr, n_homes, txns_per_rank,
                                 d_commits ? d_commits[g] : nullptr, st ? st + g : nullptr, &dfr, g + 1 < n_groups);
-        if (r) return r;  // (every rank of the communicator, at the same group)
+        if (r) {  // (every rank of the communicator, at the same group)
+            if (c) lane_fail(c);
+            return r;
+        }
     }
     return DV_OK;
 }

@@ -471,6 +471,15 @@ bool ctx_group_capable(dv_ctx *c, uint32_t nranks);
 void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey);  // table 0's local rows
 uint64_t ctx_table0_rows(dv_ctx *c);  // ... their count (buckets of its direct map)
 uint32_t *ctx_err_words(dv_ctx *c);  // &Counters::err (peer_err follows)
+// ordered lanes (dv_lanes_order): an execution of an epoch group on lane c
+// waits for its turn -- the previous group's execution, on whichever lane,
+// queued (host) and finished (its event, device) -- and hands the turn on
+// after it is queued; a lane whose group failed ends the order there (every
+// later group returns DV_ERR_STATE instead of waiting; earlier ones still
+// execute).  No-ops on a context without an order.
+int lane_exec_begin(dv_ctx *c, hipStream_t s);
+void lane_exec_end(dv_ctx *c, hipStream_t s);
+void lane_fail(dv_ctx *c);
 // the whole epoch on this rank, its own rows executed (dvcc_runtime.hip)
 // keys32: the epoch's keys as 32-bit row ids (ep->keys is then ignored)
 // route (epoch groups): committed accesses routed to their owners, nothing

@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -24,6 +27,19 @@
 using namespace dvcc;
 
 namespace {
+
+// dv_lanes_order: the execution order of epoch groups over several lanes,
+// shared by them (ticket k * n + l is lane l's k-th execution)
+struct LaneOrder {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t next = 0;             // the ticket whose execution may be queued now
+    hipEvent_t last = nullptr;     // recorded after the previous ticket's execution
+    uint64_t fail_at = ~0ull;      // a lane's group failed: this ticket never executes, nor any later one
+    uint32_t n = 0;
+};
+
+constexpr int kLaneWaitS = 120;  // lane_exec_begin's longest wait for its turn
 
 // dv_epoch_run_device_lanes: up to 8 lanes, each on its share of the CUs
 // (measured best: 4, gpurun_out r03_l8 / r03_hq)
@@ -93,6 +109,9 @@ struct dv_ctx {
     // 0.29 for two lanes, gpurun_out r03_w); lane_g: its workgroups on its share
     hipStream_t lane_stream = nullptr;
     uint32_t lane_n = 0, lane_l = 0, lane_g = 0;
+    // dv_lanes_order: this lane's place in the groups' execution order
+    std::shared_ptr<LaneOrder> order;
+    uint64_t order_k = 0;  // executions of this lane so far
 
     // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
     // execution scratch, and the operation words / o_id output of this epoch
@@ -551,6 +570,40 @@ void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey) {
     *pkey = c->pkey + c->tab[0].row_base;
 }
 uint32_t *ctx_err_words(dv_ctx *c) { return &c->ctr->err; }
+
+int lane_exec_begin(dv_ctx *c, hipStream_t s) {
+    if (!c->order) return DV_OK;
+    LaneOrder &o = *c->order;
+    const uint64_t t = c->order_k * o.n + c->lane_l;
+    std::unique_lock<std::mutex> lk(o.mu);
+    // (a lane never run for its turn -- groups not handed round the lanes in
+    // order -- ends the order after kLaneWaitS instead of hanging the caller)
+    if (!o.cv.wait_for(lk, std::chrono::seconds(kLaneWaitS), [&] { return t > o.fail_at || o.next == t; }))
+        o.fail_at = std::min(o.fail_at, o.next), o.cv.notify_all();
+    if (t > o.fail_at || o.next != t) return DV_ERR_STATE;
+    if (o.last) HIPCHK(hipStreamWaitEvent(s, o.last, 0));
+    return DV_OK;
+}
+
+void lane_exec_end(dv_ctx *c, hipStream_t s) {
+    if (!c->order) return;
+    LaneOrder &o = *c->order;
+    std::lock_guard<std::mutex> lk(o.mu);
+    if (hipEventRecord(c->lane_ev, s) != hipSuccess) o.fail_at = std::min(o.fail_at, o.next + 1);
+    o.last = c->lane_ev;
+    o.next++;
+    c->order_k++;
+    o.cv.notify_all();
+}
+
+void lane_fail(dv_ctx *c) {
+    if (!c->order) return;
+    LaneOrder &o = *c->order;
+    std::lock_guard<std::mutex> lk(o.mu);
+    const uint64_t t = c->order_k * o.n + c->lane_l;  // (the execution this lane did not reach)
+    o.fail_at = std::min(o.fail_at, t);
+    o.cv.notify_all();
+}
 
 extern "C" {
 
@@ -2380,6 +2433,36 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         [&](uint32_t k, dv_stats *st) {
             return dv_epoch_run_device(lanes[k % n_lanes], &eps[k], commit_of(k), nullptr, st);
         });
+}
+
+int dv_lanes_order(dv_ctx *const *lanes, uint32_t n_lanes) {
+    int r = check_lanes(lanes, n_lanes);
+    if (r) return r;
+    HIPCHK(hipSetDevice(lanes[0]->cfg.device));
+    for (uint32_t l = 0; l < n_lanes; l++) HIPCHK(hipStreamSynchronize(lanes[l]->stream));
+    if (n_lanes == 1) {  // (back on its own stream, no order)
+        dv_ctx *c = lanes[0];
+        if (c->order) {
+            c->stream = c->own_stream;
+            c->async_g = async_groups(c->cfg.device);
+            c->order.reset();
+        }
+        return DV_OK;
+    }
+    for (uint32_t l = 0; l < n_lanes; l++)
+        if (lanes[l]->order) return DV_ERR_STATE;  // (already ordered: dv_lanes_order(&lane, 1) first)
+    r = lane_streams(lanes, n_lanes);
+    if (r) return r;
+    auto o = std::make_shared<LaneOrder>();
+    o->n = n_lanes;
+    for (uint32_t l = 0; l < n_lanes; l++) {
+        dv_ctx *c = lanes[l];
+        c->stream = c->lane_stream;
+        c->async_g = c->lane_g;
+        c->order = o;
+        c->order_k = 0;
+    }
+    return DV_OK;
 }
 
 int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps,

@@ -368,6 +368,53 @@ class CCEngine:
         L.check(L.lib().dv_epoch_run_device_batch(self._ctx, arr, n, cps, sts), "dv_epoch_run_device_batch")
         return list(sts)
 
+    def lanes_order(self, lanes):
+        """dv_lanes_order over [self] + lanes: each on its own CU-masked
+        stream, and their epoch groups (run_epoch_group / run_epoch_groups,
+        each lane from its own host thread, group g on lane g % len) executed
+        in group order across them.  lanes=[]: this engine alone again."""
+        ctxs = [self] + list(lanes)
+        lp = (ctypes.c_void_p * len(ctxs))(*[e._ctx.value for e in ctxs])
+        L.check(L.lib().dv_lanes_order(lp, len(ctxs)), "dv_lanes_order")
+        self._order = ctxs if len(ctxs) > 1 else None
+        self._order_next = 0  # the lane of the next group (tickets continue across calls)
+
+    def run_epoch_groups_ordered(self, groups, txns_per_rank, d_commits=None):
+        """Epoch groups over the ordered lanes (lanes_order): group i of the
+        call on lane (groups so far + i) % L, every lane from its own host
+        thread (dv_epoch_group_run_batch over its groups), executions in
+        group order.  d_commits: one device tensor (or None) per group.
+        Returns the list of stats; raises the first lane's error."""
+        import threading
+        ctxs = self._order
+        n, nl = len(groups), len(ctxs)
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n
+        base = self._order_next
+        out, errs = [None] * n, []
+
+        def body(ln):
+            mine = [i for i in range(n) if (base + i) % nl == ln]
+            if not mine:
+                return
+            try:
+                sts = ctxs[ln].run_epoch_groups([groups[i] for i in mine], txns_per_rank,
+                                                [d_commits[i] for i in mine])
+                for i, st in zip(mine, sts):
+                    out[i] = st
+            except Exception as ex:  # noqa: BLE001 -- re-raised below
+                errs.append(ex)
+        th = [threading.Thread(target=body, args=(ln,)) for ln in range(nl)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        self._order_next = (base + n) % nl
+        if errs:  # (the failing group's own error first; the others stopped behind it)
+            errs.sort(key=lambda e: getattr(e, "code", 0) == L.DV_ERR_STATE)
+            raise errs[0]
+        return out
+
     def run_epochs_lanes(self, lanes, deps, d_commits=None):
         """dv_epoch_run_device_lanes over [self] + lanes (open_lane):
         epoch k decided on context k % len, executions in epoch order; same

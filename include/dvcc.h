@@ -396,6 +396,23 @@ int dv_open_lane(dv_ctx *owner, dv_ctx **lane);
 int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
                               uint8_t *const *d_commits, dv_stats *sts);
 
+/* Ordered lanes for epoch groups (dv_epoch_group_run / _batch, N > 1): an
+ * owner and its lanes (1..8; opened before dv_comm_init, each lane then
+ * given its OWN communicator) become one execution order -- each on a
+ * stream masked to its share of the CUs, driven from its own host thread;
+ * lane l runs groups l, l + n_lanes, ... (in every call: hand the groups
+ * round the lanes without gaps), decisions of different groups overlap, and
+ * a group's execution on this partition waits until the previous group's
+ * has been queued (host) and has finished (device).  A group that fails on
+ * one lane (every rank fails it, as without lanes) ends the order there: the
+ * groups before it execute, every later one returns DV_ERR_STATE; a turn
+ * not taken within 120 s also ends it.  n_lanes == 1: that context back on
+ * its own stream, unordered.  The epoch groups' results are those of one
+ * context running the groups in order.  The reference's analogue: its
+ * worker threads processing several txns' remote requests at once on one
+ * node while Calvin's sequencer fixes the order (sequencer.cpp:283-326). */
+int dv_lanes_order(dv_ctx *const *lanes, uint32_t n_lanes);
+
 /* The closed loop on the device (the reference's retry path,
  * WorkerThread::abort -> AbortQueue, worker_thread.cpp:160-172,
  * abort_queue.cpp:26-82, with a one-epoch penalty): n_epochs epochs of n_txn

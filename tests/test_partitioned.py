@@ -1070,3 +1070,114 @@ def test_epoch_group_retries(cc, world):
     assert carried_total > 0
     for eng in engines:
         eng.close()
+
+
+# ---- epoch groups over ordered lanes (dv_lanes_order): each rank runs L
+# contexts over its partition's tables, each with its own communicator and
+# host thread; group g is decided on lane g % L and the groups execute in
+# group order on every partition
+def _check_epoch_groups_lanes(cc, world, rows_pp, n_txn, mpr, groups, lanes, theta=0.9, bad_group=None):
+    import threading
+    R = 10
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
+    owners = []
+    for p in range(world):
+        eng = dvcc.CCEngine(cc, n_txn * world, n_txn * world * R + 4096, part_cnt=world, part_id=p,
+                            asynchronous=False)
+        eng.load_ycsb_partition(rows_pp)
+        owners.append(eng)
+    ctxs = [[o] + [o.open_lane() for _ in range(lanes - 1)] for o in owners]  # [rank][lane]
+    for ln in range(lanes):
+        dvcc.CCEngine.comm_init_local([ctxs[r][ln] for r in range(world)])
+        for r in range(world):
+            ctxs[r][ln].comm_set_mode(2)
+    for r in range(world):
+        ctxs[r][0].lanes_order(ctxs[r][1:])
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    homes = [[] for _ in range(world)]  # [rank][group][epoch]
+    refs = []                           # [group][epoch] (commit bytes, stats)
+    for g in range(groups):
+        hg = [[None] * world for _ in range(world)]
+        rg = []
+        for e in range(world):
+            batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 60 + g * world + e), r) for r in range(world)]
+            if bad_group == g and e == 1:
+                batches[0].keys[5] = np.uint64(rows_pp * world + 7)
+            q = dvcc.sequence(batches)
+            if bad_group is None or g < bad_group:
+                c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin,
+                                               q.keys, q.types)
+                rg.append((c_ref, st_ref))
+            for r in range(world):
+                hg[r][e] = dvcc.DeviceEpoch(batches[r])
+        for r in range(world):
+            homes[r].append(hg[r])
+        refs.append(rg)
+    out = {}
+
+    def body(r, ln):
+        mine = list(range(ln, groups, lanes))
+        try:
+            ds = [torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda") for _ in mine]
+            sts = ctxs[r][ln].run_epoch_groups([homes[r][g] for g in mine], n_txn, ds)
+            torch.cuda.synchronize()
+            for g, d, st in zip(mine, ds, sts):
+                out[(r, g)] = (d.cpu().numpy(), st)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank and lane
+            out[(r, "err", ln)] = ex
+    th = [threading.Thread(target=body, args=(r, ln)) for r in range(world) for ln in range(lanes)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a lane hung in the ordered epoch groups"
+    try:
+        if bad_group is not None:
+            errs = [v for k, v in out.items() if len(k) == 3]
+            assert errs and all(isinstance(x, dvcc.DvccError) for x in errs), out
+            # groups before the failing one are applied on every partition, nothing after them
+            for p, eng in enumerate(owners):
+                assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+            return
+        assert not [k for k in out if len(k) == 3], {k: v for k, v in out.items() if len(k) == 3}
+        for g in range(groups):
+            committed = sum(st.committed for _, st in refs[g])
+            digest = writes = 0
+            for r in range(world):
+                cs, st = out[(r, g)]
+                for e in range(world):
+                    assert (cs[e * n_txn:(e + 1) * n_txn] == refs[g][e][0][r * n_txn:(r + 1) * n_txn]).all(), \
+                        f"group {g} epoch {e} rank {r}"
+                assert st.committed == committed
+                digest = (digest + st.read_digest) % (1 << 64)
+                writes += st.write_cnt
+            assert digest == sum(st.read_digest for _, st in refs[g]) % (1 << 64), f"group {g} digest"
+            assert writes == sum(st.write_cnt for _, st in refs[g]), f"group {g} writes"
+        for p, eng in enumerate(owners):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+    finally:
+        for o in owners:
+            o.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,world,lanes", [(dvcc.NO_WAIT, 2, 2), (dvcc.WAIT_DIE, 2, 4), (dvcc.OCC, 4, 2),
+                                            (dvcc.CALVIN, 2, 2)])
+def test_epoch_groups_ordered_lanes(cc, world, lanes):
+    """Epoch groups over ordered lanes: groups decided concurrently on L
+    contexts per rank (each with its own communicator and host thread),
+    executed in group order on every partition -- every group's commit
+    bytes, digests and writes, and every partition's rows, equal the oracle
+    running all the epochs in sequence."""
+    _check_epoch_groups_lanes(cc, world, 1 << 13, 2000, 0.3, groups=2 * lanes + 1, lanes=lanes)
+
+
+@pytest.mark.gpu
+def test_epoch_groups_ordered_lanes_failure():
+    """A bad key in group 2 of 6 over two ordered lanes: that lane returns
+    DV_ERR_KEY_NOT_FOUND on every rank, the other lane stops at its next
+    turn (DV_ERR_STATE) instead of waiting for ever, and only groups 0 and 1
+    reach the rows."""
+    _check_epoch_groups_lanes(dvcc.NO_WAIT, 2, 1 << 13, 2000, 0.3, groups=6, lanes=2, bad_group=2)
