@@ -60,7 +60,7 @@ CPU_SHARE = 16  # host threads the GPU box gives one GPU's job (nproc shows the 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--cc", default="NO_WAIT")
     ap.add_argument("--config", default="D")
