@@ -303,6 +303,35 @@ def closed_loop_leg(eng, gen, n_txn, k, d_commit, open_ms=None):
     return out
 
 
+def closed_loop_lanes_leg(eng, lanes, gen, n_txn, k, open_ms=None):
+    """The same closed loop over the decision lanes
+    (dv_epoch_run_closed_loop_lanes): epoch k decided on lane k % L, each
+    lane's aborted txns retried in its next epoch (L epochs later), the pool
+    drawn in epoch order; k a multiple of 2 L."""
+    nl = 1 + len(lanes)
+    k = max(2 * nl, (k + 2 * nl - 1) // (2 * nl) * 2 * nl)
+    pool = gen.gen(2 * n_txn, dvcc.epoch_seed(0, 999))
+    dpool = dvcc.DeviceEpoch(pool)
+    pb = torch.from_numpy(pool.txn_begin.astype(np.int32)).cuda()
+    commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    sts, bufs, cursor = eng.closed_loop_lanes(lanes, dpool, pb, n_txn, 2 * nl, d_commits=commits[:2 * nl])  # warm
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sts, bufs, cursor = eng.closed_loop_lanes(lanes, dpool, pb, n_txn, k, cursor=cursor, bufs=bufs,
+                                              d_commits=commits, resume=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    committed = sum(s.committed for s in sts)
+    out = {"committed_per_s": committed / el, "ms_per_epoch": el / k * 1e3, "epochs": k, "decision_lanes": nl,
+           "carried_per_epoch": sum(s.n_txn - s.committed for s in sts[:-nl]) / max(1, k - nl),
+           "entry_point": "dv_epoch_run_closed_loop_lanes",
+           "note": f"aborted txns retried {nl} epochs later (each lane's next epoch) ahead of new ones; "
+                   "epochs built on the device, executed in epoch order"}
+    if open_ms:
+        out["vs_open_loop_ms"] = out["ms_per_epoch"] / open_ms
+    return out
+
+
 def e2e_host_leg(eng, epochs, k):
     """SURVEY.md 8(d)'s second reading: epochs from host buffers, so the H2D
     copy of the 16-B access records is inside the time (pinned host memory,
@@ -940,6 +969,9 @@ def main():
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
         out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, max(4, min(a.steps, 10)), d_commit,
                                                    out["ms_per_step"])
+        if lanes:
+            out["closed_loop_retry"]["lanes"] = closed_loop_lanes_leg(eng, lanes, gen, n_txn_total,
+                                                                      max(8, min(a.steps, 16)), out["ms_per_step"])
     else:
         try:
             extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group)

@@ -2293,10 +2293,13 @@ struct OnLaneStreams {
 // one is run again with every epoch queued behind it, synchronously and in
 // order, as run_batch does on one stream.  pipelined(k): epoch k can be
 // queued that way; decide(c, k): queues its decision on lane c (up to the
-// execution); run(k, st): runs it synchronously on its lane.
-template <class Commit, class Pipelined, class Decide, class Run>
+// execution); after(c, k): queues what follows the execution on the lane (a
+// closed loop's refill; it runs before the next epoch's execution, on any
+// lane, is queued, and is a no-op when the epoch halted); run(k, st): runs
+// it synchronously on its lane.
+template <class Commit, class Pipelined, class Decide, class After, class Run>
 int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts, Commit &&commit_of,
-              Pipelined &&pipelined, Decide &&decide, Run &&run) {
+              Pipelined &&pipelined, Decide &&decide, After &&after, Run &&run) {
     HIPCHK(hipSetDevice(lanes[0]->cfg.device));
     int r0 = lane_streams(lanes, n_lanes);
     if (r0) return r0;
@@ -2371,6 +2374,7 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
             enqueue_exec(c, commit_of(k));
             r = hip_fail(hipGetLastError(), "execution launch");
         }
+        if (!r) r = after(c, k);
         if (!r) {
             EpochSnap &sn = p.sn;
             sn.n_acc = c->n_acc;
@@ -2429,7 +2433,7 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
             dv_ctx *c = lanes[k % n_lanes];
             return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P && !c->comm;
         },
-        [&](dv_ctx *c, uint32_t k) { return run_prefix_epoch(c, &eps[k]); },
+        [&](dv_ctx *c, uint32_t k) { return run_prefix_epoch(c, &eps[k]); }, [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
             return dv_epoch_run_device(lanes[k % n_lanes], &eps[k], commit_of(k), nullptr, st);
         });
@@ -2486,6 +2490,7 @@ int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
             if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
             return rr;
         },
+        [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
             return dv_tpcc_epoch_run_device(lanes[k % n_lanes], &eps[k], d_args[k], commit_of(k), oid_of(k), st);
         });
@@ -2617,6 +2622,90 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
     }
     HIPCHK(hipStreamSynchronize(c->stream));  // (the next epoch's refill: the caller may read it)
     return DV_OK;
+}
+
+// The closed loop over decision lanes: epoch k on lanes[k % L]; each lane
+// keeps its own pair of epoch buffers (bufs[2l], bufs[2l + 1]) and its epochs
+// form a closed loop of their own -- epoch k + L is epoch k's aborted txns,
+// then fresh pool txns -- while the shared pool cursor advances in epoch
+// order (refill k is queued behind execution k, which waits for execution
+// k - 1 and the refill behind it).  The epochs are those of one sequence in
+// which an aborted txn returns L epochs later (the reference's retry after a
+// penalty, abort_queue.cpp:26-82, with a penalty of L epochs).
+int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *pool,
+                                   const uint32_t *pool_begin, uint32_t *cursor, uint32_t n_txn, dv_epoch_dev *bufs,
+                                   uint64_t buf_cap, uint32_t n_epochs, int resume, uint8_t *const *d_commits,
+                                   dv_stats *sts) {
+    int r = check_lanes(lanes, n_lanes);
+    if (r) return r;
+    if (n_lanes == 1)
+        return dv_epoch_run_closed_loop(lanes[0], pool, pool_begin, cursor, n_txn, bufs, buf_cap, n_epochs, resume,
+                                        d_commits, sts);
+    if (!pool || !pool_begin || !cursor || !bufs || !n_txn) return DV_ERR_ARG;
+    dv_ctx *const c0 = lanes[0];
+    if (c0->cfg.cc_alg == DV_CALVIN || c0->cfg.workload != DV_YCSB) return DV_ERR_STATE;
+    const uint64_t bound = (uint64_t)n_txn * pool->max_txn_acc;
+    if (!pool->max_txn_acc || n_txn > pool->n_txn || n_txn > c0->cfg.max_txn || bound > buf_cap ||
+        bound > c0->cfg.max_acc || !pool->keys || !pool->types || !pool->acc_txn)
+        return DV_ERR_ARG;
+    for (uint32_t b = 0; b < 2 * n_lanes; b++)
+        if (!bufs[b].keys || !bufs[b].types || !bufs[b].acc_txn || !bufs[b].n_acc_dev ||
+            (pool->tables && !bufs[b].tables))
+            return DV_ERR_ARG;
+    for (uint32_t l = 0; l < n_lanes; l++)
+        if (lanes[l]->comm) return DV_ERR_STATE;
+    HIPCHK(hipSetDevice(c0->cfg.device));
+    for (uint32_t l = 0; l < n_lanes; l++) {
+        r = carry_bufs(lanes[l], carry_blocks(n_txn));
+        if (r) return r;
+    }
+    // lane l's j-th epoch of this call (global k = j * L + l) sits in buffer
+    // 2l + (j & 1); its refill writes 2l + ((j + 1) & 1)
+    auto buf_of = [&](uint32_t k, uint32_t ahead) { return &bufs[2 * (k % n_lanes) + (((k / n_lanes) + ahead) & 1)]; };
+    auto desc = [&](uint32_t k) {
+        dv_epoch_dev d = *buf_of(k, 0);
+        d.tables = pool->tables ? d.tables : nullptr;
+        d.n_txn = n_txn;
+        d.n_acc = bound;
+        d.max_txn_acc = pool->max_txn_acc;
+        d.ts = nullptr;
+        return d;
+    };
+    auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
+    if (!resume)  // each lane's first epoch: fresh txns, drawn in lane order
+        for (uint32_t l = 0; l < n_lanes; l++) {
+            dv_ctx *c = lanes[l];
+            enqueue_refill(c, nullptr, pool, pool_begin, cursor, n_txn, *buf_of(l, 0));
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipStreamSynchronize(c->stream));
+        }
+    const dv_epoch_dev d0 = desc(0);
+    const bool pipelined = prefix_applies(c0, &d0) && !timing(c0) && !ktiming(c0);
+    r = run_lanes(
+        lanes, n_lanes, n_epochs, sts, commit_of, [&](uint32_t) { return pipelined; },
+        [&](dv_ctx *c, uint32_t k) {
+            const dv_epoch_dev d = desc(k);
+            return run_prefix_epoch(c, &d);
+        },
+        [&](dv_ctx *c, uint32_t k) {  // (behind the execution; a no-op when k halted)
+            const dv_epoch_dev d = desc(k);
+            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, *buf_of(k, 1));
+            return hip_fail(hipGetLastError(), "refill");
+        },
+        [&](uint32_t k, dv_stats *st) {  // (synchronous, refill included: the next refill, on
+                                         // another lane, draws from the cursor after it)
+            dv_ctx *c = lanes[k % n_lanes];
+            const dv_epoch_dev d = desc(k);
+            int e = dv_epoch_run_device(c, &d, commit_of(k), nullptr, st);
+            if (!e) {
+                enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, *buf_of(k, 1));
+                e = hip_fail(hipGetLastError(), "refill");
+            }
+            if (!e) e = hip_fail(hipStreamSynchronize(c->stream), "sync");
+            return e;
+        });
+    for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
+    return r;
 }
 
 }  // extern "C"

@@ -169,6 +169,9 @@ SIGNATURES = [
     ("dv_epoch_run_device_batch", ctypes.c_int, [_vp, _P(EpochDev), ctypes.c_uint32, _P(_vp), _P(Stats)]),
     ("dv_open_lane", ctypes.c_int, [_vp, _P(_vp)]),
     ("dv_lanes_order", ctypes.c_int, [_P(_vp), ctypes.c_uint32]),
+    ("dv_epoch_run_closed_loop_lanes", ctypes.c_int,
+     [_P(_vp), ctypes.c_uint32, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _P(EpochDev), ctypes.c_uint64,
+      ctypes.c_uint32, ctypes.c_int, _P(_vp), _P(Stats)]),
     ("dv_tpcc_epoch_run_device_lanes", ctypes.c_int,
      [_P(_vp), ctypes.c_uint32, _P(EpochDev), _vp, ctypes.c_uint32, _vp, _vp, _P(Stats)]),
     ("dv_epoch_run_device_lanes", ctypes.c_int,

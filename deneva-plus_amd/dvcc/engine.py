@@ -546,6 +546,36 @@ class CCEngine:
                                                  cps, sts), "dv_epoch_run_closed_loop")
         return list(sts)[:n_epochs], bufs, cursor
 
+    def closed_loop_lanes(self, lanes, pool, pool_begin, n_txn, n_epochs, cursor=None, bufs=None,
+                          d_commits=None, resume=False):
+        """dv_epoch_run_closed_loop_lanes over [self] + lanes: epoch k on
+        context k % L, each context's epochs a closed loop of their own
+        (aborted txns retried L epochs later), the pool cursor shared.  bufs:
+        one ClosedLoopBufs per context (allocated when None).  Returns (stats
+        list, bufs, cursor); resume needs the previous call's n_epochs to be a
+        multiple of 2 L."""
+        import torch
+        ctxs = [self] + list(lanes)
+        nl = len(ctxs)
+        dev = pool.keys.device
+        if cursor is None:
+            cursor = torch.zeros(1, dtype=torch.int32, device=dev)
+        if bufs is None:
+            bufs = [ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev) for _ in range(nl)]
+        arr = (L.EpochDev * (2 * nl))(*[b.desc(i) for b in bufs for i in range(2)])
+        if d_commits is None or not isinstance(d_commits, (list, tuple)):
+            d_commits = [d_commits] * n_epochs
+        cps = (ctypes.c_void_p * max(1, n_epochs))(*[(int(t.data_ptr()) if t is not None else None)
+                                                     for t in d_commits])
+        sts = (L.Stats * max(1, n_epochs))()
+        lp = (ctypes.c_void_p * nl)(*[e._ctx.value for e in ctxs])
+        for e in ctxs:
+            e._after_torch()
+        L.check(L.lib().dv_epoch_run_closed_loop_lanes(lp, nl, ctypes.byref(pool.desc()), _ptr(pool_begin),
+                                                       _ptr(cursor), n_txn, arr, bufs[0].cap, n_epochs,
+                                                       int(resume), cps, sts), "dv_epoch_run_closed_loop_lanes")
+        return list(sts)[:n_epochs], bufs, cursor
+
     def group_carry(self, homes, d_commit, txns_per_rank, max_txn=None):
         """Retries across epoch groups (dv_epoch_group_carry): for each of this
         rank's batches of the group just run (DeviceEpochs), a DeviceEpoch of

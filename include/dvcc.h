@@ -396,6 +396,23 @@ int dv_open_lane(dv_ctx *owner, dv_ctx **lane);
 int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *eps, uint32_t n,
                               uint8_t *const *d_commits, dv_stats *sts);
 
+/* The closed loop over decision lanes (lanes as for dv_epoch_run_device_lanes,
+ * 2..8; n_lanes == 1 is dv_epoch_run_closed_loop): epoch k is decided on
+ * lanes[k % n_lanes] and every lane runs a closed loop of its own -- epoch
+ * k + n_lanes is epoch k's aborted txns, in sequence order, then fresh txns
+ * from the shared pool -- with executions, and the refills drawing on the
+ * shared cursor, in epoch order.  One sequence of epochs in which an aborted
+ * txn is retried n_lanes epochs later (the reference's AbortQueue retries
+ * after a penalty, abort_queue.cpp:26-82).  bufs: 2 * n_lanes buffers (lane
+ * l's pair at 2l, 2l + 1); without resume each lane's first epoch is drawn
+ * fresh, lane 0 first.  resume continues the previous call: its n_epochs
+ * must have been a multiple of 2 * n_lanes (every lane's next epoch is then
+ * in its first buffer). */
+int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_epoch_dev *pool,
+                                   const uint32_t *pool_begin, uint32_t *cursor, uint32_t n_txn, dv_epoch_dev *bufs,
+                                   uint64_t buf_cap, uint32_t n_epochs, int resume, uint8_t *const *d_commits,
+                                   dv_stats *sts);
+
 /* Ordered lanes for epoch groups (dv_epoch_group_run / _batch, N > 1): an
  * owner and its lanes (1..8; opened before dv_comm_init, each lane then
  * given its OWN communicator) become one execution order -- each on a

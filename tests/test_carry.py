@@ -233,3 +233,83 @@ def test_device_closed_loop_args():
         eng.closed_loop(DeviceEpoch(_pool(rows, 400, 14, R=16)), pb, 300, 1)
     eng.closed_loop(dpool, pb, 250, 2)
     eng.close()
+
+
+def host_closed_loop_lanes(cc, tab, f0, pool, cur, n_txn, n_epochs, lanes):
+    """the oracle of dv_epoch_run_closed_loop_lanes: each lane's first epoch
+    fresh (lane 0 first), then epoch k + L = epoch k's aborts + fresh pool
+    txns drawn in epoch order.  Returns the per-epoch results, the epochs left
+    for k = n_epochs .. n_epochs + L - 1, and the cursor."""
+    inputs = {}
+    for ln in range(lanes):
+        inputs[ln] = host_take(pool, cur, n_txn)
+        cur = (cur + n_txn) % pool.n_txn
+    out = []
+    for k in range(n_epochs):
+        host = inputs.pop(k)
+        c_ref, _, st_ref = O.epoch_run(ORACLE_CC[cc], tab.ix, f0, host.n_txn, host.txn_begin, host.keys,
+                                       host.types)
+        out.append((c_ref[:host.n_txn].copy(), st_ref, host))
+        hc = host_carry(host, c_ref, n_txn)
+        fresh = n_txn - hc.n_txn
+        inputs[k + lanes] = host_concat(hc, host_take(pool, cur, fresh))
+        cur = (cur + fresh) % pool.n_txn
+    return out, inputs, cur
+
+
+def _check_loop_lanes(cc, rows, pool, n_txn, n_epochs, lanes, prefix, calls=1, async_iters=None):
+    import torch
+    eng = CCEngine(cc, n_txn, n_txn * pool.max_txn_acc())
+    eng.set_prefix(prefix)
+    eng.load_ycsb_partition(rows)
+    extra = [eng.open_lane() for _ in range(lanes - 1)]
+    if async_iters:
+        for e in [eng] + extra:
+            e.set_async_limits(async_iters, 0)
+    try:
+        tab = O.YcsbTable(rows)
+        f0 = tab.f0.copy()
+        ref, nxt, cur_ref = host_closed_loop_lanes(cc, tab, f0, pool, 0, n_txn, n_epochs * calls, lanes)
+        dpool = DeviceEpoch(pool)
+        pb = torch.from_numpy(pool.txn_begin.astype(np.int32)).cuda()
+        commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in range(n_epochs)]
+        cursor, bufs, got = None, None, []
+        for call in range(calls):
+            sts, bufs, cursor = eng.closed_loop_lanes(extra, dpool, pb, n_txn, n_epochs, cursor=cursor, bufs=bufs,
+                                                      d_commits=commits, resume=call > 0)
+            got += [(c.cpu().numpy().copy(), s) for c, s in zip(commits, sts)]
+        for k, ((c, st), (c_ref, st_ref, host)) in enumerate(zip(got, ref)):
+            assert np.array_equal(c, c_ref), k
+            assert (st.n_txn, st.n_acc, st.committed) == (host.n_txn, host.n_acc, st_ref.committed), k
+            assert (st.read_digest, st.write_cnt) == (st_ref.read_digest, st_ref.write_cnt), k
+        assert int(cursor.item()) == cur_ref
+        total = n_epochs * calls
+        for ln in range(lanes):  # each lane's next epoch, in its first buffer
+            k = total + ((ln - total) % lanes)
+            e = bufs[ln].epoch((total // lanes) & 1 if total % lanes == 0 else 0, n_txn, pool.max_txn_acc())
+            assert e.n_acc == nxt[k].n_acc, ln
+            assert np.array_equal(e.keys.cpu().numpy().view(np.uint64), nxt[k].keys), ln
+        assert np.array_equal(eng.read_table(0, rows), f0)
+    finally:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,lanes,prefix", [(dvcc.NO_WAIT, 2, 400), (dvcc.WAIT_DIE, 4, 400), (dvcc.OCC, 2, 400),
+                                             (dvcc.NO_WAIT, 3, None)])
+def test_device_closed_loop_lanes(cc, lanes, prefix):
+    """dv_epoch_run_closed_loop_lanes against the oracle's interleaved loops:
+    every epoch's commit bytes and stats, the shared cursor, each lane's next
+    epoch and the table"""
+    rows, N = 1 << 13, 2000
+    pool = _pool(rows, 5000, 21)
+    _check_loop_lanes(cc, rows, pool, N, 4 * lanes, lanes, prefix)
+
+
+@pytest.mark.gpu
+def test_device_closed_loop_lanes_halts_and_resume():
+    """forced yields (halted epochs and every epoch queued behind them run
+    again in order) and a loop continued over two calls"""
+    rows, N = 1 << 13, 3000
+    pool = _pool(rows, 4000, 22, R=12)
+    _check_loop_lanes(dvcc.NO_WAIT, rows, pool, N, 4, 2, 500, calls=2, async_iters=1)
