@@ -924,3 +924,53 @@ def test_lane_tables_frozen_and_shared():
     lane.close()
     eng.load_ycsb_partition(rows)  # (unfrozen once its lanes are closed)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_lanes_setup_error_and_short_batches():
+    """Four lanes: a batch shorter than the lanes (0, 1 and 3 epochs), and an
+    epoch the contexts cannot hold (n_txn past max_txn) at position 3 -- the
+    call returns DV_ERR_ARG at once, the earlier epochs are applied and their
+    stats filled, and the lanes run epochs again."""
+    import ctypes
+    import time
+    from dvcc import _lib as L
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(dvcc.NO_WAIT, 8_000, 8_000 * 10)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(256)
+    lanes = [eng.open_lane() for _ in range(3)]
+    try:
+        assert eng.run_epochs_lanes(lanes, []) == []
+        seed = 1300
+        for count in (1, 3):
+            es = [g.gen(8_000, seed + k) for k in range(count)]
+            seed += count
+            refs = [_oracle_epoch(dvcc.NO_WAIT, tab, f0, e) for e in es]
+            sts = eng.run_epochs_lanes(lanes, [DeviceEpoch(e) for e in es])
+            for st, (_, _, st_ref) in zip(sts, refs):
+                assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
+            assert (eng.read_table(0, rows) == f0).all()
+        es = [g.gen(8_000, seed + k) for k in range(3)] + [g.gen(8_001, seed + 3), g.gen(8_000, seed + 4)]
+        refs = [_oracle_epoch(dvcc.NO_WAIT, tab, f0, e) for e in es[:3]]
+        deps = [DeviceEpoch(e) for e in es]
+        arr = (L.EpochDev * 5)(*[d.desc() for d in deps])
+        sts = (L.Stats * 5)()
+        lp = (ctypes.c_void_p * 4)(*[e._ctx.value for e in [eng] + lanes])
+        t0 = time.perf_counter()
+        rc = L.lib().dv_epoch_run_device_lanes(lp, 4, arr, 5, None, sts)
+        assert rc == L.DV_ERR_ARG and time.perf_counter() - t0 < 30
+        for k, (_, _, st_ref) in enumerate(refs):
+            assert (sts[k].committed, sts[k].read_digest) == (st_ref.committed, st_ref.read_digest), k
+        assert (eng.read_table(0, rows) == f0).all()
+        e2 = [g.gen(8_000, seed + 10 + k) for k in range(5)]
+        refs = [_oracle_epoch(dvcc.NO_WAIT, tab, f0, e) for e in e2]
+        sts = eng.run_epochs_lanes(lanes, [DeviceEpoch(e) for e in e2])
+        for st, (_, _, st_ref) in zip(sts, refs):
+            assert (st.committed, st.read_digest) == (st_ref.committed, st_ref.read_digest)
+        assert (eng.read_table(0, rows) == f0).all()
+    finally:
+        eng.close()
