@@ -1701,7 +1701,9 @@ extern "C" {
 int dv_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, uint32_t txns_per_rank, uint8_t *d_commit,
                       dv_stats *st) {
     KProfScope kps_(c);
-    return run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
+    const int r = run_part(c, home, nullptr, nullptr, false, txns_per_rank, d_commit, nullptr, st);
+    if (r && c) lane_fail(c);  // (ordered lanes: the epochs after this one stop)
+    return r;
 }
 
 int dv_epoch_group_run(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t txns_per_rank,
@@ -1739,7 +1741,9 @@ int dv_comm_set_mode(dv_ctx *c, int mode) {
 int dv_tpcc_epoch_run_part(dv_ctx *c, const dv_epoch_dev *home, const uint64_t *d_args, const uint8_t *d_owner,
                            uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
     KProfScope kps_(c);
-    return run_part(c, home, d_owner, d_args, true, txns_per_rank, d_commit, d_oid, st);
+    const int r = run_part(c, home, d_owner, d_args, true, txns_per_rank, d_commit, d_oid, st);
+    if (r && c) lane_fail(c);  // (ordered lanes: the epochs after this one stop)
+    return r;
 }
 
 }  // extern "C"

@@ -1498,7 +1498,34 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
 }
 }  // namespace
 
+int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st);
+
+// ordered lanes (dv_lanes_order) running the per-epoch partitioned drivers
+// (dv_epoch_run_part / dv_tpcc_epoch_run_part): the epoch's execution takes
+// its turn after the previous epoch's, on whichever lane (the epoch groups
+// take theirs in run_group's execution step instead)
 int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
+    const bool ordered = c && c->phase == 1 && c->order && c->comm && !c->route;
+    if (ordered) {
+        const int r = lane_exec_begin(c, c->stream);
+        if (r) {
+            c->phase = 0;
+            c->prefix_mode = false;
+            c->tp_args = c->tp_oid = nullptr;
+            return r;
+        }
+    }
+    const int r = epoch_finish(c, d_commit, st);
+    if (ordered) {
+        if (r)
+            lane_fail(c);
+        else
+            lane_exec_end(c, c->stream);
+    }
+    return r;
+}
+
+int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     KProfScope kps_(c);
     if (!c || c->phase != 1) return DV_ERR_STATE;
     const bool calvin = c->cfg.cc_alg == DV_CALVIN;

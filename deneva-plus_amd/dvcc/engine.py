@@ -379,6 +379,37 @@ class CCEngine:
         self._order = ctxs if len(ctxs) > 1 else None
         self._order_next = 0  # the lane of the next group (tickets continue across calls)
 
+    def run_ordered(self, n, call):
+        """n epochs over the ordered lanes (lanes_order) for the per-epoch
+        partitioned drivers: epoch i of the call on lane (epochs so far + i)
+        % L, each lane from its own host thread running call(ctx, i) for its
+        epochs in order (e.g. ctx.run_epoch_part / ctx.run_tpcc_epoch_part);
+        executions in epoch order.  Returns the list of call results; raises
+        the first lane's error."""
+        import threading
+        ctxs = self._order
+        nl = len(ctxs)
+        base = self._order_next
+        out, errs = [None] * n, []
+
+        def body(ln):
+            try:
+                for i in range(n):
+                    if (base + i) % nl == ln:
+                        out[i] = call(ctxs[ln], i)
+            except Exception as ex:  # noqa: BLE001 -- re-raised below
+                errs.append(ex)
+        th = [threading.Thread(target=body, args=(ln,)) for ln in range(nl)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        self._order_next = (base + n) % nl
+        if errs:
+            errs.sort(key=lambda e: getattr(e, "code", 0) == L.DV_ERR_STATE)
+            raise errs[0]
+        return out
+
     def run_epoch_groups_ordered(self, groups, txns_per_rank, d_commits=None):
         """Epoch groups over the ordered lanes (lanes_order): group i of the
         call on lane (groups so far + i) % L, every lane from its own host

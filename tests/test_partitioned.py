@@ -1181,3 +1181,75 @@ def test_epoch_groups_ordered_lanes_failure():
     turn (DV_ERR_STATE) instead of waiting for ever, and only groups 0 and 1
     reach the rows."""
     _check_epoch_groups_lanes(dvcc.NO_WAIT, 2, 1 << 13, 2000, 0.3, groups=6, lanes=2, bad_group=2)
+
+
+# ---- the per-epoch partitioned driver (dv_epoch_run_part) over ordered lanes
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,mode,lanes", [(dvcc.NO_WAIT, 1, 2), (dvcc.WAIT_DIE, 2, 2), (dvcc.OCC, 1, 3),
+                                           (dvcc.CALVIN, 1, 2)])
+def test_part_epochs_ordered_lanes(cc, mode, lanes):
+    """dv_epoch_run_part over ordered lanes (list protocol, mode 1, or
+    replicated, mode 2): epoch k on lane k % L of every rank, each lane with
+    its own communicator and host thread, executions in epoch order -- every
+    epoch's commit bytes and the partitions' rows equal the oracle running
+    the sequenced epochs one after the other."""
+    import threading
+    world, rows_pp, n_txn, R, epochs = 2, 1 << 13, 1500, 10, 2 * lanes + 1
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=0.3)
+    owners = []
+    for p in range(world):
+        cap = n_txn * world * R + 4096
+        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p, asynchronous=False)
+        eng.load_ycsb_partition(rows_pp)
+        owners.append(eng)
+    ctxs = [[o] + [o.open_lane() for _ in range(lanes - 1)] for o in owners]
+    for ln in range(lanes):
+        dvcc.CCEngine.comm_init_local([ctxs[r][ln] for r in range(world)])
+        for r in range(world):
+            ctxs[r][ln].comm_set_mode(mode)
+    for r in range(world):
+        ctxs[r][0].lanes_order(ctxs[r][1:])
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    batches, refs = [], []
+    for k in range(epochs):
+        b = [gen.gen(n_txn, dvcc.epoch_seed(r, 80 + k), r) for r in range(world)]
+        q = dvcc.sequence(b)
+        c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin, q.keys,
+                                       q.types)
+        batches.append([dvcc.DeviceEpoch(x) for x in b])
+        refs.append((c_ref, st_ref))
+    res = [None] * world
+
+    def rank_body(r):
+        try:
+            ds = [torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda") for _ in range(epochs)]
+            sts = owners[r].run_ordered(epochs, lambda ctx, i: ctx.run_epoch_part(batches[i][r], n_txn, ds[i]))
+            torch.cuda.synchronize()
+            res[r] = ([d.cpu().numpy() for d in ds], sts)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            res[r] = ex
+    th = [threading.Thread(target=rank_body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a rank hung in the ordered partitioned epochs"
+    try:
+        for r, x in enumerate(res):
+            assert not isinstance(x, Exception), f"rank {r}: {x}"
+        for k, (c_ref, st_ref) in enumerate(refs):
+            digest = writes = 0
+            for r in range(world):
+                cs, sts = res[r]
+                assert (cs[k] == c_ref).all(), f"epoch {k} rank {r}"
+                assert sts[k].committed == st_ref.committed, f"epoch {k} rank {r}"
+                digest = (digest + sts[k].read_digest) % (1 << 64)
+                writes += sts[k].write_cnt
+            assert digest == st_ref.read_digest and writes == st_ref.write_cnt, f"epoch {k}"
+        for p, eng in enumerate(owners):
+            assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+    finally:
+        for o in owners:
+            o.close()
