@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=4,
                     help="one GPU: decision lanes (dv_epoch_run_device_lanes) -- epochs decided on this many "
                          "contexts in turn, executions in epoch order; 1 = dv_epoch_run_device_batch")
+    ap.add_argument("--part-lanes", type=int, default=1,
+                    help="N>1 TPC-C leg: ordered decision lanes per rank for dv_tpcc_epoch_run_part "
+                         "(dv_lanes_order; opt-in)")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -758,19 +761,38 @@ def tpcc_part_leg(a, world, rank, local_rank, first_step):
         n_max = max(sizes) // world
         eng = T.TpccEngine(cc_name, pp, n_max * world, device=local_rank, part_id=rank, seed=1)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
+        lanes = [eng.open_lane() for _ in range(max(1, a.part_lanes) - 1)]
         engine_comm_init(a, eng, world, rank, "tpcc_" + cc_name)
+        for ln, lane in enumerate(lanes):
+            engine_comm_init(a, lane, world, rank, f"tpcc_{cc_name}_lane{ln + 1}")
+        if lanes:
+            eng.lanes_order(lanes)
+        out["decision_lanes"] = 1 + len(lanes)
         for total in sizes:
             n_rank = total // world
             batches = [T.gen(pp, n_rank, dvcc.epoch_seed(rank, 500 + e), home_part=rank) for e in range(2)]
             dev = [(T.device_epoch(b), torch.from_numpy(b.owner).cuda()) for b in batches]
             d_commit = torch.zeros(n_rank * world, dtype=torch.uint8, device="cuda")
             d_oid = torch.zeros(n_rank * world, dtype=torch.int64, device="cuda")
+            # (lanes: one commit / o_id buffer per lane)
+            bufs = [(d_commit, d_oid)] + [(torch.zeros_like(d_commit), torch.zeros_like(d_oid)) for _ in lanes]
 
             def step(i, dev=dev, n_rank=n_rank, d_commit=d_commit, d_oid=d_oid):
                 (dep, d_args), own = dev[i % 2]
                 return eng.run_tpcc_epoch_part(dep, d_args, own, n_rank, d_commit, d_oid)
+
+            def batch(first, count, dev=dev, n_rank=n_rank, bufs=bufs):
+                ctx_ix = {id(c): j for j, c in enumerate([eng] + lanes)}
+
+                def one(ctx, i):
+                    (dep, d_args), own = dev[(first + i) % 2]
+                    dc, do = bufs[ctx_ix[id(ctx)]]
+                    return ctx.run_tpcc_epoch_part(dep, d_args, own, n_rank, dc, do)
+                return eng.run_ordered(count, one)
             k = max(a.steps, 5) if total == sizes[0] else max(a.steps, 20)
-            sts, el = timed(step, nxt, a.warmup, k, world)
+            if lanes:  # (whole rounds of the lanes per call)
+                k = (k + len(bufs) - 1) // len(bufs) * len(bufs)
+            sts, el = timed(step, nxt, a.warmup, k, world, batch if lanes else None)
             nxt += 100
             committed = sum(st.committed for st in sts)
             key = cc_name if total == sizes[0] else f"window_{total}_{cc_name}"
