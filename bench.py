@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--lanes", type=int, default=4,
                     help="one GPU: decision lanes (dv_epoch_run_device_lanes) -- epochs decided on this many "
                          "contexts in turn, executions in epoch order; 1 = dv_epoch_run_device_batch")
+    ap.add_argument("--group-lanes", type=int, default=1,
+                    help="N>1 epoch groups: ordered decision lanes per rank (dv_lanes_order, one RCCL "
+                         "communicator per lane; opt-in until run on a multi-GPU node -- see DESIGN.md 6)")
     ap.add_argument("--part-lanes", type=int, default=1,
                     help="N>1 TPC-C leg: ordered decision lanes per rank for dv_tpcc_epoch_run_part "
                          "(dv_lanes_order; opt-in)")
@@ -682,7 +685,11 @@ class PartitionedBench:
         # epoch groups over ordered decision lanes (dv_lanes_order): L contexts
         # over this partition's tables, each with its own communicator, group
         # g decided on lane g % L, executions in group order
-        nl = max(1, a.lanes) if a.protocol == "group" and not a.no_pipeline else 1
+        # (one rank: --lanes; N ranks: --group-lanes, off by default -- with
+        # more streams than hardware queues two lanes' RCCL kernels can queue
+        # behind each other in opposite orders on two GPUs and wait for ever)
+        nl = (max(1, a.lanes) if world == 1 else max(1, a.group_lanes)) \
+            if a.protocol == "group" and not a.no_pipeline else 1
         self.lanes = [self.eng.open_lane() for _ in range(nl - 1)]
         engine_comm_init(a, self.eng, world, rank, "ycsb")
         self.eng.comm_set_mode(a.part_mode)
