@@ -54,6 +54,7 @@ CONFIGS = {
     "C": (100_000_000, 1_048_576, 0.9, "YCSB config C: 100,000,000 rows, 1,048,576-txn epoch"),
     "B": (16_777_216, 65_536, 0.6, "YCSB config B: 16,777,216 rows, 65,536-txn epoch"),
 }
+TPCC_EPOCHS = 3  # distinct TPC-C epochs (coprime to the four lanes)
 CPU_SHARE = 16  # host threads the GPU box gives one GPU's job (nproc shows the whole machine)
 
 
@@ -81,7 +82,9 @@ def parse():
                          "1 list protocol; 2 replicated; + 4: 8-byte epoch-group batches (DV_COMM_WIDE_BATCHES)")
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
-    ap.add_argument("--epochs", type=int, default=4, help="distinct pre-generated epochs")
+    ap.add_argument("--epochs", type=int, default=5,
+                    help="distinct pre-generated epochs (coprime to --lanes, so every epoch is decided on every "
+                         "lane in turn)")
     ap.add_argument("--ipc-rehearsal", action="store_true",
                     help="N>1 ranks sharing fewer GPUs (a rehearsal of the N>1 path on a one-GPU box): torch "
                          "collectives over gloo, the engine's over dv_comm_init_ipc (a test transport); the "
@@ -225,7 +228,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
     sizes = [int(x) for x in str(a.tpcc_txns).split(",") if x]
     out = {}
     for si, n_txn in enumerate(sizes):
-        eps = [T.gen(p, n_txn, dvcc.epoch_seed(0, e)) for e in range(2)]
+        eps = [T.gen(p, n_txn, dvcc.epoch_seed(0, e)) for e in range(TPCC_EPOCHS)]
         res = {"workload": f"TPC-C config E share: {a.tpcc_wh} warehouses/GPU, {n_txn}-txn epochs, "
                            "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
                "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
@@ -238,8 +241,9 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
             k = max(a.steps, 5) if si == 0 else max(a.steps, 20)
 
             def batch(m):  # the pipelined entry point (epoch k+1 queued before k is read back)
-                return eng.run_tpcc_epochs_device([dev[i % 2][0] for i in range(m)],
-                                                  [dev[i % 2][1] for i in range(m)], d_commit, d_oid, lanes=lanes)
+                ne = len(dev)
+                return eng.run_tpcc_epochs_device([dev[i % ne][0] for i in range(m)],
+                                                  [dev[i % ne][1] for i in range(m)], d_commit, d_oid, lanes=lanes)
             if a.warmup:
                 batch(a.warmup)
             torch.cuda.synchronize()
@@ -248,7 +252,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             committed = sum(s.committed for s in sts)
-            byts = sum(tpcc_bytes_per_txn(eps[i % 2]) for i in range(k))
+            byts = sum(tpcc_bytes_per_txn(eps[i % len(eps)]) for i in range(k))
             res[cc_name] = {"committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el,
                             "ms_per_epoch": el / k * 1e3, "abort_rate": 1 - committed / (k * n_txn),
                             "epochs": k, "decision_lanes": 1 + len(lanes),

@@ -93,6 +93,15 @@ __global__ __launch_bounds__(kBlock) void k_owner_scan(uint32_t *__restrict__ co
     if (threadIdx.x == 0) tot[blockIdx.x] = t;
 }
 
+// A batch's txn id at or past txns_per_rank would become another origin's
+// global id (rank * tpr + id) and merge two txns: it is sent as an id past
+// every epoch (kBadTxn), which the decider's probe rejects (ERRB_TXN, an
+// input error voted out on every rank before anything executes).
+constexpr uint32_t kBadTxn = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t global_txn(uint32_t t, uint32_t tpr, uint32_t base) {
+    return t < tpr ? t + base : kBadTxn;
+}
+
 // record i of the batch -> its owner's segment, in batch order (stable: a
 // wave walks 64 consecutive records per step, ranks by ballot); TPC-C
 // records carry their table, and their operation words go the same way into
@@ -103,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
                                                           const uint8_t *__restrict__ own,
                                                           const uint8_t *__restrict__ tables,
                                                           const uint64_t *__restrict__ args,
-                                                          uint64_t n, uint32_t P, uint32_t txn_base,
+                                                          uint64_t n, uint32_t P, uint32_t tpr, uint32_t txn_base,
                                                           const uint32_t *__restrict__ counts,
                                                           const uint32_t *__restrict__ tot, uint32_t nb,
                                                           dv_access *__restrict__ out,
@@ -142,7 +151,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
         const uint64_t dst = (uint64_t)obase[o] + counts[(uint64_t)o * nb + blockIdx.x] + wpre + r[j];
         dv_access a;
         a.key = keys[idx];
-        a.txn_seq = txn_base + acc_txn[idx];
+        a.txn_seq = global_txn(acc_txn[idx], tpr, txn_base);  // (an id past tpr: rejected by the probe)
         a.type = types[idx];
         a.table = tables ? tables[idx] : 0;
         a.flags = 0;
@@ -188,15 +197,6 @@ __global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restri
             ty[off + i] = gy[src + i];
         }
     }
-}
-
-// A batch's txn id at or past txns_per_rank would become another origin's
-// global id (rank * tpr + id) and merge two txns: it is sent as an id past
-// every epoch (kBadTxn), which the decider's probe rejects (ERRB_TXN, an
-// input error voted out on every rank before anything executes).
-constexpr uint32_t kBadTxn = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t global_txn(uint32_t t, uint32_t tpr, uint32_t base) {
-    return t < tpr ? t + base : kBadTxn;
 }
 
 // epoch groups: row id | wr << 31 and the global txn id, 8 B per access
@@ -1342,7 +1342,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         DV_LAUNCH(k_owner_count, nb, kBlock, 0, s, home->keys, own, n_home, P, m->counts, nb, m->xvote);
         DV_LAUNCH(k_owner_scan, P, kBlock, 0, s, m->counts, nb, m->tot);
         DV_LAUNCH(k_owner_scatter, nb, kBlock, 0, s, home->keys, home->types, home->acc_txn, own,
-                                             tpcc ? home->tables : nullptr, args, n_home, P,
+                                             tpcc ? home->tables : nullptr, args, n_home, P, txns_per_rank,
                                              (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb, m->send,
                                              tpcc ? m->send_args : nullptr, m->xvote);
     } else {

@@ -578,9 +578,9 @@ int lane_exec_begin(dv_ctx *c, hipStream_t s) {
     std::unique_lock<std::mutex> lk(o.mu);
     // (a lane never run for its turn -- groups not handed round the lanes in
     // order -- ends the order after kLaneWaitS instead of hanging the caller)
-    if (!o.cv.wait_for(lk, std::chrono::seconds(kLaneWaitS), [&] { return t > o.fail_at || o.next == t; }))
+    if (!o.cv.wait_for(lk, std::chrono::seconds(kLaneWaitS), [&] { return t >= o.fail_at || o.next == t; }))
         o.fail_at = std::min(o.fail_at, o.next), o.cv.notify_all();
-    if (t > o.fail_at || o.next != t) return DV_ERR_STATE;
+    if (t >= o.fail_at || o.next != t) return DV_ERR_STATE;  // (fail_at itself never executes)
     if (o.last) HIPCHK(hipStreamWaitEvent(s, o.last, 0));
     return DV_OK;
 }

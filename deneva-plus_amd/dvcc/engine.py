@@ -374,6 +374,12 @@ class CCEngine:
         each lane from its own host thread, group g on lane g % len) executed
         in group order across them.  lanes=[]: this engine alone again."""
         ctxs = [self] + list(lanes)
+        if len(ctxs) == 1 and getattr(self, "_order", None):
+            # every lane of the previous order alone again too (its CU-masked
+            # stream and the shared order released), so it can be ordered anew
+            for e in self._order[1:]:
+                one = (ctypes.c_void_p * 1)(e._ctx.value)
+                L.check(L.lib().dv_lanes_order(one, 1), "dv_lanes_order")
         lp = (ctypes.c_void_p * len(ctxs))(*[e._ctx.value for e in ctxs])
         L.check(L.lib().dv_lanes_order(lp, len(ctxs)), "dv_lanes_order")
         self._order = ctxs if len(ctxs) > 1 else None

@@ -23,11 +23,18 @@ def host_carry(ep, commit, max_txn):
     """The aborted txns of `ep` (commit byte 0), in order, at most max_txn."""
     tb = ep.txn_begin.astype(np.int64)
     ab = np.flatnonzero(commit[:ep.n_txn] == 0)[:max_txn]
-    lens = tb[ab + 1] - tb[ab]
-    idx = np.concatenate([np.arange(tb[t], tb[t + 1]) for t in ab]) if len(ab) else np.zeros(0, np.int64)
-    ntb = np.zeros(len(ab) + 1, np.uint32)
-    ntb[1:] = np.cumsum(lens)
+    idx, ntb = _gather_txns(tb, ab)
     return Epoch(ep.keys[idx].copy(), ep.types[idx].copy(), ntb)
+
+
+def _gather_txns(tb, ids):
+    """access indices of txns `ids` (in that order) of an epoch with
+    txn_begin `tb`, and the new txn_begin"""
+    lens = tb[ids + 1] - tb[ids]
+    ntb = np.zeros(len(ids) + 1, np.int64)
+    ntb[1:] = np.cumsum(lens)
+    idx = np.repeat(tb[ids] - ntb[:-1], lens) + np.arange(int(ntb[-1]), dtype=np.int64)
+    return idx, ntb.astype(np.uint32)
 
 
 def host_concat(a, b):
@@ -119,11 +126,7 @@ def host_take(pool, cur, n):
     """txns [cur, cur + n) of the pool, wrapping around it (the fresh txns of
     the device closed loop)"""
     ids = (cur + np.arange(n)) % pool.n_txn
-    tb = pool.txn_begin.astype(np.int64)
-    lens = tb[ids + 1] - tb[ids]
-    idx = np.concatenate([np.arange(tb[t], tb[t + 1]) for t in ids]) if n else np.zeros(0, np.int64)
-    ntb = np.zeros(n + 1, np.uint32)
-    ntb[1:] = np.cumsum(lens)
+    idx, ntb = _gather_txns(pool.txn_begin.astype(np.int64), ids)
     return Epoch(pool.keys[idx].copy(), pool.types[idx].copy(), ntb)
 
 
@@ -313,3 +316,17 @@ def test_device_closed_loop_lanes_halts_and_resume():
     rows, N = 1 << 13, 3000
     pool = _pool(rows, 4000, 22, R=12)
     _check_loop_lanes(dvcc.NO_WAIT, rows, pool, N, 4, 2, 500, calls=2, async_iters=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_device_closed_loop_lanes_config_d_full():
+    """The bench's closed_loop_retry.lanes leg at its own size: config D
+    (16,777,216 rows, 1,048,576-txn epochs, zipf 0.9, automatic prefix), four
+    lanes, 8 epochs of the interleaved loops over a 2M-txn pool (the bench's
+    pool seed) -- every epoch, the cursor, each lane's next epoch and the
+    table against the oracle's loops"""
+    rows, N = 16_777_216, 1_048_576
+    gen = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    pool = gen.gen(2 * N, dvcc.epoch_seed(0, 999))
+    _check_loop_lanes(dvcc.NO_WAIT, rows, pool, N, 8, 4, 0)

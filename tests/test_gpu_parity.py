@@ -711,7 +711,7 @@ def test_randomized_sweep(case):
     _check(cc, rows, [g.gen(n_txn, 77 + case), g.gen(n_txn, 78 + case)], **knobs)
 
 
-def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1):
+def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1, stream=None):
     """dv_epoch_run_device_batch (lanes > 1: dv_epoch_run_device_lanes over
     the engine and lanes - 1 decision lanes) against the oracle run over the
     same epochs one after the other: every epoch's commit bytes, digest and
@@ -720,6 +720,8 @@ def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1):
     f0 = tab.f0.copy()
     refs = [_oracle_epoch(cc, tab, f0, e) for e in epochs]
     eng = CCEngine(cc, max(e.n_txn for e in epochs), max(e.n_acc for e in epochs))
+    if stream is not None:
+        eng.set_stream(stream.cuda_stream)
     eng.load_ycsb_partition(rows)
     eng.set_prefix(prefix)
     extra = [eng.open_lane() for _ in range(lanes - 1)]
@@ -974,3 +976,48 @@ def test_lanes_setup_error_and_short_batches():
         assert (eng.read_table(0, rows) == f0).all()
     finally:
         eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_bench_timed_path_config_d_lanes():
+    """bench.py's timed region at its own size: dv_epoch_run_device_lanes over
+    the engine and three decision lanes, config D (16,777,216 rows,
+    1,048,576-txn epochs, zipf 0.9, NO_WAIT, automatic n/32 prefix), the
+    bench's 5 distinct epochs (seeds epoch_seed(0, e)) cycled twice, so every
+    epoch is decided on two different lanes, on a torch stream as in the
+    bench -- commit bytes, read digest, write count of every epoch and the
+    final F0 column against the oracle running the 10 epochs in order."""
+    rows, n_txn = 16_777_216, 1_048_576
+    g = YCSBQueryGenerator(rows, part_cnt=1, req_per_query=10, zipf_theta=0.9, txn_write_perc=1.0,
+                           tup_write_perc=0.5, part_per_txn=1, strict_ppt=1, mpr=-1.0)
+    es = [g.gen(n_txn, dvcc.epoch_seed(0, e), 0) for e in range(5)]
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        sts = _check_batch(dvcc.NO_WAIT, rows, es + es, prefix=0, lanes=4, stream=s)
+    assert all(st.prefix_txn == n_txn // 32 for st in sts), [st.prefix_txn for st in sts]
+    assert sum(st.async_yields for st in sts) == 0
+
+
+@pytest.mark.gpu
+def test_lanes_order_release_and_reorder():
+    """lanes_order([]) releases the whole order (every lane back on its own
+    stream), so the same lanes can be ordered again; the owner then still
+    decides epochs bit-exact."""
+    rows = 1 << 14
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    e = g.gen(3000, 1234)
+    eng = CCEngine(dvcc.NO_WAIT, 3000, e.n_acc)
+    eng.load_ycsb_partition(rows)
+    lanes = [eng.open_lane() for _ in range(2)]
+    for _ in range(2):
+        eng.lanes_order(lanes)
+        eng.lanes_order([])
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    c_ref, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e)
+    c, _, st = _gpu_epoch(eng, e, "device")
+    assert (c == c_ref).all() and st.read_digest == st_ref.read_digest
+    for ln in lanes:
+        ln.close()
+    eng.close()

@@ -844,17 +844,18 @@ def test_epoch_groups_nondense_batch_goes_wide():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind", ["group_wide", "replicated"])
+@pytest.mark.parametrize("kind", ["group_wide", "replicated", "list"])
 def test_txn_id_past_txns_per_rank_is_rejected(kind):
     """A batch whose device txn ids reach txns_per_rank (its n_txn within the
     bound): the id would alias the next origin's txn 0 in the global order, so
-    the pack sends it as an invalid id and every rank returns
-    DV_ERR_TXN_RANGE with no row changed (the 8-byte epoch-group batches and
-    the replicated protocol; the compact batches reject it as non-dense)."""
+    the pack (the owner split, for the list protocol) sends it as an invalid
+    id and every rank returns DV_ERR_TXN_RANGE with no row changed (the 8-byte
+    epoch-group batches, the replicated and the list protocol; the compact
+    batches reject it as non-dense)."""
     world, rows_pp, n_txn = 2, 1 << 12, 500
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
                                   strict_ppt=1, mpr=0.3)
-    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=1 if kind == "list" else 2)
     if kind == "group_wide":
         for eng in engines:
             eng.comm_set_mode(2 | dvcc._lib.DV_COMM_WIDE_BATCHES)
@@ -1140,6 +1141,26 @@ def _check_epoch_groups_lanes(cc, world, rows_pp, n_txn, mpr, groups, lanes, the
             # groups before the failing one are applied on every partition, nothing after them
             for p, eng in enumerate(owners):
                 assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table"
+            # the order has ended: a later call on any lane returns DV_ERR_STATE
+            # and changes no row (the failed ticket itself never executes)
+            again = {}
+
+            def body2(r, ln):
+                try:
+                    d = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+                    again[(r, ln)] = ctxs[r][ln].run_epoch_groups([homes[r][0]], n_txn, [d])
+                except Exception as ex:  # noqa: BLE001 -- reported per rank and lane
+                    again[(r, ln)] = ex
+            th = [threading.Thread(target=body2, args=(r, ln)) for r in range(world) for ln in range(lanes)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join(timeout=300)
+                assert not t.is_alive(), "a lane hung after the order ended"
+            for k, x in again.items():
+                assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_STATE, (k, x)
+            for p, eng in enumerate(owners):
+                assert (eng.read_table(0, rows_pp) == f0[p::world]).all(), f"partition {p} table after"
             return
         assert not [k for k in out if len(k) == 3], {k: v for k, v in out.items() if len(k) == 3}
         for g in range(groups):
@@ -1179,7 +1200,8 @@ def test_epoch_groups_ordered_lanes_failure():
     """A bad key in group 2 of 6 over two ordered lanes: that lane returns
     DV_ERR_KEY_NOT_FOUND on every rank, the other lane stops at its next
     turn (DV_ERR_STATE) instead of waiting for ever, and only groups 0 and 1
-    reach the rows."""
+    reach the rows; calling the lanes again afterwards returns DV_ERR_STATE
+    and changes nothing."""
     _check_epoch_groups_lanes(dvcc.NO_WAIT, 2, 1 << 13, 2000, 0.3, groups=6, lanes=2, bad_group=2)
 
 

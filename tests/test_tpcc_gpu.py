@@ -414,3 +414,77 @@ def test_engine_matches_tpcc_golden(name):
             assert np.array_equal(rows, g[f"rows_{t}"]) and np.array_equal(after[rows], g[f"vals_{t}"]), t
     finally:
         eng.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("cc", [dvcc.WAIT_DIE, dvcc.CALVIN])
+@pytest.mark.parametrize("n_txn", [65_536, 10_000])
+def test_tpcc_bench_timed_path_lanes(cc, n_txn):
+    """bench.py's TPC-C leg at its own size: config E's share of one GPU (32
+    warehouses, full counts, engine seed 1), the leg's 3 distinct epochs
+    (seeds epoch_seed(0, e)) cycled twice over four decision lanes
+    (dv_tpcc_epoch_run_device_lanes) -- commit bytes, o_id and stats of every
+    epoch and every table after, against the oracle running them in order."""
+    po, pp = _params("e")
+    db = O.TpccDB(po, 1)
+    eng = T.TpccEngine(cc, pp, n_txn, seed=1)
+    extra = [eng.open_lane() for _ in range(3)]
+    try:
+        es = [T.gen(pp, n_txn, dvcc.epoch_seed(0, e)) for e in range(3)] * 2
+        refs = [db.epoch(ORACLE_CC[cc], e.keys, e.types, e.tables, e.args, e.txn_begin) for e in es]
+        devs = [T.device_epoch(e) for e in es]
+        commits = [torch.zeros(n_txn, dtype=torch.uint8, device="cuda") for _ in es]
+        oids = [torch.zeros(n_txn, dtype=torch.int64, device="cuda") for _ in es]
+        sts = eng.run_tpcc_epochs_device([d for d, _ in devs], [a for _, a in devs], commits, oids, lanes=extra)
+        for k, ((c_ref, o_ref, st_ref), st) in enumerate(zip(refs, sts)):
+            assert (commits[k].cpu().numpy() == c_ref).all(), k
+            assert (oids[k].cpu().numpy().view(np.uint64) == o_ref).all(), k
+            assert st.committed == st_ref.committed and st.write_cnt == st_ref.write_cnt, k
+        _check_tables(eng, db, pp)
+    finally:
+        eng.close()
+
+
+def test_tpcc_part_txn_id_past_txns_per_rank_is_rejected():
+    """dv_tpcc_epoch_run_part with a batch whose txn ids reach txns_per_rank:
+    the owner split sends them as an invalid id, and every rank returns
+    DV_ERR_TXN_RANGE with no row changed (the id would otherwise alias the next
+    origin's txn 0 and merge two txns)."""
+    import threading
+    world, n_txn = 2, 300
+    pp = T.tpcc_params(part_cnt=world, num_wh=4, cust_per_dist=1000, max_items=2000)
+    batches = [T.gen(pp, n_txn, 70 + r, home_part=r) for r in range(world)]
+    engines = [T.TpccEngine(dvcc.WAIT_DIE, pp, n_txn * world, part_id=p, seed=5) for p in range(world)]
+    dvcc.CCEngine.comm_init_local(engines)
+    before = [[eng.read_col(t, 0).copy() for t in range(5)] for eng in engines]
+    out = [None] * world
+
+    def body(r):
+        try:
+            dep, d_args = T.device_epoch(batches[r])
+            if r == 1:
+                t = dep.acc_txn.clone()
+                t[-2:] = n_txn  # the last txn's accesses name txn n_txn
+                dep = dvcc.DeviceEpoch.from_tensors(dep.keys, dep.types, t, n_txn, max_txn_acc=dep.max_txn_acc,
+                                                    tables=dep.tables)
+            own = torch.from_numpy(batches[r].owner).cuda()
+            d_commit = torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda")
+            d_oid = torch.zeros(n_txn * world, dtype=torch.int64, device="cuda")
+            out[r] = engines[r].run_tpcc_epoch_part(dep, d_args, own, n_txn, d_commit, d_oid)
+        except Exception as ex:  # noqa: BLE001 -- reported per rank
+            out[r] = ex
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+        assert not t.is_alive(), "a rank hung"
+    try:
+        for r, x in enumerate(out):
+            assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_TXN_RANGE, (r, x)
+        for eng, b in zip(engines, before):
+            for t in range(5):
+                assert (eng.read_col(t, 0) == b[t]).all()
+    finally:
+        for eng in engines:
+            eng.close()
