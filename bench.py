@@ -92,9 +92,10 @@ def parse():
     ap.add_argument("--lanes", type=int, default=4,
                     help="one GPU: decision lanes (dv_epoch_run_device_lanes) -- epochs decided on this many "
                          "contexts in turn, executions in epoch order; 1 = dv_epoch_run_device_batch")
-    ap.add_argument("--group-lanes", type=int, default=1,
+    ap.add_argument("--group-lanes", type=int, default=4,
                     help="N>1 epoch groups: ordered decision lanes per rank (dv_lanes_order, one RCCL "
-                         "communicator per lane; opt-in until run on a multi-GPU node -- see DESIGN.md 6)")
+                         "communicator per lane, each lane stream on a hardware queue of its own -- checked by "
+                         "dv_lanes_order, DESIGN.md 6; 1 = one context per rank)")
     ap.add_argument("--part-lanes", type=int, default=1,
                     help="N>1 TPC-C leg: ordered decision lanes per rank for dv_tpcc_epoch_run_part "
                          "(dv_lanes_order; opt-in)")
@@ -689,9 +690,10 @@ class PartitionedBench:
         # epoch groups over ordered decision lanes (dv_lanes_order): L contexts
         # over this partition's tables, each with its own communicator, group
         # g decided on lane g % L, executions in group order
-        # (one rank: --lanes; N ranks: --group-lanes, off by default -- with
-        # more streams than hardware queues two lanes' RCCL kernels can queue
-        # behind each other in opposite orders on two GPUs and wait for ever)
+        # (one rank: --lanes; N ranks: --group-lanes; dv_lanes_order refuses
+        # lanes whose streams share a hardware queue -- two lanes' RCCL
+        # kernels could then queue in opposite orders on two GPUs -- and the
+        # bench then runs one context per rank, saying so in the line)
         nl = (max(1, a.lanes) if world == 1 else max(1, a.group_lanes)) \
             if a.protocol == "group" and not a.no_pipeline else 1
         self.lanes = [self.eng.open_lane() for _ in range(nl - 1)]
@@ -700,8 +702,23 @@ class PartitionedBench:
         for ln, lane in enumerate(self.lanes):
             engine_comm_init(a, lane, world, rank, f"ycsb_lane{ln + 1}")
             lane.comm_set_mode(a.part_mode)
+        self.lanes_refused = None
         if self.lanes:
-            self.eng.lanes_order(self.lanes)
+            ok = 1
+            try:
+                self.eng.lanes_order(self.lanes)
+            except dvcc.DvccError as ex:  # (a shared hardware queue: no ordered lanes on this box)
+                self.lanes_refused = repr(ex)
+                ok = 0
+            if world > 1:  # every rank takes the same path
+                t = torch.tensor([ok], dtype=torch.int32, device="cpu" if dist.get_backend() == "gloo" else "cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                ok = int(t.item())
+            if not ok:
+                if self.lanes_refused is None:
+                    self.eng.lanes_order([])
+                    self.lanes_refused = "refused on another rank"
+                self.lanes = []
         self.rows = rows
         self.d_commit = torch.zeros(max_txn_rank * world, dtype=torch.uint8, device="cuda")
         self.d_commits = [self.d_commit] + [torch.zeros_like(self.d_commit) for _ in self.lanes]
@@ -712,6 +729,11 @@ class PartitionedBench:
         if self.lanes:
             self.eng.lanes_order([])
             self.eng.set_stream(torch.cuda.current_stream().cuda_stream)
+
+    def order(self):
+        """The ordered lanes again (the MPR sweep runs the headline's path)."""
+        if self.lanes:
+            self.eng.lanes_order(self.lanes)
 
     def epochs(self, n_txn_rank, mpr, theta, count):
         gen = dvcc.YCSBQueryGenerator(self.rows * self.world, part_cnt=self.world, req_per_query=self.R,
@@ -816,13 +838,16 @@ def tpcc_part_leg(a, world, rank, local_rank, first_step):
 
 
 def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
-    """N>1 extras beside the headline: strong scaling (one epoch per step),
-    weak scaling (1,048,576 txns per GPU, list protocol) and the MPR sweep."""
+    """N>1 extras beside the headline, each with the headline's warmup:
+    strong scaling (one 1,048,576-txn epoch per step, dv_epoch_run_part --
+    replicated when the epoch fits, mode 0), weak scaling (1,048,576 txns per
+    GPU, the list protocol) and the MPR sweep (the headline's path: epoch
+    groups through dv_epoch_group_run_batch over the ordered lanes)."""
     nxt = 10_000
+    k = max(1, min(a.steps, 10))
     if group:
-        # strong scaling: one 1,048,576-txn epoch per step (dv_epoch_run_part)
         sdeps = pb.epochs(n_txn_rank, mpr, theta, 2)
-        sst, sel = timed(pb.stepper(sdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+        sst, sel = timed(pb.stepper(sdeps, n_txn_rank), nxt, a.warmup, k, world)
         scm = sum(s.committed for s in sst)
         out["strong_scaling"] = {"txns_per_epoch": n_txn_total, "committed_per_s": scm / sel,
                                  "ms_per_epoch": sel / len(sst) * 1e3, "epochs": len(sst),
@@ -830,32 +855,36 @@ def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
         del sdeps
         nxt += 100
     if not a.no_weak:
-        # weak scaling: 1,048,576 txns per GPU per epoch (list protocol)
         wdeps = pb.epochs(n_txn_total, mpr, theta, 2)
-        wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, 1, min(a.steps, 5), world)
+        wst, wel = timed(pb.stepper(wdeps, n_txn_total), nxt, a.warmup, k, world)
         wc = sum(s.committed for s in wst)
         out["weak_scaling"] = {"txns_per_epoch_per_gpu": n_txn_total, "txns_per_epoch": n_txn_total * world,
                                "committed_per_s": wc / wel, "decided_txns_per_s": len(wst) * n_txn_total * world / wel,
                                "ms_per_epoch": wel / len(wst) * 1e3,
                                "abort_rate": 1 - wc / (len(wst) * n_txn_total * world), "epochs": len(wst),
-                               "mpr": mpr}
+                               "mpr": mpr, "protocol": "dv_epoch_run_part, list protocol (the epoch exceeds a context)"}
         del wdeps
         nxt += 100
     sweep = []
+    if group:
+        pb.order()
     for m in [float(x) for x in a.mpr_sweep.split(",") if x.strip()]:
         if group:
-            mg = pb.groups(n_txn_rank, m, theta, 1)
-            mst, mel = timed(pb.group_stepper(mg, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            mg = pb.groups(n_txn_rank, m, theta, 3)
+            km = (k + len(pb.d_commits) - 1) // len(pb.d_commits) * len(pb.d_commits)
+            mst, mel = timed(None, 0, a.warmup, km, world, pb.group_batcher(mg, n_txn_rank))
             mtx = len(mst) * n_txn_total * world
         else:
             mdeps = pb.epochs(n_txn_rank, m, theta, 2)
-            mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, 1, min(a.steps, 5), world)
+            mst, mel = timed(pb.stepper(mdeps, n_txn_rank), nxt, a.warmup, k, world)
             mtx = len(mst) * n_txn_total
         mc = sum(s.committed for s in mst)
         sweep.append({"mpr": m, "committed_per_s": mc / mel, "ms_per_step": mel / len(mst) * 1e3,
-                      "abort_rate": 1 - mc / mtx,
+                      "abort_rate": 1 - mc / mtx, "steps": len(mst),
                       "rounds_mean": float(np.mean([s.rounds for s in mst]))})
         nxt += 100
+    if group:
+        pb.unorder()
     if sweep:
         out["mpr_sweep"] = sweep
     if not a.no_tpcc_part and not a.no_tpcc:
@@ -991,6 +1020,8 @@ def main():
         "gen_seconds": t_gen,
         "src_hash": dvcc._lib.source_hash(),
     }
+    if part and pb.lanes_refused:
+        out["config"]["ordered_lanes_refused"] = pb.lanes_refused
     out.update(stage_summary(stats, sstats, table, el, R))
     out["kernels"] = table
     out["kernel_us_per_epoch"] = kus

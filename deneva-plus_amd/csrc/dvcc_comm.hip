@@ -1295,7 +1295,9 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     const uint64_t cap = std::min<uint64_t>(cfg.max_acc, m->acc_cap);
     uint64_t total = 0;
     for (uint32_t q = 0; q < P; q++) total += recvc[q];
-    if (!gvote[3] && (P > 1 || m->mode == 2) && total <= cap && (uint64_t)gvote[2] * P <= m->acc_cap) {
+    //    (one rank too: the replicated epoch is the single-GPU path plus a
+    //    local copy, the list protocol a host round trip per decision round)
+    if (!gvote[3] && total <= cap && (uint64_t)gvote[2] * P <= m->acc_cap) {
         // send and receive areas: [row ids 4 B | txn ids 4 B | types 1 B] per access
         uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
         uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *st_ = reinterpret_cast<uint32_t *>(sb + 4 * m->acc_cap);

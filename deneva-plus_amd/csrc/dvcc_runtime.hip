@@ -2285,6 +2285,53 @@ int lane_streams(dv_ctx *const *lanes, uint32_t n_lanes) {
     return DV_OK;
 }
 
+// Ordered lanes with communicators (dv_lanes_order at N > 1): every lane's
+// collectives go to its own stream, and RCCL kernels wait for their peers, so
+// two lanes' streams must never feed one hardware queue -- two collectives
+// queued in opposite orders on two GPUs would wait for each other for ever.
+// A CU mask is a property of the hardware queue, so a CU-masked stream gets
+// a queue of its own (measured, tools/micro/queue_share.hip: with
+// GPU_MAX_HW_QUEUES 4, plain streams 0 and 7 share one, CU-masked streams
+// never).  The order does not rest on that observation alone: for every pair
+// of lane streams a bounded probe checks it -- a kernel on lane a spins (at
+// most ~50 ms) until a kernel queued after it on lane b sets a word, which
+// only happens if b's kernel runs beside a's, i.e. on another queue.
+__global__ void k_queue_probe_wait(uint32_t *flag, uint32_t *seen) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    uint32_t v = 0;
+    while ((v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0u &&
+           wall_clock64() - t0 < 5000000ull)  // ~50 ms at the 100 MHz constant clock
+        __builtin_amdgcn_s_sleep(4);
+    *seen = v;
+}
+__global__ void k_queue_probe_set(uint32_t *flag) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+int lanes_own_queues(dv_ctx *const *lanes, uint32_t n_lanes) {
+    uint32_t *d = nullptr;
+    HIPCHK(hipMalloc(&d, 2 * sizeof(uint32_t)));
+    int r = DV_OK;
+    for (uint32_t a = 0; a < n_lanes && !r; a++)
+        for (uint32_t b = 0; b < n_lanes && !r; b++) {
+            if (a == b) continue;
+            uint32_t seen = 0;
+            hipStream_t sa = lanes[a]->lane_stream, sb = lanes[b]->lane_stream;
+            if (hipMemsetAsync(d, 0, 2 * sizeof(uint32_t), sa) != hipSuccess ||
+                hipStreamSynchronize(sa) != hipSuccess) { r = DV_ERR_HIP; break; }
+            hipLaunchKernelGGL(k_queue_probe_wait, dim3(1), dim3(64), 0, sa, d, d + 1);
+            hipLaunchKernelGGL(k_queue_probe_set, dim3(1), dim3(64), 0, sb, d);
+            if (hipStreamSynchronize(sa) != hipSuccess || hipStreamSynchronize(sb) != hipSuccess ||
+                hipMemcpy(&seen, d + 1, sizeof(seen), hipMemcpyDeviceToHost) != hipSuccess)
+                r = DV_ERR_HIP;
+            else if (!seen)
+                r = DV_ERR_STATE;  // lanes a and b share a hardware queue: no ordered lanes with collectives
+        }
+    (void)hipFree(d);
+    return r;
+}
+
 // while a lanes call runs each lane works on its masked stream, ordered after
 // the caller's stream at the start, and the caller's after it at the end
 struct OnLaneStreams {
@@ -2484,6 +2531,12 @@ int dv_lanes_order(dv_ctx *const *lanes, uint32_t n_lanes) {
         if (lanes[l]->order) return DV_ERR_STATE;  // (already ordered: dv_lanes_order(&lane, 1) first)
     r = lane_streams(lanes, n_lanes);
     if (r) return r;
+    bool comm = false;
+    for (uint32_t l = 0; l < n_lanes; l++) comm |= lanes[l]->comm != nullptr;
+    if (comm) {  // (collectives on every lane: each lane stream on a hardware queue of its own)
+        r = lanes_own_queues(lanes, n_lanes);
+        if (r) return r;
+    }
     auto o = std::make_shared<LaneOrder>();
     o->n = n_lanes;
     for (uint32_t l = 0; l < n_lanes; l++) {

@@ -425,9 +425,16 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
  * groups before it execute, every later one returns DV_ERR_STATE; a turn
  * not taken within 120 s also ends it.  n_lanes == 1: that context back on
  * its own stream, unordered.  The epoch groups' results are those of one
- * context running the groups in order.  The reference's analogue: its
- * worker threads processing several txns' remote requests at once on one
- * node while Calvin's sequencer fixes the order (sequencer.cpp:283-326). */
+ * context running the groups in order.  With communicators (N > 1) each
+ * lane's collectives run on its own stream: two lanes' streams must not feed
+ * one hardware queue (two RCCL kernels queued in opposite orders on two GPUs
+ * would wait for each other), so the call first checks, for every pair of
+ * lane streams, that a kernel queued on one runs while a kernel on the other
+ * is still running (a bounded probe, ~50 ms at most) and returns
+ * DV_ERR_STATE, unordered, if any pair shares a queue.  The
+ * reference's analogue: its worker threads processing several txns' remote
+ * requests at once on one node while Calvin's sequencer fixes the order
+ * (sequencer.cpp:283-326). */
 int dv_lanes_order(dv_ctx *const *lanes, uint32_t n_lanes);
 
 /* The closed loop on the device (the reference's retry path,

@@ -72,14 +72,29 @@ def _run_scenario(sc, world, rank, name):
     rows_pp, n_txn, cc = sc["rows_pp"], sc["n_txn"], sc["cc"]
     mode = sc.get("mode", 2)
     cap = n_txn * world * 10 + 4096 if mode == 2 else max(64, int(n_txn * world * 10 * 1.2 / world) + 4096)
-    eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=rank, asynchronous=False)
+    eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=rank, asynchronous=sc.get("asyn", False))
     try:
         eng.load_ycsb_partition(rows_pp)
-        eng.comm_init_ipc(name, world, rank)
-        eng.comm_set_mode(mode | (dvcc._lib.DV_COMM_WIDE_BATCHES if sc.get("wide") else 0))
+        # ordered lanes (bench.py --group-lanes): the lanes opened over this
+        # partition's tables before any communicator, one communicator each
+        lanes = [eng.open_lane() for _ in range(sc.get("lanes", 1) - 1)]
+        for ln, ctx in enumerate([eng] + lanes):
+            ctx.comm_init_ipc(name if ln == 0 else f"{name}_l{ln}", world, rank)
+            ctx.comm_set_mode(mode | (dvcc._lib.DV_COMM_WIDE_BATCHES if sc.get("wide") else 0))
+        if lanes:
+            eng.lanes_order(lanes)
         out = {}
         try:
-            if kind == "group":
+            if kind == "group" and lanes:
+                groups = [[dvcc.DeviceEpoch(b) for b in grp] for grp in _group_batches(sc, world, rank)]
+                ds = [torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda") for _ in groups]
+                half = len(groups) // 2  # (two calls: the order continues across them)
+                sts = eng.run_epoch_groups_ordered(groups[:half], n_txn, ds[:half])
+                sts += eng.run_epoch_groups_ordered(groups[half:], n_txn, ds[half:])
+                torch.cuda.synchronize()
+                out["commit"] = [d.cpu().numpy() for d in ds]
+                out["stats"] = [(s.committed, s.read_digest, s.write_cnt) for s in sts]
+            elif kind == "group":
                 groups = [[dvcc.DeviceEpoch(b) for b in grp] for grp in _group_batches(sc, world, rank)]
                 ds = [torch.zeros(n_txn * world, dtype=torch.uint8, device="cuda") for _ in groups]
                 sts = eng.run_epoch_groups(groups, n_txn, ds)
@@ -181,6 +196,32 @@ def test_ipc_epoch_groups_two_processes():
                 writes += w
             assert digest == sum(st.read_digest for _, st in refs[g]) % (1 << 64), (sc, g)
             assert writes == sum(st.write_cnt for _, st in refs[g]), (sc, g)
+        for r in range(WORLD):
+            assert (res[r][i]["table"] == f0[r::WORLD]).all(), (sc, r)
+
+
+def test_ipc_epoch_groups_ordered_lanes_two_processes():
+    """bench.py's N > 1 headline path (--group-lanes): each rank process opens
+    three decision lanes over its partition, one communicator per lane,
+    dv_lanes_order; 7 groups of two epochs over two calls, group g decided on
+    lane g % 4 of both ranks, executions in group order -- every epoch's
+    commit bytes, the digests and the rows against the oracle running the
+    sequenced epochs in order.  Asynchronous rounds on (the bench's)."""
+    base = dict(kind="group", rows_pp=1 << 13, n_txn=1500, mpr=0.3, groups=7, seed=140, lanes=4, asyn=True)
+    scs = [dict(base, cc=dvcc.NO_WAIT), dict(base, cc=dvcc.OCC, wide=True)]
+    res = _run_ranks(scs)
+    for i, sc in enumerate(scs):
+        refs, f0 = _oracle_groups(sc, WORLD)
+        n = sc["n_txn"]
+        for g in range(sc["groups"]):
+            committed = sum(st.committed for _, st in refs[g])
+            for r in range(WORLD):
+                out = res[r][i]
+                assert "error" not in out, (sc, r, out.get("error"))
+                for e in range(WORLD):
+                    assert (out["commit"][g][e * n:(e + 1) * n] == refs[g][e][0][r * n:(r + 1) * n]).all(), \
+                        (sc, g, e, r)
+                assert out["stats"][g][0] == committed, (sc, g, r)
         for r in range(WORLD):
             assert (res[r][i]["table"] == f0[r::WORLD]).all(), (sc, r)
 

@@ -272,13 +272,16 @@ def test_gpu_runner_single_rank_process_group():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1])
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC, dvcc.CALVIN])
-def test_rccl_engine_driver_single_rank(cc):
+def test_rccl_engine_driver_single_rank(cc, mode):
     """dv_comm_init + dv_epoch_run_part (RCCL called from the engine) on a
-    one-rank communicator: the owner split, all-to-all, list all-reduces and
-    lagged rounds run for real and must decide exactly as the single-GPU
-    path and the oracle.  (More ranks need more GPUs: the Python driver's
-    protocol, which this mirrors, is covered with gloo above.)"""
+    one-rank communicator: mode 1, the owner split, all-to-all, list
+    all-reduces and lagged rounds; mode 0, which picks the replicated epoch
+    whenever it fits (one rank too), the all-gathers -- run for real and must
+    decide exactly as the single-GPU path and the oracle.  (More ranks need
+    more GPUs: the Python driver's protocol, which this mirrors, is covered
+    with gloo above.)"""
     import torch
     rows, n_txn = 1 << 14, 6000
     gen = dvcc.YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
@@ -290,6 +293,7 @@ def test_rccl_engine_driver_single_rank(cc):
     eng = dvcc.CCEngine(cc, n_txn, e.n_acc, part_cnt=1, part_id=0)
     eng.load_ycsb_partition(rows)
     eng.comm_init(dvcc.comm_unique_id(), 1, 0)
+    eng.comm_set_mode(mode)
     c = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
     for _ in range(2):  # the communicator and buffers are reused across epochs
         eng.load_ycsb_partition(rows)
