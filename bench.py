@@ -99,11 +99,16 @@ def parse():
     ap.add_argument("--part-lanes", type=int, default=1,
                     help="N>1 TPC-C leg: ordered decision lanes per rank for dv_tpcc_epoch_run_part "
                          "(dv_lanes_order; opt-in)")
+    ap.add_argument("--no-txn-begin", action="store_true",
+                    help="A/B: device epochs without their txn boundaries (dv_epoch_dev::txn_begin), so prefix-kill "
+                         "epochs derive ranges from acc_txn and probe every access up front")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the config B (CALVIN) / C (OCC, 100M rows) legs and the CPU config A line")
     ap.add_argument("--tpcc-only", action="store_true", help="run and print only the TPC-C leg (profiling)")
     ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
     ap.add_argument("--tpcc-part-wh", type=int, default=256,
@@ -343,6 +348,94 @@ def closed_loop_lanes_leg(eng, lanes, gen, n_txn, k, open_ms=None):
     return out
 
 
+def config_leg(a, cfg, cc_name):
+    """BASELINE configs B (CALVIN, 65,536-txn epochs, zipf 0.6, 16,777,216
+    rows) and C (OCC, 1,048,576-txn epochs, zipf 0.9, 100,000,000 rows) on one
+    GPU, through the headline's entry point (decision lanes, pipelined, epochs
+    resident in HBM, 3 distinct epochs cycled), with their own kernel table
+    and roofline from one context right after the timed region, as the
+    headline's.  Not `value`."""
+    rows, n_txn, theta, desc = CONFIGS[cfg]
+    R = 10
+    gen = dvcc.YCSBQueryGenerator(rows, part_cnt=1, req_per_query=R, zipf_theta=theta, txn_write_perc=1.0,
+                                  tup_write_perc=0.5, part_per_txn=1, strict_ppt=1, mpr=-1.0)
+    t0 = time.perf_counter()
+    epochs = gen_epochs(gen, n_txn, 0, 3)
+    deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin) for e in epochs]
+    t_gen = time.perf_counter() - t0
+    eng = dvcc.CCEngine(cc_name, n_txn, max(e.n_acc for e in epochs), device=0, lsd_sort=a.lsd_sort)
+    eng.set_stream(torch.cuda.current_stream().cuda_stream)
+    eng.load_ycsb_partition(rows)
+    lanes = [eng.open_lane() for _ in range(max(1, a.lanes) - 1)]
+    d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
+    ne = len(deps)
+
+    def batch(first, count):
+        run = [deps[(first + i) % ne] for i in range(count)]
+        return eng.run_epochs_lanes(lanes, run, d_commit) if lanes else eng.run_epochs_device(run, d_commit)
+    k = max(12, min(a.steps, 24))
+    k = (k + max(1, len(lanes) + 1) - 1) // (len(lanes) + 1) * (len(lanes) + 1)
+    stats, el = timed(None, 0, a.warmup, k, 1, batch)
+    # the kernel table: one context, each launch with its own dispatch timestamps
+    eng.set_timing(False, profile=True)
+    eng.kernel_times(reset=True)
+    pstats = eng.run_epochs_device([deps[i % ne] for i in range(6)], d_commit)
+    ktimes = eng.kernel_times(reset=True)
+    eng.set_timing(False)
+    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, 1, tb=not a.no_txn_begin)
+    committed = sum(s.committed for s in stats)
+    out = {"workload": desc, "cc_alg": cc_name, "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
+           "committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el, "ms_per_epoch": el / k * 1e3,
+           "abort_rate": 1 - committed / (k * n_txn), "epochs": k, "distinct_epochs": ne,
+           "decision_lanes": 1 + len(lanes), "gen_seconds": t_gen,
+           "epoch_roofline": {"bytes_per_txn": BYTES_PER_ACCESS * R + 1,
+                              "achieved_GBps": k * n_txn / el * (BYTES_PER_ACCESS * R + 1) / 1e9,
+                              "frac": k * n_txn / el * (BYTES_PER_ACCESS * R + 1) / 1e9 / HBM_PEAK_GBPS},
+           "roofline": roofline(table, len(pstats), a), "kernels": table, "kernel_us_per_epoch": kus,
+           "stage_sizes_mean": {kk: float(np.mean([getattr(st, kk) for st in pstats]))
+                                for kk in ("n_txn", "n_acc", "prefix_txn", "prefix_acc", "surv_txn", "surv_acc")}}
+    for ln in lanes:
+        ln.close()
+    eng.close()
+    return out
+
+
+def cpu_config_a(seconds):
+    """BASELINE config A's CPU reference setting: NO_WAIT, THREAD_CNT = 4, zipf
+    0.6, 16,777,216 rows, the Deneva YCSB mix (TXN_WRITE_PERC 0.5,
+    TUP_WRITE_PERC 0.5, experiments.py:65-72), 10 requests -- on the
+    Deneva-style multi-threaded engine (oracle/mt_engine.c: per-row NO_WAIT
+    lock words, index probe, run_ycsb_1, no retry), 4 worker threads, epochs
+    of 65,536 txns, ~`seconds` of work.  A restatement of the reference CC on
+    the box's cores, not the reference binary."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    rows, threads, n = 16_777_216, 4, 65_536
+    gen = dvcc.YCSBQueryGenerator(rows, part_cnt=1, req_per_query=10, zipf_theta=0.6, txn_write_perc=0.5,
+                                  tup_write_perc=0.5, part_per_txn=1, strict_ppt=1, mpr=-1.0)
+    epochs = gen_epochs(gen, n, 0, 4)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    lock = np.zeros(rows, np.uint32)
+    committed = txns = i = 0
+    t0 = time.perf_counter()
+    while True:
+        e = epochs[i % len(epochs)]
+        c, _ = O.mt_epoch_run(tab.ix, f0, lock, e.n_txn, e.txn_begin, e.keys, e.types, threads)
+        committed += c
+        txns += e.n_txn
+        i += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": committed / el, "unit": "committed txns/s", "cores": threads, "kind": "port",
+            "abort_rate": 1 - committed / max(1, txns),
+            "sample": f"config A: NO_WAIT, THREAD_CNT=4, zipf 0.6, 16,777,216 rows, TXN_WRITE_PERC 0.5 / "
+                      f"TUP_WRITE_PERC 0.5, 10 requests; Deneva-style multi-threaded engine (oracle/mt_engine.c) "
+                      f"over {i} epoch(s) of {n} txns, {txns} txns in {el:.1f} s on 4 threads; restatement of the "
+                      "reference CC, not the reference binary"}
+
+
 def e2e_host_leg(eng, epochs, k):
     """SURVEY.md 8(d)'s second reading: epochs from host buffers, so the H2D
     copy of the 16-B access records is inside the time (pinned host memory,
@@ -484,7 +577,7 @@ def pmc_traffic(a, cc_name, world, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
-def epoch_bytes(st, rows, R, bucket=False):
+def epoch_bytes(st, rows, R, bucket=False, tb=False):
     """SURVEY.md 8(d) algorithmic bytes of each kernel for ONE epoch with the
     stats `st` (mean over the profiled epochs), counted on what the launches of
     that kernel actually processed: {kernel: (bytes per epoch, what is counted)}.
@@ -493,15 +586,16 @@ def epoch_bytes(st, rows, R, bucket=False):
     once, rounds being overhead).  Kernels not listed move only counters."""
     n_acc, n_txn = st["n_acc"], st["n_txn"]
     ka, kb = st["prefix_acc"], st["surv_acc"]          # keys the prefix's / survivors' sorts order
-    ta, tb = st["prefix_txn"], st["surv_txn"]
+    ta, tb_ = st["prefix_txn"], st["surv_txn"]
     keys = (ka + kb) if (ka or kb) else n_acc           # (no prefix: the whole epoch is sorted)
-    stage_txn = (ta + tb) if (ka or kb) else n_txn
+    stage_txn = (ta + tb_) if (ka or kb) else n_txn
     # bucket sorts (k_bucket_sort, small sorts): one histogram / scan /
     # scatter pass, then the bucket launch; else sort_passes LSD passes
     passes = 1 if bucket else max(1, st["sort_passes"])
     tiles = sum((k + 4095) // 4096 for k in ((ka, kb) if (ka or kb) else (n_acc,)))
     later = max(0, n_acc - ka)
     per_txn = n_acc / max(1, n_txn)
+    surv_all = st["surv_txn"] * per_txn if tb else 0  # tb: every access of a survivor probed by k_kill_emit
     out = {
         "k_epoch_clear": (10 * n_txn + (rows // 4 + (1 << 17) if ka else 0),
                           "per txn: status 1 + access range 8 + length 1 written; prefix epochs: the 2-bit "
@@ -524,21 +618,35 @@ def epoch_bytes(st, rows, R, bucket=False):
         "k_round_finalize": (5 * stage_txn, "per txn of the stage: fact word 4 read, status 1 written"),
         "k_prefix_mark": (9 * ta + 4 * ka * 0, "per prefix txn: status 1 + access range 8 (lower bound: the "
                                               "committed txns' rows are not counted)"),
-        "k_kill": (4 * later + later // 8, "per access after the prefix: row word 4 read + kill bit written"),
+        "k_probe_tb": (4 * n_txn + 22 * ka,
+                       "per txn: its boundary 4 read; per prefix access: key 8 + type 1 read, row word 4 + sort key 8 "
+                       "written, + 1 B of length per prefix txn (the later accesses are probed by k_kill)"),
+        "k_kill": ((9 if tb else 4) * later + later // 8,
+                   ("per access after the prefix: key 8 + type 1 read (the probe is here), kill bit written" if tb else
+                    "per access after the prefix: row word 4 read + kill bit written")),
         "k_kill_count": (13 * max(0, n_txn - ta) + later // 4,
                          "per later txn: access range 8 + status 1 + info word 4 written; kill and skip bits read"),
-        "k_kill_emit": (8 * max(0, n_txn - ta) + 12 * kb + 6 * tb,
-                        "per later txn: first access 4 + info word 4; per survivor access kept: row word 4 read + "
-                        "sort key 8 written; per survivor: map 4 + length 1 + status 1"),
-        "k_sub_scatter_back": (6 * tb, "per survivor: map 4 + status 1 read, status 1 written"),
+        "k_kill_emit": (8 * max(0, n_txn - ta) + (17 if tb else 12) * kb + 6 * tb_ + int(13 * surv_all),
+                        "per later txn: first access 4 + info word 4; per survivor access kept: "
+                        + ("key 8 + type 1 read, " if tb else "row word 4 read + ") + "sort key 8 written; per survivor: "
+                        "map 4 + length 1 + status 1" + ("; every access of a survivor: key 8 + type 1 read, row word "
+                                                          "4 written" if tb else "")),
+        "k_sub_scatter_back": (6 * tb_, "per survivor: map 4 + status 1 read, status 1 written"),
         "k_exec_txn": (10 * n_txn + int(12 * st["committed"] * per_txn),
                        "per txn: status 1 + access range 8 + commit byte 1; per committed access: row word 4 + "
                        "the 8-byte F0 field"),
+        # CALVIN (config B): row queues of the whole epoch, grant groups, execution in queue order
+        "k_seg_prepare": (16 * n_acc, "per access: sorted pair 8 read, queue element 8 written"),
+        "k_calvin_pass": (13 * n_acc, "per access: queue element 8 read, grant group 4 + read-after-write flag 1 "
+                                      "written"),
+        "k_exec": (13 * n_acc, "per launch (reads, then writes) and access: queue element 8 + flag 1 read, the "
+                               "8-byte F0 field of the half this launch executes"),
+        "k_commit_out": (2 * n_txn, "per txn: status 1 read, commit byte 1 written"),
     }
     return out
 
 
-def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1):
+def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1, tb=False):
     """Per-kernel table of the profiled epochs: launches per epoch, average
     launch time (its own dispatch timestamps), share of the epoch's kernel
     time, algorithmic bytes per launch (epoch_bytes), achieved GB/s and
@@ -550,7 +658,7 @@ def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1):
              "committed", "sort_passes")}
     mean["n_txn"] /= txn_div  # (epoch groups: the stats count the group's txns, n_acc the decided epoch's)
     mean["committed"] /= txn_div
-    eb = epoch_bytes(mean, rows, R, bucket="k_bucket_sort" in ktimes)
+    eb = epoch_bytes(mean, rows, R, bucket="k_bucket_sort" in ktimes, tb=tb)
     total_ms = sum(ms for _, ms in ktimes.values())
     rows_out = []
     for name, (launches, ms) in sorted(ktimes.items(), key=lambda kv: -kv[1][1]):
@@ -590,7 +698,7 @@ def roofline(table, epochs, a):
     out["timed_by"] = (f"each launch's own dispatch timestamps (hipExtLaunchKernelGGL events, "
                        f"dv_kernel_times) over {epochs} epochs run right after the timed region, same epochs "
                        "and stream, as the timed region runs them")
-    probe = next((r for r in table if r["kernel"] in ("k_probe", "k_probe_hist")), None)
+    probe = next((r for r in table if r["kernel"] in ("k_probe", "k_probe_hist", "k_probe_tb")), None)
     if probe is not None and probe is not top:
         out["k_probe"] = entry(probe)
     return out
@@ -937,7 +1045,7 @@ def main():
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)
-        deps = [dvcc.DeviceEpoch(e) for e in epochs]
+        deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin) for e in epochs]
         d_commit = torch.zeros(n_txn_total, dtype=torch.uint8, device="cuda")
 
         def step(i):
@@ -979,7 +1087,8 @@ def main():
         pb.unorder()
     pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats,
                                           batch1 if pipelined else None)
-    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1)
+    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1,
+                              tb=not part and not a.no_txn_begin)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"
     out = {
@@ -1056,9 +1165,22 @@ def main():
         print(out["deneva_summary"], file=sys.stderr, flush=True)
     if not part and not a.no_tpcc:
         out["tpcc"] = tpcc_leg(a)
+    if not part and not a.no_configs and a.config == "D":
+        eng.close()  # (the other configs' tables in its place)
+        eng = None
+        legs = {}
+        for cfg, cc in (("B", "CALVIN"), ("C", "OCC")):
+            try:
+                legs[f"config_{cfg.lower()}"] = config_leg(a, cfg, cc)
+            except Exception as ex:  # noqa: BLE001 -- the headline above is already measured
+                legs[f"config_{cfg.lower()}"] = {"error": repr(ex)}
+        out.update(legs)
+        if rank == 0 and not a.no_cpu_baseline:
+            out["cpu_config_a"] = cpu_config_a(min(a.cpu_seconds, 10.0))
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if world > 1:
         dist.destroy_process_group()
 

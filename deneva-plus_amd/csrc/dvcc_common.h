@@ -218,4 +218,62 @@ __device__ __forceinline__ void load_tile64(const uint64_t *__restrict__ src, ui
     if (tid == 0) *s_next = base + tile_n < n ? src[base + tile_n] : past_end;
 }
 
+// ------------------------------------------------------------------ probe
+// One index probe against table descriptor t.  Callers hand t over from
+// where it is uniform or cheap to index: the kernel arguments when the epoch
+// names no tables (YCSB: every access probes table 0, scalar registers), an
+// LDS copy of the descriptors otherwise -- indexing the kernel-argument array
+// with a per-lane table id compiles to a select chain over every descriptor
+// field, which cost a config-D probe 64 of its 172 us.
+// miss (optional): a missing key ORs true there instead of setting the error
+// bit here, so the caller can record it later (the probe keeps the tag
+// gather's latency off its path until the access's row is needed)
+__device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64_t key, uint64_t &row,
+                                          Counters *ctr, bool *miss = nullptr) {
+    if (!tb_ok) {
+        set_err(ctr, ERRB_TABLE);
+        return false;
+    }
+    if (t.rep_part != kNoRep) {  // replicated epoch: the key is the row; own keys checked here
+        uint64_t lo = 0;
+        const uint64_t q = divmod_magic(key, t.part_cnt, t.m_part, lo);
+        bool found = q < t.nbuckets;
+        if (found && lo == t.rep_part) found = direct_holds(t, q, (uint32_t)lo, key);
+        if (!found) set_err(ctr, ERRB_KEY);
+        row = key;
+        return found;
+    }
+    if (t.dense && t.part_cnt == 1 && t.htag == 0) {
+        // a dense one-partition map (every key 0 .. nbuckets - 1 in bucket =
+        // row = key, both hashes): the key check is one compare
+        const bool found = key < t.nbuckets;
+        if (!found) {
+            if (miss) *miss = true;
+            else set_err(ctr, ERRB_KEY);
+        }
+        row = key + t.row_base;
+        return found;
+    }
+    uint32_t tag;
+    const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
+    bool found = false;
+    if (t.pkey != nullptr) {                  // direct map, local row = bucket (key tags)
+        if (direct_holds(t, bk, tag, key)) { row = bk; found = true; }
+    } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
+        const IxEntry e = t.ix[bk];
+        if (e.key == key) { row = e.row; found = true; }
+    } else {                                  // chained bucket (read_item 217-231)
+        for (uint32_t j = t.bstart[bk], end = t.bstart[bk + 1]; j < end; j++) {
+            const IxEntry e = t.ix[j];
+            if (e.key == key) { row = e.row; found = true; break; }
+        }
+    }
+    if (!found) {
+        if (miss) *miss = true;
+        else set_err(ctr, ERRB_KEY);
+    }
+    row += t.row_base;
+    return found;
+}
+
 }  // namespace dvcc

@@ -277,6 +277,15 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr,
                   const uint64_t *ts = nullptr, const uint32_t *n_dev = nullptr);
 
+// prefix-kill epochs with their txn boundaries (dv_epoch_dev::txn_begin):
+// every txn's range checked, the prefix's txns [0, K) probed (acc_row, tlen,
+// sort keys; ctr->a_acc = txn_begin[K]); the later accesses are probed by
+// k_kill (launch_kill_compact with keys)
+void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
+                     const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K, uint32_t slog,
+                     uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr, const uint64_t *ts,
+                     hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
 // digit_tot: kRadix.  scatter_ev (optional): 2 events per pass for timing.
@@ -536,6 +545,15 @@ uint32_t kill_tiles(uint32_t n_after);  // look-back tiles of k_kill_compact (de
 // commits, which the survivors' sub-epoch leaves out) and k_kill_count /
 // k_kill_emit (killed txns aborted, the survivors' sub-epoch)
 uint64_t kill_words(uint64_t n_acc);
+// kk (an epoch with its txn boundaries, launch_probe_tb): the accesses after
+// the prefix were not probed -- k_kill probes their keys itself (a missing key:
+// ERRB_KEY, the epoch rejected) and k_kill_emit the survivors' (their acc_row
+// words, for the execution, and their sort keys)
+struct KillKeys {
+    Tables tabs;
+    const uint64_t *keys;
+    const uint8_t *types;
+};
 // (n_acc_dev: the epoch's real access count when n_acc is a bound, else null)
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
                          uint64_t n_acc, const uint32_t *n_acc_dev, uint32_t K, uint32_t n_txn,
@@ -543,7 +561,7 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          int nowait,
                          uint64_t *kill_bits, uint64_t *skip_bits, uint8_t *status, uint32_t *map,
                          uint8_t *status_b, uint8_t *tlen_b, uint64_t *pairs_b, uint32_t *info, uint32_t *tsum,
-                         Counters *ctr);
+                         Counters *ctr, const KillKeys *kk = nullptr);
 // (info: one word per txn after the prefix; tsum: 2 x kill_tiles words)
 // words (the survivors' asynchronous launch left their statuses there): their
 // statuses from the fact words, else from status_b

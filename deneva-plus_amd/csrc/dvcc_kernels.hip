@@ -27,52 +27,6 @@ namespace dvcc {
 
 // ------------------------------------------------------------------ probe
 
-// One index probe against table descriptor t.  Callers hand t over from
-// where it is uniform or cheap to index: the kernel arguments when the epoch
-// names no tables (YCSB: every access probes table 0, scalar registers), an
-// LDS copy of the descriptors otherwise -- indexing the kernel-argument array
-// with a per-lane table id compiles to a select chain over every descriptor
-// field, which cost a config-D probe 64 of its 172 us.
-// miss (optional): a missing key ORs true there instead of setting the error
-// bit here, so the caller can record it later (the probe keeps the tag
-// gather's latency off its path until the access's row is needed)
-__device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64_t key, uint64_t &row,
-                                          Counters *ctr, bool *miss = nullptr) {
-    if (!tb_ok) {
-        set_err(ctr, ERRB_TABLE);
-        return false;
-    }
-    if (t.rep_part != kNoRep) {  // replicated epoch: the key is the row; own keys checked here
-        uint64_t lo = 0;
-        const uint64_t q = divmod_magic(key, t.part_cnt, t.m_part, lo);
-        bool found = q < t.nbuckets;
-        if (found && lo == t.rep_part) found = direct_holds(t, q, (uint32_t)lo, key);
-        if (!found) set_err(ctr, ERRB_KEY);
-        row = key;
-        return found;
-    }
-    uint32_t tag;
-    const uint64_t bk = key_split(t, key, tag);  // (IndexHash::hash, index_hash.h:86-92)
-    bool found = false;
-    if (t.pkey != nullptr) {                  // direct map, local row = bucket (key tags)
-        if (direct_holds(t, bk, tag, key)) { row = bk; found = true; }
-    } else if (t.bstart == nullptr) {         // direct map: one {key, row} per bucket
-        const IxEntry e = t.ix[bk];
-        if (e.key == key) { row = e.row; found = true; }
-    } else {                                  // chained bucket (read_item 217-231)
-        for (uint32_t j = t.bstart[bk], end = t.bstart[bk + 1]; j < end; j++) {
-            const IxEntry e = t.ix[j];
-            if (e.key == key) { row = e.row; found = true; break; }
-        }
-    }
-    if (!found) {
-        if (miss) *miss = true;
-        else set_err(ctr, ERRB_KEY);
-    }
-    row += t.row_base;
-    return found;
-}
-
 // Input order: a txn's accesses are contiguous.  Each thread takes kPV
 // consecutive accesses (vector loads, kPV independent index probes in
 // flight).  Besides the sort key it records each txn's access range
@@ -363,6 +317,67 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
         DV_LAUNCH_EV(k_probe, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
                               tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
                               pair_limit < n_txn ? pair_limit : n_txn, ts, n_dev);
+}
+
+// The probe of a prefix-kill epoch whose txn boundaries come with it
+// (dv_epoch_dev::txn_begin): nothing per access is derived here any more --
+// each txn's range is [txn_begin[t], txn_begin[t + 1]) for every later kernel
+// -- so this launch touches only what the prefix's decision needs: a thread
+// per prefix txn (t < K) probes its accesses (IndexHash::index_read,
+// index_hash.cpp:137-153) into acc_row and the prefix's sort keys, and every
+// txn's boundaries are checked (ascending from 0 to n_acc: else ERRB_TXN; a
+// txn longer than 1 << slog: ERRB_BIG; WAIT_DIE timestamps rising: else
+// ERRB_TS).  The accesses after the prefix are probed by the kill pass
+// (k_kill with keys), which reads their keys once anyway.  Config D: 4.4 MB of
+// boundaries + the prefix's 3.3 MB instead of 190 MB.
+__global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t *__restrict__ keys,
+                                                     const uint8_t *__restrict__ types,
+                                                     const uint32_t *__restrict__ txn_begin, uint64_t n_acc,
+                                                     uint32_t n_txn, uint32_t K, uint32_t slog,
+                                                     uint64_t *__restrict__ pairs, uint8_t *__restrict__ tlen,
+                                                     uint32_t *__restrict__ acc_row, Counters *ctr,
+                                                     const uint64_t *__restrict__ ts) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctr->n_acc = (uint32_t)n_acc;
+        const uint64_t ak = txn_begin[K];
+        ctr->a_acc = (uint32_t)(ak < n_acc ? ak : n_acc);  // (a bad boundary is ERRB_TXN below)
+        if (txn_begin[0] != 0u || txn_begin[n_txn] != n_acc) set_err(ctr, ERRB_TXN);
+    }
+    bool bad = false, big_seen = false, ts_bad = false;
+    for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < n_txn; t += gridDim.x * kBlock) {
+        const uint32_t a0 = txn_begin[t], a1 = txn_begin[t + 1];
+        if (a1 < a0 || a1 > n_acc) {
+            bad = true;
+            continue;
+        }
+        const uint32_t len = a1 - a0;
+        const bool big = len > (1u << slog);
+        big_seen |= big;
+        if (ts && t > 0 && ts[t] <= ts[t - 1]) ts_bad = true;
+        if (t >= K) continue;
+        tlen[t] = (uint8_t)(big ? (1u << slog) : len);
+        for (uint32_t a = a0; a < a1; a++) {
+            uint64_t row = 0;
+            probe_row(tabs.t[0], tabs.n > 0, keys[a], row, ctr);
+            const uint32_t wr = types[a] == DV_WR ? 1u : 0u;
+            const uint32_t pos = a - a0;
+            acc_row[a] = (uint32_t)row | (wr ? AR_WR : 0u);
+            pairs[a] = pair_pack(row, t, (pos >> slog) ? 0u : pos, wr);
+        }
+    }
+    if (bad) set_err(ctr, ERRB_TXN);
+    if (big_seen) set_err(ctr, ERRB_BIG);
+    if (ts_bad) set_err(ctr, ERRB_TS);
+}
+
+void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
+                     const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K, uint32_t slog,
+                     uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr, const uint64_t *ts,
+                     hipEvent_t ev0, hipEvent_t ev1) {
+    uint32_t g = (n_txn + kBlock - 1) / kBlock;
+    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    DV_LAUNCH_EV(k_probe_tb, g, kBlock, 0, s, ev0, ev1, tabs, keys, types, txn_begin, n_acc, n_txn, K, slog, pairs,
+                 tlen, acc_row, ctr, ts);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -1175,8 +1190,10 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n_pad; i += stride) {
         status[i] = i < n_txn ? value : (uint8_t)ST_ABORT;
-        tb_start[i] = 0;
-        tb_end[i] = 0;
+        if (tb_start) {  // (null: the epoch's ranges come with it, dv_epoch_dev::txn_begin)
+            tb_start[i] = 0;
+            tb_end[i] = 0;
+        }
         if (tlen) tlen[i] = 0;
         if (zero8 && i < n_txn) zero8[i] = 0;
     }

@@ -152,12 +152,17 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
 // header comment; the txn id of an access is never needed here.)
 constexpr int kKillWords = 8;  // ballot words per wave per step (loads in flight)
 constexpr int kKillBlock = 1024;  // one block per CU (144 KiB of LDS): 16 waves to stream with
+// KEYS (an epoch with its txn boundaries, launch_probe_tb): the later
+// accesses were never probed -- their rows come from their keys here (the
+// dense YCSB map: arithmetic only), 9 bytes read per access instead of the
+// probe's 17 plus this pass's 4; a missing key rejects the epoch (ERRB_KEY)
+template <bool KEYS>
 __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
                                                  const uint32_t *__restrict__ n_dev,
                                                  const uint32_t *__restrict__ row_state, uint64_t state_words,
                                                  const uint32_t *__restrict__ bloom, int nowait,
                                                  uint64_t *__restrict__ kill_bits, uint64_t *__restrict__ skip_bits,
-                                                 const Counters *__restrict__ ctr) {
+                                                 Counters *__restrict__ ctr, KillKeys kk) {
     __shared__ uint32_t s_hot[kHotWords], s_bloom[kBloomWords];
     if (input_err(ctr) || ctr->halt) return;
     if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (rows past the real count were never probed)
@@ -171,10 +176,29 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
     for (uint64_t w = w0 + ((uint64_t)blockIdx.x * (kKillBlock / 64) + (threadIdx.x >> 6)) * kKillWords; w < nw;
          w += waves * kKillWords) {
         uint32_t ar[kKillWords];
+        if constexpr (KEYS) {
+            uint64_t key[kKillWords];
+            uint8_t ty[kKillWords];
 #pragma unroll
-        for (int q = 0; q < kKillWords; q++) {
-            const uint64_t i = ((w + q) << 6) + lane;
-            ar[q] = i >= first && i < n ? acc_row[i] : ~0u;
+            for (int q = 0; q < kKillWords; q++) {
+                const uint64_t i = ((w + q) << 6) + lane;
+                const bool in = i >= first && i < n;
+                key[q] = in ? kk.keys[i] : 0ull;
+                ty[q] = in ? kk.types[i] : (uint8_t)0xFF;
+            }
+#pragma unroll
+            for (int q = 0; q < kKillWords; q++) {
+                uint64_t row = 0;
+                ar[q] = ~0u;
+                if (ty[q] != 0xFF && probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[q], row, ctr))
+                    ar[q] = (uint32_t)row | (ty[q] == DV_WR ? AR_WR : 0u);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < kKillWords; q++) {
+                const uint64_t i = ((w + q) << 6) + lane;
+                ar[q] = i >= first && i < n ? acc_row[i] : ~0u;
+            }
         }
 #pragma unroll
         for (int q = 0; q < kKillWords; q++) {
@@ -298,15 +322,23 @@ __global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restric
     }
 }
 
+// KEYS (launch_probe_tb epochs): the survivors' accesses were never probed --
+// their rows come from their keys here: their sort keys, and acc_row for every
+// access of a survivor (the execution's, the skipped reads' included)
+template <bool KEYS>
 __global__ __launch_bounds__(kBlock) void k_kill_emit(
-    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ acc_row, uint32_t K, uint32_t n_txn,
+    const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end, uint32_t *__restrict__ acc_row,
+    uint32_t K, uint32_t n_txn,
     const uint64_t *__restrict__ skip_bits, const uint32_t *__restrict__ info, const uint32_t *__restrict__ tsum,
     uint32_t *__restrict__ map,
-    uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b, uint64_t *__restrict__ pairs_b, Counters *ctr) {
-    __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64];
-    __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc;
+    uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b, uint64_t *__restrict__ pairs_b, Counters *ctr,
+    KillKeys kk) {
+    __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64], wt_f[kBlock / 64];
+    __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc, s_nfull;
     __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
     __shared__ uint32_t l_st[kKillTile], l_len[kKillTile];      // per tile txn: first access, info word
+    // KEYS: per tile txn its end, per survivor the prefix of its whole length
+    __shared__ uint32_t l_end[KEYS ? kKillTile : 1], l_fpre[KEYS ? kKillTile + 1 : 1];
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;  // (b_txn = b_acc = 0 from the epoch clear)
@@ -318,6 +350,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
         const uint32_t t = t_lo + j * kBlock + tid;
         l_st[j * kBlock + tid] = t < n_txn ? tb_start[t] : 0u;
         l_len[j * kBlock + tid] = t < n_txn ? info[t - K] : 0u;
+        if constexpr (KEYS) l_end[j * kBlock + tid] = t < n_txn ? tb_end[t] : 0u;
     }
     if (wave < 2) {  // the tiles before this one: wave 0 survivors, wave 1 their accesses
         uint32_t sum = 0;
@@ -331,42 +364,50 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
     }
     __syncthreads();
     const uint32_t first = t_lo + tid * kKillIPT;
-    uint32_t surv = 0, cnt = 0, acc = 0;
-    uint32_t a0s[kKillIPT], lens[kKillIPT];
+    uint32_t surv = 0, cnt = 0, acc = 0, full = 0;
+    uint32_t a0s[kKillIPT], lens[kKillIPT], fls[kKillIPT];
 #pragma unroll
     for (int j = 0; j < kKillIPT; j++) {
         const uint32_t w = l_len[tid * kKillIPT + j];
         a0s[j] = l_st[tid * kKillIPT + j];
         lens[j] = w & 0x7FFFFFFFu;
+        fls[j] = KEYS ? l_end[tid * kKillIPT + j] - a0s[j] : 0u;
         if (!w) continue;
         surv |= 1u << j;
         cnt++;
         acc += lens[j];
+        full += fls[j];
     }
     const Agg inc_c = wave_incl<OpPlain>(Agg{0u, 0u, cnt}, lane);
     const Agg inc_a = wave_incl<OpPlain>(Agg{0u, 0u, acc}, lane);
+    const Agg inc_f = KEYS ? wave_incl<OpPlain>(Agg{0u, 0u, full}, lane) : Agg{0u, 0u, 0u};
     if (lane == 63) {
         wt_c[wave] = inc_c;
         wt_a[wave] = inc_a;
+        wt_f[wave] = inc_f;
     }
     __syncthreads();
     if (tid == 0) {
-        uint32_t c = 0, a = 0;
+        uint32_t c = 0, a = 0, f = 0;
         for (int w = 0; w < kBlock / 64; w++) {
             c += wt_c[w].c;
             a += wt_a[w].c;
+            f += wt_f[w].c;
         }
         s_nsurv = c;
         s_nacc = a;
+        s_nfull = f;
     }
     // this thread's survivors: their slots in the tile's list
-    uint32_t ls = 0, la = 0;
+    uint32_t ls = 0, la = 0, lf = 0;
     for (uint32_t w = 0; w < wave; w++) {
         ls += wt_c[w].c;
         la += wt_a[w].c;
+        lf += wt_f[w].c;
     }
     ls += wave_excl_from_incl<OpPlain>(inc_c, lane).c;
     la += wave_excl_from_incl<OpPlain>(inc_a, lane).c;
+    if constexpr (KEYS) lf += wave_excl_from_incl<OpPlain>(inc_f, lane).c;
     __syncthreads();
     const uint32_t sub0 = s_sub0;
 #pragma unroll
@@ -378,11 +419,47 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
         status_b[sub] = ST_UNDEC;
         l_a0[ls] = a0s[j];
         l_pre[ls] = la;
+        if constexpr (KEYS) l_fpre[ls] = lf;
         la += lens[j];
+        lf += fls[j];
         ls++;
     }
-    if (tid == 0) l_pre[s_nsurv] = s_nacc;
+    if (tid == 0) {
+        l_pre[s_nsurv] = s_nacc;
+        if constexpr (KEYS) l_fpre[s_nsurv] = s_nfull;
+    }
     __syncthreads();
+    if constexpr (KEYS) {
+        // every access of every survivor, one per thread: its acc_row word for
+        // the execution (the skipped reads' included), the key probed here
+        constexpr uint32_t kU = 4;
+        const uint32_t ns = s_nsurv, nf = s_nfull;
+        for (uint32_t g0 = 0; g0 < nf; g0 += kBlock * kU) {
+            uint32_t a[kU];
+            uint64_t key[kU];
+            uint8_t ty[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t g = g0 + u * kBlock + tid;
+                uint32_t lo = 0, hi = ns;  // largest k with l_fpre[k] <= g
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (l_fpre[mid] <= g) lo = mid;
+                    else hi = mid;
+                }
+                a[u] = l_a0[lo] + (g - l_fpre[lo]);
+                key[u] = g < nf ? kk.keys[a[u]] : 0ull;
+                ty[u] = g < nf ? kk.types[a[u]] : (uint8_t)0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                if (g0 + u * kBlock + tid >= nf) continue;
+                uint64_t row = 0;
+                probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[u], row, ctr);  // (k_kill found every key)
+                acc_row[a[u]] = (uint32_t)row | (ty[u] == DV_WR ? AR_WR : 0u);
+            }
+        }
+    }
     // the survivors' sort keys: one access per thread, its survivor found by
     // binary search over the access prefix
     // (kCompactU accesses per thread per step: their row gathers in flight together)
@@ -401,7 +478,14 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             }
             sv[u] = lo;
             qv[u] = g - l_pre[lo];
-            ar[u] = g < na ? acc_row[skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u]] : 0u;
+            const uint32_t a = g < na ? (skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u]) : 0u;
+            if constexpr (KEYS) {  // (the row from the key: this block's acc_row stores may not be visible yet)
+                uint64_t row = 0;
+                if (g < na) probe_row(kk.tabs.t[0], kk.tabs.n > 0, kk.keys[a], row, ctr);
+                ar[u] = g < na ? (uint32_t)row | (kk.types[a] == DV_WR ? AR_WR : 0u) : 0u;
+            } else {
+                ar[u] = g < na ? acc_row[a] : 0u;
+            }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kCompactU; u++) {
@@ -457,18 +541,28 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
                          int nowait,
                          uint64_t *kill_bits, uint64_t *skip_bits, uint8_t *status, uint32_t *map,
                          uint8_t *status_b, uint8_t *tlen_b, uint64_t *pairs_b, uint32_t *info, uint32_t *tsum,
-                         Counters *ctr) {
+                         Counters *ctr, const KillKeys *kk) {
     const uint32_t nt = kill_tiles(n_txn > K ? n_txn - K : 0u);
     if (!nt) return;
     const uint64_t nw = (n_acc + 63) / 64;
+    const KillKeys k0 = kk ? *kk : KillKeys{};
+    uint32_t *ar = const_cast<uint32_t *>(acc_row);  // (k_kill_emit writes the survivors' with keys)
     // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
-    DV_LAUNCH(k_kill, grid_of(nw * 64 / kKillWords / 4 + 1, 256), kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
-                                                                     row_state + (rs_words - kBloomWords), nowait,
-                                                                     kill_bits, skip_bits, ctr);
+    const uint32_t kg = grid_of(nw * 64 / kKillWords / 4 + 1, 256);
+    if (kk)
+        DV_LAUNCH(k_kill<true>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
+                  row_state + (rs_words - kBloomWords), nowait, kill_bits, skip_bits, ctr, k0);
+    else
+        DV_LAUNCH(k_kill<false>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
+                  row_state + (rs_words - kBloomWords), nowait, kill_bits, skip_bits, ctr, k0);
     DV_LAUNCH(k_kill_count, nt, kBlock, 0, s, tb_start, tb_end, K, n_txn, (const uint64_t *)kill_bits,
               (const uint64_t *)skip_bits, status, info, tsum, ctr);
-    DV_LAUNCH(k_kill_emit, nt, kBlock, 0, s, tb_start, acc_row, K, n_txn, (const uint64_t *)skip_bits, info, tsum, map,
-              status_b, tlen_b, pairs_b, ctr);
+    if (kk)
+        DV_LAUNCH(k_kill_emit<true>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
+                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0);
+    else
+        DV_LAUNCH(k_kill_emit<false>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
+                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

@@ -136,6 +136,11 @@ struct dv_ctx {
     uint32_t *acc_row = nullptr;                     // per access: row | wr << 31
     uint32_t *ulist[2] = {nullptr, nullptr};         // undecided txns, ping-pong
     uint32_t *tb_start = nullptr, *tb_end = nullptr; // per txn: its access range
+    // the current epoch's txn ranges for every kernel that reads them:
+    // tb_start / tb_end, or the epoch's own boundaries (dv_epoch_dev::txn_begin,
+    // rs = txn_begin, re = txn_begin + 1: run_prefix_epoch's tb mode)
+    const uint32_t *rs = nullptr, *re = nullptr;
+    bool tb_mode = false;
     uint64_t *desc = nullptr;                        // look-back tile descriptors
     uint32_t *tile_ctr = nullptr;                    // tile tickets, one per single-pass launch
     uint32_t *abounds = nullptr;                     // asynchronous-round slice carries
@@ -230,6 +235,7 @@ struct dv_ctx {
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
     const uint32_t *pf_n_acc_dev = nullptr;  // the epoch's device-side access count (dv_epoch_dev::n_acc_dev)
+    KillKeys pf_kk{};                        // tb mode: the keys k_kill / k_kill_emit probe
     int pf_sorted_a = 0, pf_key_bits = 0;
     uint64_t pf_n_acc = 0;
     uint32_t *row_state = nullptr; // 2 bits per row: the prefix's committed readers / writers
@@ -854,7 +860,7 @@ int dv_epoch_carry(dv_ctx *c, const dv_epoch_dev *ep, uint32_t max_txn, dv_epoch
     const uint32_t nb = carry_blocks(ep->n_txn);
     int r = carry_bufs(c, nb);
     if (r) return r;
-    launch_carry(c->stream, c->status, c->tb_start, c->tb_end, ep->n_txn, max_txn, ep->keys, ep->types,
+    launch_carry(c->stream, c->status, c->rs, c->re, ep->n_txn, max_txn, ep->keys, ep->types,
                  ep->tables, const_cast<uint64_t *>(out->keys), const_cast<uint8_t *>(out->types),
                  const_cast<uint32_t *>(out->acc_txn),
                  ep->tables ? const_cast<uint8_t *>(out->tables) : nullptr,
@@ -1266,6 +1272,9 @@ int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
     c->prefix_mode = false;
     c->rounds_prefix = 0;
     c->ms_probe = c->ms_sort = c->ms_decide = c->ms_exec = 0;
+    c->rs = c->tb_start;
+    c->re = c->tb_end;
+    c->tb_mode = false;
     view_epoch(c);
     return DV_OK;
 }
@@ -1478,7 +1487,7 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         if (c->cfg.cc_alg == DV_CALVIN)
             launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);
         else
-            launch_route_txn(c->stream, *c->route, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->ctr);
+            launch_route_txn(c->stream, *c->route, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->ctr);
     } else {
         RowMap rm{};  // replicated epoch: global rows -> this partition's
         if (c->rep_P) {
@@ -1489,7 +1498,7 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
             launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey, c->ctr,
                         rm);
         else {  // (the commit bytes and count too)
-            launch_exec_txn(c->stream, c->tb_start, c->tb_end, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
+            launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
                             c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit);
             return;
         }
@@ -1838,13 +1847,13 @@ int enqueue_survivors(dv_ctx *c) {
     const bool nowait = c->cfg.cc_alg != DV_OCC;
     const uint64_t rs_words = row_state_words(row_space(c));
     const uint32_t K = c->pf_K;
-    launch_prefix_mark(c->stream, c->status, c->tb_start, c->tb_end, c->acc_row, K, c->row_state, rs_words, nowait,
+    launch_prefix_mark(c->stream, c->status, c->rs, c->re, c->acc_row, K, c->row_state, rs_words, nowait,
                        c->ctr, c->prefix_words ? c->tword : nullptr);
-    launch_kill_compact(c->stream, c->tb_start, c->tb_end, c->acc_row, c->pf_n_acc, c->pf_n_acc_dev, K, c->n_txn,
+    launch_kill_compact(c->stream, c->rs, c->re, c->acc_row, c->pf_n_acc, c->pf_n_acc_dev, K, c->n_txn,
                         c->row_state, rs_words, nowait, c->kill_bits,
                         nowait ? c->kill_bits + kill_words(c->cfg.max_acc) : nullptr, c->status, c->b_map, c->b_status,
                         c->b_tlen,
-                        c->pairs[0], c->kinfo, c->ktsum, c->ctr);
+                        c->pairs[0], c->kinfo, c->ktsum, c->ctr, c->tb_mode ? &c->pf_kk : nullptr);
     // the survivors: renumbered 0..S-1, counts on the device
     c->sorted = sort_rows(c, c->pf_n_acc, c->pf_key_bits, nullptr, false, &c->ctr->b_acc);
     c->v_status = c->b_status;
@@ -1923,18 +1932,33 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->sort_passes = sort_launches(c, ep->n_acc, key_bits, false, true);
     c->prefix_mode = true;
     c->prefix_words = c->surv_words = false;
+    // tb mode: the epoch's own txn boundaries are every kernel's ranges, the
+    // prefix alone is probed here and the rest by the kill pass (k_probe_tb)
+    c->tb_mode = ep->txn_begin && !ep->n_acc_dev && !ep->tables && !c->keys32 && !c->rep_P && !c->route;
+    if (c->tb_mode) {
+        c->rs = ep->txn_begin;
+        c->re = ep->txn_begin + 1;
+        c->pf_kk = KillKeys{make_tables(c), ep->keys, ep->types};
+    }
     rec(c, 0);
     const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
     c->mir_pending = false;
-    launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_start, c->tb_end, c->tlen,
-                       c->tile_ctr, err_seed, c->ctr, c->row_state, rs_words, c->clear_gate,
+    launch_epoch_clear(c->stream, c->status, c->n_txn, c->n_txn_pad, ST_UNDEC, c->tb_mode ? nullptr : c->tb_start,
+                       c->tb_mode ? nullptr : c->tb_end, c->tb_mode ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr,
+                       c->row_state, rs_words, c->clear_gate,
                        mir ? c->d_mir[c->mir_slot] : nullptr, mir ? c->d_mseq[c->mir_slot] : nullptr,
                        mir ? c->mir_seq : 0ull);
     c->ticket = 0;
-    launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
-                 c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
-                 ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
-                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev);
+    if (c->tb_mode)
+        launch_probe_tb(c->stream, make_tables(c), ep->keys, ep->types, ep->txn_begin, ep->n_acc, ep->n_txn, K,
+                        c->slog, c->pairs[0], c->tlen, c->acc_row, c->ctr,
+                        c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ktiming(c) ? c->ev[kEvProbe0] : nullptr,
+                        ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+    else
+        launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
+                     c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
+                     ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
+                     c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         r = comm_combine_errors(c);
@@ -2585,7 +2609,7 @@ namespace {
 // ones from the pool
 void enqueue_refill(dv_ctx *c, const dv_epoch_dev *prev, const dv_epoch_dev *pool, const uint32_t *pool_begin,
                     uint32_t *cursor, uint32_t n_out, const dv_epoch_dev &out) {
-    launch_refill(c->stream, c->status, c->tb_start, c->tb_end, prev ? prev->n_txn : 0u,
+    launch_refill(c->stream, c->status, c->rs, c->re, prev ? prev->n_txn : 0u,
                   prev ? prev->keys : nullptr, prev ? prev->types : nullptr, prev ? prev->tables : nullptr,
                   pool->keys, pool->types, pool->tables, pool->acc_txn, pool_begin, pool->n_txn, cursor, n_out,
                   (uint64_t)n_out * pool->max_txn_acc, const_cast<uint64_t *>(out.keys),

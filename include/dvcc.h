@@ -173,6 +173,18 @@ typedef struct dv_epoch_dev {
                                 n_acc is then an upper bound.  NULL: n_acc is
                                 exact.  Single-GPU YCSB entry points, NO_WAIT /
                                 WAIT_DIE / OCC (DV_ERR_ARG otherwise). */
+    const uint32_t *txn_begin; /* (device, optional) [n_txn + 1] the same epoch's
+                                txn boundaries -- txn t's accesses are
+                                [txn_begin[t], txn_begin[t + 1]), from 0 to
+                                n_acc -- as dv_epoch_run takes them on the
+                                host.  Given (with an exact n_acc, no tables),
+                                a single-GPU prefix-kill epoch reads each txn's
+                                range from it instead of deriving it from
+                                acc_txn, and probes the accesses after the
+                                prefix inside the kill pass:
+                                acc_txn must still describe the same epoch
+                                (other paths read it).  Not ascending, or not
+                                ending at n_acc: DV_ERR_TXN_RANGE. */
 } dv_epoch_dev;
 
 typedef struct dv_stats {

@@ -1021,3 +1021,93 @@ def test_lanes_order_release_and_reorder():
     for ln in lanes:
         ln.close()
     eng.close()
+
+
+# ---- prefix-kill epochs with their txn boundaries (dv_epoch_dev::txn_begin:
+#      k_probe_tb probes the prefix, k_kill / k_kill_emit the later accesses)
+def _prefix_engine(cc, rows, n_txn, n_acc, prefix):
+    eng = CCEngine(cc, n_txn, n_acc)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(prefix)
+    return eng
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("rows,R,theta", [(1 << 18, 10, 0.9), (1 << 12, 16, 0.99), (1 << 16, 4, 0.5)])
+def test_prefix_epochs_with_and_without_txn_begin(cc, rows, R, theta):
+    """The same prefix-kill epochs through both range sources -- the epoch's
+    own boundaries and acc_txn -- give the oracle's commit bytes, digests,
+    write counts and table, epoch after epoch (repeated rows included)."""
+    g = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=R, txn_write_perc=1.0, tup_write_perc=0.5)
+    es = [g.gen(9_000, 1300 + k) for k in range(3)]
+    for with_tb in (True, False):
+        tab = O.YcsbTable(rows)
+        f0 = tab.f0.copy()
+        eng = _prefix_engine(cc, rows, 9_000, max(e.n_acc for e in es), 700)
+        for e in es:
+            c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+            d = torch.zeros(e.n_txn, dtype=torch.uint8, device="cuda")
+            dep = DeviceEpoch(e, txn_begin=with_tb)
+            st = eng.run_epoch_device(dep, d)
+            assert st.prefix_txn == 700, st.prefix_txn
+            assert (d.cpu().numpy() == c_ref).all(), with_tb
+            assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                                   st_ref.write_cnt), with_tb
+            assert (eng.read_table(0, rows) == f0).all(), with_tb
+        eng.close()
+
+
+@pytest.mark.parametrize("where", ["prefix", "later", "survivor"])
+def test_txn_begin_prefix_epoch_missing_key(where):
+    """A key no row holds -- in the prefix (k_probe_tb), in a later txn the
+    prefix kills or in one that survives (k_kill probes both) -- rejects the
+    whole epoch with DV_ERR_KEY_NOT_FOUND and no row changed; the context
+    then decides the next epoch bit-exact."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    e = g.gen(6_000, 1400)
+    i = {"prefix": 3, "later": int(e.txn_begin[3000]) + 1, "survivor": int(e.txn_begin[-2])}[where]
+    e.keys[i] = np.uint64(rows + 17)
+    eng = _prefix_engine(dvcc.NO_WAIT, rows, 6_000, e.n_acc, 500)
+    before = eng.read_table(0, rows)
+    with pytest.raises(dvcc.DvccError) as ex:
+        eng.run_epoch_device(DeviceEpoch(e), torch.zeros(6_000, dtype=torch.uint8, device="cuda"))
+    assert ex.value.code == dvcc._lib.DV_ERR_KEY_NOT_FOUND
+    assert (eng.read_table(0, rows) == before).all()
+    e2 = g.gen(6_000, 1401)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    c_ref, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e2)
+    d = torch.zeros(6_000, dtype=torch.uint8, device="cuda")
+    st = eng.run_epoch_device(DeviceEpoch(e2), d)
+    assert (d.cpu().numpy() == c_ref).all() and st.read_digest == st_ref.read_digest
+    eng.close()
+
+
+@pytest.mark.parametrize("bad", ["descending", "past_end", "short_end", "nonzero_start", "too_long"])
+def test_txn_begin_bad_boundaries(bad):
+    """Boundaries that do not describe an epoch (descending, past n_acc, not
+    ending at n_acc, not starting at 0) are DV_ERR_TXN_RANGE; a txn longer than
+    the declared bound DV_ERR_ARG -- before anything executes."""
+    rows = 1 << 14
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, req_per_query=20 if bad == "too_long" else 10)
+    e = g.gen(3_000, 1500)
+    eng = _prefix_engine(dvcc.NO_WAIT, rows, 3_000, e.n_acc, 256)
+    before = eng.read_table(0, rows)
+    dep = DeviceEpoch(e)
+    tb = dep.txn_begin
+    if bad == "descending":
+        tb[1000] = tb[1001] + 1
+    elif bad == "past_end":
+        tb[2000] = e.n_acc + 5
+    elif bad == "short_end":
+        tb[-1] = e.n_acc - 1
+    elif bad == "nonzero_start":
+        tb[0] = 1
+    else:
+        dep.max_txn_acc = 16  # 20 accesses per txn
+    with pytest.raises(dvcc.DvccError) as ex:
+        eng.run_epoch_device(dep, torch.zeros(3_000, dtype=torch.uint8, device="cuda"))
+    assert ex.value.code == (dvcc._lib.DV_ERR_ARG if bad == "too_long" else dvcc._lib.DV_ERR_TXN_RANGE), ex.value.code
+    assert (eng.read_table(0, rows) == before).all()
+    eng.close()
