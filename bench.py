@@ -102,6 +102,9 @@ def parse():
     ap.add_argument("--no-txn-begin", action="store_true",
                     help="A/B: device epochs without their txn boundaries (dv_epoch_dev::txn_begin), so prefix-kill "
                          "epochs derive ranges from acc_txn and probe every access up front")
+    ap.add_argument("--no-recs32", action="store_true",
+                    help="A/B: device epochs without their 4-byte records (dv_epoch_dev::recs32): keys and types "
+                         "read instead")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -361,7 +364,7 @@ def config_leg(a, cfg, cc_name):
                                   tup_write_perc=0.5, part_per_txn=1, strict_ppt=1, mpr=-1.0)
     t0 = time.perf_counter()
     epochs = gen_epochs(gen, n_txn, 0, 3)
-    deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin) for e in epochs]
+    deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin, recs32=not a.no_recs32) for e in epochs]
     t_gen = time.perf_counter() - t0
     eng = dvcc.CCEngine(cc_name, n_txn, max(e.n_acc for e in epochs), device=0, lsd_sort=a.lsd_sort)
     eng.set_stream(torch.cuda.current_stream().cuda_stream)
@@ -382,7 +385,8 @@ def config_leg(a, cfg, cc_name):
     pstats = eng.run_epochs_device([deps[i % ne] for i in range(6)], d_commit)
     ktimes = eng.kernel_times(reset=True)
     eng.set_timing(False)
-    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, 1, tb=not a.no_txn_begin)
+    table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, 1, tb=not a.no_txn_begin,
+                              recs=not a.no_txn_begin and not a.no_recs32)
     committed = sum(s.committed for s in stats)
     out = {"workload": desc, "cc_alg": cc_name, "zipf_theta": theta, "txn_write_perc": 1.0, "tup_write_perc": 0.5,
            "committed_per_s": committed / el, "decided_txns_per_s": k * n_txn / el, "ms_per_epoch": el / k * 1e3,
@@ -577,7 +581,7 @@ def pmc_traffic(a, cc_name, world, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(PMC_SUMMARY, ROOT)
 
 
-def epoch_bytes(st, rows, R, bucket=False, tb=False):
+def epoch_bytes(st, rows, R, bucket=False, tb=False, recs=False):
     """SURVEY.md 8(d) algorithmic bytes of each kernel for ONE epoch with the
     stats `st` (mean over the profiled epochs), counted on what the launches of
     that kernel actually processed: {kernel: (bytes per epoch, what is counted)}.
@@ -618,19 +622,25 @@ def epoch_bytes(st, rows, R, bucket=False, tb=False):
         "k_round_finalize": (5 * stage_txn, "per txn of the stage: fact word 4 read, status 1 written"),
         "k_prefix_mark": (9 * ta + 4 * ka * 0, "per prefix txn: status 1 + access range 8 (lower bound: the "
                                               "committed txns' rows are not counted)"),
-        "k_probe_tb": (4 * n_txn + 22 * ka,
-                       "per txn: its boundary 4 read; per prefix access: key 8 + type 1 read, row word 4 + sort key 8 "
-                       "written, + 1 B of length per prefix txn (the later accesses are probed by k_kill)"),
-        "k_kill": ((9 if tb else 4) * later + later // 8,
-                   ("per access after the prefix: key 8 + type 1 read (the probe is here), kill bit written" if tb else
-                    "per access after the prefix: row word 4 read + kill bit written")),
+        "k_probe_tb": (4 * n_txn + (16 if recs else 21) * ka + ta,
+                       "per txn: its boundary 4 read; per prefix access: " + ("4-byte record" if recs else
+                                                                            "key 8 + type 1") +
+                       " read, row word 4 + sort key 8 written; 1 B of length per prefix txn (the later accesses are "
+                       "probed by k_kill)"),
+        "k_kill": ((4 if (recs or not tb) else 9) * later + later // 8,
+                   ("per access after the prefix: " + ("its 4-byte record" if recs else "key 8 + type 1") +
+                    " read (the probe is here), kill bit written") if tb else
+                   "per access after the prefix: row word 4 read + kill bit written"),
         "k_kill_count": (13 * max(0, n_txn - ta) + later // 4,
                          "per later txn: access range 8 + status 1 + info word 4 written; kill and skip bits read"),
-        "k_kill_emit": (8 * max(0, n_txn - ta) + (17 if tb else 12) * kb + 6 * tb_ + int(13 * surv_all),
+        "k_kill_emit": (8 * max(0, n_txn - ta) + (12 if (recs or not tb) else 17) * kb + 6 * tb_ +
+                        int((8 if recs else 13) * surv_all),
                         "per later txn: first access 4 + info word 4; per survivor access kept: "
-                        + ("key 8 + type 1 read, " if tb else "row word 4 read + ") + "sort key 8 written; per survivor: "
-                        "map 4 + length 1 + status 1" + ("; every access of a survivor: key 8 + type 1 read, row word "
-                                                          "4 written" if tb else "")),
+                        + ("its record 4 read, " if (tb and recs) else ("key 8 + type 1 read, " if tb else
+                                                                        "row word 4 read + ")) +
+                        "sort key 8 written; per survivor: map 4 + length 1 + status 1"
+                        + (("; every access of a survivor: " + ("record 4" if recs else "key 8 + type 1") +
+                            " read, row word 4 written") if tb else "")),
         "k_sub_scatter_back": (6 * tb_, "per survivor: map 4 + status 1 read, status 1 written"),
         "k_exec_txn": (10 * n_txn + int(12 * st["committed"] * per_txn),
                        "per txn: status 1 + access range 8 + commit byte 1; per committed access: row word 4 + "
@@ -646,7 +656,7 @@ def epoch_bytes(st, rows, R, bucket=False, tb=False):
     return out
 
 
-def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1, tb=False):
+def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1, tb=False, recs=False):
     """Per-kernel table of the profiled epochs: launches per epoch, average
     launch time (its own dispatch timestamps), share of the epoch's kernel
     time, algorithmic bytes per launch (epoch_bytes), achieved GB/s and
@@ -658,7 +668,7 @@ def kernel_table(ktimes, sts, rows, R, a, cc_name, world, txn_div=1, tb=False):
              "committed", "sort_passes")}
     mean["n_txn"] /= txn_div  # (epoch groups: the stats count the group's txns, n_acc the decided epoch's)
     mean["committed"] /= txn_div
-    eb = epoch_bytes(mean, rows, R, bucket="k_bucket_sort" in ktimes, tb=tb)
+    eb = epoch_bytes(mean, rows, R, bucket="k_bucket_sort" in ktimes, tb=tb, recs=recs)
     total_ms = sum(ms for _, ms in ktimes.values())
     rows_out = []
     for name, (launches, ms) in sorted(ktimes.items(), key=lambda kv: -kv[1][1]):
@@ -970,7 +980,9 @@ def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
                                "committed_per_s": wc / wel, "decided_txns_per_s": len(wst) * n_txn_total * world / wel,
                                "ms_per_epoch": wel / len(wst) * 1e3,
                                "abort_rate": 1 - wc / (len(wst) * n_txn_total * world), "epochs": len(wst),
-                               "mpr": mpr, "protocol": "dv_epoch_run_part, list protocol (the epoch exceeds a context)"}
+                               "mpr": mpr,
+                               "protocol": ("dv_epoch_run_part, list protocol (the epoch exceeds a context)" if world > 1
+                                            else "dv_epoch_run_part on one rank: the strong leg's epoch size, replicated")}
         del wdeps
         nxt += 100
     sweep = []
@@ -1045,7 +1057,7 @@ def main():
         eng.set_prefix(None if a.prefix < 0 else a.prefix)
         eng.set_stream(torch.cuda.current_stream().cuda_stream)
         eng.load_ycsb_partition(rows)
-        deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin) for e in epochs]
+        deps = [dvcc.DeviceEpoch(e, txn_begin=not a.no_txn_begin, recs32=not a.no_recs32) for e in epochs]
         d_commit = torch.zeros(n_txn_total, dtype=torch.uint8, device="cuda")
 
         def step(i):
@@ -1088,7 +1100,7 @@ def main():
     pstats, sstats, ktimes = measure_legs(a, eng, step, a.warmup + a.steps, stats,
                                           batch1 if pipelined else None)
     table, kus = kernel_table(ktimes, pstats, rows, R, a, cc_name, world, world if (part and a.protocol == "group") else 1,
-                              tb=not part and not a.no_txn_begin)
+                              tb=not part and not a.no_txn_begin, recs=not part and not a.no_txn_begin and not a.no_recs32)
     committed = sum(s.committed for s in stats)  # global: every rank holds the same decisions
     group = part and a.protocol == "group"
     out = {

@@ -282,9 +282,9 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
 // sort keys; ctr->a_acc = txn_begin[K]); the later accesses are probed by
 // k_kill (launch_kill_compact with keys)
 void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
-                     const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K, uint32_t slog,
-                     uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr, const uint64_t *ts,
-                     hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                     const uint32_t *recs, const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K,
+                     uint32_t slog, uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr,
+                     const uint64_t *ts, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -553,7 +553,18 @@ struct KillKeys {
     Tables tabs;
     const uint64_t *keys;
     const uint8_t *types;
+    const uint32_t *recs;  // (optional) the same as 4-byte records, key | write << 31 (dv_epoch_dev::recs32)
 };
+// access a of a KillKeys epoch: its key and write bit
+__device__ __forceinline__ uint64_t kk_key(const KillKeys &kk, uint64_t a, uint32_t &wr) {
+    if (kk.recs) {
+        const uint32_t r = kk.recs[a];
+        wr = r >> 31;
+        return r & 0x7FFFFFFFu;
+    }
+    wr = kk.types[a] == DV_WR ? 1u : 0u;
+    return kk.keys[a];
+}
 // (n_acc_dev: the epoch's real access count when n_acc is a bound, else null)
 void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end, const uint32_t *acc_row,
                          uint64_t n_acc, const uint32_t *n_acc_dev, uint32_t K, uint32_t n_txn,

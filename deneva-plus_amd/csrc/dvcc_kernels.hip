@@ -332,6 +332,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
 // boundaries + the prefix's 3.3 MB instead of 190 MB.
 __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t *__restrict__ keys,
                                                      const uint8_t *__restrict__ types,
+                                                     const uint32_t *__restrict__ recs,
                                                      const uint32_t *__restrict__ txn_begin, uint64_t n_acc,
                                                      uint32_t n_txn, uint32_t K, uint32_t slog,
                                                      uint64_t *__restrict__ pairs, uint8_t *__restrict__ tlen,
@@ -356,13 +357,26 @@ __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t
         if (ts && t > 0 && ts[t] <= ts[t - 1]) ts_bad = true;
         if (t >= K) continue;
         tlen[t] = (uint8_t)(big ? (1u << slog) : len);
-        for (uint32_t a = a0; a < a1; a++) {
-            uint64_t row = 0;
-            probe_row(tabs.t[0], tabs.n > 0, keys[a], row, ctr);
-            const uint32_t wr = types[a] == DV_WR ? 1u : 0u;
-            const uint32_t pos = a - a0;
-            acc_row[a] = (uint32_t)row | (wr ? AR_WR : 0u);
-            pairs[a] = pair_pack(row, t, (pos >> slog) ? 0u : pos, wr);
+        constexpr uint32_t kU = 8;  // (a chunk's key and type loads in flight together)
+        for (uint32_t j0 = 0; j0 < len; j0 += kU) {
+            uint64_t key[kU];
+            uint32_t wrs[kU];
+            const KillKeys kk{tabs, keys, types, recs};
+#pragma unroll
+            for (uint32_t j = 0; j < kU; j++) {
+                wrs[j] = 0;
+                key[j] = j0 + j < len ? kk_key(kk, a0 + j0 + j, wrs[j]) : 0ull;
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < kU; j++) {
+                if (j0 + j >= len) break;
+                uint64_t row = 0;
+                probe_row(tabs.t[0], tabs.n > 0, key[j], row, ctr);
+                const uint32_t wr = wrs[j];
+                const uint32_t pos = j0 + j;
+                acc_row[a0 + pos] = (uint32_t)row | (wr ? AR_WR : 0u);
+                pairs[a0 + pos] = pair_pack(row, t, (pos >> slog) ? 0u : pos, wr);
+            }
         }
     }
     if (bad) set_err(ctr, ERRB_TXN);
@@ -371,13 +385,13 @@ __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t
 }
 
 void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
-                     const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K, uint32_t slog,
-                     uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr, const uint64_t *ts,
-                     hipEvent_t ev0, hipEvent_t ev1) {
+                     const uint32_t *recs, const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K,
+                     uint32_t slog, uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr,
+                     const uint64_t *ts, hipEvent_t ev0, hipEvent_t ev1) {
     uint32_t g = (n_txn + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
-    DV_LAUNCH_EV(k_probe_tb, g, kBlock, 0, s, ev0, ev1, tabs, keys, types, txn_begin, n_acc, n_txn, K, slog, pairs,
-                 tlen, acc_row, ctr, ts);
+    DV_LAUNCH_EV(k_probe_tb, g, kBlock, 0, s, ev0, ev1, tabs, keys, types, recs, txn_begin, n_acc, n_txn, K, slog,
+                 pairs, tlen, acc_row, ctr, ts);
 }
 
 // ------------------------------------------------------------- radix sort

@@ -178,20 +178,21 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
         uint32_t ar[kKillWords];
         if constexpr (KEYS) {
             uint64_t key[kKillWords];
-            uint8_t ty[kKillWords];
+            uint32_t wr[kKillWords];
+            bool in[kKillWords];
 #pragma unroll
             for (int q = 0; q < kKillWords; q++) {
                 const uint64_t i = ((w + q) << 6) + lane;
-                const bool in = i >= first && i < n;
-                key[q] = in ? kk.keys[i] : 0ull;
-                ty[q] = in ? kk.types[i] : (uint8_t)0xFF;
+                in[q] = i >= first && i < n;
+                wr[q] = 0;
+                key[q] = in[q] ? kk_key(kk, i, wr[q]) : 0ull;
             }
 #pragma unroll
             for (int q = 0; q < kKillWords; q++) {
                 uint64_t row = 0;
                 ar[q] = ~0u;
-                if (ty[q] != 0xFF && probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[q], row, ctr))
-                    ar[q] = (uint32_t)row | (ty[q] == DV_WR ? AR_WR : 0u);
+                if (in[q] && probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[q], row, ctr))
+                    ar[q] = (uint32_t)row | (wr[q] ? AR_WR : 0u);
             }
         } else {
 #pragma unroll
@@ -332,13 +333,16 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
     const uint64_t *__restrict__ skip_bits, const uint32_t *__restrict__ info, const uint32_t *__restrict__ tsum,
     uint32_t *__restrict__ map,
     uint8_t *__restrict__ status_b, uint8_t *__restrict__ tlen_b, uint64_t *__restrict__ pairs_b, Counters *ctr,
-    KillKeys kk) {
+    KillKeys kk, const uint32_t *__restrict__ row_state, int nowait) {
     __shared__ Agg wt_c[kBlock / 64], wt_a[kBlock / 64], wt_f[kBlock / 64];
     __shared__ uint32_t s_sub0, s_ab0, s_nsurv, s_nacc, s_nfull;
     __shared__ uint32_t l_a0[kKillTile], l_pre[kKillTile + 1];  // per survivor: first access, access prefix
     __shared__ uint32_t l_st[kKillTile], l_len[kKillTile];      // per tile txn: first access, info word
-    // KEYS: per tile txn its end, per survivor the prefix of its whole length
+    // KEYS: per tile txn its end; per survivor the prefix of its whole length
+    // and its skipped accesses (bit j: access j reads a row only committed
+    // prefix readers hold, k_kill's skip rule)
     __shared__ uint32_t l_end[KEYS ? kKillTile : 1], l_fpre[KEYS ? kKillTile + 1 : 1];
+    __shared__ uint32_t l_skip[KEYS ? kKillTile : 1];
     const uint32_t m = n_txn > K ? n_txn - K : 0u;
     const uint32_t ntiles = (m + kKillTile - 1) / kKillTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;  // (b_txn = b_acc = 0 from the epoch clear)
@@ -419,7 +423,10 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
         status_b[sub] = ST_UNDEC;
         l_a0[ls] = a0s[j];
         l_pre[ls] = la;
-        if constexpr (KEYS) l_fpre[ls] = lf;
+        if constexpr (KEYS) {
+            l_fpre[ls] = lf;
+            l_skip[ls] = 0;
+        }
         la += lens[j];
         lf += fls[j];
         ls++;
@@ -435,9 +442,8 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
         constexpr uint32_t kU = 4;
         const uint32_t ns = s_nsurv, nf = s_nfull;
         for (uint32_t g0 = 0; g0 < nf; g0 += kBlock * kU) {
-            uint32_t a[kU];
+            uint32_t a[kU], wr[kU];
             uint64_t key[kU];
-            uint8_t ty[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; u++) {
                 const uint32_t g = g0 + u * kBlock + tid;
@@ -448,17 +454,35 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
                     else hi = mid;
                 }
                 a[u] = l_a0[lo] + (g - l_fpre[lo]);
-                key[u] = g < nf ? kk.keys[a[u]] : 0ull;
-                ty[u] = g < nf ? kk.types[a[u]] : (uint8_t)0;
+                wr[u] = 0;
+                key[u] = g < nf ? kk_key(kk, a[u], wr[u]) : 0ull;
+            }
+            uint32_t rows[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                uint64_t row = 0;
+                if (g0 + u * kBlock + tid < nf)
+                    probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[u], row, ctr);  // (the kill found every key)
+                rows[u] = (uint32_t)row;
             }
 #pragma unroll
             for (uint32_t u = 0; u < kU; u++) {
-                if (g0 + u * kBlock + tid >= nf) continue;
-                uint64_t row = 0;
-                probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[u], row, ctr);  // (k_kill found every key)
-                acc_row[a[u]] = (uint32_t)row | (ty[u] == DV_WR ? AR_WR : 0u);
+                const uint32_t g = g0 + u * kBlock + tid;
+                if (g >= nf) continue;
+                acc_row[a[u]] = rows[u] | (wr[u] ? AR_WR : 0u);
+                // the skip rule (k_kill), from the row state itself
+                if (nowait && !wr[u] && row_bits(row_state, rows[u]) == RS_RD) {
+                    uint32_t lo = 0, hi = ns;
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (l_fpre[mid] <= g) lo = mid;
+                        else hi = mid;
+                    }
+                    atomicOr(&l_skip[lo], 1u << (g - l_fpre[lo]));
+                }
             }
         }
+        __syncthreads();
     }
     // the survivors' sort keys: one access per thread, its survivor found by
     // binary search over the access prefix
@@ -478,11 +502,21 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             }
             sv[u] = lo;
             qv[u] = g - l_pre[lo];
-            const uint32_t a = g < na ? (skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u]) : 0u;
+            uint32_t a = 0;
+            if (g < na) {
+                if constexpr (KEYS) {  // the qv-th access of the survivor whose skip bit is clear
+                    uint32_t kept = ~l_skip[lo];
+                    for (uint32_t r = qv[u]; r; r--) kept &= kept - 1;
+                    a = l_a0[lo] + (uint32_t)__builtin_ctz(kept);
+                } else {
+                    a = skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u];
+                }
+            }
             if constexpr (KEYS) {  // (the row from the key: this block's acc_row stores may not be visible yet)
                 uint64_t row = 0;
-                if (g < na) probe_row(kk.tabs.t[0], kk.tabs.n > 0, kk.keys[a], row, ctr);
-                ar[u] = g < na ? (uint32_t)row | (kk.types[a] == DV_WR ? AR_WR : 0u) : 0u;
+                uint32_t w = 0;
+                if (g < na) probe_row(kk.tabs.t[0], kk.tabs.n > 0, kk_key(kk, a, w), row, ctr);
+                ar[u] = g < na ? (uint32_t)row | (w ? AR_WR : 0u) : 0u;
             } else {
                 ar[u] = g < na ? acc_row[a] : 0u;
             }
@@ -559,10 +593,10 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
               (const uint64_t *)skip_bits, status, info, tsum, ctr);
     if (kk)
         DV_LAUNCH(k_kill_emit<true>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
-                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0);
+                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0, row_state, nowait);
     else
         DV_LAUNCH(k_kill_emit<false>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
-                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0);
+                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0, row_state, nowait);
 }
 
 void launch_sub_scatter_back(hipStream_t s, const uint32_t *map, const uint8_t *status_b, uint32_t ub,

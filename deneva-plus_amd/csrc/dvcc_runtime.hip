@@ -1938,7 +1938,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     if (c->tb_mode) {
         c->rs = ep->txn_begin;
         c->re = ep->txn_begin + 1;
-        c->pf_kk = KillKeys{make_tables(c), ep->keys, ep->types};
+        c->pf_kk = KillKeys{make_tables(c), ep->keys, ep->types, ep->recs32};
     }
     rec(c, 0);
     const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
@@ -1950,7 +1950,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
                        mir ? c->mir_seq : 0ull);
     c->ticket = 0;
     if (c->tb_mode)
-        launch_probe_tb(c->stream, make_tables(c), ep->keys, ep->types, ep->txn_begin, ep->n_acc, ep->n_txn, K,
+        launch_probe_tb(c->stream, make_tables(c), ep->keys, ep->types, ep->recs32, ep->txn_begin, ep->n_acc,
+                        ep->n_txn, K,
                         c->slog, c->pairs[0], c->tlen, c->acc_row, c->ctr,
                         c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ktiming(c) ? c->ev[kEvProbe0] : nullptr,
                         ktiming(c) ? c->ev[kEvProbe1] : nullptr);

@@ -60,7 +60,7 @@ class EpochDev(ctypes.Structure):
     _fields_ = [("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("acc_txn", ctypes.c_void_p),
                 ("tables", ctypes.c_void_p), ("n_acc", ctypes.c_uint64), ("n_txn", ctypes.c_uint32),
                 ("max_txn_acc", ctypes.c_uint32), ("ts", ctypes.c_void_p), ("n_acc_dev", ctypes.c_void_p),
-                ("txn_begin", ctypes.c_void_p)]
+                ("txn_begin", ctypes.c_void_p), ("recs32", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):

@@ -78,7 +78,7 @@ class Epoch:
 class DeviceEpoch:
     """An epoch resident in HBM (torch tensors used as device buffers)."""
 
-    def __init__(self, epoch, device="cuda", txn_begin=True):
+    def __init__(self, epoch, device="cuda", txn_begin=True, recs32=True):
         import torch
         self.n_txn = epoch.n_txn
         self.n_acc = epoch.n_acc
@@ -91,6 +91,14 @@ class DeviceEpoch:
         # the txns' boundaries too (dv_epoch_dev.txn_begin): a prefix-kill
         # epoch then reads ranges from them (acc_txn stays, other paths read it)
         self.txn_begin = torch.from_numpy(epoch.txn_begin.astype(np.int32)).to(device) if txn_begin else None
+        # ... and its accesses as 4-byte records (key | write << 31) where they
+        # fit one (dv_epoch_dev::recs32: table-0 reads / writes, keys < 2^31)
+        self.recs32 = None
+        if txn_begin and recs32:
+            try:
+                self.recs32 = torch.from_numpy(epoch.to_row_records().view(np.int32)).to(device)
+            except ValueError:
+                pass
         # every txn id below the last one used has an access (what the compact
         # epoch-group batches need, dv_epoch_group_run); None = unknown
         n = np.diff(epoch.txn_begin.astype(np.int64))
@@ -103,7 +111,7 @@ class DeviceEpoch:
         then assumes the 128-access maximum)."""
         self = cls.__new__(cls)
         self.keys, self.types, self.acc_txn, self.tables = keys, types, acc_txn, tables
-        self.txn_begin = None
+        self.txn_begin = self.recs32 = None
         self.n_acc = int(keys.numel())
         self.n_txn = int(n_txn)
         self.max_txn_acc = int(max_txn_acc)
@@ -128,10 +136,11 @@ class DeviceEpoch:
     def desc(self):
         ts = getattr(self, "ts", None)
         tb = getattr(self, "txn_begin", None)
+        r32 = getattr(self, "recs32", None)
         return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
                           self.tables.data_ptr() if self.tables is not None else None,
                           self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None,
-                          None, tb.data_ptr() if tb is not None else None)
+                          None, tb.data_ptr() if tb is not None else None, r32.data_ptr() if r32 is not None else None)
 
 
 class ClosedLoopBufs:

@@ -185,6 +185,13 @@ typedef struct dv_epoch_dev {
                                 acc_txn must still describe the same epoch
                                 (other paths read it).  Not ascending, or not
                                 ending at n_acc: DV_ERR_TXN_RANGE. */
+    const uint32_t *recs32;  /* (device, optional, with txn_begin) [n_acc] the same
+                                accesses as 4-byte records, key | write << 31
+                                (table-0 reads and writes, keys below 2^31: the
+                                records of dv_epoch_stage_host_rows).  Given, a
+                                prefix-kill epoch reads them instead of keys and
+                                types (4 bytes per access instead of 9); keys
+                                and types must still describe the same epoch. */
 } dv_epoch_dev;
 
 typedef struct dv_stats {

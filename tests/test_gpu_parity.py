@@ -1036,18 +1036,20 @@ def _prefix_engine(cc, rows, n_txn, n_acc, prefix):
 @pytest.mark.parametrize("rows,R,theta", [(1 << 18, 10, 0.9), (1 << 12, 16, 0.99), (1 << 16, 4, 0.5)])
 def test_prefix_epochs_with_and_without_txn_begin(cc, rows, R, theta):
     """The same prefix-kill epochs through both range sources -- the epoch's
-    own boundaries and acc_txn -- give the oracle's commit bytes, digests,
-    write counts and table, epoch after epoch (repeated rows included)."""
+    own boundaries (with its accesses as 4-byte records or as keys and types)
+    and acc_txn -- give the oracle's commit bytes, digests, write counts and
+    table, epoch after epoch (repeated rows included)."""
     g = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=R, txn_write_perc=1.0, tup_write_perc=0.5)
     es = [g.gen(9_000, 1300 + k) for k in range(3)]
-    for with_tb in (True, False):
+    for with_tb, recs in ((True, True), (True, False), (False, False)):  # (+ 4-byte records, dv_epoch_dev::recs32)
         tab = O.YcsbTable(rows)
         f0 = tab.f0.copy()
         eng = _prefix_engine(cc, rows, 9_000, max(e.n_acc for e in es), 700)
         for e in es:
             c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
             d = torch.zeros(e.n_txn, dtype=torch.uint8, device="cuda")
-            dep = DeviceEpoch(e, txn_begin=with_tb)
+            dep = DeviceEpoch(e, txn_begin=with_tb, recs32=recs)
+            assert (dep.recs32 is not None) == recs
             st = eng.run_epoch_device(dep, d)
             assert st.prefix_txn == 700, st.prefix_txn
             assert (d.cpu().numpy() == c_ref).all(), with_tb

@@ -19,11 +19,12 @@ run_one() {
   mkdir -p $out
   case $cmd in
   tests)
-    local sel="$*"
-    timeout -k 10 1500 python -u -m pytest ${sel:-tests} -m gpu -x -v --timeout 600 --timeout-method thread \
+    local -a sel=("$@")
+    [ ${#sel[@]} -eq 0 ] && sel=(tests)
+    timeout -k 10 1500 python -u -m pytest "${sel[@]}" -m gpu -x -v --timeout 600 --timeout-method thread \
         > $out/pytest_gpu.log 2>&1 || { tail -60 $out/pytest_gpu.log; return 1; }
     tail -3 $out/pytest_gpu.log
-    if [ -z "$sel" ]; then run_one smoke $tag; fi ;;
+    if [ $# -eq 0 ]; then run_one smoke $tag; fi ;;
   smoke)
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 \
         || { tail -30 $out/smoke.log; return 1; }
