@@ -80,6 +80,10 @@ def parse():
     ap.add_argument("--part-mode", type=int, default=0,
                     help="N>1: dv_comm_set_mode -- 0 replicated when the epoch fits, else the list protocol; "
                          "1 list protocol; 2 replicated; + 4: 8-byte epoch-group batches (DV_COMM_WIDE_BATCHES)")
+    ap.add_argument("--order", choices=["position", "origin"], default="position",
+                    help="N>1 epoch groups, NO_WAIT / WAIT_DIE / OCC: the origins' batches of an epoch sequenced txn "
+                         "by txn (DV_COMM_POSITION_ORDER, origin q's txn j at j * N + q -- clients of all nodes "
+                         "arriving together) or batch by batch (Calvin's lock order, which CALVIN always keeps)")
     ap.add_argument("--prefix", type=int, default=0,
                     help="prefix-kill decisions (dv_set_prefix): 0 automatic, -1 off, K txns")
     ap.add_argument("--epochs", type=int, default=5,
@@ -816,10 +820,12 @@ class PartitionedBench:
             if a.protocol == "group" and not a.no_pipeline else 1
         self.lanes = [self.eng.open_lane() for _ in range(nl - 1)]
         engine_comm_init(a, self.eng, world, rank, "ycsb")
-        self.eng.comm_set_mode(a.part_mode)
+        # (the order flag matters to epoch groups only)
+        mode = a.part_mode | (dvcc._lib.DV_COMM_POSITION_ORDER if a.order == "position" else 0)
+        self.eng.comm_set_mode(mode)
         for ln, lane in enumerate(self.lanes):
             engine_comm_init(a, lane, world, rank, f"ycsb_lane{ln + 1}")
-            lane.comm_set_mode(a.part_mode)
+            lane.comm_set_mode(mode)
         self.lanes_refused = None
         if self.lanes:
             ok = 1
@@ -1135,6 +1141,9 @@ def main():
                           2: "replicated"}[a.part_mode] if part else "single GPU"),
             "distinct_epochs": n_epochs,
             "decision_lanes": 1 + (len(pb.lanes) if part else len(lanes)),
+            "sequence_order": ("position-major (origin q's txn j at j * N + q, DV_COMM_POSITION_ORDER)"
+                               if group and a.order == "position" and cc_name != "CALVIN" else
+                               "origin-major (Calvin's lock order)") if part else "one origin",
         },
         "roofline": roofline(table, len(pstats), a),
         "timing_in_timed_region": a.timing,

@@ -200,16 +200,19 @@ __global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restri
 }
 
 // epoch groups: row id | wr << 31 and the global txn id, 8 B per access
+// (txn t of this origin is t * stride + txn_base: origin-major stride 1, base
+// rank * tpr; position-major stride P, base rank)
 __global__ __launch_bounds__(kBlock) void k_group_pack(const uint64_t *__restrict__ keys,
                                                        const uint8_t *__restrict__ types,
                                                        const uint32_t *__restrict__ txn, uint64_t n,
-                                                       uint32_t tpr, uint32_t txn_base, uint32_t *__restrict__ k32,
-                                                       uint32_t *__restrict__ t32) {
+                                                       uint32_t tpr, uint32_t stride, uint32_t txn_base,
+                                                       uint32_t *__restrict__ k32, uint32_t *__restrict__ t32) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = keys[i];
         // a key past 31 bits saturates and fails the decider's range check
         k32[i] = ((k >> 31) ? 0x7FFFFFFFu : (uint32_t)k) | (types[i] == DV_WR ? 0x80000000u : 0u);
-        t32[i] = global_txn(txn[i], tpr, txn_base);
+        const uint32_t t = txn[i];
+        t32[i] = t < tpr ? t * stride + txn_base : kBadTxn;
     }
 }
 
@@ -260,6 +263,7 @@ constexpr int kXIPT = 16;
 constexpr uint32_t kXTile = kBlock * kXIPT;
 struct XSegs {
     uint32_t P, tpr;
+    uint64_t mP, mT;  // div_magic(P), div_magic(tpr): position-major index arithmetic
     uint64_t eoff[kXMaxP + 1];
     uint32_t toff[kXMaxP + 1];
 };
@@ -279,11 +283,13 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t *red) {
     return t;
 }
 
-// txn starts per tile
+// txn starts per tile (and, position-major, the origins' txn counts zeroed
+// for k_group_txn_ids)
 __global__ __launch_bounds__(kBlock) void k_group_txn_count(const uint32_t *__restrict__ rk, XSegs s,
-                                                            uint32_t *__restrict__ cnt) {
+                                                            uint32_t *__restrict__ cnt, uint32_t *__restrict__ ncnt) {
     __shared__ uint32_t red[kBlock / 64];
     const uint32_t tile = blockIdx.x, q = xseg_of(s, tile);
+    if (ncnt && tile == 0 && threadIdx.x < s.P) ncnt[threadIdx.x] = 0;
     const uint64_t b0 = s.eoff[q] + (uint64_t)(tile - s.toff[q]) * kXTile;
     const uint64_t e = b0 + kXTile < s.eoff[q + 1] ? b0 + kXTile : s.eoff[q + 1];
     uint32_t c = 0;
@@ -293,9 +299,13 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_count(const uint32_t *__re
 }
 
 // global txn id of every access (origin q's txn j is q * tpr + j, the id
-// dv_epoch_group_run gives it) into rt, the start bits cleared from rk
+// dv_epoch_group_run gives it; position-major, tbo non-null: the origin-local
+// j, and each txn's first access within its origin's segment into tbo, the
+// origin's txn count into ncnt -- k_il_begin) into rt, the start bits cleared
+// from rk
 __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__ rk, XSegs s,
-                                                          const uint32_t *__restrict__ cnt, uint32_t *__restrict__ rt) {
+                                                          const uint32_t *__restrict__ cnt, uint32_t *__restrict__ rt,
+                                                          uint32_t *__restrict__ tbo, uint32_t *__restrict__ ncnt) {
     __shared__ uint32_t red[kBlock / 64], wt[2][kBlock / 64];
     const uint32_t tile = blockIdx.x, q = xseg_of(s, tile);
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -303,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
     const uint64_t e = b0 + kXTile < s.eoff[q + 1] ? b0 + kXTile : s.eoff[q + 1];
     uint32_t pre = 0;  // the starts of this origin's earlier tiles
     for (uint32_t k = s.toff[q] + threadIdx.x; k < tile; k += kBlock) pre += cnt[k];
-    uint32_t run = block_sum(pre, red) + q * s.tpr;
+    uint32_t run = block_sum(pre, red);  // (origin-local txn numbers)
     for (uint32_t u = 0; u < (uint32_t)kXIPT; u++) {  // 256 consecutive accesses per step
         const uint64_t i = b0 + (uint64_t)u * kBlock + threadIdx.x;
         const uint32_t w = i < e ? rk[i] : 0u;
@@ -316,10 +326,129 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
         for (uint32_t v = 0; v < wave; v++) base += wt[p][v];
         const uint32_t incl = base + (uint32_t)__popcll(m & ((2ull << lane) - 1ull));
         if (i < e) {
-            rt[i] = incl - 1u;
+            const uint32_t j = incl - 1u;  // (a batch with more txns than tpr fails the pack's check)
             rk[i] = w & ~GP_START;
+            if (tbo) {
+                rt[i] = j;
+                if (f && j < s.tpr) tbo[(uint64_t)q * (s.tpr + 1) + j] = (uint32_t)(i - s.eoff[q]);
+                if (i + 1 == s.eoff[q + 1]) ncnt[q] = j < s.tpr ? j + 1 : s.tpr;
+            } else {
+                rt[i] = q * s.tpr + j;
+            }
         }
         run += wt[p][0] + wt[p][1] + wt[p][2] + wt[p][3];
+    }
+}
+
+// ---- position-major epochs (DV_COMM_POSITION_ORDER; not CALVIN, whose
+// order is the sequencer's origin by origin): origin q's txn j is sequence
+// number j * P + q -- the origins' batches interleaved txn by txn, as
+// clients arriving together -- so the decider's prefix (its first n / 32
+// txns) holds every origin's first txns and kills in every partition, where
+// origin-major it holds origin 0's only.  The batches land contiguous per
+// origin; tbo[q * (tpr + 1) + j] is txn j's first access inside origin q's
+// segment, ncnt[q] entries valid (later j: the segment's end).
+__device__ __forceinline__ uint32_t il_start(const XSegs &s, const uint32_t *__restrict__ tbo,
+                                             const uint32_t *__restrict__ ncnt, uint32_t q, uint32_t j) {
+    return j < ncnt[q] ? tbo[(uint64_t)q * (s.tpr + 1) + j] : (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
+}
+
+// wide batches (the senders' ids): tbo by a lower bound over each segment's
+// ids, sorted in a well-formed batch (k_il_move checks what it moves)
+__global__ __launch_bounds__(kBlock) void k_il_bounds(const uint32_t *__restrict__ rt, XSegs s,
+                                                      uint32_t *__restrict__ tbo, uint32_t *__restrict__ ncnt) {
+    const uint64_t n = (uint64_t)s.P * (s.tpr + 1);
+    for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < n; x += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t q = (uint32_t)(x / (s.tpr + 1)), j = (uint32_t)(x % (s.tpr + 1));
+        const uint64_t t = (uint64_t)j * s.P + q;  // (j == tpr: past every id of the segment)
+        uint64_t lo = s.eoff[q], hi = s.eoff[q + 1];
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((uint64_t)rt[mid] < t) lo = mid + 1;
+            else hi = mid;
+        }
+        tbo[x] = (uint32_t)(lo - s.eoff[q]);
+        if (j == 0) ncnt[q] = s.tpr + 1;
+    }
+}
+
+// tb[t]: where sequence number t = j * P + q starts in the interleaved epoch
+// -- after txns 0..j of origins 0..q-1 and txns 0..j-1 of origins q..P-1 --
+// which is the decider's txn_begin (tb[P * tpr] = every access), and shift
+// [q * tpr + j] = tb[t] minus the txn's first access inside its segment (the
+// move's one lookup per access)
+__global__ __launch_bounds__(kBlock) void k_il_begin(XSegs s, const uint32_t *__restrict__ tbo,
+                                                     const uint32_t *__restrict__ ncnt, uint32_t *__restrict__ tb,
+                                                     uint32_t *__restrict__ shift) {
+    const uint32_t n = s.P * s.tpr;
+    for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t <= n; t += gridDim.x * kBlock) {
+        uint64_t qq = 0;
+        const uint32_t j = (uint32_t)divmod_magic(t, s.P, s.mP, qq), q = (uint32_t)qq;
+        uint32_t d = 0, own = 0;
+        for (uint32_t o = 0; o < s.P; o++) {
+            const uint32_t st = il_start(s, tbo, ncnt, o, o < q ? j + 1 : j);
+            d += st;
+            if (o == q) own = st;
+        }
+        tb[t] = d;
+        if (t < n) shift[(uint64_t)q * s.tpr + j] = d - own;
+    }
+}
+
+// every landed access to its place in the interleaved epoch (tiles of one
+// origin, as k_group_txn_ids): position i of origin q's segment goes to
+// (i - eoff[q]) + shift of its txn.  WIDE (the senders' ids in rt): an id that
+// is not this origin's, past the epoch, or out of order (a malformed batch) is
+// not moved and fails the group (*bad, voted with the outcome: DV_ERR_ARG on
+// every rank); every store stays inside its txn's [tb[t], tb[t + 1]) and below
+// n_acc.  ot (NULL when the decider reads the boundaries only, tb mode): the
+// sequence number per access.
+template <bool WIDE>
+__global__ __launch_bounds__(kBlock) void k_il_move(const uint32_t *__restrict__ rk, const uint32_t *__restrict__ rt,
+                                                    XSegs s, const uint32_t *__restrict__ shift,
+                                                    const uint32_t *__restrict__ tb, uint64_t n_acc,
+                                                    uint32_t *__restrict__ ok, uint32_t *__restrict__ ot,
+                                                    uint32_t *__restrict__ bad) {
+    const uint32_t tile = blockIdx.x, q = xseg_of(s, tile);
+    const uint64_t b0 = s.eoff[q] + (uint64_t)(tile - s.toff[q]) * kXTile;
+    const uint64_t e = b0 + kXTile < s.eoff[q + 1] ? b0 + kXTile : s.eoff[q + 1];
+    const uint32_t n = s.P * s.tpr;
+    bool b = false;
+#pragma unroll 4
+    for (uint64_t i = b0 + threadIdx.x; i < e; i += kBlock) {
+        const uint32_t v = rt[i];
+        uint32_t j = v, t = 0;
+        bool good = true;
+        if (WIDE) {
+            uint64_t qq = 0;
+            j = (uint32_t)divmod_magic(v, s.P, s.mP, qq);
+            good = v < n && (uint32_t)qq == q && (i == s.eoff[q] || rt[i - 1] <= v);
+            t = v;
+        } else {
+            good = j < s.tpr;  // (a batch with too many txns: the pack's check fails the group)
+            t = j * s.P + q;
+        }
+        if (good) {
+            const uint64_t d = (i - s.eoff[q]) + shift[(uint64_t)q * s.tpr + j];
+            good = d < n_acc && (!WIDE || (d >= tb[t] && d < tb[t + 1]));
+            if (good) {
+                ok[d] = rk[i];
+                if (ot) ot[d] = t;
+            }
+        }
+        b |= !good;
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+// the decided commit bytes back in origin order: out[q * tpr + j] = v[j * P + q]
+__global__ __launch_bounds__(kBlock) void k_il_commits(const uint8_t *__restrict__ v, XSegs s,
+                                                       uint8_t *__restrict__ out) {
+    const uint64_t n = (uint64_t)s.P * s.tpr;
+    for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < n; x += (uint64_t)gridDim.x * kBlock) {
+        uint64_t j = 0;
+        const uint64_t q = divmod_magic(x, s.tpr, s.mT, j);
+        out[x] = v[j * s.P + q];
     }
 }
 
@@ -583,9 +712,11 @@ __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const ui
 constexpr uint32_t kGroupRecHead = 8;
 __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
                               uint64_t cap, uint64_t *__restrict__ rec, uint32_t *__restrict__ pack_bad) {
-    // a compact batch with txn ids that are not dense (k_group_pack_c) fails
-    // the group as an argument error; the flag is reset for the next group
-    if (!fail && *pack_bad) fail = (uint32_t)(-DV_ERR_ARG);
+    // a compact batch with txn ids that are not dense (k_group_pack_c), or a
+    // batch the position-major move refused (k_il_move), fails the group as an
+    // argument error -- whatever its decision made of the input; the flag is
+    // reset for the next group
+    if (*pack_bad) fail = (uint32_t)(-DV_ERR_ARG);
     __syncthreads();
     if (threadIdx.x == 0) *pack_bad = 0;
     for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) rec[kGroupRecHead + q] = fail ? 0u : tot[q];
@@ -654,6 +785,11 @@ struct DvComm {
     uint64_t *gs = nullptr, *gr = nullptr;      // all-gathered vote / outcome records: [8 + P], [P][8 + P]
     uint32_t *gtc = nullptr;                    // compact batches: txn starts per received tile
     uint32_t *gbad = nullptr;                   // compact batches: a sender's txn ids were not dense
+    bool position = false;                      // epoch groups: position-major (DV_COMM_POSITION_ORDER)
+    uint32_t *ilk = nullptr, *ilt = nullptr;    // position-major: the interleaved epoch's rows, txn ids
+    uint32_t *tbo = nullptr, *ncnt = nullptr;   // k_il_begin's inputs
+    uint32_t *iltb = nullptr, *ilsh = nullptr;  // ... its outputs: the decider's txn_begin, the move's shifts
+    uint8_t *ilv = nullptr;                     // commit bytes back in origin order
 };
 
 }  // namespace dvcc
@@ -992,7 +1128,7 @@ void free_bufs(DvComm *m) {
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
-                 m->gs, m->gr, m->gtc, m->gbad};
+                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -1006,6 +1142,8 @@ void free_bufs(DvComm *m) {
     m->xacc = nullptr;
     m->gs = m->gr = nullptr;
     m->gtc = m->gbad = nullptr;
+    m->ilk = m->ilt = m->tbo = m->ncnt = m->iltb = m->ilsh = nullptr;
+    m->ilv = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -1040,6 +1178,15 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->gtc, acc / kXTile + kXMaxP + 2));
     CHK(alloc(&m->gbad, 1));
     CHK(hip_fail2(hipMemset(m->gbad, 0, sizeof(uint32_t)), "memset"));
+    if (!tpcc) {  // (position-major epoch groups)
+        CHK(alloc(&m->ilk, acc));
+        CHK(alloc(&m->ilt, acc));
+        CHK(alloc(&m->tbo, (uint64_t)txn + P));
+        CHK(alloc(&m->ncnt, kXMaxP));
+        CHK(alloc(&m->iltb, (uint64_t)txn + 1));
+        CHK(alloc(&m->ilsh, txn));
+        CHK(alloc(&m->ilv, txn));
+    }
     const size_t mail_bytes = sizeof(CommMail) + 8 * mail_words(P);
     CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), mail_bytes,
                                 hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc"));
@@ -1505,6 +1652,9 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     rec[4] = std::min<uint64_t>(cfg.max_acc, acap);
     // compact batches (k_group_pack_c) need the global row ids below 2^30
     rec[5] = capable && !m->wide && P <= kXMaxP && ctx_table0_rows(c) * P < (1ull << 30) ? 0u : 1u;
+    // position-major sequence (DV_COMM_POSITION_ORDER; CALVIN keeps its origin order)
+    const bool il = m->position && cfg.cc_alg != DV_CALVIN && P > 1 && P <= kXMaxP;  // (one origin: the same order)
+    rec[6] = il ? 1u : 0u;
     for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
     // (and the compact pack's bad flag cleared for this group: a group that
     // failed after setting it must not leave it to the next one)
@@ -1528,7 +1678,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         const uint64_t *r = &all[(size_t)q * W];
         gmax = std::max<uint64_t>(gmax, r[0]);
         compact &= r[5] == 0;
-        refuse |= r[1] || r[2] || r[3] != all[3];
+        refuse |= r[1] || r[2] || r[3] != all[3] || r[6] != all[6];  // (every rank the same order)
         uint64_t in = 0;  // what rank q receives: its epoch's batches
         for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
         refuse |= in > r[4];
@@ -1564,14 +1714,15 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         } else if (n) {
             const uint32_t blocks = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
             DV_LAUNCH(k_group_pack, blocks, kBlock, 0, s, homes[e].keys, homes[e].types, homes[e].acc_txn, n,
-                                                   txns_per_rank, (uint32_t)m->rank * txns_per_rank, sk + so, stx + so);
+                      txns_per_rank, il ? P : 1u, il ? (uint32_t)m->rank : (uint32_t)m->rank * txns_per_rank,
+                      sk + so, stx + so);
         }
         sc[e] = 4 * n;
         sd[e] = 4 * so;
         so += n;
         rc[e] = 4 * recvc[e];
         rd[e] = 4 * ro;
-        if (compact) {
+        if (compact || il) {
             xs.eoff[e] = ro;
             xs.toff[e] = xtiles;
             xtiles += (uint32_t)((recvc[e] + kXTile - 1) / kXTile);
@@ -1590,14 +1741,16 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
                               reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
     CHK(m->x->group(false));
+    xs.eoff[P] = ro;
+    xs.toff[P] = xtiles;
+    xs.mP = div_magic(P);
+    xs.mT = div_magic(txns_per_rank);
     if (compact && xtiles) {
-        xs.eoff[P] = ro;
-        xs.toff[P] = xtiles;
-        DV_LAUNCH(k_group_txn_count, xtiles, kBlock, 0, s, rk, xs, m->gtc);
-        DV_LAUNCH(k_group_txn_ids, xtiles, kBlock, 0, s, rk, xs, m->gtc, rt);
+        DV_LAUNCH(k_group_txn_count, xtiles, kBlock, 0, s, rk, xs, m->gtc, il ? m->ncnt : nullptr);
+        DV_LAUNCH(k_group_txn_ids, xtiles, kBlock, 0, s, rk, xs, m->gtc, rt, il ? m->tbo : nullptr,
+                  il ? m->ncnt : nullptr);
         CHK(hip_fail2(hipGetLastError(), "k_group_txn_ids"));
     }
-
     // 3. decide this rank's epoch; its committed accesses are routed into the
     //    send area (free again once the batches have left)
     dv_epoch_dev ep{};
@@ -1608,9 +1761,38 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     ep.n_acc = ro;
     ep.n_txn = (uint32_t)n_txn64;
     ep.max_txn_acc = glen;
+    const uint32_t *ek = rk;
+    if (il) {
+        // position-major: the landed batches interleaved txn by txn, with the
+        // epoch's boundaries -- a prefix-kill decider then reads those and the
+        // 32-bit rows as its records (tb mode), no per-access txn ids
+        ek = m->ilk;
+        ep.keys = reinterpret_cast<const uint64_t *>(ek);
+        ep.txn_begin = m->iltb;
+        ep.recs32 = ek;
+        const bool tb = group_tb_epoch(c, &ep);
+        ep.acc_txn = tb ? nullptr : m->ilt;
+        const uint64_t nt = (uint64_t)P * txns_per_rank;
+        if (!xtiles) {  // (no accesses: every txn empty)
+            CHK(hip_fail2(hipMemsetAsync(m->iltb, 0, 4 * (nt + 1), s), "memset"));
+        } else {
+            if (!compact)
+                DV_LAUNCH(k_il_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0,
+                          s, rt, xs, m->tbo, m->ncnt);
+            DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs,
+                      m->tbo, m->ncnt, m->iltb, m->ilsh);
+            if (compact)
+                DV_LAUNCH(k_il_move<false>, xtiles, kBlock, 0, s, rk, rt, xs, m->ilsh, m->iltb, ro, m->ilk,
+                          tb ? nullptr : m->ilt, m->gbad);
+            else
+                DV_LAUNCH(k_il_move<true>, xtiles, kBlock, 0, s, rk, rt, xs, m->ilsh, m->iltb, ro, m->ilk,
+                          tb ? nullptr : m->ilt, m->gbad);
+        }
+        CHK(hip_fail2(hipGetLastError(), "k_il_move"));
+    }
     const RouteOut rout{reinterpret_cast<uint2 *>(m->send), m->rblk, m->rtot, P};
     dv_stats est{};
-    const int rd_ = epoch_run_replicated(c, &ep, rk, P, m->verdict, &est, &rout);
+    const int rd_ = epoch_run_replicated(c, &ep, ek, P, m->verdict, &est, &rout);
 
     // 4. one all-gather of every rank's outcome record: a failure on any rank
     //    (or an owner whose receive area is too small) fails the group on
@@ -1650,10 +1832,18 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         ud[q] = (size_t)q * txns_per_rank;
     }
     uint8_t *commit_out = d_commit ? d_commit : m->gcommit;
+    const uint8_t *vsend = m->verdict;
+    if (il) {  // (the commit bytes in origin order again)
+        const uint64_t nt = (uint64_t)P * txns_per_rank;
+        DV_LAUNCH(k_il_commits, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nt + kBlock - 1) / kBlock, 2048)),
+                  kBlock, 0, s, m->verdict, xs, m->ilv);
+        CHK(hip_fail2(hipGetLastError(), "k_il_commits"));
+        vsend = m->ilv;
+    }
     CHK(m->x->group(true));
     CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->send), sc.data(), sd.data(),
                           reinterpret_cast<uint8_t *>(m->recv), rc.data(), rd.data(), s));
-    CHK(m->x->all_to_allv(m->verdict, tc.data(), td.data(), commit_out, uc.data(), ud.data(), s));
+    CHK(m->x->all_to_allv(vsend, tc.data(), td.data(), commit_out, uc.data(), ud.data(), s));
     CHK(m->x->group(false));
 
     // 6. epochs 0..P-1 on this partition's rows, in order (2PL: a written row
@@ -1732,11 +1922,13 @@ int dv_epoch_group_run_batch(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_gr
 }
 
 int dv_comm_set_mode(dv_ctx *c, int mode) {
-    if (!c || (mode & ~DV_COMM_WIDE_BATCHES) < 0 || (mode & ~DV_COMM_WIDE_BATCHES) > 2) return DV_ERR_ARG;
+    const int flags = DV_COMM_WIDE_BATCHES | DV_COMM_POSITION_ORDER;
+    if (!c || mode < 0 || (mode & ~flags) > 2) return DV_ERR_ARG;
     DvComm *m = ctx_comm(c);
     if (!m) return DV_ERR_STATE;
-    m->mode = mode & ~DV_COMM_WIDE_BATCHES;
+    m->mode = mode & ~flags;
     m->wide = (mode & DV_COMM_WIDE_BATCHES) != 0;
+    m->position = (mode & DV_COMM_POSITION_ORDER) != 0;
     return DV_OK;
 }
 

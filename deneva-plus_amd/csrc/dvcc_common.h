@@ -235,6 +235,15 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
         return false;
     }
     if (t.rep_part != kNoRep) {  // replicated epoch: the key is the row; own keys checked here
+        if (t.dense && t.htag == t.rep_part) {
+            // every partition a dense map of nbuckets rows (epoch groups
+            // require it): the key is there iff its bucket key / P is in range
+            // -- one compare, as direct_holds would find for the own keys
+            const bool found = key < t.nbuckets * t.part_cnt;
+            if (!found) set_err(ctr, ERRB_KEY);
+            row = key;
+            return found;
+        }
         uint64_t lo = 0;
         const uint64_t q = divmod_magic(key, t.part_cnt, t.m_part, lo);
         bool found = q < t.nbuckets;

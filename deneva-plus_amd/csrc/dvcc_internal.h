@@ -493,6 +493,9 @@ void lane_fail(dv_ctx *c);
 // keys32: the epoch's keys as 32-bit row ids (ep->keys is then ignored)
 // route (epoch groups): committed accesses routed to their owners, nothing
 // executes here
+// an epoch group's decider epoch (32-bit rows as recs32, txn_begin) takes the
+// tb mode of run_prefix_epoch: its per-access txn ids are then never read
+bool group_tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep);
 int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
                          uint8_t *d_commit, dv_stats *st, const dvcc::RouteOut *route = nullptr);
 int comm_combine_errors(dv_ctx *c);  // dvcc_comm.hip

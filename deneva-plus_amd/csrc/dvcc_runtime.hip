@@ -1226,12 +1226,16 @@ int dv_tpcc_load(dv_ctx *c, const dv_tpcc_params *p, uint64_t seed) {
 // Probe + sort + per-row queue construction; for CALVIN also the grant groups
 // (the lock thread's whole job for the epoch, calvin_thread.cpp:40-100).
 namespace {
+bool tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep);
+
 // the common start of an epoch: argument checks, the verdict-byte stride,
 // the per-epoch host state
 int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
-    // (epoch groups: no types -- the write bit rides in the 32-bit row ids)
-    if (ep->n_acc && (!ep->keys || (!ep->types && !c->keys32) || !ep->acc_txn)) return DV_ERR_ARG;
+    // (epoch groups: no types -- the write bit rides in the 32-bit row ids;
+    // no per-access txn ids where the boundaries are every range, tb_epoch)
+    if (ep->n_acc && (!ep->keys || (!ep->types && !c->keys32) || (!ep->acc_txn && !tb_epoch(c, ep))))
+        return DV_ERR_ARG;
     bool any = false;
     for (auto &t : c->tab) any |= t.loaded;
     if (!any) return DV_ERR_NO_TABLE;
@@ -1813,6 +1817,16 @@ bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {
     return prefix_size(c, ep->n_txn) < ep->n_txn;
 }
 
+// tb mode: a prefix-kill epoch whose own txn boundaries are every kernel's
+// ranges (k_probe_tb probes the prefix alone, the kill pass the rest).  Not
+// for a replicated epoch whose owners' key checks must be combined before
+// the kill (run_part); epoch groups (route) vote on the decider's outcome
+// instead, and hand their 32-bit rows over as the 4-byte records.
+bool tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep) {
+    return prefix_applies(c, ep) && ep->txn_begin && !ep->n_acc_dev && !ep->tables &&
+           (!c->keys32 || ep->recs32) && (!c->rep_P || c->route) && (ep->keys || ep->recs32);
+}
+
 // The rounds of one stage: round 0, then every remaining decision in one
 // asynchronous launch (stages are small: a declined or yielded try halts and
 // the stage is decided again synchronously), or the pipelined loop when
@@ -1934,7 +1948,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     c->prefix_words = c->surv_words = false;
     // tb mode: the epoch's own txn boundaries are every kernel's ranges, the
     // prefix alone is probed here and the rest by the kill pass (k_probe_tb)
-    c->tb_mode = ep->txn_begin && !ep->n_acc_dev && !ep->tables && !c->keys32 && !c->rep_P && !c->route;
+    c->tb_mode = tb_epoch(c, ep);
     if (c->tb_mode) {
         c->rs = ep->txn_begin;
         c->re = ep->txn_begin + 1;
@@ -2820,6 +2834,10 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
 // partition are checked against its index and the error bits combined over
 // the ranks after the probe, all txns are decided here, and only this
 // partition's rows execute.  Every rank computes the same decisions.
+bool group_tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep) {
+    return prefix_applies(c, ep) && ep->txn_begin && ep->recs32 && !ep->n_acc_dev && !ep->tables;
+}
+
 int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
                          uint8_t *d_commit, dv_stats *st, const RouteOut *route) {
     if (!c || !ep || nranks == 0) return DV_ERR_ARG;

@@ -9,4 +9,4 @@ except Exception:  # pragma: no cover
 from ._lib import (CALVIN, CC_NAMES, HASH_MOD, HASH_YCSB, NO_WAIT, OCC, RD, SCAN, WAIT_DIE, WR,  # noqa
                    DvccError, lib)
 from .engine import CCEngine, ClosedLoopBufs, DeviceEpoch, Epoch, comm_unique_id  # noqa: F401
-from .ycsb import YCSBQueryGenerator, epoch_seed, sequence  # noqa: F401
+from .ycsb import YCSBQueryGenerator, epoch_seed, sequence, sequence_position  # noqa: F401

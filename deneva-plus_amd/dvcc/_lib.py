@@ -13,6 +13,7 @@ LIB_PATH = os.environ.get("DVCC_LIB") or os.path.join(PKG_DIR, "build", "libdvcc
 DV_OK = 0
 DV_ERR_ARG = -1
 DV_COMM_WIDE_BATCHES = 4  # dv_comm_set_mode: 8-byte epoch-group batches
+DV_COMM_POSITION_ORDER = 8  # dv_comm_set_mode: epoch groups sequenced txn by txn across origins
 DV_ERR_HIP = -2
 DV_ERR_NOMEM = -3
 DV_ERR_KEY_NOT_FOUND = -4

@@ -504,7 +504,10 @@ class CCEngine:
         L.check(L.lib().dv_comm_init_ipc(self._ctx, name.encode(), nranks, rank), "dv_comm_init_ipc")
 
     def comm_set_mode(self, mode):
-        """dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when possible."""
+        """dv_comm_set_mode: 0 automatic, 1 list protocol, 2 replicated when
+        possible; | DV_COMM_WIDE_BATCHES (8-byte group batches), |
+        DV_COMM_POSITION_ORDER (epoch groups sequenced position-major,
+        dvcc.sequence_position)."""
         L.check(L.lib().dv_comm_set_mode(self._ctx, mode), "dv_comm_set_mode")
         self._comm_mode = mode
 

@@ -55,3 +55,29 @@ def sequence(batches):
     tb = np.zeros(sum(len(s) for s in sizes) + 1, dtype=np.uint32)
     tb[1:] = np.cumsum(np.concatenate(sizes))
     return Epoch(keys, types, tb)
+
+
+def sequence_position(batches, txns_per_rank=None):
+    """The same batches merged txn by txn (DV_COMM_POSITION_ORDER): origin q's
+    txn j is sequence number j * P + q, for j < txns_per_rank (default: the
+    longest batch); a batch shorter than that leaves empty txns (no accesses,
+    they commit) in its slots -- the epoch a position-major epoch group
+    decides."""
+    P = len(batches)
+    tpr = txns_per_rank or max(b.n_txn for b in batches)
+    lens = np.zeros((tpr, P), dtype=np.int64)
+    starts = np.zeros((tpr, P), dtype=np.int64)
+    off = 0
+    for q, b in enumerate(batches):
+        tb = b.txn_begin.astype(np.int64)
+        assert b.n_txn <= tpr, "a batch longer than txns_per_rank"
+        lens[:b.n_txn, q] = np.diff(tb)
+        starts[:b.n_txn, q] = tb[:-1] + off
+        off += int(tb[-1])
+    lens, starts = lens.ravel(), starts.ravel()
+    tb = np.zeros(tpr * P + 1, dtype=np.int64)
+    tb[1:] = np.cumsum(lens)
+    idx = np.repeat(starts - tb[:-1], lens) + np.arange(int(tb[-1]))
+    keys = np.concatenate([b.keys for b in batches])
+    types = np.concatenate([b.types for b in batches])
+    return Epoch(keys[idx], types[idx], tb.astype(np.uint32))

@@ -377,6 +377,17 @@ int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_r
  * per access even where the compact 4-byte form (global rows below 2^30,
  * dense txn ids) applies -- results are identical. */
 #define DV_COMM_WIDE_BATCHES 4
+/* OR DV_COMM_POSITION_ORDER into mode (epoch groups, NO_WAIT / WAIT_DIE /
+ * OCC): the sequencer merges the origins' batches of an epoch txn by txn --
+ * origin q's txn j is sequence number j * P + q, as clients of all nodes
+ * arriving together -- instead of batch by batch (origin q's txn j at
+ * q * txns_per_rank + j, Calvin's lock order, which CALVIN always keeps).
+ * Decisions are the E-schedule of that sequence (dvcc.sequence_position);
+ * every rank must set the same order (else DV_ERR_ARG on every rank).  Why:
+ * the decider's prefix (the first n / 32 txns, prefix-kill epochs) then holds
+ * every origin's first txns and kills in every partition; origin-major it
+ * holds origin 0's only, and at P = 8 four times as many txns survive it. */
+#define DV_COMM_POSITION_ORDER 8
 int dv_comm_set_mode(dv_ctx *ctx, int mode);
 
 /* Several epochs back to back (the same results as one dv_epoch_run_device
@@ -509,7 +520,11 @@ int dv_epoch_run_closed_loop(dv_ctx *ctx, const dv_epoch_dev *pool, const uint32
  * again) when P x rows < 2^30, else as 8 B (row id, txn id); the compact form
  * needs every txn id below a batch's n_txn to have an access -- a batch with
  * an empty txn fails the group with DV_ERR_ARG on every rank
- * (DV_COMM_WIDE_BATCHES lifts that). */
+ * (DV_COMM_WIDE_BATCHES lifts that).  Position-major order
+ * (DV_COMM_POSITION_ORDER, dv_comm_set_mode): the decider interleaves the
+ * landed batches txn by txn before deciding, the commit bytes come back in
+ * origin order as above; a malformed wide batch (txn ids not rising, or past
+ * txns_per_rank) fails the group with DV_ERR_ARG on every rank. */
 /* Precondition (open loop): the P epochs of a group are decided side by
  * side, so no epoch of a group may depend on the outcome of an earlier epoch
  * of the same group -- in particular a txn aborted in epoch e of group g can

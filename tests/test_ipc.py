@@ -80,7 +80,8 @@ def _run_scenario(sc, world, rank, name):
         lanes = [eng.open_lane() for _ in range(sc.get("lanes", 1) - 1)]
         for ln, ctx in enumerate([eng] + lanes):
             ctx.comm_init_ipc(name if ln == 0 else f"{name}_l{ln}", world, rank)
-            ctx.comm_set_mode(mode | (dvcc._lib.DV_COMM_WIDE_BATCHES if sc.get("wide") else 0))
+            ctx.comm_set_mode(mode | (dvcc._lib.DV_COMM_WIDE_BATCHES if sc.get("wide") else 0) |
+                              (dvcc._lib.DV_COMM_POSITION_ORDER if sc.get("position") else 0))
         if lanes:
             eng.lanes_order(lanes)
         out = {}
@@ -151,9 +152,20 @@ def _run_ranks(scenarios, world=WORLD):
     return [got[r] for r in range(world)]
 
 
+def _position(sc):
+    return sc.get("position", False) and sc["cc"] != dvcc.CALVIN
+
+
+def _mine(c, sc, r, world):
+    """Rank r's txns' commit bytes in a sequenced epoch's bytes."""
+    n = sc["n_txn"]
+    return c.reshape(n, world)[:, r] if _position(sc) else c[r * n:(r + 1) * n]
+
+
 def _oracle_groups(sc, world):
     """Commit bytes and stats of every epoch of every group, the oracle running
-    the sequenced epochs one after the other, and the final rows."""
+    the sequenced epochs one after the other (origin-major, or position-major
+    with sc["position"]: DV_COMM_POSITION_ORDER), and the final rows."""
     tab = O.YcsbTable(sc["rows_pp"] * world)
     f0 = tab.f0.copy()
     per_rank = [_group_batches(sc, world, r) for r in range(world)]
@@ -161,7 +173,8 @@ def _oracle_groups(sc, world):
     for g in range(sc["groups"]):
         grp = []
         for e in range(world):
-            q = dvcc.sequence([per_rank[r][g][e] for r in range(world)])
+            b = [per_rank[r][g][e] for r in range(world)]
+            q = dvcc.sequence_position(b) if _position(sc) else dvcc.sequence(b)
             c, _, st = O.epoch_run(ORACLE_CC[sc["cc"]], tab.ix, f0, q.n_txn, q.txn_begin, q.keys, q.types)
             grp.append((c, st))
         refs.append(grp)
@@ -169,12 +182,14 @@ def _oracle_groups(sc, world):
 
 
 GROUP_CASES = [dict(cc=dvcc.NO_WAIT, wide=False), dict(cc=dvcc.NO_WAIT, wide=True),
-               dict(cc=dvcc.OCC, wide=False), dict(cc=dvcc.CALVIN, wide=False)]
+               dict(cc=dvcc.OCC, wide=False), dict(cc=dvcc.CALVIN, wide=False),
+               dict(cc=dvcc.NO_WAIT, wide=False, position=True), dict(cc=dvcc.OCC, wide=True, position=True)]
 
 
 def test_ipc_epoch_groups_two_processes():
     """Epoch groups (dv_epoch_group_run_batch, two groups of two epochs) over
-    two processes: compact and wide batches, NO_WAIT / OCC / CALVIN."""
+    two processes: compact and wide batches, NO_WAIT / OCC / CALVIN, origin-
+    and position-major sequences."""
     base = dict(kind="group", rows_pp=1 << 13, n_txn=1500, mpr=0.3, groups=2, seed=40)
     scs = [dict(base, **c) for c in GROUP_CASES]
     res = _run_ranks(scs)
@@ -188,7 +203,7 @@ def test_ipc_epoch_groups_two_processes():
                 out = res[r][i]
                 assert "error" not in out, (sc, r, out.get("error"))
                 for e in range(WORLD):
-                    assert (out["commit"][g][e * n:(e + 1) * n] == refs[g][e][0][r * n:(r + 1) * n]).all(), \
+                    assert (out["commit"][g][e * n:(e + 1) * n] == _mine(refs[g][e][0], sc, r, WORLD)).all(), \
                         (sc, g, e, r)
                 c, d, w = out["stats"][g]
                 assert c == committed, (sc, g, r)
@@ -206,9 +221,10 @@ def test_ipc_epoch_groups_ordered_lanes_two_processes():
     dv_lanes_order; 7 groups of two epochs over two calls, group g decided on
     lane g % 4 of both ranks, executions in group order -- every epoch's
     commit bytes, the digests and the rows against the oracle running the
-    sequenced epochs in order.  Asynchronous rounds on (the bench's)."""
+    sequenced epochs in order.  Asynchronous rounds on (the bench's), NO_WAIT
+    position-major (the bench's default order) and OCC origin-major."""
     base = dict(kind="group", rows_pp=1 << 13, n_txn=1500, mpr=0.3, groups=7, seed=140, lanes=4, asyn=True)
-    scs = [dict(base, cc=dvcc.NO_WAIT), dict(base, cc=dvcc.OCC, wide=True)]
+    scs = [dict(base, cc=dvcc.NO_WAIT, position=True), dict(base, cc=dvcc.OCC, wide=True)]
     res = _run_ranks(scs)
     for i, sc in enumerate(scs):
         refs, f0 = _oracle_groups(sc, WORLD)
@@ -219,7 +235,7 @@ def test_ipc_epoch_groups_ordered_lanes_two_processes():
                 out = res[r][i]
                 assert "error" not in out, (sc, r, out.get("error"))
                 for e in range(WORLD):
-                    assert (out["commit"][g][e * n:(e + 1) * n] == refs[g][e][0][r * n:(r + 1) * n]).all(), \
+                    assert (out["commit"][g][e * n:(e + 1) * n] == _mine(refs[g][e][0], sc, r, WORLD)).all(), \
                         (sc, g, e, r)
                 assert out["stats"][g][0] == committed, (sc, g, r)
         for r in range(WORLD):

@@ -179,6 +179,25 @@ def test_sequence_is_origin_major():
     assert (e.keys[:500] == batches[0].keys).all() and (e.keys[500:1000] == batches[1].keys).all()
 
 
+def test_sequence_position_interleaves_txns():
+    """dvcc.sequence_position (DV_COMM_POSITION_ORDER's sequence): origin q's
+    txn j is txn j * P + q, a shorter batch leaves empty txns in its slots."""
+    _, batches = _global_setup(3, 50, 256, 0.5)
+    short = dvcc.Epoch(batches[1].keys[:int(batches[1].txn_begin[20])], batches[1].types[:int(batches[1].txn_begin[20])],
+                       batches[1].txn_begin[:21].copy())
+    bs = [batches[0], short, batches[2]]
+    e = dvcc.sequence_position(bs, 60)
+    assert e.n_txn == 180 and e.n_acc == sum(b.n_acc for b in bs)
+    for t in range(e.n_txn):
+        j, q = divmod(t, 3)
+        a, b = int(e.txn_begin[t]), int(e.txn_begin[t + 1])
+        if j < bs[q].n_txn:
+            s0, s1 = int(bs[q].txn_begin[j]), int(bs[q].txn_begin[j + 1])
+            assert (e.keys[a:b] == bs[q].keys[s0:s1]).all() and (e.types[a:b] == bs[q].types[s0:s1]).all()
+        else:
+            assert a == b
+
+
 # ------------------------------------------------------------------- GPU
 def _gpu_two_partitions(cc, n_txn, rows_pp, mpr, world=2):
     _, batches = _global_setup(world, n_txn, rows_pp, mpr, seed0=9)
@@ -573,8 +592,28 @@ def _run_group_batches(engines, homes, n_txn, groups):
     return out
 
 
+def _group_sequence(batches, n_txn, cc, position):
+    """The epoch a group decides from these batches: origin-major (Calvin's
+    order; batches padded with empty txns to n_txn each) or, position-major
+    (DV_COMM_POSITION_ORDER, not CALVIN), txn by txn."""
+    if position and cc != dvcc.CALVIN:
+        return dvcc.sequence_position(batches, n_txn)
+    padded = []
+    for b in batches:
+        tb = np.concatenate([b.txn_begin, np.full(n_txn - b.n_txn, b.txn_begin[-1], np.uint32)])
+        padded.append(dvcc.Epoch(b.keys, b.types, tb))
+    return dvcc.sequence(padded)
+
+
+def _group_mine(c_ref, r, n_txn, world, cc, position):
+    """Rank r's txns' commit bytes in a sequenced group epoch's bytes."""
+    if position and cc != dvcc.CALVIN:
+        return c_ref.reshape(n_txn, world)[:, r]
+    return c_ref[r * n_txn:(r + 1) * n_txn]
+
+
 def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False,
-                        wide=False):
+                        wide=False, position=False):
     """Every epoch of every group against the one-partition oracle run over
     the sequenced epochs one after the other: commit bytes (each rank holds its
     own txns' bytes of every epoch), committed count, digest and writes summed
@@ -582,13 +621,16 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
     sizes: per-rank batch sizes (unequal batches; the rest of a rank's
     sequence slots are empty txns).  batch: all groups in one
     dv_epoch_group_run_batch call (rows checked after the last group).
-    wide: 8-byte batches (DV_COMM_WIDE_BATCHES) instead of the compact ones."""
+    wide: 8-byte batches (DV_COMM_WIDE_BATCHES) instead of the compact ones.
+    position: the origins' batches sequenced txn by txn (DV_COMM_POSITION_ORDER;
+    CALVIN keeps origin order)."""
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
     engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
-    if wide:
+    if wide or position:
         for eng in engines:
-            eng.comm_set_mode(2 | dvcc._lib.DV_COMM_WIDE_BATCHES)
+            eng.comm_set_mode(2 | (dvcc._lib.DV_COMM_WIDE_BATCHES if wide else 0) |
+                              (dvcc._lib.DV_COMM_POSITION_ORDER if position else 0))
     tab = O.YcsbTable(rows_pp * world)
     f0 = tab.f0.copy()
     sizes = sizes or [n_txn] * world
@@ -600,7 +642,7 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
             refs = []
             for e in range(world):
                 batches = [gen.gen(sizes[r], dvcc.epoch_seed(r, 40 + g * world + e), r) for r in range(world)]
-                q = dvcc.sequence(batches)
+                q = _group_sequence(batches, n_txn, cc, position)
                 c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin,
                                                q.keys, q.types)
                 refs.append((c_ref, st_ref))
@@ -617,8 +659,8 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
             digest = writes = 0
             for r, (cs, sts) in enumerate(res):
                 for e in range(world):
-                    assert (cs[g][e * n_txn:(e + 1) * n_txn] == refs[e][0][r * n_txn:(r + 1) * n_txn]).all(), \
-                        f"group {g} epoch {e} rank {r}"
+                    assert (cs[g][e * n_txn:(e + 1) * n_txn] ==
+                            _group_mine(refs[e][0], r, n_txn, world, cc, position)).all(), f"group {g} epoch {e} rank {r}"
                 assert sts[g].committed == committed and sts[g].n_txn == n_txn * world * world
                 digest = (digest + sts[g].read_digest) % (1 << 64)
                 writes += sts[g].write_cnt
@@ -634,11 +676,7 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
         refs = []
         for e in range(world):
             batches = [gen.gen(sizes[r], dvcc.epoch_seed(r, 40 + g * world + e), r) for r in range(world)]
-            padded = []
-            for b in batches:
-                tb = np.concatenate([b.txn_begin, np.full(n_txn - b.n_txn, b.txn_begin[-1], np.uint32)])
-                padded.append(dvcc.Epoch(b.keys, b.types, tb))
-            q = dvcc.sequence(padded)
+            q = _group_sequence(batches, n_txn, cc, position)
             c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, q.n_txn, q.txn_begin, q.keys,
                                            q.types)
             refs.append((c_ref, st_ref))
@@ -651,7 +689,7 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
             assert not isinstance(x, Exception), f"rank {r}: {x}"
             c, st = x
             for e in range(world):
-                mine = refs[e][0][r * n_txn:(r + 1) * n_txn]
+                mine = _group_mine(refs[e][0], r, n_txn, world, cc, position)
                 assert (c[e * n_txn:(e + 1) * n_txn] == mine).all(), f"group {g} epoch {e} rank {r}"
             assert st.committed == committed and st.n_txn == n_txn * world * world
             digest = (digest + st.read_digest) % (1 << 64)
@@ -673,6 +711,70 @@ def test_epoch_groups(cc, world, mpr):
     commit bytes, digests and rows as the oracle running the epochs in
     sequence.  (The contexts share one GPU: asynchronous rounds off.)"""
     _check_epoch_groups(cc, world, 1 << 14, 3000, mpr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+@pytest.mark.parametrize("world,mpr", [(2, 0.0), (2, 0.3), (8, 0.1)])
+def test_epoch_groups_position_order(cc, world, mpr):
+    """DV_COMM_POSITION_ORDER: the decider interleaves the origins' batches
+    txn by txn (origin q's txn j at j * P + q) -- against the oracle over
+    dvcc.sequence_position of the same batches, commit bytes back in origin
+    order; CALVIN keeps its origin order under the flag."""
+    _check_epoch_groups(cc, world, 1 << 14, 3000, mpr, position=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc,wide,batch,sizes", [
+    (dvcc.NO_WAIT, True, False, None), (dvcc.OCC, True, False, None), (dvcc.WAIT_DIE, False, True, None),
+    (dvcc.NO_WAIT, False, False, [1000, 640, 913]), (dvcc.OCC, True, False, [700, 1000, 1])])
+def test_epoch_groups_position_order_forms(cc, wide, batch, sizes):
+    """Position-major groups over the 8-byte batches (the senders' ids, bounds
+    found by search), three groups in one batched call, and unequal batches
+    (empty slots in the interleaved sequence)."""
+    world = 3 if sizes else 4
+    _check_epoch_groups(cc, world, 1 << 13, 1000, 0.3, groups=3 if batch else 2, batch=batch, wide=wide,
+                        sizes=sizes, position=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_epoch_groups_position_order_prefix_kill():
+    """Position-major groups with epochs large enough for the decider's
+    prefix-kill path (4 x 40,000 txns, MPR 0 and 0.1)."""
+    _check_epoch_groups(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.0, groups=1, position=True)
+    _check_epoch_groups(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, groups=1, position=True)
+
+
+@pytest.mark.gpu
+def test_epoch_groups_position_order_malformed_wide_batch():
+    """A raw wide batch whose txn ids do not rise (handed over as tensors):
+    the position-major move refuses it -- DV_ERR_ARG on every rank, no row
+    changes -- and the group then runs normally."""
+    world, rows_pp, n_txn = 2, 1 << 12, 600
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    for eng in engines:
+        eng.comm_set_mode(2 | dvcc._lib.DV_COMM_WIDE_BATCHES | dvcc._lib.DV_COMM_POSITION_ORDER)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    homes = [[dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(r, 90 + e), r)) for e in range(world)]
+             for r in range(world)]
+    h = homes[1][0]
+    txn = h.acc_txn.clone()
+    a, b = int(txn.numel()) // 2, int(txn.numel()) // 2 + 40
+    txn[a:b] = txn[a:b].flip(0)  # ids falling inside the batch
+    bad = [list(x) for x in homes]
+    bad[1][0] = dvcc.DeviceEpoch.from_tensors(h.keys, h.types, txn, h.n_txn, max_txn_acc=h.max_txn_acc)
+    res = _run_group_epochs(engines, bad, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
+    for eng, b0 in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b0).all()
+    res = _run_group_epochs(engines, homes, n_txn)
+    assert all(not isinstance(x, Exception) for x in res), res
+    for eng in engines:
+        eng.close()
 
 
 @pytest.mark.gpu
@@ -707,13 +809,15 @@ def test_epoch_groups_prefix_kill():
 
 @pytest.mark.gpu
 @pytest.mark.slow
-def test_epoch_groups_config_d_size():
+@pytest.mark.parametrize("position", [False, True])
+def test_epoch_groups_config_d_size(position):
     """The N>1 headline's exact shape: config D at 8 partitions -- 16,777,216
     rows per partition, 131,072 txns per batch (1,048,576-txn epochs), zipf
     0.9, MPR 0.1 -- one group of 8 epochs, NO_WAIT: every epoch's commit
     bytes, the digests and every partition's rows against the oracle running
-    the 8 sequenced epochs one after the other."""
-    _check_epoch_groups(dvcc.NO_WAIT, 8, 16_777_216, 131_072, 0.1, groups=1)
+    the 8 sequenced epochs one after the other; origin-major and, as the
+    bench runs it, position-major."""
+    _check_epoch_groups(dvcc.NO_WAIT, 8, 16_777_216, 131_072, 0.1, groups=1, position=position)
 
 
 @pytest.mark.gpu
