@@ -285,4 +285,19 @@ __device__ __forceinline__ bool probe_row(const TableDesc &t, bool tb_ok, uint64
     return found;
 }
 
+// the row of a KillKeys epoch's key (k_kill / k_kill_emit with keys): DENSE
+// (KillKeys::dense_lim) one compare -- a missing key rejects the epoch --
+// else the full probe
+template <bool DENSE>
+__device__ __forceinline__ bool kk_row(const KillKeys &kk, uint64_t key, uint64_t &row, Counters *ctr) {
+    if constexpr (DENSE) {
+        row = key + kk.dense_base;
+        if (key < kk.dense_lim) return true;
+        set_err(ctr, ERRB_KEY);
+        return false;
+    } else {
+        return probe_row(kk.tabs.t[0], kk.tabs.n > 0, key, row, ctr);
+    }
+}
+
 }  // namespace dvcc

@@ -557,7 +557,24 @@ struct KillKeys {
     const uint64_t *keys;
     const uint8_t *types;
     const uint32_t *recs;  // (optional) the same as 4-byte records, key | write << 31 (dv_epoch_dev::recs32)
+    // table 0 a dense map (dv_load_ycsb_partition; every partition's, for a
+    // replicated epoch): a key is there iff key < dense_lim, its row key +
+    // dense_base -- the kill and emit passes then instantiate only that
+    // compare (kk_row), not the general probe; 0 = probe
+    uint64_t dense_lim, dense_base;
 };
+inline KillKeys kill_keys(const Tables &t, const uint64_t *keys, const uint8_t *types, const uint32_t *recs) {
+    KillKeys k{t, keys, types, recs, 0, 0};
+    if (t.n == 0) return k;
+    const TableDesc &d = t.t[0];
+    if (d.rep_part != kNoRep) {  // (probe_row's replicated dense branch)
+        if (d.dense && d.htag == d.rep_part) k.dense_lim = d.nbuckets * d.part_cnt;
+    } else if (d.dense && d.part_cnt == 1 && d.htag == 0) {  // (its one-partition dense branch)
+        k.dense_lim = d.nbuckets;
+        k.dense_base = d.row_base;
+    }
+    return k;
+}
 // access a of a KillKeys epoch: its key and write bit
 __device__ __forceinline__ uint64_t kk_key(const KillKeys &kk, uint64_t a, uint32_t &wr) {
     if (kk.recs) {

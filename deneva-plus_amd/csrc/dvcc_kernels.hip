@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t
         for (uint32_t j0 = 0; j0 < len; j0 += kU) {
             uint64_t key[kU];
             uint32_t wrs[kU];
-            const KillKeys kk{tabs, keys, types, recs};
+            const KillKeys kk{tabs, keys, types, recs, 0, 0};
 #pragma unroll
             for (uint32_t j = 0; j < kU; j++) {
                 wrs[j] = 0;

@@ -156,18 +156,37 @@ constexpr int kKillBlock = 1024;  // one block per CU (144 KiB of LDS): 16 waves
 // accesses were never probed -- their rows come from their keys here (the
 // dense YCSB map: arithmetic only), 9 bytes read per access instead of the
 // probe's 17 plus this pass's 4; a missing key rejects the epoch (ERRB_KEY)
-template <bool KEYS>
+template <int KEYS>  // 0: acc_row; 1: keys, probed; 2: keys of a dense map (KillKeys::dense_lim)
 __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict__ acc_row, uint64_t n,
                                                  const uint32_t *__restrict__ n_dev,
                                                  const uint32_t *__restrict__ row_state, uint64_t state_words,
                                                  const uint32_t *__restrict__ bloom, int nowait,
                                                  uint64_t *__restrict__ kill_bits, uint64_t *__restrict__ skip_bits,
                                                  Counters *__restrict__ ctr, KillKeys kk) {
-    __shared__ uint32_t s_hot[kHotWords], s_bloom[kBloomWords];
+    __shared__ __align__(16) uint32_t s_lds[kHotWords + kBloomWords];
+    uint32_t *const s_hot = s_lds, *const s_bloom = s_lds + kHotWords;
     if (input_err(ctr) || ctr->halt) return;
     if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (rows past the real count were never probed)
-    for (uint32_t i = threadIdx.x; i < kHotWords; i += kKillBlock) s_hot[i] = i < state_words ? row_state[i] : 0u;
-    for (uint32_t i = threadIdx.x; i < kBloomWords; i += kKillBlock) s_bloom[i] = bloom[i];
+    {
+        // the 144 KiB in 16-byte loads, all of a thread's in flight before its
+        // first LDS store (a load-store loop waited out one L2 round trip per
+        // 4 KiB); the bitmap part and the filter are multiples of 4 words
+        constexpr uint32_t kH4 = kHotWords / 4, kAll4 = (kHotWords + kBloomWords) / 4;
+        static_assert(kAll4 % kKillBlock == 0, "k_kill's LDS fill: whole 16-byte steps per thread");
+        constexpr uint32_t kSteps = kAll4 / kKillBlock;
+        const uint32_t sw4 = (uint32_t)(state_words / 4 < kH4 ? state_words / 4 : kH4);
+        const uint4 *hot4 = reinterpret_cast<const uint4 *>(row_state);
+        const uint4 *blm4 = reinterpret_cast<const uint4 *>(bloom);
+        uint4 v[kSteps];
+#pragma unroll
+        for (uint32_t k = 0; k < kSteps; k++) {
+            const uint32_t i = k * kKillBlock + threadIdx.x;
+            v[k] = i < kH4 ? (i < sw4 ? hot4[i] : make_uint4(0u, 0u, 0u, 0u)) : blm4[i - kH4];
+        }
+        uint4 *dst = reinterpret_cast<uint4 *>(s_lds);
+#pragma unroll
+        for (uint32_t k = 0; k < kSteps; k++) dst[k * kKillBlock + threadIdx.x] = v[k];
+    }
     __syncthreads();
     const uint64_t first = ctr->a_acc;
     const uint32_t lane = threadIdx.x & 63;
@@ -191,7 +210,7 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
             for (int q = 0; q < kKillWords; q++) {
                 uint64_t row = 0;
                 ar[q] = ~0u;
-                if (in[q] && probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[q], row, ctr))
+                if (in[q] && kk_row<KEYS == 2>(kk, key[q], row, ctr))
                     ar[q] = (uint32_t)row | (wr[q] ? AR_WR : 0u);
             }
         } else {
@@ -326,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_count(const uint32_t *__restric
 // KEYS (launch_probe_tb epochs): the survivors' accesses were never probed --
 // their rows come from their keys here: their sort keys, and acc_row for every
 // access of a survivor (the execution's, the skipped reads' included)
-template <bool KEYS>
+template <int KEYS>  // as k_kill
 __global__ __launch_bounds__(kBlock) void k_kill_emit(
     const uint32_t *__restrict__ tb_start, const uint32_t *__restrict__ tb_end, uint32_t *__restrict__ acc_row,
     uint32_t K, uint32_t n_txn,
@@ -462,7 +481,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             for (uint32_t u = 0; u < kU; u++) {
                 uint64_t row = 0;
                 if (g0 + u * kBlock + tid < nf)
-                    probe_row(kk.tabs.t[0], kk.tabs.n > 0, key[u], row, ctr);  // (the kill found every key)
+                    kk_row<KEYS == 2>(kk, key[u], row, ctr);  // (the kill found every key)
                 rows[u] = (uint32_t)row;
             }
 #pragma unroll
@@ -515,7 +534,7 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             if constexpr (KEYS) {  // (the row from the key: this block's acc_row stores may not be visible yet)
                 uint64_t row = 0;
                 uint32_t w = 0;
-                if (g < na) probe_row(kk.tabs.t[0], kk.tabs.n > 0, kk_key(kk, a, w), row, ctr);
+                if (g < na) kk_row<KEYS == 2>(kk, kk_key(kk, a, w), row, ctr);
                 ar[u] = g < na ? (uint32_t)row | (w ? AR_WR : 0u) : 0u;
             } else {
                 ar[u] = g < na ? acc_row[a] : 0u;
@@ -583,19 +602,25 @@ void launch_kill_compact(hipStream_t s, const uint32_t *tb_start, const uint32_t
     uint32_t *ar = const_cast<uint32_t *>(acc_row);  // (k_kill_emit writes the survivors' with keys)
     // (144 KiB of LDS per block: one per CU, each loads the hot words and the filter once)
     const uint32_t kg = grid_of(nw * 64 / kKillWords / 4 + 1, 256);
-    if (kk)
-        DV_LAUNCH(k_kill<true>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
+    if (kk && k0.dense_lim)
+        DV_LAUNCH(k_kill<2>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
+                  row_state + (rs_words - kBloomWords), nowait, kill_bits, skip_bits, ctr, k0);
+    else if (kk)
+        DV_LAUNCH(k_kill<1>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
                   row_state + (rs_words - kBloomWords), nowait, kill_bits, skip_bits, ctr, k0);
     else
-        DV_LAUNCH(k_kill<false>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
+        DV_LAUNCH(k_kill<0>, kg, kKillBlock, 0, s, acc_row, n_acc, n_acc_dev, row_state, rs_words - kBloomWords,
                   row_state + (rs_words - kBloomWords), nowait, kill_bits, skip_bits, ctr, k0);
     DV_LAUNCH(k_kill_count, nt, kBlock, 0, s, tb_start, tb_end, K, n_txn, (const uint64_t *)kill_bits,
               (const uint64_t *)skip_bits, status, info, tsum, ctr);
-    if (kk)
-        DV_LAUNCH(k_kill_emit<true>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
+    if (kk && k0.dense_lim)
+        DV_LAUNCH(k_kill_emit<2>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
+                  info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0, row_state, nowait);
+    else if (kk)
+        DV_LAUNCH(k_kill_emit<1>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
                   info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0, row_state, nowait);
     else
-        DV_LAUNCH(k_kill_emit<false>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
+        DV_LAUNCH(k_kill_emit<0>, nt, kBlock, 0, s, tb_start, tb_end, ar, K, n_txn, (const uint64_t *)skip_bits,
                   info, tsum, map, status_b, tlen_b, pairs_b, ctr, k0, row_state, nowait);
 }
 

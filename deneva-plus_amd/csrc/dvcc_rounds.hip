@@ -935,7 +935,19 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
     // does a queue run in from the previous slice / out into the next one?
     const bool cont_in = lo > 0 && lo < n_all && !(src[lo] & F_HEAD);
     const bool cont_out = hi < n_all && !(src[hi] & F_HEAD);
-    for (uint32_t i = tid; i < n; i += kAsyncThreads) sel[i] = src[lo + i] & ~(i == 0 && cont_in ? F_HEAD : 0u);
+    {  // (the slice's loads all in flight before the first LDS store)
+        uint32_t v[IPT];
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            const uint32_t i = (uint32_t)j * kAsyncThreads + tid;
+            v[j] = i < n ? src[lo + i] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            const uint32_t i = (uint32_t)j * kAsyncThreads + tid;
+            if (i < n) sel[i] = v[j] & ~(i == 0 && cont_in ? F_HEAD : 0u);
+        }
+    }
     if (tid == 0) s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
     __syncthreads();
     uint32_t it = 0;

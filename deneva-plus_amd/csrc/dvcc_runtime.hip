@@ -1952,7 +1952,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     if (c->tb_mode) {
         c->rs = ep->txn_begin;
         c->re = ep->txn_begin + 1;
-        c->pf_kk = KillKeys{make_tables(c), ep->keys, ep->types, ep->recs32};
+        c->pf_kk = kill_keys(make_tables(c), ep->keys, ep->types, ep->recs32);
     }
     rec(c, 0);
     const bool mir = c->mir_pending;  // (the previous pipelined epoch's read-back rides on this clear)
