@@ -229,6 +229,7 @@ constexpr uint32_t kXMaxP = 64;
 struct PackSrc {
     const uint64_t *keys[kXMaxP];
     const uint8_t *types[kXMaxP];
+    const uint32_t *recs[kXMaxP];  // (optional: dv_epoch_dev::recs32, read instead of keys + types)
     const uint32_t *txn[kXMaxP];
     uint64_t n[kXMaxP], off[kXMaxP];
     uint32_t n_txn[kXMaxP];
@@ -238,20 +239,29 @@ __global__ __launch_bounds__(kBlock) void k_group_pack_c(PackSrc src, uint32_t *
     const uint32_t e = blockIdx.y;
     const uint64_t *__restrict__ keys = src.keys[e];
     const uint8_t *__restrict__ types = src.types[e];
+    const uint32_t *__restrict__ recs = src.recs[e];
     const uint32_t *__restrict__ txn = src.txn[e];
     const uint64_t n = src.n[e];
     const uint32_t n_txn = src.n_txn[e];
     uint32_t *__restrict__ k32 = k32_all + src.off[e];
     bool b = false;
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t k = keys[i];
+        uint64_t k;
+        bool wr;
+        if (recs) {  // (4 bytes per access instead of 9)
+            const uint32_t r = recs[i];
+            k = r & 0x7FFFFFFFu;
+            wr = (r >> 31) != 0;
+        } else {
+            k = keys[i];
+            wr = types[i] == DV_WR;
+        }
         const uint32_t t = txn[i];
         const uint32_t pt = i ? txn[i - 1] : 0u;
         const bool start = i == 0 || t != pt;
         if (t >= n_txn || (i == 0 ? t != 0u : (t != pt && t != pt + 1u))) b = true;
         // (a key past 30 bits saturates and fails the decider's range check)
-        k32[i] = ((k >> 30) ? 0x3FFFFFFFu : (uint32_t)k) | (start ? GP_START : 0u) |
-                 (types[i] == DV_WR ? 0x80000000u : 0u);
+        k32[i] = ((k >> 30) ? 0x3FFFFFFFu : (uint32_t)k) | (start ? GP_START : 0u) | (wr ? 0x80000000u : 0u);
     }
     if (b) atomicOr(bad, 1u);
 }
@@ -302,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_count(const uint32_t *__re
 // dv_epoch_group_run gives it; position-major, tbo non-null: the origin-local
 // j, and each txn's first access within its origin's segment into tbo, the
 // origin's txn count into ncnt -- k_il_begin) into rt, the start bits cleared
-// from rk
+// from rk (position-major: left for k_il_move, which copies rk anyway)
 __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__ rk, XSegs s,
                                                           const uint32_t *__restrict__ cnt, uint32_t *__restrict__ rt,
                                                           uint32_t *__restrict__ tbo, uint32_t *__restrict__ ncnt) {
@@ -327,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
         const uint32_t incl = base + (uint32_t)__popcll(m & ((2ull << lane) - 1ull));
         if (i < e) {
             const uint32_t j = incl - 1u;  // (a batch with more txns than tpr fails the pack's check)
-            rk[i] = w & ~GP_START;
+            if (!tbo) rk[i] = w & ~GP_START;  // (position-major: k_il_move clears it on the way)
             if (tbo) {
                 rt[i] = j;
                 if (f && j < s.tpr) tbo[(uint64_t)q * (s.tpr + 1) + j] = (uint32_t)(i - s.eoff[q]);
@@ -432,7 +442,7 @@ __global__ __launch_bounds__(kBlock) void k_il_move(const uint32_t *__restrict__
             const uint64_t d = (i - s.eoff[q]) + shift[(uint64_t)q * s.tpr + j];
             good = d < n_acc && (!WIDE || (d >= tb[t] && d < tb[t + 1]));
             if (good) {
-                ok[d] = rk[i];
+                ok[d] = rk[i] & ~(WIDE ? 0u : GP_START);
                 if (ot) ot[d] = t;
             }
         }
@@ -1706,6 +1716,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         if (compact) {
             ps.keys[e] = homes[e].keys;
             ps.types[e] = homes[e].types;
+            ps.recs[e] = homes[e].recs32;
             ps.txn[e] = homes[e].acc_txn;
             ps.n[e] = n;
             ps.off[e] = so;
