@@ -117,6 +117,9 @@ def parse():
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the config B (CALVIN) / C (OCC, 100M rows) legs and the CPU config A line")
     ap.add_argument("--tpcc-only", action="store_true", help="run and print only the TPC-C leg (profiling)")
+    ap.add_argument("--tpcc-no-async", action="store_true",
+                    help="A/B: TPC-C decisions without the asynchronous round launch (DV_FLAG_NO_ASYNC: pipelined "
+                         "rounds, then the one-workgroup LDS tail)")
     ap.add_argument("--tpcc-wh", type=int, default=32, help="warehouses per GPU (config E: 256 / 8)")
     ap.add_argument("--tpcc-part-wh", type=int, default=256,
                     help="N>1 (or --part1): warehouses of the partitioned TPC-C leg, split over the ranks")
@@ -246,7 +249,7 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
                            "Payment 50 % / NewOrder 50 %, full schema counts (100,000 items, 3,000 customers/district)",
                "bytes_per_txn_mean": tpcc_bytes_per_txn(eps[0]) / n_txn}
         for cc_name in cc_names:
-            eng = T.TpccEngine(cc_name, p, n_txn, seed=1, lsd_sort=a.lsd_sort)
+            eng = T.TpccEngine(cc_name, p, n_txn, seed=1, lsd_sort=a.lsd_sort, asynchronous=not a.tpcc_no_async)
             lanes = [eng.open_lane() for _ in range(max(1, a.lanes) - 1)]  # decision lanes, as config D
             dev = [T.device_epoch(e) for e in eps]
             d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")

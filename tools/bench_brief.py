@@ -3,6 +3,12 @@ import json
 import sys
 
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+if "value" not in d:  # (--tpcc-only: the TPC-C leg alone)
+    for size, leg in [("", d.get("tpcc", {}))] + [(k, v) for k, v in d.get("tpcc", {}).items() if k.startswith("window")]:
+        for cc, v in leg.items():
+            if isinstance(v, dict) and "ms_per_epoch" in v:
+                print(f"tpcc {size or 'main'} {cc}: {v['ms_per_epoch']:.4f} ms/epoch, {v['committed_per_s']:.4g} committed/s")
+    sys.exit(0)
 print(f"value {d['value']:.4g} {d['unit']}  ms/step {d['ms_per_step']:.4f}  abort {d.get('abort_rate', 0):.4f}")
 r = d["roofline"]
 print(f"roofline {r['kernel']}: {r['achieved']:.1f} GB/s frac {r['frac']:.4f} share {r.get('share_of_epoch', 0):.3f}")
