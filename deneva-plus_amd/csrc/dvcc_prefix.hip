@@ -150,7 +150,10 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
 // access, and the wave's verdicts stored as one ballot word -- k_kill_compact
 // then ORs each txn's range of bits.  (The conflict rule is the one in the
 // header comment; the txn id of an access is never needed here.)
-constexpr int kKillWords = 8;  // ballot words per wave per step (loads in flight)
+#ifndef DVCC_KILL_WORDS
+#define DVCC_KILL_WORDS 8
+#endif
+constexpr int kKillWords = DVCC_KILL_WORDS;  // ballot words per wave per step (loads in flight)
 constexpr int kKillBlock = 1024;  // one block per CU (144 KiB of LDS): 16 waves to stream with
 // KEYS (an epoch with its txn boundaries, launch_probe_tb): the later
 // accesses were never probed -- their rows come from their keys here (the

@@ -2435,6 +2435,12 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
     };
     auto run_sync = [&](uint32_t k) { return run(k, stats_of(k)); };
+    // DVCC_HOST_PROF=1: the host's time queueing epochs vs waiting for their
+    // read-backs, to stderr (is the host or the device the bound?)
+    static const bool hprof = std::getenv("DVCC_HOST_PROF") != nullptr;
+    using hclock = std::chrono::steady_clock;
+    double t_queue = 0, t_wait = 0;
+    const auto t_all = hclock::now();
     // read back the oldest queued epoch; a halted one and all behind it run again
     auto settle = [&]() -> int {
         Pend &p = ring[head];
@@ -2470,10 +2476,15 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
             prev = nullptr;
             continue;
         }
-        while (count >= window) {
-            const int r = settle();
-            if (r) return r;
+        {
+            const auto tw = hclock::now();
+            while (count >= window) {
+                const int r = settle();
+                if (r) return r;
+            }
+            t_wait += std::chrono::duration<double>(hclock::now() - tw).count();
         }
+        const auto tq = hclock::now();
         const uint32_t l = k % n_lanes;
         const int slot = (int)(lane_slot[l]++ & 1u);
         Pend &p = ring[(head + count) % (2 * kMaxLanes)];
@@ -2520,11 +2531,18 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         count++;
         prev = c;
         prev_slot = slot;
+        t_queue += std::chrono::duration<double>(hclock::now() - tq).count();
     }
+    const auto tw = hclock::now();
     while (count) {
         const int r = settle();
         if (r) return r;
     }
+    t_wait += std::chrono::duration<double>(hclock::now() - tw).count();
+    if (hprof && n)
+        std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f, waiting %.1f\n", n,
+                     n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
+                     t_queue * 1e6 / n, t_wait * 1e6 / n);
     return DV_OK;
 }
 
