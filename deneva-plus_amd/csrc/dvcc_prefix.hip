@@ -223,18 +223,30 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
                 ar[q] = i >= first && i < n ? acc_row[i] : ~0u;
             }
         }
+        // every access's state word first -- LDS (hot rows; the filter) or,
+        // a filter hit, the bitmap word from L2, all of the step's gathers in
+        // flight together -- then the verdicts (a gather per word, each
+        // awaited before the next word's, left k_kill latency-bound)
+        uint32_t sw[kKillWords];
+#pragma unroll
+        for (int q = 0; q < kKillWords; q++) {
+            sw[q] = 0;
+            if (ar[q] != ~0u) {
+                const uint32_t row = ar[q] & ~AR_WR;
+                if (row < kHotRows) {
+                    sw[q] = s_hot[row >> 4];
+                } else {
+                    const uint32_t h = bloom_bit(row);
+                    if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) sw[q] = row_state[row >> 4];  // maybe marked
+                }
+            }
+        }
 #pragma unroll
         for (int q = 0; q < kKillWords; q++) {
             bool kill = false, skip = false;
             if (ar[q] != ~0u) {
                 const uint32_t row = ar[q] & ~AR_WR;
-                uint32_t st = 0;
-                if (row < kHotRows) {
-                    st = (s_hot[row >> 4] >> ((row & 15u) * 2u)) & 3u;
-                } else {
-                    const uint32_t h = bloom_bit(row);
-                    if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) st = row_bits(row_state, row);  // maybe marked
-                }
+                const uint32_t st = (sw[q] >> ((row & 15u) * 2u)) & 3u;
                 kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
                 skip = st == RS_RD && !(ar[q] & AR_WR);  // (nowait only: skip_bits is null for OCC)
             }
