@@ -235,7 +235,7 @@ struct PackSrc {
     uint32_t n_txn[kXMaxP];
 };
 __global__ __launch_bounds__(kBlock) void k_group_pack_c(PackSrc src, uint32_t *__restrict__ k32_all,
-                                                         uint32_t *__restrict__ bad) {
+                                                         uint32_t *__restrict__ bad, int tbx) {
     const uint32_t e = blockIdx.y;
     const uint64_t *__restrict__ keys = src.keys[e];
     const uint8_t *__restrict__ types = src.types[e];
@@ -256,10 +256,13 @@ __global__ __launch_bounds__(kBlock) void k_group_pack_c(PackSrc src, uint32_t *
             k = keys[i];
             wr = types[i] == DV_WR;
         }
-        const uint32_t t = txn[i];
-        const uint32_t pt = i ? txn[i - 1] : 0u;
-        const bool start = i == 0 || t != pt;
-        if (t >= n_txn || (i == 0 ? t != 0u : (t != pt && t != pt + 1u))) b = true;
+        bool start = false;
+        if (!tbx) {  // (tbx: the batch's txn_begin travels beside it, k_group_pack_tb)
+            const uint32_t t = txn[i];
+            const uint32_t pt = i ? txn[i - 1] : 0u;
+            start = i == 0 || t != pt;
+            if (t >= n_txn || (i == 0 ? t != 0u : (t != pt && t != pt + 1u))) b = true;
+        }
         // (a key past 30 bits saturates and fails the decider's range check)
         k32[i] = ((k >> 30) ? 0x3FFFFFFFu : (uint32_t)k) | (start ? GP_START : 0u) | (wr ? 0x80000000u : 0u);
     }
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
 // segment, ncnt[q] entries valid (later j: the segment's end).
 __device__ __forceinline__ uint32_t il_start(const XSegs &s, const uint32_t *__restrict__ tbo,
                                              const uint32_t *__restrict__ ncnt, uint32_t q, uint32_t j) {
-    return j < ncnt[q] ? tbo[(uint64_t)q * (s.tpr + 1) + j] : (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
+    return !ncnt || j < ncnt[q] ? tbo[(uint64_t)q * (s.tpr + 1) + j] : (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
 }
 
 // wide batches (the senders' ids): tbo by a lower bound over each segment's
@@ -447,6 +450,105 @@ __global__ __launch_bounds__(kBlock) void k_il_move(const uint32_t *__restrict__
             }
         }
         b |= !good;
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+// ---- epoch groups whose batches bring their txn boundaries (every rank's
+// homes carry dv_epoch_dev::txn_begin and the decider takes tb mode; the
+// vote's "tbx"): each batch's txn_begin travels beside its rows, padded to
+// tpr + 1 entries (later entries: the batch's access count), so the decider
+// needs no start bits, no renumbering and no per-access txn ids.  A sender
+// checks its own boundaries (0 first, rising, its access count last): a bad
+// one fails the group (*bad, DV_ERR_ARG on every rank).
+struct PackTb {
+    const uint32_t *tb[kXMaxP];
+    uint32_t n_txn[kXMaxP];
+    uint64_t n_acc[kXMaxP];
+};
+__global__ __launch_bounds__(kBlock) void k_group_pack_tb(PackTb src, uint32_t tpr, uint32_t *__restrict__ out,
+                                                          uint32_t *__restrict__ bad) {
+    const uint32_t e = blockIdx.y, nt = src.n_txn[e];
+    const uint32_t *__restrict__ tb = src.tb[e];
+    const uint32_t na = (uint32_t)src.n_acc[e];
+    bool b = false;
+    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j <= tpr; j += gridDim.x * kBlock) {
+        uint32_t v = na;
+        if (j <= nt && tb) {
+            v = tb[j];
+            if ((j == 0 && v != 0u) || (j == nt && v != na) || (j > 0 && tb[j - 1] > v)) b = true;
+        } else if (j <= nt) {
+            b = na != 0u;  // (no boundaries: an empty batch only)
+        }
+        out[(uint64_t)e * (tpr + 1) + j] = v;
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+// origin-major: the decider's txn_begin -- origin q's txn j at q * tpr + j
+// starts at eoff[q] + its offset in q's batch; tb[P * tpr] = every access
+__global__ __launch_bounds__(kBlock) void k_tb_origin(XSegs s, const uint32_t *__restrict__ tbr,
+                                                      uint32_t *__restrict__ tb) {
+    const uint64_t n = (uint64_t)s.P * s.tpr;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t <= n; t += (uint64_t)gridDim.x * kBlock) {
+        if (t == n) {
+            tb[t] = (uint32_t)s.eoff[s.P];
+            continue;
+        }
+        uint64_t j = 0;
+        const uint64_t q = divmod_magic(t, s.tpr, s.mT, j);
+        tb[t] = (uint32_t)(s.eoff[q] + tbr[q * (s.tpr + 1) + j]);
+    }
+}
+
+// position-major with the boundaries (no per-access ids): a block per origin
+// and tile of kIlTxns txns stages their starts and shifts in LDS and each
+// txn's index over its accesses (a byte per access, runs of up to kIlOwn
+// accesses; a longer run finds its txns by a binary search of the starts),
+// then moves the tile's accesses, one per thread
+constexpr uint32_t kIlTxns = 256, kIlOwn = 8192;
+__global__ __launch_bounds__(kBlock) void k_il_move_tb(const uint32_t *__restrict__ rk, XSegs s,
+                                                       const uint32_t *__restrict__ tbo,
+                                                       const uint32_t *__restrict__ shift, uint64_t n_acc,
+                                                       uint32_t *__restrict__ ok, uint32_t *__restrict__ bad) {
+    __shared__ uint32_t l_st[kIlTxns + 1], l_sh[kIlTxns];
+    __shared__ uint8_t l_own[kIlOwn];
+    const uint32_t tiles = (s.tpr + kIlTxns - 1) / kIlTxns;
+    const uint32_t q = blockIdx.x / tiles, j0 = (blockIdx.x % tiles) * kIlTxns;
+    const uint32_t nj = s.tpr - j0 < kIlTxns ? s.tpr - j0 : kIlTxns;
+    const uint32_t *tq = tbo + (uint64_t)q * (s.tpr + 1);
+    const uint64_t seg = s.eoff[q + 1] - s.eoff[q];
+    for (uint32_t i = threadIdx.x; i <= nj; i += kBlock) l_st[i] = tq[j0 + i];
+    for (uint32_t i = threadIdx.x; i < nj; i += kBlock) l_sh[i] = shift[(uint64_t)q * s.tpr + j0 + i];
+    __syncthreads();
+    const uint32_t a0 = l_st[0], a1 = l_st[nj];
+    bool b = a1 < a0 || a1 > seg;
+    const bool own = !b && a1 - a0 <= kIlOwn;
+    if (own)
+        for (uint32_t i = threadIdx.x; i < nj; i += kBlock)
+            for (uint32_t a = l_st[i]; a < l_st[i + 1] && a >= a0 && a < a1; a++) l_own[a - a0] = (uint8_t)i;
+    __syncthreads();
+    for (uint32_t p = a0 + threadIdx.x; !b && p < a1; p += kBlock) {
+        uint32_t lo = 0;
+        if (own) {
+            lo = l_own[p - a0];
+        } else {
+            uint32_t hi = nj;  // largest k with l_st[k] <= p
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (l_st[mid] <= p) lo = mid;
+                else hi = mid;
+            }
+        }
+        if (lo >= nj) {  // (boundaries a sender already reported bad)
+            b = true;
+            break;
+        }
+        // (every sender checked its boundaries, k_group_pack_tb: the stores
+        // need only stay inside the epoch when one reported them bad)
+        const uint64_t d = (uint64_t)p + l_sh[lo];
+        if (d < n_acc) ok[d] = rk[s.eoff[q] + p];
+        else b = true;
     }
     if (b) atomicOr(bad, 1u);
 }
@@ -800,6 +902,7 @@ struct DvComm {
     uint32_t *tbo = nullptr, *ncnt = nullptr;   // k_il_begin's inputs
     uint32_t *iltb = nullptr, *ilsh = nullptr;  // ... its outputs: the decider's txn_begin, the move's shifts
     uint8_t *ilv = nullptr;                     // commit bytes back in origin order
+    uint32_t *tbs = nullptr, *tbr = nullptr;    // tbx: the batches' txn_begin, padded (sent, received)
 };
 
 }  // namespace dvcc
@@ -1138,7 +1241,7 @@ void free_bufs(DvComm *m) {
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
-                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv};
+                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv, m->tbs, m->tbr};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -1154,6 +1257,7 @@ void free_bufs(DvComm *m) {
     m->gtc = m->gbad = nullptr;
     m->ilk = m->ilt = m->tbo = m->ncnt = m->iltb = m->ilsh = nullptr;
     m->ilv = nullptr;
+    m->tbs = m->tbr = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -1196,6 +1300,8 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
         CHK(alloc(&m->iltb, (uint64_t)txn + 1));
         CHK(alloc(&m->ilsh, txn));
         CHK(alloc(&m->ilv, txn));
+        CHK(alloc(&m->tbs, (uint64_t)txn + P));
+        CHK(alloc(&m->tbr, (uint64_t)txn + P));
     }
     const size_t mail_bytes = sizeof(CommMail) + 8 * mail_words(P);
     CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), mail_bytes,
@@ -1665,6 +1771,18 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     // position-major sequence (DV_COMM_POSITION_ORDER; CALVIN keeps its origin order)
     const bool il = m->position && cfg.cc_alg != DV_CALVIN && P > 1 && P <= kXMaxP;  // (one origin: the same order)
     rec[6] = il ? 1u : 0u;
+    // tbx: every batch brings its txn_begin and the decider will take tb mode
+    // (a prefix-kill epoch) -- the boundaries travel, nothing is renumbered
+    bool has_tb = m->tbs != nullptr;
+    for (uint32_t e = 0; e < P && !bad; e++) has_tb &= homes[e].txn_begin != nullptr || homes[e].n_txn == 0;
+    {
+        dv_epoch_dev probe{};
+        probe.n_txn = (uint32_t)n_txn64;
+        probe.txn_begin = m->iltb;
+        probe.recs32 = m->ilk;
+        has_tb = has_tb && group_tb_epoch(c, &probe);
+    }
+    rec[7] = has_tb ? 1u : 0u;
     for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
     // (and the compact pack's bad flag cleared for this group: a group that
     // failed after setting it must not leave it to the next one)
@@ -1683,11 +1801,12 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         }
     }
     uint64_t gmax = 0;
-    bool refuse = false, compact = true;
+    bool refuse = false, compact = true, tbx = true;
     for (uint32_t q = 0; q < P; q++) {
         const uint64_t *r = &all[(size_t)q * W];
         gmax = std::max<uint64_t>(gmax, r[0]);
         compact &= r[5] == 0;
+        tbx &= r[7] == 1;
         refuse |= r[1] || r[2] || r[3] != all[3] || r[6] != all[6];  // (every rank the same order)
         uint64_t in = 0;  // what rank q receives: its epoch's batches
         for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
@@ -1695,6 +1814,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         recvc[q] = r[kGroupRecHead + m->rank];
     }
     if (refuse) return DV_ERR_ARG;  // every rank
+    tbx = tbx && compact;
     const uint32_t glen = (uint32_t)std::min<uint64_t>(gmax ? gmax : 1u, kMaxPos);
 
     // 2. every batch to its decider: [row id | wr << 31, 4 B | txn id, 4 B],
@@ -1742,12 +1862,28 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     }
     if (compact && nmax) {
         const uint32_t bx = (uint32_t)std::min<uint64_t>((nmax + kBlock - 1) / kBlock, std::max(1u, 2048u / P));
-        DV_LAUNCH(k_group_pack_c, dim3(bx, P), kBlock, 0, s, ps, sk, m->gbad);
+        DV_LAUNCH(k_group_pack_c, dim3(bx, P), kBlock, 0, s, ps, sk, m->gbad, tbx ? 1 : 0);
+    }
+    std::vector<size_t> bc(P), bd(P);  // tbx: the boundaries, tpr + 1 words per batch either way
+    if (tbx) {
+        PackTb pt{};
+        for (uint32_t e = 0; e < P; e++) {
+            pt.tb[e] = homes[e].txn_begin;
+            pt.n_txn[e] = homes[e].n_txn;
+            pt.n_acc[e] = homes[e].n_acc;
+            bc[e] = 4ull * (txns_per_rank + 1);
+            bd[e] = bc[e] * e;
+        }
+        const uint32_t bx = std::max(1u, std::min((txns_per_rank + kBlock) / kBlock, std::max(1u, 2048u / P)));
+        DV_LAUNCH(k_group_pack_tb, dim3(bx, P), kBlock, 0, s, pt, txns_per_rank, m->tbs, m->gbad);
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
     CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
                           reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
+    if (tbx)
+        CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->tbs), bc.data(), bd.data(),
+                              reinterpret_cast<uint8_t *>(m->tbr), bc.data(), bd.data(), s));
     if (!compact)
         CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
                               reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
@@ -1756,7 +1892,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     xs.toff[P] = xtiles;
     xs.mP = div_magic(P);
     xs.mT = div_magic(txns_per_rank);
-    if (compact && xtiles) {
+    if (compact && xtiles && !tbx) {
         DV_LAUNCH(k_group_txn_count, xtiles, kBlock, 0, s, rk, xs, m->gtc, il ? m->ncnt : nullptr);
         DV_LAUNCH(k_group_txn_ids, xtiles, kBlock, 0, s, rk, xs, m->gtc, rt, il ? m->tbo : nullptr,
                   il ? m->ncnt : nullptr);
@@ -1773,7 +1909,27 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     ep.n_txn = (uint32_t)n_txn64;
     ep.max_txn_acc = glen;
     const uint32_t *ek = rk;
-    if (il) {
+    const uint64_t ntx = (uint64_t)P * txns_per_rank;
+    if (tbx && !il) {  // origin-major with the boundaries: the landed batches as they are, tb mode
+        DV_LAUNCH(k_tb_origin, (uint32_t)std::min<uint64_t>((ntx + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbr,
+                  m->iltb);
+        CHK(hip_fail2(hipGetLastError(), "k_tb_origin"));
+        ep.txn_begin = m->iltb;
+        ep.recs32 = rk;
+        ep.acc_txn = nullptr;
+    } else if (tbx) {  // position-major with the boundaries: interleaved by txn tiles
+        ek = m->ilk;
+        ep.keys = reinterpret_cast<const uint64_t *>(ek);
+        ep.txn_begin = m->iltb;
+        ep.recs32 = ek;
+        ep.acc_txn = nullptr;
+        DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((ntx + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbr,
+                  (const uint32_t *)nullptr, m->iltb, m->ilsh);
+        const uint32_t tiles = (txns_per_rank + kIlTxns - 1) / kIlTxns;
+        if (ro && tiles)
+            DV_LAUNCH(k_il_move_tb, P * tiles, kBlock, 0, s, rk, xs, m->tbr, m->ilsh, ro, m->ilk, m->gbad);
+        CHK(hip_fail2(hipGetLastError(), "k_il_move_tb"));
+    } else if (il) {
         // position-major: the landed batches interleaved txn by txn, with the
         // epoch's boundaries -- a prefix-kill decider then reads those and the
         // 32-bit rows as its records (tb mode), no per-access txn ids
