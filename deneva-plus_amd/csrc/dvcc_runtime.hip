@@ -2319,7 +2319,10 @@ int lane_streams(dv_ctx *const *lanes, uint32_t n_lanes) {
         // (3/4 of what the share holds: with all of it, three lanes' launches
         // never found their workgroups co-resident -- the CU mask's bits do
         // not split every way evenly -- 2.7 ms per epoch; with 3/4, 0.29)
-        c->lane_g = std::max(1u, (uint32_t)((uint64_t)c->async_g * mine * 3 / 4 / (uint32_t)cus));
+#ifndef DVCC_LANE_G_EIGHTHS
+#define DVCC_LANE_G_EIGHTHS 6  // (the asynchronous launch's share of a lane's workgroups, in eighths)
+#endif
+        c->lane_g = std::max(1u, (uint32_t)((uint64_t)c->async_g * mine * DVCC_LANE_G_EIGHTHS / 8 / (uint32_t)cus));
     }
     return DV_OK;
 }
