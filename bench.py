@@ -254,14 +254,16 @@ def tpcc_leg(a, cc_names=("WAIT_DIE", "CALVIN")):
             dev = [T.device_epoch(e) for e in eps]
             d_commit = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
             d_oid = torch.zeros(n_txn, dtype=torch.int64, device="cuda")
-            k = max(a.steps, 5) if si == 0 else max(a.steps, 20)
+            # (the window's epochs are short: 200 of them amortise the lanes'
+            # fill and drain, ~2 ms in all)
+            k = max(a.steps, 50) if si == 0 else max(4 * a.steps, 200)
 
             def batch(m):  # the pipelined entry point (epoch k+1 queued before k is read back)
                 ne = len(dev)
                 return eng.run_tpcc_epochs_device([dev[i % ne][0] for i in range(m)],
                                                   [dev[i % ne][1] for i in range(m)], d_commit, d_oid, lanes=lanes)
             if a.warmup:
-                batch(a.warmup)
+                batch(max(a.warmup, 2 * (1 + len(lanes))))
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             sts = batch(k)
