@@ -130,6 +130,8 @@ struct Counters {
     unsigned long long pass_live;  // live accesses every k_round_pass of the epoch read, summed
     unsigned long long async_live; // live accesses entering every asynchronous launch that ran, summed
     uint32_t spin_site;       // with ERRB_SPIN: 1 look-back, 2 asynchronous rounds, 3 tail (max seen)
+    uint32_t async_done;      // workgroups of the asynchronous launch that finished (its last one finalizes;
+                              // reset by it)
     uint32_t nlive[2];    // live accesses of the current / next decision round
     uint32_t nund[2];     // undecided-txn list lengths (single-GPU settle)
     uint32_t log_live[kRoundLog];  // per round: live accesses entering it

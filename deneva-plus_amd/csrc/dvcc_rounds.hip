@@ -1096,6 +1096,66 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
 // 28 elements per thread 0.565 ms per epoch, 4 / 28 0.574-0.585, 28 alone 0.615)
 constexpr int kAsyncIPTTiny = 1, kAsyncIPTSmall = 4;
 
+// after the asynchronous rounds: the status bytes from the words and the
+// count of txns left undecided (an error).  The outcome goes to pub->tl
+// (r0 << 32 | code, RoundPub).  A declined launch changed nothing; like a
+// yielded one it halts execution (Counters::halt) and blocks further tries, and
+// the host resumes the synchronous rounds at r0.
+__device__ __forceinline__ void publish_try(RoundPub *pub, uint32_t r0, uint32_t code) {
+    if (pub)
+        __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | code, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// fin (small epochs, words == 0): the launch's last workgroup does
+// k_round_finalize's work itself -- one launch fewer per epoch, for epochs
+// whose txns one workgroup writes back in a few passes (kFinTxns)
+constexpr uint32_t kFinTxns = 16384;
+__device__ void finalize_go(uint8_t *__restrict__ status, const uint32_t *__restrict__ tword, uint32_t n_txn,
+                            uint32_t r0, RoundPub *pub, const uint32_t *__restrict__ n_txn_dev, Counters *ctr) {
+    __shared__ uint32_t s_und;
+    const bool yielded = __hip_atomic_load(&ctr->halt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (threadIdx.x == 0) {
+        s_und = 0;
+        if (yielded) {
+            ctr->async_yields++;
+            ctr->async_block = 1u;
+            publish_try(pub, r0, 3u);
+        } else {
+            ctr->async_r0 = r0;
+            ctr->nund[r0 & 1] = 0;
+            if (pub)
+                __hip_atomic_store(&pub->ai, ((unsigned long long)r0 << 32) | ctr->async_iters, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            publish_try(pub, r0, 4u);
+        }
+    }
+    if (n_txn_dev && *n_txn_dev < n_txn) n_txn = *n_txn_dev;
+    uint32_t und = 0;
+    constexpr uint32_t kU = 8;  // (a thread's word loads in flight together)
+    for (uint32_t t0 = 0; t0 < n_txn; t0 += kU * blockDim.x) {
+        uint32_t w[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t t = t0 + u * blockDim.x + threadIdx.x;
+            w[u] = t < n_txn ? __hip_atomic_load(tword + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t t = t0 + u * blockDim.x + threadIdx.x;
+            if (t < n_txn) {
+                const uint8_t st = word_status(w[u]);
+                status[t] = st;
+                und += st == ST_UNDEC ? 1u : 0u;
+            }
+        }
+    }
+    __syncthreads();
+    if (und) atomicAdd(&s_und, und);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_und && !yielded) atomicAdd(&my_slot(ctr).undecided, s_und);
+}
+
 // words: no finalize follows (a prefix-kill stage: k_prefix_mark /
 // k_sub_scatter_back read the statuses from the words); the launch then does
 // the finalize's bookkeeping itself -- a declined try halts, a yield halts
@@ -1104,7 +1164,8 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
                                                                uint32_t r0, uint32_t thresh,
                                                                uint32_t *tword, uint32_t *carry,
                                                                int nowait, uint32_t max_iters,
-                                                               uint64_t idle, int words) {
+                                                               uint64_t idle, int words, int fin, uint32_t n_txn,
+                                                               RoundPub *pub) {
     __shared__ uint32_t sel[kAsyncCap];
     __shared__ RAgg rw[kAsyncWaves];
     __shared__ Agg wt[kAsyncWaves];
@@ -1120,11 +1181,12 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
         ctr->async_go = go;  // for the finalize (its inputs change there)
         if (go == 1u) ctr->async_live += n_all;
         if (words && go == 1u) ctr->async_wr0 = r0;
-        if (words && go == 2u) {
+        if ((words || fin) && go == 2u) {
             ctr->async_declined++;
             ctr->async_block = 1u;
             ctr->halt = 1u;
         }
+        if (fin) publish_try(pub, r0, go == 2u ? 2u : 5u);
     }
     if (go != 1u) return;  // declined or nothing to do: the synchronous rounds go on
     const uint64_t per = ((uint64_t)n_all + G - 1) / G;  // the largest slice (uniform)
@@ -1137,17 +1199,20 @@ __global__ __launch_bounds__(kAsyncThreads, 4) void k_round_async(RoundBufs b, c
     else
         async_slices<kAsyncIPT>(b, src, n_all, tword, carry, nowait, max_iters, idle, sel, rw, wt, s_needy,
                                 s_moved, s_cin, s_quit, words != 0);
-}
-
-// after the asynchronous rounds: the status bytes from the words and the
-// count of txns left undecided (an error).  The outcome goes to pub->tl
-// (r0 << 32 | code, RoundPub).  A declined launch changed nothing; like a
-// yielded one it halts execution (Counters::halt) and blocks further tries, and
-// the host resumes the synchronous rounds at r0.
-__device__ __forceinline__ void publish_try(RoundPub *pub, uint32_t r0, uint32_t code) {
-    if (pub)
-        __hip_atomic_store(&pub->tl, ((unsigned long long)r0 << 32) | code, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (fin) {  // the last workgroup to finish finalizes (every other's facts are published)
+        __shared__ uint32_t s_last;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence();
+            s_last = atomicAdd(&ctr->async_done, 1u) == G - 1u ? 1u : 0u;
+        }
+        __syncthreads();
+        if (s_last) {
+            __threadfence();
+            finalize_go(b.status, tword, n_txn, r0, pub, b.n_txn_dev, ctr);
+            if (threadIdx.x == 0) ctr->async_done = 0;
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_round_finalize(uint8_t *__restrict__ status,
@@ -1258,9 +1323,10 @@ void round_async(hipStream_t s, const RoundBufs &b, uint32_t r0, int nowait, uin
         DV_LAUNCH(k_async_words, txn_grid(n_txn > G ? n_txn : G), kBlock, 0, s, b.status, b.vb8, b.slog, b.tlen,
                                                                     n_txn, tword, carry, G, thresh, r0,
                                                                     b.n_txn_dev, b.ctr);
+    const bool fin = !words && n_txn <= kFinTxns;  // (the last workgroup finalizes)
     DV_LAUNCH(k_round_async, G, kAsyncThreads, 0, s, b, src, r0, thresh, tword, carry, nowait, max_iters, idle_ticks,
-              words ? 1 : 0);
-    if (!words)
+              words ? 1 : 0, fin ? 1 : 0, n_txn, pub);
+    if (!words && !fin)
         DV_LAUNCH(k_round_finalize, txn_grid(n_txn), kBlock, 0, s, b.status, tword, n_txn, r0, pub, b.n_txn_dev,
                   b.ctr);
 }

@@ -2442,7 +2442,7 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     // read-backs, to stderr (is the host or the device the bound?)
     static const bool hprof = std::getenv("DVCC_HOST_PROF") != nullptr;
     using hclock = std::chrono::steady_clock;
-    double t_queue = 0, t_wait = 0;
+    double t_queue = 0, t_wait = 0, t_decide = 0;
     const auto t_all = hclock::now();
     // read back the oldest queued epoch; a halted one and all behind it run again
     auto settle = [&]() -> int {
@@ -2492,7 +2492,9 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         const int slot = (int)(lane_slot[l]++ & 1u);
         Pend &p = ring[(head + count) % (2 * kMaxLanes)];
         p.k = k;
+        const auto td = hclock::now();
         int r = decide(c, k);
+        t_decide += std::chrono::duration<double>(hclock::now() - td).count();
         if (!r && prev) {
             r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
             if (!r) launch_lane_gate(c->stream, prev->d_gate + prev_slot, c->ctr);
@@ -2543,9 +2545,9 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     }
     t_wait += std::chrono::duration<double>(hclock::now() - tw).count();
     if (hprof && n)
-        std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f, waiting %.1f\n", n,
-                     n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
-                     t_queue * 1e6 / n, t_wait * 1e6 / n);
+        std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f (decision %.1f), "
+                     "waiting %.1f\n", n, n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
+                     t_queue * 1e6 / n, t_decide * 1e6 / n, t_wait * 1e6 / n);
     return DV_OK;
 }
 
