@@ -195,10 +195,86 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t w0 = first >> 6, nw = (n + 63) >> 6;
     const uint64_t waves = (uint64_t)gridDim.x * (kKillBlock / 64);
-    for (uint64_t w = w0 + ((uint64_t)blockIdx.x * (kKillBlock / 64) + (threadIdx.x >> 6)) * kKillWords; w < nw;
-         w += waves * kKillWords) {
-        uint32_t ar[kKillWords];
-        if constexpr (KEYS) {
+    const uint64_t wstep = waves * kKillWords;
+    // the state words of a step's accesses -- LDS (hot rows; the filter) or, a
+    // filter hit, the bitmap word from L2, all of the step's gathers in flight
+    // together -- then the verdicts
+    auto states = [&](const uint32_t *ar, uint32_t *sw) {
+#pragma unroll
+        for (int q = 0; q < kKillWords; q++) {
+            sw[q] = 0;
+            if (ar[q] != ~0u) {
+                const uint32_t row = ar[q] & ~AR_WR;
+                if (row < kHotRows) {
+                    sw[q] = s_hot[row >> 4];
+                } else {
+                    const uint32_t h = bloom_bit(row);
+                    if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) sw[q] = row_state[row >> 4];  // maybe marked
+                }
+            }
+        }
+    };
+    auto verdicts = [&](uint64_t w, const uint32_t *ar, const uint32_t *sw) {
+#pragma unroll
+        for (int q = 0; q < kKillWords; q++) {
+            bool kill = false, skip = false;
+            if (ar[q] != ~0u) {
+                const uint32_t row = ar[q] & ~AR_WR;
+                const uint32_t st = (sw[q] >> ((row & 15u) * 2u)) & 3u;
+                kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
+                skip = st == RS_RD && !(ar[q] & AR_WR);  // (nowait only: skip_bits is null for OCC)
+            }
+            const uint64_t m = __ballot(kill), sm = __ballot(skip);
+            if (lane == 0 && w + q < nw) {
+                kill_bits[w + q] = m;
+                if (skip_bits) skip_bits[w + q] = sm;
+            }
+        }
+    };
+    const uint64_t wbeg = w0 + ((uint64_t)blockIdx.x * (kKillBlock / 64) + (threadIdx.x >> 6)) * kKillWords;
+    if (KEYS == 0 || (KEYS == 2 && kk.recs)) {
+        // one 4-byte word per access (acc_row, or the dense map's records):
+        // software-pipelined -- the next step's words are loaded behind this
+        // step's gathers, so the stream's latency overlaps the verdicts
+        const uint32_t *src = KEYS == 0 ? acc_row : kk.recs;
+        uint32_t nxt[kKillWords];
+        auto load = [&](uint64_t w) {
+#pragma unroll
+            for (int q = 0; q < kKillWords; q++) {
+                const uint64_t i = ((w + q) << 6) + lane;
+                nxt[q] = w < nw && i >= first && i < n ? src[i] : ~0u;
+            }
+        };
+        load(wbeg);
+        for (uint64_t w = wbeg; w < nw; w += wstep) {
+            uint32_t ar[kKillWords], sw[kKillWords];
+#pragma unroll
+            for (int q = 0; q < kKillWords; q++) {
+                ar[q] = nxt[q];
+                if constexpr (KEYS == 2) {  // key | wr << 31 -> row | AR_WR (a missing key rejects the epoch)
+                    const uint64_t i = ((w + q) << 6) + lane;
+                    if (i >= first && i < n) {
+                        const uint32_t key = nxt[q] & 0x7FFFFFFFu;
+                        if (key < kk.dense_lim) {
+                            ar[q] = (uint32_t)(key + kk.dense_base) | (nxt[q] & AR_WR);
+                        } else {
+                            set_err(ctr, ERRB_KEY);
+                            ar[q] = ~0u;
+                        }
+                    } else {
+                        ar[q] = ~0u;
+                    }
+                }
+            }
+            states(ar, sw);
+            load(w + wstep);
+            verdicts(w, ar, sw);
+        }
+        return;
+    }
+    for (uint64_t w = wbeg; w < nw; w += wstep) {
+        uint32_t ar[kKillWords], sw[kKillWords];
+        if constexpr (KEYS != 0) {
             uint64_t key[kKillWords];
             uint32_t wr[kKillWords];
             bool in[kKillWords];
@@ -216,46 +292,9 @@ __global__ __launch_bounds__(kKillBlock) void k_kill(const uint32_t *__restrict_
                 if (in[q] && kk_row<KEYS == 2>(kk, key[q], row, ctr))
                     ar[q] = (uint32_t)row | (wr[q] ? AR_WR : 0u);
             }
-        } else {
-#pragma unroll
-            for (int q = 0; q < kKillWords; q++) {
-                const uint64_t i = ((w + q) << 6) + lane;
-                ar[q] = i >= first && i < n ? acc_row[i] : ~0u;
-            }
         }
-        // every access's state word first -- LDS (hot rows; the filter) or,
-        // a filter hit, the bitmap word from L2, all of the step's gathers in
-        // flight together -- then the verdicts (a gather per word, each
-        // awaited before the next word's, left k_kill latency-bound)
-        uint32_t sw[kKillWords];
-#pragma unroll
-        for (int q = 0; q < kKillWords; q++) {
-            sw[q] = 0;
-            if (ar[q] != ~0u) {
-                const uint32_t row = ar[q] & ~AR_WR;
-                if (row < kHotRows) {
-                    sw[q] = s_hot[row >> 4];
-                } else {
-                    const uint32_t h = bloom_bit(row);
-                    if ((s_bloom[h >> 5] >> (h & 31u)) & 1u) sw[q] = row_state[row >> 4];  // maybe marked
-                }
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kKillWords; q++) {
-            bool kill = false, skip = false;
-            if (ar[q] != ~0u) {
-                const uint32_t row = ar[q] & ~AR_WR;
-                const uint32_t st = (sw[q] >> ((row & 15u) * 2u)) & 3u;
-                kill = (st & RS_WR) || (nowait && st && (ar[q] & AR_WR));
-                skip = st == RS_RD && !(ar[q] & AR_WR);  // (nowait only: skip_bits is null for OCC)
-            }
-            const uint64_t m = __ballot(kill), sm = __ballot(skip);
-            if (lane == 0 && w + q < nw) {
-                kill_bits[w + q] = m;
-                if (skip_bits) skip_bits[w + q] = sm;
-            }
-        }
+        states(ar, sw);
+        verdicts(w, ar, sw);
     }
 }
 
