@@ -119,17 +119,26 @@ __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict_
         } else if (status[t] != ST_COMMIT) {
             continue;
         }
-        for (uint32_t a = tb_start[t], e = tb_end[t]; a < e; a++) {
-            const uint32_t ar = acc_row[a];
-            const uint32_t row = ar & ~AR_WR;
-            const uint32_t bit = (ar & AR_WR) ? RS_WR : (nowait ? RS_RD : 0u);
-            if (!bit) continue;
-            if (row < kHotRows) {
-                atomicOr(&s_hot[row >> 4], bit << ((row & 15u) * 2u));
-            } else {
-                atomicOr(&row_state[row >> 4], bit << ((row & 15u) * 2u));
-                const uint32_t h = bloom_bit(row);
-                atomicOr(&bloom[h >> 5], 1u << (h & 31u));
+        // (a chunk's row words loaded before any of its atomics)
+        constexpr uint32_t kMU = 8;
+        for (uint32_t a0 = tb_start[t], e = tb_end[t]; a0 < e; a0 += kMU) {
+            uint32_t arw[kMU];
+#pragma unroll
+            for (uint32_t u = 0; u < kMU; u++) arw[u] = a0 + u < e ? acc_row[a0 + u] : 0u;
+#pragma unroll
+            for (uint32_t u = 0; u < kMU; u++) {
+                if (a0 + u >= e) continue;
+                const uint32_t ar = arw[u];
+                const uint32_t row = ar & ~AR_WR;
+                const uint32_t bit = (ar & AR_WR) ? RS_WR : (nowait ? RS_RD : 0u);
+                if (!bit) continue;
+                if (row < kHotRows) {
+                    atomicOr(&s_hot[row >> 4], bit << ((row & 15u) * 2u));
+                } else {
+                    atomicOr(&row_state[row >> 4], bit << ((row & 15u) * 2u));
+                    const uint32_t h = bloom_bit(row);
+                    atomicOr(&bloom[h >> 5], 1u << (h & 31u));
+                }
             }
         }
     }
