@@ -440,7 +440,17 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
     }
     if (wave < 2) {  // the tiles before this one: wave 0 survivors, wave 1 their accesses
         uint32_t sum = 0;
-        for (uint32_t q = lane; q < tile; q += 64) sum += tsum[2 * q + wave];
+        // (8 loads per lane in flight at once: a late tile sums ~1,000 earlier ones)
+        for (uint32_t q0 = 0; q0 < tile; q0 += 8 * 64) {
+            uint32_t v[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t q = q0 + u * 64 + lane;
+                v[u] = q < tile ? tsum[2 * q + wave] : 0u;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) sum += v[u];
+        }
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
         if (lane == 0) {
