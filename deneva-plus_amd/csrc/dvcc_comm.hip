@@ -828,7 +828,8 @@ __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint
     // batch the position-major move refused (k_il_move), fails the group as an
     // argument error -- whatever its decision made of the input; the flag is
     // reset for the next group
-    if (*pack_bad) fail = (uint32_t)(-DV_ERR_ARG);
+    const bool refused = *pack_bad != 0;
+    if (refused) fail = (uint32_t)(-DV_ERR_ARG);
     __syncthreads();
     if (threadIdx.x == 0) *pack_bad = 0;
     for (uint32_t q = threadIdx.x; q < P; q += blockDim.x) rec[kGroupRecHead + q] = fail ? 0u : tot[q];
@@ -836,7 +837,8 @@ __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint
         rec[0] = fail;
         rec[1] = committed;
         rec[2] = cap;
-        for (uint32_t k = 3; k < kGroupRecHead; k++) rec[k] = 0;
+        rec[3] = refused ? 1u : 0u;  // (a refused batch decides the group's code on every rank)
+        for (uint32_t k = 4; k < kGroupRecHead; k++) rec[k] = 0;
     }
 }
 
@@ -1970,14 +1972,19 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
     uint64_t gfail = 0, committed = 0;
+    bool refused = false;
     for (uint32_t q = 0; q < P; q++) {
         const uint64_t *r = &all[(size_t)q * W];
         gfail = std::max<uint64_t>(gfail, r[0]);
+        refused |= r[3] != 0;
         committed += r[1];
         uint64_t in = 0;
         for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
         if (in > r[2]) gfail = std::max<uint64_t>(gfail, (uint64_t)(-DV_ERR_ARG));
     }
+    // a batch its sender (or the move) refused makes the group an argument
+    // error on every rank, whatever the deciders made of it
+    if (refused) gfail = (uint64_t)(-DV_ERR_ARG);
     if (gfail) return -(int)gfail;
 
     // 5. records to their owners, commit bytes back to their origins

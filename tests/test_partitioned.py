@@ -613,7 +613,7 @@ def _group_mine(c_ref, r, n_txn, world, cc, position):
 
 
 def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False,
-                        wide=False, position=False):
+                        wide=False, position=False, prefix=0):
     """Every epoch of every group against the one-partition oracle run over
     the sequenced epochs one after the other: commit bytes (each rank holds its
     own txns' bytes of every epoch), committed count, digest and writes summed
@@ -623,10 +623,14 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
     dv_epoch_group_run_batch call (rows checked after the last group).
     wide: 8-byte batches (DV_COMM_WIDE_BATCHES) instead of the compact ones.
     position: the origins' batches sequenced txn by txn (DV_COMM_POSITION_ORDER;
-    CALVIN keeps origin order)."""
+    CALVIN keeps origin order).  prefix: dv_set_prefix on every decider (a
+    prefix-kill epoch at any size: the groups' boundaries path, tbx)."""
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
     engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
+    if prefix:
+        for eng in engines:
+            eng.set_prefix(prefix)
     if wide or position:
         for eng in engines:
             eng.comm_set_mode(2 | (dvcc._lib.DV_COMM_WIDE_BATCHES if wide else 0) |
@@ -744,6 +748,49 @@ def test_epoch_groups_position_order_prefix_kill():
     prefix-kill path (4 x 40,000 txns, MPR 0 and 0.1)."""
     _check_epoch_groups(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.0, groups=1, position=True)
     _check_epoch_groups(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, groups=1, position=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("world,position", [(2, False), (2, True), (4, True)])
+def test_epoch_groups_with_boundaries(cc, world, position):
+    """Prefix-kill deciders (a forced prefix of 400 txns) over batches that
+    carry their txn_begin: the boundaries travel beside rows without start
+    bits (the vote's tbx), the decider renumbers nothing -- origin-major as
+    landed, position-major through the tile move -- against the oracle; and
+    unequal batches (padded boundaries)."""
+    _check_epoch_groups(cc, world, 1 << 13, 2000, 0.3, position=position, prefix=400)
+    _check_epoch_groups(cc, 3, 1 << 13, 1000, 0.3, sizes=[1000, 640, 1], position=position, prefix=300)
+
+
+@pytest.mark.gpu
+def test_epoch_groups_bad_boundaries_fail_collectively():
+    """A batch whose txn_begin falls inside (handed over as a DeviceEpoch with
+    a tampered boundary): its sender's check fails the group with DV_ERR_ARG
+    on every rank, no row changes, and the next group runs normally."""
+    world, rows_pp, n_txn = 2, 1 << 12, 1500
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2)
+    for eng in engines:
+        eng.set_prefix(300)
+        eng.comm_set_mode(2 | dvcc._lib.DV_COMM_POSITION_ORDER)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    homes = [[dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(r, 120 + e), r)) for e in range(world)]
+             for r in range(world)]
+    bad = dvcc.DeviceEpoch(gen.gen(n_txn, dvcc.epoch_seed(1, 130), 1))
+    bad.txn_begin[9] = bad.txn_begin[11] + 1  # (not rising)
+    bad_homes = [list(h) for h in homes]
+    bad_homes[1][0] = bad
+    res = _run_group_epochs(engines, bad_homes, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_ARG, (r, x)
+    for eng, b0 in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b0).all()
+    res = _run_group_epochs(engines, homes, n_txn)
+    assert all(not isinstance(x, Exception) for x in res), res
+    for eng in engines:
+        eng.close()
 
 
 @pytest.mark.gpu
