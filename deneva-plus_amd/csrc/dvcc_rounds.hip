@@ -162,12 +162,21 @@ template <class EIn>
 #ifndef DVCC_ROUND_T64
 #define DVCC_ROUND_T64 512
 #endif
+// 64-bit elements (round 0 over the sorted pairs): 8 per thread, 4,096-element
+// tiles -- a prefix-kill stage's 328K / 563K pairs in 80 / 138 workgroups
+// instead of 40 / 69 (round 0 18.9 -> 16.2 us at config D; 16 per thread 18.9,
+// 256 threads x 16 21.3; profiles/r04_rt2)
+#ifndef DVCC_ROUND_IPT64
+#define DVCC_ROUND_IPT64 8
+#endif
 struct Geo {
     static constexpr int kThreads = sizeof(EIn) == 4 ? 1024 : DVCC_ROUND_T64;
     static constexpr int kMinWaves = sizeof(EIn) == 4 ? 4 : 3;  // per SIMD: <= 128 / 168 VGPRs
     static constexpr int kWaves = kThreads / 64;
-    static constexpr int kIPT = DVCC_ROUND_IPT;
+    static constexpr int kIPT = sizeof(EIn) == 4 ? DVCC_ROUND_IPT : DVCC_ROUND_IPT64;
     static constexpr uint32_t kTile = kThreads * kIPT;
+    // the look-back descriptors are sized for kRTile-element tiles (dvcc_common.h)
+    static_assert(kTile >= (uint32_t)kRTile, "round tiles at least kRTile elements");
 };
 __device__ __forceinline__ uint32_t pad16(uint32_t j) { return j + (j >> 4); }
 
@@ -955,24 +964,15 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
     uint64_t last_move = wall_clock64();  // thread 0's: the last iteration that decided something
     for (; it < max_iters; it++) {
         const uint32_t p = it & 1u;
-        // the value in front of the slice: carries back to the nearest head
-        // (read by wave 0 here, taken from LDS after keep_bits' barrier)
-        if (cont_in && wave == 0) {
-            uint32_t acc = 0;
-            for (int64_t j0 = (int64_t)g - 1;; j0 -= 64) {
-                const int64_t j = j0 - (int64_t)lane;
-                const uint32_t w = j >= 0 ? __hip_atomic_load(carry + j, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT)
-                                          : kCarryHead;  // (slice 0 starts with a head)
-                const uint64_t hm = __ballot((w & kCarryHead) != 0);
-                const uint32_t stop = hm ? (uint32_t)__builtin_ctzll(hm) : 64u;
-                uint32_t v = lane <= stop ? (w & ~kCarryHead) : 0u;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
-                acc |= v;
-                if (hm) break;
-            }
-            if (lane == 0) s_cin = acc;
+        // the value in front of the slice: carries back to the nearest head,
+        // read by wave 0; the first 64 carry words are loaded here, before
+        // the facts, and resolved after them (one round trip for both)
+        const bool look = cont_in && wave == 0;
+        uint32_t cw = 0u;
+        if (look) {
+            const int64_t j = (int64_t)g - 1 - (int64_t)lane;
+            cw = j >= 0 ? __hip_atomic_load(carry + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : kCarryHead;  // (slice 0 starts with a head)
         }
         const uint32_t k = (n + kAsyncThreads - 1) / kAsyncThreads;
         const uint32_t first = tid * k;
@@ -994,6 +994,22 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
                 const bool single = (e[j] & F_HEAD) && nh;
                 blk |= (M)(s != ST_ABORT && !single ? 1u : 0u) << j;
             }
+        }
+        if (look) {  // (taken from LDS after keep_bits' barrier)
+            uint32_t acc = 0;
+            for (int64_t j0 = (int64_t)g - 1;; j0 -= 64) {
+                const uint64_t hm = __ballot((cw & kCarryHead) != 0);
+                const uint32_t stop = hm ? (uint32_t)__builtin_ctzll(hm) : 64u;
+                uint32_t v = lane <= stop ? (cw & ~kCarryHead) : 0u;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
+                acc |= v;
+                if (hm) break;
+                const int64_t j = j0 - 64 - (int64_t)lane;
+                cw = j >= 0 ? __hip_atomic_load(carry + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                            : kCarryHead;
+            }
+            if (lane == 0) s_cin = acc;
         }
         // a queue running into the next slice is assumed to be followed by a
         // needy element there (keep_bits holds a barrier: every thread is done
