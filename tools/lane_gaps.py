@@ -3,6 +3,7 @@ rocprofv3 kernel trace, per queue its busy fraction and the idle time before
 each kernel, summed by that kernel's name (a gap before k_lane_gate / the
 execution is a wait for the previous epoch's execution on another lane; a gap
 before k_epoch_clear is the lane waiting for the host to queue its next epoch).
+Also each kernel's mean duration in that window (on its lane's CU share).
     python tools/lane_gaps.py run_kernel_trace.csv [--gap 200]"""
 import csv
 import sys
@@ -53,6 +54,15 @@ def main():
               + ", ".join(f"{n} {t / 1e3:.1f}" for n, t in top))
     print("idle before, all queues: " + ", ".join(f"{n} {t / 1e3:.1f}" for n, t in
                                                  sorted(tot_gap.items(), key=lambda kv: -kv[1])[:8]))
+    # each kernel's duration beside the other lanes (its CU share), per epoch
+    dur = {}
+    for s_, e_, _, n in w:
+        d = dur.setdefault(n, [0, 0])
+        d[0] += 1
+        d[1] += e_ - s_
+    print("kernel durations in the window (launches per epoch, mean us, us per epoch):")
+    for n, (c, t) in sorted(dur.items(), key=lambda kv: -kv[1][1]):
+        print(f"  {n:24s} x {c / max(1, epochs):5.2f} {t / c / 1e3:8.1f} {t / 1e3 / max(1, epochs):8.1f}")
 
 
 if __name__ == "__main__":
