@@ -29,3 +29,15 @@ def test_summary_line_parses_like_helper_py():
     assert s["tput"] == [75.0] and s["total_runtime"] == [2.0]
     assert s["local_txn_start_cnt"] == [256.0] and s["record_write_cnt"] == [750.0]
     assert summary_line(1.0, st, prog=True).startswith("[prog] ")
+    # single / multi-partition counts and parts touched are commit-time
+    # counters (txn.cpp:581-587, 600-602), not per started txn
+    assert s["single_part_txn_cnt"] == [150.0] and s["multi_part_txn_cnt"] == [0.0]
+    assert s["parts_touched"] == [150.0] and s["avg_parts_touched"] == [1.0]
+    s2 = {}
+    _process_results(s2, re.split(",", summary_line(2.0, st, multi_part_txn_cnt=30, parts_touched=180)[10:]))
+    assert s2["single_part_txn_cnt"] == [120.0] and s2["avg_parts_touched"] == [1.2]
+    # txn_run_time: each committed txn's latency is its epoch's time (txn.cpp:580)
+    assert s["txn_run_time"] == [150.0] and s["txn_run_avg_time"] == [1.0]
+    s3 = {}
+    _process_results(s3, re.split(",", summary_line(2.0, st, epoch_seconds=[0.5, 2.0])[10:]))
+    assert s3["txn_run_time"] == [150.0] and s3["txn_run_avg_time"] == [1.0]
