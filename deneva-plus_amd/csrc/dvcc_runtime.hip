@@ -2311,11 +2311,8 @@ int lane_streams(dv_ctx *const *lanes, uint32_t n_lanes) {
         c->lane_stream = nullptr;
         std::vector<uint32_t> mask((cus + 31) / 32, 0u);
         uint32_t mine = 0;
-#ifndef DVCC_LANE_MASK_RUN
-#define DVCC_LANE_MASK_RUN 1  // CUs per run of mask bits given to one lane
-#endif
         for (int i = 0; i < cus; i++)
-            if ((uint32_t)(i / DVCC_LANE_MASK_RUN) % n_lanes == l) mask[i / 32] |= 1u << (i % 32), mine++;
+            if ((uint32_t)i % n_lanes == l) mask[i / 32] |= 1u << (i % 32), mine++;
         HIPCHK(hipExtStreamCreateWithCUMask(&c->lane_stream, (uint32_t)mask.size(), mask.data()));
         c->lane_n = n_lanes;
         c->lane_l = l;
