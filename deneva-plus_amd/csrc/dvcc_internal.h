@@ -623,10 +623,13 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
                  Counters *ctr, RowMap rm = RowMap{});
 // NO_WAIT / WAIT_DIE / OCC: in txn order over the committed txns, with the
 // commit bytes into d_commit (may be NULL) and the committed count, as
-// launch_commit_out would
+// launch_commit_out would.  pk_dense: the rows are a dense one-partition YCSB
+// map whose row r holds key r - pk_base (k_ycsb_load), so a read's primary
+// key comes from its row instead of a second random line of the pkey column
 void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
-                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit);
+                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
+                     bool pk_dense = false, uint64_t pk_base = 0);
 void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
                        Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,

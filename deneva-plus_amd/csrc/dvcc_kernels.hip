@@ -1348,7 +1348,8 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      const uint8_t *__restrict__ status,
                                                      uint64_t *__restrict__ f0,
                                                      const uint64_t *__restrict__ pkey,
-                                                     Counters *ctr, RowMap rm, uint8_t *__restrict__ commit_out) {
+                                                     Counters *ctr, RowMap rm, uint8_t *__restrict__ commit_out,
+                                                     int pk_dense, uint64_t pk_base) {
     __shared__ unsigned long long part[3][4];
     if (ctr->halt) return;  // rounds not finished (dv_epoch_finish resumes them)
     const bool rows = !input_err(ctr);  // a rejected epoch changes no row
@@ -1393,7 +1394,7 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
             uint64_t row = ar & ~AR_WR;
             if (!own_row(rm, row)) continue;  // (replicated epochs: another partition's row)
             if ((MODE & EX_READS) && !(ar & AR_WR))
-                dig += mix64(f0[row] ^ mix64(((uint64_t)tt << 32) ^ pkey[row]));
+                dig += mix64(f0[row] ^ mix64(((uint64_t)tt << 32) ^ (pk_dense ? row - pk_base : pkey[row])));
             if ((MODE & EX_WRITES) && (ar & AR_WR)) {
                 f0[row] = 0;  // *(uint64_t*)&data[0] = 0 (ycsb_txn.cpp:239-242)
                 wcnt++;
@@ -1423,18 +1424,20 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
 
 void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
-                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit) {
+                     const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
+                     bool pk_dense, uint64_t pk_base) {
+    const int pkd = pk_dense && rm.P == 0 ? 1 : 0;  // (replicated epochs read the column)
     if (n_txn == 0) return;
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
         DV_LAUNCH((k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn,
-                                                                              status, f0, pkey, ctr, rm, d_commit);
+                                                                              status, f0, pkey, ctr, rm, d_commit, pkd, pk_base);
     } else {
         DV_LAUNCH((k_exec_txn<EX_READS | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                                   pkey, ctr, rm, d_commit);
+                                                                   pkey, ctr, rm, d_commit, pkd, pk_base);
         DV_LAUNCH((k_exec_txn<EX_WRITES>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                        pkey, ctr, rm, nullptr);
+                                                        pkey, ctr, rm, nullptr, pkd, pk_base);
     }
 }
 
