@@ -111,6 +111,9 @@ def parse():
                          "read instead")
     ap.add_argument("--lsd-sort", action="store_true",
                     help="A/B: sort with the plain LSD passes (DV_FLAG_LSD_SORT), no bucket sort")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="the full record (kernel tables, every leg) as JSON; stdout carries one compact line "
+                         "('' = not written)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tpcc", action="store_true", help="skip the TPC-C (config E) leg")
@@ -184,7 +187,7 @@ def cpu_baseline_mt(epochs, rows, seconds):
 
     def run(threads, secs):
         f0 = tab.f0.copy()
-        lock = np.zeros(rows, np.uint32)
+        lock = O.mt_lock(rows)
         committed = txns = 0
         t0 = time.perf_counter()
         i = 0
@@ -429,7 +432,7 @@ def cpu_config_a(seconds):
     epochs = gen_epochs(gen, n, 0, 4)
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
-    lock = np.zeros(rows, np.uint32)
+    lock = O.mt_lock(rows)
     committed = txns = i = 0
     t0 = time.perf_counter()
     while True:
@@ -1022,6 +1025,127 @@ def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
         out["tpcc_partitioned"] = tpcc_part_leg(a, world, pb.rank, int(os.environ.get("LOCAL_RANK", 0)), nxt)
 
 
+LINE_LIMIT = 8192  # bytes of the stdout record (the driver parses the tail of stdout)
+
+
+def _r(v, sig=4):
+    """A float at `sig` significant digits (the record's numbers)."""
+    if isinstance(v, float):
+        return float(f"{v:.{sig}g}")
+    return v
+
+
+def _pick(d, keys):
+    return {k: _r(d[k]) for k in keys if isinstance(d, dict) and k in d and not isinstance(d[k], (dict, list))}
+
+
+def headline_record(out, detail_path=None):
+    """The ONE stdout line: the headline (metric, value, unit, n_gpus, steps,
+    warmup, ms_per_step, ...), the dominant kernel's roofline, the CPU
+    baseline and a few numbers per side leg; everything else -- kernel
+    tables, leg detail, samples -- stays in the detail file (`detail_path`).
+    Stays under LINE_LIMIT bytes whatever the legs hold."""
+    rec = {k: _r(out[k]) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                   "higher_is_better", "scaling", "vs_baseline", "dtype", "data") if k in out}
+    cfg = out.get("config", {})
+    rec["config"] = {k: cfg[k] for k in ("workload", "cc_alg", "rows_per_partition", "txns_per_epoch",
+                                         "txns_per_epoch_per_gpu", "req_per_query", "zipf_theta", "mpr",
+                                         "parallelism", "decision_lanes", "epochs_per_step", "sequence_order",
+                                         "ordered_lanes_refused") if k in cfg}
+    for k in ("sequence_order", "ordered_lanes_refused"):
+        if isinstance(rec["config"].get(k), str):
+            rec["config"][k] = rec["config"][k][:80]
+    rf = out.get("roofline") or {}
+    rec["roofline"] = {k: _r(rf.get(k)) for k in ("kernel", "bound", "achieved", "peak", "unit", "frac", "traffic",
+                                                  "bytes_per_launch", "avg_launch_ms", "launches_per_epoch",
+                                                  "share_of_epoch")}
+    if isinstance(rf.get("k_probe"), dict):
+        rec["roofline"]["k_probe"] = _pick(rf["k_probe"], ("kernel", "frac", "achieved", "avg_launch_ms"))
+    cb = out.get("cpu_baseline")
+    if isinstance(cb, dict):
+        rec["cpu_baseline"] = _pick(cb, ("value", "unit", "cores", "kind"))
+        rec["cpu_baseline"]["sample"] = str(cb.get("sample", ""))[:160]
+        if isinstance(cb.get("threads_scaling"), dict):
+            rec["cpu_baseline"]["threads_scaling"] = {k: _r(v) for k, v in cb["threads_scaling"].items()}
+    if isinstance(out.get("cpu_baseline_single_thread"), dict):
+        rec["cpu_baseline_single_thread"] = _pick(out["cpu_baseline_single_thread"], ("value", "cores", "kind"))
+    for k in ("abort_rate", "decided_txns_per_s"):
+        if k in out:
+            rec[k] = _r(out[k])
+    for k in ("epoch_roofline", "decide_stage_roofline"):
+        if isinstance(out.get(k), dict):
+            rec[k] = _r(out[k].get("frac"))
+    if "kernel_us_per_epoch" in out:
+        rec["kernel_us_per_epoch"] = _r(out["kernel_us_per_epoch"])
+    legs = {}
+    for leg in ("config_b", "config_c"):
+        d = out.get(leg)
+        if isinstance(d, dict):
+            legs[leg] = _pick(d, ("cc_alg", "ms_per_epoch", "committed_per_s", "abort_rate", "error"))
+            if isinstance(d.get("roofline"), dict):
+                legs[leg]["roofline"] = _pick(d["roofline"], ("kernel", "frac", "avg_launch_ms"))
+            if isinstance(d.get("epoch_roofline"), dict):
+                legs[leg]["epoch_roofline"] = _r(d["epoch_roofline"].get("frac"))
+    tp = out.get("tpcc")
+    if isinstance(tp, dict):
+        t = {}
+        for name, d in [(k, v) for k, v in tp.items() if isinstance(v, dict)]:
+            for cc, v in ([(name, d)] if "ms_per_epoch" in d else [(f"{name}_{c}", x) for c, x in d.items()
+                                                                  if isinstance(x, dict)]):
+                if "ms_per_epoch" in v:
+                    t[cc] = _pick(v, ("ms_per_epoch", "committed_per_s", "abort_rate"))
+                    if isinstance(v.get("epoch_roofline"), dict):
+                        t[cc]["epoch_roofline"] = _r(v["epoch_roofline"].get("frac"))
+                    if isinstance(v.get("cpu_baseline"), dict):
+                        t[cc]["cpu_baseline"] = _r(v["cpu_baseline"].get("value"))
+        legs["tpcc"] = t
+    if isinstance(out.get("cpu_config_a"), dict):
+        legs["cpu_config_a"] = _pick(out["cpu_config_a"], ("value", "unit", "cores", "kind", "abort_rate"))
+    cl = out.get("closed_loop_retry")
+    if isinstance(cl, dict):
+        legs["closed_loop_retry"] = _pick(cl, ("ms_per_epoch", "committed_per_s"))
+        if isinstance(cl.get("lanes"), dict):
+            legs["closed_loop_retry"]["lanes"] = _pick(cl["lanes"], ("ms_per_epoch", "committed_per_s",
+                                                                     "decision_lanes"))
+    for leg in ("strong_scaling", "weak_scaling"):
+        if isinstance(out.get(leg), dict):
+            legs[leg] = _pick(out[leg], ("txns_per_epoch", "ms_per_epoch", "committed_per_s", "abort_rate"))
+    if isinstance(out.get("mpr_sweep"), list):
+        legs["mpr_sweep"] = [_pick(m, ("mpr", "ms_per_step", "committed_per_s", "abort_rate"))
+                             for m in out["mpr_sweep"][:8]]
+    tpp = out.get("tpcc_partitioned")
+    if isinstance(tpp, dict):
+        legs["tpcc_partitioned"] = {k: _pick(v, ("txns_per_epoch", "ms_per_epoch", "committed_per_s"))
+                                    for k, v in tpp.items() if isinstance(v, dict)}
+    for k in ("extra_legs_error",):
+        if k in out:
+            legs[k] = str(out[k])[:200]
+    rec["legs"] = legs
+    for k in ("src_hash", "timing_in_timed_region"):
+        if k in out:
+            rec[k] = out[k]
+    if detail_path:
+        rec["detail"] = detail_path
+    line = json.dumps(rec)
+    if len(line) > LINE_LIMIT:  # (never expected: the legs are the first to go)
+        rec["legs"] = {"dropped": f"{len(line)} B > {LINE_LIMIT}: see the detail file"}
+        line = json.dumps(rec)
+    return line
+
+
+def write_detail(out, path):
+    """The full record (kernel tables, every leg) beside the stdout line."""
+    try:
+        d = os.path.dirname(os.path.abspath(path))
+        os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(out, f)
+        return os.path.relpath(os.path.abspath(path), ROOT)
+    except OSError as ex:
+        print(f"bench: detail file not written: {ex!r}", file=sys.stderr)
+        return None
+
+
 def main():
     a = parse()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -1187,7 +1311,9 @@ def main():
             out["cpu_baseline"] = single
     if rank == 0:  # Deneva's [summary] line (stats.cpp:425-500) for scripts/helper.py, on stderr
         from dvcc.stats import summary_line
-        out["deneva_summary"] = summary_line(el, stats)
+        # (partitioned runs do not count their multi-partition commits: those
+        # four counters are left out rather than printed as one-partition)
+        out["deneva_summary"] = summary_line(el, stats, part_counts=not part)
         print(out["deneva_summary"], file=sys.stderr, flush=True)
     if not part and not a.no_tpcc:
         out["tpcc"] = tpcc_leg(a)
@@ -1204,7 +1330,9 @@ def main():
         if rank == 0 and not a.no_cpu_baseline:
             out["cpu_config_a"] = cpu_config_a(min(a.cpu_seconds, 10.0))
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        path = write_detail(out, a.detail_out) if a.detail_out else None
+        sys.stderr.flush()
+        print(headline_record(out, path), flush=True)
     if eng is not None:
         eng.close()
     if world > 1:

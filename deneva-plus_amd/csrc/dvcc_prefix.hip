@@ -570,7 +570,9 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
                         if (l_fpre[mid] <= g) lo = mid;
                         else hi = mid;
                     }
-                    atomicOr(&l_skip[lo], 1u << (g - l_fpre[lo]));
+                    // (one word holds a survivor of <= 32 accesses; a longer
+                    // one takes its kept accesses from k_kill's skip_bits)
+                    if (l_fpre[lo + 1] - l_fpre[lo] <= 32u) atomicOr(&l_skip[lo], 1u << (g - l_fpre[lo]));
                 }
             }
         }
@@ -597,9 +599,13 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
             uint32_t a = 0;
             if (g < na) {
                 if constexpr (KEYS) {  // the qv-th access of the survivor whose skip bit is clear
-                    uint32_t kept = ~l_skip[lo];
-                    for (uint32_t r = qv[u]; r; r--) kept &= kept - 1;
-                    a = l_a0[lo] + (uint32_t)__builtin_ctz(kept);
+                    if (l_fpre[lo + 1] - l_fpre[lo] <= 32u) {
+                        uint32_t kept = ~l_skip[lo];
+                        for (uint32_t r = qv[u]; r; r--) kept &= kept - 1;
+                        a = l_a0[lo] + (uint32_t)__builtin_ctz(kept);
+                    } else {  // (longer than one skip word: k_kill's bits, the same rule)
+                        a = skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u];
+                    }
                 } else {
                     a = skip_bits ? nth_kept(skip_bits, l_a0[lo], qv[u]) : l_a0[lo] + qv[u];
                 }

@@ -1502,10 +1502,12 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
             launch_exec(c->stream, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->f0, c->pkey, c->ctr,
                         rm);
         else {  // (the commit bytes and count too)
-            const KillKeys dk = kill_keys(make_tables(c), nullptr, nullptr, nullptr);  // (its dense test)
+            // (its dense test; only with table 0 the context's one table -- a
+            // row of another table takes its key from the pkey column)
+            const KillKeys dk = kill_keys(make_tables(c), nullptr, nullptr, nullptr);
             launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
                             c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit,
-                            dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep, dk.dense_base);
+                            dk.tabs.n == 1 && dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep, dk.dense_base);
             return;
         }
     }

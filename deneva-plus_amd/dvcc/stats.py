@@ -10,7 +10,8 @@ prints them (x / BILLION).  Counters of subsystems outside this path
 """
 
 
-def summary_fields(total_runtime_s, stats, multi_part_txn_cnt=0, parts_touched=None, epoch_seconds=None):
+def summary_fields(total_runtime_s, stats, multi_part_txn_cnt=0, parts_touched=None, epoch_seconds=None,
+                   part_counts=True):
     """stats: dv_stats of the epochs run in total_runtime_s (one partition's
     view; committed/aborted are global per epoch, as every rank decides every
     txn).  multi_part_txn_cnt / parts_touched: over the COMMITTED txns, as
@@ -19,7 +20,9 @@ def summary_fields(total_runtime_s, stats, multi_part_txn_cnt=0, parts_touched=N
     committed txns' latencies (txn.cpp:580): an epoch's txns start together
     and commit when it is decided, so each one's latency is its epoch's time --
     epoch_seconds[e] when given, else the epoch's share of the run (a lower
-    bound when epochs overlap on decision lanes)."""
+    bound when epochs overlap on decision lanes).  part_counts=False leaves
+    the four partition counters out (a partitioned run that did not count
+    them: the one-partition default would understate them)."""
     txn_cnt = sum(int(s.committed) for s in stats)       # INC_STATS(txn_cnt) on commit (txn.cpp:578)
     aborts = sum(int(s.aborted) for s in stats)           # total_txn_abort_cnt (stats.cpp:447)
     started = sum(int(s.n_txn) for s in stats)
@@ -31,7 +34,7 @@ def summary_fields(total_runtime_s, stats, multi_part_txn_cnt=0, parts_touched=N
     tput = txn_cnt / run if run > 0 else 0.0             # stats.cpp:436-437
     parts = txn_cnt if parts_touched is None else int(parts_touched)
     single = txn_cnt - int(multi_part_txn_cnt)
-    return [
+    out = [
         ("total_runtime", run),
         ("tput", tput),
         ("txn_cnt", txn_cnt),
@@ -54,6 +57,10 @@ def summary_fields(total_runtime_s, stats, multi_part_txn_cnt=0, parts_touched=N
         ("parts_touched", parts),
         ("avg_parts_touched", parts / txn_cnt if txn_cnt else 0.0),
     ]
+    if not part_counts:
+        drop = {"multi_part_txn_cnt", "single_part_txn_cnt", "parts_touched", "avg_parts_touched"}
+        out = [kv for kv in out if kv[0] not in drop]
+    return out
 
 
 def summary_line(total_runtime_s, stats, prog=False, **kw):

@@ -143,6 +143,7 @@ uint64_t or_table_digest(const uint64_t *f0, uint64_t n);
 
 /* ---- Deneva-style multi-threaded NO_WAIT engine (mt_engine.c),
  * a throughput baseline; its aborts depend on the interleaving ---- */
+uint64_t or_mt_lock_words(uint64_t nrows);  /* the lock array or_mt_epoch_run takes */
 int or_mt_epoch_run(const or_index *ix, uint64_t *f0, uint32_t *lock, uint64_t nrows, uint32_t n_txn,
                     const uint32_t *tb, const uint64_t *keys, const uint8_t *types, int threads,
                     uint64_t *committed, uint64_t *digest);

@@ -84,6 +84,8 @@ def lib():
         L.or_mt_epoch_run.argtypes = [ctypes.c_void_p, u64p, u32p, ctypes.c_uint64, ctypes.c_uint32, u32p,
                                       u64p, u8p, ctypes.c_int, u64p, u64p]
         L.or_mt_epoch_run.restype = ctypes.c_int
+        L.or_mt_lock_words.argtypes = [ctypes.c_uint64]
+        L.or_mt_lock_words.restype = ctypes.c_uint64
         L.or_index_read_mid.argtypes = [ctypes.c_void_p, ctypes.c_uint64, u64p]
         L.or_index_read_mid.restype = ctypes.c_int
         L.or_grand_seed.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
@@ -249,10 +251,17 @@ class MultiIndex:
             pass
 
 
+def mt_lock(rows):
+    """The zeroed lock array mt_epoch_run takes for `rows` rows (the hot rows'
+    words one per cache line, or_mt_lock_words)."""
+    return np.zeros(lib().or_mt_lock_words(rows), np.uint32)
+
+
 def mt_epoch_run(ix, f0, lock, n_txn, tb, keys, types, threads):
     """SURVEY.md 8(d)(ii) baseline: Deneva-style multi-threaded NO_WAIT
-    (oracle/mt_engine.c).  lock: uint32 zeros, one per row.  Returns
-    (committed, read digest); its aborts depend on the interleaving."""
+    (oracle/mt_engine.c).  lock: mt_lock(len(f0)).  Returns (committed, read
+    digest); its aborts depend on the interleaving."""
+    assert len(lock) >= lib().or_mt_lock_words(len(f0))
     c, d = ctypes.c_uint64(), ctypes.c_uint64()
     rc = lib().or_mt_epoch_run(ix, _p(f0, ctypes.c_uint64), _p(lock, ctypes.c_uint32), len(f0), n_txn,
                                _p(tb, ctypes.c_uint32), _p(keys, ctypes.c_uint64), _p(types, ctypes.c_uint8),

@@ -536,6 +536,47 @@ def test_direct_index_table(order):
         eng.close()
 
 
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+def test_dense_ycsb_table_beside_a_second_table(cc):
+    """A dense YCSB partition (table 0) beside a chained table 1 in one
+    context: the execution takes a table-0 read's primary key from its row
+    (row - base, the dense map), but a table-1 row's from its pkey column --
+    the committed-read digest and both tables equal the oracle's over the
+    combined key space."""
+    rows0, n1 = 1 << 14, 3000
+    rng = np.random.default_rng(21)
+    keys1 = (np.uint64(rows0 * 10) + rng.permutation(n1 * 4)[:n1].astype(np.uint64))
+    f01 = rng.integers(1, 2**63, size=n1, dtype=np.uint64)
+    base = O.YcsbTable(rows0)
+    ix = O.MultiIndex(rows0 + n1, 1, 0, list(zip(range(rows0), range(rows0)))
+                      + list(zip(keys1.tolist(), range(rows0, rows0 + n1))))
+    n_txn, R = 2000, 8
+    ak = np.empty(n_txn * R, np.uint64)
+    tabs = np.zeros(n_txn * R, np.uint8)
+    at = rng.integers(0, 2, size=n_txn * R).astype(np.uint8)
+    for t in range(n_txn):
+        half = R // 2
+        ak[t * R:t * R + half] = rng.choice(rows0 // 4, size=half, replace=False).astype(np.uint64)
+        ak[t * R + half:(t + 1) * R] = keys1[rng.choice(n1, size=R - half, replace=False)]
+        tabs[t * R + half:(t + 1) * R] = 1
+    tb = (np.arange(n_txn + 1) * R).astype(np.uint32)
+    ref_f0 = np.concatenate([base.f0, f01])
+    c_ref, _, st_ref = O.epoch_run(ORACLE_CC[cc], ix.ix, ref_f0, n_txn, tb, ak, at)
+    eng = CCEngine(cc, n_txn, n_txn * R)
+    try:
+        eng.load_ycsb_partition(rows0)
+        eng.create_table(1, n1, 2 * n1, dvcc.HASH_MOD)
+        eng.load_table(1, keys1, f01)
+        c, _, st = eng.run_epoch(Epoch(ak, at, tb, tables=tabs))
+        assert (c == c_ref).all()
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt)
+        assert (eng.read_table(0, rows0) == ref_f0[:rows0]).all()
+        assert (eng.read_rows(keys1, table=1) == ref_f0[rows0:]).all()
+    finally:
+        eng.close()
+
+
 # ---- BASELINE.json sizes (configs B, C, D at N=1), bit-exact against the oracle
 @pytest.mark.slow
 def test_config_b_calvin_full():
@@ -1033,12 +1074,15 @@ def _prefix_engine(cc, rows, n_txn, n_acc, prefix):
 
 
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
-@pytest.mark.parametrize("rows,R,theta", [(1 << 18, 10, 0.9), (1 << 12, 16, 0.99), (1 << 16, 4, 0.5)])
+@pytest.mark.parametrize("rows,R,theta", [(1 << 18, 10, 0.9), (1 << 12, 16, 0.99), (1 << 16, 4, 0.5),
+                                          (1 << 20, 48, 0.5), (1 << 22, 64, 0.3)])
 def test_prefix_epochs_with_and_without_txn_begin(cc, rows, R, theta):
     """The same prefix-kill epochs through both range sources -- the epoch's
     own boundaries (with its accesses as 4-byte records or as keys and types)
     and acc_txn -- give the oracle's commit bytes, digests, write counts and
-    table, epoch after epoch (repeated rows included)."""
+    table, epoch after epoch (repeated rows included).  R = 48 / 64: survivors
+    longer than one 32-bit skip word, several hundred of them with skipped
+    reads (k_kill_emit takes their kept accesses from k_kill's skip bits)."""
     g = YCSBQueryGenerator(rows, zipf_theta=theta, req_per_query=R, txn_write_perc=1.0, tup_write_perc=0.5)
     es = [g.gen(9_000, 1300 + k) for k in range(3)]
     for with_tb, recs in ((True, True), (True, False), (False, False)):  # (+ 4-byte records, dv_epoch_dev::recs32)

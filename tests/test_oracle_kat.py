@@ -333,7 +333,7 @@ def test_mt_baseline_engine():
     for threads in (1, 4):
         tab = O.YcsbTable(rows)
         f0 = tab.f0.copy()
-        lock = np.zeros(rows, np.uint32)
+        lock = O.mt_lock(rows)
         committed, _ = O.mt_epoch_run(tab.ix, f0, lock, n, tb, keys, types, threads)
         assert not lock.any()
         if threads == 1:

@@ -41,3 +41,15 @@ def test_summary_line_parses_like_helper_py():
     s3 = {}
     _process_results(s3, re.split(",", summary_line(2.0, st, epoch_seconds=[0.5, 2.0])[10:]))
     assert s3["txn_run_time"] == [150.0] and s3["txn_run_avg_time"] == [1.0]
+
+
+def test_summary_line_without_partition_counts():
+    """A partitioned run that did not count its multi-partition commits leaves
+    the four partition counters out instead of printing the one-partition
+    default (multi_part_txn_cnt=0, avg_parts_touched=1)."""
+    st = [types.SimpleNamespace(committed=100, aborted=28, n_txn=128, write_cnt=500)]
+    s = {}
+    _process_results(s, re.split(",", summary_line(1.0, st, part_counts=False)[10:]))
+    assert s["txn_cnt"] == [100.0]
+    for k in ("multi_part_txn_cnt", "single_part_txn_cnt", "parts_touched", "avg_parts_touched"):
+        assert k not in s

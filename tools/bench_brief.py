@@ -1,8 +1,13 @@
 """One-screen summary of a bench.py JSON line: headline, roofline, kernel table."""
 import json
+import os
 import sys
 
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+if os.path.exists(str(d.get("detail"))):  # (the compact line: the full record is in the detail file)
+    line = d
+    d = json.load(open(d["detail"]))
+    print(f"stdout line {len(json.dumps(line))} B; detail {line['detail']}")
 if "value" not in d:  # (--tpcc-only: the TPC-C leg alone)
     for size, leg in [("", d.get("tpcc", {}))] + [(k, v) for k, v in d.get("tpcc", {}).items() if k.startswith("window")]:
         for cc, v in leg.items():

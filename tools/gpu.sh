@@ -30,7 +30,7 @@ run_one() {
         || { tail -30 $out/smoke.log; return 1; }
     tail -3 $out/smoke.log ;;
   bench)
-    timeout -k 10 900 python -u bench.py "$@" > $out/bench.json 2> $out/bench.err \
+    timeout -k 10 900 python -u bench.py --detail-out $out/bench_detail.json "$@" > $out/bench.json 2> $out/bench.err \
         || { tail -30 $out/bench.err; return 1; }
     python3 tools/bench_brief.py $out/bench.json ;;
   ab)
