@@ -698,11 +698,13 @@ class CCEngine:
                 "dv_epoch_begin")
 
     def round_local(self, d_verdict):
+        self._after_torch()  # (d_verdict may come from a torch kernel still queued)
         L.check(L.lib().dv_epoch_round_local(self._ctx, _ptr(d_verdict)), "dv_epoch_round_local")
 
     def round_apply(self, d_verdict, wait=True):
         """Applies the combined verdicts; wait=False only enqueues the apply
         (read its outcome with round_wait)."""
+        self._after_torch()
         und = ctypes.c_uint32()
         L.check(L.lib().dv_epoch_round_apply(self._ctx, _ptr(d_verdict),
                                              ctypes.byref(und) if wait else None),
@@ -718,14 +720,17 @@ class CCEngine:
     def errors_local(self, d_word):
         """Partitioned epochs: enqueue this partition's input-error bits into
         the device int32 tensor d_word (combine with MAX across ranks)."""
+        self._after_torch()
         L.check(L.lib().dv_epoch_errors_local(self._ctx, _ptr(d_word)), "dv_epoch_errors_local")
 
     def errors_combined(self, d_word):
         """... and hand the combined word back: an error anywhere rejects the
         epoch on every partition, at the same round."""
+        self._after_torch()
         L.check(L.lib().dv_epoch_errors_combined(self._ctx, _ptr(d_word)), "dv_epoch_errors_combined")
 
     def finish(self, d_commit=None):
+        self._after_torch()  # (d_commit may be a torch.zeros still queued)
         st = L.Stats()
         L.check(L.lib().dv_epoch_finish(self._ctx, _ptr(d_commit), ctypes.byref(st)),
                 "dv_epoch_finish")
