@@ -869,6 +869,16 @@ constexpr int kAsyncIPT = DVCC_ASYNC_IPT;
 constexpr uint32_t kAsyncCap = (uint32_t)kAsyncThreads * kAsyncIPT;  // elements per workgroup
 
 constexpr uint32_t TW_OK = 1u << 8;  // one more access OK
+
+#ifdef DVCC_ASYNC_STAMPS
+// measurement builds only (tools/exp_variant.sh ... -DDVCC_ASYNC_STAMPS): per
+// workgroup of k_round_async, summed over launches, thread 0's wall-clock
+// ticks (100 MHz) -- [0] launches, [1] iterations, [2] ticks in the loop,
+// [3] iteration start -> facts loaded, [4] -> carry walk done, [5] -> end of
+// the iteration's work (decide, compact, publish, barriers), [6] back-off,
+// [7] iterations that decided something; read by dv_debug_async_stamps
+__device__ unsigned long long g_async_stamps[kAsyncGroups * 8];
+#endif
 // the status fact of txn t
 __device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t) {
     return word_status(__hip_atomic_load(tword + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -962,8 +972,15 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
     uint32_t it = 0;
     bool yielded = true;                  // cleared when the slice has nothing left to learn
     uint64_t last_move = wall_clock64();  // thread 0's: the last iteration that decided something
+#ifdef DVCC_ASYNC_STAMPS
+    uint64_t st_facts = 0, st_carry = 0, st_work = 0, st_sleep = 0, st_moved = 0, st_ti = 0, st_tf = 0;
+    const uint64_t st_begin = wall_clock64();
+#endif
     for (; it < max_iters; it++) {
         const uint32_t p = it & 1u;
+#ifdef DVCC_ASYNC_STAMPS
+        st_ti = wall_clock64();
+#endif
         // the value in front of the slice: carries back to the nearest head,
         // read by wave 0; the first 64 carry words are loaded here, before
         // the facts, and resolved after them (one round trip for both)
@@ -995,6 +1012,11 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
                 blk |= (M)(s != ST_ABORT && !single ? 1u : 0u) << j;
             }
         }
+#ifdef DVCC_ASYNC_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st_tf = wall_clock64();
+        st_facts += st_tf - st_ti;
+#endif
         if (look) {  // (taken from LDS after keep_bits' barrier)
             uint32_t acc = 0;
             for (int64_t j0 = (int64_t)g - 1;; j0 -= 64) {
@@ -1011,6 +1033,13 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             }
             if (lane == 0) s_cin = acc;
         }
+#ifdef DVCC_ASYNC_STAMPS
+        {
+            const uint64_t tc = wall_clock64();
+            st_carry += tc - st_tf;
+            st_tf = tc;
+        }
+#endif
         // a queue running into the next slice is assumed to be followed by a
         // needy element there (keep_bits holds a barrier: every thread is done
         // with slot p ^ 1 of the previous iteration)
@@ -1094,9 +1123,33 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             s_quit = now - last_move > idle;
         }
         __syncthreads();
+#ifdef DVCC_ASYNC_STAMPS
+        {
+            const uint64_t tw = wall_clock64();
+            st_work += tw - st_tf;
+            st_moved += s_moved[p] ? 1u : 0u;
+            st_tf = tw;
+        }
+#endif
         if (s_quit) break;
         if (DVCC_ASYNC_SLEEP && !s_moved[p]) __builtin_amdgcn_s_sleep(DVCC_ASYNC_SLEEP);
+#ifdef DVCC_ASYNC_STAMPS
+        st_sleep += wall_clock64() - st_tf;
+#endif
     }
+#ifdef DVCC_ASYNC_STAMPS
+    if (tid == 0) {
+        unsigned long long *w = g_async_stamps + (size_t)g * 8;
+        atomicAdd(w + 0, 1ull);
+        atomicAdd(w + 1, (unsigned long long)it + (it < max_iters ? 1u : 0u));
+        atomicAdd(w + 2, (unsigned long long)(wall_clock64() - st_begin));
+        atomicAdd(w + 3, (unsigned long long)st_facts);
+        atomicAdd(w + 4, (unsigned long long)st_carry);
+        atomicAdd(w + 5, (unsigned long long)st_work);
+        atomicAdd(w + 6, (unsigned long long)st_sleep);
+        atomicAdd(w + 7, (unsigned long long)st_moved);
+    }
+#endif
     if (tid == 0) {
         // the finalize (or, with the statuses left in the words, dv_epoch_finish)
         // hands the rest to the synchronous rounds; one yield counted per launch
@@ -1361,6 +1414,18 @@ uint32_t async_groups(int device) {
 }
 
 uint32_t async_try_limit(uint32_t G) { return G * kAsyncCap; }
+
+#ifdef DVCC_ASYNC_STAMPS
+// measurement builds: the stamps (kAsyncGroups x 8 words) copied out and reset
+extern "C" int dv_debug_async_stamps(uint64_t *out, uint32_t n) {
+    if (!out || n > kAsyncGroups * 8) return DV_ERR_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return DV_ERR_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_async_stamps), n * 8) != hipSuccess) return DV_ERR_HIP;
+    static const unsigned long long zero[kAsyncGroups * 8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_async_stamps), zero, sizeof(zero)) != hipSuccess) return DV_ERR_HIP;
+    return DV_OK;
+}
+#endif
 
 void round_settle(hipStream_t s, const RoundBufs &b, uint32_t round, uint32_t n_txn, uint32_t ub, uint32_t *tword,
                   uint32_t *carry, uint32_t G) {
