@@ -93,44 +93,61 @@ struct RAgg {
 __device__ __forceinline__ RAgg rcomb(RAgg near, RAgg far) {
     return RAgg{near.f | far.f, near.f ? near.v : (near.v | far.v)};
 }
-__device__ __forceinline__ RAgg wave_incl_rev(RAgg p, uint32_t lane) {
+
+// ---- wave scans from ballots (no LDS traffic).  The scan fields are a few
+//      bits wide (a head flag, the 5-bit status OR, a per-thread count below
+//      2^CB), so each bit of a field is one ballot and a lane's prefix over a
+//      run of lanes is masks and popcounts of the ballots -- VALU and SALU
+//      work only, where the shuffle ladders (ds_bpermute) were ~20 dependent
+//      LDS round trips per iteration of the asynchronous rounds.
+__device__ __forceinline__ uint64_t lanes_before(uint32_t lane) { return (1ull << lane) - 1ull; }
+__device__ __forceinline__ uint64_t lanes_after(uint32_t lane) { return lane >= 63u ? 0ull : (~0ull << (lane + 1u)); }
+constexpr int bits_for(int n) { return n < 2 ? 1 : 1 + bits_for(n >> 1); }  // bits of a count 0..n
+
+template <int CB>  // Agg values: f 0/1, v below 32, c below 2^CB
+struct WaveScan {
+    uint64_t H, V[5], C[CB];
+    __device__ __forceinline__ explicit WaveScan(Agg p) {
+        H = __ballot(p.f != 0u);
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        RAgg o;
-        o.f = __shfl_down(p.f, off, 64);
-        o.v = __shfl_down(p.v, off, 64);
-        if (lane + off < 64) p = rcomb(p, o);
+        for (int b = 0; b < 5; b++) V[b] = __ballot((p.v >> b) & 1u);
+#pragma unroll
+        for (int b = 0; b < CB; b++) C[b] = __ballot((p.c >> b) & 1u);
     }
-    return p;
+    // OpPlain over the lanes of m, a run of lanes starting at lane 0
+    __device__ __forceinline__ Agg over(uint64_t m) const {
+        const uint64_t hm = H & m;
+        const uint64_t from = hm ? ~((1ull << (63 - __clzll((long long)hm))) - 1ull) : ~0ull;  // the last head on
+        const uint64_t R = m & from;
+        uint32_t v = 0, c = 0;
+#pragma unroll
+        for (int b = 0; b < 5; b++) v |= (V[b] & R) ? (1u << b) : 0u;
+#pragma unroll
+        for (int b = 0; b < CB; b++) c += (uint32_t)__popcll(C[b] & m) << b;
+        return Agg{hm != 0 ? 1u : 0u, v, c};
+    }
+};
+
+// the OR of a 5-bit field over the wave
+__device__ __forceinline__ uint32_t wave_or5(uint32_t x) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 5; b++) v |= __ballot((x >> b) & 1u) ? (1u << b) : 0u;
+    return v;
 }
 
-// Which elements survive into the next round: an element of an undecided
-// txn that still waits (needy), and a potential blocker (committed or
-// undecided txn) followed in its queue by a needy element.  Each thread holds
-// IPT consecutive elements; nhm bit j = the element after j starts a queue.
-// `far` describes what follows the last thread's chunk.  Returns keep bits.
-template <int IPT, int WAVES, class M = uint32_t>
-__device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw, RAgg far, uint32_t lane,
-                                       uint32_t wave) {
-    constexpr int kBits = 8 * (int)sizeof(M);
-    const M valid = cnt >= kBits ? ~(M)0 : (((M)1 << cnt) - 1);
-    RAgg x{0u, 0u};  // a thread past the end is transparent: `far` reaches the last element
-    if (cnt > 0) {
-        const M cuts = nhm & valid;
-        x.f = cuts != 0;
-        const int c0 = sizeof(M) == 8 ? __builtin_ctzll((uint64_t)cuts) : __builtin_ctz((uint32_t)cuts);
-        const M upto = cuts ? (c0 + 1 >= kBits ? ~(M)0 : (((M)2 << c0) - 1)) : valid;
-        x.v = (needy & upto) != 0;
-    }
-    const RAgg inc_r = wave_incl_rev(x, lane);
-    if (lane == 0) rw[wave] = inc_r;
-    RAgg ex_r;
-    ex_r.f = __shfl_down(inc_r.f, 1, 64);
-    ex_r.v = __shfl_down(inc_r.v, 1, 64);
-    if (lane == 63) ex_r = RAgg{0u, 0u};
-    __syncthreads();
-    for (int w = WAVES - 1; w > (int)wave; w--) far = rcomb(rw[w], far);
-    uint32_t r = rcomb(ex_r, far).v;  // needy after my last element, same queue
+// reverse OR (rcomb) over the lanes of m, a run of lanes ending at lane 63,
+// from the ballots of f and v
+__device__ __forceinline__ RAgg rover(uint64_t F, uint64_t Vb, uint64_t m) {
+    const uint64_t fm = F & m;
+    const uint64_t upto = fm ? ((2ull << __builtin_ctzll(fm)) - 1ull) : ~0ull;  // through the first cut
+    return RAgg{fm != 0 ? 1u : 0u, (Vb & m & upto) != 0 ? 1u : 0u};
+}
+
+// the keep bits of a thread's IPT elements from r, "a needy element follows
+// my last one in its queue"
+template <int IPT, class M>
+__device__ __forceinline__ M keep_from(int cnt, M nhm, M needy, M blk, uint32_t r) {
     M keep = 0;
 #pragma unroll
     for (int j = IPT - 1; j >= 0; j--) {
@@ -142,6 +159,49 @@ __device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw,
         }
     }
     return keep;
+}
+
+// a thread's reverse aggregate: f = a queue ends inside its elements, v = an
+// element of its first queue piece is needy (a thread past the end is
+// transparent, so what follows reaches the last element)
+template <class M>
+__device__ __forceinline__ RAgg thread_rev(int cnt, M nhm, M needy) {
+    constexpr int kBits = 8 * (int)sizeof(M);
+    const M valid = cnt >= kBits ? ~(M)0 : (((M)1 << cnt) - 1);
+    RAgg x{0u, 0u};
+    if (cnt > 0) {
+        const M cuts = nhm & valid;
+        x.f = cuts != 0;
+        const int c0 = sizeof(M) == 8 ? __builtin_ctzll((uint64_t)cuts) : __builtin_ctz((uint32_t)cuts);
+        const M upto = cuts ? (c0 + 1 >= kBits ? ~(M)0 : (((M)2 << c0) - 1)) : valid;
+        x.v = (needy & upto) != 0;
+    }
+    return x;
+}
+
+// Which elements survive into the next round: an element of an undecided
+// txn that still waits (needy), and a potential blocker (committed or
+// undecided txn) followed in its queue by a needy element.  Each thread holds
+// IPT consecutive elements; nhm bit j = the element after j starts a queue.
+// `far` describes what follows the last thread's chunk.  Returns keep bits.
+template <int IPT, int WAVES, class M = uint32_t>
+__device__ __forceinline__ M keep_bits(int cnt, M nhm, M needy, M blk, RAgg *rw, RAgg far, uint32_t lane,
+                                       uint32_t wave) {
+    const RAgg x = thread_rev<M>(cnt, nhm, needy);
+    const uint64_t F = __ballot(x.f != 0u), Vb = __ballot(x.v != 0u);
+    if (lane == 0) rw[wave] = rover(F, Vb, ~0ull);   // the wave's aggregate
+    const RAgg ex_r = rover(F, Vb, lanes_after(lane));  // the lanes after mine
+    __syncthreads();
+    for (int w = WAVES - 1; w > (int)wave; w--) far = rcomb(rw[w], far);
+    return keep_from<IPT, M>(cnt, nhm, needy, blk, rcomb(ex_r, far).v);
+}
+
+// ... the same for a chunk one wave holds alone (no workgroup barrier)
+template <int IPT, class M = uint32_t>
+__device__ __forceinline__ M keep_bits_wave(int cnt, M nhm, M needy, M blk, RAgg far, uint32_t lane) {
+    const RAgg x = thread_rev<M>(cnt, nhm, needy);
+    const uint64_t F = __ballot(x.f != 0u), Vb = __ballot(x.v != 0u);
+    return keep_from<IPT, M>(cnt, nhm, needy, blk, rcomb(rover(F, Vb, lanes_after(lane)), far).v);
 }
 
 }  // namespace
@@ -348,8 +408,8 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
         const Agg x{(uint32_t)((e[j] & F_HEAD) != 0), v[j], (keep >> j) & 1u};
         if (j < cnt) a = OpPlain::comb(a, x);
     }
-    const Agg inc = wave_incl<OpPlain>(a, lane);
-    if (lane == 63) sh.wt[wave] = inc;
+    const WaveScan<bits_for(IPT)> ws(a);
+    if (lane == 63) sh.wt[wave] = ws.over(~0ull);
     __syncthreads();
     // The decisions need only the OR in front of the tile (a walk back to the
     // nearest tile holding a head); the output offset needs the full count
@@ -373,7 +433,7 @@ __device__ __forceinline__ void round_tile(TileLds<EIn> &sh, uint32_t tile, uint
     }
     Agg wpre{0u, 0u, 0u};  // this wave's prefix within the tile
     for (uint32_t w = 0; w < wave; w++) wpre = OpPlain::comb(wpre, sh.wt[w]);
-    const Agg lex = wave_excl_from_incl<OpPlain>(inc, lane);
+    const Agg lex = ws.over(lanes_before(lane));
     uint32_t lpos = wpre.c + lex.c;                                   // block-local slot
     uint32_t run = OpPlain::comb(OpPlain::comb(sh.pre, wpre), lex).v;  // OR since queue head
     E *s_out = reinterpret_cast<E *>(sh.el);  // every lane holds its elements: reuse the tile
@@ -967,7 +1027,10 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             if (i < n) sel[i] = v[j] & ~(i == 0 && cont_in ? F_HEAD : 0u);
         }
     }
-    if (tid == 0) s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
+    if (tid == 0) {
+        s_needy[0] = s_needy[1] = s_moved[0] = s_moved[1] = 0;
+        s_quit = 0;
+    }
     __syncthreads();
     uint32_t it = 0;
     bool yielded = true;                  // cleared when the slice has nothing left to learn
@@ -1022,10 +1085,7 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             for (int64_t j0 = (int64_t)g - 1;; j0 -= 64) {
                 const uint64_t hm = __ballot((cw & kCarryHead) != 0);
                 const uint32_t stop = hm ? (uint32_t)__builtin_ctzll(hm) : 64u;
-                uint32_t v = lane <= stop ? (cw & ~kCarryHead) : 0u;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) v |= __shfl_xor(v, off, 64);
-                acc |= v;
+                acc |= wave_or5(lane <= stop ? (cw & ~kCarryHead) : 0u);
                 if (hm) break;
                 const int64_t j = j0 - 64 - (int64_t)lane;
                 cw = j >= 0 ? __hip_atomic_load(carry + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
@@ -1041,16 +1101,17 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
         }
 #endif
         // a queue running into the next slice is assumed to be followed by a
-        // needy element there (keep_bits holds a barrier: every thread is done
-        // with slot p ^ 1 of the previous iteration)
-        M keep = keep_bits<IPT, kAsyncWaves, M>(cnt, nhm, needy, blk, rw, RAgg{1u, cont_out ? 1u : 0u},
-                                                lane, wave);
+        // needy element there; each wave decides its keep bits alone (no
+        // barrier), assuming the same past its own last element unless it
+        // holds the slice's end -- a few blockers kept one iteration longer
+        const bool wave_end = (64u * wave + 64u) * k >= n;
+        M keep = keep_bits_wave<IPT, M>(cnt, nhm, needy, blk,
+                                        RAgg{1u, wave_end ? (cont_out ? 1u : 0u) : 1u}, lane);
         // ... and the slice's last element anchors that queue here: it is kept
         // whatever its txn, so the carry is always the OR of that queue (were
         // the queue's elements all dropped, the last head would be an
         // earlier queue's)
         if (cont_out && cnt > 0 && first + (uint32_t)cnt == n) keep |= (M)1 << (cnt - 1);
-        if (tid == 0) { s_needy[p ^ 1u] = 0; s_moved[p ^ 1u] = 0; }
         if (needy) atomicAdd(&s_needy[p], (uint32_t)__popcll(needy));
         Agg a{0u, 0u, 0u};
 #pragma unroll
@@ -1062,9 +1123,13 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
                 a = OpPlain::comb(a, Agg{(uint32_t)((e[j] & F_HEAD) != 0), vj, kj});
             }
         }
-        const Agg inc = wave_incl<OpPlain>(a, lane);
-        if (lane == 63) wt[wave] = inc;
+        const WaveScan<bits_for(IPT)> ws(a);
+        if (lane == 63) wt[wave] = ws.over(~0ull);
         __syncthreads();
+        // (every thread is past its reads of slot p ^ 1, the previous
+        // iteration's; and thread 0's quit flag of that iteration is read here)
+        if (s_quit) break;
+        if (tid == 0) { s_needy[p ^ 1u] = 0; s_moved[p ^ 1u] = 0; }
         const uint32_t cin = cont_in ? s_cin : 0u;
         // wpre: the carry is in front of the slice; own: the slice alone
         Agg wpre{0u, cin, 0u}, own{0u, 0u, 0u};
@@ -1072,7 +1137,7 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             if (w < (int)wave) wpre = OpPlain::comb(wpre, wt[w]);
             own = OpPlain::comb(own, wt[w]);
         }
-        const Agg pre = OpPlain::comb(wpre, wave_excl_from_incl<OpPlain>(inc, lane));
+        const Agg pre = OpPlain::comb(wpre, ws.over(lanes_before(lane)));
         uint32_t lpos = pre.c, run = pre.v, moved = 0;
 #pragma unroll
         for (int j = 0; j < IPT; j++) {
@@ -1116,13 +1181,13 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
         // nothing decided here: the facts this slice waits for come from other
         // workgroups -- back off before reading them again, and yield once
         // they have not come for `idle` ticks (their producer may not be
-        // resident).  Thread 0's clock decides for the workgroup.
+        // resident).  Thread 0's clock decides for the workgroup; every
+        // thread reads its flag after the next iteration's barrier.
         if (tid == 0) {
             const uint64_t now = wall_clock64();
             if (s_moved[p]) last_move = now;
             s_quit = now - last_move > idle;
         }
-        __syncthreads();
 #ifdef DVCC_ASYNC_STAMPS
         {
             const uint64_t tw = wall_clock64();
@@ -1131,7 +1196,6 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
             st_tf = tw;
         }
 #endif
-        if (s_quit) break;
         if (DVCC_ASYNC_SLEEP && !s_moved[p]) __builtin_amdgcn_s_sleep(DVCC_ASYNC_SLEEP);
 #ifdef DVCC_ASYNC_STAMPS
         st_sleep += wall_clock64() - st_tf;
