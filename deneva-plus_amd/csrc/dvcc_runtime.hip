@@ -1821,6 +1821,32 @@ bool prefix_applies(const dv_ctx *c, const dv_epoch_dev *ep) {
     return prefix_size(c, ep->n_txn) < ep->n_txn;
 }
 
+// A small YCSB epoch that queues without a host wait too: CALVIN (the grant
+// scan and the execution are all launches), or NO_WAIT / WAIT_DIE / OCC whose
+// rounds are round 0 plus one asynchronous launch (decide_epoch, at most
+// kAsyncSmallAcc accesses and 32-bit round elements) -- so the pipelined batch
+// and the decision lanes take it like a prefix-kill epoch (config B: 65,536
+// CALVIN txns per epoch ran one synchronous epoch at a time before).
+bool small_pipelined(const dv_ctx *c, const dv_epoch_dev *ep) {
+    if (c->cfg.workload != DV_YCSB || ep->n_acc_dev || prefix_applies(c, ep)) return false;
+    if (c->cfg.cc_alg == DV_CALVIN) return true;
+    if (ep->n_acc > kAsyncSmallAcc || !c->async_g || (c->cfg.flags & DV_FLAG_NO_ASYNC) || !ep->n_txn) return false;
+    uint32_t slog = 4;  // (epoch_setup's verdict-byte stride)
+    const uint32_t hint = ep->max_txn_acc ? ep->max_txn_acc : kMaxPos;
+    while ((1u << slog) < hint) slog++;
+    return round_el32(ep->n_txn, slog) && !(c->cfg.flags & DV_FLAG_EL64);
+}
+
+// ... queued: begin (probe, sort; CALVIN's grant scan), then the rounds
+int small_enqueue(dv_ctx *c, const dv_epoch_dev *ep) {
+    int r = dv_epoch_begin(c, ep, nullptr);
+    if (!r && c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
+        r = decide_epoch(c);
+        if (r) c->phase = 0;
+    }
+    return r;
+}
+
 // tb mode: a prefix-kill epoch whose own txn boundaries are every kernel's
 // ranges (k_probe_tb probes the prefix alone, the kill pass the rest).  Not
 // for a replicated epoch whose owners' key checks must be combined before
@@ -2248,8 +2274,11 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
     auto commit_of = [&](uint32_t k) { return d_commits ? d_commits[k] : nullptr; };
     return run_batch(
         c, n, sts, commit_of,
-        [&](uint32_t k) { return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P; },
-        [&](uint32_t k) { return run_prefix_epoch(c, &eps[k]); },
+        [&](uint32_t k) {
+            return (prefix_applies(c, &eps[k]) || small_pipelined(c, &eps[k])) && !timing(c) && !ktiming(c) &&
+                   !c->rep_P;
+        },
+        [&](uint32_t k) { return prefix_applies(c, &eps[k]) ? run_prefix_epoch(c, &eps[k]) : small_enqueue(c, &eps[k]); },
         [&](uint32_t k, dv_stats *st) { return dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, st); });
 }
 
@@ -2571,9 +2600,13 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
         lanes, n_lanes, n, sts, commit_of,
         [&](uint32_t k) {
             dv_ctx *c = lanes[k % n_lanes];
-            return prefix_applies(c, &eps[k]) && !timing(c) && !ktiming(c) && !c->rep_P && !c->comm;
+            return (prefix_applies(c, &eps[k]) || small_pipelined(c, &eps[k])) && !timing(c) && !ktiming(c) &&
+                   !c->rep_P && !c->comm;
         },
-        [&](dv_ctx *c, uint32_t k) { return run_prefix_epoch(c, &eps[k]); }, [](dv_ctx *, uint32_t) { return 0; },
+        [&](dv_ctx *c, uint32_t k) {
+            return prefix_applies(c, &eps[k]) ? run_prefix_epoch(c, &eps[k]) : small_enqueue(c, &eps[k]);
+        },
+        [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
             return dv_epoch_run_device(lanes[k % n_lanes], &eps[k], commit_of(k), nullptr, st);
         });

@@ -902,6 +902,43 @@ def test_lanes_mixed_and_halted_epochs():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc,lanes", [(dvcc.CALVIN, 1), (dvcc.CALVIN, 4), (dvcc.NO_WAIT, 1), (dvcc.NO_WAIT, 4),
+                                      (dvcc.WAIT_DIE, 3), (dvcc.OCC, 1), (dvcc.OCC, 4)])
+def test_small_epochs_pipelined(cc, lanes):
+    """Epochs below the prefix-kill size queue without a host wait too (CALVIN,
+    and round 0 + one asynchronous launch for the others): through the batch
+    and the decision lanes, ragged sizes and a one-txn epoch included, every
+    epoch equals the sequential oracle's."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.8, txn_write_perc=1.0, tup_write_perc=0.5)
+    sizes = [5000, 5000, 1, 3000, 5000, 5000, 4000, 5000, 5000]
+    _check_batch(cc, rows, [g.gen(n, 1200 + k) for k, n in enumerate(sizes)], lanes=lanes)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_small_epochs_pipelined_halted(lanes):
+    """... with the asynchronous rounds forced to yield: a halted small epoch
+    and every epoch queued behind it run again in order, results unchanged."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    epochs = [g.gen(5000, 1300 + k) for k in range(8)]
+    sts = _check_batch(dvcc.NO_WAIT, rows, epochs, max_iters=1, lanes=lanes)
+    assert sum(st.async_yields for st in sts) > 0, "no asynchronous launch yielded"
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_config_b_lanes_timed_path():
+    """The bench's config-B leg as timed: 65,536-txn CALVIN epochs (zipf 0.6,
+    16,777,216 rows), three distinct epochs cycled over four decision lanes."""
+    rows = 16_777_216
+    g = YCSBQueryGenerator(rows, zipf_theta=0.6, txn_write_perc=1.0, tup_write_perc=0.5)
+    base = [g.gen(65_536, dvcc.epoch_seed(0, e)) for e in range(3)]
+    _check_batch(dvcc.CALVIN, rows, [base[k % 3] for k in range(8)], lanes=4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bad", [1, 2, 3])
 def test_lanes_error_stops_before_execution(bad):
     """A missing key in epoch `bad` (either lane): the call returns the error,
