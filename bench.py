@@ -33,6 +33,9 @@ from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "deneva-plus_amd"))
+# HIP graphs in packet-capture mode (the epoch graphs' replay: ~4 us of host
+# time instead of 15-50), before anything initialises the HIP runtime
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -17,6 +17,9 @@ namespace dvcc {
 // stream); the entry reads them once its work has completed.
 struct KProf;
 extern thread_local KProf *tl_kprof;
+// epoch graphs (dvcc_runtime.hip): while a captured epoch is replayed, the
+// host walks the same enqueue code for its state with every launch skipped
+extern thread_local bool tl_dry;
 // a fresh event pair for one launch of `kernel` (both null when the pool is spent)
 void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1);
 // events the caller owns and records itself (the probe / scatter / pass
@@ -37,6 +40,7 @@ class KProfScope {
 };
 #define DV_LAUNCH(kernel, grid, block, shm, stream, ...)                                                     \
     do {                                                                                                     \
+        if (::dvcc::tl_dry) break;                                                                           \
         hipEvent_t dv_e0_ = nullptr, dv_e1_ = nullptr;                                                       \
         if (::dvcc::tl_kprof) ::dvcc::kprof_events(#kernel, &dv_e0_, &dv_e1_);                              \
         hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), shm, stream, dv_e0_, dv_e1_, 0, __VA_ARGS__); \
@@ -44,6 +48,7 @@ class KProfScope {
 // the same with the caller's own events (may be null)
 #define DV_LAUNCH_EV(kernel, grid, block, shm, stream, ev0, ev1, ...)                                        \
     do {                                                                                                     \
+        if (::dvcc::tl_dry) break;                                                                           \
         hipEvent_t dv_e0_ = (ev0), dv_e1_ = (ev1);                                                           \
         if (::dvcc::tl_kprof) {                                                                              \
             if (dv_e0_ && dv_e1_) ::dvcc::kprof_add(#kernel, dv_e0_, dv_e1_);                                \
@@ -610,7 +615,8 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero = nullptr,
                         uint64_t zero_words = 0, bool gate = false, Counters *hctr = nullptr,
                         unsigned long long *hseq = nullptr, unsigned long long seq = 0,
-                        uint64_t *txn_zero8 = nullptr);  // (one 8-byte word per txn zeroed: TPC-C o_ids)
+                        uint64_t *txn_zero8 = nullptr,  // (one 8-byte word per txn zeroed: TPC-C o_ids)
+                        uint64_t *desc = nullptr, uint32_t n_desc = 0);  // (descriptors zeroed: epoch graphs)
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,

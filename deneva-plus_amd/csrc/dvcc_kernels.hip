@@ -1175,7 +1175,8 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
                                                         const uint32_t *__restrict__ err_seed, Counters *ctr,
                                                         uint4 *__restrict__ zero, uint64_t zero_n, int gate,
                                                         Counters *hctr, unsigned long long *hseq,
-                                                        unsigned long long seq, uint64_t *__restrict__ zero8) {
+                                                        unsigned long long seq, uint64_t *__restrict__ zero8,
+                                                        uint64_t *__restrict__ desc, uint32_t n_desc) {
     if (blockIdx.x == 0) {
         // pipelined epochs: the previous epoch's counters into their host
         // mirror first (what k_ctr_out would have done as one more launch)
@@ -1196,6 +1197,9 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
         uint32_t *w = reinterpret_cast<uint32_t *>(ctr);
         for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) w[i] = 0;
         for (uint32_t i = threadIdx.x; i < kTileCtrs; i += kBlock) tile_ctr[i] = 0;
+        // an epoch replayed from a graph reuses its look-back tags: no
+        // descriptor of an earlier epoch may carry one of them
+        for (uint32_t i = threadIdx.x; i < n_desc; i += kBlock) desc[i] = 0;
         __syncthreads();
         // errors found before the epoch began (the host-record check)
         if (threadIdx.x == 0 && err_seed) ctr->err = *err_seed;
@@ -1250,13 +1254,14 @@ void launch_lane_gate(hipStream_t s, const uint32_t *prev_gate, Counters *ctr) {
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
                         uint32_t *tb_start, uint32_t *tb_end, uint8_t *tlen, uint32_t *tile_ctr,
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
-                        Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint64_t *txn_zero8) {
+                        Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint64_t *txn_zero8,
+                        uint64_t *desc, uint32_t n_desc) {
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,
-                                       gate ? 1 : 0, hctr, hseq, seq, txn_zero8);
+                                       gate ? 1 : 0, hctr, hseq, seq, txn_zero8, desc, n_desc);
 }
 
 // ---------------------------------------------------------------- execute

@@ -169,6 +169,23 @@ struct dv_ctx {
     bool mir_pending = false;
     int mir_slot = 0;
     unsigned long long mir_seq = 0;
+    // epoch graphs (graph_decide): a pipelined epoch's decision launches --
+    // everything after its clear -- captured once per (epoch buffers, sizes,
+    // knobs) and replayed; ws_gen counts the workspace reallocations that
+    // would invalidate a captured graph's pointers
+    struct EpochGraph {
+        uint64_t key[18] = {};
+        hipGraphExec_t exec = nullptr;
+        uint32_t seen = 0;
+        uint64_t used = 0;
+    };
+    std::vector<EpochGraph> graphs;
+    uint64_t graph_clock = 0, ws_gen = 0;
+    // dv_tpcc_epoch_begin: the last-name resolution, launched right after the clear
+    bool rsv_pending = false;
+    const uint64_t *rsv_keys = nullptr;
+    const uint8_t *rsv_tables = nullptr;
+    uint64_t rsv_n = 0;
     uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
     const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
@@ -262,6 +279,7 @@ struct dv_ctx {
 // ---- per-launch kernel timing (dvcc_internal.h, DV_LAUNCH)
 namespace dvcc {
 thread_local KProf *tl_kprof = nullptr;
+thread_local bool tl_dry = false;
 
 void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1) {
     KProf *p = tl_kprof;
@@ -639,6 +657,9 @@ int dv_device_count(int *count) {
 void dv_close(dv_ctx *c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto &g : c->graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    c->graphs.clear();
     comm_free(c->comm);
     c->comm = nullptr;
     if (c->table_owner) {  // a lane: the tables are its owner's
@@ -1228,6 +1249,136 @@ int dv_tpcc_load(dv_ctx *c, const dv_tpcc_params *p, uint64_t seed) {
 namespace {
 bool tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep);
 
+// ---- epoch graphs.  A pipelined epoch's host work is ~15-25 launches (the
+// TPC-C window and config B were bound by it: ~3 us of host time per
+// launch).  Its decision -- every launch after the epoch's clear -- depends
+// on the epoch's buffers, sizes and the context's knobs only, so the second
+// time the same (buffers, sizes, knobs) come, the launches are captured into
+// a graph (hipStreamBeginCapture right after the clear), and from then on
+// replayed with one hipGraphLaunch: the host walks the same enqueue code for
+// its state with every launch skipped (tl_dry).  What a replay reuses and
+// the kernels must not see stale: the look-back tags baked into the graph --
+// the clear of a graph epoch zeroes the descriptors -- and the tile tickets,
+// which every clear zeroes.  The clear itself stays a plain launch (its
+// gate, mirror slot and sequence differ per epoch).  A capture that fails
+// (a call the capture cannot take) runs the decision again uncaptured and
+// the key is never captured again; DVCC_NO_GRAPHS=1 turns the graphs off.
+extern "C++" {  // (templates, inside the C API's block)
+// (prefix-kill epochs take no graphs: their ~25 launches overlap the device
+// work under decision lanes -- config D is device-bound -- and a bench cycles
+// too few of them per lane for a capture to pay)
+constexpr size_t kMaxGraphs = 24;  // per context
+constexpr uint32_t kGraphNever = 0xFFFFFFFFu;
+constexpr uint32_t kGraphAfter = 3;  // encounters of a key before its capture
+struct GraphRun {
+    dv_ctx *c = nullptr;
+    dv_ctx::EpochGraph *g = nullptr;
+    bool capture = false, began = false;
+};
+thread_local GraphRun *tl_graph = nullptr;
+// DVCC_HOST_PROF: host seconds in graph_decide's replays -- the walk of the
+// enqueue code (its clear launch included) and hipGraphLaunch -- and captures
+thread_local double tl_hp_walk = 0, tl_hp_glaunch = 0;
+thread_local uint32_t tl_hp_replays = 0, tl_hp_captures = 0;
+
+bool graph_active(const dv_ctx *c) {
+    const GraphRun *g = tl_graph;
+    return g && g->c == c && (g->g->exec || g->capture);
+}
+uint64_t *graph_desc(dv_ctx *c) { return graph_active(c) ? c->desc : nullptr; }
+uint32_t graph_ndesc(dv_ctx *c) {
+    return graph_active(c) ? (uint32_t)((c->cfg.max_acc + kRTile - 1) / kRTile) : 0u;
+}
+
+// right after an epoch's clear: start the capture, or skip the launches of a replay
+void graph_after_clear(dv_ctx *c) {
+    GraphRun *g = tl_graph;
+    if (!g || g->c != c || g->began) return;
+    g->began = true;
+    if (g->g->exec) {
+        tl_dry = true;
+    } else if (g->capture && hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        g->capture = false;
+        g->g->seen = kGraphNever;
+    }
+}
+
+// decide(): an epoch's queueing from its epoch_setup through its decision
+// (the clear first); ep / args name its buffers.
+template <class F>
+int graph_decide(dv_ctx *c, const dv_epoch_dev *ep, const void *args, F &&decide) {
+    static const bool off = std::getenv("DVCC_NO_GRAPHS") != nullptr;
+    if (off || timing(c) || ktiming(c) || (c->cfg.flags & DV_FLAG_KERNEL_PROFILE) || tl_kprof || c->comm ||
+        c->rep_P || c->route || tl_graph)
+        return decide();
+    const uint64_t key[18] = {(uint64_t)ep->keys, (uint64_t)ep->types, (uint64_t)ep->acc_txn, (uint64_t)ep->tables,
+                              (uint64_t)ep->txn_begin, (uint64_t)ep->recs32, (uint64_t)ep->ts,
+                              (uint64_t)ep->n_acc_dev, ep->n_acc, ep->n_txn | (uint64_t)ep->max_txn_acc << 32,
+                              (uint64_t)args, c->async_g | (uint64_t)c->async_max_iters << 32, c->async_idle_ticks,
+                              c->cfg.flags | (uint64_t)c->prefix_txns << 32, c->ws_gen, (uint64_t)c->keys32,
+                              (uint64_t)c->stream, (uint64_t)c->cfg.max_acc};
+    dv_ctx::EpochGraph *e = nullptr;
+    for (auto &g : c->graphs)
+        if (std::equal(key, key + 18, g.key)) e = &g;
+    if (!e) {
+        if (c->graphs.size() >= kMaxGraphs) {  // (the least recently used goes)
+            auto lru = std::min_element(c->graphs.begin(), c->graphs.end(),
+                                        [](const dv_ctx::EpochGraph &a, const dv_ctx::EpochGraph &b) {
+                                            return a.used < b.used;
+                                        });
+            if (lru->exec) (void)hipGraphExecDestroy(lru->exec);
+            *lru = dv_ctx::EpochGraph{};
+            e = &*lru;
+        } else {
+            c->graphs.emplace_back();
+            e = &c->graphs.back();
+        }
+        std::copy(key, key + 18, e->key);
+    }
+    e->used = ++c->graph_clock;
+    if (e->seen != kGraphNever) e->seen++;
+    GraphRun g;
+    g.c = c;
+    g.g = e;
+    // (the first two times run as they are: a short batch pays no capture
+    // it will not replay, and the buffers have grown to their sizes)
+    g.capture = !e->exec && e->seen >= kGraphAfter && e->seen != kGraphNever;
+    tl_graph = &g;
+    const auto t0 = std::chrono::steady_clock::now();
+    int r = decide();
+    tl_graph = nullptr;
+    if (tl_dry) {  // a replay: the host state is the epoch's, the launches are the graph's
+        tl_dry = false;
+        const auto t1 = std::chrono::steady_clock::now();
+        if (!r) r = hip_fail(hipGraphLaunch(e->exec, c->stream), "hipGraphLaunch");
+        tl_hp_walk += std::chrono::duration<double>(t1 - t0).count();
+        tl_hp_glaunch += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+        tl_hp_replays++;
+        return r;
+    }
+    if (!g.capture || !g.began) return r;
+    hipGraph_t graph = nullptr;
+    const hipError_t ee = hipStreamEndCapture(c->stream, &graph);
+    hipGraphExec_t ex = nullptr;
+    hipError_t ei = hipErrorUnknown;
+    if (!r && ee == hipSuccess && graph) ei = hipGraphInstantiate(&ex, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (!r && ee == hipSuccess && ei == hipSuccess) {
+        e->exec = ex;
+        tl_hp_captures++;
+        return hip_fail(hipGraphLaunch(ex, c->stream), "hipGraphLaunch");
+    }
+    // nothing the capture recorded ran: the decision again, uncaptured (its
+    // clear repeats harmlessly -- the previous epoch's read-back was written
+    // by the first one, and the gate it set stands)
+    (void)hipGetLastError();
+    if (ex) (void)hipGraphExecDestroy(ex);
+    e->seen = kGraphNever;
+    return decide();
+}
+}  // extern "C++"
+
 // the common start of an epoch: argument checks, the verdict-byte stride,
 // the per-epoch host state
 int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
@@ -1253,6 +1404,7 @@ int epoch_setup(dv_ctx *c, const dv_epoch_dev *ep) {
         const uint64_t need = (uint64_t)((ep->n_txn + 3u) & ~3u) << slog;
         if (need > c->vb8_cap) {
             HIPCHK(hipStreamSynchronize(c->stream));
+            c->ws_gen++;
             dfree(c->vb8);
             c->vb8 = nullptr;
             c->vb8_cap = 0;
@@ -1303,8 +1455,14 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
                        c->tb_start, c->tb_end, calvin ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr, nullptr,
                        0, c->clear_gate, mir ? c->d_mir[c->mir_slot] : nullptr,
                        mir ? c->d_mseq[c->mir_slot] : nullptr, mir ? c->mir_seq : 0ull,
-                       c->cfg.workload == DV_TPCC ? c->tp_oid : nullptr);
+                       c->cfg.workload == DV_TPCC ? c->tp_oid : nullptr, graph_desc(c), graph_ndesc(c));
+    graph_after_clear(c);
     c->ticket = 0;
+    if (c->rsv_pending) {  // (dv_tpcc_epoch_begin's last-name resolution)
+        c->rsv_pending = false;
+        launch_tpcc_resolve(c->stream, make_tables(c), c->rsv_keys, c->rsv_tables, c->rsv_n, c->f0, c->tp_keys,
+                            c->tp_tables, c->ctr);
+    }
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles && !ep->n_acc_dev;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
@@ -1955,6 +2113,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
     const uint64_t rs_words = row_state_words(row_space(c));
     if (!c->row_state || c->row_state_cap < rs_words) {
         HIPCHK(hipStreamSynchronize(c->stream));
+        c->ws_gen++;
         dfree(c->row_state);
         c->row_state = nullptr;
         c->row_state_cap = 0;
@@ -1963,6 +2122,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
         c->row_state_cap = rs_words;
     }
     if (!c->b_status) {
+        c->ws_gen++;
         r = dalloc(&c->b_status, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_tlen, (T + 3u) & ~3u);
         if (!r) r = dalloc(&c->b_map, T);
@@ -1991,7 +2151,8 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
                        c->tb_mode ? nullptr : c->tb_end, c->tb_mode ? nullptr : c->tlen, c->tile_ctr, err_seed, c->ctr,
                        c->row_state, rs_words, c->clear_gate,
                        mir ? c->d_mir[c->mir_slot] : nullptr, mir ? c->d_mseq[c->mir_slot] : nullptr,
-                       mir ? c->mir_seq : 0ull);
+                       mir ? c->mir_seq : 0ull, nullptr, graph_desc(c), graph_ndesc(c));
+    graph_after_clear(c);
     c->ticket = 0;
     if (c->tb_mode)
         launch_probe_tb(c->stream, make_tables(c), ep->keys, ep->types, ep->recs32, ep->txn_begin, ep->n_acc,
@@ -2278,7 +2439,10 @@ int dv_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, uint32_t n, ui
             return (prefix_applies(c, &eps[k]) || small_pipelined(c, &eps[k])) && !timing(c) && !ktiming(c) &&
                    !c->rep_P;
         },
-        [&](uint32_t k) { return prefix_applies(c, &eps[k]) ? run_prefix_epoch(c, &eps[k]) : small_enqueue(c, &eps[k]); },
+        [&](uint32_t k) {
+            if (prefix_applies(c, &eps[k])) return run_prefix_epoch(c, &eps[k]);
+            return graph_decide(c, &eps[k], nullptr, [&] { return small_enqueue(c, &eps[k]); });
+        },
         [&](uint32_t k, dv_stats *st) { return dv_epoch_run_device(c, &eps[k], commit_of(k), nullptr, st); });
 }
 
@@ -2293,15 +2457,17 @@ int dv_tpcc_epoch_run_device_batch(dv_ctx *c, const dv_epoch_dev *eps, const uin
     return run_batch(
         c, n, sts, commit_of, [&](uint32_t) { return !timing(c) && !ktiming(c); },
         [&](uint32_t k) {
-            int r = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
-            if (!r && c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
-                r = decide_epoch(c);
-                if (r) {
-                    c->phase = 0;
-                    c->tp_args = c->tp_oid = nullptr;
+            return graph_decide(c, &eps[k], d_args[k], [&] {
+                int r = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
+                if (!r && c->cfg.cc_alg != DV_CALVIN && c->n_txn) {
+                    r = decide_epoch(c);
+                    if (r) {
+                        c->phase = 0;
+                        c->tp_args = c->tp_oid = nullptr;
+                    }
                 }
-            }
-            return r;
+                return r;
+            });
         },
         [&](uint32_t k, dv_stats *st) {
             return dv_tpcc_epoch_run_device(c, &eps[k], d_args[k], commit_of(k), oid_of(k), st);
@@ -2476,6 +2642,8 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     static const bool hprof = std::getenv("DVCC_HOST_PROF") != nullptr;
     using hclock = std::chrono::steady_clock;
     double t_queue = 0, t_wait = 0, t_decide = 0;
+    tl_hp_walk = tl_hp_glaunch = 0;
+    tl_hp_replays = tl_hp_captures = 0;
     const auto t_all = hclock::now();
     // read back the oldest queued epoch; a halted one and all behind it run again
     auto settle = [&]() -> int {
@@ -2581,6 +2749,10 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f (decision %.1f), "
                      "waiting %.1f\n", n, n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
                      t_queue * 1e6 / n, t_decide * 1e6 / n, t_wait * 1e6 / n);
+    if (hprof && tl_hp_replays)
+        std::fprintf(stderr, "dvcc host: %u graph replays (%u captures): walk %.1f us, hipGraphLaunch %.1f us each\n",
+                     tl_hp_replays, tl_hp_captures, tl_hp_walk * 1e6 / tl_hp_replays,
+                     tl_hp_glaunch * 1e6 / tl_hp_replays);
     return DV_OK;
 }
 
@@ -2604,7 +2776,8 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
                    !c->rep_P && !c->comm;
         },
         [&](dv_ctx *c, uint32_t k) {
-            return prefix_applies(c, &eps[k]) ? run_prefix_epoch(c, &eps[k]) : small_enqueue(c, &eps[k]);
+            if (prefix_applies(c, &eps[k])) return run_prefix_epoch(c, &eps[k]);
+            return graph_decide(c, &eps[k], nullptr, [&] { return small_enqueue(c, &eps[k]); });
         },
         [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
@@ -2665,9 +2838,11 @@ int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
             return !timing(c) && !ktiming(c) && !c->comm;
         },
         [&](dv_ctx *c, uint32_t k) {
-            int rr = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
-            if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
-            return rr;
+            return graph_decide(c, &eps[k], d_args[k], [&] {
+                int rr = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
+                if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
+                return rr;
+            });
         },
         [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
@@ -2924,6 +3099,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
     const uint64_t A = c->cfg.max_acc;
     int r = DV_OK;
     if (!c->tp_keys) {
+        c->ws_gen++;
         r = dalloc(&c->tp_keys, A);
         if (!r) r = dalloc(&c->tp_tables, A);
         if (r) return r;
@@ -2931,6 +3107,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
     const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
     const uint64_t drows = dt.created ? dt.cap_rows : 1;
     if (c->tp_dsnap_cap < drows) {
+        c->ws_gen++;
         dfree(c->tp_dsnap);
         c->tp_dsnap = nullptr;
         r = dalloc(&c->tp_dsnap, drows);
@@ -2938,9 +3115,13 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
         c->tp_dsnap_cap = drows;
     }
     // no host wait: a last name without customers resolves to key ~0, which
-    // the probe of dv_epoch_begin then reports as DV_ERR_KEY_NOT_FOUND
-    launch_tpcc_resolve(c->stream, make_tables(c), ep->keys, ep->tables, ep->n_acc, c->f0, c->tp_keys,
-                        c->tp_tables, c->ctr);
+    // the probe of dv_epoch_begin then reports as DV_ERR_KEY_NOT_FOUND; the
+    // resolution is launched by dv_epoch_begin right after the epoch's clear
+    // (everything after the clear is the part an epoch graph replays)
+    c->rsv_pending = true;
+    c->rsv_keys = ep->keys;
+    c->rsv_tables = ep->tables;
+    c->rsv_n = ep->n_acc;
     dv_epoch_dev e = *ep;
     e.keys = c->tp_keys;
     e.tables = c->tp_tables;
@@ -2948,6 +3129,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
     c->tp_args = d_args ? d_args : &kNoArgs;  // an empty partition still finishes
     c->tp_oid = d_oid;
     r = dv_epoch_begin(c, &e, nullptr);
+    c->rsv_pending = false;
     if (r) c->tp_args = c->tp_oid = nullptr;
     return r;
 }

@@ -1,6 +1,14 @@
 """dvcc -- MI355X batched concurrency-control engine for Deneva's
 transaction-scheduling hot path (probe -> lock/validate -> grant/abort ->
 execute), exposed through libdvcc.so (include/dvcc.h)."""
+import os
+
+# The HIP runtime's packet-capture mode for graphs: an epoch graph
+# (dvcc_runtime.hip graph_decide) then replays in ~4 us of host time instead
+# of 15-50 (measured, profiles/r05_k).  Read once when HIP initialises, so it
+# only takes effect if nothing has touched the GPU yet (bench.py sets it
+# before importing torch); a caller's own setting wins.
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1")
 try:  # share torch's HIP runtime when torch is present (one libamdhip64 per process)
     import torch  # noqa: F401
 except Exception:  # pragma: no cover

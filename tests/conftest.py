@@ -1,6 +1,8 @@
 import os
 import sys
 
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1")  # (as bench.py runs the epoch graphs)
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(ROOT, "deneva-plus_amd"), os.path.join(ROOT, "tests"), ROOT):
     if p not in sys.path:

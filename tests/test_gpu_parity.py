@@ -752,11 +752,13 @@ def test_randomized_sweep(case):
     _check(cc, rows, [g.gen(n_txn, 77 + case), g.gen(n_txn, 78 + case)], **knobs)
 
 
-def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1, stream=None):
+def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1, stream=None, reuse=False):
     """dv_epoch_run_device_batch (lanes > 1: dv_epoch_run_device_lanes over
     the engine and lanes - 1 decision lanes) against the oracle run over the
     same epochs one after the other: every epoch's commit bytes, digest and
-    write count, and the table after the batch."""
+    write count, and the table after the batch.  reuse: an epoch listed again
+    runs from the same device buffers (so its decision is captured into an
+    epoch graph the second time and replayed after)."""
     tab = O.YcsbTable(rows)
     f0 = tab.f0.copy()
     refs = [_oracle_epoch(cc, tab, f0, e) for e in epochs]
@@ -769,7 +771,11 @@ def _check_batch(cc, rows, epochs, prefix=None, max_iters=None, lanes=1, stream=
     for e in [eng] + extra:
         if max_iters:
             e.set_async_limits(max_iters, 0)
-    deps = [DeviceEpoch(e) for e in epochs]
+    if reuse:
+        made = {}
+        deps = [made.setdefault(id(e), DeviceEpoch(e)) for e in epochs]
+    else:
+        deps = [DeviceEpoch(e) for e in epochs]
     commits = [torch.zeros(max(1, e.n_txn), dtype=torch.uint8, device="cuda") for e in epochs]
     if lanes > 1:
         sts = eng.run_epochs_lanes(extra, deps, commits)
@@ -928,6 +934,69 @@ def test_small_epochs_pipelined_halted(lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc,lanes,prefix", [(dvcc.CALVIN, 1, None), (dvcc.CALVIN, 4, None), (dvcc.NO_WAIT, 1, None),
+                                             (dvcc.OCC, 4, None), (dvcc.WAIT_DIE, 3, None), (dvcc.NO_WAIT, 1, 512),
+                                             (dvcc.OCC, 4, 512)])
+def test_epoch_graphs_replayed(cc, lanes, prefix):
+    """Epochs from the same device buffers, again and again (as the bench
+    cycles them): the third time a (lane, buffers) pair comes, its decision
+    is captured into a graph, from the fourth on it is replayed -- every
+    epoch's results equal the sequential oracle's, small epochs (prefix-kill
+    ones run as they are), batch and lanes."""
+    import math
+    rows = 1 << 18
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    n = 20_000 if prefix else 5000
+    base = [g.gen(n, 1400 + k) for k in range(3)]
+    period = lanes * 3 // math.gcd(lanes, 3)  # (every lane meets every buffer once per period)
+    _check_batch(cc, rows, [base[k % 3] for k in range(5 * period)], prefix=prefix, lanes=lanes, reuse=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("lanes", [1, 4])
+def test_epoch_graphs_new_content_and_halts(lanes):
+    """The same device buffers refilled with new epochs of the same sizes
+    between calls (a graph replays whatever the buffers hold), and forced
+    yields: every epoch equals the oracle's, halted ones run again."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(dvcc.NO_WAIT, 5000, 50_000)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(None)
+    extra = [eng.open_lane() for _ in range(lanes - 1)]
+    bufs = [DeviceEpoch(g.gen(5000, 1500 + k)) for k in range(lanes)]
+    commits = [torch.zeros(5000, dtype=torch.uint8, device="cuda") for _ in range(lanes)]
+    yields = 0
+    for call in range(9):  # (a key's graph: captured at its 3rd call, replayed from its 4th)
+        if call == 4:
+            for e in [eng] + extra:
+                e.set_async_limits(1, 0)  # (forced yields from here on)
+        epochs = [g.gen(5000, 1600 + lanes * call + k) for k in range(lanes)]
+        for b, e in zip(bufs, epochs):
+            b.keys.copy_(torch.from_numpy(e.keys.view(np.int64)))
+            b.types.copy_(torch.from_numpy(e.types))
+            b.acc_txn.copy_(torch.from_numpy(e.acc_txn().view(np.int32)))
+            b.txn_begin.copy_(torch.from_numpy(e.txn_begin.astype(np.int32)))
+            if b.recs32 is not None:
+                b.recs32.copy_(torch.from_numpy(e.to_row_records().view(np.int32)))
+        torch.cuda.synchronize()
+        sts = eng.run_epochs_lanes(extra, bufs, commits) if extra else eng.run_epochs_device(bufs, commits)
+        for k, (e, st) in enumerate(zip(epochs, sts)):
+            c_ref, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e)
+            assert (commits[k].cpu().numpy() == c_ref).all(), (call, k)
+            assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                                   st_ref.write_cnt), (call, k)
+            yields += st.async_yields
+    assert (eng.read_table(0, rows) == f0).all()
+    assert yields > 0, "no asynchronous launch yielded"
+    for ln in extra:
+        ln.close()
+    eng.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 def test_config_b_lanes_timed_path():
     """The bench's config-B leg as timed: 65,536-txn CALVIN epochs (zipf 0.6,
@@ -935,7 +1004,7 @@ def test_config_b_lanes_timed_path():
     rows = 16_777_216
     g = YCSBQueryGenerator(rows, zipf_theta=0.6, txn_write_perc=1.0, tup_write_perc=0.5)
     base = [g.gen(65_536, dvcc.epoch_seed(0, e)) for e in range(3)]
-    _check_batch(dvcc.CALVIN, rows, [base[k % 3] for k in range(8)], lanes=4)
+    _check_batch(dvcc.CALVIN, rows, [base[k % 3] for k in range(12)], lanes=4, reuse=True)
 
 
 @pytest.mark.gpu
