@@ -57,6 +57,34 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 __device__ __forceinline__ void set_err(Counters *ctr, uint32_t bit) { atomicOr(&ctr->err, bit); }
 
+// commit bytes (1 = committed) of txns [0, n) from their status bytes, 16 per
+// thread per step over the whole grid; returns this thread's committed count
+__device__ __forceinline__ uint32_t commit_bytes_grid(const uint8_t *__restrict__ status, uint32_t n,
+                                                      uint8_t *__restrict__ out) {
+    uint32_t cnt = 0;
+    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u; i0 < n; i0 += gridDim.x * blockDim.x * 16u) {
+        if (i0 + 16 <= n && ((uintptr_t)out & 15u) == 0) {
+            const uint4 s4 = *reinterpret_cast<const uint4 *>(status + i0);
+            uint32_t w[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                // byte == ST_COMMIT (1) -> 1, else 0 (statuses are 0, 1 or 2)
+                const uint32_t c = w[q] & ~(w[q] >> 1) & 0x01010101u;
+                cnt += __popc(c);
+                w[q] = c;
+            }
+            if (out) *reinterpret_cast<uint4 *>(out + i0) = uint4{w[0], w[1], w[2], w[3]};
+        } else {
+            for (uint32_t i = i0; i < n; i++) {
+                const uint32_t c = status[i] == ST_COMMIT ? 1u : 0u;
+                if (out) out[i] = (uint8_t)c;
+                cnt += c;
+            }
+        }
+    }
+    return cnt;
+}
+
 __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x, uint32_t lane) {
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {

@@ -1450,29 +1450,7 @@ __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict
                                                        uint8_t *__restrict__ out, Counters *ctr) {
     __shared__ uint32_t part[4];
     if (ctr->halt) return;  // the rounds resume first (dv_epoch_finish)
-    uint32_t cnt = 0;
-    // 16 txns per thread per step
-    for (uint32_t i0 = (blockIdx.x * blockDim.x + threadIdx.x) * 16u; i0 < n;
-         i0 += gridDim.x * blockDim.x * 16u) {
-        if (i0 + 16 <= n && ((uintptr_t)out & 15u) == 0) {
-            uint4 s4 = *reinterpret_cast<const uint4 *>(status + i0);
-            uint32_t w[4] = {s4.x, s4.y, s4.z, s4.w};
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                // byte == ST_COMMIT (1) -> 1, else 0 (statuses are 0, 1 or 2)
-                const uint32_t c = w[q] & ~(w[q] >> 1) & 0x01010101u;
-                cnt += __popc(c);
-                w[q] = c;
-            }
-            if (out) *reinterpret_cast<uint4 *>(out + i0) = uint4{w[0], w[1], w[2], w[3]};
-        } else {
-            for (uint32_t i = i0; i < n; i++) {
-                const uint32_t c = status[i] == ST_COMMIT ? 1u : 0u;
-                if (out) out[i] = (uint8_t)c;
-                cnt += c;
-            }
-        }
-    }
+    uint32_t cnt = commit_bytes_grid(status, n, out);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
     if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;

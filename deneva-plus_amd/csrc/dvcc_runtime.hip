@@ -1265,8 +1265,10 @@ bool tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep);
 // the key is never captured again; DVCC_NO_GRAPHS=1 turns the graphs off.
 extern "C++" {  // (templates, inside the C API's block)
 // (prefix-kill epochs take no graphs: their ~25 launches overlap the device
-// work under decision lanes -- config D is device-bound -- and a bench cycles
-// too few of them per lane for a capture to pay)
+// work under decision lanes -- config D is device-bound.  Measured with every
+// prefix epoch replayed (4 distinct epochs over 4 lanes, 100 steps): host
+// queueing 89-103 -> 47-49 us per epoch, epoch 0.1608-0.1613 -> 0.1623-0.1642
+// ms, profiles/r05_n)
 constexpr size_t kMaxGraphs = 24;  // per context
 constexpr uint32_t kGraphNever = 0xFFFFFFFFu;
 constexpr uint32_t kGraphAfter = 3;  // encounters of a key before its capture
@@ -1644,7 +1646,10 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.tile_ctr = next_ticket(c);
         x.oid = c->tp_oid;
         x.ctr = c->ctr;
-        launch_tpcc_exec(c->stream, x);
+        x.n_txn = c->n_txn;
+        x.commit_out = d_commit;
+        launch_tpcc_exec(c->stream, x);  // (the commit bytes too)
+        return;
     } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
         if (c->cfg.cc_alg == DV_CALVIN)
             launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);

@@ -24,9 +24,11 @@ struct TpccExec {
     uint32_t *tile_ctr;        // a zeroed tile ticket
     uint64_t *oid;             // per txn (may be null)
     Counters *ctr;
+    uint32_t n_txn;            // the commit bytes of every txn (and the committed count) ...
+    uint8_t *commit_out;       // ... written by the update pass (may be null: the count only)
 };
-// updates (+ D_NEXT_O_ID snapshots), then -- CALVIN, several committed
-// NewOrders per district -- the o_id numbering
+// updates (+ D_NEXT_O_ID snapshots) and the commit bytes, then -- CALVIN,
+// several committed NewOrders per district -- the o_id numbering
 constexpr uint32_t kTpccCols = 3;
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x);
 

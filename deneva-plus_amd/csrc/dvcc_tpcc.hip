@@ -102,9 +102,17 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                                                        const uint64_t *__restrict__ args, uint64_t *cols,
                                                        int oid_direct, uint64_t *__restrict__ oid,
                                                        uint64_t *__restrict__ dsnap, uint64_t dist_base,
-                                                       uint64_t dist_rows, Counters *ctr) {
-    if (input_err(ctr) || ctr->halt) return;  // rejected epoch / rounds not finished
+                                                       uint64_t dist_rows, Counters *ctr, uint32_t n_txn,
+                                                       uint8_t *__restrict__ commit_out) {
+    if (ctr->halt) return;  // rounds not finished
     const uint32_t lane = threadIdx.x & 63;
+    {  // the commit bytes and the committed count (k_commit_out's work, one launch fewer)
+        uint32_t cc = commit_bytes_grid(status, n_txn, commit_out);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cc += __shfl_down(cc, off, 64);
+        if (lane == 0 && cc) atomicAdd(&my_slot(ctr).committed, cc);
+    }
+    if (input_err(ctr)) return;  // a rejected epoch changes no row
     unsigned long long wcnt = 0;
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock + (threadIdx.x & ~63u); base < n; base += stride) {
@@ -219,21 +227,35 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
     const uint32_t first = tid * kRIPT;
     const int cnt = first >= tile_n ? 0 : (tile_n - first < (uint32_t)kRIPT ? (int)(tile_n - first) : kRIPT);
     uint64_t e[kRIPT];
-    uint32_t flags = 0, heads = 0;
+    uint32_t flags = 0, heads = 0, dmask = 0;
     Agg a{0u, 0u, 0u};
     uint64_t pp = first == 0 ? s_prev : s_el[rpad(first - 1)];
 #pragma unroll
     for (int j = 0; j < kRIPT; j++) {
         e[j] = j < cnt ? s_el[rpad(first + j)] : ~0ull;
+        const uint32_t row = pair_row(e[j]);
+        dmask |= (j < cnt && row >= dist_base && row < dist_base + dist_rows ? 1u : 0u) << j;
+    }
+    // the district elements' status and first-access words, then their
+    // operation words: every load of a step in flight together (one at a time
+    // they were three round trips per district element)
+    uint8_t sv[kRIPT];
+    uint32_t tbv[kRIPT];
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++) {
+        const uint32_t t = (dmask >> j) & 1u ? pair_txn(e[j]) : 0u;
+        sv[j] = (dmask >> j) & 1u ? status[t] : (uint8_t)ST_ABORT;
+        tbv[j] = (dmask >> j) & 1u ? tb_start[t] : 0u;
+    }
+    uint64_t av[kRIPT];
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++) av[j] = sv[j] == ST_COMMIT ? args[tbv[j] + pair_pos(e[j])] : 0ull;
+#pragma unroll
+    for (int j = 0; j < kRIPT; j++) {
         if (j < cnt) {
             const uint32_t row = pair_row(e[j]);
             const bool head = pair_row(pp) != row;
-            bool f = false;
-            if (row >= dist_base && row < dist_base + dist_rows) {
-                const uint32_t t = pair_txn(e[j]);
-                f = status[t] == ST_COMMIT &&
-                    (uint32_t)(args[tb_start[t] + pair_pos(e[j])] >> 56) == DV_TOP_NO_DIST;
-            }
+            const bool f = sv[j] == ST_COMMIT && (uint32_t)(av[j] >> 56) == DV_TOP_NO_DIST;
             flags |= (f ? 1u : 0u) << j;
             heads |= (head ? 1u : 0u) << j;
             a = OpSeg::comb(a, Agg{head ? 1u : 0u, 0u, f ? 1u : 0u});
@@ -285,9 +307,13 @@ void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys
 }
 
 void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
-    if (x.n == 0) return;
-    DV_LAUNCH(k_tpcc_apply, grid_for(x.n), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.cols,
-              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr);
+    if (x.n == 0) {  // (no access to update: the commit bytes alone)
+        launch_commit_out(s, x.status, x.n_txn, x.commit_out, x.ctr);
+        return;
+    }
+    const uint64_t g = std::max<uint64_t>(x.n, (x.n_txn + 15u) / 16u);
+    DV_LAUNCH(k_tpcc_apply, grid_for(g), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.cols,
+              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr, x.n_txn, x.commit_out);
     if (x.oid_direct) return;
     const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
     DV_LAUNCH(k_tpcc_oid, ntiles, kBlock, 0, s, x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
