@@ -986,7 +986,8 @@ def extra_legs(a, out, pb, mpr, theta, n_txn_rank, n_txn_total, world, group):
         scm = sum(s.committed for s in sst)
         out["strong_scaling"] = {"txns_per_epoch": n_txn_total, "committed_per_s": scm / sel,
                                  "ms_per_epoch": sel / len(sst) * 1e3, "epochs": len(sst),
-                                 "protocol": "dv_epoch_run_part, mode %d" % a.part_mode}
+                                 "protocol": "dv_epoch_run_part, mode %d" % a.part_mode,
+                                 "sequence_order": a.order if a.cc.upper() != "CALVIN" else "origin"}
         del sdeps
         nxt += 100
     if not a.no_weak:

@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void k_rep_compact(const uint32_t *__restri
         for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
             k32[off + i] = gk[src + i];
             t32[off + i] = gt[src + i];
-            ty[off + i] = gy[src + i];
+            if (gy) ty[off + i] = gy[src + i];  // (position-major: the write bit rides in the row ids)
         }
     }
 }
@@ -1523,6 +1523,94 @@ int put_words(hipStream_t s, const uint64_t *v64, uint32_t n64, uint64_t *d64, c
 // o_ids -- computed where the district row lives -- are all-reduced (MAX)
 // into every rank's d_oid: Calvin's RFWD of o_id to the other participants
 // (tpcc_txn.cpp:1040, txn.cpp:960-972, transport/message.cpp:982-1025), for every protocol.
+// Replicated epochs in position-major order (DV_COMM_POSITION_ORDER; NO_WAIT
+// / WAIT_DIE / OCC): the batches are all-gathered as row id | wr << 31 and
+// position-major txn ids (origin q's txn j is j * P + q), interleaved txn by
+// txn into the sequence order the E-schedule decides in -- the epoch groups'
+// k_il_bounds / k_il_begin / k_il_move -- and decided by every rank with the
+// single-GPU path; the commit bytes go back to origin order (k_il_commits).
+// A malformed batch (txn ids not rising, past txns_per_rank) is not moved and
+// every rank -- each interleaves the same gathered batches -- reads the
+// refusal and returns DV_ERR_TXN_RANGE before anything is decided.  Why: the prefix
+// of a prefix-kill epoch (the first n / 32 txns) then holds every origin's
+// first txns and kills in every partition.
+int run_part_position(dv_ctx *c, DvComm *m, const dv_epoch_dev *home, uint64_t n_home,
+                      const std::vector<uint64_t> &recvc, uint64_t total, uint32_t txns_per_rank, uint32_t n_txn,
+                      uint32_t max_len, uint8_t *d_commit, dv_stats *st) {
+    const uint32_t P = (uint32_t)m->nranks;
+    hipStream_t s = ctx_stream(c);
+    uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);
+    uint32_t *sk = reinterpret_cast<uint32_t *>(sb), *stx = reinterpret_cast<uint32_t *>(sb + 4 * m->acc_cap);
+    uint32_t *rk = reinterpret_cast<uint32_t *>(rb), *rt = reinterpret_cast<uint32_t *>(rb + 4 * m->acc_cap);
+    if (n_home)
+        DV_LAUNCH(k_group_pack, (uint32_t)std::min<uint64_t>((n_home + kBlock - 1) / kBlock, 2048), kBlock, 0, s,
+                  home->keys, home->types, home->acc_txn, n_home, txns_per_rank, P, (uint32_t)m->rank, sk, stx);
+    CHK(hip_fail2(hipGetLastError(), "pack"));
+    uint64_t hmax = 0;
+    bool equal = true;
+    for (uint32_t q = 0; q < P; q++) {
+        hmax = std::max<uint64_t>(hmax, recvc[q]);
+        equal &= recvc[q] == recvc[0];
+    }
+    CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(sk), 4 * hmax, reinterpret_cast<uint8_t *>(rk), s));
+    CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(stx), 4 * hmax, reinterpret_cast<uint8_t *>(rt), s));
+    if (!equal) {  // (the padded parts packed, origin after origin)
+        uint32_t *ck = reinterpret_cast<uint32_t *>(m->keys), *ct = m->txn;
+        const dim3 grid((uint32_t)std::min<uint64_t>((hmax + kBlock - 1) / kBlock, 1024), std::min<uint32_t>(P, 64));
+        DV_LAUNCH(k_rep_compact, grid, kBlock, 0, s, rk, rt, (const uint8_t *)nullptr, hmax, m->xcnt + P, P, ck, ct,
+                  (uint8_t *)nullptr);
+        CHK(hip_fail2(hipGetLastError(), "compact"));
+        rk = ck;
+        rt = ct;
+    }
+    XSegs xs{};
+    xs.P = P;
+    xs.tpr = txns_per_rank;
+    uint64_t ro = 0;
+    uint32_t xtiles = 0;
+    for (uint32_t q = 0; q < P; q++) {
+        xs.eoff[q] = ro;
+        xs.toff[q] = xtiles;
+        xtiles += (uint32_t)((recvc[q] + kXTile - 1) / kXTile);
+        ro += recvc[q];
+    }
+    xs.eoff[P] = ro;
+    xs.toff[P] = xtiles;
+    xs.mP = div_magic(P);
+    xs.mT = div_magic(txns_per_rank);
+    const uint64_t nt = (uint64_t)P * txns_per_rank;
+    CHK(hip_fail2(hipMemsetAsync(m->gbad, 0, sizeof(uint32_t), s), "memset"));
+    if (!xtiles) {  // (no accesses: every txn empty)
+        CHK(hip_fail2(hipMemsetAsync(m->iltb, 0, 4 * (nt + 1), s), "memset"));
+    } else {
+        DV_LAUNCH(k_il_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0, s, rt, xs,
+                  m->tbo, m->ncnt);
+        DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbo,
+                  m->ncnt, m->iltb, m->ilsh);
+        DV_LAUNCH(k_il_move<true>, xtiles, kBlock, 0, s, rk, rt, xs, m->ilsh, m->iltb, ro, m->ilk, m->ilt, m->gbad);
+    }
+    CHK(hip_fail2(hipGetLastError(), "k_il_move"));
+    // every rank moved the same gathered batches, so every rank reads the
+    // same refusal here and returns the same error -- no collective needed
+    uint32_t refused = 0;
+    CHK(mail_get(m, s, nullptr, 0, m->gbad, 1, nullptr, &refused));
+    if (refused) return DV_ERR_TXN_RANGE;
+    dv_epoch_dev ep{};
+    ep.keys = reinterpret_cast<const uint64_t *>(m->ilk);  // (read as 32-bit row ids with the write bit)
+    ep.types = nullptr;
+    ep.acc_txn = m->ilt;
+    ep.tables = nullptr;
+    ep.n_acc = total;
+    ep.n_txn = n_txn;
+    ep.max_txn_acc = max_len;
+    const int r = epoch_run_replicated(c, &ep, m->ilk, P, d_commit ? m->verdict : nullptr, st);
+    if (r || !d_commit) return r;
+    DV_LAUNCH(k_il_commits, (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nt + kBlock - 1) / kBlock, 2048)),
+              kBlock, 0, s, m->verdict, xs, d_commit);
+    CHK(hip_fail2(hipGetLastError(), "k_il_commits"));
+    return hip_fail2(hipStreamSynchronize(s), "sync");
+}
+
 int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint64_t *args, bool tpcc,
              uint32_t txns_per_rank, uint8_t *d_commit, uint64_t *d_oid, dv_stats *st) {
     if (!c) return DV_ERR_ARG;
@@ -1545,15 +1633,19 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     //    rank), bad arguments, longest batch, what blocks a replicated epoch
     //    -- and every rank's batch size
     const bool rep_here = !tpcc && m->mode != 1 && ctx_rep_capable(c, P);
-    const uint32_t vote[4] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u,
-                              (uint32_t)std::min<uint64_t>(n_home, 0xFFFFFFFFull), rep_here ? 0u : kRepBlockOff};
+    // (and the sequence order: a replicated epoch may merge the origins' batches
+    // txn by txn, DV_COMM_POSITION_ORDER -- every rank the same order, else
+    // DV_ERR_ARG on every rank)
+    const uint32_t vote[6] = {(!bad && home->max_txn_acc) ? home->max_txn_acc : kMaxPos, bad ? kVoteBadArg : 0u,
+                              (uint32_t)std::min<uint64_t>(n_home, 0xFFFFFFFFull), rep_here ? 0u : kRepBlockOff,
+                              m->position ? 1u : 0u, m->position ? 0u : 1u};
     std::vector<uint64_t> sendc(P, n_home), recvc(P);
-    CHK(put_words(s, sendc.data(), P, m->xcnt, vote, 4, m->xvote));
+    CHK(put_words(s, sendc.data(), P, m->xcnt, vote, 6, m->xvote));
     CHK(m->x->all_to_all_u64(m->xcnt, m->xcnt + P, s));
-    CHK(m->x->max_u32(m->xvote, 4, s));
-    uint32_t gvote[4] = {0, 0, 0, 0};
-    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 4, recvc.data(), gvote));
-    if (gvote[1]) return DV_ERR_ARG;  // every rank: some rank's arguments were bad
+    CHK(m->x->max_u32(m->xvote, 6, s));
+    uint32_t gvote[6] = {0, 0, 0, 0, 0, 0};
+    CHK(mail_get(m, s, m->xcnt + P, P, m->xvote, 6, recvc.data(), gvote));
+    if (gvote[1] || (gvote[4] && gvote[5])) return DV_ERR_ARG;  // every rank: bad arguments, or mixed orders
     const uint32_t max_len = std::min<uint32_t>(gvote[0], kMaxPos);
     // 2. replicated when every rank allows it and the whole epoch fits this
     //    context (the same decision on every rank: voted and gathered values)
@@ -1562,6 +1654,11 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     for (uint32_t q = 0; q < P; q++) total += recvc[q];
     //    (one rank too: the replicated epoch is the single-GPU path plus a
     //    local copy, the list protocol a host round trip per decision round)
+    // position-major replicated epochs: the write bit in bit 31 of the row ids
+    // (global keys below 2^31), as the epoch groups' batches
+    const bool il = gvote[4] && cfg.cc_alg != DV_CALVIN && P > 1 && P <= kXMaxP && ctx_table0_rows(c) * P < (1ull << 31);
+    if (!gvote[3] && total <= cap && (uint64_t)gvote[2] * P <= m->acc_cap && il)
+        return run_part_position(c, m, home, n_home, recvc, total, txns_per_rank, n_txn, max_len, d_commit, st);
     if (!gvote[3] && total <= cap && (uint64_t)gvote[2] * P <= m->acc_cap) {
         // send and receive areas: [row ids 4 B | txn ids 4 B | types 1 B] per access
         uint8_t *sb = reinterpret_cast<uint8_t *>(m->send), *rb = reinterpret_cast<uint8_t *>(m->recv);

@@ -398,11 +398,13 @@ def _run_group(engines, homes, n_txn):
 
 def _engine_group(cc, world, rows_pp, n_txn, R=10, mode=1):
     """mode: dv_comm_set_mode -- 1 the list protocol (capacity for this
-    rank's share), 2 replicated (capacity for the whole epoch)."""
+    rank's share), 2 replicated (capacity for the whole epoch); + 8
+    (DV_COMM_POSITION_ORDER) position-major replicated epochs."""
     engines = []
     for p in range(world):
-        cap = n_txn * world * R + 4096 if mode == 2 else max(64, int(n_txn * world * R * 1.2 / world) + 4096)
-        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p, asynchronous=(mode != 2))
+        rep = (mode & 3) == 2
+        cap = n_txn * world * R + 4096 if rep else max(64, int(n_txn * world * R * 1.2 / world) + 4096)
+        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p, asynchronous=not rep)
         eng.load_ycsb_partition(rows_pp)
         engines.append(eng)
     dvcc.CCEngine.comm_init_local(engines)
@@ -411,17 +413,27 @@ def _engine_group(cc, world, rows_pp, n_txn, R=10, mode=1):
     return engines
 
 
-def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9, mode=1):
+def _origin_order(c_pos, world, n_txn):
+    """commit bytes of a position-major sequence (origin q's txn j at j * P +
+    q) in origin order (q * n_txn + j), as the engine returns them"""
+    return np.asarray(c_pos).reshape(n_txn, world).T.reshape(-1)
+
+
+def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9, mode=1, position=False):
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
-    engines = _engine_group(cc, world, rows_pp, n_txn, mode=mode)
+    engines = _engine_group(cc, world, rows_pp, n_txn,
+                            mode=mode | (dvcc._lib.DV_COMM_POSITION_ORDER if position else 0))
     tab = O.YcsbTable(rows_pp * world)  # one-partition view: row == key
     f0 = tab.f0.copy()
+    pos = position and cc != dvcc.CALVIN and (mode & 3) == 2  # (CALVIN, the list protocol: origin order)
     for k in range(epochs):
         batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 20 + k), r) for r in range(world)]
-        e = dvcc.sequence(batches)
+        e = dvcc.sequence_position(batches, n_txn) if pos else dvcc.sequence(batches)
         c_ref, _, st_ref = O.epoch_run(ORACLE_CC.get(cc, O.CALVIN), tab.ix, f0, e.n_txn, e.txn_begin, e.keys,
                                        e.types)
+        if pos:
+            c_ref = _origin_order(c_ref, world, n_txn)
         res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], n_txn)
         digest = writes = 0
         for r, x in enumerate(res):
@@ -462,7 +474,53 @@ def test_engine_driver_replicated(cc, world, mpr):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
+@pytest.mark.parametrize("world,mpr,mode", [(2, 0.3, 2), (4, 0.1, 2), (8, 0.5, 2), (3, 0.3, 1), (8, 0.1, 0)])
+def test_engine_driver_position_order(cc, world, mpr, mode):
+    """DV_COMM_POSITION_ORDER for the per-epoch driver: a replicated epoch
+    (mode 2, or mode 0 choosing it) merges the origins' batches txn by txn --
+    origin q's txn j at j * P + q -- against the oracle over
+    dvcc.sequence_position, commit bytes back in origin order; CALVIN and the
+    list protocol (mode 1) keep the origin order under the flag."""
+    _check_group(cc, world, 1 << 14, 3000, mpr, mode=mode, position=True)
+
+
+@pytest.mark.gpu
+def test_engine_driver_position_order_malformed_batch():
+    """A position-major replicated epoch whose batch on one rank has txn ids
+    that do not rise: the interleave refuses to move it and every rank
+    returns DV_ERR_TXN_RANGE before anything executes; the next epoch runs."""
+    world, rows_pp, n_txn = 2, 1 << 12, 800
+    gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
+                                  strict_ppt=1, mpr=0.3)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2 | dvcc._lib.DV_COMM_POSITION_ORDER)
+    before = [eng.read_table(0, rows_pp) for eng in engines]
+    batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 70), r) for r in range(world)]
+    homes = [dvcc.DeviceEpoch(b) for b in batches]
+    t = homes[1].acc_txn.clone()
+    a, b = int(batches[1].txn_begin[5]), int(batches[1].txn_begin[6])
+    t[a:b] = 9  # (txn 5's accesses claim txn 9: the ids no longer rise)
+    homes[1] = dvcc.DeviceEpoch.from_tensors(homes[1].keys, homes[1].types, t, n_txn, max_txn_acc=10)
+    res = _run_group(engines, homes, n_txn)
+    for r, x in enumerate(res):
+        assert isinstance(x, dvcc.DvccError) and x.code == dvcc._lib.DV_ERR_TXN_RANGE, (r, x)
+    for eng, b0 in zip(engines, before):
+        assert (eng.read_table(0, rows_pp) == b0).all()
+    batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 71), r) for r in range(world)]
+    e = dvcc.sequence_position(batches, n_txn)
+    tab = O.YcsbTable(rows_pp * world)
+    f0 = tab.f0.copy()
+    c_ref, _, st_ref = O.epoch_run(O.NO_WAIT, tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types)
+    res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], n_txn)
+    for r, x in enumerate(res):
+        assert not isinstance(x, Exception), (r, x)
+        assert (x[0] == _origin_order(c_ref, world, n_txn)).all(), r
+    for eng in engines:
+        eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [1, 2, 10])
 def test_engine_driver_unequal_batches(mode):
     """Ranks with fewer txns than txns_per_rank (the rest of their sequence
     slots are empty txns): unequal parts through the list protocol and the
@@ -475,10 +533,13 @@ def test_engine_driver_unequal_batches(mode):
     for b in batches:  # the oracle's epoch: each batch's unused slots as empty txns
         tb = np.concatenate([b.txn_begin, np.full(tpr - b.n_txn, b.txn_begin[-1], np.uint32)])
         padded.append(dvcc.Epoch(b.keys, b.types, tb))
-    e = dvcc.sequence(padded)
+    pos = mode & dvcc._lib.DV_COMM_POSITION_ORDER  # (mode 10: position-major replicated epochs)
+    e = dvcc.sequence_position(padded, tpr) if pos else dvcc.sequence(padded)
     tab = O.YcsbTable(rows_pp * world)
     f0 = tab.f0.copy()
     c_ref, _, st_ref = O.epoch_run(O.NO_WAIT, tab.ix, f0, e.n_txn, e.txn_begin, e.keys, e.types)
+    if pos:
+        c_ref = _origin_order(c_ref, world, tpr)
     engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, tpr, mode=mode)
     res = _run_group(engines, [dvcc.DeviceEpoch(b) for b in batches], tpr)
     digest = 0
@@ -497,8 +558,10 @@ def test_engine_driver_unequal_batches(mode):
 @pytest.mark.slow
 def test_engine_driver_replicated_prefix_kill():
     """Config-D-shaped epoch large enough for the prefix-kill path inside the
-    replicated protocol: 4 partitions x 40,000 txns (160,000 in total)."""
+    replicated protocol: 4 partitions x 40,000 txns (160,000 in total), in
+    origin and in position order."""
     _check_group(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, epochs=1, mode=2)
+    _check_group(dvcc.NO_WAIT, 4, 1 << 18, 40_000, 0.1, epochs=1, mode=2, position=True)
 
 
 @pytest.mark.gpu
