@@ -145,6 +145,18 @@ struct Counters {
 };
 __device__ inline CtrSlot &my_slot(Counters *ctr) { return ctr->slot[blockIdx.x & (kSlots - 1)]; }
 
+// Decision lanes: an epoch's execution keeps the lanes' epoch order through
+// two device words (run_lanes) -- prev: the gate word of the epoch executed
+// before it (nonzero: that one halted or failed, so this one starts halted),
+// read by every workgroup of the execution's first launch; out: this epoch's
+// gate word, written by that launch (exec_gate, dvcc_common.h).  The lane's event then
+// follows the execution directly (no gate launch before it, no counter
+// read-back launch between it and the next epoch's execution).
+struct ExecGate {
+    const uint32_t *prev = nullptr;
+    uint32_t *out = nullptr;
+};
+
 struct IxEntry {
     uint64_t key;
     uint64_t row;
@@ -631,13 +643,15 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
 // commit bytes into d_commit (may be NULL) and the committed count, as
 // launch_commit_out would.  pk_dense: the rows are a dense one-partition YCSB
 // map whose row r holds key r - pk_base (k_ycsb_load), so a read's primary
-// key comes from its row instead of a second random line of the pkey column
-void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+// key comes from its row instead of a second random line of the pkey column.
+// These two and launch_tpcc_exec take the lanes' ExecGate and return whether
+// they launched anything (false: the gate words are the caller's to handle).
+bool launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
                      const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
-                     bool pk_dense = false, uint64_t pk_base = 0);
-void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
-                       Counters *ctr);
+                     bool pk_dense = false, uint64_t pk_base = 0, ExecGate eg = ExecGate{});
+bool launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
+                       Counters *ctr, ExecGate eg = ExecGate{});
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag);
 // bits[w] bit j = (ktag[32 w + j] == htag), rows [0, n)

@@ -1354,9 +1354,10 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      uint64_t *__restrict__ f0,
                                                      const uint64_t *__restrict__ pkey,
                                                      Counters *ctr, RowMap rm, uint8_t *__restrict__ commit_out,
-                                                     int pk_dense, uint64_t pk_base) {
+                                                     int pk_dense, uint64_t pk_base, ExecGate eg) {
     __shared__ unsigned long long part[3][4];
-    if (ctr->halt) return;  // rounds not finished (dv_epoch_finish resumes them)
+    // rounds not finished (dv_epoch_finish resumes them), or the epoch before halted
+    if (exec_gate(ctr, eg)) return;
     const bool rows = !input_err(ctr);  // a rejected epoch changes no row
     if (!(MODE & EX_COMMIT) && !rows) return;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1427,29 +1428,31 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
     }
 }
 
-void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+bool launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
                      const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
-                     bool pk_dense, uint64_t pk_base) {
+                     bool pk_dense, uint64_t pk_base, ExecGate eg) {
     const int pkd = pk_dense && rm.P == 0 ? 1 : 0;  // (replicated epochs read the column)
-    if (n_txn == 0) return;
+    if (n_txn == 0) return false;
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
         DV_LAUNCH((k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn,
-                                                                              status, f0, pkey, ctr, rm, d_commit, pkd, pk_base);
-    } else {
+                                                                              status, f0, pkey, ctr, rm, d_commit, pkd, pk_base, eg);
+    } else {  // (both gate words in the first launch)
         DV_LAUNCH((k_exec_txn<EX_READS | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                                   pkey, ctr, rm, d_commit, pkd, pk_base);
+                                                                   pkey, ctr, rm, d_commit, pkd, pk_base, eg);
         DV_LAUNCH((k_exec_txn<EX_WRITES>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                        pkey, ctr, rm, nullptr, pkd, pk_base);
+                                                        pkey, ctr, rm, nullptr, pkd, pk_base, ExecGate{});
     }
+    return true;
 }
 
 __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict__ status, uint32_t n,
-                                                       uint8_t *__restrict__ out, Counters *ctr) {
+                                                       uint8_t *__restrict__ out, Counters *ctr, ExecGate eg) {
     __shared__ uint32_t part[4];
-    if (ctr->halt) return;  // the rounds resume first (dv_epoch_finish)
+    // the rounds resume first (dv_epoch_finish), or the epoch before halted
+    if (exec_gate(ctr, eg)) return;
     uint32_t cnt = commit_bytes_grid(status, n, out);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
@@ -1461,12 +1464,13 @@ __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict
     }
 }
 
-void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
-                       Counters *ctr) {
-    if (!n_txn) return;
+bool launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
+                       Counters *ctr, ExecGate eg) {
+    if (!n_txn) return false;
     uint32_t blocks = (n_txn + kBlock * 16 - 1) / (kBlock * 16);
     if (blocks > 1024) blocks = 1024;
-    DV_LAUNCH(k_commit_out, blocks, kBlock, 0, s, status, n_txn, d_commit, ctr);
+    DV_LAUNCH(k_commit_out, blocks, kBlock, 0, s, status, n_txn, d_commit, ctr, eg);
+    return true;
 }
 
 // ------------------------------------------------------------- loaders

@@ -1624,10 +1624,21 @@ int redo_survivors(dv_ctx *c);
 // the execution of the committed txns and the commit bytes (every execution
 // kernel is a no-op for a rejected epoch, input_err, and while the rounds
 // are halted, Counters::halt)
-void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
-    if (c->prefix_mode)  // the survivors' decisions back to their txns
+// the last of the epoch's decision that enqueue_exec would queue: the
+// survivors' decisions back to their txns (a prefix-kill epoch; the epoch's
+// own state) -- decision lanes queue it before the wait for the previous
+// epoch's execution
+void exec_prologue(dv_ctx *c) {
+    if (c->prefix_mode)
         launch_sub_scatter_back(c->stream, c->b_map, c->b_status, c->v_n_txn, c->status, c->ctr,
                                 c->surv_words ? c->tword : nullptr);
+}
+
+// eg (decision lanes, run_lanes): the gate words of the previous epoch's
+// execution and of this one's; returns whether eg.out is written (false: the
+// caller's counter read-back writes it).  prologue_done: exec_prologue ran.
+bool enqueue_exec(dv_ctx *c, uint8_t *d_commit, ExecGate eg = ExecGate{}, bool prologue_done = false) {
+    if (!prologue_done) exec_prologue(c);
     if (c->cfg.workload == DV_TPCC) {
         const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
         TpccExec x{};
@@ -1648,9 +1659,15 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
         x.ctr = c->ctr;
         x.n_txn = c->n_txn;
         x.commit_out = d_commit;
-        launch_tpcc_exec(c->stream, x);  // (the commit bytes too)
-        return;
-    } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
+        x.gate = eg;
+        if (launch_tpcc_exec(c->stream, x)) return true;  // (the commit bytes too)
+        if (eg.prev) launch_lane_gate(c->stream, eg.prev, c->ctr);
+        return false;
+    }
+    // (launches that read no gate word: the gate's own launch first)
+    const bool txn_exec = !c->route && c->cfg.cc_alg != DV_CALVIN;
+    if (eg.prev && !txn_exec) launch_lane_gate(c->stream, eg.prev, c->ctr);
+    if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
         if (c->cfg.cc_alg == DV_CALVIN)
             launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);
         else
@@ -1668,13 +1685,16 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit) {
             // (its dense test; only with table 0 the context's one table -- a
             // row of another table takes its key from the pkey column)
             const KillKeys dk = kill_keys(make_tables(c), nullptr, nullptr, nullptr);
-            launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
-                            c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit,
-                            dk.tabs.n == 1 && dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep, dk.dense_base);
-            return;
+            if (launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
+                                c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit,
+                                dk.tabs.n == 1 && dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep,
+                                dk.dense_base, eg))
+                return true;
+            if (eg.prev) launch_lane_gate(c->stream, eg.prev, c->ctr);  // (nothing launched)
+            return false;
         }
     }
-    launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
+    return launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr, ExecGate{nullptr, eg.out});
 }
 }  // namespace
 
@@ -2701,15 +2721,19 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         const auto td = hclock::now();
         int r = decide(c, k);
         t_decide += std::chrono::duration<double>(hclock::now() - td).count();
-        if (!r && prev) {
-            r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
-            if (!r) launch_lane_gate(c->stream, prev->d_gate + prev_slot, c->ctr);
-        }
+        if (!r) exec_prologue(c);
+        if (!r && prev) r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
+        // the execution reads the previous epoch's gate word and writes this
+        // one's, so the event follows it (and the refill) directly; the
+        // counter read-back is off the lanes' chain of executions
+        bool gated = false;
         if (!r) {
-            enqueue_exec(c, commit_of(k));
+            gated = enqueue_exec(c, commit_of(k), ExecGate{prev ? prev->d_gate + prev_slot : nullptr, c->d_gate + slot},
+                                 true);
             r = hip_fail(hipGetLastError(), "execution launch");
         }
         if (!r) r = after(c, k);
+        if (!r && gated) r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
         if (!r) {
             EpochSnap &sn = p.sn;
             sn.n_acc = c->n_acc;
@@ -2723,8 +2747,8 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
             sn.n_acc_is_bound = c->n_acc_is_bound;
             sn.async_unconfirmed = c->async_unconfirmed;
             sn.slot = slot;
-            sn.seq = mirror_out(c, slot, true);
-            r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
+            sn.seq = mirror_out(c, slot, !gated);
+            if (!gated) r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
         }
         c->phase = 0;
         c->prefix_mode = false;

@@ -26,10 +26,11 @@ struct TpccExec {
     Counters *ctr;
     uint32_t n_txn;            // the commit bytes of every txn (and the committed count) ...
     uint8_t *commit_out;       // ... written by the update pass (may be null: the count only)
+    ExecGate gate;             // decision lanes: read by the first launch, written by the last
 };
 // updates (+ D_NEXT_O_ID snapshots) and the commit bytes, then -- CALVIN,
 // several committed NewOrders per district -- the o_id numbering
 constexpr uint32_t kTpccCols = 3;
-void launch_tpcc_exec(hipStream_t s, const TpccExec &x);
+bool launch_tpcc_exec(hipStream_t s, const TpccExec &x);
 
 }  // namespace dvcc

@@ -103,8 +103,8 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                                                        int oid_direct, uint64_t *__restrict__ oid,
                                                        uint64_t *__restrict__ dsnap, uint64_t dist_base,
                                                        uint64_t dist_rows, Counters *ctr, uint32_t n_txn,
-                                                       uint8_t *__restrict__ commit_out) {
-    if (ctr->halt) return;  // rounds not finished
+                                                       uint8_t *__restrict__ commit_out, ExecGate eg) {
+    if (exec_gate(ctr, eg)) return;  // rounds not finished, or the epoch before halted
     const uint32_t lane = threadIdx.x & 63;
     {  // the commit bytes and the committed count (k_commit_out's work, one launch fewer)
         uint32_t cc = commit_bytes_grid(status, n_txn, commit_out);
@@ -208,12 +208,14 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
                                                      const uint64_t *__restrict__ dsnap, uint64_t dist_base,
                                                      uint64_t dist_rows, uint64_t *__restrict__ cols,
                                                      uint64_t *__restrict__ oid, uint64_t *desc,
-                                                     uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
+                                                     uint32_t *tile_ctr, uint32_t tag, Counters *ctr,
+                                                     uint32_t *gate_out) {
     __shared__ uint64_t s_el[kRTile + kRTile / kRIPT];
     __shared__ uint64_t s_next, s_prev;
     __shared__ uint32_t s_tile;
     __shared__ Agg wt[4];
     __shared__ Agg s_pre;
+    // (k_tpcc_apply read the gate word of the epoch before and wrote this one's)
     const uint32_t ntiles = (n + kRTile - 1) / kRTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -271,6 +273,10 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
         for (int w = 1; w < 4; w++) bagg = OpSeg::comb(bagg, wt[w]);
         const Agg pre = look_back<OpSeg>(desc, tile, tag, bagg, lane, ctr);
         if (lane == 0) s_pre = pre;
+        // a look-back that gave up (ERRB_SPIN) fails the epoch: the gate word
+        // k_tpcc_apply wrote becomes 1 (no other write to it is in flight)
+        if (gate_out && lane == 0 && __hip_atomic_load(&ctr->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            *gate_out = 1u;
     }
     __syncthreads();
     Agg run = s_pre;
@@ -306,18 +312,19 @@ void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys
     DV_LAUNCH(k_tpcc_resolve, grid_for(n), kBlock, 0, s, tabs, keys, tables, n, cols, okeys, otables);
 }
 
-void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
-    if (x.n == 0) {  // (no access to update: the commit bytes alone)
-        launch_commit_out(s, x.status, x.n_txn, x.commit_out, x.ctr);
-        return;
-    }
+bool launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
+    if (x.n == 0)  // (no access to update: the commit bytes alone)
+        return launch_commit_out(s, x.status, x.n_txn, x.commit_out, x.ctr, x.gate);
     const uint64_t g = std::max<uint64_t>(x.n, (x.n_txn + 15u) / 16u);
     DV_LAUNCH(k_tpcc_apply, grid_for(g), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.cols,
-              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr, x.n_txn, x.commit_out);
-    if (x.oid_direct) return;
+              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr, x.n_txn, x.commit_out,
+              x.gate);
+    if (x.oid_direct) return true;
     const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
     DV_LAUNCH(k_tpcc_oid, ntiles, kBlock, 0, s, x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
-                                         x.dist_base, x.dist_rows, x.cols, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
+                                         x.dist_base, x.dist_rows, x.cols, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr,
+                                         x.gate.out);
+    return true;
 }
 
 }  // namespace dvcc
