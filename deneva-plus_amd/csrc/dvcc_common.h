@@ -57,23 +57,6 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
 
 __device__ __forceinline__ void set_err(Counters *ctr, uint32_t bit) { atomicOr(&ctr->err, bit); }
 
-// ExecGate at an execution launch's start (block-uniform): is the epoch
-// halted -- its rounds unfinished, or the epoch executed before it halted or
-// failed (then this one halts too: k_lane_gate's work, done by every
-// workgroup reading the word instead of a launch before them)?  And this
-// epoch's gate word for the next one, from its counters (k_ctr_out's gate):
-// the execution launches set no error and no halt but this one, so workgroup
-// 0 writes it here -- one store, where a last-workgroup count needs a
-// device-scope fence per workgroup (an L2 write-back each: 4,096 of them took
-// a config-D epoch from 0.18 to 0.39 ms)
-__device__ __forceinline__ bool exec_gate(Counters *ctr, const ExecGate &eg) {
-    const bool prev = eg.prev && *eg.prev;
-    if (prev && threadIdx.x == 0) ctr->halt = 1u;
-    if (eg.out && blockIdx.x == 0 && threadIdx.x == 0)
-        *eg.out = (prev || ctr->halt || ctr->a_halt || ctr->err || ctr->peer_err) ? 1u : 0u;
-    return prev || ctr->halt;
-}
-
 // commit bytes (1 = committed) of txns [0, n) from their status bytes, 16 per
 // thread per step over the whole grid; returns this thread's committed count
 __device__ __forceinline__ uint32_t commit_bytes_grid(const uint8_t *__restrict__ status, uint32_t n,

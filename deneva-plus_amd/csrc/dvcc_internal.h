@@ -145,18 +145,6 @@ struct Counters {
 };
 __device__ inline CtrSlot &my_slot(Counters *ctr) { return ctr->slot[blockIdx.x & (kSlots - 1)]; }
 
-// Decision lanes: an epoch's execution keeps the lanes' epoch order through
-// two device words (run_lanes) -- prev: the gate word of the epoch executed
-// before it (nonzero: that one halted or failed, so this one starts halted),
-// read by every workgroup of the execution's first launch; out: this epoch's
-// gate word, written by that launch (exec_gate, dvcc_common.h).  The lane's event then
-// follows the execution directly (no gate launch before it, no counter
-// read-back launch between it and the next epoch's execution).
-struct ExecGate {
-    const uint32_t *prev = nullptr;
-    uint32_t *out = nullptr;
-};
-
 struct IxEntry {
     uint64_t key;
     uint64_t row;
@@ -294,7 +282,8 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
                   hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *keys32 = nullptr,
-                  const uint64_t *ts = nullptr, const uint32_t *n_dev = nullptr);
+                  const uint64_t *ts = nullptr, const uint32_t *n_dev = nullptr,
+                  const uint64_t *rsv_cols = nullptr);  // (TPC-C: last names resolved, tpcc_last_name_key)
 
 // prefix-kill epochs with their txn boundaries (dv_epoch_dev::txn_begin):
 // every txn's range checked, the prefix's txns [0, K) probed (acc_row, tlen,
@@ -632,9 +621,12 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // the counters into their host-mapped mirror hctr, then *hseq = seq (device
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
-                    unsigned long long seq, uint32_t *gate = nullptr);
-// decision lanes (dv_epoch_run_device_lanes): halt this epoch if *prev_gate
-void launch_lane_gate(hipStream_t s, const uint32_t *prev_gate, Counters *ctr);
+                    unsigned long long seq);
+// decision lanes (dv_epoch_run_device_lanes): after an epoch's execution,
+// *word = seq << 1 | (it halted or failed); before the next one's, wait for
+// that seq and halt if the bit is set (or after 1 s without it)
+void launch_lane_post(hipStream_t s, uint32_t *word, uint32_t seq, const Counters *ctr);
+void launch_lane_wait(hipStream_t s, const uint32_t *word, uint32_t seq, Counters *ctr);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,
@@ -643,15 +635,13 @@ void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const
 // commit bytes into d_commit (may be NULL) and the committed count, as
 // launch_commit_out would.  pk_dense: the rows are a dense one-partition YCSB
 // map whose row r holds key r - pk_base (k_ycsb_load), so a read's primary
-// key comes from its row instead of a second random line of the pkey column.
-// These two and launch_tpcc_exec take the lanes' ExecGate and return whether
-// they launched anything (false: the gate words are the caller's to handle).
-bool launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+// key comes from its row instead of a second random line of the pkey column
+void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
                      const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
-                     bool pk_dense = false, uint64_t pk_base = 0, ExecGate eg = ExecGate{});
-bool launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
-                       Counters *ctr, ExecGate eg = ExecGate{});
+                     bool pk_dense = false, uint64_t pk_base = 0);
+void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
+                       Counters *ctr);
 void launch_ycsb_load(hipStream_t s, uint64_t rows, uint32_t part_cnt, uint32_t part_id,
                       uint64_t *f0, uint64_t *pkey, uint8_t *ktag);
 // bits[w] bit j = (ktag[32 w + j] == htag), rows [0, n)

@@ -18,6 +18,7 @@
 #include <hip/hip_ext.h>
 
 #include "dvcc_common.h"
+#include "dvcc_tpcc.h"
 
 #ifndef DVCC_PROBE_HIST_WAVES
 #define DVCC_PROBE_HIST_WAVES 6
@@ -35,7 +36,9 @@ namespace dvcc {
 // began in an earlier wave is walked back in memory (at most one per wave).
 // Repeated rows inside a txn are detected later, in row order (seg_prepare).
 constexpr int kPV = 4;  // (8 measured slower: fewer waves per SIMD)
-template <bool HIST>
+// RSV (TPC-C): CUST_LAST accesses name a customer by last name, resolved
+// here against the name index and rsv_cols (tpcc_last_name_key)
+template <bool HIST, bool RSV>
 __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *__restrict__ keys,
                                            const uint32_t *__restrict__ keys32,
                                                   const uint8_t *__restrict__ types,
@@ -49,7 +52,8 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
                                                   uint32_t *__restrict__ acc_row, Counters *ctr,
                                                   uint32_t *__restrict__ counts, uint32_t ntiles,
                                                   uint32_t pair_limit, const uint64_t *__restrict__ ts,
-                                                  const uint32_t *__restrict__ n_dev) {
+                                                  const uint32_t *__restrict__ n_dev,
+                                                  const uint64_t *__restrict__ rsv_cols) {
     if (n_dev && (uint64_t)*n_dev < n) n = *n_dev;  // (the real count of a device-built epoch)
     if (blockIdx.x == 0 && threadIdx.x == 0) ctr->n_acc = (uint32_t)n;
     // The first radix pass's histogram (digit = row bits [0, 8)) is counted
@@ -119,9 +123,15 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
         for (int j = 0; j < kPV; j++) {
             row[j] = 0;
             if (i0 + j < n) {
-                if (tables)
-                    probe_row(s_td[tb[j] < kMaxTables ? tb[j] : 0], tb[j] < tabs.n, key[j], row[j], ctr, &miss);
-                else
+                if (tables) {
+                    uint32_t t = tb[j];
+                    uint64_t k = key[j];
+                    if (RSV && t == DV_TPCC_CUST_LAST && t < tabs.n) {  // (else: the missing table reported)
+                        k = tpcc_last_name_key(s_td[t], rsv_cols, k);
+                        t = DV_TPCC_CUSTOMER;
+                    }
+                    probe_row(s_td[t < kMaxTables ? t : 0], t < tabs.n, k, row[j], ctr, &miss);
+                } else
                     probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr, &miss);
             }
         }
@@ -273,6 +283,7 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
 }
 
 // the fused-histogram variant needs more registers: capped at 6 waves per SIMD
+template <bool RSV>
 __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *__restrict__ keys,
                                                   const uint32_t *__restrict__ keys32,
                                                   const uint8_t *__restrict__ types,
@@ -282,19 +293,21 @@ __global__ __launch_bounds__(kBlock) void k_probe(Tables tabs, const uint64_t *_
                                                   uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
                                                   uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row,
                                                   Counters *ctr, uint32_t pair_limit, const uint64_t *__restrict__ ts,
-                                                  const uint32_t *__restrict__ n_dev) {
-    probe_body<false>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                      ctr, nullptr, 0, pair_limit, ts, n_dev);
+                                                  const uint32_t *__restrict__ n_dev,
+                                                  const uint64_t *__restrict__ rsv_cols) {
+    probe_body<false, RSV>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen,
+                           acc_row, ctr, nullptr, 0, pair_limit, ts, n_dev, rsv_cols);
 }
+template <bool RSV>
 __global__ __launch_bounds__(kBlock, DVCC_PROBE_HIST_WAVES) void k_probe_hist(
     Tables tabs, const uint64_t *__restrict__ keys, const uint32_t *__restrict__ keys32,
     const uint8_t *__restrict__ types,
     const uint32_t *__restrict__ acc_txn, const uint8_t *__restrict__ tables, uint64_t n, uint32_t n_txn,
     uint32_t slog, uint64_t *__restrict__ pairs, uint32_t *__restrict__ tb_start, uint32_t *__restrict__ tb_end,
     uint8_t *__restrict__ tlen, uint32_t *__restrict__ acc_row, Counters *ctr, uint32_t *__restrict__ counts,
-    uint32_t ntiles, const uint64_t *__restrict__ ts) {
-    probe_body<true>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row,
-                     ctr, counts, ntiles, n_txn, ts, nullptr);
+    uint32_t ntiles, const uint64_t *__restrict__ ts, const uint64_t *__restrict__ rsv_cols) {
+    probe_body<true, RSV>(tabs, keys, keys32, types, acc_txn, tables, n, n_txn, slog, pairs, tb_start, tb_end, tlen,
+                          acc_row, ctr, counts, ntiles, n_txn, ts, nullptr, rsv_cols);
 }
 
 void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
@@ -302,21 +315,30 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
                   uint32_t slog, uint64_t *pairs, uint32_t *tb_start, uint32_t *tb_end,
                   uint8_t *tlen, uint32_t *acc_row, Counters *ctr, uint32_t *counts, uint32_t pair_limit,
                   hipEvent_t ev0, hipEvent_t ev1, const uint32_t *keys32, const uint64_t *ts,
-                  const uint32_t *n_dev) {
+                  const uint32_t *n_dev, const uint64_t *rsv_cols) {
     if (n_acc == 0) return;
     const uint32_t ntiles = nblocks_for(n_acc);
     if (pair_limit < n_txn || n_dev) counts = nullptr;  // the prefix's keys only / a device count: no first histogram
     const uint64_t units = counts ? ntiles : (n_acc + (uint64_t)kBlock * kPV - 1) / ((uint64_t)kBlock * kPV);
     const uint32_t blocks = units > 4096 ? 4096u : (uint32_t)units;
     // (ev0 / ev1: the launch's own dispatch timestamps, no extra packets)
-    if (counts)
-        DV_LAUNCH_EV(k_probe_hist, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types,
+    const uint32_t lim = pair_limit < n_txn ? pair_limit : n_txn;
+    if (counts && rsv_cols)
+        DV_LAUNCH_EV(k_probe_hist<true>, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types,
                               acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              counts, ntiles, ts);
+                              counts, ntiles, ts, rsv_cols);
+    else if (counts)
+        DV_LAUNCH_EV(k_probe_hist<false>, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types,
+                              acc_txn, tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
+                              counts, ntiles, ts, nullptr);
+    else if (rsv_cols)
+        DV_LAUNCH_EV(k_probe<true>, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
+                              tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr, lim, ts, n_dev,
+                              rsv_cols);
     else
-        DV_LAUNCH_EV(k_probe, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
-                              tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr,
-                              pair_limit < n_txn ? pair_limit : n_txn, ts, n_dev);
+        DV_LAUNCH_EV(k_probe<false>, blocks, kBlock, 0, s, ev0, ev1, tabs, keys, keys32, types, acc_txn,
+                              tables, n_acc, n_txn, slog, pairs, tb_start, tb_end, tlen, acc_row, ctr, lim, ts, n_dev,
+                              nullptr);
 }
 
 // The probe of a prefix-kill epoch whose txn boundaries come with it
@@ -1221,34 +1243,60 @@ __global__ __launch_bounds__(kBlock) void k_epoch_clear(uint8_t *__restrict__ st
 // the counters into their host-mapped mirror, then the sequence word the
 // host spins on (sync_counters): no blit and no stream synchronisation
 // between an epoch's last kernel and the host reading its outcome
-// gate (decision lanes, optional): one device word for the epoch executed
-// after this one on another lane -- nonzero when this epoch halted or failed
 __global__ __launch_bounds__(kBlock) void k_ctr_out(const Counters *__restrict__ ctr, Counters *hctr,
-                                                    unsigned long long *hseq, unsigned long long seq,
-                                                    uint32_t *gate) {
+                                                    unsigned long long *hseq, unsigned long long seq) {
     const uint32_t *src = reinterpret_cast<const uint32_t *>(ctr);
     uint32_t *dst = reinterpret_cast<uint32_t *>(hctr);
     for (uint32_t i = threadIdx.x; i < sizeof(Counters) / 4; i += kBlock) dst[i] = src[i];
-    if (gate && threadIdx.x == 0) *gate = (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(hseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
-                    unsigned long long seq, uint32_t *gate) {
-    DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq, gate);
+                    unsigned long long seq) {
+    DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq);
 }
 
-// decision lanes: before an epoch executes, the epoch executed before it (on
-// another lane) must have neither halted nor failed -- else this one halts
-// too (nothing of it executes; the host runs both again, in order)
-__global__ void k_lane_gate(const uint32_t *__restrict__ prev_gate, Counters *ctr) {
-    if (threadIdx.x == 0 && *prev_gate) ctr->halt = 1u;
+// Decision lanes' execution order (run_lanes), kept on the device: after an
+// epoch's execution its lane posts one word, (sequence << 1) | gate -- the
+// gate set when the epoch halted or failed -- and the lane of the next epoch
+// waits for that sequence before its execution, which starts halted when the
+// gate is set (nothing of it executes; the host runs both again, in order).
+// A kernel boundary on either side orders the rows: the execution's writes
+// are released before the post, the next execution starts after the wait.
+// (An event recorded on one lane's stream and waited for on the next cost
+// the host 13-15 us per graph launch behind it instead of 3-4: the TPC-C
+// window was host-bound at 0.058 ms per epoch.)
+__global__ void k_lane_post(uint32_t *word, uint32_t seq, const Counters *__restrict__ ctr) {
+    if (threadIdx.x != 0) return;
+    const uint32_t gate = (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
+    __hip_atomic_store(word, (seq << 1) | gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-void launch_lane_gate(hipStream_t s, const uint32_t *prev_gate, Counters *ctr) {
-    DV_LAUNCH(k_lane_gate, 1, 64, 0, s, prev_gate, ctr);
+// the wait is bounded: a predecessor that has not posted after kLaneWaitTicks
+// (1 s of the 100-MHz clock) halts this epoch too, so the grid always drains
+constexpr uint64_t kLaneWaitTicks = 100000000ull;
+__global__ void k_lane_wait(const uint32_t *word, uint32_t seq, Counters *ctr) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    uint32_t v;
+    while (((v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != (seq & 0x7FFFFFFFu)) {
+        if (wall_clock64() - t0 > kLaneWaitTicks) {
+            ctr->halt = 1u;
+            return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (v & 1u) ctr->halt = 1u;
+}
+
+void launch_lane_post(hipStream_t s, uint32_t *word, uint32_t seq, const Counters *ctr) {
+    DV_LAUNCH(k_lane_post, 1, 64, 0, s, word, seq, ctr);
+}
+
+void launch_lane_wait(hipStream_t s, const uint32_t *word, uint32_t seq, Counters *ctr) {
+    DV_LAUNCH(k_lane_wait, 1, 64, 0, s, word, seq, ctr);
 }
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,
@@ -1354,10 +1402,9 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
                                                      uint64_t *__restrict__ f0,
                                                      const uint64_t *__restrict__ pkey,
                                                      Counters *ctr, RowMap rm, uint8_t *__restrict__ commit_out,
-                                                     int pk_dense, uint64_t pk_base, ExecGate eg) {
+                                                     int pk_dense, uint64_t pk_base) {
     __shared__ unsigned long long part[3][4];
-    // rounds not finished (dv_epoch_finish resumes them), or the epoch before halted
-    if (exec_gate(ctr, eg)) return;
+    if (ctr->halt) return;  // rounds not finished (dv_epoch_finish resumes them)
     const bool rows = !input_err(ctr);  // a rejected epoch changes no row
     if (!(MODE & EX_COMMIT) && !rows) return;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1428,31 +1475,29 @@ __global__ __launch_bounds__(kBlock) void k_exec_txn(const uint32_t *__restrict_
     }
 }
 
-bool launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
+void launch_exec_txn(hipStream_t s, const uint32_t *tb_start, const uint32_t *tb_end,
                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, uint64_t *f0,
                      const uint64_t *pkey, bool fused, Counters *ctr, RowMap rm, uint8_t *d_commit,
-                     bool pk_dense, uint64_t pk_base, ExecGate eg) {
+                     bool pk_dense, uint64_t pk_base) {
     const int pkd = pk_dense && rm.P == 0 ? 1 : 0;  // (replicated epochs read the column)
-    if (n_txn == 0) return false;
+    if (n_txn == 0) return;
     uint32_t blocks = (n_txn + kBlock - 1) / kBlock;
     if (blocks > 4096) blocks = 4096;
     if (fused) {
         DV_LAUNCH((k_exec_txn<EX_READS | EX_WRITES | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn,
-                                                                              status, f0, pkey, ctr, rm, d_commit, pkd, pk_base, eg);
-    } else {  // (both gate words in the first launch)
+                                                                              status, f0, pkey, ctr, rm, d_commit, pkd, pk_base);
+    } else {
         DV_LAUNCH((k_exec_txn<EX_READS | EX_COMMIT>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                                   pkey, ctr, rm, d_commit, pkd, pk_base, eg);
+                                                                   pkey, ctr, rm, d_commit, pkd, pk_base);
         DV_LAUNCH((k_exec_txn<EX_WRITES>), blocks, kBlock, 0, s, tb_start, tb_end, acc_row, n_txn, status, f0,
-                                                        pkey, ctr, rm, nullptr, pkd, pk_base, ExecGate{});
+                                                        pkey, ctr, rm, nullptr, pkd, pk_base);
     }
-    return true;
 }
 
 __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict__ status, uint32_t n,
-                                                       uint8_t *__restrict__ out, Counters *ctr, ExecGate eg) {
+                                                       uint8_t *__restrict__ out, Counters *ctr) {
     __shared__ uint32_t part[4];
-    // the rounds resume first (dv_epoch_finish), or the epoch before halted
-    if (exec_gate(ctr, eg)) return;
+    if (ctr->halt) return;  // the rounds resume first (dv_epoch_finish)
     uint32_t cnt = commit_bytes_grid(status, n, out);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
@@ -1464,13 +1509,12 @@ __global__ __launch_bounds__(kBlock) void k_commit_out(const uint8_t *__restrict
     }
 }
 
-bool launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
-                       Counters *ctr, ExecGate eg) {
-    if (!n_txn) return false;
+void launch_commit_out(hipStream_t s, const uint8_t *status, uint32_t n_txn, uint8_t *d_commit,
+                       Counters *ctr) {
+    if (!n_txn) return;
     uint32_t blocks = (n_txn + kBlock * 16 - 1) / (kBlock * 16);
     if (blocks > 1024) blocks = 1024;
-    DV_LAUNCH(k_commit_out, blocks, kBlock, 0, s, status, n_txn, d_commit, ctr, eg);
-    return true;
+    DV_LAUNCH(k_commit_out, blocks, kBlock, 0, s, status, n_txn, d_commit, ctr);
 }
 
 // ------------------------------------------------------------- loaders

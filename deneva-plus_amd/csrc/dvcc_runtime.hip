@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <memory>
@@ -99,7 +100,7 @@ struct dv_ctx {
     // here); lanes_open counts the lanes of an owner (its tables are frozen)
     dv_ctx *table_owner = nullptr;
     uint32_t lanes_open = 0;
-    uint32_t *d_gate = nullptr;    // 2 words: this context's epochs' gate words (k_ctr_out)
+    uint32_t *d_gate = nullptr;    // 2 words: this context's epochs' lane posts (k_lane_post)
     hipEvent_t lane_ev = nullptr;  // recorded after this context's last queued execution
     // dv_epoch_run_device_lanes runs lane l of n on lane_stream, masked to
     // the CUs i with i % n == l: a lane's asynchronous round launch needs all
@@ -113,10 +114,8 @@ struct dv_ctx {
     std::shared_ptr<LaneOrder> order;
     uint64_t order_k = 0;  // executions of this lane so far
 
-    // TPC-C epoch (dv_tpcc_epoch_run_device): resolved copy of the epoch,
-    // execution scratch, and the operation words / o_id output of this epoch
-    uint64_t *tp_keys = nullptr;
-    uint8_t *tp_tables = nullptr;
+    // TPC-C epoch (dv_tpcc_epoch_run_device): execution scratch, and the
+    // operation words / o_id output of this epoch
     uint64_t *tp_dsnap = nullptr;  // per district row: D_NEXT_O_ID before the epoch
     uint64_t tp_dsnap_cap = 0;
     const uint64_t *tp_args = nullptr;
@@ -181,11 +180,8 @@ struct dv_ctx {
     };
     std::vector<EpochGraph> graphs;
     uint64_t graph_clock = 0, ws_gen = 0;
-    // dv_tpcc_epoch_begin: the last-name resolution, launched right after the clear
-    bool rsv_pending = false;
-    const uint64_t *rsv_keys = nullptr;
-    const uint8_t *rsv_tables = nullptr;
-    uint64_t rsv_n = 0;
+    // dv_tpcc_epoch_begin: the probe resolves the last-name accesses (k_probe<RSV>)
+    bool tp_resolve = false;
     uint32_t r0_n = 0;                    // round 0's live accesses (RoundBufs::n0)
     const uint32_t *r0_n_dev = nullptr;   // ... or their count on the device
     uint32_t n_txn_cap_pad = 0;
@@ -534,9 +530,9 @@ float elapsed(dv_ctx *c, int a, int b) {
 // host spins on (a blit plus a stream synchronisation cost ~25 us per epoch)
 // the counters into mirror slot k behind everything queued so far; returns
 // the sequence number mirror_wait waits for
-unsigned long long mirror_out(dv_ctx *c, int k, bool gate = false) {
+unsigned long long mirror_out(dv_ctx *c, int k) {
     const unsigned long long want = ++c->cseq;
-    launch_ctr_out(c->stream, c->ctr, c->d_mir[k], c->d_mseq[k], want, gate ? c->d_gate + k : nullptr);
+    launch_ctr_out(c->stream, c->ctr, c->d_mir[k], c->d_mseq[k], want);
     return want;
 }
 
@@ -681,7 +677,7 @@ void dv_close(dv_ctx *c) {
                     c->abounds, c->tword, c->carry_b, c->carry_tot,
                     c->status, c->verdict, c->ctr, c->d_acc, c->d_keys, c->d_types,
                     c->d_tables, c->d_commit, c->d_txn, c->d_grant, c->d_tb, c->split_err,
-                    c->d_args, c->d_oid, c->tp_keys, c->tp_tables, c->tp_dsnap,
+                    c->d_args, c->d_oid, c->tp_dsnap,
                     c->row_state, c->b_status, c->b_tlen, c->b_map, c->kinfo, c->ktsum, c->kill_bits, c->gc_tb, c->gc_tot,
                     c->hslot[0].acc, c->hslot[0].tb, c->hslot[1].acc, c->hslot[1].tb};
     for (void *b : bufs) dfree(b);
@@ -746,6 +742,7 @@ int dv_open(dv_ctx **out, const dv_config *cfg) {
     if (!r) r = dalloc(&c->d_gate, 2);
     if (!r) r = hip_fail(hipEventCreateWithFlags(&c->lane_ev, hipEventDisableTiming), "hipEventCreate");
     if (!r) r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)rnb * 8, c->stream), "memset");
+    if (!r) r = hip_fail(hipMemsetAsync(c->d_gate, 0, 2 * sizeof(uint32_t), c->stream), "memset");
     if (!r && cfg->cc_alg != DV_CALVIN) {
         r = dalloc(&c->rel[0], A);
         if (!r) r = dalloc(&c->rel[1], A);
@@ -1460,17 +1457,12 @@ int dv_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, uint32_t *d_grant) {
                        c->cfg.workload == DV_TPCC ? c->tp_oid : nullptr, graph_desc(c), graph_ndesc(c));
     graph_after_clear(c);
     c->ticket = 0;
-    if (c->rsv_pending) {  // (dv_tpcc_epoch_begin's last-name resolution)
-        c->rsv_pending = false;
-        launch_tpcc_resolve(c->stream, make_tables(c), c->rsv_keys, c->rsv_tables, c->rsv_n, c->f0, c->tp_keys,
-                            c->tp_tables, c->ctr);
-    }
     const bool fuse_hist = nblocks_for(ep->n_acc) >= kProbeHistTiles && !ep->n_acc_dev;
     launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc,
                  ep->n_txn, slog, c->pairs[0], c->tb_start, c->tb_end, calvin ? nullptr : c->tlen,
                  calvin ? nullptr : c->acc_row, c->ctr, fuse_hist ? c->counts : nullptr, ep->n_txn,
                  ktiming(c) ? c->ev[kEvProbe0] : nullptr, ktiming(c) ? c->ev[kEvProbe1] : nullptr, c->keys32,
-                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev);
+                 c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ep->n_acc_dev, c->tp_resolve ? c->f0 : nullptr);
     if (c->rep_P && !c->route) {  // replicated epoch: owners' key checks combined before anything depends on
         // them (epoch groups vote on every decider's outcome before anything executes)
         const int re = comm_combine_errors(c);
@@ -1634,10 +1626,8 @@ void exec_prologue(dv_ctx *c) {
                                 c->surv_words ? c->tword : nullptr);
 }
 
-// eg (decision lanes, run_lanes): the gate words of the previous epoch's
-// execution and of this one's; returns whether eg.out is written (false: the
-// caller's counter read-back writes it).  prologue_done: exec_prologue ran.
-bool enqueue_exec(dv_ctx *c, uint8_t *d_commit, ExecGate eg = ExecGate{}, bool prologue_done = false) {
+// prologue_done: exec_prologue ran (decision lanes)
+void enqueue_exec(dv_ctx *c, uint8_t *d_commit, bool prologue_done = false) {
     if (!prologue_done) exec_prologue(c);
     if (c->cfg.workload == DV_TPCC) {
         const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
@@ -1659,15 +1649,9 @@ bool enqueue_exec(dv_ctx *c, uint8_t *d_commit, ExecGate eg = ExecGate{}, bool p
         x.ctr = c->ctr;
         x.n_txn = c->n_txn;
         x.commit_out = d_commit;
-        x.gate = eg;
-        if (launch_tpcc_exec(c->stream, x)) return true;  // (the commit bytes too)
-        if (eg.prev) launch_lane_gate(c->stream, eg.prev, c->ctr);
-        return false;
-    }
-    // (launches that read no gate word: the gate's own launch first)
-    const bool txn_exec = !c->route && c->cfg.cc_alg != DV_CALVIN;
-    if (eg.prev && !txn_exec) launch_lane_gate(c->stream, eg.prev, c->ctr);
-    if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
+        launch_tpcc_exec(c->stream, x);  // (the commit bytes too)
+        return;
+    } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
         if (c->cfg.cc_alg == DV_CALVIN)
             launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);
         else
@@ -1685,16 +1669,13 @@ bool enqueue_exec(dv_ctx *c, uint8_t *d_commit, ExecGate eg = ExecGate{}, bool p
             // (its dense test; only with table 0 the context's one table -- a
             // row of another table takes its key from the pkey column)
             const KillKeys dk = kill_keys(make_tables(c), nullptr, nullptr, nullptr);
-            if (launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
-                                c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit,
-                                dk.tabs.n == 1 && dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep,
-                                dk.dense_base, eg))
-                return true;
-            if (eg.prev) launch_lane_gate(c->stream, eg.prev, c->ctr);  // (nothing launched)
-            return false;
+            launch_exec_txn(c->stream, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->f0, c->pkey,
+                            c->cfg.cc_alg != DV_OCC, c->ctr, rm, d_commit,
+                            dk.tabs.n == 1 && dk.dense_lim != 0 && dk.tabs.t[0].rep_part == kNoRep, dk.dense_base);
+            return;
         }
     }
-    return launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr, ExecGate{nullptr, eg.out});
+    launch_commit_out(c->stream, c->status, c->n_txn, d_commit, c->ctr);
 }
 }  // namespace
 
@@ -2627,9 +2608,9 @@ struct OnLaneStreams {
 
 // Decision lanes: epoch k is decided on lanes[k % n_lanes] (each lane its own
 // stream and workspace), so one lane's rounds overlap another's; executions
-// stay in epoch order -- epoch k's waits for epoch k-1's (an event across the
-// lanes' streams) and starts halted when k-1 halted or failed (its gate word,
-// k_ctr_out / k_lane_gate).  The host reads epochs back oldest first; a halted
+// stay in epoch order -- epoch k's waits for epoch k-1's post (k_lane_wait /
+// k_lane_post: a device word, not an event across the lanes' streams) and
+// starts halted when k-1 halted or failed.  The host reads epochs back oldest first; a halted
 // one is run again with every epoch queued behind it, synchronously and in
 // order, as run_batch does on one stream.  pipelined(k): epoch k can be
 // queued that way; decide(c, k): queues its decision on lane c (up to the
@@ -2651,13 +2632,17 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         EpochSnap sn;
     };
     // queued and unread epochs, oldest first; each lane holds at most two
-    // (its two mirror slots and gate words)
+    // (its two mirror slots and post words)
     const uint32_t window = 2 * n_lanes - 1;
     Pend ring[2 * kMaxLanes];
     uint32_t head = 0, count = 0;
     uint32_t lane_slot[kMaxLanes] = {};
     dv_ctx *prev = nullptr;  // the lane of the last queued epoch (nullptr: nothing queued is unfinished)
     int prev_slot = 0;
+    // post sequences: unique across calls (a stale post never matches)
+    static std::atomic<uint32_t> g_lane_seq{0};
+    const uint32_t seq0 = g_lane_seq.fetch_add(n + 1);
+    uint32_t prev_seq = 0;
     auto drain = [&] {
         for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
     };
@@ -2721,19 +2706,18 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         const auto td = hclock::now();
         int r = decide(c, k);
         t_decide += std::chrono::duration<double>(hclock::now() - td).count();
+        // the epoch order of the executions, on the device: wait for the
+        // previous epoch's post (its gate halts this one), execute (and
+        // refill), post -- the counter read-back after it, off that chain
         if (!r) exec_prologue(c);
-        if (!r && prev) r = hip_fail(hipStreamWaitEvent(c->stream, prev->lane_ev, 0), "hipStreamWaitEvent");
-        // the execution reads the previous epoch's gate word and writes this
-        // one's, so the event follows it (and the refill) directly; the
-        // counter read-back is off the lanes' chain of executions
-        bool gated = false;
+        if (!r && prev) launch_lane_wait(c->stream, prev->d_gate + prev_slot, prev_seq, c->ctr);
         if (!r) {
-            gated = enqueue_exec(c, commit_of(k), ExecGate{prev ? prev->d_gate + prev_slot : nullptr, c->d_gate + slot},
-                                 true);
+            enqueue_exec(c, commit_of(k), true);
             r = hip_fail(hipGetLastError(), "execution launch");
         }
         if (!r) r = after(c, k);
-        if (!r && gated) r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
+        const uint32_t seq = seq0 + k + 1;
+        if (!r) launch_lane_post(c->stream, c->d_gate + slot, seq, c->ctr);
         if (!r) {
             EpochSnap &sn = p.sn;
             sn.n_acc = c->n_acc;
@@ -2747,8 +2731,8 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
             sn.n_acc_is_bound = c->n_acc_is_bound;
             sn.async_unconfirmed = c->async_unconfirmed;
             sn.slot = slot;
-            sn.seq = mirror_out(c, slot, !gated);
-            if (!gated) r = hip_fail(hipEventRecord(c->lane_ev, c->stream), "hipEventRecord");
+            sn.seq = mirror_out(c, slot);
+            r = hip_fail(hipGetLastError(), "lane post");
         }
         c->phase = 0;
         c->prefix_mode = false;
@@ -2766,6 +2750,7 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         count++;
         prev = c;
         prev_slot = slot;
+        prev_seq = seq;
         t_queue += std::chrono::duration<double>(hclock::now() - tq).count();
     }
     const auto tw = hclock::now();
@@ -3125,14 +3110,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
     if (!c || !ep || (ep->n_acc && (!d_args || !ep->tables)) || c->cfg.workload != DV_TPCC) return DV_ERR_ARG;
     if (ep->n_acc > c->cfg.max_acc || ep->n_txn > c->cfg.max_txn) return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
-    const uint64_t A = c->cfg.max_acc;
     int r = DV_OK;
-    if (!c->tp_keys) {
-        c->ws_gen++;
-        r = dalloc(&c->tp_keys, A);
-        if (!r) r = dalloc(&c->tp_tables, A);
-        if (r) return r;
-    }
     const HostTable &dt = c->tab[DV_TPCC_DISTRICT];
     const uint64_t drows = dt.created ? dt.cap_rows : 1;
     if (c->tp_dsnap_cap < drows) {
@@ -3143,22 +3121,15 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
         if (r) return r;
         c->tp_dsnap_cap = drows;
     }
-    // no host wait: a last name without customers resolves to key ~0, which
-    // the probe of dv_epoch_begin then reports as DV_ERR_KEY_NOT_FOUND; the
-    // resolution is launched by dv_epoch_begin right after the epoch's clear
-    // (everything after the clear is the part an epoch graph replays)
-    c->rsv_pending = true;
-    c->rsv_keys = ep->keys;
-    c->rsv_tables = ep->tables;
-    c->rsv_n = ep->n_acc;
-    dv_epoch_dev e = *ep;
-    e.keys = c->tp_keys;
-    e.tables = c->tp_tables;
+    // no host wait: the probe of dv_epoch_begin resolves the last names in
+    // place, and one without customers resolves to key ~0, which it then
+    // reports as DV_ERR_KEY_NOT_FOUND
     static const uint64_t kNoArgs = 0;
     c->tp_args = d_args ? d_args : &kNoArgs;  // an empty partition still finishes
     c->tp_oid = d_oid;
-    r = dv_epoch_begin(c, &e, nullptr);
-    c->rsv_pending = false;
+    c->tp_resolve = true;
+    r = dv_epoch_begin(c, ep, nullptr);
+    c->tp_resolve = false;
     if (r) c->tp_args = c->tp_oid = nullptr;
     return r;
 }

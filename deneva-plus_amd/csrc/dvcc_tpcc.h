@@ -4,9 +4,6 @@
 
 namespace dvcc {
 
-// customer-by-last-name accesses -> CUSTOMER/custKey; every other access copied
-void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *tables,
-                         uint64_t n, const uint64_t *cols, uint64_t *okeys, uint8_t *otables, Counters *ctr);
 
 struct TpccExec {
     const uint64_t *pairs;     // row-sorted pairs of the epoch
@@ -26,11 +23,40 @@ struct TpccExec {
     Counters *ctr;
     uint32_t n_txn;            // the commit bytes of every txn (and the committed count) ...
     uint8_t *commit_out;       // ... written by the update pass (may be null: the count only)
-    ExecGate gate;             // decision lanes: read by the first launch, written by the last
 };
 // updates (+ D_NEXT_O_ID snapshots) and the commit bytes, then -- CALVIN,
 // several committed NewOrders per district -- the o_id numbering
 constexpr uint32_t kTpccCols = 3;
-bool launch_tpcc_exec(hipStream_t s, const TpccExec &x);
+
+// A customer-by-last-name access (payment / order-status by last name,
+// tpcc_txn.cpp:600-626): the customer it names is the middle one of the
+// name's entries in i_customer_last (t: the CUST_LAST table; equal keys are
+// contiguous in a chained bucket, the floor(cnt/2)-th is taken) -- its
+// custKey, column 0 of that CUST_LAST row -- or key ~0 when the name has no
+// customer (the probe then reports DV_ERR_KEY_NOT_FOUND).  The probe resolves
+// these in place (k_probe<HIST, true>), so the access is a CUSTOMER access
+// from there on.
+__device__ inline uint64_t tpcc_last_name_key(const TableDesc &t, const uint64_t *__restrict__ cols, uint64_t key) {
+    uint32_t tag;
+    const uint64_t bk = key_split(t, key, tag);
+    uint64_t row = ~0ull;
+    if (t.pkey != nullptr) {
+        if (direct_holds(t, bk, tag, key)) row = bk;
+    } else if (t.bstart == nullptr) {
+        if (t.ix[bk].key == key) row = t.ix[bk].row;
+    } else {
+        const uint32_t lo = t.bstart[bk], hi = t.bstart[bk + 1];
+        uint32_t cnt = 0, first = hi;
+        for (uint32_t j = lo; j < hi; j++) {
+            if (t.ix[j].key == key) {
+                if (first == hi) first = j;
+                cnt++;
+            }
+        }
+        if (cnt) row = t.ix[first + cnt / 2].row;
+    }
+    return row == ~0ull ? ~0ull : cols[(t.row_base + row) * kTpccCols];
+}
+void launch_tpcc_exec(hipStream_t s, const TpccExec &x);
 
 }  // namespace dvcc

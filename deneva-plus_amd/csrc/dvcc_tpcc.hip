@@ -2,7 +2,7 @@
 //
 // Two pieces around the generic probe -> sort -> decide pipeline:
 //
-// k_tpcc_resolve   Payment's customer-by-last-name lookup (run_payment_4,
+// last names       Payment's customer-by-last-name lookup (run_payment_4,
 //                  tpcc_txn.cpp:600-626): index_read on i_customer_last
 //                  returns the item list of the key, newest insert first
 //                  (BucketHeader::insert_item prepends, index_hash.cpp:
@@ -11,8 +11,9 @@
 //                  equal keys grouped newest first (dv_load_table), so the
 //                  lookup counts the key's entries and takes the middle one;
 //                  its payload (col 0) is the customer's primary key.  The
-//                  access is rewritten to CUSTOMER/custKey in the engine's
-//                  scratch copy of the epoch.
+//                  probe does this in place (tpcc_last_name_key, dvcc_tpcc.h)
+//                  and probes CUSTOMER/custKey: no launch or scratch copy of
+//                  the epoch of its own.
 //
 // execution        run_payment_1/3/5 and new_order_5/9 (tpcc_txn.cpp:530-933)
 //                  for committed txns, over the row-sorted pairs so that every
@@ -49,45 +50,6 @@ namespace {
 constexpr uint64_t kOpMask = (1ull << 56) - 1;
 
 
-__global__ __launch_bounds__(kBlock) void k_tpcc_resolve(Tables tabs, const uint64_t *__restrict__ keys,
-                                                         const uint8_t *__restrict__ tables, uint64_t n,
-                                                         const uint64_t *__restrict__ cols,
-                                                         uint64_t *__restrict__ okeys,
-                                                         uint8_t *__restrict__ otables) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        uint64_t key = keys[i];
-        uint8_t tb = tables[i];
-        if (tb == DV_TPCC_CUST_LAST) {
-            if (tb < tabs.n) {  // else the probe reports the missing table
-                const TableDesc &t = tabs.t[tb];
-                uint32_t tag;
-                const uint64_t bk = key_split(t, key, tag);
-                uint64_t row = ~0ull;
-                if (t.pkey != nullptr) {
-                    if (direct_holds(t, bk, tag, key)) row = bk;
-                } else if (t.bstart == nullptr) {
-                    if (t.ix[bk].key == key) row = t.ix[bk].row;
-                } else {
-                    const uint32_t lo = t.bstart[bk], hi = t.bstart[bk + 1];
-                    uint32_t cnt = 0, first = hi;
-                    for (uint32_t j = lo; j < hi; j++) {
-                        if (t.ix[j].key == key) {
-                            if (first == hi) first = j;
-                            cnt++;
-                        }
-                    }
-                    // equal keys are contiguous: the floor(cnt/2)-th of the list
-                    if (cnt) row = t.ix[first + cnt / 2].row;
-                }
-                // no customer of that name: key ~0 misses in the probe (DV_ERR_KEY_NOT_FOUND)
-                key = row == ~0ull ? ~0ull : cols[(t.row_base + row) * kTpccCols];
-                tb = DV_TPCC_CUSTOMER;
-            }
-        }
-        okeys[i] = key;
-        otables[i] = tb;
-    }
-}
 
 // pass 1: additive updates, stock queues, D_NEXT_O_ID snapshots at the
 // district queue heads.
@@ -103,8 +65,8 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_apply(const uint64_t *__restric
                                                        int oid_direct, uint64_t *__restrict__ oid,
                                                        uint64_t *__restrict__ dsnap, uint64_t dist_base,
                                                        uint64_t dist_rows, Counters *ctr, uint32_t n_txn,
-                                                       uint8_t *__restrict__ commit_out, ExecGate eg) {
-    if (exec_gate(ctr, eg)) return;  // rounds not finished, or the epoch before halted
+                                                       uint8_t *__restrict__ commit_out) {
+    if (ctr->halt) return;  // rounds not finished
     const uint32_t lane = threadIdx.x & 63;
     {  // the commit bytes and the committed count (k_commit_out's work, one launch fewer)
         uint32_t cc = commit_bytes_grid(status, n_txn, commit_out);
@@ -208,14 +170,12 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
                                                      const uint64_t *__restrict__ dsnap, uint64_t dist_base,
                                                      uint64_t dist_rows, uint64_t *__restrict__ cols,
                                                      uint64_t *__restrict__ oid, uint64_t *desc,
-                                                     uint32_t *tile_ctr, uint32_t tag, Counters *ctr,
-                                                     uint32_t *gate_out) {
+                                                     uint32_t *tile_ctr, uint32_t tag, Counters *ctr) {
     __shared__ uint64_t s_el[kRTile + kRTile / kRIPT];
     __shared__ uint64_t s_next, s_prev;
     __shared__ uint32_t s_tile;
     __shared__ Agg wt[4];
     __shared__ Agg s_pre;
-    // (k_tpcc_apply read the gate word of the epoch before and wrote this one's)
     const uint32_t ntiles = (n + kRTile - 1) / kRTile;
     if (blockIdx.x >= ntiles || input_err(ctr) || ctr->halt) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -273,10 +233,6 @@ __global__ __launch_bounds__(kBlock) void k_tpcc_oid(const uint64_t *__restrict_
         for (int w = 1; w < 4; w++) bagg = OpSeg::comb(bagg, wt[w]);
         const Agg pre = look_back<OpSeg>(desc, tile, tag, bagg, lane, ctr);
         if (lane == 0) s_pre = pre;
-        // a look-back that gave up (ERRB_SPIN) fails the epoch: the gate word
-        // k_tpcc_apply wrote becomes 1 (no other write to it is in flight)
-        if (gate_out && lane == 0 && __hip_atomic_load(&ctr->err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-            *gate_out = 1u;
     }
     __syncthreads();
     Agg run = s_pre;
@@ -305,26 +261,18 @@ uint32_t grid_for(uint64_t n) {
 
 }  // namespace
 
-void launch_tpcc_resolve(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *tables,
-                         uint64_t n, const uint64_t *cols, uint64_t *okeys, uint8_t *otables, Counters *ctr) {
-    if (n == 0) return;
-    (void)ctr;
-    DV_LAUNCH(k_tpcc_resolve, grid_for(n), kBlock, 0, s, tabs, keys, tables, n, cols, okeys, otables);
-}
-
-bool launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
-    if (x.n == 0)  // (no access to update: the commit bytes alone)
-        return launch_commit_out(s, x.status, x.n_txn, x.commit_out, x.ctr, x.gate);
+void launch_tpcc_exec(hipStream_t s, const TpccExec &x) {
+    if (x.n == 0) {  // (no access to update: the commit bytes alone)
+        launch_commit_out(s, x.status, x.n_txn, x.commit_out, x.ctr);
+        return;
+    }
     const uint64_t g = std::max<uint64_t>(x.n, (x.n_txn + 15u) / 16u);
     DV_LAUNCH(k_tpcc_apply, grid_for(g), kBlock, 0, s, x.pairs, x.n, x.status, x.tb_start, x.args, x.cols,
-              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr, x.n_txn, x.commit_out,
-              x.gate);
-    if (x.oid_direct) return true;
+              x.oid_direct ? 1 : 0, x.oid, x.dsnap, x.dist_base, x.dist_rows, x.ctr, x.n_txn, x.commit_out);
+    if (x.oid_direct) return;
     const uint32_t ntiles = (uint32_t)((x.n + kRTile - 1) / kRTile);
     DV_LAUNCH(k_tpcc_oid, ntiles, kBlock, 0, s, x.pairs, (uint32_t)x.n, x.status, x.tb_start, x.args, x.dsnap,
-                                         x.dist_base, x.dist_rows, x.cols, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr,
-                                         x.gate.out);
-    return true;
+                                         x.dist_base, x.dist_rows, x.cols, x.oid, x.desc, x.tile_ctr, x.tag, x.ctr);
 }
 
 }  // namespace dvcc
