@@ -622,11 +622,12 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
 // pointers of host-mapped memory)
 void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned long long *hseq,
                     unsigned long long seq);
-// decision lanes (dv_epoch_run_device_lanes): after an epoch's execution,
-// *word = seq << 1 | (it halted or failed); before the next one's, wait for
-// that seq and halt if the bit is set (or after 1 s without it)
-void launch_lane_post(hipStream_t s, uint32_t *word, uint32_t seq, const Counters *ctr);
-void launch_lane_wait(hipStream_t s, const uint32_t *word, uint32_t seq, Counters *ctr);
+// decision lanes (dv_epoch_run_device_lanes): before an epoch's execution,
+// wait until *done >> 1 reaches this lane's *turn (halt if the gate bit is
+// set, or after 1 s without it); after it, *done = (turn + 1) << 1 | (it
+// halted or failed) and *turn += n_lanes
+void launch_lane_post(hipStream_t s, uint32_t *turn, uint32_t *done, uint32_t n_lanes, const Counters *ctr);
+void launch_lane_wait(hipStream_t s, const uint32_t *turn, const uint32_t *done, Counters *ctr);
 // Calvin: in row order over the sorted queues
 void launch_exec(hipStream_t s, const uint64_t *pairs, const uint64_t *el, const uint8_t *ew,
                  uint64_t n, const uint8_t *status, uint64_t *f0, const uint64_t *pkey,

@@ -1258,30 +1258,37 @@ void launch_ctr_out(hipStream_t s, const Counters *ctr, Counters *hctr, unsigned
     DV_LAUNCH(k_ctr_out, 1, kBlock, 0, s, ctr, hctr, hseq, seq);
 }
 
-// Decision lanes' execution order (run_lanes), kept on the device: after an
-// epoch's execution its lane posts one word, (sequence << 1) | gate -- the
-// gate set when the epoch halted or failed -- and the lane of the next epoch
-// waits for that sequence before its execution, which starts halted when the
-// gate is set (nothing of it executes; the host runs both again, in order).
-// A kernel boundary on either side orders the rows: the execution's writes
-// are released before the post, the next execution starts after the wait.
-// (An event recorded on one lane's stream and waited for on the next cost
-// the host 13-15 us per graph launch behind it instead of 3-4: the TPC-C
-// window was host-bound at 0.058 ms per epoch.)
-__global__ void k_lane_post(uint32_t *word, uint32_t seq, const Counters *__restrict__ ctr) {
+// Decision lanes' execution order (run_lanes), kept on the device in words
+// that stay the same from epoch to epoch, so an epoch's execution can be part
+// of its replayed graph: each lane holds its next turn in the chain of
+// executions (*turn), the lanes share one word *done = (turns executed << 1)
+// | gate, the gate set when the last one halted or failed.  An execution
+// waits until *done reaches its turn and starts halted when the gate is set
+// (nothing of it executes; the host runs both again, in order); after it,
+// its lane posts turn + 1 with its own gate and advances its turn by the
+// lane count.  The host sets the words while the lanes are idle (run_lanes,
+// at the start of every run of pipelined epochs).  Kernel boundaries on
+// either side order the rows: the execution's writes are released before the
+// post, the next execution starts after the wait.  (An event recorded on one
+// lane's stream and waited for on the next cost the host 13-15 us per graph
+// launch behind it instead of 3-4.)
+__global__ void k_lane_post(uint32_t *turn, uint32_t *done, uint32_t n_lanes, const Counters *__restrict__ ctr) {
     if (threadIdx.x != 0) return;
+    const uint32_t t = *turn;
     const uint32_t gate = (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
-    __hip_atomic_store(word, (seq << 1) | gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(done, ((t + 1u) << 1) | gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *turn = t + n_lanes;
 }
 
 // the wait is bounded: a predecessor that has not posted after kLaneWaitTicks
 // (1 s of the 100-MHz clock) halts this epoch too, so the grid always drains
 constexpr uint64_t kLaneWaitTicks = 100000000ull;
-__global__ void k_lane_wait(const uint32_t *word, uint32_t seq, Counters *ctr) {
+__global__ void k_lane_wait(const uint32_t *turn, const uint32_t *done, Counters *ctr) {
     if (threadIdx.x != 0) return;
+    const uint32_t t = *turn & 0x7FFFFFFFu;
     const uint64_t t0 = wall_clock64();
     uint32_t v;
-    while (((v = __hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != (seq & 0x7FFFFFFFu)) {
+    while (((v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != t) {
         if (wall_clock64() - t0 > kLaneWaitTicks) {
             ctr->halt = 1u;
             return;
@@ -1291,12 +1298,12 @@ __global__ void k_lane_wait(const uint32_t *word, uint32_t seq, Counters *ctr) {
     if (v & 1u) ctr->halt = 1u;
 }
 
-void launch_lane_post(hipStream_t s, uint32_t *word, uint32_t seq, const Counters *ctr) {
-    DV_LAUNCH(k_lane_post, 1, 64, 0, s, word, seq, ctr);
+void launch_lane_post(hipStream_t s, uint32_t *turn, uint32_t *done, uint32_t n_lanes, const Counters *ctr) {
+    DV_LAUNCH(k_lane_post, 1, 64, 0, s, turn, done, n_lanes, ctr);
 }
 
-void launch_lane_wait(hipStream_t s, const uint32_t *word, uint32_t seq, Counters *ctr) {
-    DV_LAUNCH(k_lane_wait, 1, 64, 0, s, word, seq, ctr);
+void launch_lane_wait(hipStream_t s, const uint32_t *turn, const uint32_t *done, Counters *ctr) {
+    DV_LAUNCH(k_lane_wait, 1, 64, 0, s, turn, done, ctr);
 }
 
 void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t n_txn_pad4, uint8_t value,

@@ -173,7 +173,7 @@ struct dv_ctx {
     // knobs) and replayed; ws_gen counts the workspace reallocations that
     // would invalidate a captured graph's pointers
     struct EpochGraph {
-        uint64_t key[18] = {};
+        uint64_t key[22] = {};
         hipGraphExec_t exec = nullptr;
         uint32_t seen = 0;
         uint64_t used = 0;
@@ -1304,22 +1304,27 @@ void graph_after_clear(dv_ctx *c) {
 }
 
 // decide(): an epoch's queueing from its epoch_setup through its decision
-// (the clear first); ep / args name its buffers.
+// (the clear first) -- and, under decision lanes, its execution (run_lanes'
+// tail); ep / args name its buffers, xk whatever else the launches' arguments
+// hold (the tail's commit / o_id outputs and ordering words)
+struct GraphKeyX {
+    uint64_t w[4] = {0, 0, 0, 0};
+};
 template <class F>
-int graph_decide(dv_ctx *c, const dv_epoch_dev *ep, const void *args, F &&decide) {
+int graph_decide(dv_ctx *c, const dv_epoch_dev *ep, const void *args, F &&decide, const GraphKeyX &xk = {}) {
     static const bool off = std::getenv("DVCC_NO_GRAPHS") != nullptr;
     if (off || timing(c) || ktiming(c) || (c->cfg.flags & DV_FLAG_KERNEL_PROFILE) || tl_kprof || c->comm ||
         c->rep_P || c->route || tl_graph)
         return decide();
-    const uint64_t key[18] = {(uint64_t)ep->keys, (uint64_t)ep->types, (uint64_t)ep->acc_txn, (uint64_t)ep->tables,
+    const uint64_t key[22] = {(uint64_t)ep->keys, (uint64_t)ep->types, (uint64_t)ep->acc_txn, (uint64_t)ep->tables,
                               (uint64_t)ep->txn_begin, (uint64_t)ep->recs32, (uint64_t)ep->ts,
                               (uint64_t)ep->n_acc_dev, ep->n_acc, ep->n_txn | (uint64_t)ep->max_txn_acc << 32,
                               (uint64_t)args, c->async_g | (uint64_t)c->async_max_iters << 32, c->async_idle_ticks,
                               c->cfg.flags | (uint64_t)c->prefix_txns << 32, c->ws_gen, (uint64_t)c->keys32,
-                              (uint64_t)c->stream, (uint64_t)c->cfg.max_acc};
+                              (uint64_t)c->stream, (uint64_t)c->cfg.max_acc, xk.w[0], xk.w[1], xk.w[2], xk.w[3]};
     dv_ctx::EpochGraph *e = nullptr;
     for (auto &g : c->graphs)
-        if (std::equal(key, key + 18, g.key)) e = &g;
+        if (std::equal(key, key + 22, g.key)) e = &g;
     if (!e) {
         if (c->graphs.size() >= kMaxGraphs) {  // (the least recently used goes)
             auto lru = std::min_element(c->graphs.begin(), c->graphs.end(),
@@ -1333,7 +1338,7 @@ int graph_decide(dv_ctx *c, const dv_epoch_dev *ep, const void *args, F &&decide
             c->graphs.emplace_back();
             e = &c->graphs.back();
         }
-        std::copy(key, key + 18, e->key);
+        std::copy(key, key + 22, e->key);
     }
     e->used = ++c->graph_clock;
     if (e->seen != kGraphNever) e->seen++;
@@ -2613,11 +2618,24 @@ struct OnLaneStreams {
 // starts halted when k-1 halted or failed.  The host reads epochs back oldest first; a halted
 // one is run again with every epoch queued behind it, synchronously and in
 // order, as run_batch does on one stream.  pipelined(k): epoch k can be
-// queued that way; decide(c, k): queues its decision on lane c (up to the
-// execution); after(c, k): queues what follows the execution on the lane (a
+// queued that way; decide(c, k, tail): queues its decision on lane c, then
+// tail() -- the execution in epoch order -- inside the epoch's graph when it
+// replays one (graph_decide with lanes_key); after(c, k): queues what follows the execution on the lane (a
 // closed loop's refill; it runs before the next epoch's execution, on any
 // lane, is queued, and is a no-op when the epoch halted); run(k, st): runs
 // it synchronously on its lane.
+// the graph key words of a lanes epoch's execution (run_lanes' tail): its
+// outputs and the lanes' shared order word (lanes[0]'s); the lane's own turn
+// word is its context's
+GraphKeyX lanes_key(dv_ctx *const *lanes, uint32_t n_lanes, const void *commit, const void *oid) {
+    GraphKeyX x;
+    x.w[0] = (uint64_t)commit;
+    x.w[1] = (uint64_t)oid;
+    x.w[2] = (uint64_t)lanes[0];
+    x.w[3] = n_lanes | 1ull << 32;
+    return x;
+}
+
 template <class Commit, class Pipelined, class Decide, class After, class Run>
 int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts, Commit &&commit_of,
               Pipelined &&pipelined, Decide &&decide, After &&after, Run &&run) {
@@ -2632,17 +2650,26 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         EpochSnap sn;
     };
     // queued and unread epochs, oldest first; each lane holds at most two
-    // (its two mirror slots and post words)
+    // (its two mirror slots)
     const uint32_t window = 2 * n_lanes - 1;
     Pend ring[2 * kMaxLanes];
     uint32_t head = 0, count = 0;
     uint32_t lane_slot[kMaxLanes] = {};
     dv_ctx *prev = nullptr;  // the lane of the last queued epoch (nullptr: nothing queued is unfinished)
-    int prev_slot = 0;
-    // post sequences: unique across calls (a stale post never matches)
-    static std::atomic<uint32_t> g_lane_seq{0};
-    const uint32_t seq0 = g_lane_seq.fetch_add(n + 1);
-    uint32_t prev_seq = 0;
+    // the executions' order words (k_lane_wait / k_lane_post): each lane's
+    // turn (its d_gate[0]) and the shared count of executed turns (lanes[0]'s
+    // d_gate[1]), set while every lane is idle -- at the start and after a
+    // synchronous run -- the turns counting from the next epoch's lane
+    uint32_t *const done_w = lanes[0]->d_gate + 1;
+    auto order_init = [&](uint32_t k0) -> int {
+        uint32_t turn[kMaxLanes];
+        for (uint32_t i = 0; i < n_lanes; i++) turn[(k0 + i) % n_lanes] = i;
+        hipStream_t s0 = lanes[0]->stream;
+        for (uint32_t l = 0; l < n_lanes; l++)
+            HIPCHK(hipMemcpyAsync(lanes[l]->d_gate, &turn[l], sizeof(uint32_t), hipMemcpyHostToDevice, s0));
+        HIPCHK(hipMemsetAsync(done_w, 0, sizeof(uint32_t), s0));
+        return hip_fail(hipStreamSynchronize(s0), "lane order words");
+    };
     auto drain = [&] {
         for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
     };
@@ -2680,6 +2707,10 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     };
     for (uint32_t k = 0; k < n; k++) {
         dv_ctx *c = lane_of(k);
+        if (!prev && pipelined(k)) {  // (every lane idle: nothing queued is unfinished)
+            const int r = order_init(k);
+            if (r) return r;
+        }
         if (!pipelined(k)) {
             while (count) {
                 const int r = settle();
@@ -2703,21 +2734,22 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         const int slot = (int)(lane_slot[l]++ & 1u);
         Pend &p = ring[(head + count) % (2 * kMaxLanes)];
         p.k = k;
-        const auto td = hclock::now();
-        int r = decide(c, k);
-        t_decide += std::chrono::duration<double>(hclock::now() - td).count();
-        // the epoch order of the executions, on the device: wait for the
-        // previous epoch's post (its gate halts this one), execute (and
-        // refill), post -- the counter read-back after it, off that chain
-        if (!r) exec_prologue(c);
-        if (!r && prev) launch_lane_wait(c->stream, prev->d_gate + prev_slot, prev_seq, c->ctr);
-        if (!r) {
+        // the execution in epoch order, on the device: wait for the previous
+        // epoch's post (its gate halts this one), execute (and refill), post
+        // -- queued by decide() behind the decision, inside its graph when it
+        // replays one; the counter read-back after it, off that chain
+        auto tail = [&]() -> int {
+            exec_prologue(c);
+            launch_lane_wait(c->stream, c->d_gate, done_w, c->ctr);
             enqueue_exec(c, commit_of(k), true);
-            r = hip_fail(hipGetLastError(), "execution launch");
-        }
-        if (!r) r = after(c, k);
-        const uint32_t seq = seq0 + k + 1;
-        if (!r) launch_lane_post(c->stream, c->d_gate + slot, seq, c->ctr);
+            int rt = hip_fail(hipGetLastError(), "execution launch");
+            if (!rt) rt = after(c, k);
+            if (!rt) launch_lane_post(c->stream, c->d_gate, done_w, n_lanes, c->ctr);
+            return rt;
+        };
+        const auto td = hclock::now();
+        int r = decide(c, k, tail);
+        t_decide += std::chrono::duration<double>(hclock::now() - td).count();
         if (!r) {
             EpochSnap &sn = p.sn;
             sn.n_acc = c->n_acc;
@@ -2749,8 +2781,6 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         }
         count++;
         prev = c;
-        prev_slot = slot;
-        prev_seq = seq;
         t_queue += std::chrono::duration<double>(hclock::now() - tq).count();
     }
     const auto tw = hclock::now();
@@ -2789,9 +2819,18 @@ int dv_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const dv_e
             return (prefix_applies(c, &eps[k]) || small_pipelined(c, &eps[k])) && !timing(c) && !ktiming(c) &&
                    !c->rep_P && !c->comm;
         },
-        [&](dv_ctx *c, uint32_t k) {
-            if (prefix_applies(c, &eps[k])) return run_prefix_epoch(c, &eps[k]);
-            return graph_decide(c, &eps[k], nullptr, [&] { return small_enqueue(c, &eps[k]); });
+        [&](dv_ctx *c, uint32_t k, auto &tail) {
+            if (prefix_applies(c, &eps[k])) {
+                const int r = run_prefix_epoch(c, &eps[k]);
+                return r ? r : tail();
+            }
+            return graph_decide(
+                c, &eps[k], nullptr,
+                [&] {
+                    const int r = small_enqueue(c, &eps[k]);
+                    return r ? r : tail();
+                },
+                lanes_key(lanes, n_lanes, commit_of(k), nullptr));
         },
         [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
@@ -2851,12 +2890,15 @@ int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
             dv_ctx *c = lanes[k % n_lanes];
             return !timing(c) && !ktiming(c) && !c->comm;
         },
-        [&](dv_ctx *c, uint32_t k) {
-            return graph_decide(c, &eps[k], d_args[k], [&] {
-                int rr = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
-                if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
-                return rr;
-            });
+        [&](dv_ctx *c, uint32_t k, auto &tail) {
+            return graph_decide(
+                c, &eps[k], d_args[k],
+                [&] {
+                    int rr = dv_tpcc_epoch_begin(c, &eps[k], d_args[k], oid_of(k));
+                    if (!rr && c->cfg.cc_alg != DV_CALVIN && c->n_txn) rr = decide_epoch(c);
+                    return rr ? rr : tail();
+                },
+                lanes_key(lanes, n_lanes, commit_of(k), oid_of(k)));
         },
         [](dv_ctx *, uint32_t) { return 0; },
         [&](uint32_t k, dv_stats *st) {
@@ -3051,9 +3093,10 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
     const bool pipelined = prefix_applies(c0, &d0) && !timing(c0) && !ktiming(c0);
     r = run_lanes(
         lanes, n_lanes, n_epochs, sts, commit_of, [&](uint32_t) { return pipelined; },
-        [&](dv_ctx *c, uint32_t k) {
+        [&](dv_ctx *c, uint32_t k, auto &tail) {
             const dv_epoch_dev d = desc(k);
-            return run_prefix_epoch(c, &d);
+            const int e = run_prefix_epoch(c, &d);
+            return e ? e : tail();
         },
         [&](dv_ctx *c, uint32_t k) {  // (behind the execution; a no-op when k halted)
             const dv_epoch_dev d = desc(k);
