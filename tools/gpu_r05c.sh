@@ -1,17 +1,14 @@
-# TPC-C legs and the headline, host profile (one box)
+# epoch groups over ordered lanes at one rank (--part1): event order vs the order dropped (experiment: timing only)
 set -e
 export PYTHONUNBUFFERED=1
-T=${1:-r05_z}
+T=${1:-r05_ab}
 O=gpurun_out/$T
 mkdir -p $O
 for rep in 1 2; do
-  DVCC_HOST_PROF=1 timeout -k 10 300 python -u bench.py --tpcc-only --no-cpu-baseline > $O/t.$rep.json 2> $O/t.$rep.err || { tail -20 $O/t.$rep.err; exit 1; }
-  python3 - $O/t.$rep.json <<'PY'
-import json, sys
-t = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])["tpcc"]
-w = t.get("window_10000", {})
-print("tpcc65k", {cc: round(t[cc]["ms_per_epoch"], 4) for cc in ("WAIT_DIE", "CALVIN") if cc in t},
-      "window", {cc: round(w[cc]["ms_per_epoch"], 4) for cc in ("WAIT_DIE", "CALVIN") if cc in w})
-PY
-  grep "dvcc host" $O/t.$rep.err | tail -4
+for X in 0 1; do
+  if [ $X = 1 ]; then export DVCC_EXP_NO_ORDER=1; else unset DVCC_EXP_NO_ORDER; fi
+  timeout -k 10 300 python -u bench.py --part1 --no-cpu-baseline --no-tpcc --no-configs --steps 20 --warmup 5 \
+      --detail-out $O/x$X.$rep.detail.json > $O/x$X.$rep.json 2> $O/x$X.$rep.err || { tail -20 $O/x$X.$rep.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/x$X.$rep.detail.json')); print('no_order $X', d['ms_per_step'], d.get('config', {}).get('parallelism'))"
+done
 done
