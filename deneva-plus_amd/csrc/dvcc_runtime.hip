@@ -100,7 +100,8 @@ struct dv_ctx {
     // here); lanes_open counts the lanes of an owner (its tables are frozen)
     dv_ctx *table_owner = nullptr;
     uint32_t lanes_open = 0;
-    uint32_t *d_gate = nullptr;    // 2 words: this context's epochs' lane posts (k_lane_post)
+    uint32_t *d_gate = nullptr;    // 2 words: decision lanes' turn, and (lanes[0]) the executed turns
+    uint32_t lane_issued = 0;      // (lanes[0]) turns queued through d_gate[1] so far (run_lanes)
     hipEvent_t lane_ev = nullptr;  // recorded after this context's last queued execution
     // dv_epoch_run_device_lanes runs lane l of n on lane_stream, masked to
     // the CUs i with i % n == l: a lane's asynchronous round launch needs all
@@ -2658,17 +2659,22 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     dv_ctx *prev = nullptr;  // the lane of the last queued epoch (nullptr: nothing queued is unfinished)
     // the executions' order words (k_lane_wait / k_lane_post): each lane's
     // turn (its d_gate[0]) and the shared count of executed turns (lanes[0]'s
-    // d_gate[1]), set while every lane is idle -- at the start and after a
-    // synchronous run -- the turns counting from the next epoch's lane
+    // d_gate[1]), set at the start of every run of pipelined epochs (the
+    // call's, and after a synchronous run), while nothing queued is
+    // unfinished: the turns count on from every turn ever issued through that
+    // word, from the run's first lane, each written on its own lane's stream,
+    // and the count is set to where they start on the first lane's stream --
+    // no older post can match a turn of this run (none reached past the
+    // issued count), so no host wait
     uint32_t *const done_w = lanes[0]->d_gate + 1;
     auto order_init = [&](uint32_t k0) -> int {
-        uint32_t turn[kMaxLanes];
-        for (uint32_t i = 0; i < n_lanes; i++) turn[(k0 + i) % n_lanes] = i;
-        hipStream_t s0 = lanes[0]->stream;
-        for (uint32_t l = 0; l < n_lanes; l++)
-            HIPCHK(hipMemcpyAsync(lanes[l]->d_gate, &turn[l], sizeof(uint32_t), hipMemcpyHostToDevice, s0));
-        HIPCHK(hipMemsetAsync(done_w, 0, sizeof(uint32_t), s0));
-        return hip_fail(hipStreamSynchronize(s0), "lane order words");
+        const uint32_t base = lanes[0]->lane_issued & 0x7FFFFFFFu;
+        for (uint32_t i = 0; i < n_lanes; i++) {
+            dv_ctx *l = lanes[(k0 + i) % n_lanes];
+            HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(l->d_gate), base + i, 1, l->stream));
+        }
+        HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(done_w), base << 1, 1, lanes[k0 % n_lanes]->stream));
+        return DV_OK;
     };
     auto drain = [&] {
         for (uint32_t l = 0; l < n_lanes; l++) (void)hipStreamSynchronize(lanes[l]->stream);
@@ -2749,6 +2755,9 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         };
         const auto td = hclock::now();
         int r = decide(c, k, tail);
+        // (this epoch's turn, counted whether or not its post was queued:
+        // a count past the posts is safe, one short of them is not)
+        lanes[0]->lane_issued++;
         t_decide += std::chrono::duration<double>(hclock::now() - td).count();
         if (!r) {
             EpochSnap &sn = p.sn;
