@@ -954,6 +954,9 @@ struct dvcc::Xport {
     // bytes: send segment [sd[q], sd[q] + sc[q]) to peer q, receive rc[q] at rd[q]
     virtual int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv,
                             const size_t *rc, const size_t *rd, hipStream_t s) = 0;
+    // the same with a buffer of its own per peer: send[q] (sc[q] bytes) to peer q
+    virtual int all_to_allv_segs(const uint8_t *const *send, const size_t *sc, uint8_t *recv, const size_t *rc,
+                                 const size_t *rd, hipStream_t s) = 0;
     // in place, element-wise MAX
     virtual int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) = 0;
     virtual int max_u8(uint8_t *buf, uint64_t n, hipStream_t s) = 0;
@@ -979,6 +982,16 @@ struct RcclXport final : Xport {
     int all_to_allv(const uint8_t *send, const size_t *sc, const size_t *sd, uint8_t *recv, const size_t *rc,
                     const size_t *rd, hipStream_t s) override {
         return nccl_fail(ncclAllToAllv(send, sc, sd, recv, rc, rd, ncclUint8, comm, s), "ncclAllToAllv");
+    }
+    int all_to_allv_segs(const uint8_t *const *send, const size_t *sc, uint8_t *recv, const size_t *rc,
+                         const size_t *rd, hipStream_t s) override {
+        int r = nccl_fail(ncclGroupStart(), "ncclGroupStart");
+        for (int q = 0; q < P && !r; q++) {
+            if (sc[q]) r = nccl_fail(ncclSend(send[q], sc[q], ncclUint8, q, comm, s), "ncclSend");
+            if (!r && rc[q]) r = nccl_fail(ncclRecv(recv + rd[q], rc[q], ncclUint8, q, comm, s), "ncclRecv");
+        }
+        const int e = nccl_fail(ncclGroupEnd(), "ncclGroupEnd");
+        return r ? r : e;
     }
     int max_u32(uint32_t *buf, uint64_t n, hipStream_t s) override {
         return nccl_fail(ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, comm, s), "ncclAllReduce");
@@ -1011,6 +1024,7 @@ struct LocalGroup {
     struct Slot {
         const uint8_t *send = nullptr;
         const size_t *sd = nullptr;
+        const uint8_t *const *segs = nullptr;  // all_to_allv_segs: the buffer per peer
         hipEvent_t ready = nullptr, done = nullptr;
     };
     std::vector<Slot> slot;
@@ -1074,6 +1088,17 @@ struct LocalXport final : Xport {
             if (rc[q])
                 CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], g->slot[q].send + g->slot[q].sd[r], rc[q],
                                              hipMemcpyDeviceToDevice, s), "copy"));
+        return retire(s);
+    }
+    int all_to_allv_segs(const uint8_t *const *send, const size_t *sc, uint8_t *recv, const size_t *rc,
+                         const size_t *rd, hipStream_t s) override {
+        (void)sc;
+        g->slot[r].segs = send;  // (read by the peers after publish's barrier)
+        CHK(publish(nullptr, nullptr, s));
+        for (int q = 0; q < g->P; q++)
+            if (rc[q])
+                CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], g->slot[q].segs[r], rc[q], hipMemcpyDeviceToDevice, s),
+                              "copy"));
         return retire(s);
     }
     template <class T>
@@ -1189,6 +1214,25 @@ struct IpcXport final : Xport {
             end = std::max<uint64_t>(end, sd[q] + sc[q]);
         }
         CHK(stage(send, end, s));
+        for (int q = 0; q < P; q++)
+            if (rc[q])
+                CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], peer[q] + shm->slot[q].sd[r], rc[q],
+                                             hipMemcpyDeviceToDevice, s), "copy"));
+        return drain(s);
+    }
+    int all_to_allv_segs(const uint8_t *const *send, const size_t *sc, uint8_t *recv, const size_t *rc,
+                         const size_t *rd, hipStream_t s) override {
+        uint64_t off = 0;
+        for (int q = 0; q < P; q++) off += sc[q];
+        if (off > staging_cap) return DV_ERR_ARG;
+        off = 0;
+        for (int q = 0; q < P; q++) {  // (the segments staged back to back)
+            shm->slot[r].sd[q] = off;
+            if (sc[q])
+                CHK(hip_fail2(hipMemcpyAsync(staging + off, send[q], sc[q], hipMemcpyDeviceToDevice, s), "stage"));
+            off += sc[q];
+        }
+        CHK(stage(nullptr, 0, s));
         for (int q = 0; q < P; q++)
             if (rc[q])
                 CHK(hip_fail2(hipMemcpyAsync(recv + rd[q], peer[q] + shm->slot[q].sd[r], rc[q],
@@ -1959,7 +2003,17 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         }
         ro += recvc[e];
     }
-    if (compact && nmax) {
+    // the batches' 4-byte records as they are (dv_epoch_dev::recs32, key | wr
+    // << 31): with the boundaries travelling (tbx) the compact record is the
+    // same word -- the pack would only saturate a key past 30 bits, which the
+    // decider's range check refuses either way (rows * P < 2^30) -- so each
+    // batch goes to the all-to-allv straight from its buffer
+    bool direct = compact && tbx;
+    for (uint32_t e = 0; e < P && direct; e++) direct = sendc[e] == 0 || homes[e].recs32 != nullptr;
+    std::vector<const uint8_t *> segs(P);
+    if (direct)
+        for (uint32_t e = 0; e < P; e++) segs[e] = reinterpret_cast<const uint8_t *>(homes[e].recs32);
+    if (compact && nmax && !direct) {
         const uint32_t bx = (uint32_t)std::min<uint64_t>((nmax + kBlock - 1) / kBlock, std::max(1u, 2048u / P));
         DV_LAUNCH(k_group_pack_c, dim3(bx, P), kBlock, 0, s, ps, sk, m->gbad, tbx ? 1 : 0);
     }
@@ -1978,8 +2032,11 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
-    CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
-                          reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
+    if (direct)
+        CHK(m->x->all_to_allv_segs(segs.data(), sc.data(), reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
+    else
+        CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
+                              reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
     if (tbx)
         CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->tbs), bc.data(), bd.data(),
                               reinterpret_cast<uint8_t *>(m->tbr), bc.data(), bd.data(), s));
