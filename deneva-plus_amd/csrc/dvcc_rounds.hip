@@ -534,7 +534,10 @@ __device__ __forceinline__ uint8_t txn_verdict(const uint8_t *__restrict__ v, ui
 // Walks the undecided-txn list (round 0: every txn) and writes the survivors
 // to the other list: each block takes kSettleChunk consecutive entries,
 // compacts its survivors in LDS and reserves space with ONE atomic.
-constexpr uint32_t kSettleIPT = 4, kSettleChunk = kBlock * kSettleIPT;
+#ifndef DVCC_SETTLE_IPT
+#define DVCC_SETTLE_IPT 1  // (txns per thread: 1 took the settle from 8.3-8.9 to 5.9-6.1 us at config D, profiles/r05_af)
+#endif
+constexpr uint32_t kSettleIPT = DVCC_SETTLE_IPT, kSettleChunk = kBlock * kSettleIPT;
 
 // tword (round 0 with an asynchronous launch behind it): also the txn's fact
 // word for k_round_async, as k_async_words would write it from the settled
