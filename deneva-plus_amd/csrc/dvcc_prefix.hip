@@ -38,7 +38,7 @@ namespace dvcc {
 
 namespace {
 #ifndef DVCC_KILL_IPT
-#define DVCC_KILL_IPT 4
+#define DVCC_KILL_IPT 2  // (4: k_kill_count 8.1 / k_kill_emit 19.5 us; 2: 6.5 / 18.2; 1: 7.7 / 27.8 -- profiles/r05_ah)
 #endif
 constexpr int kKillIPT = DVCC_KILL_IPT;                 // txns per thread in k_kill_compact
 constexpr uint32_t kKillTile = kBlock * kKillIPT;       // txns per tile
@@ -84,7 +84,10 @@ uint64_t row_state_words(uint64_t rows) { return (((rows + 15) / 16 + 3) & ~3ull
 // their bitmap words first, then each nonzero word into the bitmap with one
 // atomic per block (one device-scope atomic per access on a shared word ran
 // at ~88 per us); other rows go straight to the bitmap and the Bloom filter.
-constexpr int kMarkBlock = 1024;  // (16 KiB of LDS per block)
+#ifndef DVCC_MARK_BLOCK
+#define DVCC_MARK_BLOCK 512  // (threads per block: 1024 9.0 us, 512 6.9, 256 9.2 -- profiles/r05_ah)
+#endif
+constexpr int kMarkBlock = DVCC_MARK_BLOCK;  // (16 KiB of LDS per block)
 __global__ __launch_bounds__(kMarkBlock) void k_prefix_mark(uint8_t *__restrict__ status,
                                                             const uint32_t *__restrict__ tb_start,
                                                             const uint32_t *__restrict__ tb_end,
