@@ -410,8 +410,11 @@ void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, co
                      const uint32_t *recs, const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K,
                      uint32_t slog, uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr,
                      const uint64_t *ts, hipEvent_t ev0, hipEvent_t ev1) {
+#ifndef DVCC_PROBE_TB_GRID
+#define DVCC_PROBE_TB_GRID 4096  // (2048: 9.5-9.6 us, 4096: 9.2-9.3, 1024: 11.1 -- profiles/r05_ai)
+#endif
     uint32_t g = (n_txn + kBlock - 1) / kBlock;
-    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    g = g < 1 ? 1 : (g > DVCC_PROBE_TB_GRID ? DVCC_PROBE_TB_GRID : g);
     DV_LAUNCH_EV(k_probe_tb, g, kBlock, 0, s, ev0, ev1, tabs, keys, types, recs, txn_begin, n_acc, n_txn, K, slog,
                  pairs, tlen, acc_row, ctr, ts);
 }
@@ -1311,8 +1314,11 @@ void launch_epoch_clear(hipStream_t s, uint8_t *status, uint32_t n_txn, uint32_t
                         const uint32_t *err_seed, Counters *ctr, uint32_t *zero, uint64_t zero_words, bool gate,
                         Counters *hctr, unsigned long long *hseq, unsigned long long seq, uint64_t *txn_zero8,
                         uint64_t *desc, uint32_t n_desc) {
+#ifndef DVCC_CLEAR_GRID
+#define DVCC_CLEAR_GRID 2048
+#endif
     uint32_t g = (n_txn_pad4 + kBlock - 1) / kBlock;
-    g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+    g = g < 1 ? 1 : (g > DVCC_CLEAR_GRID ? DVCC_CLEAR_GRID : g);
     // zero: a 16-byte aligned area of zero_words 32-bit words (a multiple of 4)
     DV_LAUNCH(k_epoch_clear, g, kBlock, 0, s, status, n_txn, n_txn_pad4, value, tb_start, tb_end, tlen, tile_ctr,
                                        err_seed, ctr, reinterpret_cast<uint4 *>(zero), zero ? zero_words / 4 : 0,

@@ -220,14 +220,15 @@ template <class EIn>
 #define DVCC_ROUND_IPT 16
 #endif
 #ifndef DVCC_ROUND_T64
-#define DVCC_ROUND_T64 512
+#define DVCC_ROUND_T64 1024
 #endif
-// 64-bit elements (round 0 over the sorted pairs): 8 per thread, 4,096-element
+// 64-bit elements (round 0 over the sorted pairs): 4 per thread, 4,096-element
 // tiles -- a prefix-kill stage's 328K / 563K pairs in 80 / 138 workgroups
 // instead of 40 / 69 (round 0 18.9 -> 16.2 us at config D; 16 per thread 18.9,
-// 256 threads x 16 21.3; profiles/r04_rt2)
+// 256 threads x 16 21.3; profiles/r04_rt2); 1,024 threads x 4 instead of
+// 512 x 8: 16.5 -> 15.5 us (profiles/r05_aj)
 #ifndef DVCC_ROUND_IPT64
-#define DVCC_ROUND_IPT64 8
+#define DVCC_ROUND_IPT64 4
 #endif
 struct Geo {
     static constexpr int kThreads = sizeof(EIn) == 4 ? 1024 : DVCC_ROUND_T64;
