@@ -61,6 +61,9 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
     // launch and its 8-byte-per-access re-read of the pairs.
     __shared__ uint32_t wc[4][kRadix];
     __shared__ TableDesc s_td[kMaxTables];  // per-lane table ids index this copy
+    // RSV: a chunk's last-name keys, resolved in place (unused otherwise)
+    __shared__ uint64_t s_rk[RSV ? kBlock * kPV : 1];
+    __shared__ uint32_t s_rn;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (tables) {
         if (threadIdx.x < kMaxTables) s_td[threadIdx.x] = tabs.t[threadIdx.x];
@@ -119,19 +122,40 @@ __device__ __forceinline__ void probe_body(const Tables &tabs, const uint64_t *_
             }
         }
         bool miss = false, ts_bad = false;
+        // the chunk's last names first: listed in LDS and resolved one per
+        // thread (a name lookup is a chain of dependent loads; taken by the
+        // thread that holds the access, four per thread, the probe ran 32 us
+        // per TPC-C launch against 12 + 13 for the probe and a resolve launch)
+        if (RSV && tables) {
+            uint32_t slot[kPV];
+            if (threadIdx.x == 0) s_rn = 0;
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPV; j++) {
+                slot[j] = ~0u;
+                if (i0 + j < n && tb[j] == DV_TPCC_CUST_LAST && tb[j] < tabs.n) {  // (else: the missing table reported)
+                    slot[j] = atomicAdd(&s_rn, 1u);
+                    s_rk[slot[j]] = key[j];
+                }
+            }
+            __syncthreads();
+            for (uint32_t u = threadIdx.x; u < s_rn; u += kBlock)
+                s_rk[u] = tpcc_last_name_key(s_td[DV_TPCC_CUST_LAST], rsv_cols, s_rk[u]);
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < kPV; j++)
+                if (slot[j] != ~0u) {
+                    key[j] = s_rk[slot[j]];
+                    tb[j] = DV_TPCC_CUSTOMER;
+                }
+        }
 #pragma unroll
         for (int j = 0; j < kPV; j++) {
             row[j] = 0;
             if (i0 + j < n) {
-                if (tables) {
-                    uint32_t t = tb[j];
-                    uint64_t k = key[j];
-                    if (RSV && t == DV_TPCC_CUST_LAST && t < tabs.n) {  // (else: the missing table reported)
-                        k = tpcc_last_name_key(s_td[t], rsv_cols, k);
-                        t = DV_TPCC_CUSTOMER;
-                    }
-                    probe_row(s_td[t < kMaxTables ? t : 0], t < tabs.n, k, row[j], ctr, &miss);
-                } else
+                if (tables)
+                    probe_row(s_td[tb[j] < kMaxTables ? tb[j] : 0], tb[j] < tabs.n, key[j], row[j], ctr, &miss);
+                else
                     probe_row(tabs.t[0], tabs.n > 0, key[j], row[j], ctr, &miss);
             }
         }

@@ -47,11 +47,16 @@ __device__ inline uint64_t tpcc_last_name_key(const TableDesc &t, const uint64_t
     } else {
         const uint32_t lo = t.bstart[bk], hi = t.bstart[bk + 1];
         uint32_t cnt = 0, first = hi;
-        for (uint32_t j = lo; j < hi; j++) {
-            if (t.ix[j].key == key) {
-                if (first == hi) first = j;
-                cnt++;
-            }
+        for (uint32_t j0 = lo; j0 < hi; j0 += 4) {  // (four entries' keys in flight per step)
+            uint64_t k4[4];
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++) k4[q] = j0 + q < hi ? t.ix[j0 + q].key : ~key;
+#pragma unroll
+            for (uint32_t q = 0; q < 4; q++)
+                if (k4[q] == key) {
+                    if (first == hi) first = j0 + q;
+                    cnt++;
+                }
         }
         if (cnt) row = t.ix[first + cnt / 2].row;
     }
