@@ -997,6 +997,50 @@ def test_epoch_graphs_new_content_and_halts(lanes):
 
 
 @pytest.mark.gpu
+def test_lanes_rotated_orders_and_ragged_calls():
+    """Decision lanes handed over in different orders from call to call (the
+    shared order word is lanes[0]'s, each context's turn its own) and calls of
+    1 to 5 epochs, from the same device buffers refilled with new epochs (so
+    the graphs, keyed by the lanes' order, replay): every epoch equals the
+    sequential oracle's and the table ends as the oracle's."""
+    rows = 1 << 16
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(dvcc.NO_WAIT, 5000, 50_000)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(None)
+    l1, l2 = eng.open_lane(), eng.open_lane()
+    orders = [(eng, [l1, l2]), (l1, [l2, eng]), (l2, [eng, l1])]
+    bufs = [DeviceEpoch(g.gen(5000, 1700 + k)) for k in range(5)]
+    commits = [torch.zeros(5000, dtype=torch.uint8, device="cuda") for _ in range(5)]
+    seed = 1800
+    for call in range(12):
+        first, rest = orders[call % 3]
+        n = (1, 3, 5, 2)[call % 4]
+        epochs = [g.gen(5000, seed + k) for k in range(n)]
+        seed += n
+        for b, e in zip(bufs, epochs):
+            b.keys.copy_(torch.from_numpy(e.keys.view(np.int64)))
+            b.types.copy_(torch.from_numpy(e.types))
+            b.acc_txn.copy_(torch.from_numpy(e.acc_txn().view(np.int32)))
+            b.txn_begin.copy_(torch.from_numpy(e.txn_begin.astype(np.int32)))
+            if b.recs32 is not None:
+                b.recs32.copy_(torch.from_numpy(e.to_row_records().view(np.int32)))
+        torch.cuda.synchronize()
+        sts = first.run_epochs_lanes(rest, bufs[:n], commits[:n])
+        for k, (e, st) in enumerate(zip(epochs, sts)):
+            c_ref, _, st_ref = _oracle_epoch(dvcc.NO_WAIT, tab, f0, e)
+            assert (commits[k].cpu().numpy() == c_ref).all(), (call, k)
+            assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                                   st_ref.write_cnt), (call, k)
+    assert (eng.read_table(0, rows) == f0).all()
+    for ln in (l1, l2):
+        ln.close()
+    eng.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.slow
 def test_config_b_lanes_timed_path():
     """The bench's config-B leg as timed: 65,536-txn CALVIN epochs (zipf 0.6,
