@@ -117,7 +117,7 @@ struct dv_ctx {
 
     // TPC-C epoch (dv_tpcc_epoch_run_device): execution scratch, and the
     // operation words / o_id output of this epoch
-    uint64_t *tp_dsnap = nullptr;  // per district row: D_NEXT_O_ID before the epoch
+    uint64_t *tp_dsnap = nullptr;  // per district row: D_NEXT_O_ID before the epoch, then its queue's start
     uint64_t tp_dsnap_cap = 0;
     const uint64_t *tp_args = nullptr;
     uint64_t *tp_oid = nullptr;
@@ -1648,9 +1648,6 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit, bool prologue_done = false) {
         x.dsnap = c->tp_dsnap;
         x.dist_base = dt.row_base;
         x.dist_rows = dt.created ? dt.cap_rows : 0;
-        x.desc = c->desc;
-        x.tag = next_tag(c);
-        x.tile_ctr = next_ticket(c);
         x.oid = c->tp_oid;
         x.ctr = c->ctr;
         x.n_txn = c->n_txn;
@@ -3169,7 +3166,7 @@ int dv_tpcc_epoch_begin(dv_ctx *c, const dv_epoch_dev *ep, const uint64_t *d_arg
         c->ws_gen++;
         dfree(c->tp_dsnap);
         c->tp_dsnap = nullptr;
-        r = dalloc(&c->tp_dsnap, drows);
+        r = dalloc(&c->tp_dsnap, 2 * drows);  // (snapshots, then the queue starts: k_tpcc_oid)
         if (r) return r;
         c->tp_dsnap_cap = drows;
     }

@@ -14,11 +14,9 @@ struct TpccExec {
     uint64_t *cols;            // state columns, row-major: cols[3 * row + k] (global row id)
     bool oid_direct;           // NO_WAIT / WAIT_DIE / OCC: at most one committed writer per district
                                // row, so o_id = D_NEXT_O_ID + 1 in the update pass (no numbering pass)
-    uint64_t *dsnap;           // per district row: D_NEXT_O_ID before the epoch (scratch, CALVIN)
+    uint64_t *dsnap;           // per district row: D_NEXT_O_ID before the epoch, then where its queue
+                               // starts in pairs ([2 * dist_rows], scratch, CALVIN)
     uint64_t dist_base, dist_rows;
-    uint64_t *desc;            // look-back descriptors (>= n / kRTile), tagged
-    uint32_t tag;
-    uint32_t *tile_ctr;        // a zeroed tile ticket
     uint64_t *oid;             // per txn (may be null)
     Counters *ctr;
     uint32_t n_txn;            // the commit bytes of every txn (and the committed count) ...
