@@ -31,9 +31,9 @@
 //     most one writer of a district row (NewOrder and Payment both write it),
 //     so the update pass sets o_id = ++D_NEXT_O_ID itself.  CALVIN commits
 //     them all: the apply pass snapshots D_NEXT_O_ID at each district queue's
-//     head, then one single-pass segmented count (decoupled look-back,
-//     dvcc_common.h) numbers the committed NewOrders of every queue and the
-//     queue's last element stores the grown word.
+//     head and records where the queue starts, then a wave per district
+//     (k_tpcc_oid) numbers the queue's committed NewOrders by ballot ranks and
+//     stores the grown word.
 //   - The three state columns of a row are one 24-byte group (row-major): a
 //     row's updates touch one or two 128-B lines instead of three.
 //   - S_QUANTITY is piecewise (s > q + 10 ? s - q : s - q + 91): the queue
