@@ -1307,3 +1307,89 @@ def test_txn_begin_bad_boundaries(bad):
     assert ex.value.code == (dvcc._lib.DV_ERR_ARG if bad == "too_long" else dvcc._lib.DV_ERR_TXN_RANGE), ex.value.code
     assert (eng.read_table(0, rows) == before).all()
     eng.close()
+
+
+def _max_len_epoch(rows, n_txn, seed, longest=128):
+    """Ragged txns of 0..longest accesses (one in ten exactly `longest`, the
+    first one too; a few empty), half the keys from a hot set, every fifth
+    txn ending on its own first row again."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(1, longest + 1, size=n_txn)
+    lens[rng.random(n_txn) < 0.1] = longest
+    lens[rng.random(n_txn) < 0.02] = 0
+    lens[0] = longest
+    tb = np.zeros(n_txn + 1, np.uint32)
+    tb[1:] = np.cumsum(lens)
+    n = int(tb[-1])
+    hot = max(8, rows // 256)
+    keys = np.where(rng.random(n) < 0.5, rng.integers(0, hot, size=n), rng.integers(0, rows, size=n))
+    for t in range(0, n_txn, 5):
+        a, b = int(tb[t]), int(tb[t + 1])
+        if b - a >= 2:
+            keys[b - 1] = keys[a]
+    types = (rng.random(n) < 0.5).astype(np.uint8)
+    return Epoch(keys.astype(np.uint64), types, tb)
+
+
+@pytest.mark.parametrize("cc", CCS)
+def test_longest_txns(cc):
+    """Txns of up to 128 accesses -- the engine's bound (kMaxPos, a txn's
+    positions in 7 bits of a sort key) -- mixed with short and empty ones:
+    every decision path (one context without and with the prefix kill, which
+    takes the epoch's own boundaries; the synchronous rounds alone; 64-bit
+    round elements) gives the oracle's commit bytes, digest, write count and
+    table, epoch after epoch."""
+    rows = 1 << 16
+    epochs = [_max_len_epoch(rows, 3000, 1600 + k) for k in range(2)]
+    assert max(int(np.diff(e.txn_begin).max()) for e in epochs) == 128
+    _check(cc, rows, epochs, prefix=None)
+    _check(cc, rows, epochs, prefix=None, asynchronous=False, tail=False)
+    _check(cc, rows, epochs, prefix=None, el64=True)
+    if cc != dvcc.CALVIN:  # (CALVIN takes no prefix)
+        st = _check(cc, rows, epochs, prefix=300)
+        assert st.prefix_txn == 300, st.prefix_txn
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.OCC, dvcc.CALVIN])
+def test_longest_txns_lanes(cc):
+    """The same 128-access txns through the pipelined batch and four decision
+    lanes (prefix-kill epochs with 4-byte records for NO_WAIT / OCC, small
+    pipelined epochs for CALVIN)."""
+    rows = 1 << 16
+    epochs = [_max_len_epoch(rows, 2500, 1700 + k) for k in range(6)]
+    prefix = None if cc == dvcc.CALVIN else 256
+    _check_batch(cc, rows, epochs, prefix=prefix)
+    _check_batch(cc, rows, epochs, prefix=prefix, lanes=4)
+
+
+@pytest.mark.parametrize("declared", [True, False])
+@pytest.mark.parametrize("cc", CCS)
+def test_txn_past_the_longest_is_rejected(cc, declared):
+    """A txn of 129 accesses, one past the bound: declared (max_txn_acc 129)
+    the epoch is refused before any launch, undeclared (0) the probe finds
+    it (ERRB_BIG) -- DV_ERR_ARG either way, no row changed, and the context
+    decides the next epoch bit-exact."""
+    rows = 1 << 12
+    bad = _max_len_epoch(rows, 400, 1800, longest=129)
+    assert int(np.diff(bad.txn_begin).max()) == 129
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, 400, bad.n_acc)
+    try:
+        eng.load_ycsb_partition(rows)
+        before = eng.read_table(0, rows)
+        dep = DeviceEpoch(bad)
+        assert dep.max_txn_acc == 129
+        if not declared:
+            dep.max_txn_acc = 0
+        with pytest.raises(dvcc.DvccError) as ex:
+            eng.run_epoch_device(dep, torch.zeros(400, dtype=torch.uint8, device="cuda"))
+        assert ex.value.code == dvcc._lib.DV_ERR_ARG, ex.value.code
+        assert (eng.read_table(0, rows) == before).all(), "a rejected epoch changed the table"
+        good = _max_len_epoch(rows, 400, 1801)
+        c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, good)
+        c, _, st = _gpu_epoch(eng, good, "device")
+        assert (c == c_ref).all() and st.read_digest == st_ref.read_digest
+        assert (eng.read_table(0, rows) == f0).all()
+    finally:
+        eng.close()
