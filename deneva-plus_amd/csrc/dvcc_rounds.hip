@@ -918,9 +918,14 @@ __global__ __launch_bounds__(kTailThreads) void k_round_tail(RoundBufs b, uint32
 #ifndef DVCC_ASYNC_SLEEP
 #define DVCC_ASYNC_SLEEP 8  // back-off (x 64 cycles) of a workgroup whose iteration decided nothing
 #endif
-constexpr int kAsyncThreads = 512;
+// 1,024-thread workgroups, one per CU: half the slices of 512-thread ones, so
+// a queue crosses fewer slice boundaries and a fact fewer workgroups, while
+// the ballot scans take the extra waves for little (config D, one context:
+// 37.3-39.2 against 42.2-42.4 us per launch; 512-thread ones two per CU, and
+// 256-thread ones four, 44.6-45.6 -- profiles/r05_aw)
+constexpr int kAsyncThreads = 1024;
 constexpr int kAsyncWaves = kAsyncThreads / 64;
-// 28 elements per thread (128 VGPRs, two workgroups per CU): 7.3M live
+// 28 elements per thread (128 VGPRs, one workgroup per CU): 7.3M live
 // accesses chip-wide.  Measured on a 1M-txn zipf-0.9 epoch, the launch pays
 // off once the live set has halved: from round 1 (9.2M live) it took 570 us,
 // more than the synchronous rounds it replaces -- every iteration re-reads
