@@ -24,7 +24,7 @@ HEADERS = [os.path.join(INCLUDE, "dvcc.h"), os.path.join(CSRC, "dvcc_internal.h"
            os.path.join(CSRC, "dvcc_common.h"), os.path.join(CSRC, "dvcc_tpcc.h")]
 HIP_SRCS = ["dvcc_kernels.hip", "dvcc_rounds.hip", "dvcc_prefix.hip", "dvcc_carry.hip", "dvcc_comm.hip", "dvcc_tpcc.hip",
             "dvcc_runtime.hip"]
-CPP_SRCS = ["ycsb_gen.cpp", "tpcc_gen.cpp"]
+CPP_SRCS = ["ycsb_gen.cpp", "tpcc_gen.cpp", "wire.cpp"]
 
 
 def _newer(target, deps):

@@ -74,8 +74,9 @@ __device__ __forceinline__ uint32_t commit_bytes_grid(const uint8_t *__restrict_
                 w[q] = c;
             }
             if (out) *reinterpret_cast<uint4 *>(out + i0) = uint4{w[0], w[1], w[2], w[3]};
-        } else {
-            for (uint32_t i = i0; i < n; i++) {
+        } else {  // (this thread's 16 txns only: a ragged end or an unaligned `out`)
+            const uint32_t i1 = n - i0 < 16u ? n : i0 + 16u;
+            for (uint32_t i = i0; i < i1; i++) {
                 const uint32_t c = status[i] == ST_COMMIT ? 1u : 0u;
                 if (out) out[i] = (uint8_t)c;
                 cnt += c;

@@ -1303,7 +1303,14 @@ __global__ void k_lane_post(uint32_t *turn, uint32_t *done, uint32_t n_lanes, co
     if (threadIdx.x != 0) return;
     const uint32_t t = *turn;
     const uint32_t gate = (ctr->halt | ctr->a_halt | ctr->err | ctr->peer_err) ? 1u : 0u;
-    __hip_atomic_store(done, ((t + 1u) << 1) | gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // done only moves forward: a successor whose wait timed out has posted a
+    // later turn already (halted, gate set), and a late post must not take it back
+    const uint32_t want = ((t + 1u) << 1) | gate;
+    uint32_t old = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((int32_t)((old >> 1) - (t + 1u)) < 0 &&
+           !__hip_atomic_compare_exchange_strong(done, &old, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT)) {
+    }
     *turn = t + n_lanes;
 }
 
@@ -1315,7 +1322,8 @@ __global__ void k_lane_wait(const uint32_t *turn, const uint32_t *done, Counters
     const uint32_t t = *turn & 0x7FFFFFFFu;
     const uint64_t t0 = wall_clock64();
     uint32_t v;
-    while (((v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) != t) {
+    // (past this turn already: a later epoch timed out and posted, gate set)
+    while ((int32_t)(((v = __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) >> 1) - t) < 0) {
         if (wall_clock64() - t0 > kLaneWaitTicks) {
             ctr->halt = 1u;
             return;

@@ -415,12 +415,24 @@ RoundBufs round_bufs(dv_ctx *c) {
 // c->ev slots of the probe launch's dispatch timestamps (0-5: stage markers)
 constexpr int kEvProbe0 = 8, kEvProbe1 = 9;
 
+// Something a captured epoch graph's launch arguments name has moved or
+// changed meaning -- a table's index, bucket bitmap, state columns (f0, pkey,
+// ktag: dv_create_table grows them), the carry-over's block counts, or the
+// look-back tags after a wrap: no graph captured before this replays again
+// (ws_gen is part of every graph key).  Lanes share their owner's tables, but
+// those are frozen while any lane is open, so the owner's counter covers them.
+void graphs_stale(dv_ctx *c) { c->ws_gen++; }
+
 // descriptor tag of the next single-pass launch (tags are kTagBits wide)
 uint32_t next_tag(dv_ctx *c) {
     if (++c->round_tag >= (1u << 25)) {
         (void)hipMemsetAsync(c->desc, 0, (size_t)((c->cfg.max_acc + kRTile - 1) / kRTile) * 8,
                              c->stream);
         c->round_tag = 1;
+        // a replayed graph writes the tags it was captured with: once the
+        // tags come round again, one of them could meet a later non-graph
+        // epoch's tag in a stale descriptor
+        graphs_stale(c);
     }
     return c->round_tag;
 }
@@ -855,6 +867,7 @@ namespace {
 int carry_bufs(dv_ctx *c, uint32_t nb) {
     if (nb <= c->carry_nb && c->carry_tot) return DV_OK;
     HIPCHK(hipStreamSynchronize(c->stream));
+    graphs_stale(c);
     dfree(c->carry_b);
     c->carry_b = nullptr;
     c->carry_nb = 0;
@@ -1020,6 +1033,7 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
     HIPCHK(hipMemsetAsync(npk + c->total_rows, 0xFF, capacity_rows * 8, c->stream));
     HIPCHK(hipMemsetAsync(ntg + c->total_rows, kTagWide, capacity_rows, c->stream));  // (no key: pkey decides)
     HIPCHK(hipStreamSynchronize(c->stream));
+    graphs_stale(c);
     dfree(c->f0);
     dfree(c->pkey);
     dfree(c->ktag);
@@ -1038,6 +1052,7 @@ int dv_create_table(dv_ctx *c, uint32_t table, uint64_t capacity_rows, uint64_t 
 // The home-tag bitmap of an implicit-row table: one bit per row, set where
 // the row's key tag is htag (TableDesc::hbits; htag = kTagWide: none).
 int build_home_bits(dv_ctx *c, HostTable &t, uint32_t htag) {
+    graphs_stale(c);
     dfree(t.hbits);
     t.hbits = nullptr;
     t.htag = kTagWide;
@@ -1089,6 +1104,7 @@ int dv_load_table(dv_ctx *c, uint32_t table, const uint64_t *keys, const uint64_
             std::copy(outv.begin(), outv.end(), ent.begin() + lo);
         }
     }
+    graphs_stale(c);
     dfree(t.ix);
     dfree(t.bstart);
     dfree(t.hbits);
@@ -1144,6 +1160,7 @@ int dv_load_ycsb_partition(dv_ctx *c, uint64_t rows_per_part) {
     if (t.cap_rows < rows_per_part || t.nbuckets != rows_per_part || t.hash_kind != DV_HASH_YCSB)
         return DV_ERR_ARG;
     HIPCHK(hipSetDevice(c->cfg.device));
+    graphs_stale(c);
     dfree(t.ix);
     dfree(t.bstart);
     t.ix = nullptr;
@@ -1351,12 +1368,18 @@ int graph_decide(dv_ctx *c, const dv_epoch_dev *ep, const void *args, F &&decide
     g.capture = !e->exec && e->seen >= kGraphAfter && e->seen != kGraphNever;
     tl_graph = &g;
     const auto t0 = std::chrono::steady_clock::now();
+    const uint64_t gen0 = c->ws_gen;
     int r = decide();
     tl_graph = nullptr;
     if (tl_dry) {  // a replay: the host state is the epoch's, the launches are the graph's
         tl_dry = false;
         const auto t1 = std::chrono::steady_clock::now();
         if (!r) r = hip_fail(hipGraphLaunch(e->exec, c->stream), "hipGraphLaunch");
+        // the look-back tags wrapped during the walk (next_tag): the replay
+        // has just written pre-wrap tags into the descriptors, zero them again
+        if (!r && c->ws_gen != gen0)
+            r = hip_fail(hipMemsetAsync(c->desc, 0, (size_t)((c->cfg.max_acc + kRTile - 1) / kRTile) * 8,
+                                        c->stream), "hipMemsetAsync");
         tl_hp_walk += std::chrono::duration<double>(t1 - t0).count();
         tl_hp_glaunch += std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
         tl_hp_replays++;

@@ -189,13 +189,92 @@ extern "C" int dv_tpcc_table(const dv_tpcc_params *p, uint64_t seed, uint32_t pa
     return o.n == nrows ? DV_OK : DV_ERR_STATE;
 }
 
-extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
-                           uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args,
-                           uint32_t *txn_begin, uint8_t *txn_type, uint8_t *owner) {
-    if (!valid(p) || home_part >= p->part_cnt || !keys || !types || !tables || !args || !txn_begin)
-        return DV_ERR_ARG;
-    const Keys K{p->dist_per_wh, p->cust_per_dist, p->max_items};
+// the client queries (gen_payment / gen_new_order, tpcc_query.cpp:150-263),
+// every draw in the reference's order; fields the reference leaves unset for
+// a txn type stay 0, TPCCQuery::remote is never assigned (H5)
+extern "C" int dv_tpcc_gen_queries(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                                   dv_tpcc_query *q) {
+    if (!valid(p) || home_part >= p->part_cnt || (!q && n_txn)) return DV_ERR_ARG;
     TpccRand R((uint32_t)seed);
+    auto home_wh = [&]() {  // FIRST_PART_LOCAL (config.h:158)
+        uint64_t w;
+        while (wh_to_part(p, w = R.URand(1, p->num_wh)) != home_part) {}
+        return w;
+    };
+    for (uint32_t t = 0; t < n_txn; t++) {
+        dv_tpcc_query &o = q[t];
+        std::memset(&o, 0, sizeof(o));
+        std::set<uint64_t> parts;
+        const double x = (double)(R.raw() % 100) / 100.0;  // create_query (tpcc_query.cpp:26-32)
+        if (x < p->perc_payment) {
+            o.txn_type = 1;  // TPCC_PAYMENT
+            o.w_id = o.d_w_id = home_wh();
+            parts.insert(wh_to_part(p, o.w_id));
+            o.d_id = R.URand(1, p->dist_per_wh);
+            o.h_amount = R.URand(1, 5000);
+            const double xr = (double)(R.raw() % 10000) / 10000;
+            const uint64_t y = R.URand(1, 100);
+            if (xr > 0.15) {  // home warehouse
+                o.c_d_id = o.d_id;
+                o.c_w_id = o.w_id;
+            } else {          // remote warehouse
+                o.c_d_id = R.URand(1, p->dist_per_wh);
+                if (p->num_wh > 1) {
+                    while ((o.c_w_id = R.URand(1, p->num_wh)) == o.w_id) {}
+                    parts.insert(wh_to_part(p, o.c_w_id));
+                } else {
+                    o.c_w_id = o.w_id;
+                }
+            }
+            if (y <= 60) {
+                o.by_last_name = 1;
+                const std::string last = last_name(R.NURand(255, 0, 999));
+                std::memcpy(o.c_last, last.c_str(), last.size() + 1);
+            } else {
+                o.c_id = R.NURand(1023, 1, p->cust_per_dist);
+            }
+        } else {
+            o.txn_type = 2;  // TPCC_NEW_ORDER
+            o.w_id = home_wh();
+            o.d_id = R.URand(1, p->dist_per_wh);
+            o.c_id = R.NURand(1023, 1, p->cust_per_dist);
+            o.ol_cnt = R.URand(5, p->max_items_per_txn);
+            o.o_entry_d = 2013;
+            parts.insert(wh_to_part(p, o.w_id));
+            const double r_mpr = (double)(R.raw() % 10000) / 10000;
+            const uint64_t part_limit = r_mpr < p->mpr ? p->part_per_txn : 1;
+            std::set<uint64_t> ids;
+            for (uint64_t k = 0; k < o.ol_cnt; k++) {
+                dv_tpcc_item &it = o.items[k];
+                while (ids.count(it.ol_i_id = R.NURand(8191, 1, p->max_items)) > 0) {}
+                ids.insert(it.ol_i_id);
+                it.ol_quantity = R.URand(1, 10);
+                const double r_rem = (double)(R.raw() % 100000) / 100000;
+                if (r_rem > 0.01 || r_mpr > p->mpr || p->num_wh == 1) {
+                    it.ol_supply_w_id = o.w_id;
+                } else if (parts.size() < part_limit) {
+                    it.ol_supply_w_id = R.URand(1, p->num_wh);
+                    parts.insert(wh_to_part(p, it.ol_supply_w_id));
+                } else {
+                    while (parts.count(wh_to_part(p, it.ol_supply_w_id = R.URand(1, p->num_wh))) == 0) {}
+                }
+            }
+        }
+        for (uint64_t v : parts) o.parts[o.n_parts++] = v;
+    }
+    return DV_OK;
+}
+
+// TPCCTxnManager's access lists (acquire_locks / run_txn_state,
+// tpcc_txn.cpp:117-244, 500-933) of n queries
+extern "C" int dv_tpcc_expand(const dv_tpcc_params *p, const dv_tpcc_query *q, uint32_t n_txn, uint64_t acc_cap,
+                              uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args, uint32_t *txn_begin,
+                              uint8_t *txn_type, uint8_t *owner) {
+    if (!valid(p) || (!q && n_txn) || !keys || !types || !tables || !args || !txn_begin) return DV_ERR_ARG;
+    const Keys K{p->dist_per_wh, p->cust_per_dist, p->max_items};
+    constexpr uint64_t kOperand = (1ull << 56) - 1;
+    auto wh_ok = [&](uint64_t w) { return w >= 1 && w <= p->num_wh; };
+    auto d_ok = [&](uint64_t d) { return d >= 1 && d <= p->dist_per_wh; };
     uint64_t n = 0;
     // owner: the partition whose node runs the access (acquire_locks tests
     // GET_NODE_ID(wh_to_part(...)) per access; ITEM goes with its supply
@@ -208,81 +287,63 @@ extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home
         args[n] = op << 56 | v;
         n++;
     };
-    auto home_wh = [&]() {  // FIRST_PART_LOCAL (config.h:158)
-        uint64_t w;
-        while (wh_to_part(p, w = R.URand(1, p->num_wh)) != home_part) {}
-        return w;
-    };
     for (uint32_t t = 0; t < n_txn; t++) {
+        const dv_tpcc_query &o = q[t];
         txn_begin[t] = (uint32_t)n;
-        const double x = (double)(R.raw() % 100) / 100.0;  // create_query (tpcc_query.cpp:26-32)
-        if (x < p->perc_payment) {
-            if (txn_type) txn_type[t] = 1;
-            // gen_payment (tpcc_query.cpp:150-205)
-            const uint64_t w = home_wh();
-            const uint64_t d = R.URand(1, p->dist_per_wh);
-            const uint64_t h_amount = R.URand(1, 5000);
-            const double xr = (double)(R.raw() % 10000) / 10000;
-            const uint64_t y = R.URand(1, 100);
-            uint64_t c_d, c_w;
-            if (xr > 0.15) {
-                c_d = d;
-                c_w = w;
-            } else {
-                c_d = R.URand(1, p->dist_per_wh);
-                if (p->num_wh > 1) {
-                    while ((c_w = R.URand(1, p->num_wh)) == w) {}
-                } else {
-                    c_w = w;
-                }
-            }
+        if (txn_type) txn_type[t] = (uint8_t)o.txn_type;
+        if (o.txn_type == 1) {
+            if (!wh_ok(o.w_id) || !d_ok(o.d_id) || !wh_ok(o.c_w_id) || !d_ok(o.c_d_id) || o.h_amount > kOperand)
+                return DV_ERR_ARG;
+            if (!o.by_last_name && (o.c_id < 1 || o.c_id > p->cust_per_dist)) return DV_ERR_ARG;
+            if (o.by_last_name && std::memchr(o.c_last, 0, sizeof(o.c_last)) == nullptr) return DV_ERR_ARG;
+            if (n + 3 > acc_cap) return DV_ERR_ARG;
             // run_payment_0..5 (tpcc_txn.cpp:500-660): WH, DIST, CUST
-            acc(DV_TPCC_WAREHOUSE, w, p->wh_update ? DV_WR : DV_RD, p->wh_update ? DV_TOP_PAY_WH : DV_TOP_NONE,
-                h_amount, w);
-            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_PAY_DIST, h_amount, w);
-            if (y <= 60) {  // by last name: index_read(i_customer_last) + mid (600-626)
-                const std::string last = last_name(R.NURand(255, 0, 999));
-                acc(DV_TPCC_CUST_LAST, K.cust_np(last, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount, c_w);
-            } else {
-                const uint64_t c = R.NURand(1023, 1, p->cust_per_dist);
-                acc(DV_TPCC_CUSTOMER, K.cust(c, c_d, c_w), DV_WR, DV_TOP_PAY_CUST, h_amount, c_w);
+            acc(DV_TPCC_WAREHOUSE, o.w_id, p->wh_update ? DV_WR : DV_RD, p->wh_update ? DV_TOP_PAY_WH : DV_TOP_NONE,
+                o.h_amount, o.w_id);
+            acc(DV_TPCC_DISTRICT, K.dist(o.d_id, o.w_id), DV_WR, DV_TOP_PAY_DIST, o.h_amount, o.w_id);
+            if (o.by_last_name)  // index_read(i_customer_last) + mid (600-626)
+                acc(DV_TPCC_CUST_LAST, K.cust_np(std::string(o.c_last), o.c_d_id, o.c_w_id), DV_WR, DV_TOP_PAY_CUST,
+                    o.h_amount, o.c_w_id);
+            else
+                acc(DV_TPCC_CUSTOMER, K.cust(o.c_id, o.c_d_id, o.c_w_id), DV_WR, DV_TOP_PAY_CUST, o.h_amount, o.c_w_id);
+        } else if (o.txn_type == 2) {
+            if (!wh_ok(o.w_id) || !d_ok(o.d_id) || o.c_id < 1 || o.c_id > p->cust_per_dist || o.ol_cnt < 1 ||
+                o.ol_cnt > DV_TPCC_MAX_OL)
+                return DV_ERR_ARG;
+            for (uint64_t k = 0; k < o.ol_cnt; k++) {
+                const dv_tpcc_item &it = o.items[k];
+                if (it.ol_i_id < 1 || it.ol_i_id > p->max_items || !wh_ok(it.ol_supply_w_id) ||
+                    it.ol_quantity > kOperand)
+                    return DV_ERR_ARG;
+            }
+            if (n + 3 + 2 * o.ol_cnt > acc_cap) return DV_ERR_ARG;
+            // new_order_0..5 (tpcc_txn.cpp:663-800): WH RD, CUST RD, DIST WR
+            acc(DV_TPCC_WAREHOUSE, o.w_id, DV_RD, DV_TOP_NONE, 0, o.w_id);
+            acc(DV_TPCC_CUSTOMER, K.cust(o.c_id, o.d_id, o.w_id), DV_RD, DV_TOP_NONE, 0, o.w_id);
+            acc(DV_TPCC_DISTRICT, K.dist(o.d_id, o.w_id), DV_WR, DV_TOP_NO_DIST, 0, o.w_id);
+            for (uint64_t k = 0; k < o.ol_cnt; k++) {
+                const dv_tpcc_item &it = o.items[k];
+                // new_order_6..9 (tpcc_txn.cpp:801-933): ITEM RD, STOCK WR
+                acc(DV_TPCC_ITEM, it.ol_i_id, DV_RD, DV_TOP_NONE, 0, it.ol_supply_w_id);
+                acc(DV_TPCC_STOCK, K.stock(it.ol_i_id, it.ol_supply_w_id), DV_WR, DV_TOP_NO_STOCK, it.ol_quantity,
+                    it.ol_supply_w_id);
             }
         } else {
-            if (txn_type) txn_type[t] = 2;
-            // gen_new_order (tpcc_query.cpp:207-263)
-            const uint64_t w = home_wh();
-            const uint64_t d = R.URand(1, p->dist_per_wh);
-            const uint64_t c = R.NURand(1023, 1, p->cust_per_dist);
-            const uint64_t ol_cnt = R.URand(5, p->max_items_per_txn);
-            std::set<uint32_t> parts{wh_to_part(p, w)};
-            const double r_mpr = (double)(R.raw() % 10000) / 10000;
-            const uint64_t part_limit = r_mpr < p->mpr ? p->part_per_txn : 1;
-            // new_order_0..5 (tpcc_txn.cpp:663-800): WH RD, CUST RD, DIST WR
-            acc(DV_TPCC_WAREHOUSE, w, DV_RD, DV_TOP_NONE, 0, w);
-            acc(DV_TPCC_CUSTOMER, K.cust(c, d, w), DV_RD, DV_TOP_NONE, 0, w);
-            acc(DV_TPCC_DISTRICT, K.dist(d, w), DV_WR, DV_TOP_NO_DIST, 0, w);
-            std::set<uint64_t> ids;
-            for (uint64_t k = 0; k < ol_cnt; k++) {
-                uint64_t i_id;
-                while (ids.count(i_id = R.NURand(8191, 1, p->max_items)) > 0) {}
-                ids.insert(i_id);
-                const uint64_t qty = R.URand(1, 10);
-                const double r_rem = (double)(R.raw() % 100000) / 100000;
-                uint64_t sw;
-                if (r_rem > 0.01 || r_mpr > p->mpr || p->num_wh == 1) {
-                    sw = w;
-                } else if (parts.size() < part_limit) {
-                    sw = R.URand(1, p->num_wh);
-                    parts.insert(wh_to_part(p, sw));
-                } else {
-                    while (parts.count(wh_to_part(p, sw = R.URand(1, p->num_wh))) == 0) {}
-                }
-                // new_order_6..9 (tpcc_txn.cpp:801-933): ITEM RD, STOCK WR
-                acc(DV_TPCC_ITEM, i_id, DV_RD, DV_TOP_NONE, 0, sw);
-                acc(DV_TPCC_STOCK, K.stock(i_id, sw), DV_WR, DV_TOP_NO_STOCK, qty, sw);
-            }
+            return DV_ERR_ARG;
         }
     }
     txn_begin[n_txn] = (uint32_t)n;
     return DV_OK;
+}
+
+extern "C" int dv_tpcc_gen(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                           uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args,
+                           uint32_t *txn_begin, uint8_t *txn_type, uint8_t *owner) {
+    if (!valid(p) || home_part >= p->part_cnt || !keys || !types || !tables || !args || !txn_begin)
+        return DV_ERR_ARG;
+    std::vector<dv_tpcc_query> q(n_txn ? n_txn : 1);
+    int r = dv_tpcc_gen_queries(p, seed, home_part, n_txn, q.data());
+    if (r) return r;
+    return dv_tpcc_expand(p, q.data(), n_txn, (uint64_t)n_txn * (3 + 2 * p->max_items_per_txn), keys, types, tables,
+                          args, txn_begin, txn_type, owner);
 }

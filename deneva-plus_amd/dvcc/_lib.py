@@ -105,6 +105,49 @@ class TpccParams(ctypes.Structure):
                 ("perc_payment", ctypes.c_double), ("mpr", ctypes.c_double)]
 
 
+TPCC_MAX_OL, TPCC_MAX_PARTS = 62, 64
+
+
+class TpccItem(ctypes.Structure):  # dv_tpcc_item (Item_no)
+    _fields_ = [("ol_i_id", ctypes.c_uint64), ("ol_supply_w_id", ctypes.c_uint64), ("ol_quantity", ctypes.c_uint64)]
+
+
+class TpccQuery(ctypes.Structure):  # dv_tpcc_query (TPCCQuery / TPCCClientQueryMessage)
+    _fields_ = [("txn_type", ctypes.c_uint64), ("w_id", ctypes.c_uint64), ("d_id", ctypes.c_uint64),
+                ("c_id", ctypes.c_uint64), ("d_w_id", ctypes.c_uint64), ("c_w_id", ctypes.c_uint64),
+                ("c_d_id", ctypes.c_uint64), ("c_last", ctypes.c_char * 16), ("h_amount", ctypes.c_uint64),
+                ("by_last_name", ctypes.c_uint8), ("rbk", ctypes.c_uint8), ("remote", ctypes.c_uint8),
+                ("pad_", ctypes.c_uint8 * 5), ("ol_cnt", ctypes.c_uint64), ("o_entry_d", ctypes.c_uint64),
+                ("n_parts", ctypes.c_uint32), ("pad2_", ctypes.c_uint32),
+                ("parts", ctypes.c_uint64 * TPCC_MAX_PARTS), ("items", TpccItem * TPCC_MAX_OL)]
+
+
+# Deneva wire format (include/dvcc.h)
+WIRE_MSG_MAX, WIRE_HDR = 4096, 12
+WIRE_CL_QRY, WIRE_RDONE, WIRE_CL_RSP, WIRE_CALVIN_ACK = 3, 19, 20, 24
+WIRE_MORE = 1
+
+
+class WireCfg(ctypes.Structure):
+    _fields_ = [("workload", ctypes.c_int32), ("calvin", ctypes.c_uint32), ("node_id", ctypes.c_uint32),
+                ("node_cnt", ctypes.c_uint32), ("part_cnt", ctypes.c_uint32), ("max_req", ctypes.c_uint32),
+                ("synth_table_size", ctypes.c_uint64), ("tpcc", ctypes.POINTER(TpccParams))]
+
+
+class WireEpoch(ctypes.Structure):
+    _fields_ = [("max_txn", ctypes.c_uint32), ("pad_", ctypes.c_uint32), ("max_acc", ctypes.c_uint64),
+                ("keys", ctypes.c_void_p), ("types", ctypes.c_void_p), ("txn_begin", ctypes.c_void_p),
+                ("tables", ctypes.c_void_p), ("args", ctypes.c_void_p), ("txn_type", ctypes.c_void_p),
+                ("owner", ctypes.c_void_p), ("txn_id", ctypes.c_void_p), ("client_startts", ctypes.c_void_p),
+                ("return_node", ctypes.c_void_p), ("n_txn", ctypes.c_uint32), ("rdone", ctypes.c_uint32),
+                ("n_acc", ctypes.c_uint64), ("batch_id", ctypes.c_uint64), ("next_txn", ctypes.c_uint64)]
+
+
+class WireCursor(ctypes.Structure):
+    _fields_ = [("buf", ctypes.c_void_p), ("len", ctypes.c_uint64), ("off", ctypes.c_uint64),
+                ("left", ctypes.c_uint32), ("src", ctypes.c_uint32)]
+
+
 # TPC-C table ids and operation words (include/dvcc.h)
 T_WAREHOUSE, T_DISTRICT, T_CUSTOMER, T_ITEM, T_STOCK, T_CUST_LAST = 0, 1, 2, 3, 4, 5
 TOP_NONE, TOP_PAY_WH, TOP_PAY_DIST, TOP_PAY_CUST, TOP_NO_DIST, TOP_NO_STOCK = 0, 1, 2, 3, 4, 5
@@ -189,6 +232,15 @@ SIGNATURES = [
     ("dv_epoch_run_staged", ctypes.c_int, [_vp, ctypes.c_int, _vp, _vp, _vp, _P(Stats)]),
     ("dv_tpcc_epoch_run_part", ctypes.c_int, [_vp, _P(EpochDev), _vp, _vp, ctypes.c_uint32, _vp, _vp,
                                               _P(Stats)]),
+    ("dv_tpcc_gen_queries", ctypes.c_int, [_P(TpccParams), ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           _P(TpccQuery)]),
+    ("dv_tpcc_expand", ctypes.c_int, [_P(TpccParams), _P(TpccQuery), ctypes.c_uint32, ctypes.c_uint64,
+                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("dv_wire_epoch_reset", ctypes.c_int, [_P(WireEpoch)]),
+    ("dv_wire_open", ctypes.c_int, [_P(WireCfg), _vp, ctypes.c_uint64, _P(WireCursor)]),
+    ("dv_wire_decode", ctypes.c_int, [_P(WireCfg), _P(WireCursor), _P(WireEpoch)]),
+    ("dv_wire_respond", ctypes.c_int, [_P(WireCfg), _P(WireEpoch), _vp, _vp, ctypes.c_uint64, _vp,
+                                       ctypes.c_uint32, _P(ctypes.c_uint32)]),
 ]
 
 _lib = None

@@ -731,6 +731,152 @@ int dv_tpcc_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, const uint64_t
                            const uint8_t *d_owner, uint32_t txns_per_rank, uint8_t *d_commit,
                            uint64_t *d_oid, dv_stats *st);
 
+/* ---------------------------------------------------------------- TPC-C queries
+ * A client query as TPCCQuery and TPCCClientQueryMessage hold it
+ * (benchmarks/tpcc_query.h; transport/message.h:280-312): what runcl sends.
+ * dv_tpcc_gen is dv_tpcc_gen_queries followed by dv_tpcc_expand. */
+#define DV_TPCC_MAX_OL 62   /* longest NewOrder accepted (MAX_ITEMS_PER_TXN bound here) */
+#define DV_TPCC_MAX_PARTS 64
+typedef struct dv_tpcc_item {  /* Item_no (benchmarks/tpcc_query.h:30-38) */
+    uint64_t ol_i_id, ol_supply_w_id, ol_quantity;
+} dv_tpcc_item;
+typedef struct dv_tpcc_query {
+    uint64_t txn_type;                 /* TPCCTxnType (config.h:209): 1 PAYMENT, 2 NEW_ORDER */
+    uint64_t w_id, d_id, c_id;         /* both; c_id: NewOrder, Payment by id          */
+    uint64_t d_w_id, c_w_id, c_d_id;   /* Payment                                       */
+    char c_last[16];                   /* LASTNAME_LEN, NUL-terminated: Payment by name */
+    uint64_t h_amount;                 /* Payment                                       */
+    uint8_t by_last_name, rbk, remote, pad_[5];
+    uint64_t ol_cnt, o_entry_d;        /* NewOrder                                      */
+    uint32_t n_parts, pad2_;           /* BaseQuery::partitions, ascending (std::set)   */
+    uint64_t parts[DV_TPCC_MAX_PARTS];
+    dv_tpcc_item items[DV_TPCC_MAX_OL];  /* NewOrder: ol_cnt of them                    */
+} dv_tpcc_query;
+
+/* the queries of dv_tpcc_gen (same seed, same draws: gen_payment /
+ * gen_new_order, tpcc_query.cpp:150-263); fields the reference leaves unset
+ * for a txn type are 0 */
+int dv_tpcc_gen_queries(const dv_tpcc_params *p, uint64_t seed, uint32_t home_part, uint32_t n_txn,
+                        dv_tpcc_query *q);
+/* the accesses of n queries in run_txn_state order (tpcc_txn.cpp:500-933),
+ * arrays as dv_tpcc_gen's, at most acc_cap accesses (DV_ERR_ARG beyond; a
+ * query naming a warehouse, district, customer or item outside p, or an
+ * unknown txn type, is DV_ERR_ARG too) */
+int dv_tpcc_expand(const dv_tpcc_params *p, const dv_tpcc_query *q, uint32_t n_txn, uint64_t acc_cap,
+                   uint64_t *keys, uint8_t *types, uint8_t *tables, uint64_t *args, uint32_t *txn_begin,
+                   uint8_t *txn_type, uint8_t *owner);
+
+/* ---------------------------------------------------------------- Deneva wire format
+ * Ingress of Deneva's own client stream (transport row): the
+ * message batches runcl's MessageThread sends (transport/msg_thread.cpp:
+ * 53-111) -- one mbuf of at most MSG_SIZE_MAX bytes, a 12-byte header
+ * {u32 dest, u32 src, u32 count} (msg_thread.h:24-62), then `count`
+ * messages back to back, each copy_to_buf's fields packed with no padding
+ * between them (COPY_BUF, system/helper.h:163-165; x86-64 sizes: RemReqType
+ * and access_t 4 bytes, size_t 8, bool 1):
+ *   Message header (message.cpp:196-270): rtype u32, txn_id u64, [CALVIN:
+ *     batch_id u64], mq_time u64, 7 latency doubles
+ *   ClientQueryMessage (856-916): client_startts u64, size_t n, n x u64 partition
+ *   YCSBClientQueryMessage (451-526): size_t n, n x ycsb_request (24 bytes:
+ *     acctype u32, 4 pad, key u64, value char, 7 pad; ycsb_query.h:35-50)
+ *   TPCCClientQueryMessage (544-687): txn_type, w_id, d_id, c_id, d_w_id,
+ *     c_w_id, c_d_id (u64), c_last[16], h_amount u64, by_last_name bool,
+ *     size_t n, n x Item_no (3 x u64), rbk bool, remote bool, ol_cnt u64,
+ *     o_entry_d u64
+ *   DoneMessage RDONE (954-977): the header alone (CALVIN: ends a sequencer's batch)
+ * The decoder fills a host epoch (dv_epoch_dev's host arrays) straight from
+ * the bytes -- Message::create_messages + copy_from_buf + the txn managers'
+ * access lists, without a Message object per txn; the epoch then runs as any
+ * other (dv_epoch_run / DeviceEpoch).  Replies go back the same way:
+ * dv_wire_respond packs the epoch's outcome as CL_RSP batches to the
+ * clients (worker_thread.cpp:152; ClientResponseMessage, message.cpp:
+ * 921-949), or, under CALVIN, CALVIN_ACK batches to the sequencers
+ * (worker_thread.cpp:127-136; AckMessage, message.cpp:1057-1110). */
+#define DV_WIRE_MSG_MAX 4096    /* MSG_SIZE_MAX (config.h:94): one mbuf          */
+#define DV_WIRE_HDR 12          /* {dest, src, count}                            */
+#define DV_WIRE_CL_QRY 3        /* RemReqType (system/global.h:237-262)          */
+#define DV_WIRE_RDONE 19
+#define DV_WIRE_CL_RSP 20
+#define DV_WIRE_CALVIN_ACK 24
+#define DV_WIRE_MORE 1          /* dv_wire_decode: the epoch takes no more of this batch */
+
+typedef struct dv_wire_cfg {
+    int32_t workload;            /* DV_YCSB / DV_TPCC                                      */
+    uint32_t calvin;             /* CC_ALG == CALVIN: the header carries batch_id          */
+    uint32_t node_id;            /* g_node_id: every batch's dest                          */
+    uint32_t node_cnt;           /* g_node_cnt (servers)                                   */
+    uint32_t part_cnt;           /* g_part_cnt: every partition named below it             */
+    uint32_t max_req;            /* YCSB: longest request list accepted (<= 128)           */
+    uint64_t synth_table_size;   /* YCSB: every key below it (copy_from_buf's assert)      */
+    const dv_tpcc_params *tpcc;  /* TPC-C: the knobs the access lists follow               */
+} dv_wire_cfg;
+
+typedef struct dv_wire_epoch {
+    /* the caller's host buffers and their capacity */
+    uint32_t max_txn, pad_;
+    uint64_t max_acc;
+    uint64_t *keys;              /* [max_acc]                                              */
+    uint8_t *types;              /* [max_acc] DV_RD / DV_WR                                */
+    uint32_t *txn_begin;         /* [max_txn + 1]                                          */
+    uint8_t *tables;             /* [max_acc] TPC-C (NULL for YCSB)                        */
+    uint64_t *args;              /* [max_acc] TPC-C operation words                        */
+    uint8_t *txn_type;           /* [max_txn] TPC-C, optional                              */
+    uint8_t *owner;              /* [max_acc] optional: the partition that runs the access */
+    uint64_t *txn_id;            /* [max_txn] optional: the server's txn id (CALVIN: the sequencer's) */
+    uint64_t *client_startts;    /* [max_txn] optional: echoed in CL_RSP                   */
+    uint32_t *return_node;       /* [max_txn] optional: the batch's src (client / sequencer) */
+    /* kept by the decoder */
+    uint32_t n_txn, rdone;       /* txns so far; CALVIN: RDONEs taken for batch_id        */
+    uint64_t n_acc;
+    uint64_t batch_id;           /* CALVIN: the batch its messages name (UINT64_MAX: none yet) */
+    uint64_t next_txn;           /* not CALVIN: txn k gets id node_id + node_cnt * k (one worker,
+                                    WorkerThread::get_next_txn_id, worker_thread.cpp:453-458);
+                                    kept across dv_wire_epoch_reset */
+} dv_wire_epoch;
+
+typedef struct dv_wire_cursor {
+    const uint8_t *buf;
+    uint64_t len;
+    uint64_t off;                /* the next message                                       */
+    uint32_t left;               /* messages not decoded yet                               */
+    uint32_t src;                /* the batch's return node                                */
+} dv_wire_cursor;
+
+/* an empty epoch (n_txn = n_acc = 0, txn_begin[0] = 0, batch_id none) */
+int dv_wire_epoch_reset(dv_wire_epoch *ep);
+/* checks a received batch whole and positions a cursor at its first
+ * message: the header (dest == node_id, src != node_id, count >= 1, len
+ * within MSG_SIZE_MAX; create_messages' asserts, message.cpp:39-41) and
+ * every message -- exactly `count` of them filling exactly `len` bytes, each
+ * a CL_QRY (or, under CALVIN, RDONE) with its batch id under CALVIN, keys
+ * below synth_table_size, RD / WR requests, at most max_req of them,
+ * partitions below part_cnt, TPC-C fields inside the tables (as
+ * dv_tpcc_expand checks them).  A malformed batch is DV_ERR_ARG and nothing
+ * of it is decoded. */
+int dv_wire_open(const dv_wire_cfg *cfg, const uint8_t *batch, uint64_t len, dv_wire_cursor *cur);
+/* decodes the cursor's messages into the epoch, in order.  DV_OK: the batch
+ * is consumed.  DV_WIRE_MORE: the next message does not fit the epoch's
+ * capacity, or (CALVIN) names a later batch -- run the epoch, reset it and
+ * call again with the same cursor.  CALVIN: a message naming an earlier
+ * batch than the epoch's is DV_ERR_ARG (the cursor stays at it).
+ * CALVIN: epoch = one sequencer's batch; RDONE of the epoch's batch_id
+ * counts in ep->rdone (the batch is complete at 1 per sequencer); the lock
+ * order of several sequencers' batches is origin-major, so decode each
+ * sequencer's stream into its own epoch and concatenate them in node order
+ * (the Python mirror's dvcc.sequence, QWorkQueue::sched_dequeue,
+ * work_queue.cpp:105-151). */
+int dv_wire_decode(const dv_wire_cfg *cfg, dv_wire_cursor *cur, dv_wire_epoch *ep);
+/* the epoch's replies: not CALVIN, one CL_RSP per committed txn (commit[t]
+ * != 0) to its return node; CALVIN, one CALVIN_ACK (rc RCOK) per txn to its
+ * sequencer.  Packed into mbufs like MessageThread (a destination's
+ * messages in txn order, a batch sent when the next message does not fit),
+ * destinations ascending; batch b is out[batch_off[b] .. batch_off[b + 1]).
+ * Latency fields are 0 (statistics only).  DV_ERR_ARG if out (cap bytes) or
+ * batch_off (max_batches + 1 entries) is too small, or the epoch holds no
+ * txn_id / return_node (and, not CALVIN, client_startts) arrays. */
+int dv_wire_respond(const dv_wire_cfg *cfg, const dv_wire_epoch *ep, const uint8_t *commit, uint8_t *out,
+                    uint64_t cap, uint64_t *batch_off, uint32_t max_batches, uint32_t *n_batches);
+
 #ifdef __cplusplus
 }
 #endif

@@ -42,7 +42,8 @@ def test_struct_layouts_match_header(tmp_path):
     from dvcc import _lib
     structs = {"dv_access": _lib.Access, "dv_config": _lib.Config, "dv_epoch_dev": _lib.EpochDev,
                "dv_ycsb_params": _lib.YcsbParams, "dv_stats": _lib.Stats, "dv_tpcc_params": _lib.TpccParams,
-               "dv_kernel_time": _lib.KernelTime}
+               "dv_kernel_time": _lib.KernelTime, "dv_tpcc_item": _lib.TpccItem, "dv_tpcc_query": _lib.TpccQuery,
+               "dv_wire_cfg": _lib.WireCfg, "dv_wire_epoch": _lib.WireEpoch, "dv_wire_cursor": _lib.WireCursor}
     src = tmp_path / "sz.c"
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "dvcc.h"', "int main(void) {"]
     for name, cls in structs.items():

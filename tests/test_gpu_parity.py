@@ -997,6 +997,97 @@ def test_epoch_graphs_new_content_and_halts(lanes):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("cc,lanes", [(dvcc.NO_WAIT, 1), (dvcc.NO_WAIT, 4), (dvcc.CALVIN, 1), (dvcc.OCC, 3)])
+def test_epoch_graphs_after_table_changes(cc, lanes):
+    """Graphs captured, then the tables change under them: a
+    second table created (the state columns f0 / pkey / ktag reallocated and
+    copied, the dense primary-key shortcut off), then table 0 reloaded (its
+    bucket bitmap reallocated, every row back to its initial F0).  The same
+    epoch buffers run again -- no graph captured before the change may replay
+    against the freed storage: every epoch equals the oracle's."""
+    rows = 1 << 16
+    n = 5000
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, n, 60_000)
+    eng.load_ycsb_partition(rows)
+    eng.set_prefix(None)
+    bufs_src = [g.gen(n, 1700 + k) for k in range(lanes)]
+    bufs = [DeviceEpoch(e) for e in bufs_src]
+    commits = [torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(lanes)]
+
+    def run(calls):
+        extra = [eng.open_lane() for _ in range(lanes - 1)]
+        for _ in range(calls):
+            sts = eng.run_epochs_lanes(extra, bufs, commits) if extra else eng.run_epochs_device(bufs, commits)
+            for k, (e, st) in enumerate(zip(bufs_src, sts)):
+                c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+                assert (commits[k].cpu().numpy() == c_ref).all(), k
+                assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                                       st_ref.write_cnt), k
+        for ln in extra:
+            ln.close()
+        assert (eng.read_table(0, rows) == f0).all()
+
+    run(6)  # (captured at a key's 3rd call, replayed from its 4th)
+    eng.create_table(1, 4096, 4096)
+    eng.load_table(1, np.arange(4096, dtype=np.uint64) * 7 + 3)
+    run(6)
+    eng.load_ycsb_partition(rows)
+    f0[:] = tab.f0
+    run(6)
+    eng.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("offset", [1, 5])
+def test_unaligned_commit_buffer(cc, offset):
+    """Commit bytes into a caller's buffer at an odd offset:
+    every commit byte and count equals the oracle's, guard bytes on both
+    sides of the slice untouched."""
+    rows, n = 1 << 16, 5000
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9, txn_write_perc=1.0, tup_write_perc=0.5)
+    tab = O.YcsbTable(rows)
+    f0 = tab.f0.copy()
+    eng = CCEngine(cc, n, 60_000)
+    eng.load_ycsb_partition(rows)
+    for k in range(3):
+        e = g.gen(n - k, 1900 + k)
+        c_ref, _, st_ref = _oracle_epoch(cc, tab, f0, e)
+        big = torch.full((e.n_txn + offset + 32,), 0xAB, dtype=torch.uint8, device="cuda")
+        d_commit = big[offset:offset + e.n_txn]
+        d_grant = torch.zeros(e.n_acc, dtype=torch.int32, device="cuda") if cc == dvcc.CALVIN else None
+        st = eng.run_epoch_device(DeviceEpoch(e), d_commit, d_grant)
+        hb = big.cpu().numpy()
+        assert (hb[:offset] == 0xAB).all() and (hb[offset + e.n_txn:] == 0xAB).all()
+        assert (hb[offset:offset + e.n_txn] == c_ref).all(), k
+        assert (st.committed, st.read_digest, st.write_cnt) == (st_ref.committed, st_ref.read_digest,
+                                                               st_ref.write_cnt), k
+    assert (eng.read_table(0, rows) == f0).all()
+    eng.close()
+
+
+@pytest.mark.gpu
+def test_epoch_graphs_default_capture_mode():
+    """The epoch graphs with HIP's default graph capture (the package no
+    longer sets DEBUG_CLR_GRAPH_PACKET_CAPTURE; the suite's
+    conftest does, as the bench): tests/graph_mode_check.py replays epoch
+    graphs through the batch and four lanes in a fresh process with the
+    variable unset and checks every epoch against the oracle."""
+    import os
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "DVCC_PACKET_CAPTURE")}
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, os.path.join(here, "graph_mode_check.py")], env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "graph mode ok" in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
 def test_lanes_rotated_orders_and_ragged_calls():
     """Decision lanes handed over in different orders from call to call (the
     shared order word is lanes[0]'s, each context's turn its own) and calls of

@@ -41,11 +41,17 @@ def _check_tables(eng, db, p):
             assert (got == ref[1 + col]).all(), f"table {t} col {col}: {np.flatnonzero(got != ref[1 + col])[:5]}"
 
 
-def _run(eng, e):
+def _run(eng, e, offset=0):
+    """offset: the commit bytes land `offset` bytes into a larger buffer
+    (an unaligned slice), whose guard bytes on either side must survive."""
     dep, d_args = T.device_epoch(e)
-    d_commit = torch.zeros(max(1, e.n_txn), dtype=torch.uint8, device="cuda")
-    d_oid = torch.zeros(max(1, e.n_txn), dtype=torch.int64, device="cuda")
+    n = max(1, e.n_txn)
+    big = torch.full((n + offset + 32,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_commit = big[offset:offset + n]
+    d_oid = torch.zeros(n, dtype=torch.int64, device="cuda")
     st = eng.run_tpcc_epoch_device(dep, d_args, d_commit, d_oid)
+    hb = big.cpu().numpy()
+    assert (hb[:offset] == 0xAB).all() and (hb[offset + n:] == 0xAB).all(), "commit bytes outside the slice"
     return d_commit.cpu().numpy()[:e.n_txn], d_oid.cpu().numpy().view(np.uint64)[:e.n_txn], st
 
 
@@ -62,6 +68,28 @@ def test_tpcc_epoch_parity(cc, kind, n_txn, perc):
         c, o, st = _run(eng, e)
         assert (c == c_ref).all(), f"commit mismatch at {np.flatnonzero(c != c_ref)[:5]}"
         assert (o == o_ref).all(), f"o_id mismatch at {np.flatnonzero(o != o_ref)[:5]}"
+        assert st.committed == st_ref.committed and st.write_cnt == st_ref.write_cnt
+        _check_tables(eng, db, pp)
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("offset", [1, 3, 8])
+def test_tpcc_unaligned_commit_buffer(cc, offset):
+    """The caller's commit-byte buffer at an odd offset (the
+    commit-byte pass's scalar path ran past its own 16 txns when `out` was not
+    16-byte aligned): commit bytes, counts and tables still equal the oracle's,
+    and nothing outside the slice is written."""
+    po, pp = _params("small")
+    db = O.TpccDB(po, 5)
+    eng = T.TpccEngine(cc, pp, 4096, seed=5)
+    try:
+        e = T.gen(pp, 4000, 13)
+        c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], e.keys, e.types, e.tables, e.args, e.txn_begin)
+        c, o, st = _run(eng, e, offset=offset)
+        assert (c == c_ref).all(), f"commit mismatch at {np.flatnonzero(c != c_ref)[:5]}"
+        assert (o == o_ref).all()
         assert st.committed == st_ref.committed and st.write_cnt == st_ref.write_cnt
         _check_tables(eng, db, pp)
     finally:
