@@ -455,6 +455,46 @@ def cpu_config_a(seconds):
                       "reference CC, not the reference binary"}
 
 
+def wire_ingress_leg(eng, epoch, rows, d_commit, reps=3):
+    """Deneva's wire format in front of the engine (never the `value`): the
+    epoch as runcl's client batches (CL_QRY mbufs of at most 4 KB,
+    tests/wire_fmt.py builds them as synthetic traffic), decoded by
+    dv_wire_decode_batches into a host epoch on one core, run on the GPU --
+    its commit bytes must equal the generated epoch's -- and the replies
+    (CL_RSP per committed txn) packed by dv_wire_respond."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import wire_fmt as W
+    from dvcc.wire import WireIngress
+    buf, off = W.ycsb_epoch_buffer_np(epoch, 0, 1)
+    w = WireIngress(dvcc._lib.YCSB, epoch.n_txn, epoch.n_acc, node_id=0, node_cnt=1, synth_table_size=rows)
+    best = None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        closed = w.feed_buffer(buf, off)
+        ep = w.take()
+        dt = time.perf_counter() - t0
+        best = dt if best is None else min(best, dt)
+    if closed or not ((ep.keys == epoch.keys).all() and (ep.types == epoch.types).all()
+                      and (ep.txn_begin == epoch.txn_begin).all()):
+        return {"error": "decoded epoch differs from the generated one"}
+    d_ref = torch.zeros_like(d_commit)
+    eng.run_epoch_device(dvcc.DeviceEpoch(epoch), d_ref)
+    st = eng.run_epoch_device(dvcc.DeviceEpoch(ep), d_commit)
+    commit = d_commit.cpu().numpy()[:ep.n_txn]
+    if not (commit == d_ref.cpu().numpy()[:ep.n_txn]).all():
+        return {"error": "commit bytes of the decoded epoch differ"}
+    t0 = time.perf_counter()
+    replies = w.respond(ep, commit)
+    t_rsp = time.perf_counter() - t0
+    return {"decoded_txns_per_s": ep.n_txn / best, "wire_MBps": len(buf) / best / 1e6, "batches": len(off) - 1,
+            "wire_bytes": int(len(buf)), "decode_ms": best * 1e3, "committed": int(st.committed),
+            "reply_batches": len(replies), "respond_txns_per_s": ep.n_txn / t_rsp, "cores": 1,
+            "entry_points": "dv_wire_decode_batches, dv_wire_respond (include/dvcc.h)",
+            "note": "host-side ingress of one config-D epoch (1,048,576 CL_QRY messages); decode time is the "
+                    "best of %d passes on one core; the GPU run checks the decoded epoch's commit bytes "
+                    "against the generated epoch's" % reps}
+
+
 def e2e_host_leg(eng, epochs, k):
     """SURVEY.md 8(d)'s second reading: epochs from host buffers, so the H2D
     copy of the 16-B access records is inside the time (pinned host memory,
@@ -628,7 +668,9 @@ def epoch_bytes(st, rows, R, bucket=False, tb=False, recs=False):
         "k_radix_scatter": (16 * passes * keys, "per pass: 8 B per key read + 8 B written"),
         "k_bucket_sort": (16 * keys, "8 B per key read + 8 B written (the bucket's sort by the rest of the row "
                                      "hash, in LDS)"),
-        "k_round_pass": (SCAN_BYTES * st["pass_live"], f"{SCAN_BYTES} B per live access read (scan 8 + verdict 1)"),
+        "k_round_pass": (SCAN_BYTES * (keys + st["pass_live"]),
+                         f"{SCAN_BYTES} B per live access read (scan 8 + verdict 1): round 0 of each stage scans "
+                         "every sorted key once, a later pass its live accesses"),
         "k_round_settle": (17 * stage_txn, "per txn of the stage: length 1, status 1 + 1, verdict bytes 10, "
                                            "fact word 4"),
         "k_round_async": (SCAN_BYTES * st["async_live"],
@@ -781,10 +823,20 @@ def stage_summary(stats, sstats, table, el, R):
     sc = next((r for r in table if r["kernel"] == "k_radix_scatter" and "bytes_per_launch" in r), None)
     if sc is not None:  # keys each scatter launch actually ordered (the prefix's and the survivors' sorts)
         keys = sc["bytes_per_launch"] / 16
-        out["sort"] = {"kernel": "k_radix_scatter", "avg_launch_ms": sc["avg_us"] * 1e-3,
-                       "keys_per_launch": keys, "keys_per_s": keys / (sc["avg_us"] * 1e-6),
-                       "achieved_GBps": sc["achieved_GBps"], "frac": sc["frac"],
-                       "bytes": "16 B per key per pass (read 8 + write 8)"}
+        # the whole sort stage: every launch of it (histogram, digit scan, scatter, bucket sort) per epoch
+        stage_kernels = ("k_radix_hist", "k_radix_scan", "k_radix_scatter", "k_bucket_sort")
+        stage_us = sum(r["us_per_epoch"] for r in table if r["kernel"] in stage_kernels)
+        keys_epoch = keys * sc["launches_per_epoch"]
+        sorts = sc["launches_per_epoch"] if "k_bucket_sort" in {r["kernel"] for r in table} else 1.0
+        out["sort"] = {"keys_per_epoch": keys_epoch, "sorts_per_epoch": sorts,
+                       "stage_us_per_epoch": stage_us, "stage_us_per_sort": stage_us / max(1e-9, sorts),
+                       "keys_per_s": keys_epoch / (stage_us * 1e-6) if stage_us > 0 else 0.0,
+                       "keys_per_s_counts": "every launch of the sort stage: " + " + ".join(
+                           k for k in stage_kernels if any(r["kernel"] == k for r in table)),
+                       "scatter": {"kernel": "k_radix_scatter", "avg_launch_ms": sc["avg_us"] * 1e-3,
+                                   "keys_per_launch": keys, "keys_per_s": keys / (sc["avg_us"] * 1e-6),
+                                   "achieved_GBps": sc["achieved_GBps"], "frac": sc["frac"],
+                                   "bytes": "16 B per key per pass (read 8 + write 8)"}}
     return out
 
 
@@ -1103,6 +1155,11 @@ def headline_record(out, detail_path=None):
                     if isinstance(v.get("cpu_baseline"), dict):
                         t[cc]["cpu_baseline"] = _r(v["cpu_baseline"].get("value"))
         legs["tpcc"] = t
+    if isinstance(out.get("sort"), dict):
+        legs["sort"] = _pick(out["sort"], ("keys_per_s", "stage_us_per_sort", "keys_per_epoch"))
+    if isinstance(out.get("wire_ingress"), dict):
+        legs["wire_ingress"] = _pick(out["wire_ingress"], ("decoded_txns_per_s", "wire_MBps", "batches",
+                                                            "respond_txns_per_s", "cores", "error"))
     if isinstance(out.get("cpu_config_a"), dict):
         legs["cpu_config_a"] = _pick(out["cpu_config_a"], ("value", "unit", "cores", "kind", "abort_rate"))
     cl = out.get("closed_loop_retry")
@@ -1294,6 +1351,10 @@ def main():
         live, und = eng.round_log()
         out["round_log_last_epoch"] = {"live": live, "undecided": und}
         out["e2e_host_input"] = e2e_host_leg(eng, epochs, min(a.steps, 5))
+        try:
+            out["wire_ingress"] = wire_ingress_leg(eng, epochs[0], rows, d_commit)
+        except Exception as ex:  # noqa: BLE001 -- the headline above is already measured
+            out["wire_ingress"] = {"error": repr(ex)[:200]}
         out["closed_loop_retry"] = closed_loop_leg(eng, gen, n_txn_total, max(4, min(a.steps, 10)), d_commit,
                                                    out["ms_per_step"])
         if lanes:

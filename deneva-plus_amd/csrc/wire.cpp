@@ -77,7 +77,7 @@ struct Msg {
 };
 
 // Message header + ClientQueryMessage part; false if malformed
-bool read_client_part(const dv_wire_cfg *c, Reader &r, Msg &m) {
+bool read_client_part(const dv_wire_cfg *c, Reader &r, Msg &m, bool check) {
     m.rtype = r.get<uint32_t>();
     m.txn_id = r.get<uint64_t>();
     if (c->calvin) m.batch_id = r.get<uint64_t>();
@@ -87,6 +87,10 @@ bool read_client_part(const dv_wire_cfg *c, Reader &r, Msg &m) {
     m.client_startts = r.get<uint64_t>();
     const uint64_t np = r.get<uint64_t>();  // size_t partitions
     if (!r.ok || np > DV_TPCC_MAX_PARTS) return false;
+    if (!check) {
+        r.skip(np * 8);
+        return r.ok;
+    }
     for (uint64_t i = 0; i < np; i++) {
         const uint64_t part = r.get<uint64_t>();
         if (part >= c->part_cnt) return false;
@@ -94,13 +98,13 @@ bool read_client_part(const dv_wire_cfg *c, Reader &r, Msg &m) {
     return r.ok;
 }
 
-bool read_ycsb(const dv_wire_cfg *c, Reader &r, Msg &m) {
+bool read_ycsb(const dv_wire_cfg *c, Reader &r, Msg &m, bool check) {
     const uint64_t n = r.get<uint64_t>();  // size_t requests
     const uint32_t lim = std::min<uint32_t>(c->max_req ? c->max_req : kMaxReq, kMaxReq);
     if (!r.ok || n > lim || (uint64_t)(r.end - r.p) < n * kYcsbReq) return false;
     m.reqs = r.p;
     m.n_acc = (uint32_t)n;
-    for (uint64_t i = 0; i < n; i++) {
+    for (uint64_t i = 0; check && i < n; i++) {
         uint32_t acctype;
         uint64_t key;
         std::memcpy(&acctype, r.p + i * kYcsbReq, 4);
@@ -158,13 +162,15 @@ extern "C" int dv_wire_epoch_reset(dv_wire_epoch *ep) {
 
 namespace {
 // one message at r: header, client part and body, every field checked (the
-// TPC-C ones by the access-list expansion into scratch arrays)
-bool read_msg(const dv_wire_cfg *c, Reader &r, Msg &m) {
-    if (!read_client_part(c, r, m)) return false;
+// TPC-C ones by the access-list expansion into scratch arrays) -- or, for a
+// batch dv_wire_open has checked (check false), only parsed
+bool read_msg(const dv_wire_cfg *c, Reader &r, Msg &m, bool check = true) {
+    if (!read_client_part(c, r, m, check)) return false;
     if (c->calvin ? m.batch_id == kU64Max : m.rtype == DV_WIRE_RDONE) return false;  // (RDONE ends Calvin batches)
     if (m.rtype == DV_WIRE_RDONE) return true;
-    if (c->workload != DV_TPCC) return read_ycsb(c, r, m);
+    if (c->workload != DV_TPCC) return read_ycsb(c, r, m, check);
     if (!read_tpcc(r, m)) return false;
+    if (!check) return true;
     uint64_t k[3 + 2 * DV_TPCC_MAX_OL], a[3 + 2 * DV_TPCC_MAX_OL];
     uint8_t ty[3 + 2 * DV_TPCC_MAX_OL], tb[3 + 2 * DV_TPCC_MAX_OL];
     uint32_t beg[2];
@@ -204,7 +210,7 @@ extern "C" int dv_wire_decode(const dv_wire_cfg *cfg, dv_wire_cursor *cur, dv_wi
     Msg m;
     while (cur->left > 0) {
         Reader r{cur->buf + cur->off, cur->buf + cur->len};
-        if (!read_msg(cfg, r, m)) return DV_ERR_ARG;  // (checked by dv_wire_open: a cursor not from it)
+        if (!read_msg(cfg, r, m, false)) return DV_ERR_ARG;  // (checked whole by dv_wire_open)
         if (cfg->calvin && ep->batch_id != kU64Max) {  // the sequencer's batch (sequencer.cpp:207-210)
             if (m.batch_id < ep->batch_id) return DV_ERR_ARG;  // stale
             if (m.batch_id > ep->batch_id) return DV_WIRE_MORE;
@@ -253,6 +259,24 @@ extern "C" int dv_wire_decode(const dv_wire_cfg *cfg, dv_wire_cursor *cur, dv_wi
         cur->left--;
     }
     return DV_OK;
+}
+
+extern "C" int dv_wire_decode_batches(const dv_wire_cfg *cfg, const uint8_t *buf, const uint64_t *off,
+                                      uint32_t n_batches, dv_wire_cursor *cur, uint32_t *next_batch,
+                                      dv_wire_epoch *ep) {
+    if (!cfg || !buf || !off || !cur || !next_batch || !ep) return DV_ERR_ARG;
+    for (;;) {
+        if (cur->buf && cur->left > 0) {
+            const int rc = dv_wire_decode(cfg, cur, ep);
+            if (rc) return rc;  // DV_WIRE_MORE (the cursor holds the rest) or an error
+        }
+        if (*next_batch >= n_batches) return DV_OK;
+        const uint32_t b = *next_batch;
+        if (off[b + 1] < off[b]) return DV_ERR_ARG;
+        const int rc = dv_wire_open(cfg, buf + off[b], off[b + 1] - off[b], cur);
+        if (rc) return rc;  // (*next_batch stays at the refused batch)
+        *next_batch = b + 1;
+    }
 }
 
 extern "C" int dv_wire_respond(const dv_wire_cfg *cfg, const dv_wire_epoch *ep, const uint8_t *commit, uint8_t *out,

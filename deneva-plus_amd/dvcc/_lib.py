@@ -239,6 +239,8 @@ SIGNATURES = [
     ("dv_wire_epoch_reset", ctypes.c_int, [_P(WireEpoch)]),
     ("dv_wire_open", ctypes.c_int, [_P(WireCfg), _vp, ctypes.c_uint64, _P(WireCursor)]),
     ("dv_wire_decode", ctypes.c_int, [_P(WireCfg), _P(WireCursor), _P(WireEpoch)]),
+    ("dv_wire_decode_batches", ctypes.c_int, [_P(WireCfg), _vp, _vp, ctypes.c_uint32, _P(WireCursor),
+                                              _P(ctypes.c_uint32), _P(WireEpoch)]),
     ("dv_wire_respond", ctypes.c_int, [_P(WireCfg), _P(WireEpoch), _vp, _vp, ctypes.c_uint64, _vp,
                                        ctypes.c_uint32, _P(ctypes.c_uint32)]),
 ]

@@ -93,6 +93,33 @@ class WireIngress:
         self.ready.extend(closed)
         return closed
 
+    def feed_many(self, batches):
+        """Decodes a list of received batches with one call per epoch
+        (dv_wire_decode_batches); returns the epochs it closed."""
+        if not batches:
+            return []
+        off = np.zeros(len(batches) + 1, np.uint64)
+        off[1:] = np.cumsum([len(b) for b in batches])
+        buf = np.frombuffer(b"".join(bytes(b) for b in batches), dtype=np.uint8)
+        return self.feed_buffer(buf, off)
+
+    def feed_buffer(self, buf, off):
+        """The same over batches already back to back in one uint8 array,
+        batch b at buf[off[b]:off[b + 1]]."""
+        cur = L.WireCursor()
+        nxt = ctypes.c_uint32(0)
+        closed = []
+        while True:
+            rc = L.lib().dv_wire_decode_batches(ctypes.byref(self.cfg), _ptr(buf), _ptr(off), len(off) - 1,
+                                                ctypes.byref(cur), ctypes.byref(nxt), ctypes.byref(self.ep))
+            if rc == L.WIRE_MORE:
+                closed.append(self._close())
+                continue
+            L.check(rc, "dv_wire_decode_batches")
+            break
+        self.ready.extend(closed)
+        return closed
+
     def take(self):
         """Closes and returns the epoch being filled."""
         return self._close()

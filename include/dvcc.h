@@ -866,6 +866,15 @@ int dv_wire_open(const dv_wire_cfg *cfg, const uint8_t *batch, uint64_t len, dv_
  * (the Python mirror's dvcc.sequence, QWorkQueue::sched_dequeue,
  * work_queue.cpp:105-151). */
 int dv_wire_decode(const dv_wire_cfg *cfg, dv_wire_cursor *cur, dv_wire_epoch *ep);
+/* a receive queue's batches at once: batch b is buf[off[b] .. off[b + 1]);
+ * decoding starts with what the cursor still holds (cur->buf NULL or
+ * cur->left 0: nothing) and goes on from batch *next_batch, which advances
+ * past every batch opened.  DV_OK: all consumed.  DV_WIRE_MORE: the epoch
+ * is full (or a CALVIN batch ends) -- run it, reset it, call again with the
+ * same cursor and *next_batch.  A refused batch (dv_wire_open) returns its
+ * error with *next_batch at it. */
+int dv_wire_decode_batches(const dv_wire_cfg *cfg, const uint8_t *buf, const uint64_t *off, uint32_t n_batches,
+                           dv_wire_cursor *cur, uint32_t *next_batch, dv_wire_epoch *ep);
 /* the epoch's replies: not CALVIN, one CL_RSP per committed txn (commit[t]
  * != 0) to its return node; CALVIN, one CALVIN_ACK (rc RCOK) per txn to its
  * sequencer.  Packed into mbufs like MessageThread (a destination's

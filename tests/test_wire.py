@@ -98,6 +98,25 @@ def test_ycsb_batches_decode_to_the_generators_epoch(P, theta):
     assert (d.txn_id == 1 + 3 * np.arange(3000, dtype=np.uint64)).all()
 
 
+def test_decode_batches_in_one_call():
+    """dv_wire_decode_batches over a receive queue equals batch-by-batch
+    decoding, the epoch splits included; a refused batch stops it there."""
+    g = dvcc.YCSBQueryGenerator(1 << 16, zipf_theta=0.9)
+    e = g.gen(2000, 8)
+    bs = W.batches(0, 1, W.ycsb_epoch_messages(e))
+    w1, w2 = _ycsb_ingress(max_txn=300), _ycsb_ingress(max_txn=300)
+    a = [x for b in bs for x in w1.feed(b)] + [w1.take()]
+    c = w2.feed_many(bs) + [w2.take()]
+    assert [x.n_txn for x in a] == [x.n_txn for x in c]
+    assert all((x.keys == y.keys).all() and (x.txn_id == y.txn_id).all() for x, y in zip(a, c))
+    assert (np.concatenate([x.keys for x in c]) == e.keys).all()
+    w3 = _ycsb_ingress()
+    _expect_refused(w3, bs[0][:4] + struct.pack("<I", 0) + bs[0][8:])  # (from itself)
+    with pytest.raises(L.DvccError):
+        w3.feed_many(bs[:3] + [bs[3][:-1]] + bs[4:])
+    assert w3.take().n_txn == sum(struct.unpack_from("<I", b, 8)[0] for b in bs[:3])
+
+
 def test_numpy_batches_equal_the_message_path():
     g = dvcc.YCSBQueryGenerator(1 << 16, zipf_theta=0.9)
     e = g.gen(500, 3)

@@ -94,6 +94,16 @@ def ycsb_epoch_messages(ep, part_cnt=1, client_startts=None, batch_id=None, txn_
     return out
 
 
+def ycsb_epoch_buffer_np(ep, dest, src, client_startts_base=0):
+    """ycsb_epoch_batches_np's batches back to back in one uint8 array and
+    their offsets (batch b at buf[off[b]:off[b + 1]]), as a receive queue
+    holds them, without a bytes object per batch."""
+    bs = ycsb_epoch_batches_np(ep, dest, src, client_startts_base)
+    off = np.zeros(len(bs) + 1, np.uint64)
+    off[1:] = np.cumsum([len(b) for b in bs])
+    return np.frombuffer(b"".join(bs), np.uint8), off
+
+
 def ycsb_epoch_batches_np(ep, dest, src, client_startts_base=0):
     """The same messages and batches for an epoch of equal-length txns on one
     partition (config D), built with numpy for a million txns: every message
