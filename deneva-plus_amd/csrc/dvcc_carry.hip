@@ -71,7 +71,8 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
     const uint32_t *__restrict__ ba, uint32_t max_txn, const uint64_t *__restrict__ keys,
     const uint8_t *__restrict__ types, const uint8_t *__restrict__ tables, uint64_t *__restrict__ okeys,
     uint8_t *__restrict__ otypes, uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
-    uint32_t *__restrict__ tot, const uint32_t *__restrict__ skip) {
+    uint32_t *__restrict__ tot, const uint32_t *__restrict__ skip, const uint32_t *__restrict__ recs,
+    uint32_t *__restrict__ orecs, uint32_t *__restrict__ otb) {
     __shared__ uint32_t lds4[4];
     if (skip && *skip) return;  // (a refill behind a halted epoch: k_refill_plan)
     const uint32_t lane = threadIdx.x & 63;
@@ -88,6 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
         tot[1] = pos + len;
     }
     if (!cr || id >= max_txn) len = 0;  // (ids grow with t: the cap cuts a suffix)
+    else if (otb) otb[id] = pos;        // (tb form: the carried txn's boundary, dv_epoch_dev::txn_begin)
     uint32_t incl = len;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -112,6 +114,8 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
         const uint32_t sid = __shfl(id, (int)src, 64);
         if (g >= wtot) continue;
         const uint32_t in = sa0 + (g - spre), o = wpos + g;
+        if (orecs) orecs[o] = recs[in];  // tb form: the 4-byte records (key | write << 31)
+        if (!okeys) continue;
         okeys[o] = keys[in];
         otypes[o] = types[in];
         otxn[o] = sid;
@@ -180,13 +184,24 @@ __global__ __launch_bounds__(kBlock) void k_refill_fresh(const uint64_t *__restr
                                                          const uint32_t *__restrict__ tot, uint32_t n_out,
                                                          uint64_t *__restrict__ okeys, uint8_t *__restrict__ otypes,
                                                          uint32_t *__restrict__ otxn, uint8_t *__restrict__ otables,
-                                                         uint32_t *__restrict__ n_acc_dev) {
+                                                         uint32_t *__restrict__ n_acc_dev,
+                                                         const uint32_t *__restrict__ precs,
+                                                         uint32_t *__restrict__ orecs, uint32_t *__restrict__ otb) {
     if (tot[4]) return;
     const uint32_t C = tot[2] < n_out ? tot[2] : n_out, A = tot[1], cur = tot[3], F = tot[5];
     const uint32_t e1 = cur + F < pool_n ? cur + F : pool_n;     // [cur, e1) then [0, F - (e1 - cur))
     const uint32_t n2 = F - (e1 - cur);
     const uint32_t b1 = tb[cur], fa1 = tb[e1] - b1, fa2 = tb[n2] - tb[0];
     if (blockIdx.x == 0 && threadIdx.x == 0) *n_acc_dev = A + fa1 + fa2;
+    if (orecs) {  // tb form: the fresh txns' boundaries (and the epoch's end), then their records
+        for (uint32_t f = blockIdx.x * kBlock + threadIdx.x; f <= F; f += gridDim.x * kBlock) {
+            const uint32_t n1 = e1 - cur;
+            otb[C + f] = A + (f <= n1 ? tb[cur + f] - b1 : fa1 + (tb[f - n1] - tb[0]));
+        }
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < fa1 + fa2; i += gridDim.x * kBlock)
+            orecs[A + i] = precs[i < fa1 ? b1 + i : tb[0] + (i - fa1)];
+    }
+    if (!okeys) return;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < fa1 + fa2; i += gridDim.x * kBlock) {
         const bool first = i < fa1;
         const uint32_t src = first ? b1 + i : tb[0] + (i - fa1);
@@ -203,7 +218,8 @@ void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_star
                    const uint64_t *pkeys, const uint8_t *ptypes, const uint8_t *ptables, const uint32_t *ptxn,
                    const uint32_t *ptb, uint32_t pool_n, uint32_t *cursor, uint32_t n_out, uint64_t fresh_bound,
                    uint64_t *okeys, uint8_t *otypes, uint32_t *otxn, uint8_t *otables, uint32_t *n_acc_dev,
-                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr) {
+                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr, const uint32_t *recs,
+                   const uint32_t *precs, uint32_t *orecs, uint32_t *otb) {
     const uint32_t nb = carry_blocks(n_txn);
     if (nb) {
         DV_LAUNCH(k_carry_count, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba);
@@ -212,10 +228,10 @@ void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_star
     DV_LAUNCH(k_refill_plan, 1, 64, 0, s, status, n_txn, bt, nb, tot, n_out, cursor, pool_n, ctr);
     if (nb)
         DV_LAUNCH(k_carry_copy, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba, n_out, keys, types, tables,
-                  okeys, otypes, otxn, otables, tot, (const uint32_t *)(tot + 4));
+                  okeys, otypes, otxn, otables, tot, (const uint32_t *)(tot + 4), recs, orecs, otb);
     const uint64_t g = (fresh_bound + kBlock - 1) / kBlock;
     DV_LAUNCH(k_refill_fresh, (uint32_t)(g < 1 ? 1 : (g > 4096 ? 4096 : g)), kBlock, 0, s, pkeys, ptypes, ptables,
-              ptxn, ptb, pool_n, tot, n_out, okeys, otypes, otxn, otables, n_acc_dev);
+              ptxn, ptb, pool_n, tot, n_out, okeys, otypes, otxn, otables, n_acc_dev, precs, orecs, otb);
 }
 
 // a client batch's per-txn access ranges from its acc_txn (non-decreasing;
@@ -260,7 +276,8 @@ void launch_carry(hipStream_t s, const uint8_t *status, const uint32_t *tb_start
     DV_LAUNCH(k_carry_scan, 1, kBlock, 0, s, bt, ba, nb);
     DV_LAUNCH(k_carry_total, 1, 64, 0, s, status, n_txn, bt, nb, tot);
     DV_LAUNCH(k_carry_copy, nb, kBlock, 0, s, status, tb_start, tb_end, n_txn, bt, ba, max_txn, keys, types, tables,
-                                       okeys, otypes, otxn, otables, tot, (const uint32_t *)nullptr);
+                                       okeys, otypes, otxn, otables, tot, (const uint32_t *)nullptr,
+                                       (const uint32_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr);
 }
 
 }  // namespace dvcc

@@ -292,7 +292,7 @@ void launch_probe(hipStream_t s, const Tables &tabs, const uint64_t *keys, const
 void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                      const uint32_t *recs, const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K,
                      uint32_t slog, uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr,
-                     const uint64_t *ts, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                     const uint64_t *ts, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, const uint32_t *n_acc_dev = nullptr);
 
 // stable LSD radix sort of pairs on bits [32, 32 + key_bits); returns the index
 // (0/1) of the buffer holding the result.  counts: >= kRadix * nblocks(n),
@@ -530,14 +530,18 @@ void launch_txn_ranges(hipStream_t s, const uint32_t *acc_txn, uint64_t n, uint3
 // from *cursor on (advanced, wrapping), into o*; *n_acc_dev = the accesses
 // written.  fresh_bound: a bound on the fresh accesses (grid size).  A halted
 // or rejected epoch (Counters; NULL for the loop's first epoch, n_txn 0) makes
-// every kernel a no-op.  tot: kRefillTot words.
+// every kernel a no-op.  tot: kRefillTot words.  tb form (orecs, otb): the
+// next epoch as 4-byte records (recs: the previous epoch's, precs: the
+// pool's) and its txn boundaries otb[0..n_out]; okeys NULL: only that form
+// (o{keys,types,txn,tables} are not written).
 constexpr uint32_t kRefillTot = 6;
 void launch_refill(hipStream_t s, const uint8_t *status, const uint32_t *tb_start, const uint32_t *tb_end,
                    uint32_t n_txn, const uint64_t *keys, const uint8_t *types, const uint8_t *tables,
                    const uint64_t *pkeys, const uint8_t *ptypes, const uint8_t *ptables, const uint32_t *ptxn,
                    const uint32_t *ptb, uint32_t pool_n, uint32_t *cursor, uint32_t n_out, uint64_t fresh_bound,
                    uint64_t *okeys, uint8_t *otypes, uint32_t *otxn, uint8_t *otables, uint32_t *n_acc_dev,
-                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr);
+                   uint32_t *bt, uint32_t *ba, uint32_t *tot, const Counters *ctr, const uint32_t *recs = nullptr,
+                   const uint32_t *precs = nullptr, uint32_t *orecs = nullptr, uint32_t *otb = nullptr);
 
 // ---- prefix-kill epochs (dvcc_prefix.hip)
 // the row-state bitmap (2 bits per row): its 32-bit words for `rows` rows;

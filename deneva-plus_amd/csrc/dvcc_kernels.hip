@@ -383,7 +383,10 @@ __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t
                                                      uint32_t n_txn, uint32_t K, uint32_t slog,
                                                      uint64_t *__restrict__ pairs, uint8_t *__restrict__ tlen,
                                                      uint32_t *__restrict__ acc_row, Counters *ctr,
-                                                     const uint64_t *__restrict__ ts) {
+                                                     const uint64_t *__restrict__ ts,
+                                                     const uint32_t *__restrict__ n_acc_dev) {
+    // (a device-side count: n_acc is its bound -- the closed loop's epochs)
+    if (n_acc_dev && (uint64_t)*n_acc_dev < n_acc) n_acc = *n_acc_dev;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         ctr->n_acc = (uint32_t)n_acc;
         const uint64_t ak = txn_begin[K];
@@ -433,14 +436,14 @@ __global__ __launch_bounds__(kBlock) void k_probe_tb(Tables tabs, const uint64_t
 void launch_probe_tb(hipStream_t s, const Tables &tabs, const uint64_t *keys, const uint8_t *types,
                      const uint32_t *recs, const uint32_t *txn_begin, uint64_t n_acc, uint32_t n_txn, uint32_t K,
                      uint32_t slog, uint64_t *pairs, uint8_t *tlen, uint32_t *acc_row, Counters *ctr,
-                     const uint64_t *ts, hipEvent_t ev0, hipEvent_t ev1) {
+                     const uint64_t *ts, hipEvent_t ev0, hipEvent_t ev1, const uint32_t *n_acc_dev) {
 #ifndef DVCC_PROBE_TB_GRID
 #define DVCC_PROBE_TB_GRID 4096  // (2048: 9.5-9.6 us, 4096: 9.2-9.3, 1024: 11.1 -- profiles/r05_ai)
 #endif
     uint32_t g = (n_txn + kBlock - 1) / kBlock;
     g = g < 1 ? 1 : (g > DVCC_PROBE_TB_GRID ? DVCC_PROBE_TB_GRID : g);
     DV_LAUNCH_EV(k_probe_tb, g, kBlock, 0, s, ev0, ev1, tabs, keys, types, recs, txn_begin, n_acc, n_txn, K, slog,
-                 pairs, tlen, acc_row, ctr, ts);
+                 pairs, tlen, acc_row, ctr, ts, n_acc_dev);
 }
 
 // ------------------------------------------------------------- radix sort
@@ -832,9 +835,62 @@ __device__ __forceinline__ void bucket_bases(uint32_t (*wc)[kRadix], uint32_t *t
     __syncthreads();
 }
 
+#ifdef DVCC_BUCKET_STAMPS
+// measurement builds only (tools/exp_variant.sh ... -DDVCC_BUCKET_STAMPS): per
+// bucket, summed over launches -- [0] launches, [1] wall-clock ticks (100 MHz)
+// from the workgroup's start to its end, [2] keys, [3] the most ticks of one
+// launch; g_bucket_launch: [0] launches, [1] sum of the launch's slowest
+// bucket's ticks, [2] that bucket's keys, [3] the last-workgroup ticket
+__device__ unsigned long long g_bucket_stamps[1024 * 4];
+__device__ unsigned long long g_bucket_launch[4];
+__device__ unsigned long long g_bucket_lmax;
+struct BucketStamp {
+    uint64_t t0;
+    __device__ BucketStamp() : t0(wall_clock64()) {}
+    __device__ void done(uint32_t b, uint32_t m) {
+        __syncthreads();
+        if (threadIdx.x != 0) return;
+        const unsigned long long dt = wall_clock64() - t0;
+        unsigned long long *w = g_bucket_stamps + (size_t)b * 4;
+        atomicAdd(w + 0, 1ull);
+        atomicAdd(w + 1, dt);
+        atomicAdd(w + 2, (unsigned long long)m);
+        atomicMax(w + 3, dt);
+        atomicMax(&g_bucket_lmax, (dt << 20) | m);
+        __threadfence();
+        if (atomicAdd(&g_bucket_launch[3], 1ull) == (unsigned long long)gridDim.x - 1) {
+            __threadfence();
+            const unsigned long long mx = atomicExch(&g_bucket_lmax, 0ull);
+            atomicAdd(&g_bucket_launch[0], 1ull);
+            atomicAdd(&g_bucket_launch[1], mx >> 20);
+            atomicAdd(&g_bucket_launch[2], mx & 0xFFFFFull);
+            g_bucket_launch[3] = 0;
+        }
+    }
+};
+extern "C" int dv_debug_bucket_stamps(uint64_t *out, uint64_t *launch) {
+    if (!out || !launch) return DV_ERR_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return DV_ERR_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bucket_stamps), 1024 * 4 * 8) != hipSuccess) return DV_ERR_HIP;
+    if (hipMemcpyFromSymbol(launch, HIP_SYMBOL(g_bucket_launch), 4 * 8) != hipSuccess) return DV_ERR_HIP;
+    static const unsigned long long zero[1024 * 4] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bucket_stamps), zero, sizeof(zero)) != hipSuccess) return DV_ERR_HIP;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_bucket_launch), zero, 4 * 8) != hipSuccess) return DV_ERR_HIP;
+    return DV_OK;
+}
+#endif
+
 __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint64_t *__restrict__ in, uint64_t *__restrict__ out,
                                                                 const uint32_t *__restrict__ digit_tot,
                                                                 uint32_t hmul, int hbits, int hi_bits) {
+#ifdef DVCC_BUCKET_STAMPS
+    BucketStamp stamp_;
+    struct StampAtExit {
+        BucketStamp &s;
+        uint32_t b, m;
+        __device__ ~StampAtExit() { s.done(b, m); }
+    } stamp_exit_{stamp_, blockIdx.x, 0u};
+#endif
     __shared__ uint32_t tg[2][kBucketCap];
     __shared__ uint32_t wc[kBucketWaves][kRadix];
     __shared__ uint32_t tot[kRadix], run[kRadix];
@@ -851,6 +907,9 @@ __global__ __launch_bounds__(kBucketThreads) void k_bucket_sort(uint64_t *__rest
 #pragma unroll
     for (int w = 0; w < kBucketWaves; w++) base += s_part[w];
     const uint32_t m = digit_tot[b];
+#ifdef DVCC_BUCKET_STAMPS
+    stamp_exit_.m = m;
+#endif
     if (m <= 1) {  // nothing to order (one key: copied into place)
         if (m == 1 && tid == 0) out[base] = in[base];
         return;

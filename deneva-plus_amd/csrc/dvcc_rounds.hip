@@ -947,6 +947,11 @@ constexpr uint32_t TW_OK = 1u << 8;  // one more access OK
 // the iteration's work (decide, compact, publish, barriers), [6] back-off,
 // [7] iterations that decided something; read by dv_debug_async_stamps
 __device__ unsigned long long g_async_stamps[kAsyncGroups * 8];
+// per launch: [0] launches, [1] the sum over launches of the most iterations
+// any of its workgroups ran, [2] the sum of its workgroups' mean iterations
+// (x 1024), [3] the last-workgroup ticket (reset per launch)
+__device__ unsigned long long g_async_launch[4];
+__device__ unsigned int g_async_lsum;
 #endif
 // the status fact of txn t
 __device__ __forceinline__ uint8_t fact_status(const uint32_t *tword, uint32_t t) {
@@ -1221,6 +1226,20 @@ __device__ __forceinline__ void async_slices(const RoundBufs &b, const uint32_t 
         atomicAdd(w + 5, (unsigned long long)st_work);
         atomicAdd(w + 6, (unsigned long long)st_sleep);
         atomicAdd(w + 7, (unsigned long long)st_moved);
+        // the launch's mean against its maximum: the last workgroup to get
+        // here adds the launch's record (every other's atomicMax is older)
+        const unsigned int done_it = it + (it < max_iters ? 1u : 0u);
+        atomicMax(&ctr->async_iters, it);
+        atomicAdd(&g_async_lsum, done_it);
+        __threadfence();
+        if (atomicAdd(&g_async_launch[3], 1ull) == (unsigned long long)G - 1) {
+            __threadfence();
+            const unsigned int sum = atomicExch(&g_async_lsum, 0u);
+            atomicAdd(&g_async_launch[0], 1ull);
+            atomicAdd(&g_async_launch[1], (unsigned long long)atomicAdd(&ctr->async_iters, 0u) + 1ull);
+            atomicAdd(&g_async_launch[2], (unsigned long long)sum * 1024ull / G);
+            g_async_launch[3] = 0;
+        }
     }
 #endif
     if (tid == 0) {
@@ -1496,6 +1515,15 @@ extern "C" int dv_debug_async_stamps(uint64_t *out, uint32_t n) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_async_stamps), n * 8) != hipSuccess) return DV_ERR_HIP;
     static const unsigned long long zero[kAsyncGroups * 8] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_async_stamps), zero, sizeof(zero)) != hipSuccess) return DV_ERR_HIP;
+    return DV_OK;
+}
+// ... and the per-launch record (4 words), reset
+extern "C" int dv_debug_async_launches(uint64_t *out) {
+    if (!out) return DV_ERR_ARG;
+    if (hipDeviceSynchronize() != hipSuccess) return DV_ERR_HIP;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_async_launch), 4 * 8) != hipSuccess) return DV_ERR_HIP;
+    static const unsigned long long zero[4] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_async_launch), zero, sizeof(zero)) != hipSuccess) return DV_ERR_HIP;
     return DV_OK;
 }
 #endif

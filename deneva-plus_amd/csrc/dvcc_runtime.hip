@@ -2043,7 +2043,8 @@ int small_enqueue(dv_ctx *c, const dv_epoch_dev *ep) {
 // the kill (run_part); epoch groups (route) vote on the decider's outcome
 // instead, and hand their 32-bit rows over as the 4-byte records.
 bool tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep) {
-    return prefix_applies(c, ep) && ep->txn_begin && !ep->n_acc_dev && !ep->tables &&
+    // (a device-side access count: the closed loop's tb-form epochs, loop_tb)
+    return prefix_applies(c, ep) && ep->txn_begin && (!ep->n_acc_dev || ep->recs32) && !ep->tables &&
            (!c->keys32 || ep->recs32) && (!c->rep_P || c->route) && (ep->keys || ep->recs32);
 }
 
@@ -2191,7 +2192,7 @@ int run_prefix_epoch(dv_ctx *c, const dv_epoch_dev *ep) {
                         ep->n_txn, K,
                         c->slog, c->pairs[0], c->tlen, c->acc_row, c->ctr,
                         c->cfg.cc_alg == DV_WAIT_DIE ? ep->ts : nullptr, ktiming(c) ? c->ev[kEvProbe0] : nullptr,
-                        ktiming(c) ? c->ev[kEvProbe1] : nullptr);
+                        ktiming(c) ? c->ev[kEvProbe1] : nullptr, ep->n_acc_dev);
     else
         launch_probe(c->stream, make_tables(c), ep->keys, ep->types, ep->acc_txn, ep->tables, ep->n_acc, ep->n_txn,
                      c->slog, c->pairs[0], c->tb_start, c->tb_end, c->tlen, c->acc_row, c->ctr, nullptr, K,
@@ -2939,18 +2940,45 @@ int dv_tpcc_epoch_run_device_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
 
 namespace {
 
+// The closed loop's epochs in tb form: every buffer carries 4-byte records and
+// txn boundaries (dv_epoch_dev::recs32, txn_begin), the pool records, and no
+// table bytes.  The refill then writes that form -- 4 B per access and 4 per
+// txn -- and, only when the epochs do not take the prefix-kill path (whose tb
+// mode reads nothing else: k_probe_tb probes the prefix, the kill pass the
+// later keys), also keys / types / txn ids (8 + 1 + 4 B).
+struct LoopForm {
+    bool tb = false, old = true;
+};
+LoopForm loop_form(const dv_ctx *c, const dv_epoch_dev *pool, const dv_epoch_dev *bufs, uint32_t n_bufs,
+                   uint32_t n_txn) {
+    LoopForm f;
+    if (std::getenv("DVCC_LOOP_NO_TB") || !pool->recs32 || pool->tables) return f;
+    for (uint32_t b = 0; b < n_bufs; b++)
+        if (!bufs[b].recs32 || !bufs[b].txn_begin) return f;
+    dv_epoch_dev d = bufs[0];
+    d.n_txn = n_txn;
+    d.tables = nullptr;
+    f.tb = true;
+    f.old = !tb_epoch(c, &d);
+    return f;
+}
+
 // the closed loop's next epoch (launch_refill) into `out`: prev's aborted txns
-// (prev: the epoch the context decided last; NULL: none, all fresh), then fresh
-// ones from the pool
-void enqueue_refill(dv_ctx *c, const dv_epoch_dev *prev, const dv_epoch_dev *pool, const uint32_t *pool_begin,
-                    uint32_t *cursor, uint32_t n_out, const dv_epoch_dev &out) {
+// (prev: the epoch the context decided last, prev_buf: its buffer; NULL: none,
+// all fresh), then fresh ones from the pool, in the forms f names
+void enqueue_refill(dv_ctx *c, const dv_epoch_dev *prev, const dv_epoch_dev *prev_buf, const dv_epoch_dev *pool,
+                    const uint32_t *pool_begin, uint32_t *cursor, uint32_t n_out, const dv_epoch_dev &out,
+                    LoopForm f = {}) {
     launch_refill(c->stream, c->status, c->rs, c->re, prev ? prev->n_txn : 0u,
-                  prev ? prev->keys : nullptr, prev ? prev->types : nullptr, prev ? prev->tables : nullptr,
-                  pool->keys, pool->types, pool->tables, pool->acc_txn, pool_begin, pool->n_txn, cursor, n_out,
-                  (uint64_t)n_out * pool->max_txn_acc, const_cast<uint64_t *>(out.keys),
-                  const_cast<uint8_t *>(out.types), const_cast<uint32_t *>(out.acc_txn),
-                  const_cast<uint8_t *>(out.tables), const_cast<uint32_t *>(out.n_acc_dev), c->carry_b,
-                  c->carry_b + c->carry_nb, c->carry_tot, prev ? c->ctr : nullptr);
+                  prev && f.old ? prev->keys : nullptr, prev && f.old ? prev->types : nullptr,
+                  prev && f.old ? prev->tables : nullptr, pool->keys, pool->types, pool->tables, pool->acc_txn,
+                  pool_begin, pool->n_txn, cursor, n_out, (uint64_t)n_out * pool->max_txn_acc,
+                  f.old ? const_cast<uint64_t *>(out.keys) : nullptr, const_cast<uint8_t *>(out.types),
+                  const_cast<uint32_t *>(out.acc_txn), const_cast<uint8_t *>(out.tables),
+                  const_cast<uint32_t *>(out.n_acc_dev), c->carry_b, c->carry_b + c->carry_nb, c->carry_tot,
+                  prev ? c->ctr : nullptr, f.tb && prev_buf ? prev_buf->recs32 : nullptr,
+                  f.tb ? pool->recs32 : nullptr, f.tb ? const_cast<uint32_t *>(out.recs32) : nullptr,
+                  f.tb ? const_cast<uint32_t *>(out.txn_begin) : nullptr);
 }
 
 }  // namespace
@@ -2975,9 +3003,11 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
     HIPCHK(hipSetDevice(c->cfg.device));
     int r = carry_bufs(c, carry_blocks(n_txn));
     if (r) return r;
+    const LoopForm form = loop_form(c, pool, bufs, 2, n_txn);
     // epoch k's descriptor: buffer k & 1, its access count on the device
     auto desc = [&](uint32_t k) {
         dv_epoch_dev d = bufs[k & 1];
+        if (form.old) d.txn_begin = d.recs32 = nullptr;  // (the engine reads the old form)
         d.tables = pool->tables ? bufs[k & 1].tables : nullptr;
         d.n_txn = n_txn;
         d.n_acc = bound;
@@ -2992,7 +3022,7 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
         (void)hipStreamSynchronize(c->stream);
         return e;
     };
-    if (!resume) enqueue_refill(c, nullptr, pool, pool_begin, cursor, n_txn, bufs[0]);
+    if (!resume) enqueue_refill(c, nullptr, nullptr, pool, pool_begin, cursor, n_txn, bufs[0], form);
     const dv_epoch_dev d0 = desc(0);
     const bool pipelined = prefix_applies(c, &d0) && !timing(c) && !ktiming(c) && !c->rep_P;
     EpochSnap snap[2];
@@ -3002,7 +3032,7 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
         const dv_epoch_dev d = desc(k);
         int e = dv_epoch_run_device(c, &d, commit_of(k), nullptr, stats_of(k));
         if (!e) {
-            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1]);
+            enqueue_refill(c, &d, &bufs[k & 1], pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1], form);
             e = hip_fail(hipGetLastError(), "refill");
         }
         return e;
@@ -3019,7 +3049,7 @@ int dv_epoch_run_closed_loop(dv_ctx *c, const dv_epoch_dev *pool, const uint32_t
         if (!r) {
             // behind the execution: epoch k + 1 from epoch k's final statuses (a
             // no-op when k halted -- the host redoes both below)
-            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1]);
+            enqueue_refill(c, &d, &bufs[k & 1], pool, pool_begin, cursor, n_txn, bufs[(k + 1) & 1], form);
             r = hip_fail(hipGetLastError(), "refill");
         }
         if (r) {
@@ -3098,11 +3128,13 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
         r = carry_bufs(lanes[l], carry_blocks(n_txn));
         if (r) return r;
     }
+    const LoopForm form = loop_form(c0, pool, bufs, 2 * n_lanes, n_txn);
     // lane l's j-th epoch of this call (global k = j * L + l) sits in buffer
     // 2l + (j & 1); its refill writes 2l + ((j + 1) & 1)
     auto buf_of = [&](uint32_t k, uint32_t ahead) { return &bufs[2 * (k % n_lanes) + (((k / n_lanes) + ahead) & 1)]; };
     auto desc = [&](uint32_t k) {
         dv_epoch_dev d = *buf_of(k, 0);
+        if (form.old) d.txn_begin = d.recs32 = nullptr;  // (the engine reads the old form)
         d.tables = pool->tables ? d.tables : nullptr;
         d.n_txn = n_txn;
         d.n_acc = bound;
@@ -3114,7 +3146,7 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
     if (!resume)  // each lane's first epoch: fresh txns, drawn in lane order
         for (uint32_t l = 0; l < n_lanes; l++) {
             dv_ctx *c = lanes[l];
-            enqueue_refill(c, nullptr, pool, pool_begin, cursor, n_txn, *buf_of(l, 0));
+            enqueue_refill(c, nullptr, nullptr, pool, pool_begin, cursor, n_txn, *buf_of(l, 0), form);
             HIPCHK(hipGetLastError());
             HIPCHK(hipStreamSynchronize(c->stream));
         }
@@ -3129,7 +3161,7 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
         },
         [&](dv_ctx *c, uint32_t k) {  // (behind the execution; a no-op when k halted)
             const dv_epoch_dev d = desc(k);
-            enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, *buf_of(k, 1));
+            enqueue_refill(c, &d, buf_of(k, 0), pool, pool_begin, cursor, n_txn, *buf_of(k, 1), form);
             return hip_fail(hipGetLastError(), "refill");
         },
         [&](uint32_t k, dv_stats *st) {  // (synchronous, refill included: the next refill, on
@@ -3138,7 +3170,7 @@ int dv_epoch_run_closed_loop_lanes(dv_ctx *const *lanes, uint32_t n_lanes, const
             const dv_epoch_dev d = desc(k);
             int e = dv_epoch_run_device(c, &d, commit_of(k), nullptr, st);
             if (!e) {
-                enqueue_refill(c, &d, pool, pool_begin, cursor, n_txn, *buf_of(k, 1));
+                enqueue_refill(c, &d, buf_of(k, 0), pool, pool_begin, cursor, n_txn, *buf_of(k, 1), form);
                 e = hip_fail(hipGetLastError(), "refill");
             }
             if (!e) e = hip_fail(hipStreamSynchronize(c->stream), "sync");

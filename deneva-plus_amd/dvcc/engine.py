@@ -144,9 +144,12 @@ class DeviceEpoch:
 
 
 class ClosedLoopBufs:
-    """The closed loop's two epoch buffers (dv_epoch_run_closed_loop)."""
+    """The closed loop's two epoch buffers (dv_epoch_run_closed_loop).  With
+    n_txn (and no table bytes) they also hold the tb form -- 4-byte records and
+    txn boundaries -- which the refill then writes instead of keys / types /
+    txn ids when the pool has records too (the engine's tb-mode path)."""
 
-    def __init__(self, cap, tables, device):
+    def __init__(self, cap, tables, device, n_txn=None):
         import torch
         self.cap = int(cap)
         n = max(1, self.cap)
@@ -155,24 +158,47 @@ class ClosedLoopBufs:
         self.acc_txn = [torch.empty(n, dtype=torch.int32, device=device) for _ in range(2)]
         self.tables = [torch.empty(n, dtype=torch.uint8, device=device) for _ in range(2)] if tables else None
         self.n_acc = [torch.zeros(1, dtype=torch.int32, device=device) for _ in range(2)]
+        tb = n_txn is not None and not tables
+        self.recs32 = [torch.empty(n, dtype=torch.int32, device=device) for _ in range(2)] if tb else None
+        self.txn_begin = ([torch.zeros(int(n_txn) + 1, dtype=torch.int32, device=device) for _ in range(2)]
+                          if tb else None)
+        self.tb = False  # (set by the engine: the last call wrote the tb form)
 
     def desc(self, b):
         return L.EpochDev(self.keys[b].data_ptr(), self.types[b].data_ptr(), self.acc_txn[b].data_ptr(),
                           self.tables[b].data_ptr() if self.tables is not None else None, 0, 0, 0, None,
-                          self.n_acc[b].data_ptr())
+                          self.n_acc[b].data_ptr(),
+                          self.txn_begin[b].data_ptr() if self.txn_begin is not None else None,
+                          self.recs32[b].data_ptr() if self.recs32 is not None else None)
 
     def swap(self):
         """after a call of n_epochs odd: the next epoch moves to buffer 0"""
-        for a in (self.keys, self.types, self.acc_txn, self.tables, self.n_acc):
+        for a in (self.keys, self.types, self.acc_txn, self.tables, self.n_acc, self.recs32, self.txn_begin):
             if a is not None:
                 a.reverse()
 
     def epoch(self, b, n_txn, max_txn_acc):
         """buffer b's epoch as a DeviceEpoch (reads its access count)"""
+        import torch
         n = int(self.n_acc[b].item())
+        if self.tb:  # (keys / types / txn ids from the tb form)
+            r = self.recs32[b][:n].to(torch.int64) & 0xFFFFFFFF
+            keys = r & 0x7FFFFFFF
+            types = (r >> 31).to(torch.uint8)
+            tb = self.txn_begin[b][:n_txn + 1].to(torch.int64)
+            acc_txn = torch.repeat_interleave(torch.arange(n_txn, device=keys.device, dtype=torch.int32),
+                                              tb[1:] - tb[:-1])
+            return DeviceEpoch.from_tensors(keys, types, acc_txn, n_txn, max_txn_acc=max_txn_acc)
         return DeviceEpoch.from_tensors(self.keys[b][:n], self.types[b][:n], self.acc_txn[b][:n], n_txn,
                                         tables=self.tables[b][:n] if self.tables is not None else None,
                                         max_txn_acc=max_txn_acc)
+
+
+def _loop_tb(pool, bufs):
+    """dv_epoch_run_closed_loop writes the tb form (loop_tb, dvcc_runtime.hip)"""
+    import os
+    return (not os.environ.get("DVCC_LOOP_NO_TB") and getattr(pool, "recs32", None) is not None
+            and pool.tables is None and all(b.recs32 is not None for b in bufs))
 
 
 class CCEngine:
@@ -588,7 +614,8 @@ class CCEngine:
         if cursor is None:
             cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         if bufs is None:
-            bufs = ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev)
+            bufs = ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev, n_txn=n_txn)
+        bufs.tb = _loop_tb(pool, [bufs])
         arr = (L.EpochDev * 2)(*[bufs.desc(b) for b in range(2)])
         if d_commits is None or not isinstance(d_commits, (list, tuple)):
             d_commits = [d_commits] * n_epochs
@@ -616,7 +643,11 @@ class CCEngine:
         if cursor is None:
             cursor = torch.zeros(1, dtype=torch.int32, device=dev)
         if bufs is None:
-            bufs = [ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev) for _ in range(nl)]
+            bufs = [ClosedLoopBufs(n_txn * pool.max_txn_acc, pool.tables is not None, dev, n_txn=n_txn)
+                    for _ in range(nl)]
+        tb = _loop_tb(pool, bufs)
+        for b in bufs:
+            b.tb = tb
         arr = (L.EpochDev * (2 * nl))(*[b.desc(i) for b in bufs for i in range(2)])
         if d_commits is None or not isinstance(d_commits, (list, tuple)):
             d_commits = [d_commits] * n_epochs

@@ -28,12 +28,16 @@ eng.load_ycsb_partition(rows)
 d = torch.zeros(n_txn, dtype=torch.uint8, device="cuda")
 lib = L.lib()
 lib.dv_debug_async_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+lib.dv_debug_async_launches.argtypes = [ctypes.c_void_p]
+lrec = np.zeros(4, np.uint64)
 buf = np.zeros(512 * 8, np.uint64)
 eng.run_epochs_device([deps[i % 3] for i in range(6)], d)
 assert lib.dv_debug_async_stamps(buf.ctypes.data, buf.size) == 0
+assert lib.dv_debug_async_launches(lrec.ctypes.data) == 0
 sts = eng.run_epochs_device([deps[i % 3] for i in range(epochs)], d)
 torch.cuda.synchronize()
 assert lib.dv_debug_async_stamps(buf.ctypes.data, buf.size) == 0
+assert lib.dv_debug_async_launches(lrec.ctypes.data) == 0
 w = buf.reshape(512, 8).astype(np.float64)
 used = w[:, 0] > 0
 w = w[used]
@@ -47,6 +51,9 @@ out = {"epochs": epochs, "workgroups": int(used.sum()), "launches_per_wg": float
        "per_iteration_us": {"facts": float(tot[3] / it * tick_us), "carry_walk": float(tot[4] / it * tick_us),
                             "work": float(tot[5] / it * tick_us), "backoff": float(tot[6] / it * tick_us)},
        "moved_frac": float(tot[7] / it),
+       "per_launch": {"launches": int(lrec[0]),
+                      "mean_of_wg_iterations": float(lrec[2]) / 1024.0 / max(1, int(lrec[0])),
+                      "max_wg_iterations": float(lrec[1]) / max(1, int(lrec[0]))},
        "rounds_mean": float(np.mean([s.rounds for s in sts])),
        "async_live_per_epoch": float(np.mean([s.async_live for s in sts]))}
 print(json.dumps(out))
