@@ -50,6 +50,15 @@
  *                               for the committed txns
  *   dv_load_table_cols /        row_t::set_value / get_value on the mutated TPC-C
  *   dv_read_table_col           columns (storage/row.cpp:95-180)
+ *   dv_tpcc_gen_queries /       TPCCQueryGenerator::gen_payment / gen_new_order's TPCCQuery
+ *   dv_tpcc_expand              (tpcc_query.cpp:150-263), then TPCCTxnManager's access lists
+ *   dv_wire_open / _decode /    the server's receive path: Transport::recv_msg ->
+ *   dv_wire_decode_batches      Message::create_messages -> *ClientQueryMessage::copy_from_buf
+ *                               (transport/transport.cpp:245-300; transport/message.cpp:29-59,
+ *                               493-510, 620-655, 889-903) into an epoch's host arrays
+ *   dv_wire_respond             CL_RSP / CALVIN_ACK replies (worker_thread.cpp:127-152;
+ *                               message.cpp:921-949, 1057-1110) packed as MessageThread does
+ *                               (transport/msg_thread.cpp:53-111)
  *
  * Decisions follow SURVEY.md 8.0 ("E-schedule"): commit/abort of every txn and
  * the final table state equal a single worker thread running the same epoch
