@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <chrono>
+
 #include "dvcc.h"
 
 namespace dvcc {
@@ -20,6 +22,22 @@ extern thread_local KProf *tl_kprof;
 // epoch graphs (dvcc_runtime.hip): while a captured epoch is replayed, the
 // host walks the same enqueue code for its state with every launch skipped
 extern thread_local bool tl_dry;
+// DVCC_HOST_PROF (run_lanes): host time inside the launch calls themselves
+extern thread_local bool tl_hprof;
+extern thread_local double tl_hp_launch_s;
+extern thread_local uint32_t tl_hp_launch_n;
+struct HpTimer {
+    bool on;
+    std::chrono::steady_clock::time_point t0;
+    HpTimer() : on(tl_hprof) {
+        if (on) t0 = std::chrono::steady_clock::now();
+    }
+    ~HpTimer() {
+        if (!on) return;
+        tl_hp_launch_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        tl_hp_launch_n++;
+    }
+};
 // a fresh event pair for one launch of `kernel` (both null when the pool is spent)
 void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1);
 // events the caller owns and records itself (the probe / scatter / pass
@@ -43,6 +61,7 @@ class KProfScope {
         if (::dvcc::tl_dry) break;                                                                           \
         hipEvent_t dv_e0_ = nullptr, dv_e1_ = nullptr;                                                       \
         if (::dvcc::tl_kprof) ::dvcc::kprof_events(#kernel, &dv_e0_, &dv_e1_);                              \
+        ::dvcc::HpTimer dv_hp_;                                                                              \
         hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), shm, stream, dv_e0_, dv_e1_, 0, __VA_ARGS__); \
     } while (0)
 // the same with the caller's own events (may be null)
@@ -54,6 +73,7 @@ class KProfScope {
             if (dv_e0_ && dv_e1_) ::dvcc::kprof_add(#kernel, dv_e0_, dv_e1_);                                \
             else ::dvcc::kprof_events(#kernel, &dv_e0_, &dv_e1_);                                            \
         }                                                                                                    \
+        ::dvcc::HpTimer dv_hp_;                                                                              \
         hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), shm, stream, dv_e0_, dv_e1_, 0, __VA_ARGS__); \
     } while (0)
 

@@ -277,6 +277,9 @@ struct dv_ctx {
 namespace dvcc {
 thread_local KProf *tl_kprof = nullptr;
 thread_local bool tl_dry = false;
+thread_local bool tl_hprof = false;
+thread_local double tl_hp_launch_s = 0;
+thread_local uint32_t tl_hp_launch_n = 0;
 
 void kprof_events(const char *kernel, hipEvent_t *e0, hipEvent_t *e1) {
     KProf *p = tl_kprof;
@@ -2661,6 +2664,7 @@ GraphKeyX lanes_key(dv_ctx *const *lanes, uint32_t n_lanes, const void *commit, 
 template <class Commit, class Pipelined, class Decide, class After, class Run>
 int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts, Commit &&commit_of,
               Pipelined &&pipelined, Decide &&decide, After &&after, Run &&run) {
+    const auto t_enter = std::chrono::steady_clock::now();
     HIPCHK(hipSetDevice(lanes[0]->cfg.device));
     int r0 = lane_streams(lanes, n_lanes);
     if (r0) return r0;
@@ -2708,6 +2712,9 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     double t_queue = 0, t_wait = 0, t_decide = 0;
     tl_hp_walk = tl_hp_glaunch = 0;
     tl_hp_replays = tl_hp_captures = 0;
+    tl_hprof = hprof;
+    tl_hp_launch_s = 0;
+    tl_hp_launch_n = 0;
     const auto t_all = hclock::now();
     // read back the oldest queued epoch; a halted one and all behind it run again
     auto settle = [&]() -> int {
@@ -2821,8 +2828,15 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     t_wait += std::chrono::duration<double>(hclock::now() - tw).count();
     if (hprof && n)
         std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f (decision %.1f), "
-                     "waiting %.1f\n", n, n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
-                     t_queue * 1e6 / n, t_decide * 1e6 / n, t_wait * 1e6 / n);
+                     "waiting %.1f; %.1f us of set-up before the first epoch\n", n, n_lanes,
+                     std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
+                     t_queue * 1e6 / n, t_decide * 1e6 / n, t_wait * 1e6 / n,
+                     std::chrono::duration<double>(t_all - t_enter).count() * 1e6);
+    tl_hprof = false;
+    if (hprof && n)
+        std::fprintf(stderr, "dvcc host: %.1f kernel launches per epoch, %.2f us of host time each (%.1f us per "
+                     "epoch)\n", (double)tl_hp_launch_n / n, tl_hp_launch_n ? tl_hp_launch_s * 1e6 / tl_hp_launch_n : 0.0,
+                     tl_hp_launch_s * 1e6 / n);
     if (hprof && tl_hp_replays)
         std::fprintf(stderr, "dvcc host: %u graph replays (%u captures): walk %.1f us, hipGraphLaunch %.1f us each\n",
                      tl_hp_replays, tl_hp_captures, tl_hp_walk * 1e6 / tl_hp_replays,

@@ -134,13 +134,24 @@ class DeviceEpoch:
                                 max_txn_acc=max(first.max_txn_acc, second.max_txn_acc))
 
     def desc(self):
+        """the dv_epoch_dev of these buffers (kept while the same tensor
+        objects and sizes stand: the pipelined entry points take one per
+        epoch, and data_ptr() is a few microseconds a call)"""
         ts = getattr(self, "ts", None)
         tb = getattr(self, "txn_begin", None)
         r32 = getattr(self, "recs32", None)
-        return L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
-                          self.tables.data_ptr() if self.tables is not None else None,
-                          self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None,
-                          None, tb.data_ptr() if tb is not None else None, r32.data_ptr() if r32 is not None else None)
+        key = (id(self.keys), id(self.types), id(self.acc_txn), id(self.tables), id(ts), id(tb), id(r32),
+               self.n_acc, self.n_txn, self.max_txn_acc)
+        memo = getattr(self, "_desc_memo", None)
+        if memo is not None and memo[0] == key:
+            return memo[1]
+        d = L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
+                       self.tables.data_ptr() if self.tables is not None else None,
+                       self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None,
+                       None, tb.data_ptr() if tb is not None else None, r32.data_ptr() if r32 is not None else None)
+        # (the tensors themselves are held too, so no id above can be reused by a new object)
+        self._desc_memo = (key, d, (self.keys, self.types, self.acc_txn, self.tables, ts, tb, r32))
+        return d
 
 
 class ClosedLoopBufs:
@@ -199,6 +210,27 @@ def _loop_tb(pool, bufs):
     import os
     return (not os.environ.get("DVCC_LOOP_NO_TB") and getattr(pool, "recs32", None) is not None
             and pool.tables is None and all(b.recs32 is not None for b in bufs))
+
+
+def _after_torch_all(engines):
+    """CCEngine._after_torch for several contexts: one event recorded on
+    torch's current stream, every other context's stream waits on it"""
+    import sys
+    torch = sys.modules.get("torch")
+    if torch is None or not torch.cuda.is_initialized():
+        return
+    cur = torch.cuda.current_stream()
+    ev = None
+    for e in engines:
+        sp = e.stream_ptr or 0
+        if sp == cur.cuda_stream:
+            continue
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(cur)
+        if getattr(e, "_ext", None) is None or e._ext.cuda_stream != sp:
+            e._ext = torch.cuda.ExternalStream(sp)
+        e._ext.wait_event(ev)
 
 
 class CCEngine:
@@ -498,8 +530,7 @@ class CCEngine:
         epoch k decided on context k % len, executions in epoch order; same
         results as run_epochs_device.  Returns the list of stats."""
         ctxs = [self] + list(lanes)
-        for e in ctxs:
-            e._after_torch()
+        _after_torch_all(ctxs)
         n = len(deps)
         arr = (L.EpochDev * n)(*[d.desc() for d in deps])
         if d_commits is None or not isinstance(d_commits, (list, tuple)):

@@ -714,6 +714,34 @@ def test_lsd_sort_knob(cc):
         _check(cc, rows, eps, prefix=3000, lsd_sort=True)
 
 
+def _repeat_epoch(rows, n_txn, seed, R=6):
+    """txns that touch some row two or three times (mixed types): round 0's
+    repeats -- transparent, the group's first access carrying the OR of the
+    types"""
+    rng = np.random.default_rng(seed)
+    keys = rng.integers(0, rows, size=(n_txn, R)).astype(np.uint64)
+    keys[:, 3] = keys[:, 1]
+    keys[::3, 5] = keys[::3, 1]
+    types = (rng.random((n_txn, R)) < 0.3).astype(np.uint8)
+    tb = (np.arange(n_txn + 1) * R).astype(np.uint32)
+    return Epoch(keys.reshape(-1), types.reshape(-1), tb)
+
+
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("lsd", [False, True])
+def test_small_sorts_round0(cc, lsd):
+    """round 0 behind the small sorts (bucket sort, or DV_FLAG_LSD_SORT's
+    passes): zipf, repeat-access and one-hot-row epochs, two txns; whole
+    epochs and prefix-kill stages, asynchronous rounds and synchronous"""
+    rows = 1 << 20
+    g = YCSBQueryGenerator(rows, zipf_theta=0.9)
+    eps = [g.gen(30_000, 151), _repeat_epoch(1 << 12, 9_000, 152), _hot_read_epoch(rows, 20_000, 9),
+           g.gen(2, 153)]
+    _check(cc, rows, eps, prefix=None, lsd_sort=lsd)
+    _check(cc, rows, eps, prefix=3000, lsd_sort=lsd)
+    _check(cc, rows, eps[:2], prefix=None, lsd_sort=lsd, asynchronous=False, tail=False)
+
+
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
 def test_medium_epoch_without_tail(cc):
     g = YCSBQueryGenerator(1 << 20, zipf_theta=0.9)

@@ -96,7 +96,28 @@ for t, dlt in pts:
     hist[lv] = hist.get(lv, 0) + (t - last) * us
     lv += dlt
     last = t
+# a short call (the driver's 20 epochs): every epoch's clear / decided /
+# turn / posted, in us from the call's first stamp, lane by lane
+timeline = None
+if epochs <= 40:
+    t_min = ts.min()
+    timeline = {}
+    for c, li in lane_ids.items():
+        m = ctx == c
+        order = np.argsort(ts[m], kind="stable")
+        rows_l, cur = [], None
+        for e, t in zip(ev[m][order].tolist(), ts[m][order].tolist()):
+            if e == 0:
+                if cur:
+                    rows_l.append(cur)
+                cur = [round((t - t_min) * us, 1), None, None, None]
+            elif cur is not None:
+                cur[e] = round((t - t_min) * us, 1)
+        if cur:
+            rows_l.append(cur)
+        timeline[str(li)] = rows_l
 out = {"epochs": epochs, "lanes": nl, "ms_per_epoch_host": el / epochs * 1e3, "stamp_span_us": span,
+       "timeline": timeline,
        "us_per_epoch_device": span / epochs, "lane_epochs": per_lane,
        "mean_us": {k: float(np.mean(v)) for k, v in phases.items() if v},
        "p90_us": {k: float(np.percentile(v, 90)) for k, v in phases.items() if v},
