@@ -2611,25 +2611,40 @@ int lanes_own_queues(dv_ctx *const *lanes, uint32_t n_lanes) {
 
 // while a lanes call runs each lane works on its masked stream, ordered after
 // the caller's stream at the start, and the caller's after it at the end
+// nothing queued on s is unfinished (a "not ready" answer is not left
+// behind as the thread's last error)
+bool stream_idle(hipStream_t s) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipErrorNotReady && hipPeekAtLastError() == hipErrorNotReady) (void)hipGetLastError();
+    return q == hipSuccess;
+}
+
 struct OnLaneStreams {
     dv_ctx *const *ls;
     uint32_t n;
     hipStream_t saved[kMaxLanes];
     uint32_t saved_g[kMaxLanes];
+    // (a stream with nothing unfinished needs no event: what it ran is
+    // visible to every later launch -- the common case at both ends of a
+    // pipelined call, whose event pairs cost the host ~10 us per lane)
     OnLaneStreams(dv_ctx *const *l, uint32_t m) : ls(l), n(m) {
         for (uint32_t i = 0; i < n; i++) {
             saved[i] = ls[i]->stream;
             saved_g[i] = ls[i]->async_g;
-            (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
-            (void)hipStreamWaitEvent(ls[i]->lane_stream, ls[i]->lane_ev, 0);
+            if (!stream_idle(ls[i]->stream)) {
+                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+                (void)hipStreamWaitEvent(ls[i]->lane_stream, ls[i]->lane_ev, 0);
+            }
             ls[i]->stream = ls[i]->lane_stream;
             ls[i]->async_g = ls[i]->lane_g;
         }
     }
     ~OnLaneStreams() {
         for (uint32_t i = 0; i < n; i++) {
-            (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
-            (void)hipStreamWaitEvent(saved[i], ls[i]->lane_ev, 0);
+            if (!stream_idle(ls[i]->stream)) {
+                (void)hipEventRecord(ls[i]->lane_ev, ls[i]->stream);
+                (void)hipStreamWaitEvent(saved[i], ls[i]->lane_ev, 0);
+            }
             ls[i]->stream = saved[i];
             ls[i]->async_g = saved_g[i];
         }
@@ -2668,7 +2683,20 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
     HIPCHK(hipSetDevice(lanes[0]->cfg.device));
     int r0 = lane_streams(lanes, n_lanes);
     if (r0) return r0;
+    // DVCC_HOST_PROF: the host time from the last read-back to the return
+    // (the lane streams handed back below), printed on the way out
+    struct ExitProf {
+        bool on = false;
+        std::chrono::steady_clock::time_point t0;
+        ~ExitProf() {
+            if (on)
+                std::fprintf(stderr, "dvcc host: %.1f us from the last read-back to the return\n",
+                             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e6);
+        }
+    } exit_prof_;
+    const auto t_streams = std::chrono::steady_clock::now();
     OnLaneStreams on_lanes_(lanes, n_lanes);
+    const double us_streams = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_streams).count() * 1e6;
     auto stats_of = [&](uint32_t k) { return sts ? &sts[k] : nullptr; };
     auto lane_of = [&](uint32_t k) { return lanes[k % n_lanes]; };
     struct Pend {
@@ -2826,12 +2854,16 @@ int run_lanes(dv_ctx *const *lanes, uint32_t n_lanes, uint32_t n, dv_stats *sts,
         if (r) return r;
     }
     t_wait += std::chrono::duration<double>(hclock::now() - tw).count();
+    if (hprof) {
+        exit_prof_.on = true;
+        exit_prof_.t0 = hclock::now();
+    }
     if (hprof && n)
         std::fprintf(stderr, "dvcc host: %u epochs over %u lanes, %.1f us per epoch: queueing %.1f (decision %.1f), "
-                     "waiting %.1f; %.1f us of set-up before the first epoch\n", n, n_lanes,
-                     std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
+                     "waiting %.1f; %.1f us of set-up before the first epoch (%.1f handing over the streams)\n",
+                     n, n_lanes, std::chrono::duration<double>(hclock::now() - t_all).count() * 1e6 / n,
                      t_queue * 1e6 / n, t_decide * 1e6 / n, t_wait * 1e6 / n,
-                     std::chrono::duration<double>(t_all - t_enter).count() * 1e6);
+                     std::chrono::duration<double>(t_all - t_enter).count() * 1e6, us_streams);
     tl_hprof = false;
     if (hprof && n)
         std::fprintf(stderr, "dvcc host: %.1f kernel launches per epoch, %.2f us of host time each (%.1f us per "

@@ -10,6 +10,9 @@ Everything here is plumbing around libdvcc.so: no decision is computed in
 Python, and nothing falls back to the CPU.
 """
 import ctypes
+import os
+import sys
+import time
 from dataclasses import dataclass
 
 import numpy as np
@@ -75,8 +78,19 @@ class Epoch:
         return a
 
 
+# DVCC_PY_PROF=1: the lanes wrapper's own time around the C call, to stderr
+_PY_PROF = bool(os.environ.get("DVCC_PY_PROF"))
+
+
 class DeviceEpoch:
     """An epoch resident in HBM (torch tensors used as device buffers)."""
+
+    def __setattr__(self, name, value):
+        # every public attribute set bumps the version the descriptor cache
+        # (desc, desc_bytes) is keyed on
+        object.__setattr__(self, name, value)
+        if name[0] != "_":
+            object.__setattr__(self, "_ver", self.__dict__.get("_ver", 0) + 1)
 
     def __init__(self, epoch, device="cuda", txn_begin=True, recs32=True):
         import torch
@@ -134,24 +148,29 @@ class DeviceEpoch:
                                 max_txn_acc=max(first.max_txn_acc, second.max_txn_acc))
 
     def desc(self):
-        """the dv_epoch_dev of these buffers (kept while the same tensor
-        objects and sizes stand: the pipelined entry points take one per
-        epoch, and data_ptr() is a few microseconds a call)"""
+        """the dv_epoch_dev of these buffers (kept until an attribute is set
+        again: the pipelined entry points take one per epoch, and data_ptr()
+        is a few microseconds a call)"""
+        memo = self.__dict__.get("_desc_memo")
+        if memo is not None and memo[0] == self._ver:
+            return memo[1]
         ts = getattr(self, "ts", None)
         tb = getattr(self, "txn_begin", None)
         r32 = getattr(self, "recs32", None)
-        key = (id(self.keys), id(self.types), id(self.acc_txn), id(self.tables), id(ts), id(tb), id(r32),
-               self.n_acc, self.n_txn, self.max_txn_acc)
-        memo = getattr(self, "_desc_memo", None)
-        if memo is not None and memo[0] == key:
-            return memo[1]
         d = L.EpochDev(self.keys.data_ptr(), self.types.data_ptr(), self.acc_txn.data_ptr(),
                        self.tables.data_ptr() if self.tables is not None else None,
                        self.n_acc, self.n_txn, self.max_txn_acc, ts.data_ptr() if ts is not None else None,
                        None, tb.data_ptr() if tb is not None else None, r32.data_ptr() if r32 is not None else None)
-        # (the tensors themselves are held too, so no id above can be reused by a new object)
-        self._desc_memo = (key, d, (self.keys, self.types, self.acc_txn, self.tables, ts, tb, r32))
+        self._desc_memo = (self._ver, d, bytes(d))
         return d
+
+    def desc_bytes(self):
+        """desc() as bytes (cached the same way)"""
+        memo = self.__dict__.get("_desc_memo")
+        if memo is None or memo[0] != self._ver:
+            self.desc()
+            memo = self._desc_memo
+        return memo[2]
 
 
 class ClosedLoopBufs:
@@ -212,6 +231,15 @@ def _loop_tb(pool, bufs):
             and pool.tables is None and all(b.recs32 is not None for b in bufs))
 
 
+def _commit_ptrs(d_commits, n):
+    """the n commit-byte pointers: one device tensor (or None) for every
+    epoch, or a list of them"""
+    if d_commits is None or not isinstance(d_commits, (list, tuple)):
+        p = int(d_commits.data_ptr()) if d_commits is not None else None
+        return (ctypes.c_void_p * n)(*([p] * n))
+    return (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+
+
 def _after_torch_all(engines):
     """CCEngine._after_torch for several contexts: one event recorded on
     torch's current stream, every other context's stream waits on it"""
@@ -220,13 +248,17 @@ def _after_torch_all(engines):
     if torch is None or not torch.cuda.is_initialized():
         return
     cur = torch.cuda.current_stream()
+    if cur.query():  # (nothing queued on it is unfinished: its results are visible to any later launch)
+        return
     ev = None
     for e in engines:
         sp = e.stream_ptr or 0
         if sp == cur.cuda_stream:
             continue
         if ev is None:
-            ev = torch.cuda.Event()
+            ev = getattr(engines[0], "_ev_all", None)
+            if ev is None:
+                ev = engines[0]._ev_all = torch.cuda.Event()
             ev.record(cur)
         if getattr(e, "_ext", None) is None or e._ext.cuda_stream != sp:
             e._ext = torch.cuda.ExternalStream(sp)
@@ -433,10 +465,8 @@ class CCEngine:
         stats."""
         self._after_torch()
         n = len(deps)
-        arr = (L.EpochDev * n)(*[d.desc() for d in deps])
-        if d_commits is None or not isinstance(d_commits, (list, tuple)):
-            d_commits = [d_commits] * n
-        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        arr = self._epoch_array(deps)
+        cps = _commit_ptrs(d_commits, n)
         sts = (L.Stats * n)()
         L.check(L.lib().dv_epoch_run_device_batch(self._ctx, arr, n, cps, sts), "dv_epoch_run_device_batch")
         return list(sts)
@@ -525,21 +555,38 @@ class CCEngine:
             raise errs[0]
         return out
 
+    @staticmethod
+    def _epoch_array(deps):
+        """the dv_epoch_dev array of `deps` (DeviceEpoch: one copy of the
+        descriptors' cached bytes)"""
+        n = len(deps)
+        if all(isinstance(d, DeviceEpoch) for d in deps):
+            return (L.EpochDev * n).from_buffer_copy(b"".join([d.desc_bytes() for d in deps]))
+        return (L.EpochDev * n)(*[d.desc() for d in deps])
+
     def run_epochs_lanes(self, lanes, deps, d_commits=None):
         """dv_epoch_run_device_lanes over [self] + lanes (open_lane):
         epoch k decided on context k % len, executions in epoch order; same
         results as run_epochs_device.  Returns the list of stats."""
+        prof = _PY_PROF and time.perf_counter()
         ctxs = [self] + list(lanes)
         _after_torch_all(ctxs)
+        t_ev = _PY_PROF and time.perf_counter()
         n = len(deps)
-        arr = (L.EpochDev * n)(*[d.desc() for d in deps])
-        if d_commits is None or not isinstance(d_commits, (list, tuple)):
-            d_commits = [d_commits] * n
-        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        arr = self._epoch_array(deps)
+        cps = _commit_ptrs(d_commits, n)
         sts = (L.Stats * n)()
         lp = (ctypes.c_void_p * len(ctxs))(*[e._ctx.value for e in ctxs])
+        t1 = _PY_PROF and time.perf_counter()
         L.check(L.lib().dv_epoch_run_device_lanes(lp, len(ctxs), arr, n, cps, sts), "dv_epoch_run_device_lanes")
-        return list(sts)
+        t_ret = _PY_PROF and time.perf_counter()
+        out = list(sts)
+        if _PY_PROF:
+            t2 = time.perf_counter()
+            print(f"dvcc python: {n} epochs over {len(ctxs)} lanes, {(t1 - prof) * 1e6:.1f} us before the call "
+                  f"({(t_ev - prof) * 1e6:.1f} ordering after torch), {(t_ret - t1) * 1e6:.1f} us in it, "
+                  f"{(t2 - t_ret) * 1e6:.1f} after", file=sys.stderr)
+        return out
 
     # ---- partitioned epochs over RCCL from the engine (dv_comm_init)
     def comm_init(self, unique_id, nranks, rank):
@@ -617,10 +664,8 @@ class CCEngine:
         P = len(groups[0]) if n else 0
         if any(len(g) != P for g in groups):
             raise ValueError("every group holds one batch per rank")
-        arr = (L.EpochDev * (n * P))(*[h.desc() for g in groups for h in g])
-        if d_commits is None or not isinstance(d_commits, (list, tuple)):
-            d_commits = [d_commits] * n
-        cps = (ctypes.c_void_p * n)(*[(int(t.data_ptr()) if t is not None else None) for t in d_commits])
+        arr = self._epoch_array([h for g in groups for h in g])
+        cps = _commit_ptrs(d_commits, n)
         sts = (L.Stats * n)()
         prev = self._wide_for([h for g in groups for h in g])
         try:
