@@ -98,8 +98,9 @@ __global__ __launch_bounds__(kBlock) void k_owner_scan(uint32_t *__restrict__ co
 // every epoch (kBadTxn), which the decider's probe rejects (ERRB_TXN, an
 // input error voted out on every rank before anything executes).
 constexpr uint32_t kBadTxn = 0xFFFFFFFFu;
-__device__ __forceinline__ uint32_t global_txn(uint32_t t, uint32_t tpr, uint32_t base) {
-    return t < tpr ? t + base : kBadTxn;
+// (origin-major: stride 1, base rank * tpr; position-major: stride P, base rank)
+__device__ __forceinline__ uint32_t global_txn(uint32_t t, uint32_t tpr, uint32_t base, uint32_t stride = 1) {
+    return t < tpr ? t * stride + base : kBadTxn;
 }
 
 // record i of the batch -> its owner's segment, in batch order (stable: a
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
                                                           const uint8_t *__restrict__ tables,
                                                           const uint64_t *__restrict__ args,
                                                           uint64_t n, uint32_t P, uint32_t tpr, uint32_t txn_base,
-                                                          const uint32_t *__restrict__ counts,
+                                                          uint32_t txn_stride, const uint32_t *__restrict__ counts,
                                                           const uint32_t *__restrict__ tot, uint32_t nb,
                                                           dv_access *__restrict__ out,
                                                           uint64_t *__restrict__ args_out, uint32_t *xvote) {
@@ -151,7 +152,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scatter(const uint64_t *__rest
         const uint64_t dst = (uint64_t)obase[o] + counts[(uint64_t)o * nb + blockIdx.x] + wpre + r[j];
         dv_access a;
         a.key = keys[idx];
-        a.txn_seq = global_txn(acc_txn[idx], tpr, txn_base);  // (an id past tpr: rejected by the probe)
+        a.txn_seq = global_txn(acc_txn[idx], tpr, txn_base, txn_stride);  // (an id past tpr: rejected by the probe)
         a.type = types[idx];
         a.table = tables ? tables[idx] : 0;
         a.flags = 0;
@@ -564,6 +565,89 @@ __global__ __launch_bounds__(kBlock) void k_il_commits(const uint8_t *__restrict
     }
 }
 
+// ---- the list protocol in position-major order (DV_COMM_POSITION_ORDER; not
+// CALVIN).  An owner receives, from every origin q, the records of q's txns
+// that touch its rows, txn ids j * P + q rising inside q's segment; the
+// partition's epoch wants them txn by txn in sequence order.  k_il_begin
+// places txn j * P + q after txns 0..j of origins < q and 0..j-1 of origins
+// >= q (from where each txn starts inside its segment: k_ilist_bounds), and
+// k_ilist_move writes every record's fields to its place -- the split of the
+// records (k_split_access) and the interleave in one pass.
+
+// tbo[q * (tpr + 1) + j]: where txn j * P + q starts inside origin q's
+// segment of the received records (a lower bound over the segment's ids)
+__global__ __launch_bounds__(kBlock) void k_ilist_bounds(const dv_access *__restrict__ rec, XSegs s,
+                                                         uint32_t *__restrict__ tbo, uint32_t *__restrict__ ncnt) {
+    const uint64_t n = (uint64_t)s.P * (s.tpr + 1);
+    for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < n; x += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t q = (uint32_t)(x / (s.tpr + 1)), j = (uint32_t)(x % (s.tpr + 1));
+        const uint64_t t = (uint64_t)j * s.P + q;  // (j == tpr: past every id of the segment)
+        uint64_t lo = s.eoff[q], hi = s.eoff[q + 1];
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((uint64_t)rec[mid].txn_seq < t) lo = mid + 1;
+            else hi = mid;
+        }
+        tbo[x] = (uint32_t)(lo - s.eoff[q]);
+        if (j == 0) ncnt[q] = s.tpr + 1;
+    }
+}
+
+// every received record to its place in sequence order: keys, types, txn
+// ids, tables and (TPC-C) operation words.  A record whose id is past the
+// epoch, not its origin's or out of order is not moved: ERRB_TXN in *err,
+// which the epoch's error combine makes every rank's (k_refusal_err)
+__global__ __launch_bounds__(kBlock) void k_ilist_move(const dv_access *__restrict__ rec,
+                                                       const uint64_t *__restrict__ args, XSegs s,
+                                                       const uint32_t *__restrict__ shift,
+                                                       const uint32_t *__restrict__ tb, uint64_t n_acc,
+                                                       uint64_t *__restrict__ keys, uint8_t *__restrict__ types,
+                                                       uint32_t *__restrict__ txn, uint8_t *__restrict__ tables,
+                                                       uint64_t *__restrict__ args_out, uint32_t *__restrict__ err) {
+    const uint32_t n = s.P * s.tpr;
+    bool bad = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n_acc; i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t q = 0;
+        while (q + 1 < s.P && s.eoff[q + 1] <= i) q++;
+        const dv_access a = rec[i];
+        const uint32_t v = a.txn_seq;
+        uint64_t qq = 0;
+        const uint32_t j = (uint32_t)divmod_magic(v, s.P, s.mP, qq);
+        bool good = v < n && (uint32_t)qq == q && (i == s.eoff[q] || rec[i - 1].txn_seq <= v);
+        if (good) {
+            const uint64_t d = (i - s.eoff[q]) + shift[(uint64_t)q * s.tpr + j];
+            good = d < n_acc && d >= tb[v] && d < tb[v + 1];
+            if (good) {
+                keys[d] = a.key;
+                types[d] = a.type;
+                txn[d] = v;
+                tables[d] = a.table;
+                if (args_out) args_out[d] = args[i];
+            }
+        }
+        bad |= !good;
+    }
+    if (bad) atomicOr(err, ERRB_TXN);
+}
+
+// per-txn values back in origin order: out[q * tpr + j] = v[j * P + q]
+__global__ __launch_bounds__(kBlock) void k_il_words(const uint64_t *__restrict__ v, XSegs s,
+                                                     uint64_t *__restrict__ out) {
+    const uint64_t n = (uint64_t)s.P * s.tpr;
+    for (uint64_t x = (uint64_t)blockIdx.x * kBlock + threadIdx.x; x < n; x += (uint64_t)gridDim.x * kBlock) {
+        uint64_t j = 0;
+        const uint64_t q = divmod_magic(x, s.tpr, s.mT, j);
+        out[x] = v[j * s.P + q];
+    }
+}
+
+// the interleave's refusal as the epoch's only input error: the refused
+// records left holes the probe reads as missing keys, but the batch is what
+// is malformed (DV_ERR_TXN_RANGE, as a refused replicated epoch returns)
+__global__ void k_refusal_err(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src) {
+    if (threadIdx.x == 0 && *src) *dst = *src;
+}
+
 __global__ __launch_bounds__(kBlock) void k_rep_pack(const uint64_t *__restrict__ keys,
                                                      const uint8_t *__restrict__ types,
                                                      const uint32_t *__restrict__ txn, uint64_t n,
@@ -904,6 +988,7 @@ struct DvComm {
     uint32_t *tbo = nullptr, *ncnt = nullptr;   // k_il_begin's inputs
     uint32_t *iltb = nullptr, *ilsh = nullptr;  // ... its outputs: the decider's txn_begin, the move's shifts
     uint8_t *ilv = nullptr;                     // commit bytes back in origin order
+    uint64_t *iloid = nullptr;                  // TPC-C list protocol, position-major: o_id by sequence number
     uint32_t *tbs = nullptr, *tbr = nullptr;    // tbx: the batches' txn_begin, padded (sent, received)
 };
 
@@ -1287,7 +1372,8 @@ void free_bufs(DvComm *m) {
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
-                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv, m->tbs, m->tbr};
+                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv, m->tbs, m->tbr,
+                 m->iloid};
     for (void *p : b)
         if (p) (void)hipFree(p);
     m->send = m->recv = nullptr;
@@ -1303,6 +1389,7 @@ void free_bufs(DvComm *m) {
     m->gtc = m->gbad = nullptr;
     m->ilk = m->ilt = m->tbo = m->ncnt = m->iltb = m->ilsh = nullptr;
     m->ilv = nullptr;
+    m->iloid = nullptr;
     m->tbs = m->tbr = nullptr;
 }
 
@@ -1338,16 +1425,20 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
     CHK(alloc(&m->gtc, acc / kXTile + kXMaxP + 2));
     CHK(alloc(&m->gbad, 1));
     CHK(hip_fail2(hipMemset(m->gbad, 0, sizeof(uint32_t)), "memset"));
+    // the interleave's index arrays (position-major epoch groups, replicated
+    // epochs and list-protocol epochs)
+    CHK(alloc(&m->tbo, (uint64_t)txn + P));
+    CHK(alloc(&m->ncnt, kXMaxP));
+    CHK(alloc(&m->iltb, (uint64_t)txn + 1));
+    CHK(alloc(&m->ilsh, txn));
     if (!tpcc) {  // (position-major epoch groups)
         CHK(alloc(&m->ilk, acc));
         CHK(alloc(&m->ilt, acc));
-        CHK(alloc(&m->tbo, (uint64_t)txn + P));
-        CHK(alloc(&m->ncnt, kXMaxP));
-        CHK(alloc(&m->iltb, (uint64_t)txn + 1));
-        CHK(alloc(&m->ilsh, txn));
         CHK(alloc(&m->ilv, txn));
         CHK(alloc(&m->tbs, (uint64_t)txn + P));
         CHK(alloc(&m->tbr, (uint64_t)txn + P));
+    } else {
+        CHK(alloc(&m->iloid, txn));
     }
     const size_t mail_bytes = sizeof(CommMail) + 8 * mail_words(P);
     CHK(hip_fail2(hipHostMalloc(reinterpret_cast<void **>(&m->h_mail), mail_bytes,
@@ -1745,13 +1836,18 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         ep.max_txn_acc = max_len;
         return epoch_run_replicated(c, &ep, rk, P, d_commit, st);
     }
-    // 3. the list protocol: split the batch by owner (a bad rank sends nothing)
+    // 3. the list protocol: split the batch by owner (a bad rank sends nothing).
+    //    Position-major (the vote's order flag; not CALVIN, whose order is the
+    //    sequencer's): origin q's txn j is sequence number j * P + q, as in the
+    //    epoch groups and the replicated epochs
+    const bool ilist = gvote[4] && cfg.cc_alg != DV_CALVIN && P > 1 && P <= kXMaxP;
     if (n_home) {
         DV_LAUNCH(k_owner_count, nb, kBlock, 0, s, home->keys, own, n_home, P, m->counts, nb, m->xvote);
         DV_LAUNCH(k_owner_scan, P, kBlock, 0, s, m->counts, nb, m->tot);
         DV_LAUNCH(k_owner_scatter, nb, kBlock, 0, s, home->keys, home->types, home->acc_txn, own,
                                              tpcc ? home->tables : nullptr, args, n_home, P, txns_per_rank,
-                                             (uint32_t)m->rank * txns_per_rank, m->counts, m->tot, nb, m->send,
+                                             ilist ? (uint32_t)m->rank : (uint32_t)m->rank * txns_per_rank,
+                                             ilist ? P : 1u, m->counts, m->tot, nb, m->send,
                                              tpcc ? m->send_args : nullptr, m->xvote);
     } else {
         CHK(hip_fail2(hipMemsetAsync(m->tot, 0, P * sizeof(uint32_t), s), "memset"));
@@ -1791,7 +1887,32 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
                               reinterpret_cast<uint8_t *>(m->recv_args), rc8.data(), rd8.data(), s));
     }
     CHK(hip_fail2(hipMemsetAsync(m->err, 0, 4, s), "memset"));
-    launch_split_access(s, m->recv, n_recv, nullptr, n_txn, m->keys, m->types, m->txn, m->tables, m->err);
+    XSegs xs{};
+    const uint64_t *recv_args = tpcc ? m->recv_args : nullptr;
+    if (ilist) {  // the records split into the epoch's arrays in sequence order (k_ilist_move)
+        xs.P = P;
+        xs.tpr = txns_per_rank;
+        xs.mP = div_magic(P);
+        xs.mT = div_magic(txns_per_rank);
+        uint64_t off = 0;
+        for (uint32_t q = 0; q < P; q++) {
+            xs.eoff[q] = off;
+            off += recvc[q];
+        }
+        xs.eoff[P] = off;
+        const uint64_t nt = (uint64_t)P * txns_per_rank;
+        DV_LAUNCH(k_ilist_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0, s,
+                  reinterpret_cast<const dv_access *>(m->recv), xs, m->tbo, m->ncnt);
+        DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbo,
+                  m->ncnt, m->iltb, m->ilsh);
+        if (n_recv)
+            DV_LAUNCH(k_ilist_move, (uint32_t)std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, 4096), kBlock, 0, s,
+                      reinterpret_cast<const dv_access *>(m->recv), recv_args, xs, m->ilsh, m->iltb, n_recv, m->keys,
+                      m->types, m->txn, m->tables, tpcc ? m->send_args : nullptr, m->err);
+        if (tpcc) recv_args = m->send_args;  // (the send area is free once the records have landed)
+    } else {
+        launch_split_access(s, m->recv, n_recv, nullptr, n_txn, m->keys, m->types, m->txn, m->tables, m->err);
+    }
     CHK(hip_fail2(hipGetLastError(), "unpack"));
 
     // 3. the partition's epoch: input errors combined, then the rounds closed
@@ -1804,10 +1925,16 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     ep.n_acc = n_recv;
     ep.n_txn = n_txn;
     ep.max_txn_acc = max_len;
+    // (position-major: the o_id land by sequence number and go back to origin order after the all-reduce)
+    uint64_t *oid = ilist && d_oid ? m->iloid : d_oid;
     if (tpcc) {
-        CHK(dv_tpcc_epoch_begin(c, &ep, m->recv_args, d_oid));
+        CHK(dv_tpcc_epoch_begin(c, &ep, recv_args, oid));
     } else {
         CHK(dv_epoch_begin(c, &ep, nullptr));
+    }
+    if (ilist) {  // a record the interleave refused rejects the epoch on every rank (the combine below)
+        DV_LAUNCH(k_refusal_err, 1, 64, 0, s, ctx_err_words(c), (const uint32_t *)m->err);
+        CHK(hip_fail2(hipGetLastError(), "k_refusal_err"));
     }
     CHK(dv_epoch_errors_local(c, m->gerr));
     CHK(m->x->max_u32(m->gerr, 1, s));
@@ -1833,9 +1960,19 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
     // 4. execute and report (CALVIN: a rejected epoch executes nothing, and
     //    every rank reports the combined error); the errors are combined, so
     //    every rank takes the o_id all-reduce or none does
-    const int r = dv_epoch_finish(c, d_commit, st);
-    if (r || !tpcc || !d_oid || !n_txn) return r;
-    CHK(m->x->max_u64(d_oid, n_txn, s));
+    const int r = dv_epoch_finish(c, ilist && d_commit ? m->verdict : d_commit, st);
+    if (r) return r;
+    const uint32_t ilg = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(((uint64_t)n_txn + kBlock - 1) / kBlock, 2048));
+    if (ilist && d_commit && n_txn) {  // (commit bytes back in origin order)
+        DV_LAUNCH(k_il_commits, ilg, kBlock, 0, s, m->verdict, xs, d_commit);
+        CHK(hip_fail2(hipGetLastError(), "k_il_commits"));
+    }
+    if (!tpcc || !d_oid || !n_txn) return ilist && d_commit ? hip_fail2(hipStreamSynchronize(s), "sync") : DV_OK;
+    CHK(m->x->max_u64(oid, n_txn, s));
+    if (ilist) {
+        DV_LAUNCH(k_il_words, ilg, kBlock, 0, s, m->iloid, xs, d_oid);
+        CHK(hip_fail2(hipGetLastError(), "k_il_words"));
+    }
     return hip_fail2(hipStreamSynchronize(s), "sync");
 }
 

@@ -56,24 +56,33 @@ def owner_order(epoch, world):
     return owner, np.argsort(owner, kind="stable")
 
 
-def split_by_owner(epoch, txn_base, world):
+def split_by_owner(epoch, txn_base, world, txn_stride=1):
     """Host-side split of one origin batch into per-owner fragments.
 
     Returns (keys, types, txn, counts): arrays ordered by owner rank and, inside
     an owner, by (txn, request position); txn is the global sequence number
-    txn_base + local txn index."""
+    local txn index * txn_stride + txn_base (origin-major: stride 1, base
+    rank * txns_per_rank; position-major: stride world, base rank)."""
     owner, order = owner_order(epoch, world)
-    txn = epoch.acc_txn().astype(np.int64) + txn_base
+    txn = epoch.acc_txn().astype(np.int64) * txn_stride + txn_base
     counts = np.bincount(owner, minlength=world)
     return (epoch.keys[order], epoch.types[order], txn[order].astype(np.int32), counts)
 
 
 class PartitionedEpoch:
     """One rank's outgoing fragments of one epoch, resident on `device`.
-    TPC-C epochs also carry each access's table and operation word."""
+    TPC-C epochs also carry each access's table and operation word.
+    position: the origins' batches sequenced txn by txn (origin q's txn j is
+    sequence number j * world + q, as DV_COMM_POSITION_ORDER in the engine's
+    own drivers) instead of origin after origin."""
 
-    def __init__(self, batch, rank, world, txns_per_rank, device):
-        k, t, x, counts = split_by_owner(batch, rank * txns_per_rank, world)
+    def __init__(self, batch, rank, world, txns_per_rank, device, position=False):
+        self.position = bool(position) and world > 1
+        self.world, self.txns_per_rank = world, txns_per_rank
+        if self.position:
+            k, t, x, counts = split_by_owner(batch, rank, world, txn_stride=world)
+        else:
+            k, t, x, counts = split_by_owner(batch, rank * txns_per_rank, world)
         self.send_counts = [int(c) for c in counts]
         self.keys = torch.from_numpy(k.view(np.int64)).to(device)
         self.types = torch.from_numpy(t).to(device)
@@ -124,6 +133,12 @@ class PartitionedRunner:
         if recv_counts is None:
             recv_counts = self.exchange_counts(pe)
         cols = self.exchange(pe, recv_counts)
+        if getattr(pe, "position", False):
+            # each origin's fragment holds its txns' accesses in order, ids
+            # j * world + q rising: a stable sort by id merges them into the
+            # sequence order (the engine's drivers interleave the same way)
+            order = torch.sort(cols[2], stable=True).indices
+            cols = [c[order] for c in cols]
         n_txn = pe.n_txn_global
         extra = {"tables": cols[3], "args": cols[4]} if len(cols) > 3 else {}
         self.engine.begin_partition(*cols[:3], n_txn, max_txn_acc=pe.max_txn_acc, **extra)
@@ -148,7 +163,18 @@ class PartitionedRunner:
                         raise RuntimeError(f"decision rounds stalled at {und} undecided txns")
                     counts.append(und)
             rounds = len(counts) - 1
-        st = self.engine.finish(commit)
+        if not getattr(pe, "position", False):
+            return self.engine.finish(commit), rounds
+        # position-major: the decisions (and TPC-C's o_id) are per sequence
+        # number; they go back to origin order, origin q's txn j at q * tpr + j
+        tpr, world = pe.txns_per_rank, pe.world
+        seq = None if commit is None else torch.zeros_like(commit[:n_txn])
+        st = self.engine.finish(seq)
+        if commit is not None:
+            commit[:n_txn] = seq.view(tpr, world).t().reshape(-1)
+        oid = getattr(self.engine, "oid", None)
+        if oid is not None:
+            self.engine.oid = oid[:n_txn].view(tpr, world).t().reshape(-1).clone()
         return st, rounds
 
 

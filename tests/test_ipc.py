@@ -246,15 +246,16 @@ def test_ipc_epoch_groups_ordered_lanes_two_processes():
 def test_ipc_part_protocols_two_processes(cc):
     """dv_epoch_run_part over two processes: the list protocol (owner split,
     all-to-allv of records, per-round verdict all-reduce) and the replicated
-    one (all-gathered epoch) in origin and in position order
+    one (all-gathered epoch), each in origin and in position order
     (DV_COMM_POSITION_ORDER: the origins' batches merged txn by txn; CALVIN
     keeps its origin order), two epochs each, and a missing key on one rank
     failing a group on both ranks with no row changed."""
     base = dict(kind="part", rows_pp=1 << 13, n_txn=2000, mpr=0.3, epochs=2, seed=20, cc=cc)
     bad = dict(kind="group", rows_pp=1 << 12, n_txn=800, mpr=0.3, groups=1, seed=60, cc=cc, bad_key=(1, 0, 1))
-    scs = [dict(base, mode=1), dict(base, mode=2), dict(base, mode=2, position=True), bad]
+    scs = [dict(base, mode=1), dict(base, mode=2), dict(base, mode=2, position=True),
+           dict(base, mode=1, position=True), bad]
     res = _run_ranks(scs)
-    for i, sc in enumerate(scs[:3]):
+    for i, sc in enumerate(scs[:4]):
         tab = O.YcsbTable(sc["rows_pp"] * WORLD)
         f0 = tab.f0.copy()
         per_rank = [_part_batches(sc, WORLD, r) for r in range(WORLD)]
@@ -276,8 +277,8 @@ def test_ipc_part_protocols_two_processes(cc):
             assert (res[r][i]["table"] == f0[r::WORLD]).all(), (sc, r)
     fresh = O.YcsbTable(bad["rows_pp"] * WORLD).f0
     for r in range(WORLD):
-        assert res[r][3].get("error") == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, res[r][3].get("error"))
-        assert (res[r][3]["table"] == fresh[r::WORLD]).all()
+        assert res[r][4].get("error") == dvcc._lib.DV_ERR_KEY_NOT_FOUND, (r, res[r][4].get("error"))
+        assert (res[r][4]["table"] == fresh[r::WORLD]).all()
 
 
 @pytest.mark.parametrize("cc", [dvcc.WAIT_DIE, dvcc.CALVIN])

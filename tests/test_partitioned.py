@@ -126,12 +126,12 @@ def _oracle_global(cc, batches, world, rows_pp):
     return c, st, f0
 
 
-def _gloo_worker(rank, world, port, cc, n_txn, rows_pp, mpr, q):
+def _gloo_worker(rank, world, port, cc, n_txn, rows_pp, mpr, q, position=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         _, batches = _global_setup(world, n_txn, rows_pp, mpr)
-        pe = PartitionedEpoch(batches[rank], rank, world, n_txn, "cpu")
+        pe = PartitionedEpoch(batches[rank], rank, world, n_txn, "cpu", position=position)
         runner = PartitionedRunner(NumpyPartition(cc), world, rank, device="cpu")
         commit = torch.zeros(n_txn * world, dtype=torch.uint8)
         st, rounds = runner.run(pe, commit=commit)
@@ -161,6 +161,37 @@ def test_runner_protocol_gloo_world2(cc, mpr):
         got = np.frombuffer(buf, np.uint8)
         assert (got == c_ref).all(), f"rank {rank}: {(got != c_ref).sum()} mismatches"
         assert rounds >= 1
+
+
+@pytest.mark.parametrize("cc,mpr", [(dvcc.NO_WAIT, 0.3), (dvcc.OCC, 0.5), (dvcc.WAIT_DIE, 0.1)])
+def test_runner_protocol_gloo_world2_position_order(cc, mpr):
+    """The torch.distributed list protocol with the origins' batches
+    sequenced txn by txn (PartitionedEpoch(position=True): origin q's txn j
+    is sequence number j * P + q, each owner merging its fragments by id):
+    commit bytes, back in origin order, equal the oracle over
+    dvcc.sequence_position of the same batches."""
+    world, n_txn, rows_pp = 2, 600, 1 << 10
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gloo_worker, args=(r, world, port, cc, n_txn, rows_pp, mpr, q, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, batches = _global_setup(world, n_txn, rows_pp, mpr)
+    e = dvcc.sequence_position(batches, n_txn)
+    tab = O.YcsbTable(rows_pp * world)
+    c_pos, _, _ = O.epoch_run(ORACLE_CC[cc], tab.ix, tab.f0.copy(), e.n_txn, e.txn_begin, e.keys, e.types)
+    c_ref = _origin_order(c_pos, world, n_txn)
+    c_org, _, _ = _oracle_global(cc, batches, world, rows_pp)
+    assert (c_ref != c_org).any(), "the two orders decide alike here: the test would not tell them apart"
+    for rank, buf, rounds in res:
+        got = np.frombuffer(buf, np.uint8)
+        assert (got == c_ref).all(), f"rank {rank}: {(got != c_ref).sum()} mismatches"
 
 
 def test_split_by_owner_orders_fragments():
@@ -426,7 +457,7 @@ def _check_group(cc, world, rows_pp, n_txn, mpr, epochs=2, theta=0.9, mode=1, po
                             mode=mode | (dvcc._lib.DV_COMM_POSITION_ORDER if position else 0))
     tab = O.YcsbTable(rows_pp * world)  # one-partition view: row == key
     f0 = tab.f0.copy()
-    pos = position and cc != dvcc.CALVIN and (mode & 3) == 2  # (CALVIN, the list protocol: origin order)
+    pos = position and cc != dvcc.CALVIN  # (CALVIN keeps the sequencer's origin order)
     for k in range(epochs):
         batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 20 + k), r) for r in range(world)]
         e = dvcc.sequence_position(batches, n_txn) if pos else dvcc.sequence(batches)
@@ -475,25 +506,31 @@ def test_engine_driver_replicated(cc, world, mpr):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC, dvcc.CALVIN])
-@pytest.mark.parametrize("world,mpr,mode", [(2, 0.3, 2), (4, 0.1, 2), (8, 0.5, 2), (3, 0.3, 1), (8, 0.1, 0)])
+@pytest.mark.parametrize("world,mpr,mode", [(2, 0.3, 2), (4, 0.1, 2), (8, 0.5, 2), (3, 0.3, 1), (8, 0.1, 0),
+                                            (2, 0.3, 1), (8, 0.5, 1)])
 def test_engine_driver_position_order(cc, world, mpr, mode):
     """DV_COMM_POSITION_ORDER for the per-epoch driver: a replicated epoch
     (mode 2, or mode 0 choosing it) merges the origins' batches txn by txn --
     origin q's txn j at j * P + q -- against the oracle over
-    dvcc.sequence_position, commit bytes back in origin order; CALVIN and the
-    list protocol (mode 1) keep the origin order under the flag."""
+    dvcc.sequence_position, commit bytes back in origin order; the list
+    protocol (mode 1, or mode 0 choosing it) interleaves each owner's records
+    the same way; CALVIN keeps the origin order under the flag."""
     _check_group(cc, world, 1 << 14, 3000, mpr, mode=mode, position=True)
 
 
 @pytest.mark.gpu
-def test_engine_driver_position_order_malformed_batch():
-    """A position-major replicated epoch whose batch on one rank has txn ids
-    that do not rise: the interleave refuses to move it and every rank
-    returns DV_ERR_TXN_RANGE before anything executes; the next epoch runs."""
+@pytest.mark.parametrize("mode", [2, 1])
+def test_engine_driver_position_order_malformed_batch(mode):
+    """A position-major epoch (replicated, mode 2, or the list protocol, mode
+    1) whose batch on one rank has txn ids that do not rise: the interleave
+    refuses to move it (the list protocol: on the owners that receive the
+    records, its refusal combined with the epoch's input errors) and every
+    rank returns DV_ERR_TXN_RANGE before anything executes; the next epoch
+    runs."""
     world, rows_pp, n_txn = 2, 1 << 12, 800
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=0.9, part_per_txn=2,
                                   strict_ppt=1, mpr=0.3)
-    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=2 | dvcc._lib.DV_COMM_POSITION_ORDER)
+    engines = _engine_group(dvcc.NO_WAIT, world, rows_pp, n_txn, mode=mode | dvcc._lib.DV_COMM_POSITION_ORDER)
     before = [eng.read_table(0, rows_pp) for eng in engines]
     batches = [gen.gen(n_txn, dvcc.epoch_seed(r, 70), r) for r in range(world)]
     homes = [dvcc.DeviceEpoch(b) for b in batches]

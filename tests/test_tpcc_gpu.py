@@ -187,6 +187,32 @@ def test_tpcc_missing_last_name():
         eng.close()
 
 
+def _global_position(batches):
+    """Origin batches -> one epoch in position-major order
+    (DV_COMM_POSITION_ORDER: origin q's txn j is sequence number j * P + q);
+    also the index of every access in the origin-major concatenation"""
+    P = len(batches)
+    tpr = batches[0].n_txn
+    assert all(b.n_txn == tpr for b in batches)
+    offs = np.cumsum([0] + [len(b.keys) for b in batches])
+    idx = []
+    for j in range(tpr):
+        for q, b in enumerate(batches):
+            lo, hi = int(b.txn_begin[j]), int(b.txn_begin[j + 1])
+            idx.append(np.arange(offs[q] + lo, offs[q] + hi))
+    idx = np.concatenate(idx).astype(np.int64)
+    keys, types, tables, args, _ = _global(batches)
+    sizes = np.array([int(b.txn_begin[j + 1] - b.txn_begin[j]) for j in range(tpr) for b in batches], np.int64)
+    tb = np.zeros(len(sizes) + 1, np.uint32)
+    tb[1:] = np.cumsum(sizes)
+    return (keys[idx], types[idx], tables[idx], args[idx], tb), idx
+
+
+def _origin_order(v, world, n_txn):
+    """per-txn values of a position-major sequence in origin order (q * n_txn + j)"""
+    return np.asarray(v).reshape(n_txn, world).T.reshape(-1)
+
+
 def _global(batches):
     """Origin batches -> one epoch in Calvin's global order (rank-major)."""
     keys = np.concatenate([b.keys for b in batches])
@@ -266,15 +292,20 @@ def test_tpcc_partitioned_engines(cc, world):
     assert (oid_sum == o_ref).all()
 
 
-def _tpcc_group(cc, kw, world, n_txn, seed, gen_seed):
+def _tpcc_group(cc, kw, world, n_txn, seed, gen_seed, position=False):
     """`world` TPC-C contexts on this GPU joined by the in-process transport
     (dv_comm_init_local), one epoch through dv_tpcc_epoch_run_part on one
-    host thread each; returns (engines, params, batches, per-rank results)."""
+    host thread each; returns (engines, params, batches, per-rank results).
+    position: DV_COMM_POSITION_ORDER (the list protocol sequences the
+    origins' batches txn by txn)."""
     import threading
     pp = T.tpcc_params(part_cnt=world, **kw)
     batches = [T.gen(pp, n_txn, gen_seed + r, home_part=r) for r in range(world)]
     engines = [T.TpccEngine(cc, pp, n_txn * world, part_id=p, seed=seed) for p in range(world)]
     dvcc.CCEngine.comm_init_local(engines)
+    if position:
+        for eng in engines:
+            eng.comm_set_mode(dvcc._lib.DV_COMM_POSITION_ORDER)
     out = [None] * world
 
     def body(r):
@@ -297,13 +328,19 @@ def _tpcc_group(cc, kw, world, n_txn, seed, gen_seed):
     return engines, pp, batches, out
 
 
-def _check_tpcc_group(cc, kw, world, n_txn, full_tables):
-    engines, pp, batches, out = _tpcc_group(cc, kw, world, n_txn, 5, 60)
+def _check_tpcc_group(cc, kw, world, n_txn, full_tables, position=False):
+    engines, pp, batches, out = _tpcc_group(cc, kw, world, n_txn, 5, 60, position=position)
     try:
         # the oracle's all-warehouse image with last-name lists per partition
         # of this layout (custNPKey collides across warehouses from 103 on)
         db = O.TpccDB(O.tpcc_params(**dict(kw, part_cnt=1)), 5, index_parts=world)
-        c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], *_global(batches), owner=np.concatenate([b.owner for b in batches]))
+        owner = np.concatenate([b.owner for b in batches])
+        if position and cc != dvcc.CALVIN:  # (CALVIN keeps the sequencer's origin order)
+            ep, idx = _global_position(batches)
+            c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], *ep, owner=owner[idx])
+            c_ref, o_ref = _origin_order(c_ref, world, n_txn), _origin_order(o_ref, world, n_txn)
+        else:
+            c_ref, o_ref, st_ref = db.epoch(ORACLE_CC[cc], *_global(batches), owner=owner)
         committed = 0
         for r, x in enumerate(out):
             assert not isinstance(x, Exception), f"rank {r}: {x}"
@@ -343,6 +380,18 @@ def test_tpcc_engine_driver(cc, world):
     single-thread E-schedule over the sequenced global epoch."""
     kw = dict(num_wh=2 * world, cust_per_dist=1000, max_items=2000, part_per_txn=2, mpr=1.0)
     _check_tpcc_group(cc, kw, world, 1500, full_tables=True)
+
+
+@pytest.mark.parametrize("cc", CCS)
+@pytest.mark.parametrize("world", [2, 4])
+def test_tpcc_engine_driver_position_order(cc, world):
+    """dv_tpcc_epoch_run_part under DV_COMM_POSITION_ORDER: each owner
+    interleaves the records it receives txn by txn (origin q's txn j at
+    j * P + q; CALVIN keeps the origin order) -- commit bytes and o_id, in
+    origin order, equal the oracle over the position-major sequence, and so
+    do the rows."""
+    kw = dict(num_wh=2 * world, cust_per_dist=1000, max_items=2000, part_per_txn=2, mpr=1.0)
+    _check_tpcc_group(cc, kw, world, 1500, full_tables=True, position=True)
 
 
 @pytest.mark.slow
