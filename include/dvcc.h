@@ -386,9 +386,10 @@ int dv_epoch_run_part(dv_ctx *ctx, const dv_epoch_dev *home, uint32_t txns_per_r
  * per access even where the compact 4-byte form (global rows below 2^30,
  * dense txn ids) applies -- results are identical. */
 #define DV_COMM_WIDE_BATCHES 4
-/* OR DV_COMM_POSITION_ORDER into mode (epoch groups, and the replicated
- * epochs of dv_epoch_run_part; NO_WAIT / WAIT_DIE / OCC -- the list protocol
- * and CALVIN keep the origin order): the sequencer merges the origins'
+/* OR DV_COMM_POSITION_ORDER into mode (epoch groups, and the replicated and
+ * list-protocol epochs of dv_epoch_run_part / dv_tpcc_epoch_run_part;
+ * NO_WAIT / WAIT_DIE / OCC -- CALVIN keeps the origin order): the sequencer
+ * merges the origins'
  * batches of an epoch txn by txn --
  * origin q's txn j is sequence number j * P + q, as clients of all nodes
  * arriving together -- instead of batch by batch (origin q's txn j at
