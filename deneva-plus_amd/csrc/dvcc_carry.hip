@@ -44,6 +44,33 @@ __global__ __launch_bounds__(kBlock) void k_carry_scan(uint32_t *__restrict__ bt
     __shared__ uint32_t lds4[4];
     const uint32_t per = (nb + kBlock - 1) / kBlock;
     const uint32_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+    constexpr uint32_t kR = 16;  // (nb <= 4,096 blocks, 1M txns: a thread's chunk in registers)
+    if (per <= kR) {  // every load in flight at once (the loop waited out one round trip per entry: 10 us)
+        uint32_t vt[kR], va[kR], st = 0, sa = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kR; k++) {
+            const bool in = k < per && lo + k < nb;
+            vt[k] = in ? bt[lo + k] : 0u;
+            va[k] = in ? ba[lo + k] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kR; k++) {
+            st += vt[k];
+            sa += va[k];
+        }
+        uint32_t pt = block_excl_scan256(st, lds4, nullptr);
+        uint32_t pa = block_excl_scan256(sa, lds4, nullptr);
+#pragma unroll
+        for (uint32_t k = 0; k < kR; k++) {
+            if (k < per && lo + k < nb) {
+                bt[lo + k] = pt;
+                ba[lo + k] = pa;
+            }
+            pt += vt[k];
+            pa += va[k];
+        }
+        return;
+    }
     uint32_t st = 0, sa = 0;
     for (uint32_t i = lo; i < hi; i++) {
         st += bt[i];
@@ -90,6 +117,64 @@ __global__ __launch_bounds__(kBlock) void k_carry_copy(
     }
     if (!cr || id >= max_txn) len = 0;  // (ids grow with t: the cap cuts a suffix)
     else if (otb) otb[id] = pos;        // (tb form: the carried txn's boundary, dv_epoch_dev::txn_begin)
+#ifndef DVCC_CARRY_COPY_WAVE
+    // The block's txns hold one contiguous run of source accesses: the block
+    // streams it (coalesced loads and stores), each access going to its txn's
+    // destination plus its offset in the txn.  An access's txn: the last one
+    // starting at or before it, by a binary search over the block's starts in
+    // LDS -- made monotone by a suffix minimum, since an empty txn's range
+    // (never written by the probe) may hold anything.  (The wave form below
+    // spread each wave's carried accesses over its lanes by a shuffle search:
+    // at a ~97 % carry rate that search, not the bytes, set its time.)
+    {
+        constexpr uint32_t kNone = 0xFFFFFFFFu;
+        __shared__ uint32_t s_a0[kCarryTpb], s_id[kCarryTpb], s_sh[kCarryTpb], s_w[2][kCarryTpb / 64];
+        const uint32_t tid = threadIdx.x, wave = tid >> 6;
+        const uint32_t a0s = t < n_txn ? tb_start[t] : 0u;
+        const uint32_t src_len = t < n_txn ? tb_end[t] - a0s : 0u;
+        uint32_t v = src_len ? a0s : kNone;  // suffix min of the non-empty txns' starts
+        uint32_t e = src_len ? a0s + src_len : 0u;  // and the block's end of accesses (max)
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t o = __shfl_down(v, off, 64), oe = __shfl_down(e, off, 64);
+            if (lane + (uint32_t)off < 64u) {
+                v = o < v ? o : v;
+                e = oe > e ? oe : e;
+            }
+        }
+        if (lane == 0) {
+            s_w[0][wave] = v;  // (lane 0: the wave's whole suffix)
+            s_w[1][wave] = e;
+        }
+        __syncthreads();
+        uint32_t hi = 0;
+        for (uint32_t w = 0; w < kCarryTpb / 64; w++) {
+            if (w > wave) v = s_w[0][w] < v ? s_w[0][w] : v;
+            hi = s_w[1][w] > hi ? s_w[1][w] : hi;
+        }
+        s_a0[tid] = v;
+        s_id[tid] = len ? id : kNone;
+        s_sh[tid] = pos - a0;  // (mod 2^32: destination = source + shift)
+        __syncthreads();
+        const uint32_t lo = s_a0[0];
+        for (uint32_t i = lo + tid; lo != kNone && i < hi; i += kCarryTpb) {
+            uint32_t k = 0;
+#pragma unroll
+            for (uint32_t w = kCarryTpb / 2; w > 0; w >>= 1)
+                if (s_a0[k + w] <= i) k += w;
+            const uint32_t sid = s_id[k];
+            if (sid == kNone) continue;
+            const uint32_t o = i + s_sh[k];
+            if (orecs) orecs[o] = recs[i];  // tb form: the 4-byte records (key | write << 31)
+            if (!okeys) continue;
+            okeys[o] = keys[i];
+            otypes[o] = types[i];
+            otxn[o] = sid;
+            if (tables) otables[o] = tables[i];
+        }
+        return;
+    }
+#endif
     uint32_t incl = len;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {

@@ -79,17 +79,7 @@ __global__ __launch_bounds__(kBlock) void k_owner_scan(uint32_t *__restrict__ co
                                                        uint32_t *__restrict__ tot) {
     __shared__ uint32_t lds4[4];
     uint32_t *c = counts + (uint64_t)blockIdx.x * nb;
-    const uint32_t per = (nb + kBlock - 1) / kBlock;
-    const uint32_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
-    uint32_t sum = 0;
-    for (uint32_t i = lo; i < hi; i++) sum += c[i];
-    uint32_t t = 0;
-    uint32_t pre = block_excl_scan256(sum, lds4, &t);
-    for (uint32_t i = lo; i < hi; i++) {
-        const uint32_t v = c[i];
-        c[i] = pre;
-        pre += v;
-    }
+    const uint32_t t = block_chunk_scan256(c, nb, lds4);
     if (threadIdx.x == 0) tot[blockIdx.x] = t;
 }
 

@@ -49,6 +49,40 @@ __device__ __forceinline__ uint32_t block_excl_scan256(uint32_t v, uint32_t *lds
     return pre + x - v;
 }
 
+// exclusive scan of c[0, n) in place by one 256-thread block, each thread a
+// contiguous chunk; returns the total.  Chunks of up to kChunkRegs entries
+// are loaded into registers all at once (a load-add loop waits out one round
+// trip per entry); longer ones take the loop.
+constexpr uint32_t kChunkRegs = 12;
+__device__ __forceinline__ uint32_t block_chunk_scan256(uint32_t *c, uint32_t n, uint32_t *lds4) {
+    const uint32_t per = (n + 255) / 256;
+    const uint32_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+    uint32_t tot = 0;
+    if (per <= kChunkRegs) {
+        uint32_t v[kChunkRegs], sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < kChunkRegs; k++) v[k] = lo + k < hi ? c[lo + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kChunkRegs; k++) sum += v[k];
+        uint32_t pre = block_excl_scan256(sum, lds4, &tot);
+#pragma unroll
+        for (uint32_t k = 0; k < kChunkRegs; k++) {
+            if (lo + k < hi) c[lo + k] = pre;
+            pre += v[k];
+        }
+        return tot;
+    }
+    uint32_t sum = 0;
+    for (uint32_t i = lo; i < hi; i++) sum += c[i];
+    uint32_t pre = block_excl_scan256(sum, lds4, &tot);
+    for (uint32_t i = lo; i < hi; i++) {
+        const uint32_t x = c[i];
+        c[i] = pre;
+        pre += x;
+    }
+    return tot;
+}
+
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
     z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;

@@ -522,19 +522,7 @@ __global__ __launch_bounds__(kBlock) void k_radix_scan(uint32_t *__restrict__ co
     __shared__ uint32_t lds4[4];
     uint32_t *c = counts + (uint64_t)blockIdx.x * nblocks;  // (row stride: the upper bound)
     if (n_dev && nblocks_for(*n_dev) < nblocks) nblocks = nblocks_for(*n_dev);
-    const uint32_t per = (nblocks + kBlock - 1) / kBlock;
-    const uint32_t lo = threadIdx.x * per;
-    uint32_t hi = lo + per;
-    if (hi > nblocks) hi = nblocks;
-    uint32_t sum = 0;
-    for (uint32_t i = lo; i < hi; i++) sum += c[i];
-    uint32_t tot;
-    uint32_t pre = block_excl_scan256(sum, lds4, &tot);
-    for (uint32_t i = lo; i < hi; i++) {
-        const uint32_t v = c[i];
-        c[i] = pre;
-        pre += v;
-    }
+    const uint32_t tot = block_chunk_scan256(c, nblocks, lds4);
     if (threadIdx.x == 0) digit_tot[blockIdx.x] = tot;
 }
 
