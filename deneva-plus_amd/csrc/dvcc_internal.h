@@ -125,7 +125,10 @@ constexpr uint64_t kMaxRows = 0x7FFFFFFFull;
 // "dequeue"), so 4096 blocks on one word would cost ~50 us.  The host adds
 // the slots up.
 constexpr int kRoundLog = 64;
-constexpr int kSlots = 32;
+#ifndef DVCC_SLOTS
+#define DVCC_SLOTS 32
+#endif
+constexpr int kSlots = DVCC_SLOTS;
 struct alignas(128) CtrSlot {
     unsigned long long read_digest;
     unsigned long long write_cnt;
