@@ -565,8 +565,15 @@ __global__ __launch_bounds__(kBlock) void k_kill_emit(
                 const uint32_t g = g0 + u * kBlock + tid;
                 if (g >= nf) continue;
                 acc_row[a[u]] = rows[u] | (wr[u] ? AR_WR : 0u);
-                // the skip rule (k_kill), from the row state itself
-                if (nowait && !wr[u] && row_bits(row_state, rows[u]) == RS_RD) {
+                // the skip rule: k_kill's bit for this access (one 64-bit word
+                // per 64 consecutive accesses), not a second gather of the row
+                // state's random word
+#ifdef DVCC_EMIT_ROW_STATE
+                const bool skip = nowait && !wr[u] && row_bits(row_state, rows[u]) == RS_RD;
+#else
+                const bool skip = skip_bits && ((skip_bits[a[u] >> 6] >> (a[u] & 63u)) & 1ull) != 0;
+#endif
+                if (skip) {
                     uint32_t lo = 0, hi = ns;
                     while (hi - lo > 1) {
                         const uint32_t mid = (lo + hi) >> 1;
