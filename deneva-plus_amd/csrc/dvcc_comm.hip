@@ -248,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void k_group_pack_c(PackSrc src, uint32_t *
             wr = types[i] == DV_WR;
         }
         bool start = false;
-        if (!tbx) {  // (tbx: the batch's txn_begin travels beside it, k_group_pack_tb)
+        if (!tbx) {  // (tbx: the batch's txn_begin travels beside it)
             const uint32_t t = txn[i];
             const uint32_t pt = i ? txn[i - 1] : 0u;
             start = i == 0 || t != pt;
@@ -270,6 +270,10 @@ struct XSegs {
     uint64_t mP, mT;  // div_magic(P), div_magic(tpr): position-major index arithmetic
     uint64_t eoff[kXMaxP + 1];
     uint32_t toff[kXMaxP + 1];
+    // tbx: the words of origin q's txn_begin that landed at q * (tpr + 1) (its
+    // n_txn + 1, or 0 for a batch without txns); the later entries stand for
+    // the segment's end
+    uint32_t tbw[kXMaxP];
 };
 __device__ __forceinline__ uint32_t xseg_of(const XSegs &s, uint32_t tile) {
     uint32_t q = 0;
@@ -352,9 +356,33 @@ __global__ __launch_bounds__(kBlock) void k_group_txn_ids(uint32_t *__restrict__
 // origin-major it holds origin 0's only.  The batches land contiguous per
 // origin; tbo[q * (tpr + 1) + j] is txn j's first access inside origin q's
 // segment, ncnt[q] entries valid (later j: the segment's end).
+// ncnt null: tbx, the senders' own boundaries (XSegs::tbw entries landed)
 __device__ __forceinline__ uint32_t il_start(const XSegs &s, const uint32_t *__restrict__ tbo,
                                              const uint32_t *__restrict__ ncnt, uint32_t q, uint32_t j) {
-    return !ncnt || j < ncnt[q] ? tbo[(uint64_t)q * (s.tpr + 1) + j] : (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
+    return j < (ncnt ? ncnt[q] : s.tbw[q]) ? tbo[(uint64_t)q * (s.tpr + 1) + j]
+                                           : (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
+}
+
+// tbx: the receiver checks each landed batch's boundaries -- 0 first, rising,
+// its access count last -- in the launch that reads them (k_tb_origin,
+// k_il_begin).  Txn j < tpr of origin q checks entry j against entry j + 1;
+// a batch of tpr = 0 txns is checked at the epoch's end entry (tbx_bad_end).
+__device__ __forceinline__ bool tbx_bad(const XSegs &s, const uint32_t *__restrict__ tbr, uint32_t q, uint32_t j) {
+    const uint32_t w = s.tbw[q], seg = (uint32_t)(s.eoff[q + 1] - s.eoff[q]);
+    if (w == 0) return j == 0 && seg != 0u;  // (no boundaries: an empty batch only)
+    const uint32_t nt = w - 1u;
+    if (j > nt) return false;
+    const uint32_t *tq = tbr + (uint64_t)q * (s.tpr + 1);
+    const uint32_t v = tq[j];
+    if (j == 0 && v != 0u) return true;
+    if (j == nt) return v != seg;
+    return v > tq[j + 1] || (j + 1 == nt && tq[nt] != seg);
+}
+__device__ __forceinline__ bool tbx_bad_end(const XSegs &s, const uint32_t *__restrict__ tbr) {
+    bool b = false;
+    if (s.tpr == 0)
+        for (uint32_t q = 0; q < s.P; q++) b |= tbx_bad(s, tbr, q, 0);
+    return b;
 }
 
 // wide batches (the senders' ids): tbo by a lower bound over each segment's
@@ -383,8 +411,9 @@ __global__ __launch_bounds__(kBlock) void k_il_bounds(const uint32_t *__restrict
 // move's one lookup per access)
 __global__ __launch_bounds__(kBlock) void k_il_begin(XSegs s, const uint32_t *__restrict__ tbo,
                                                      const uint32_t *__restrict__ ncnt, uint32_t *__restrict__ tb,
-                                                     uint32_t *__restrict__ shift) {
+                                                     uint32_t *__restrict__ shift, uint32_t *__restrict__ bad) {
     const uint32_t n = s.P * s.tpr;
+    bool b = false;
     for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t <= n; t += gridDim.x * kBlock) {
         uint64_t qq = 0;
         const uint32_t j = (uint32_t)divmod_magic(t, s.P, s.mP, qq), q = (uint32_t)qq;
@@ -396,7 +425,9 @@ __global__ __launch_bounds__(kBlock) void k_il_begin(XSegs s, const uint32_t *__
         }
         tb[t] = d;
         if (t < n) shift[(uint64_t)q * s.tpr + j] = d - own;
+        if (bad) b |= t < n ? tbx_bad(s, tbo, q, j) : tbx_bad_end(s, tbo);  // (tbx: the landed boundaries)
     }
+    if (b) atomicOr(bad, 1u);
 }
 
 // every landed access to its place in the interleaved epoch (tiles of one
@@ -447,49 +478,34 @@ __global__ __launch_bounds__(kBlock) void k_il_move(const uint32_t *__restrict__
 
 // ---- epoch groups whose batches bring their txn boundaries (every rank's
 // homes carry dv_epoch_dev::txn_begin and the decider takes tb mode; the
-// vote's "tbx"): each batch's txn_begin travels beside its rows, padded to
-// tpr + 1 entries (later entries: the batch's access count), so the decider
-// needs no start bits, no renumbering and no per-access txn ids.  A sender
-// checks its own boundaries (0 first, rising, its access count last): a bad
-// one fails the group (*bad, DV_ERR_ARG on every rank).
-struct PackTb {
-    const uint32_t *tb[kXMaxP];
-    uint32_t n_txn[kXMaxP];
-    uint64_t n_acc[kXMaxP];
-};
-__global__ __launch_bounds__(kBlock) void k_group_pack_tb(PackTb src, uint32_t tpr, uint32_t *__restrict__ out,
-                                                          uint32_t *__restrict__ bad) {
-    const uint32_t e = blockIdx.y, nt = src.n_txn[e];
-    const uint32_t *__restrict__ tb = src.tb[e];
-    const uint32_t na = (uint32_t)src.n_acc[e];
-    bool b = false;
-    for (uint32_t j = blockIdx.x * kBlock + threadIdx.x; j <= tpr; j += gridDim.x * kBlock) {
-        uint32_t v = na;
-        if (j <= nt && tb) {
-            v = tb[j];
-            if ((j == 0 && v != 0u) || (j == nt && v != na) || (j > 0 && tb[j - 1] > v)) b = true;
-        } else if (j <= nt) {
-            b = na != 0u;  // (no boundaries: an empty batch only)
-        }
-        out[(uint64_t)e * (tpr + 1) + j] = v;
-    }
-    if (b) atomicOr(bad, 1u);
-}
+// vote's "tbx"): each batch's txn_begin travels beside its rows, straight from
+// the caller's buffer (n_txn + 1 words, landing at q * (tpr + 1); XSegs::tbw),
+// so the decider needs no start bits, no renumbering and no per-access txn
+// ids.  The receiver checks every landed batch (tbx_bad: 0 first, rising, its
+// access count last) in the launch that reads it: a bad one fails the group
+// (*bad, DV_ERR_ARG on every rank).
 
 // origin-major: the decider's txn_begin -- origin q's txn j at q * tpr + j
-// starts at eoff[q] + its offset in q's batch; tb[P * tpr] = every access
+// starts at eoff[q] + its offset in q's batch; tb[P * tpr] = every access.
+// Each landed batch's boundaries are checked here (tbx_bad): a bad one fails
+// the group (*bad, DV_ERR_ARG on every rank); the decider's own range checks
+// keep it inside the epoch meanwhile
 __global__ __launch_bounds__(kBlock) void k_tb_origin(XSegs s, const uint32_t *__restrict__ tbr,
-                                                      uint32_t *__restrict__ tb) {
+                                                      uint32_t *__restrict__ tb, uint32_t *__restrict__ bad) {
     const uint64_t n = (uint64_t)s.P * s.tpr;
+    bool b = false;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t <= n; t += (uint64_t)gridDim.x * kBlock) {
         if (t == n) {
             tb[t] = (uint32_t)s.eoff[s.P];
+            b |= tbx_bad_end(s, tbr);
             continue;
         }
         uint64_t j = 0;
         const uint64_t q = divmod_magic(t, s.tpr, s.mT, j);
-        tb[t] = (uint32_t)(s.eoff[q] + tbr[q * (s.tpr + 1) + j]);
+        tb[t] = (uint32_t)(s.eoff[q] + il_start(s, tbr, nullptr, (uint32_t)q, (uint32_t)j));
+        b |= tbx_bad(s, tbr, (uint32_t)q, (uint32_t)j);
     }
+    if (b) atomicOr(bad, 1u);
 }
 
 // position-major with the boundaries (no per-access ids): a block per origin
@@ -507,9 +523,8 @@ __global__ __launch_bounds__(kBlock) void k_il_move_tb(const uint32_t *__restric
     const uint32_t tiles = (s.tpr + kIlTxns - 1) / kIlTxns;
     const uint32_t q = blockIdx.x / tiles, j0 = (blockIdx.x % tiles) * kIlTxns;
     const uint32_t nj = s.tpr - j0 < kIlTxns ? s.tpr - j0 : kIlTxns;
-    const uint32_t *tq = tbo + (uint64_t)q * (s.tpr + 1);
     const uint64_t seg = s.eoff[q + 1] - s.eoff[q];
-    for (uint32_t i = threadIdx.x; i <= nj; i += kBlock) l_st[i] = tq[j0 + i];
+    for (uint32_t i = threadIdx.x; i <= nj; i += kBlock) l_st[i] = il_start(s, tbo, nullptr, q, j0 + i);
     for (uint32_t i = threadIdx.x; i < nj; i += kBlock) l_sh[i] = shift[(uint64_t)q * s.tpr + j0 + i];
     __syncthreads();
     const uint32_t a0 = l_st[0], a1 = l_st[nj];
@@ -535,8 +550,8 @@ __global__ __launch_bounds__(kBlock) void k_il_move_tb(const uint32_t *__restric
             b = true;
             break;
         }
-        // (every sender checked its boundaries, k_group_pack_tb: the stores
-        // need only stay inside the epoch when one reported them bad)
+        // (k_il_begin checked the boundaries: the stores need only stay
+        // inside the epoch when it found them bad)
         const uint64_t d = (uint64_t)p + l_sh[lo];
         if (d < n_acc) ok[d] = rk[s.eoff[q] + p];
         else b = true;
@@ -752,11 +767,27 @@ __host__ __device__ inline uint32_t owner_bits(uint32_t P) {
 }
 
 // pass 1: records per owner per block (a halted or rejected epoch routes
-// nothing: zero counts)
+// nothing: zero counts).  The txn walk (SRC 0) also writes the epoch's commit
+// bytes (commit, may be null) and adds its committed count, as k_commit_out
+// would one launch later
 template <int SRC>
-__global__ __launch_bounds__(kBlock) void k_route_count(RouteSrc<SRC> src, RouteOut ro, const Counters *ctr) {
+__global__ __launch_bounds__(kBlock) void k_route_count(RouteSrc<SRC> src, RouteOut ro, Counters *ctr,
+                                                        uint8_t *__restrict__ commit) {
     __shared__ uint32_t c[kRadix];
+    __shared__ uint32_t part[kBlock / 64];
     for (uint32_t o = threadIdx.x; o < ro.P; o += kBlock) c[o] = 0;
+    if (SRC == 0 && !ctr->halt) {  // (halted: the rounds resume first, dv_epoch_finish)
+        uint32_t cnt = commit_bytes_grid(src.status, src.n_txn, commit);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) cnt += __shfl_down(cnt, off, 64);
+        if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kBlock / 64; w++) t += part[w];
+            if (t) atomicAdd(&my_slot(ctr).committed, t);
+        }
+    }
     __syncthreads();
     if (!(input_err(ctr) || ctr->halt)) {
         const uint32_t lane = threadIdx.x & 63, P = ro.P, ob = owner_bits(P);
@@ -896,8 +927,12 @@ __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const ui
 // this rank's outcome record, all-gathered (epoch groups, step 4): failure
 // code, committed txns, receive capacity, then records per owner
 constexpr uint32_t kGroupRecHead = 8;
+// (and the execution's digest slots zeroed for step 6: the previous group's
+// were read by this group's vote)
 __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
-                              uint64_t cap, uint64_t *__restrict__ rec, uint32_t *__restrict__ pack_bad) {
+                              uint64_t cap, uint64_t *__restrict__ rec, uint32_t *__restrict__ pack_bad,
+                              unsigned long long *__restrict__ xacc) {
+    for (uint32_t i = threadIdx.x; i < 2u * kSlots; i += blockDim.x) xacc[i] = 0;
     // a compact batch with txn ids that are not dense (k_group_pack_c), or a
     // batch the position-major move refused (k_il_move), fails the group as an
     // argument error -- whatever its decision made of the input; the flag is
@@ -917,17 +952,18 @@ __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint
 }
 
 void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
-                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr) {
+                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, Counters *ctr,
+                      uint8_t *d_commit) {
     const RouteSrc<0> src{tb_start, tb_end, acc_row, n_txn, nullptr, nullptr, nullptr, 0, status};
-    DV_LAUNCH((k_route_count<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
+    DV_LAUNCH((k_route_count<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr, d_commit);
     DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
     DV_LAUNCH((k_route_scatter<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
 
 void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs, const uint64_t *el,
-                       const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr) {
+                       const uint8_t *ew, uint64_t n, const uint8_t *status, Counters *ctr) {
     const RouteSrc<1> src{nullptr, nullptr, nullptr, 0, pairs, el, ew, n, status};
-    DV_LAUNCH((k_route_count<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
+    DV_LAUNCH((k_route_count<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr, (uint8_t *)nullptr);
     DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
     DV_LAUNCH((k_route_scatter<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
@@ -979,7 +1015,7 @@ struct DvComm {
     uint32_t *iltb = nullptr, *ilsh = nullptr;  // ... its outputs: the decider's txn_begin, the move's shifts
     uint8_t *ilv = nullptr;                     // commit bytes back in origin order
     uint64_t *iloid = nullptr;                  // TPC-C list protocol, position-major: o_id by sequence number
-    uint32_t *tbs = nullptr, *tbr = nullptr;    // tbx: the batches' txn_begin, padded (sent, received)
+    uint32_t *tbr = nullptr;                    // tbx: the batches' txn_begin as landed (tpr + 1 words each)
 };
 
 }  // namespace dvcc
@@ -1362,7 +1398,7 @@ void free_bufs(DvComm *m) {
     m->h_mail = m->d_mail = nullptr;
     void *b[] = {m->send, m->recv, m->send_args, m->recv_args, m->keys, m->types, m->tables, m->verdict, m->txn,
                  m->counts, m->tot, m->err, m->xcnt, m->xvote, m->gerr, m->rblk, m->rtot, m->gcommit, m->xacc,
-                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv, m->tbs, m->tbr,
+                 m->gs, m->gr, m->gtc, m->gbad, m->ilk, m->ilt, m->tbo, m->ncnt, m->iltb, m->ilsh, m->ilv, m->tbr,
                  m->iloid};
     for (void *p : b)
         if (p) (void)hipFree(p);
@@ -1380,7 +1416,7 @@ void free_bufs(DvComm *m) {
     m->ilk = m->ilt = m->tbo = m->ncnt = m->iltb = m->ilsh = nullptr;
     m->ilv = nullptr;
     m->iloid = nullptr;
-    m->tbs = m->tbr = nullptr;
+    m->tbr = nullptr;
 }
 
 // every buffer an epoch of this context can need, sized once (dv_comm_init):
@@ -1425,7 +1461,6 @@ int reserve(DvComm *m, uint64_t acc, uint32_t txn, bool tpcc) {
         CHK(alloc(&m->ilk, acc));
         CHK(alloc(&m->ilt, acc));
         CHK(alloc(&m->ilv, txn));
-        CHK(alloc(&m->tbs, (uint64_t)txn + P));
         CHK(alloc(&m->tbr, (uint64_t)txn + P));
     } else {
         CHK(alloc(&m->iloid, txn));
@@ -1711,7 +1746,7 @@ int run_part_position(dv_ctx *c, DvComm *m, const dv_epoch_dev *home, uint64_t n
         DV_LAUNCH(k_il_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0, s, rt, xs,
                   m->tbo, m->ncnt);
         DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbo,
-                  m->ncnt, m->iltb, m->ilsh);
+                  m->ncnt, m->iltb, m->ilsh, (uint32_t *)nullptr);
         DV_LAUNCH(k_il_move<true>, xtiles, kBlock, 0, s, rk, rt, xs, m->ilsh, m->iltb, ro, m->ilk, m->ilt, m->gbad);
     }
     CHK(hip_fail2(hipGetLastError(), "k_il_move"));
@@ -1894,7 +1929,7 @@ int run_part(dv_ctx *c, const dv_epoch_dev *home, const uint8_t *own, const uint
         DV_LAUNCH(k_ilist_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0, s,
                   reinterpret_cast<const dv_access *>(m->recv), xs, m->tbo, m->ncnt);
         DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbo,
-                  m->ncnt, m->iltb, m->ilsh);
+                  m->ncnt, m->iltb, m->ilsh, (uint32_t *)nullptr);
         if (n_recv)
             DV_LAUNCH(k_ilist_move, (uint32_t)std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, 4096), kBlock, 0, s,
                       reinterpret_cast<const dv_access *>(m->recv), recv_args, xs, m->ilsh, m->iltb, n_recv, m->keys,
@@ -2013,7 +2048,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     for (uint32_t e = 0; e < P && !bad; e++) {
         const dv_epoch_dev &h = homes[e];
         bad = h.n_txn > txns_per_rank || (h.n_acc && (!h.keys || !h.types || !h.acc_txn)) ||
-              (h.ts && cfg.cc_alg == DV_WAIT_DIE);
+              (h.ts && cfg.cc_alg == DV_WAIT_DIE) || (h.n_acc >> 32) != 0;
         n_send += h.n_acc;
         if (h.n_acc) max_len = std::max<uint32_t>(max_len, h.max_txn_acc ? h.max_txn_acc : kMaxPos);
     }
@@ -2043,7 +2078,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     rec[6] = il ? 1u : 0u;
     // tbx: every batch brings its txn_begin and the decider will take tb mode
     // (a prefix-kill epoch) -- the boundaries travel, nothing is renumbered
-    bool has_tb = m->tbs != nullptr;
+    bool has_tb = m->tbr != nullptr;
     for (uint32_t e = 0; e < P && !bad; e++) has_tb &= homes[e].txn_begin != nullptr || homes[e].n_txn == 0;
     {
         dv_epoch_dev probe{};
@@ -2053,7 +2088,12 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         has_tb = has_tb && group_tb_epoch(c, &probe);
     }
     rec[7] = has_tb ? 1u : 0u;
-    for (uint32_t e = 0; e < P && !bad; e++) rec[kGroupRecHead + e] = sendc[e] = homes[e].n_acc;
+    // per epoch: the batch's accesses, and above bit 32 the words of its
+    // txn_begin it would send (tbx: n_txn + 1 straight from its buffer)
+    for (uint32_t e = 0; e < P && !bad; e++) {
+        sendc[e] = homes[e].n_acc;
+        rec[kGroupRecHead + e] = sendc[e] | (uint64_t)(homes[e].txn_begin ? homes[e].n_txn + 1u : 0u) << 32;
+    }
     // (and the compact pack's bad flag cleared for this group: a group that
     // failed after setting it must not leave it to the next one)
     const uint32_t zero = 0;
@@ -2072,6 +2112,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     }
     uint64_t gmax = 0;
     bool refuse = false, compact = true, tbx = true;
+    std::vector<uint32_t> rtbw(P);  // words of txn_begin origin q sends for this rank's epoch
     for (uint32_t q = 0; q < P; q++) {
         const uint64_t *r = &all[(size_t)q * W];
         gmax = std::max<uint64_t>(gmax, r[0]);
@@ -2079,9 +2120,10 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         tbx &= r[7] == 1;
         refuse |= r[1] || r[2] || r[3] != all[3] || r[6] != all[6];  // (every rank the same order)
         uint64_t in = 0;  // what rank q receives: its epoch's batches
-        for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
+        for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q] & 0xFFFFFFFFull;
         refuse |= in > r[4];
-        recvc[q] = r[kGroupRecHead + m->rank];
+        recvc[q] = r[kGroupRecHead + m->rank] & 0xFFFFFFFFull;
+        rtbw[q] = (uint32_t)(r[kGroupRecHead + m->rank] >> 32);
     }
     if (refuse) return DV_ERR_ARG;  // every rank
     tbx = tbx && compact;
@@ -2144,19 +2186,19 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         const uint32_t bx = (uint32_t)std::min<uint64_t>((nmax + kBlock - 1) / kBlock, std::max(1u, 2048u / P));
         DV_LAUNCH(k_group_pack_c, dim3(bx, P), kBlock, 0, s, ps, sk, m->gbad, tbx ? 1 : 0);
     }
-    std::vector<size_t> bc(P), bd(P);  // tbx: the boundaries, tpr + 1 words per batch either way
-    if (tbx) {
-        PackTb pt{};
+    // tbx: each batch's txn_begin straight from its buffer (n_txn + 1 words,
+    // none for a batch without boundaries), landing at q * (tpr + 1); the
+    // receiver checks them (k_tb_origin / k_il_begin)
+    std::vector<size_t> bc(P), bcr(P), bdr(P);
+    std::vector<const uint8_t *> tsegs(P);
+    if (tbx)
         for (uint32_t e = 0; e < P; e++) {
-            pt.tb[e] = homes[e].txn_begin;
-            pt.n_txn[e] = homes[e].n_txn;
-            pt.n_acc[e] = homes[e].n_acc;
-            bc[e] = 4ull * (txns_per_rank + 1);
-            bd[e] = bc[e] * e;
+            tsegs[e] = reinterpret_cast<const uint8_t *>(homes[e].txn_begin);
+            bc[e] = homes[e].txn_begin ? 4ull * (homes[e].n_txn + 1) : 0;
+            bcr[e] = 4ull * rtbw[e];
+            bdr[e] = 4ull * (txns_per_rank + 1) * e;
+            xs.tbw[e] = rtbw[e];
         }
-        const uint32_t bx = std::max(1u, std::min((txns_per_rank + kBlock) / kBlock, std::max(1u, 2048u / P)));
-        DV_LAUNCH(k_group_pack_tb, dim3(bx, P), kBlock, 0, s, pt, txns_per_rank, m->tbs, m->gbad);
-    }
     CHK(hip_fail2(hipGetLastError(), "pack"));
     CHK(m->x->group(true));
     if (direct)
@@ -2165,8 +2207,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(sk), sc.data(), sd.data(),
                               reinterpret_cast<uint8_t *>(rk), rc.data(), rd.data(), s));
     if (tbx)
-        CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(m->tbs), bc.data(), bd.data(),
-                              reinterpret_cast<uint8_t *>(m->tbr), bc.data(), bd.data(), s));
+        CHK(m->x->all_to_allv_segs(tsegs.data(), bc.data(), reinterpret_cast<uint8_t *>(m->tbr), bcr.data(),
+                                   bdr.data(), s));
     if (!compact)
         CHK(m->x->all_to_allv(reinterpret_cast<const uint8_t *>(stx), sc.data(), sd.data(),
                               reinterpret_cast<uint8_t *>(rt), rc.data(), rd.data(), s));
@@ -2195,7 +2237,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     const uint64_t ntx = (uint64_t)P * txns_per_rank;
     if (tbx && !il) {  // origin-major with the boundaries: the landed batches as they are, tb mode
         DV_LAUNCH(k_tb_origin, (uint32_t)std::min<uint64_t>((ntx + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbr,
-                  m->iltb);
+                  m->iltb, m->gbad);
         CHK(hip_fail2(hipGetLastError(), "k_tb_origin"));
         ep.txn_begin = m->iltb;
         ep.recs32 = rk;
@@ -2207,7 +2249,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         ep.recs32 = ek;
         ep.acc_txn = nullptr;
         DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((ntx + kBlock) / kBlock, 4096), kBlock, 0, s, xs, m->tbr,
-                  (const uint32_t *)nullptr, m->iltb, m->ilsh);
+                  (const uint32_t *)nullptr, m->iltb, m->ilsh, m->gbad);
         const uint32_t tiles = (txns_per_rank + kIlTxns - 1) / kIlTxns;
         if (ro && tiles)
             DV_LAUNCH(k_il_move_tb, P * tiles, kBlock, 0, s, rk, xs, m->tbr, m->ilsh, ro, m->ilk, m->gbad);
@@ -2230,7 +2272,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
                 DV_LAUNCH(k_il_bounds, (uint32_t)std::min<uint64_t>((nt + P + kBlock - 1) / kBlock, 4096), kBlock, 0,
                           s, rt, xs, m->tbo, m->ncnt);
             DV_LAUNCH(k_il_begin, (uint32_t)std::min<uint64_t>((nt + kBlock) / kBlock, 4096), kBlock, 0, s, xs,
-                      m->tbo, m->ncnt, m->iltb, m->ilsh);
+                      m->tbo, m->ncnt, m->iltb, m->ilsh, (uint32_t *)nullptr);
             if (compact)
                 DV_LAUNCH(k_il_move<false>, xtiles, kBlock, 0, s, rk, rt, xs, m->ilsh, m->iltb, ro, m->ilk,
                           tb ? nullptr : m->ilt, m->gbad);
@@ -2248,7 +2290,8 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    (or an owner whose receive area is too small) fails the group on
     //    every rank; committed txns; records per owner
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad);
+    DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad,
+              m->xacc);
     CHK(hip_fail2(hipGetLastError(), "k_route_words"));
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
@@ -2305,7 +2348,7 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    has one committed txn, reads and writes in one launch; OCC / CALVIN:
     //    reads first)
     ctx_table0_cols(c, &f0, &pkey);
-    CHK(hip_fail2(hipMemsetAsync(m->xacc, 0, 2 * kSlots * sizeof(unsigned long long), s), "memset"));
+    // (xacc, the digest slots, zeroed by k_route_words)
     // (ordered lanes: after the previous group's execution, dv_lanes_order)
     CHK(lane_exec_begin(c, s));
     const bool fused = cfg.cc_alg == DV_NO_WAIT || cfg.cc_alg == DV_WAIT_DIE;

@@ -486,13 +486,15 @@ struct RouteOut {
     uint32_t *tot;  // [P] records per owner
     uint32_t P;
 };
-// NO_WAIT / WAIT_DIE / OCC: the committed txns' accesses (txn-major acc_row)
+// NO_WAIT / WAIT_DIE / OCC: the committed txns' accesses (txn-major acc_row),
+// and the commit bytes and count in the same pass (k_commit_out's work)
 void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_start, const uint32_t *tb_end,
-                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, const Counters *ctr);
+                      const uint32_t *acc_row, uint32_t n_txn, const uint8_t *status, Counters *ctr,
+                      uint8_t *d_commit);
 // CALVIN: every access, in row order (sorted pairs, queue elements, "an
 // earlier write precedes" flags)
 void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs, const uint64_t *el,
-                       const uint8_t *ew, uint64_t n, const uint8_t *status, const Counters *ctr);
+                       const uint8_t *ew, uint64_t n, const uint8_t *status, Counters *ctr);
 
 // ---- runtime accessors for the RCCL driver (dvcc_comm.hip)
 struct DvComm;  // defined in dvcc_comm.hip

@@ -1681,10 +1681,12 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit, bool prologue_done = false) {
         launch_tpcc_exec(c->stream, x);  // (the commit bytes too)
         return;
     } else if (c->route) {  // epoch groups: the owners execute (dvcc_comm.hip), nothing here
-        if (c->cfg.cc_alg == DV_CALVIN)
+        if (c->cfg.cc_alg == DV_CALVIN) {
             launch_route_rowq(c->stream, *c->route, c->pairs[c->sorted], c->el, c->ew, c->n_acc, c->status, c->ctr);
-        else
-            launch_route_txn(c->stream, *c->route, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->ctr);
+        } else {  // (the commit bytes too)
+            launch_route_txn(c->stream, *c->route, c->rs, c->re, c->acc_row, c->n_txn, c->status, c->ctr, d_commit);
+            return;
+        }
     } else {
         RowMap rm{};  // replicated epoch: global rows -> this partition's
         if (c->rep_P) {
