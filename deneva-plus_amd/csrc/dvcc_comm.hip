@@ -802,8 +802,13 @@ __global__ __launch_bounds__(kBlock) void k_route_count(RouteSrc<SRC> src, Route
     for (uint32_t o = threadIdx.x; o < ro.P; o += kBlock) ro.blk[o * kRouteBlocks + blockIdx.x] = c[o];
 }
 
+// this rank's outcome record, all-gathered (epoch groups, step 4): failure
+// code, committed txns, receive capacity, refused, then records per owner
+constexpr uint32_t kGroupRecHead = 8;
+
 // per owner (one block each): the blocks' counts -> exclusive prefix in
-// place, tot[o] = the owner's records
+// place, tot[o] = the owner's records; orec: the outcome record of a decided
+// epoch group too (a failed decision's is written again by k_route_words)
 __global__ __launch_bounds__(kBlock) void k_route_scan(RouteOut ro) {
     __shared__ uint32_t lds4[4];
     uint32_t *c = ro.blk + (uint64_t)blockIdx.x * kRouteBlocks;
@@ -822,6 +827,25 @@ __global__ __launch_bounds__(kBlock) void k_route_scan(RouteOut ro) {
         pre += v[j];
     }
     if (threadIdx.x == 0) ro.tot[blockIdx.x] = t;
+    if (ro.orec) {  // the outcome record, as k_route_words writes it for a decided epoch
+        const bool refused = *ro.bad != 0;
+        if (threadIdx.x == 0) ro.orec[kGroupRecHead + blockIdx.x] = refused ? 0u : t;
+        if (blockIdx.x == 0) {
+            for (uint32_t i = threadIdx.x; i < 2u * kSlots; i += kBlock) ro.xacc[i] = 0;
+            uint64_t committed = 0;  // (wave 0: a slot per lane, all loads in flight at once)
+            for (uint32_t k = threadIdx.x; k < (uint32_t)kSlots && threadIdx.x < 64; k += 64)
+                committed += ro.ctr->slot[k].committed;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) committed += __shfl_down(committed, off, 64);
+            if (threadIdx.x == 0) {
+                ro.orec[0] = refused ? (uint32_t)(-DV_ERR_ARG) : 0u;
+                ro.orec[1] = committed;
+                ro.orec[2] = ro.cap;
+                ro.orec[3] = refused ? 1u : 0u;
+                for (uint32_t k = 4; k < kGroupRecHead; k++) ro.orec[k] = 0;
+            }
+        }
+    }
 }
 
 // pass 2: the same walk (same grid, same items per block), each block
@@ -924,9 +948,7 @@ __global__ void k_mail_out(const uint64_t *__restrict__ a, uint32_t na, const ui
     if (threadIdx.x == 0) __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// this rank's outcome record, all-gathered (epoch groups, step 4): failure
-// code, committed txns, receive capacity, then records per owner
-constexpr uint32_t kGroupRecHead = 8;
+// (this rank's outcome record: kGroupRecHead, k_route_words)
 // (and the execution's digest slots zeroed for step 6: the previous group's
 // were read by this group's vote)
 __global__ void k_route_words(const uint32_t *__restrict__ tot, uint32_t P, uint64_t committed, uint32_t fail,
@@ -957,6 +979,7 @@ void launch_route_txn(hipStream_t s, const RouteOut &ro, const uint32_t *tb_star
     const RouteSrc<0> src{tb_start, tb_end, acc_row, n_txn, nullptr, nullptr, nullptr, 0, status};
     DV_LAUNCH((k_route_count<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr, d_commit);
     DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
+    if (ro.wrote) *ro.wrote = ro.orec != nullptr;
     DV_LAUNCH((k_route_scatter<0>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
 
@@ -964,7 +987,9 @@ void launch_route_rowq(hipStream_t s, const RouteOut &ro, const uint64_t *pairs,
                        const uint8_t *ew, uint64_t n, const uint8_t *status, Counters *ctr) {
     const RouteSrc<1> src{nullptr, nullptr, nullptr, 0, pairs, el, ew, n, status};
     DV_LAUNCH((k_route_count<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr, (uint8_t *)nullptr);
-    DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, ro);
+    RouteOut r0 = ro;  // (CALVIN's commit count comes after the route: k_route_words writes the record)
+    r0.orec = nullptr;
+    DV_LAUNCH(k_route_scan, ro.P, kBlock, 0, s, r0);
     DV_LAUNCH((k_route_scatter<1>), kRouteBlocks, kBlock, 0, s, src, ro, ctr);
 }
 
@@ -2282,7 +2307,14 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
         }
         CHK(hip_fail2(hipGetLastError(), "k_il_move"));
     }
-    const RouteOut rout{reinterpret_cast<uint2 *>(m->send), m->rblk, m->rtot, P};
+    bool rec_written = false;  // (the owner scan wrote the outcome record)
+    RouteOut rout{reinterpret_cast<uint2 *>(m->send), m->rblk, m->rtot, P};
+    rout.orec = m->gs;
+    rout.bad = m->gbad;
+    rout.xacc = m->xacc;
+    rout.cap = 2 * acap;
+    rout.ctr = ctx_counters(c);
+    rout.wrote = &rec_written;
     dv_stats est{};
     const int rd_ = epoch_run_replicated(c, &ep, ek, P, m->verdict, &est, &rout);
 
@@ -2290,9 +2322,11 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     //    (or an owner whose receive area is too small) fails the group on
     //    every rank; committed txns; records per owner
     const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad,
-              m->xacc);
-    CHK(hip_fail2(hipGetLastError(), "k_route_words"));
+    if (rd_ || !rec_written) {
+        DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad,
+                  m->xacc);
+        CHK(hip_fail2(hipGetLastError(), "k_route_words"));
+    }
     CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
     CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
     uint64_t gfail = 0, committed = 0;

@@ -485,6 +485,15 @@ struct RouteOut {
     uint32_t *blk;  // [P][kRouteBlocks] records per owner per block (then their exclusive prefix)
     uint32_t *tot;  // [P] records per owner
     uint32_t P;
+    // the epoch group's outcome record (step 4 of run_group), written by the
+    // owner scan when the txn walk routes (null: the host launches
+    // k_route_words); *wrote (host) is set when that scan was queued
+    uint64_t *orec = nullptr;
+    const uint32_t *bad = nullptr;         // a refused batch: the group fails as DV_ERR_ARG
+    unsigned long long *xacc = nullptr;    // the execution's digest slots, zeroed for step 6
+    uint64_t cap = 0;                      // receive capacity
+    const Counters *ctr = nullptr;         // committed count: the slots' sum
+    bool *wrote = nullptr;
 };
 // NO_WAIT / WAIT_DIE / OCC: the committed txns' accesses (txn-major acc_row),
 // and the commit bytes and count in the same pass (k_commit_out's work)
@@ -513,6 +522,7 @@ bool ctx_group_capable(dv_ctx *c, uint32_t nranks);
 void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey);  // table 0's local rows
 uint64_t ctx_table0_rows(dv_ctx *c);  // ... their count (buckets of its direct map)
 uint32_t *ctx_err_words(dv_ctx *c);  // &Counters::err (peer_err follows)
+const dvcc::Counters *ctx_counters(dv_ctx *c);
 // ordered lanes (dv_lanes_order): an execution of an epoch group on lane c
 // waits for its turn -- the previous group's execution, on whichever lane,
 // queued (host) and finished (its event, device) -- and hands the turn on

@@ -606,6 +606,7 @@ void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey) {
     *pkey = c->pkey + c->tab[0].row_base;
 }
 uint32_t *ctx_err_words(dv_ctx *c) { return &c->ctr->err; }
+const Counters *ctx_counters(dv_ctx *c) { return c->ctr; }
 
 int lane_exec_begin(dv_ctx *c, hipStream_t s) {
     if (!c->order) return DV_OK;
