@@ -828,8 +828,10 @@ __global__ __launch_bounds__(kBlock) void k_route_scan(RouteOut ro) {
     }
     if (threadIdx.x == 0) ro.tot[blockIdx.x] = t;
     if (ro.orec) {  // the outcome record, as k_route_words writes it for a decided epoch
+        // (a refused batch decides the code; else the decision's error bits)
         const bool refused = *ro.bad != 0;
-        if (threadIdx.x == 0) ro.orec[kGroupRecHead + blockIdx.x] = refused ? 0u : t;
+        const uint32_t fail = refused ? (uint32_t)(-DV_ERR_ARG) : (uint32_t)(-err_code_of(ro.ctr->err | ro.ctr->peer_err));
+        if (threadIdx.x == 0) ro.orec[kGroupRecHead + blockIdx.x] = fail ? 0u : t;
         if (blockIdx.x == 0) {
             for (uint32_t i = threadIdx.x; i < 2u * kSlots; i += kBlock) ro.xacc[i] = 0;
             uint64_t committed = 0;  // (wave 0: a slot per lane, all loads in flight at once)
@@ -838,11 +840,14 @@ __global__ __launch_bounds__(kBlock) void k_route_scan(RouteOut ro) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) committed += __shfl_down(committed, off, 64);
             if (threadIdx.x == 0) {
-                ro.orec[0] = refused ? (uint32_t)(-DV_ERR_ARG) : 0u;
-                ro.orec[1] = committed;
+                ro.orec[0] = fail;
+                ro.orec[1] = fail ? 0u : committed;
                 ro.orec[2] = ro.cap;
                 ro.orec[3] = refused ? 1u : 0u;
-                for (uint32_t k = 4; k < kGroupRecHead; k++) ro.orec[k] = 0;
+                // a halted decision (its rounds yielded): its route was a
+                // no-op; the decider finishes it and every rank votes again
+                ro.orec[4] = !fail && (ro.ctr->halt | ro.ctr->a_halt) ? 1u : 0u;
+                for (uint32_t k = 5; k < kGroupRecHead; k++) ro.orec[k] = 0;
             }
         }
     }
@@ -2315,35 +2320,62 @@ int run_group(dv_ctx *c, const dv_epoch_dev *homes, uint32_t n_homes, uint32_t t
     rout.cap = 2 * acap;
     rout.ctr = ctx_counters(c);
     rout.wrote = &rec_written;
+    // (CALVIN counts its commits after the route: its record needs the host)
+    rout.defer = cfg.cc_alg != DV_CALVIN;
     dv_stats est{};
-    const int rd_ = epoch_run_replicated(c, &ep, ek, P, m->verdict, &est, &rout);
+    int rd_ = epoch_run_replicated(c, &ep, ek, P, m->verdict, &est, &rout);
+    // the decider's counters are still on their way (RouteOut::defer): the
+    // outcome vote's round trip brings them, and a context left between the
+    // two is finished before returning
+    bool pending = rd_ == DV_OK && ctx_finish_pending(c);
+    auto settle = [&]() {
+        if (pending) {
+            rd_ = epoch_replicated_complete(c, &est);
+            pending = false;
+        }
+    };
 
     // 4. one all-gather of every rank's outcome record: a failure on any rank
     //    (or an owner whose receive area is too small) fails the group on
-    //    every rank; committed txns; records per owner
-    const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
-    if (rd_ || !rec_written) {
-        DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs, m->gbad,
-                  m->xacc);
-        CHK(hip_fail2(hipGetLastError(), "k_route_words"));
-    }
-    CHK(m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s));
-    CHK(mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr));
+    //    every rank; committed txns; records per owner.  A decider whose
+    //    rounds halted (record word 4) finishes them once the vote is in, and
+    //    every rank votes again.
     uint64_t gfail = 0, committed = 0;
-    bool refused = false;
-    for (uint32_t q = 0; q < P; q++) {
-        const uint64_t *r = &all[(size_t)q * W];
-        gfail = std::max<uint64_t>(gfail, r[0]);
-        refused |= r[3] != 0;
-        committed += r[1];
-        uint64_t in = 0;
-        for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
-        if (in > r[2]) gfail = std::max<uint64_t>(gfail, (uint64_t)(-DV_ERR_ARG));
+    for (int vote = 0;; vote++) {
+        const uint32_t fail = rd_ ? (uint32_t)(-rd_) : 0u;
+        if (rd_ || !rec_written) {
+            DV_LAUNCH(k_route_words, 1, 64, 0, s, m->rtot, P, rd_ ? 0ull : est.committed, fail, 2 * acap, m->gs,
+                      m->gbad, m->xacc);
+            int e = hip_fail2(hipGetLastError(), "k_route_words");
+            if (e) { settle(); return e; }
+        }
+        int e = m->x->all_gather(reinterpret_cast<const uint8_t *>(m->gs), 8ull * W, reinterpret_cast<uint8_t *>(m->gr), s);
+        if (!e) e = mail_get(m, s, m->gr, P * W, nullptr, 0, all.data(), nullptr);
+        settle();  // (its counters arrived with the vote)
+        if (e) return e;
+        gfail = committed = 0;
+        bool refused = false, halted = false;
+        for (uint32_t q = 0; q < P; q++) {
+            const uint64_t *r = &all[(size_t)q * W];
+            gfail = std::max<uint64_t>(gfail, r[0]);
+            refused |= r[3] != 0;
+            halted |= r[4] != 0;
+            committed += r[1];
+            uint64_t in = 0;
+            for (uint32_t o = 0; o < P; o++) in += all[(size_t)o * W + kGroupRecHead + q];
+            if (in > r[2]) gfail = std::max<uint64_t>(gfail, (uint64_t)(-DV_ERR_ARG));
+        }
+        // a batch its sender (or the move) refused makes the group an argument
+        // error on every rank, whatever the deciders made of it
+        if (refused) gfail = (uint64_t)(-DV_ERR_ARG);
+        if (gfail) return -(int)gfail;
+        // (a finished decision is not halted again: a second one cannot happen)
+        if (!halted) break;
+        if (vote > 0) return DV_ERR_STATE;
     }
-    // a batch its sender (or the move) refused makes the group an argument
-    // error on every rank, whatever the deciders made of it
-    if (refused) gfail = (uint64_t)(-DV_ERR_ARG);
-    if (gfail) return -(int)gfail;
+    // a decider whose finish failed after an outcome it voted as good (an
+    // invariant the finish checks, or HIP itself): its peers go on
+    if (rd_) return rd_;
 
     // 5. records to their owners, commit bytes back to their origins
     std::vector<uint64_t> rcnt(P);

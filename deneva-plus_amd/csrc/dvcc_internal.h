@@ -289,6 +289,17 @@ constexpr uint32_t ERRB_INPUT = ERRB_KEY | ERRB_DUP | ERRB_TXN | ERRB_TABLE | ER
 __device__ __forceinline__ uint32_t input_err(const Counters *ctr) {
     return (ctr->err | ctr->peer_err) & ERRB_INPUT;
 }
+// the return code of an epoch whose counters hold error bits b (the host's
+// epoch finish, and the epoch groups' outcome record on the device)
+__host__ __device__ inline int err_code_of(uint32_t b) {
+    if (b & ERRB_TABLE) return DV_ERR_NO_TABLE;
+    if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
+    if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
+    if (b & (ERRB_BIG | ERRB_TS)) return DV_ERR_ARG;  // a txn longer than max_txn_acc; WAIT_DIE ts not rising
+    if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
+    if (b & ERRB_SPIN) return DV_ERR_HIP;
+    return DV_OK;
+}
 
 // ---- probe / queues (dvcc_kernels.hip)
 // counts (optional): the first radix pass's per-tile digit counts (k_radix_hist
@@ -494,6 +505,7 @@ struct RouteOut {
     uint64_t cap = 0;                      // receive capacity
     const Counters *ctr = nullptr;         // committed count: the slots' sum
     bool *wrote = nullptr;
+    bool defer = false;                    // the decider's counter read waits for the outcome vote
 };
 // NO_WAIT / WAIT_DIE / OCC: the committed txns' accesses (txn-major acc_row),
 // and the commit bytes and count in the same pass (k_commit_out's work)
@@ -541,6 +553,11 @@ void lane_fail(dv_ctx *c);
 bool group_tb_epoch(const dv_ctx *c, const dv_epoch_dev *ep);
 int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys32, uint32_t nranks,
                          uint8_t *d_commit, dv_stats *st, const dvcc::RouteOut *route = nullptr);
+// RouteOut::defer: epoch_run_replicated returned with its counters still on
+// the way (ctx_finish_pending); this reads them and finishes the decision
+// (a halted one is finished and routed again)
+int epoch_replicated_complete(dv_ctx *c, dv_stats *st);
+bool ctx_finish_pending(dv_ctx *c);
 int comm_combine_errors(dv_ctx *c);  // dvcc_comm.hip
 void comm_free(dvcc::DvComm *m);
 namespace dvcc {

@@ -246,6 +246,11 @@ struct dv_ctx {
     uint32_t rep_P = 0;           // replicated epoch in flight over rep_P partitions (epoch_run_replicated)
     const uint32_t *keys32 = nullptr;  // ... its keys as 32-bit row ids
     const RouteOut *route = nullptr;   // epoch groups: committed accesses go to their owners (run_group)
+    // epoch groups (RouteOut::defer): the finish waits for its counters after
+    // the outcome vote (epoch_finish_complete)
+    bool fin_pending = false;
+    unsigned long long fin_want = 0;
+    uint8_t *fin_commit = nullptr;
     // what a synchronous redo of the prefix needs (dv_epoch_finish, Counters::a_halt)
     uint32_t pf_K = 0, pf_ub_a = 0;
     const uint32_t *pf_n_acc_dev = nullptr;  // the epoch's device-side access count (dv_epoch_dev::n_acc_dev)
@@ -513,15 +518,7 @@ uint64_t row_space(const dv_ctx *c) {
     return c->rep_P ? (uint64_t)c->rep_P * c->tab[0].nbuckets : c->total_rows;
 }
 
-int err_from_bits(uint32_t b) {
-    if (b & ERRB_TABLE) return DV_ERR_NO_TABLE;
-    if (b & ERRB_KEY) return DV_ERR_KEY_NOT_FOUND;
-    if (b & ERRB_TXN) return DV_ERR_TXN_RANGE;
-    if (b & (ERRB_BIG | ERRB_TS)) return DV_ERR_ARG;  // a txn longer than max_txn_acc; WAIT_DIE ts not rising
-    if (b & ERRB_DUP) return DV_ERR_DUP_ROW;
-    if (b & ERRB_SPIN) return DV_ERR_HIP;
-    return DV_OK;
-}
+int err_from_bits(uint32_t b) { return err_code_of(b); }
 
 // idle time after which an asynchronous workgroup yields: the
 // whole asynchronous phase of a config-D epoch takes ~130 us
@@ -607,6 +604,7 @@ void ctx_table0_cols(dv_ctx *c, uint64_t **f0, const uint64_t **pkey) {
 }
 uint32_t *ctx_err_words(dv_ctx *c) { return &c->ctr->err; }
 const Counters *ctx_counters(dv_ctx *c) { return c->ctr; }
+bool ctx_finish_pending(dv_ctx *c) { return c && c->fin_pending; }
 
 int lane_exec_begin(dv_ctx *c, hipStream_t s) {
     if (!c->order) return DV_OK;
@@ -1712,6 +1710,7 @@ void enqueue_exec(dv_ctx *c, uint8_t *d_commit, bool prologue_done = false) {
 }  // namespace
 
 int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st);
+int finish_tail(dv_ctx *c, uint8_t *d_commit, dv_stats *st, int r);
 
 // ordered lanes (dv_lanes_order) running the per-epoch partitioned drivers
 // (dv_epoch_run_part / dv_tpcc_epoch_run_part): the epoch's execution takes
@@ -1740,8 +1739,7 @@ int dv_epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
 
 int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     KProfScope kps_(c);
-    if (!c || c->phase != 1) return DV_ERR_STATE;
-    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
+    if (!c || c->phase != 1 || c->fin_pending) return DV_ERR_STATE;
     if (c->cfg.workload == DV_TPCC && !c->tp_args) {  // only through dv_tpcc_epoch_begin
         c->phase = 0;
         return DV_ERR_STATE;
@@ -1750,7 +1748,30 @@ int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
     enqueue_exec(c, d_commit);
     rec(c, 5);
     int r = hip_fail(hipGetLastError(), "execution launch");
+    if (!r && c->route && c->route->defer) {
+        // epoch groups: the counters are queued for the host now and read
+        // after the outcome vote, whose own round trip brings them
+        // (epoch_finish_complete; run_group votes again on a halted decider)
+        c->fin_want = mirror_out(c, 0);
+        c->fin_commit = d_commit;
+        c->fin_pending = true;
+        return hip_fail(hipGetLastError(), "counter mirror");
+    }
     if (!r) r = sync_counters(c);
+    return finish_tail(c, d_commit, st, r);
+}
+
+int epoch_finish_complete(dv_ctx *c, dv_stats *st) {
+    if (!c || !c->fin_pending) return DV_ERR_STATE;
+    c->fin_pending = false;
+    const int r = mirror_wait(c, 0, c->fin_want);
+    return finish_tail(c, c->fin_commit, st, r);
+}
+
+// after the counters reached the host: a halted decision is finished and
+// executed again (each redo reads the counters itself), then the outcome
+int finish_tail(dv_ctx *c, uint8_t *d_commit, dv_stats *st, int r) {
+    const bool calvin = c->cfg.cc_alg == DV_CALVIN;
     if (!r && c->prefix_mode && c->h_ctr->a_halt) {
         // the prefix's rounds halted and nothing behind them ran
         c->async_unconfirmed = false;
@@ -3247,6 +3268,16 @@ int epoch_run_replicated(dv_ctx *c, const dv_epoch_dev *ep, const uint32_t *keys
     c->keys32 = keys32;
     c->route = route;
     const int r = dv_epoch_run_device(c, ep, d_commit, nullptr, st);
+    if (c->fin_pending) return r;  // (the route stays set for epoch_replicated_complete's redo)
+    c->rep_P = 0;
+    c->keys32 = nullptr;
+    c->route = nullptr;
+    return r;
+}
+
+int epoch_replicated_complete(dv_ctx *c, dv_stats *st) {
+    if (!c || !c->fin_pending) return DV_ERR_STATE;
+    const int r = epoch_finish_complete(c, st);
     c->rep_P = 0;
     c->keys32 = nullptr;
     c->route = nullptr;

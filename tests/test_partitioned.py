@@ -427,15 +427,20 @@ def _run_group(engines, homes, n_txn):
     return out
 
 
-def _engine_group(cc, world, rows_pp, n_txn, R=10, mode=1):
+def _engine_group(cc, world, rows_pp, n_txn, R=10, mode=1, async_iters=None):
     """mode: dv_comm_set_mode -- 1 the list protocol (capacity for this
     rank's share), 2 replicated (capacity for the whole epoch); + 8
-    (DV_COMM_POSITION_ORDER) position-major replicated epochs."""
+    (DV_COMM_POSITION_ORDER) position-major replicated epochs.  async_iters:
+    asynchronous rounds on every context, yielding after that many iterations
+    (dv_set_async_limits; replicated contexts otherwise run without them)."""
     engines = []
     for p in range(world):
         rep = (mode & 3) == 2
         cap = n_txn * world * R + 4096 if rep else max(64, int(n_txn * world * R * 1.2 / world) + 4096)
-        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p, asynchronous=not rep)
+        eng = dvcc.CCEngine(cc, n_txn * world, cap, part_cnt=world, part_id=p,
+                            asynchronous=not rep or async_iters is not None)
+        if async_iters is not None:
+            eng.set_async_limits(async_iters, 0)
         eng.load_ycsb_partition(rows_pp)
         engines.append(eng)
     dvcc.CCEngine.comm_init_local(engines)
@@ -713,7 +718,7 @@ def _group_mine(c_ref, r, n_txn, world, cc, position):
 
 
 def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, sizes=None, batch=False,
-                        wide=False, position=False, prefix=0):
+                        wide=False, position=False, prefix=0, async_iters=None):
     """Every epoch of every group against the one-partition oracle run over
     the sequenced epochs one after the other: commit bytes (each rank holds its
     own txns' bytes of every epoch), committed count, digest and writes summed
@@ -724,10 +729,12 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
     wide: 8-byte batches (DV_COMM_WIDE_BATCHES) instead of the compact ones.
     position: the origins' batches sequenced txn by txn (DV_COMM_POSITION_ORDER;
     CALVIN keeps origin order).  prefix: dv_set_prefix on every decider (a
-    prefix-kill epoch at any size: the groups' boundaries path, tbx)."""
+    prefix-kill epoch at any size: the groups' boundaries path, tbx).
+    async_iters: the deciders' asynchronous rounds on, yielding after that
+    many iterations (_engine_group)."""
     gen = dvcc.YCSBQueryGenerator(rows_pp * world, part_cnt=world, zipf_theta=theta, txn_write_perc=1.0,
                                   tup_write_perc=0.5, part_per_txn=2, strict_ppt=1, mpr=mpr)
-    engines = _engine_group(cc, world, rows_pp, n_txn, mode=2)
+    engines = _engine_group(cc, world, rows_pp, n_txn, mode=2, async_iters=async_iters)
     if prefix:
         for eng in engines:
             eng.set_prefix(prefix)
@@ -789,6 +796,8 @@ def _check_epoch_groups(cc, world, rows_pp, n_txn, mpr, groups=2, theta=0.9, siz
         res = _run_group_epochs(engines, homes, n_txn)
         committed = sum(st.committed for _, st in refs)
         digest = writes = 0
+        if async_iters == 1:  # (forced yields: some decider halted and finished after the vote)
+            assert any(not isinstance(x, Exception) and x[1].async_yields for x in res), f"group {g}: no yield"
         for r, x in enumerate(res):
             assert not isinstance(x, Exception), f"rank {r}: {x}"
             c, st = x
@@ -861,6 +870,21 @@ def test_epoch_groups_with_boundaries(cc, world, position):
     unequal batches (padded boundaries)."""
     _check_epoch_groups(cc, world, 1 << 13, 2000, 0.3, position=position, prefix=400)
     _check_epoch_groups(cc, 3, 1 << 13, 1000, 0.3, sizes=[1000, 640, 1], position=position, prefix=300)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cc", [dvcc.NO_WAIT, dvcc.WAIT_DIE, dvcc.OCC])
+@pytest.mark.parametrize("async_iters,prefix,batch", [(1, 0, False), (1, 400, False), (1, 400, True),
+                                                      (1 << 18, 400, False)])
+def test_epoch_groups_asynchronous_deciders(cc, async_iters, prefix, batch):
+    """Deciders with asynchronous rounds, as the bench runs them: a decided
+    group's counters reach the host with the outcome vote (no read of their
+    own).  Forced yields (one iteration) halt every decision: the vote carries
+    the halted decider, which finishes its rounds (and, prefix-kill, its
+    prefix) and routes again, and every rank votes again -- against the
+    oracle; then the same without forced yields."""
+    _check_epoch_groups(cc, 2, 1 << 13, 2000, 0.3, position=True, prefix=prefix, async_iters=async_iters,
+                        groups=3 if batch else 2, batch=batch)
 
 
 @pytest.mark.gpu
