@@ -1753,9 +1753,11 @@ int epoch_finish(dv_ctx *c, uint8_t *d_commit, dv_stats *st) {
         // after the outcome vote, whose own round trip brings them
         // (epoch_finish_complete; run_group votes again on a halted decider)
         c->fin_want = mirror_out(c, 0);
+        r = hip_fail(hipGetLastError(), "counter mirror");
+        if (r) return finish_tail(c, d_commit, st, r);  // (the context is free again)
         c->fin_commit = d_commit;
         c->fin_pending = true;
-        return hip_fail(hipGetLastError(), "counter mirror");
+        return DV_OK;
     }
     if (!r) r = sync_counters(c);
     return finish_tail(c, d_commit, st, r);
